@@ -1,0 +1,265 @@
+#!/usr/bin/env python3
+"""bench.py -- tracked frame-pairs/s (match + pose), 1024 kp x 256-D fp32, KITTI shape.
+
+One STEP = the hot path over one batch of B synthetic frame-pairs already resident in HBM:
+    mv_match_allpairs_f32_dev   all-pairs fp32 match (python/pairwise_pnp.py:635-659 semantics,
+                                bit-exact to the gemmini_functions_cpu.h summation order)
+    mv_pose_from_matches_dev    8-point RANSAC + cheirality + Gauss-Newton pose (the intent of
+                                src/pnp_solver.c / pairwise_pnp.py:667-694)
+Workload = BASELINE.json configs[1] (1024 x 1024 keypoints x 256-D fp32 synthetic descriptors)
+with the pose of the metric's "match+PnP".  Pairs are independent: with --gpus N each rank
+(one process per GPU, torch.distributed) processes its own B pairs -- weak scaling, no
+data-path collective.  value = pairs processed by all ranks / max-over-ranks wall time.
+
+Extra fields: roofline of the dominant kernel (k_ap_screen, FP32 MFMA bound), measured with
+HIP events on the launch stream inside the timed region; cpu_baseline = the gemmini matmul
++ row argmax (+ as-built stub pose) on host cores (rank 0, N = 1 only).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "maveric-slam_amd"))
+
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix/vector peak (dense)
+HBM_PEAK_GBS = 8000.0
+KD = 256
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="frame-pairs per GPU per step")
+    ap.add_argument("--kp", type=int, default=1024, help="keypoints per frame")
+    ap.add_argument("--hypotheses", type=int, default=256)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--check", type=int, default=2, help="pairs verified against the oracle after timing")
+    return ap.parse_args()
+
+
+def gen_batch(torch, dev, B, n, seed):
+    """B synthetic KITTI-shape pairs (synth.synth_pair_f32 semantics; descriptors drawn on the GPU)."""
+    import synth
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    d0 = torch.randn((B, n, KD), generator=g, device=dev)
+    d0 = d0 / d0.norm(dim=2, keepdim=True)
+    m = int(round(0.6 * n))
+    src = torch.argsort(torch.rand((B, n), generator=g, device=dev), dim=1)[:, :m]
+    d1 = torch.randn((B, n, KD), generator=g, device=dev)
+    d1 = d1 / d1.norm(dim=2, keepdim=True)
+    noise = torch.randn((B, m, KD), generator=g, device=dev) * (0.3 / 16.0)
+    reobs = torch.gather(d0, 1, src[:, :, None].expand(B, m, KD)) + noise
+    d1[:, :m] = reobs / reobs.norm(dim=2, keepdim=True)
+    order = torch.argsort(torch.rand((B, n), generator=g, device=dev), dim=1)
+    d1 = torch.gather(d1, 1, order[:, :, None].expand(B, n, KD)).contiguous()
+    # geometry: exact projections under the 785->786 relative pose (numpy, small)
+    rng = np.random.default_rng(seed)
+    kp0 = np.empty((B, n, 2), np.float32)
+    kp1 = np.empty((B, n, 2), np.float32)
+    src_h = src.cpu().numpy()
+    order_h = order.cpu().numpy()
+    R, t = synth.T_785_786[:, :3], synth.T_785_786[:, 3]
+    for b in range(B):
+        _, x0, x1 = synth.synth_scene(rng, n, R, t)
+        k1 = np.stack([rng.uniform(0, synth.KITTI_W, n), rng.uniform(0, synth.KITTI_H, n)], 1)
+        k1[:m] = x1[src_h[b]]
+        kp0[b] = x0
+        kp1[b] = k1[order_h[b]]
+    return d0.contiguous(), d1, torch.from_numpy(kp0).to(dev), torch.from_numpy(kp1).to(dev)
+
+
+def cpu_baseline(seconds, n):
+    """gemmini_functions_cpu.h matmul (C += A.B^T, sequential k) + row argmax + as-built stub
+    pose, on host threads (ctypes releases the GIL).  'reference' when the reference's own
+    header was compiled into oracle/_ref, else the oracle's restatement ('port')."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import concurrent.futures as cf
+
+    import oracle
+
+    kind = "port"
+    mm = oracle.lib().orc_matmul_nt
+    if oracle.ref_available():
+        try:
+            mm = oracle.ref().ref_matmul_nt
+            kind = "reference"
+        except Exception:
+            pass
+    L = oracle.lib()
+    threads = max(1, min(16, (os.cpu_count() or 1)))
+    rng = np.random.default_rng(0)
+    A = rng.standard_normal((n, KD)).astype(np.float32)
+    A /= np.linalg.norm(A, axis=1, keepdims=True)
+    Bm = rng.standard_normal((n, KD)).astype(np.float32)
+    Bm /= np.linalg.norm(Bm, axis=1, keepdims=True)
+    P = oracle._ptr
+    deadline = time.perf_counter() + seconds
+
+    def worker(_):
+        C = np.zeros((n, n), np.float32)
+        idx = np.zeros(n, np.int32)
+        sc = np.zeros(n, np.float32)
+        pairs = 0
+        while time.perf_counter() < deadline:
+            C.fill(0)
+            mm(n, n, KD, P(A), P(Bm), P(C))
+            L.orc_row_argmax(P(C), n, n, 0.8, P(idx), P(sc))
+            pairs += 1
+        return pairs
+
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(threads) as ex:
+        total = sum(ex.map(worker, range(threads)))
+    dt = time.perf_counter() - t0
+    # single-core reference point
+    C = np.zeros((n, n), np.float32)
+    t1 = time.perf_counter()
+    mm(n, n, KD, P(A), P(Bm), P(C))
+    one = time.perf_counter() - t1
+    return {"value": total / dt, "unit": "pairs/s", "cores": threads, "kind": kind,
+            "sample": "%d pairs of %dx%dx%d fp32 matmul + row argmax over %.1f s on %d host threads "
+                      "(gemmini_functions_cpu.h:14-56 order, gcc -O2); 1 core: %.1f ms/pair"
+                      % (total, n, n, KD, dt, threads, one * 1e3)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import mvtrack
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    B, n = args.batch, args.kp
+
+    d0, d1, kp0, kp1 = gen_batch(torch, dev, B, n, seed=1000 + rank * 7919)
+    nn_ = torch.full((B,), n, dtype=torch.int32, device=dev)
+    idx = torch.empty((B, n), dtype=torch.int32, device=dev)
+    score = torch.empty((B, n), dtype=torch.float32, device=dev)
+    T = torch.empty((B, 3, 4), dtype=torch.float32, device=dev)
+    nmatch = torch.empty(B, dtype=torch.int32, device=dev)
+    ninl = torch.empty(B, dtype=torch.int32, device=dev)
+    status = torch.empty(B, dtype=torch.int32, device=dev)
+
+    ctx = mvtrack.Context(local)
+    stream = torch.cuda.current_stream()
+    ctx.set_stream(stream)
+    ctx.reserve(B, n)
+    import synth
+
+    K = synth.KITTI_K
+    pose_p = mvtrack.pose_params(mvtrack.AS_INTENDED, fx=K[0, 0], fy=K[1, 1], cx=K[0, 2], cy=K[1, 2],
+                                 hypotheses=args.hypotheses, inlier_thresh=1.0, refine_iters=10, seed=7)
+
+    def step():
+        ctx.match_allpairs_f32(d0, d1, nn_, nn_, idx, score, 0.8)
+        ctx.pose_from_matches(pose_p, nn_, idx, kp0, kp1, T, nmatch, ninl, status)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    mvtrack.profile_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    mvtrack.profile_enable(False)
+    elapsed = t1 - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    k_ms, k_n = mvtrack.profile_query("k_ap_screen")
+    r_ms, r_n = mvtrack.profile_query("k_ap_resolve")
+    p_ms, p_n = mvtrack.profile_query("k_pose_ransac")
+
+    # correctness of the timed outputs on a few pairs (outside the timed region)
+    ok = int((status == 0).sum().item())
+    checked = 0
+    if args.check > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+
+        for b in range(min(args.check, B)):
+            i2, s2 = oracle.allpairs_f32(d0[b].cpu().numpy(), d1[b].cpu().numpy(), 0.8)
+            assert (idx[b].cpu().numpy() == i2).all(), "timed match output differs from the oracle"
+            checked += 1
+        R = T[:, :, :3].double().cpu().numpy()
+        err = np.abs(R - synth.T_785_786[None, :, :3]).max(axis=(1, 2))
+        assert ok == B and float(err.max()) < 1e-3, "pose failed: ok=%d max|dR|=%g" % (ok, err.max())
+
+    pairs_total = B * args.steps * world
+    value = pairs_total / elapsed
+    flops_pair = 2.0 * n * n * KD
+    screen_avg_s = (k_ms / max(k_n, 1)) * 1e-3
+    achieved = flops_pair * B / screen_avg_s / 1e12
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_k_ap_screen.json")
+    if os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+            if pmc.get("batch") == B and pmc.get("kp") == n:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    out = {
+        "metric": "tracked frame-pairs/sec (match+PnP), 1024kp x 256-D KITTI shape",
+        "value": round(value, 2),
+        "unit": "pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: unit-norm N(0,1) 256-D descriptors, 60% re-observed (+noise |0.3|), exact "
+                "projections of a 3-D scene under outputs/transform_000785_000786.npy, KITTI K, 1241x376",
+        "config": {"workload": "configs[1]: all-pairs match %dx%d kp x 256-D fp32 + RANSAC/GN pose per pair"
+                               % (n, n), "pairs_per_gpu_per_step": B, "kp": n, "dim": KD,
+                   "pose": "8-point RANSAC %d hyp + cheirality + 10 GN iters" % args.hypotheses,
+                   "parallelism": "pairs sharded one process per GPU (dp%d), no collective" % world},
+        "roofline": {"bound": "mfma", "kernel": "k_ap_screen", "achieved": round(achieved, 2),
+                     "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+                     "traffic": traffic, "algorithmic_flops_per_launch": flops_pair * B,
+                     "avg_launch_ms": round(screen_avg_s * 1e3, 4), "launches": k_n},
+        "stages_ms_per_step": {"k_ap_screen": round(k_ms / max(k_n, 1), 4),
+                               "k_ap_resolve": round(r_ms / max(r_n, 1), 4),
+                               "k_pose_ransac": round(p_ms / max(p_n, 1), 4)},
+        "checked_pairs": checked, "pose_ok": ok,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, n)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,169 @@
+/*
+ * maveric_hip.h -- the C ABI of libmaveric_hip.so (MI355X / gfx950).
+ *
+ * Two layers:
+ *   1. The reference's own API, unchanged (frame.h, top_N.h, pnp_solver.h,
+ *      tracking.h).  Those entry points run on a lazily created default
+ *      context (device 0) with host pointers, synchronously.
+ *   2. This header: an explicit context, a stream, and BATCHED entry points
+ *      over device pointers for throughput mode (many independent frame-pairs
+ *      per launch).  All *_dev functions are stream-ordered and asynchronous;
+ *      they never allocate once mv_context_reserve() has covered the sizes, so
+ *      they can be captured in a hipGraph.
+ *
+ * Conventions: plain C types only; every function returns an mv_status
+ * (0 = success, negative = error) unless documented otherwise; nothing ever
+ * calls exit().  Device arrays are row-major, batch-major:
+ *   semi  [B][cells][65]  int8      desc  [B][cells][256] int8   (cell p = gx*rows + gy)
+ *   fdesc [B][cap][256]   float     kp    [B][cap][2]     float (x, y pixels)
+ *   T     [B][3][4]       float     ([R | t], x1 ~ R x0 + t, |t| = 1)
+ */
+#ifndef MV_MAVERIC_HIP_H
+#define MV_MAVERIC_HIP_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MV_VERSION 100
+
+typedef enum {
+    MV_OK = 0,
+    MV_ERR_INVALID_ARG = -1,
+    MV_ERR_CAPACITY = -2,    /* a validity filter passed `cap` cells (reference: exit(1)) */
+    MV_ERR_HIP = -3,         /* a HIP runtime call failed (mv_last_error_message()) */
+    MV_ERR_NO_DEVICE = -4,   /* no usable gfx950 device: the library never falls back to the CPU */
+    MV_ERR_NO_POINTS = -5,   /* pose requested on an empty correspondence set */
+    MV_ERR_OUT_OF_MEMORY = -6,
+    MV_ERR_DEGENERATE = -7   /* pose: no hypothesis with enough support */
+} mv_status;
+
+typedef enum {
+    MV_AS_BUILT = 0,   /* the reference exactly as it runs: F7 scale, stale-norm/64-dim/int32-wrap match, E = I */
+    MV_AS_INTENDED = 1 /* true scale, exact cosine, real essential-matrix RANSAC + Gauss-Newton */
+} mv_semantics;
+
+typedef struct mv_context mv_context;
+
+int mv_version(void);
+const char *mv_status_string(int status);
+int mv_last_status(void);               /* thread-local status of the last drop-in (void) call */
+const char *mv_last_error_message(void);
+int mv_device_count(void);              /* 0 when no HIP device is visible */
+
+int mv_context_create(int device, mv_context **out);
+int mv_context_destroy(mv_context *ctx);
+int mv_context_set_stream(mv_context *ctx, void *hip_stream); /* NULL: the context's own stream */
+void *mv_context_stream(mv_context *ctx);
+int mv_context_synchronize(mv_context *ctx);
+/* Pre-size scratch for up to `batch` pairs of `cap` keypoints / cells. */
+int mv_context_reserve(mv_context *ctx, int batch, int cap);
+mv_context *mv_default_context(void); /* NULL (and a stderr message) without a device */
+
+/* Kernel profiler: while enabled, every kernel launch is bracketed by two
+ * hipEvents recorded on its own stream (no synchronisation is added).
+ * mv_profile_query() synchronises the recorded events and returns the summed
+ * device time and the launch count of one kernel (e.g. "k_ap_screen"). */
+int mv_profile_enable(int on); /* on != 0 clears previous records */
+int mv_profile_query(const char *kernel, double *total_ms, int *launches);
+
+/* ------------------------------------------------------------------------ */
+/* Windowed int8 front end  (src/top_N.c, src/tracking_main.c:84-194)        */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    int shift_x, shift_y, radius; /* 4, 4, 4            (tracking_main.c:104-106) */
+    int max_matches;              /* 150                (tracking_main.c:13)      */
+    int semantics;                /* mv_semantics                                  */
+    double match_thresh_sq;       /* 0.9 * 0.9          (tracking_main.c:12,155)  */
+    double prob_thresh;           /* 0.2                (tracking_main.c:146)     */
+} mv_window_params;
+void mv_window_params_default(mv_window_params *p);
+
+/* Per-frame / per-pair, host pointers, synchronous on the context's stream. */
+int mv_softmax_host(mv_context *ctx, float scale, const int8_t *semi, int cells, int *num_valid,
+                    int *max_indices, float *probs);
+int mv_top_n_host(mv_context *ctx, float scale, const int8_t *semi, int cells, int N, int cap,
+                  int *num_selected, int *patches, int *indices, float *probs);
+int mv_window_match_host(mv_context *ctx, const mv_window_params *p, int rows, int cols, const int8_t *desc0,
+                         const int *max_idx0, const float *probs0, const int8_t *desc1, int num_queries,
+                         const int *patches1, const int *indices1, int *num_matches, float *points1,
+                         float *points2, int *query_of_match);
+
+/* Batched over B frames: softmax of every cell (compute_softmax, top_N.c:136-165).
+ * scale[B] are the EFFECTIVE scales (apply mv_scale_as_built() for MV_AS_BUILT). */
+int mv_softmax_batch_dev(mv_context *ctx, int batch, int cells, const float *scales, const int8_t *semi,
+                         int *max_idx, float *probs, int *num_valid);
+/* Batched top-N selection from softmax outputs (compute_top_N, top_N.c:53-134).
+ * status[B] = 0 or MV_ERR_CAPACITY.  Outputs [B][N]. */
+int mv_top_n_select_batch_dev(mv_context *ctx, int batch, int cells, const int *max_idx, const float *probs,
+                              int N, int cap, int *num_selected, int *patches, int *indices, float *sel_probs,
+                              int *status);
+/* Batched windowed match (tracking_main.c:103-194).  Queries are the top-N
+ * lists ([B][N] + num_selected[B]); outputs points [B][max_matches][2]. */
+int mv_window_match_batch_dev(mv_context *ctx, const mv_window_params *p, int batch, int rows, int cols,
+                              const int8_t *desc0, const int *max_idx0, const float *probs0, const int8_t *desc1,
+                              int N, const int *num_selected, const int *patches1, const int *indices1,
+                              int *num_matches, float *points1, float *points2, int *query_of_match);
+float mv_scale_as_built(float scale); /* low 32 bits of (double)scale, SURVEY F7 */
+
+/* ------------------------------------------------------------------------ */
+/* All-pairs descriptor match  (python/pairwise_pnp.py:635-659)              */
+/* ------------------------------------------------------------------------ */
+/* For every row i < n0[b] of desc0[b]: the FIRST j < n1[b] attaining the
+ * maximum of the fp32 score s_ij = sum_k d0[i][k]*d1[j][k] (summed k = 0..255
+ * sequentially, mul then add: the gemmini_functions_cpu.h:45-49 order), kept
+ * when (double)s > thresh.  match_idx = -1 otherwise.  Bit-exact: an MFMA
+ * screen plus an exact re-score of every candidate within the rounding bound.
+ * Rows must be finite.  cap = row stride (keypoints per frame slot). */
+int mv_match_allpairs_f32_dev(mv_context *ctx, int batch, int cap, const int *n0, const int *n1,
+                              const float *desc0, const float *desc1, double thresh, int *match_idx,
+                              float *match_score);
+/* int8 descriptors: exact cosine (dot > 0, 100 dot^2 > 81 |a|^2 |b|^2, first
+ * maximum of dot^2/|b|^2); integer-exact (MFMA i8). */
+int mv_match_allpairs_i8_dev(mv_context *ctx, int batch, int cap, const int *n0, const int *n1,
+                             const int8_t *desc0, const int8_t *desc1, int *match_idx, int *match_dot);
+
+/* ------------------------------------------------------------------------ */
+/* Pose  (src/pnp_solver.c; python/pairwise_pnp.py:667-694)                  */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    float fx, fy, cx, cy;  /* intrinsics */
+    int semantics;         /* MV_AS_BUILT: stub RANSAC (E = I) + McAdams pose; MV_AS_INTENDED: below */
+    int hypotheses;        /* RANSAC 8-point hypotheses per pair (as-built: iterations, 10) */
+    float inlier_thresh;   /* as-built: ||E p1 - p2||^2 threshold (1.1); as-intended: Sampson, pixels */
+    int refine_iters;      /* Gauss-Newton iterations on the inliers */
+    unsigned long long seed;
+} mv_pose_params;
+void mv_pose_params_default(mv_pose_params *p, int semantics);
+
+/* Pose from matched points: pts0/pts1 [B][cap][2] pixels, n[b] points.
+ * T[B][3][4], num_inliers[B], status[B]. */
+int mv_pose_batch_dev(mv_context *ctx, const mv_pose_params *p, int batch, int cap, const int *n,
+                      const float *pts0, const float *pts1, float *T, int *num_inliers, int *status);
+/* Pose from an all-pairs match: correspondences (kp0[i], kp1[match_idx[i]]). */
+int mv_pose_from_matches_dev(mv_context *ctx, const mv_pose_params *p, int batch, int cap, const int *n0,
+                             const int *match_idx, const float *kp0, const float *kp1, float *T,
+                             int *num_matches, int *num_inliers, int *status);
+
+/* Single pair, host pointers (the pnp_solver.h drop-ins are built on these). */
+int mv_ransac_stub_host(mv_context *ctx, int n, const float *pts1, const float *pts2, float thresh,
+                        float *best_E, int *best_inliers, int *num_inliers);
+int mv_recover_pose_host(mv_context *ctx, const float *E, float *R1, float *R2, float *t);
+int mv_svd3_host(mv_context *ctx, const float *A, float *U, float *S, float *V);
+
+/* tracking.h with explicit parameters and outputs. */
+typedef struct {
+    mv_window_params window;
+    mv_pose_params pose;
+    int top_n;       /* 100 */
+    int valid_cap;   /* 1000 (MAX_VALID_FEATURES, top_N.c:51) */
+} mv_track_params;
+void mv_track_params_default(mv_track_params *p, int semantics);
+int mv_track_pair_host(mv_context *ctx, const mv_track_params *p, int rows, int cols, float semi_scale0,
+                       const int8_t *semi0, const int8_t *desc0, float semi_scale1, const int8_t *semi1,
+                       const int8_t *desc1, float *T, int *num_matches, float *points1, float *points2);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

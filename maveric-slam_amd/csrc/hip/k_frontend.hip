@@ -1,0 +1,514 @@
+// k_frontend.hip -- the windowed int8 front end of src/tracking_main.c on gfx950:
+//   k_softmax         approx softmax of every cell        (src/top_N.c:12-49,136-165)
+//   k_top_n_select    validity filter + interpolated threshold + ordered
+//                     compaction to N                     (src/top_N.c:53-134)
+//   k_window_eval     one wave per query, lanes = window candidates
+//                                                         (src/tracking_main.c:18-43,114-165)
+//   k_window_compact  query-ordered compaction, cap MAX_NUM_MATCH
+//                                                         (src/tracking_main.c:167-192)
+// All float arithmetic keeps the reference's evaluation order; the TU is built
+// with -ffp-contract=off and IEEE division.  Data are int8 and HBM/L2 bound:
+// no MFMA here (the window dot is 64..256 int8 MACs per candidate, v_dot4).
+#include "mv_internal.hpp"
+
+namespace {
+
+constexpr int kSemiC = 65;
+constexpr int kDescD = 256;
+
+// top_N.c:59-63 ; :12-20
+__device__ __forceinline__ void scale_poly(float scale, float sp[5]) {
+    sp[0] = 1.0f;
+#pragma unroll
+    for (int i = 1; i < 5; i++) sp[i] = sp[i - 1] * scale / (float)i;
+}
+
+__device__ __forceinline__ float approx_exp(const float sp[5], int x) {
+    float acc = 1.0f;
+    int xp = x;
+    acc += sp[1] * (float)xp;
+    xp *= x;
+    acc += sp[2] * (float)xp;
+    xp *= x;
+    acc += sp[3] * (float)xp;
+    xp *= x;
+    acc += sp[4] * (float)xp;
+    return acc;
+}
+
+// ---------------------------------------------------------------------------
+// k_softmax: block = 256 consecutive (frame, cell) rows of 65 int8.
+// The 16,640-byte row block is staged into LDS with coalesced dword loads;
+// each lane then walks its own row (65 logits) in the reference order.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_softmax(int total_rows, int cells, const float *__restrict__ scales,
+                                                 const int8_t *__restrict__ semi, int *__restrict__ max_idx,
+                                                 float *__restrict__ probs, int *__restrict__ num_valid) {
+    __shared__ int lds32[256 * kSemiC / 4];
+    const int8_t *lds8 = reinterpret_cast<const int8_t *>(lds32);
+    const int t = threadIdx.x;
+    const long r0 = (long)blockIdx.x * 256;
+    const int nrows = (int)min((long)256, (long)total_rows - r0);
+    const int nbytes = nrows * kSemiC;
+    const long base = r0 * kSemiC;  // multiple of 4 (256*65 = 16640)
+    const int *g32 = reinterpret_cast<const int *>(semi + base);
+    for (int i = t; i < nbytes / 4; i += 256) lds32[i] = g32[i];
+    for (int i = (nbytes / 4) * 4 + t; i < nbytes; i += 256)
+        reinterpret_cast<int8_t *>(lds32)[i] = semi[base + i];
+    __syncthreads();
+    if (t >= nrows) return;
+    const long r = r0 + t;
+    const int frame = (int)(r / cells);
+    float sp[5];
+    scale_poly(scales[frame], sp);
+    const int8_t *row = lds8 + t * kSemiC;
+    int best = 64;
+    float best_e = 0.0f;
+    float den = 1.17549435e-38f;  // FLT_MIN (top_N.c:30)
+    for (int i = 0; i < kSemiC; i++) {
+        int x = row[i];
+        if (x < 0) continue;
+        float e = approx_exp(sp, x);
+        if (i != 64 && e > best_e) {
+            best_e = e;
+            best = i;
+        }
+        den += e;
+    }
+    max_idx[r] = best;
+    probs[r] = best != 64 ? best_e / den : -1.0f;
+    if (best != 64) atomicAdd(&num_valid[frame], 1);
+}
+
+// ---------------------------------------------------------------------------
+// Block-wide exclusive scan helper (1024 threads = 16 waves).
+// ---------------------------------------------------------------------------
+template <int NT>
+__device__ __forceinline__ int block_exclusive_scan(int v, int *total, int *wsum) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    if (w == 0) {
+        int s = lane < NT / 64 ? wsum[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            int y = __shfl_up(s, o, 64);
+            if (lane >= o) s += y;
+        }
+        if (lane < NT / 64) wsum[lane] = s;  // inclusive wave prefix
+    }
+    __syncthreads();
+    int off = (w > 0 ? wsum[w - 1] : 0) + x - v;
+    *total = wsum[NT / 64 - 1];
+    __syncthreads();
+    return off;
+}
+
+// k_top_n_select: one 1024-thread block per frame; thread t owns the
+// contiguous cells [t*per, (t+1)*per) so that scans preserve patch order.
+__global__ __launch_bounds__(1024) void k_top_n_select(int cells, const int *__restrict__ max_idx,
+                                                       const float *__restrict__ probs, int N, int cap,
+                                                       int *__restrict__ num_sel, int *__restrict__ patches,
+                                                       int *__restrict__ indices, float *__restrict__ sel_probs,
+                                                       int *__restrict__ status) {
+    __shared__ int wsum[16];
+    __shared__ float red_max[16], red_min[16];
+    const int f = blockIdx.x, t = threadIdx.x;
+    const int per = (cells + 1023) / 1024;
+    const int c0 = t * per, c1 = min(c0 + per, cells);
+    const int *mi = max_idx + (long)f * cells;
+    const float *pr = probs + (long)f * cells;
+    int nv_local = 0;
+    float pmax = 0.0f, pmin = 3.40282347e+38f;  // FLT_MAX
+    for (int c = c0; c < c1; c++) {
+        if (mi[c] != 64 && (double)pr[c] > 0.01) {
+            nv_local++;
+            pmax = fmaxf(pmax, pr[c]);
+            pmin = fminf(pmin, pr[c]);
+        }
+    }
+    int nv;
+    int off = block_exclusive_scan<1024>(nv_local, &nv, wsum);
+    // block max / min (exact, order-independent)
+    for (int o = 32; o > 0; o >>= 1) {
+        pmax = fmaxf(pmax, __shfl_xor(pmax, o, 64));
+        pmin = fminf(pmin, __shfl_xor(pmin, o, 64));
+    }
+    if ((t & 63) == 0) {
+        red_max[t >> 6] = pmax;
+        red_min[t >> 6] = pmin;
+    }
+    __syncthreads();
+    if (t == 0) {
+        for (int i = 1; i < 16; i++) {
+            red_max[0] = fmaxf(red_max[0], red_max[i]);
+            red_min[0] = fminf(red_min[0], red_min[i]);
+        }
+    }
+    __syncthreads();
+    pmax = red_max[0];
+    pmin = red_min[0];
+    int *op = patches + (long)f * N;
+    int *oi = indices + (long)f * N;
+    float *opr = sel_probs + (long)f * N;
+    if (nv >= cap) {  // the reference exits here (top_N.c:91-94)
+        if (t == 0) {
+            num_sel[f] = 0;
+            status[f] = MV_ERR_CAPACITY;
+        }
+        return;
+    }
+    if (nv <= N) {
+        int k = off;
+        for (int c = c0; c < c1; c++) {
+            if (mi[c] != 64 && (double)pr[c] > 0.01) {
+                op[k] = c;
+                oi[k] = mi[c];
+                opr[k] = pr[c];
+                k++;
+            }
+        }
+        if (t == 0) {
+            num_sel[f] = nv;
+            status[f] = MV_OK;
+        }
+        return;
+    }
+    const float split = (float)N / (float)nv;
+    const float thr = pmax * split + pmin * (1 - split);
+    int ns_local = 0;
+    for (int c = c0; c < c1; c++)
+        if (mi[c] != 64 && (double)pr[c] > 0.01 && pr[c] >= thr) ns_local++;
+    int ns;
+    int k = block_exclusive_scan<1024>(ns_local, &ns, wsum);
+    for (int c = c0; c < c1 && k < N; c++) {
+        if (mi[c] != 64 && (double)pr[c] > 0.01 && pr[c] >= thr) {
+            op[k] = c;
+            oi[k] = mi[c];
+            opr[k] = pr[c];
+            k++;
+        }
+    }
+    if (t == 0) {
+        num_sel[f] = min(ns, N);
+        status[f] = MV_OK;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Windowed match.
+// ---------------------------------------------------------------------------
+struct WinArgs {
+    int rows, cols, N;
+    int shift_x, shift_y, radius, as_built;
+    double thr_sq, prob_thr;
+};
+
+struct QueryResult {  // one per (pair, query slot), consumed by k_window_compact
+    int found, bx, by, best_index;
+    float score;
+};
+
+__device__ __forceinline__ int wrap_mul(int a, int b) { return (int)((unsigned)a * (unsigned)b); }
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// dot and squared norm of 64 int8 (16 dwords) against q (16 dwords)
+__device__ __forceinline__ void dot64(const int4 *c, const int *q, int &dot, int &nrm) {
+#pragma unroll
+    for (int v = 0; v < 4; v++) {
+        int4 x = c[v];
+        dot = __builtin_amdgcn_sdot4(x.x, q[4 * v + 0], dot, false);
+        dot = __builtin_amdgcn_sdot4(x.y, q[4 * v + 1], dot, false);
+        dot = __builtin_amdgcn_sdot4(x.z, q[4 * v + 2], dot, false);
+        dot = __builtin_amdgcn_sdot4(x.w, q[4 * v + 3], dot, false);
+        nrm = __builtin_amdgcn_sdot4(x.x, x.x, nrm, false);
+        nrm = __builtin_amdgcn_sdot4(x.y, x.y, nrm, false);
+        nrm = __builtin_amdgcn_sdot4(x.z, x.z, nrm, false);
+        nrm = __builtin_amdgcn_sdot4(x.w, x.w, nrm, false);
+    }
+}
+
+// strict "a better than b" for as-intended (dot^2/na) with tie -> lower order
+__device__ __forceinline__ bool exact_better(long long da, long long na, int ka, long long db, long long nb,
+                                             int kb) {
+    if (ka < 0) return false;
+    if (kb < 0) return true;
+    unsigned __int128 l = (unsigned __int128)(unsigned long long)(da * da) * (unsigned long long)nb;
+    unsigned __int128 r = (unsigned __int128)(unsigned long long)(db * db) * (unsigned long long)na;
+    if (l != r) return l > r;
+    return ka < kb;
+}
+
+// one wave per query slot; 4 waves per block
+__global__ __launch_bounds__(256) void k_window_eval(WinArgs a, const int8_t *__restrict__ desc0,
+                                                     const int *__restrict__ max_idx0,
+                                                     const float *__restrict__ probs0,
+                                                     const int8_t *__restrict__ desc1,
+                                                     const int *__restrict__ num_sel,
+                                                     const int *__restrict__ patches1,
+                                                     QueryResult *__restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int qslot = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int pair = blockIdx.y;
+    if (qslot >= a.N) return;
+    QueryResult res = {0, 0, 0, -1, 0.0f};
+    const int nsel = num_sel[pair];
+    const int cells = a.rows * a.cols;
+    if (qslot < nsel) {
+        const int patch1 = __builtin_amdgcn_readfirstlane(patches1[(long)pair * a.N + qslot]);
+        const int x1 = patch1 / a.rows, y1 = patch1 % a.rows;
+        const int8_t *qd = desc1 + ((long)pair * cells + patch1) * kDescD;
+        const int8_t *d0 = desc0 + (long)pair * cells * kDescD;
+        const int *mi0 = max_idx0 + (long)pair * cells;
+        const float *pr0 = probs0 + (long)pair * cells;
+        // query: lane holds dword `lane` (bytes 4*lane .. 4*lane+3) for cooperative 256-D work,
+        // and every lane holds the first 64 bytes for the per-candidate 64-D dot.
+        const int qv = reinterpret_cast<const int *>(qd)[lane];
+        int q64[16];
+#pragma unroll
+        for (int v = 0; v < 16; v++) q64[v] = __shfl(qv, v, 64);
+        const int n2_256 = wave_sum(__builtin_amdgcn_sdot4(qv, qv, 0, false));
+        const int n2_64 = wave_sum(lane < 16 ? __builtin_amdgcn_sdot4(qv, qv, 0, false) : 0);
+
+        int xlo = max(x1 + a.shift_x - a.radius, 0), xhi = min(x1 + a.shift_x + a.radius, a.cols - 1);
+        int ylo = max(y1 + a.shift_y - a.radius, 0), yhi = min(y1 + a.shift_y + a.radius, a.rows - 1);
+        const int ny = yhi - ylo + 1;
+        const int ncand = (xhi >= xlo && yhi >= ylo) ? (xhi - xlo + 1) * ny : 0;
+
+        // as-built latch state (carried across 64-candidate chunks)
+        bool latched = false;
+        int n1f = 0;
+        // running best
+        float best_d = 0.0f;
+        int best_k = -1;
+        long long best_dot = 0, best_na = 1;
+        int best_patch = 0;
+
+        for (int base = 0; base < ncand; base += 64) {
+            const int k = base + lane;
+            int patch0 = 0;
+            bool valid = false;
+            if (k < ncand) {
+                const int x0 = xlo + k / ny, y0 = ylo + k % ny;
+                patch0 = x0 * a.rows + y0;
+                valid = mi0[patch0] != 64 && !((double)pr0[patch0] < a.prob_thr);
+            }
+            const int4 *cd = reinterpret_cast<const int4 *>(d0 + (long)patch0 * kDescD);
+            float d = __builtin_nanf("");
+            long long cdot = 0, cna = 0;
+            if (a.as_built) {
+                int dot_64 = 0, n1_64 = 0;
+                if (valid) dot64(cd, q64, dot_64, n1_64);
+                // resolve the latch: the first valid candidate (scan order) whose
+                // full 256-D norm is non-zero computes the full dot; candidates
+                // before it (all-zero descriptors) divide 0 by 0.
+                unsigned long long vm = __ballot(valid);
+                int f_lane = -1;   // lane of the latching candidate in this chunk
+                int dot_f = 0;
+                while (!latched && vm) {
+                    const int l = __ffsll((long long)vm) - 1;
+                    const int p0 = __shfl(patch0, l, 64);
+                    const int cv = reinterpret_cast<const int *>(d0 + (long)p0 * kDescD)[lane];
+                    const int full_n1 = wave_sum(__builtin_amdgcn_sdot4(cv, cv, 0, false));
+                    const int full_dot = wave_sum(__builtin_amdgcn_sdot4(cv, qv, 0, false));
+                    vm &= vm - 1;
+                    if (full_n1 != 0) {
+                        latched = true;
+                        n1f = full_n1;
+                        f_lane = l;
+                        dot_f = full_dot;
+                    } else if (lane == l) {
+                        d = (float)wrap_mul(full_dot, full_dot) / (float)wrap_mul(full_n1, n2_256);
+                    }
+                }
+                if (valid) {
+                    if (lane == f_lane) {
+                        d = (float)wrap_mul(dot_f, dot_f) / (float)wrap_mul(n1f, n2_256);
+                    } else if (latched && (f_lane < 0 || lane > f_lane)) {
+                        d = (float)wrap_mul(dot_64, dot_64) / (float)wrap_mul(n1f, n2_64);
+                    }
+                }
+                bool pass = valid && (double)d > a.thr_sq;
+                // first strict maximum in scan order: max d, ties -> smallest k
+                float bd = pass ? d : -__builtin_inff();
+                int bk = pass ? k : 0x7fffffff;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    float od = __shfl_xor(bd, o, 64);
+                    int ok = __shfl_xor(bk, o, 64);
+                    if (od > bd || (od == bd && ok < bk)) {
+                        bd = od;
+                        bk = ok;
+                    }
+                }
+                if (bk != 0x7fffffff && (best_k < 0 || bd > best_d)) {
+                    best_d = bd;
+                    best_k = bk;
+                    best_patch = __shfl(patch0, bk - base, 64);
+                }
+            } else {
+                int dot = 0, na = 0;
+                if (valid) {
+                    const int4 *q4 = reinterpret_cast<const int4 *>(qd);  // wave-uniform address
+#pragma unroll
+                    for (int v = 0; v < 16; v++) {
+                        int4 x = cd[v], y = q4[v];
+                        dot = __builtin_amdgcn_sdot4(x.x, y.x, dot, false);
+                        dot = __builtin_amdgcn_sdot4(x.y, y.y, dot, false);
+                        dot = __builtin_amdgcn_sdot4(x.z, y.z, dot, false);
+                        dot = __builtin_amdgcn_sdot4(x.w, y.w, dot, false);
+                        na = __builtin_amdgcn_sdot4(x.x, x.x, na, false);
+                        na = __builtin_amdgcn_sdot4(x.y, x.y, na, false);
+                        na = __builtin_amdgcn_sdot4(x.z, x.z, na, false);
+                        na = __builtin_amdgcn_sdot4(x.w, x.w, na, false);
+                    }
+                }
+                cdot = dot;
+                cna = na;
+                bool pass = valid && dot > 0 && na != 0 && n2_256 != 0 &&
+                            (unsigned __int128)(100ll * cdot * cdot) >
+                                (unsigned __int128)81 * (unsigned long long)(cna * (long long)n2_256);
+                long long bd = pass ? cdot : 0, bn = pass ? cna : 1;
+                int bk = pass ? k : -1;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    long long od = __shfl_xor(bd, o, 64), on = __shfl_xor(bn, o, 64);
+                    int ok = __shfl_xor(bk, o, 64);
+                    if (exact_better(od, on, ok, bd, bn, bk)) {
+                        bd = od;
+                        bn = on;
+                        bk = ok;
+                    }
+                }
+                if (bk >= 0 && exact_better(bd, bn, bk, best_dot, best_na, best_k)) {
+                    best_dot = bd;
+                    best_na = bn;
+                    best_k = bk;
+                    best_d = (float)((double)bd * (double)bd / ((double)bn * (double)n2_256));
+                    best_patch = __shfl(patch0, bk - base, 64);
+                }
+            }
+        }
+        if (best_k >= 0) {
+            res.found = 1;
+            res.bx = xlo + best_k / ny;
+            res.by = ylo + best_k % ny;
+            res.best_index = mi0[best_patch];
+            res.score = best_d;
+        }
+    }
+    if (lane == 0) out[(long)pair * a.N + qslot] = res;
+}
+
+// query-ordered compaction, cap max_matches (tracking_main.c:167-192)
+__global__ __launch_bounds__(1024) void k_window_compact(int N, int rows, int max_matches,
+                                                         const QueryResult *__restrict__ qr,
+                                                         const int *__restrict__ num_sel,
+                                                         const int *__restrict__ patches1,
+                                                         const int *__restrict__ indices1,
+                                                         int *__restrict__ num_matches, float *__restrict__ points1,
+                                                         float *__restrict__ points2, int *__restrict__ qom) {
+    __shared__ int wsum[16];
+    const int pair = blockIdx.x, t = threadIdx.x;
+    const int per = (N + 1023) / 1024;
+    const int q0 = t * per, q1 = min(q0 + per, N);
+    const int nsel = num_sel[pair];
+    const QueryResult *r = qr + (long)pair * N;
+    int cnt = 0;
+    for (int q = q0; q < q1; q++) cnt += (q < nsel && r[q].found) ? 1 : 0;
+    int total;
+    int k = block_exclusive_scan<1024>(cnt, &total, wsum);
+    for (int q = q0; q < q1; q++) {
+        if (!(q < nsel && r[q].found)) continue;
+        if (k < max_matches) {
+            const int patch1 = patches1[(long)pair * N + q];
+            const int x1 = patch1 / rows, y1 = patch1 % rows;
+            const int idx1 = indices1[(long)pair * N + q];
+            const QueryResult m = r[q];
+            float *p1 = points1 + ((long)pair * max_matches + k) * 2;
+            float *p2 = points2 + ((long)pair * max_matches + k) * 2;
+            p1[0] = (float)(m.bx * 8 + m.best_index % 8);
+            p1[1] = (float)(m.by * 8 + m.best_index / 8);
+            p2[0] = (float)(x1 * 8 + idx1 % 8);
+            p2[1] = (float)(y1 * 8 + idx1 / 8);
+            if (qom) qom[(long)pair * max_matches + k] = q;
+        }
+        k++;
+    }
+    if (t == 0) num_matches[pair] = min(total, max_matches);
+}
+
+}  // namespace
+
+namespace mv {
+
+int launch_softmax(hipStream_t s, int batch, int cells, const float *scales, const int8_t *semi, int *max_idx,
+                   float *probs, int *num_valid) {
+    MV_REQUIRE(batch > 0 && cells > 0 && scales && semi && max_idx && probs && num_valid);
+    MV_REQUIRE(((uintptr_t)semi & 3) == 0);
+    const long rows = (long)batch * cells;
+    MV_HIP_TRY(hipMemsetAsync(num_valid, 0, sizeof(int) * batch, s));
+    const int blocks = (int)((rows + 255) / 256);
+    MV_PROF_BEGIN(s, "k_softmax");
+    hipLaunchKernelGGL(k_softmax, dim3(blocks), dim3(256), 0, s, (int)rows, cells, scales, semi, max_idx, probs,
+                       num_valid);
+    MV_PROF_END(s);
+    MV_LAUNCH_CHECK();
+    return MV_OK;
+}
+
+int launch_top_n_select(hipStream_t s, int batch, int cells, const int *max_idx, const float *probs, int N,
+                        int cap, int *num_sel, int *patches, int *indices, float *sel_probs, int *status) {
+    MV_REQUIRE(batch > 0 && cells > 0 && N > 0 && cap > 0);
+    hipLaunchKernelGGL(k_top_n_select, dim3(batch), dim3(1024), 0, s, cells, max_idx, probs, N, cap, num_sel,
+                       patches, indices, sel_probs, status);
+    MV_LAUNCH_CHECK();
+    return MV_OK;
+}
+
+}  // namespace mv
+
+// The window match needs per-query scratch; it is taken from the context.
+extern "C" int mv_window_match_batch_dev(mv_context *ctx, const mv_window_params *p, int batch, int rows, int cols,
+                                         const int8_t *desc0, const int *max_idx0, const float *probs0,
+                                         const int8_t *desc1, int N, const int *num_selected, const int *patches1,
+                                         const int *indices1, int *num_matches, float *points1, float *points2,
+                                         int *query_of_match) {
+    MV_REQUIRE(ctx && p && batch > 0 && rows > 0 && cols > 0 && N > 0 && p->max_matches > 0);
+    MV_REQUIRE(desc0 && max_idx0 && probs0 && desc1 && num_selected && patches1 && indices1);
+    MV_REQUIRE(num_matches && points1 && points2);
+    MV_REQUIRE(((uintptr_t)desc0 & 15) == 0 && ((uintptr_t)desc1 & 15) == 0);
+    MV_HIP_TRY(hipSetDevice(ctx->device));
+    QueryResult *qr = (QueryResult *)mv::scratch(ctx, sizeof(QueryResult) * (size_t)batch * N);
+    if (!qr) return MV_ERR_OUT_OF_MEMORY;
+    WinArgs a;
+    a.rows = rows;
+    a.cols = cols;
+    a.N = N;
+    a.shift_x = p->shift_x;
+    a.shift_y = p->shift_y;
+    a.radius = p->radius;
+    a.as_built = p->semantics == MV_AS_BUILT;
+    a.thr_sq = p->match_thresh_sq;
+    a.prob_thr = p->prob_thresh;
+    MV_PROF_BEGIN(ctx->stream, "k_window_eval");
+    hipLaunchKernelGGL(k_window_eval, dim3((N + 3) / 4, batch), dim3(256), 0, ctx->stream, a, desc0, max_idx0,
+                       probs0, desc1, num_selected, patches1, qr);
+    MV_PROF_END(ctx->stream);
+    MV_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_window_compact, dim3(batch), dim3(1024), 0, ctx->stream, N, rows, p->max_matches, qr,
+                       num_selected, patches1, indices1, num_matches, points1, points2, query_of_match);
+    MV_LAUNCH_CHECK();
+    return MV_OK;
+}

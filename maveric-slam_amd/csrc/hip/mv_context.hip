@@ -1,0 +1,179 @@
+// mv_context.hip -- context, stream, scratch and status plumbing of the C ABI.
+#include <pthread.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "mv_internal.hpp"
+
+namespace {
+thread_local int g_last_status = MV_OK;
+thread_local char g_last_msg[512] = "";
+pthread_once_t g_default_once = PTHREAD_ONCE_INIT;
+mv_context *g_default = nullptr;
+
+void create_default() {
+    int n = mv_device_count();
+    if (n <= 0) {
+        fprintf(stderr,
+                "maveric_hip: no HIP device visible -- this library has no CPU fallback "
+                "(hipGetDeviceCount = %d)\n", n);
+        return;
+    }
+    if (mv_context_create(0, &g_default) != MV_OK) {
+        fprintf(stderr, "maveric_hip: cannot create the default context: %s\n", g_last_msg);
+        g_default = nullptr;
+    }
+}
+}  // namespace
+
+namespace mv {
+void set_error(int status, const char *fmt, ...) {
+    g_last_status = status;
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_last_msg, sizeof g_last_msg, fmt, ap);
+    va_end(ap);
+}
+
+int set_status(int status) {
+    g_last_status = status;
+    if (status == MV_OK) g_last_msg[0] = 0;
+    return status;
+}
+
+void *scratch(mv_context *ctx, size_t bytes) {
+    if (bytes <= ctx->scratch_bytes) return ctx->scratch;
+    if (ctx->scratch) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipFree(ctx->scratch);
+        ctx->scratch = nullptr;
+        ctx->scratch_bytes = 0;
+    }
+    size_t b = align_up(bytes, 1 << 20);
+    if (hipMalloc(&ctx->scratch, b) != hipSuccess) {
+        set_error(MV_ERR_OUT_OF_MEMORY, "scratch allocation of %zu bytes failed", b);
+        ctx->scratch = nullptr;
+        return nullptr;
+    }
+    ctx->scratch_bytes = b;
+    return ctx->scratch;
+}
+
+void *stage(mv_context *ctx, size_t bytes) {
+    if (bytes <= ctx->stage_bytes) return ctx->stage_dev;
+    if (ctx->stage_dev) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipFree(ctx->stage_dev);
+        ctx->stage_dev = nullptr;
+        ctx->stage_bytes = 0;
+    }
+    size_t b = align_up(bytes, 1 << 20);
+    if (hipMalloc(&ctx->stage_dev, b) != hipSuccess) {
+        set_error(MV_ERR_OUT_OF_MEMORY, "staging allocation of %zu bytes failed", b);
+        ctx->stage_dev = nullptr;
+        return nullptr;
+    }
+    ctx->stage_bytes = b;
+    return ctx->stage_dev;
+}
+}  // namespace mv
+
+extern "C" {
+
+int mv_version(void) { return MV_VERSION; }
+
+const char *mv_status_string(int s) {
+    switch (s) {
+        case MV_OK: return "ok";
+        case MV_ERR_INVALID_ARG: return "invalid argument";
+        case MV_ERR_CAPACITY: return "capacity exceeded";
+        case MV_ERR_HIP: return "HIP runtime error";
+        case MV_ERR_NO_DEVICE: return "no HIP device";
+        case MV_ERR_NO_POINTS: return "no correspondences";
+        case MV_ERR_OUT_OF_MEMORY: return "out of device memory";
+        case MV_ERR_DEGENERATE: return "degenerate pose";
+        default: return "unknown status";
+    }
+}
+
+int mv_last_status(void) { return g_last_status; }
+const char *mv_last_error_message(void) { return g_last_msg; }
+
+int mv_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int mv_context_create(int device, mv_context **out) {
+    MV_REQUIRE(out != nullptr);
+    *out = nullptr;
+    int n = mv_device_count();
+    if (device < 0 || device >= n) {
+        mv::set_error(MV_ERR_NO_DEVICE, "device %d requested, %d visible", device, n);
+        return MV_ERR_NO_DEVICE;
+    }
+    hipDeviceProp_t prop;
+    MV_HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        mv::set_error(MV_ERR_NO_DEVICE, "device %d is %s, this build targets gfx950 only", device,
+                      prop.gcnArchName);
+        return MV_ERR_NO_DEVICE;
+    }
+    MV_HIP_TRY(hipSetDevice(device));
+    mv_context *c = new mv_context();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        mv::set_error(MV_ERR_HIP, "hipStreamCreate failed");
+        return MV_ERR_HIP;
+    }
+    c->stream = c->own_stream;
+    *out = c;
+    return mv::set_status(MV_OK);
+}
+
+int mv_context_destroy(mv_context *ctx) {
+    if (!ctx) return MV_OK;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->scratch) (void)hipFree(ctx->scratch);
+    if (ctx->stage_dev) (void)hipFree(ctx->stage_dev);
+    (void)hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+    return MV_OK;
+}
+
+int mv_context_set_stream(mv_context *ctx, void *s) {
+    MV_REQUIRE(ctx != nullptr);
+    ctx->stream = s ? (hipStream_t)s : ctx->own_stream;
+    return MV_OK;
+}
+
+void *mv_context_stream(mv_context *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+int mv_context_synchronize(mv_context *ctx) {
+    MV_REQUIRE(ctx != nullptr);
+    MV_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return MV_OK;
+}
+
+int mv_context_reserve(mv_context *ctx, int batch, int cap) {
+    MV_REQUIRE(ctx != nullptr && batch > 0 && cap > 0);
+    size_t need = mv::allpairs_f32_scratch_bytes(batch, cap);
+    size_t b = mv::allpairs_i8_scratch_bytes(batch, cap);
+    if (b > need) need = b;
+    b = mv::pose_scratch_bytes(batch, cap);
+    if (b > need) need = b;
+    if (!mv::scratch(ctx, need)) return MV_ERR_OUT_OF_MEMORY;
+    return MV_OK;
+}
+
+mv_context *mv_default_context(void) {
+    pthread_once(&g_default_once, create_default);
+    if (g_default) (void)hipSetDevice(g_default->device);
+    return g_default;
+}
+
+}  // extern "C"

@@ -1,0 +1,92 @@
+// mv_internal.hpp -- shared internals of libmaveric_hip.so (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "maveric_hip.h"
+
+struct mv_context {
+    int device;
+    hipStream_t own_stream;
+    hipStream_t stream;  // where every *_dev launch goes
+    void *scratch;       // device scratch, grown by mv_scratch()/mv_context_reserve()
+    size_t scratch_bytes;
+    // small host<->device staging for the single-pair host entry points
+    void *stage_dev;
+    size_t stage_bytes;
+};
+
+namespace mv {
+
+void set_error(int status, const char *fmt, ...);
+int set_status(int status);
+
+// Grow (never shrink) the context scratch; returns nullptr on failure.
+void *scratch(mv_context *ctx, size_t bytes);
+void *stage(mv_context *ctx, size_t bytes);
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Kernel profiler (mv_profile_* in maveric_hip.h): when enabled, launchers
+// bracket each kernel with hipEventRecord on the launch stream -- no sync.
+bool prof_on();
+void prof_begin(hipStream_t s, const char *kernel);
+void prof_end(hipStream_t s);
+
+}  // namespace mv
+
+#define MV_PROF_BEGIN(s, name) \
+    do {                       \
+        if (mv::prof_on()) mv::prof_begin((s), (name)); \
+    } while (0)
+#define MV_PROF_END(s)         \
+    do {                       \
+        if (mv::prof_on()) mv::prof_end(s); \
+    } while (0)
+
+#define MV_HIP_TRY(expr)                                                                   \
+    do {                                                                                   \
+        hipError_t _e = (expr);                                                            \
+        if (_e != hipSuccess) {                                                            \
+            mv::set_error(MV_ERR_HIP, "%s:%d %s: %s", __FILE__, __LINE__, #expr,           \
+                          hipGetErrorString(_e));                                          \
+            return MV_ERR_HIP;                                                             \
+        }                                                                                  \
+    } while (0)
+
+#define MV_LAUNCH_CHECK() MV_HIP_TRY(hipGetLastError())
+
+#define MV_REQUIRE(cond)                                                                   \
+    do {                                                                                   \
+        if (!(cond)) {                                                                     \
+            mv::set_error(MV_ERR_INVALID_ARG, "%s:%d invalid argument: %s", __FILE__,      \
+                          __LINE__, #cond);                                                \
+            return MV_ERR_INVALID_ARG;                                                     \
+        }                                                                                  \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// Launchers implemented in the kernel translation units (stream-ordered).
+// ---------------------------------------------------------------------------
+namespace mv {
+int launch_softmax(hipStream_t s, int batch, int cells, const float *scales, const int8_t *semi,
+                   int *max_idx, float *probs, int *num_valid);
+int launch_top_n_select(hipStream_t s, int batch, int cells, const int *max_idx, const float *probs, int N,
+                        int cap, int *num_sel, int *patches, int *indices, float *sel_probs, int *status);
+size_t allpairs_f32_scratch_bytes(int batch, int cap);
+int launch_allpairs_f32(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
+                        const float *desc0, const float *desc1, double thresh, int *match_idx,
+                        float *match_score);
+size_t allpairs_i8_scratch_bytes(int batch, int cap);
+int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
+                       const int8_t *desc0, const int8_t *desc1, int *match_idx, int *match_dot);
+size_t pose_scratch_bytes(int batch, int cap);
+int launch_pose(hipStream_t s, void *scratch, const mv_pose_params *p, int batch, int cap, const int *n,
+                const float *pts0, const float *pts1, const int *match_idx, const float *kp1, float *T,
+                int *num_matches, int *num_inliers, int *status);
+int launch_ransac_stub(hipStream_t s, int n, const float *pts1, const float *pts2, float thresh, float *E,
+                       int *inliers, int *num_inliers);
+int launch_recover_pose(hipStream_t s, const float *E, float *R1, float *R2, float *t);
+int launch_svd3(hipStream_t s, const float *A, float *U, float *S, float *V);
+}  // namespace mv

@@ -1,0 +1,335 @@
+"""mvtrack -- Python front-end over libmaveric_hip.so (the C ABI of include/*.h).
+
+The product is the C/HIP library; this module only marshals numpy arrays and
+torch device tensors into it (ctypes), for tests, smoke() and bench.py.
+It never computes anything itself and never falls back to the CPU: if the
+library or a gfx950 device is missing, every call raises.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmaveric_hip.so")
+CSRC = os.path.join(HERE, "csrc")
+INCLUDE = os.path.join(os.path.dirname(HERE), "include")
+
+MV_OK = 0
+MV_ERR_INVALID_ARG = -1
+MV_ERR_CAPACITY = -2
+MV_ERR_HIP = -3
+MV_ERR_NO_DEVICE = -4
+MV_ERR_NO_POINTS = -5
+MV_ERR_OUT_OF_MEMORY = -6
+MV_ERR_DEGENERATE = -7
+AS_BUILT = 0
+AS_INTENDED = 1
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+_D = ctypes.c_double
+
+
+class MVError(RuntimeError):
+    pass
+
+
+class WindowParams(ctypes.Structure):
+    _fields_ = [("shift_x", _I), ("shift_y", _I), ("radius", _I), ("max_matches", _I), ("semantics", _I),
+                ("match_thresh_sq", _D), ("prob_thresh", _D)]
+
+
+class PoseParams(ctypes.Structure):
+    _fields_ = [("fx", _F), ("fy", _F), ("cx", _F), ("cy", _F), ("semantics", _I), ("hypotheses", _I),
+                ("inlier_thresh", _F), ("refine_iters", _I), ("seed", ctypes.c_ulonglong)]
+
+
+class TrackParams(ctypes.Structure):
+    _fields_ = [("window", WindowParams), ("pose", PoseParams), ("top_n", _I), ("valid_cap", _I)]
+
+
+def build(force=False):
+    """Compile the HIP library in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
+    cmd = ["make", "-s", "-C", CSRC, "-j8"]
+    if force:
+        subprocess.run(["make", "-s", "-C", CSRC, "clean"], check=True)
+    subprocess.run(cmd, check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        sig = {
+            "mv_version": (_I, []),
+            "mv_status_string": (ctypes.c_char_p, [_I]),
+            "mv_last_status": (_I, []),
+            "mv_last_error_message": (ctypes.c_char_p, []),
+            "mv_device_count": (_I, []),
+            "mv_context_create": (_I, [_I, ctypes.POINTER(_P)]),
+            "mv_context_destroy": (_I, [_P]),
+            "mv_context_set_stream": (_I, [_P, _P]),
+            "mv_context_stream": (_P, [_P]),
+            "mv_context_synchronize": (_I, [_P]),
+            "mv_context_reserve": (_I, [_P, _I, _I]),
+            "mv_default_context": (_P, []),
+            "mv_profile_enable": (_I, [_I]),
+            "mv_profile_query": (_I, [ctypes.c_char_p, ctypes.POINTER(_D), ctypes.POINTER(_I)]),
+            "mv_window_params_default": (None, [_P]),
+            "mv_pose_params_default": (None, [_P, _I]),
+            "mv_track_params_default": (None, [_P, _I]),
+            "mv_scale_as_built": (_F, [_F]),
+            "mv_softmax_host": (_I, [_P, _F, _P, _I, _P, _P, _P]),
+            "mv_top_n_host": (_I, [_P, _F, _P, _I, _I, _I, _P, _P, _P, _P]),
+            "mv_window_match_host": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P]),
+            "mv_softmax_batch_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _P]),
+            "mv_top_n_select_batch_dev": (_I, [_P, _I, _I, _P, _P, _I, _I, _P, _P, _P, _P, _P]),
+            "mv_window_match_batch_dev": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P,
+                                               _P]),
+            "mv_match_allpairs_f32_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _D, _P, _P]),
+            "mv_match_allpairs_i8_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P]),
+            "mv_pose_batch_dev": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P]),
+            "mv_pose_from_matches_dev": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+            "mv_ransac_stub_host": (_I, [_P, _I, _P, _P, _F, _P, _P, _P]),
+            "mv_recover_pose_host": (_I, [_P, _P, _P, _P, _P]),
+            "mv_svd3_host": (_I, [_P, _P, _P, _P, _P]),
+            "mv_track_pair_host": (_I, [_P, _P, _I, _I, _F, _P, _P, _F, _P, _P, _P, _P, _P, _P]),
+            "compute_top_N": (None, [_F, _P, _I, _P, _P, _P, _P]),
+            "compute_softmax": (None, [_F, _P, _P, _P, _P]),
+            "normalize_points": (None, [_I, _P, _P, _P]),
+            "compute_essential_matrix": (None, [_I, _P, _P, _P]),
+            "compute_reprojection_error": (_F, [_P, _P, _P]),
+            "ransac_essential_matrix": (None, [_I, _P, _P, _P, _I, _F, _P, _P, _P]),
+            "recover_pose_from_essential_matrix": (None, [_P, _P, _P, _P]),
+            "track": (_I, [_P, _P, _I, _I, _I, _F, _P]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _np(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _t(x):
+    """device pointer of a torch tensor (or None)"""
+    return None if x is None else ctypes.c_void_p(x.data_ptr())
+
+
+def check(st, what=""):
+    if st != MV_OK:
+        L = lib()
+        raise MVError("%s: %s (%s)" % (what, L.mv_status_string(st).decode(), L.mv_last_error_message().decode()))
+
+
+def device_count():
+    return lib().mv_device_count()
+
+
+def profile_enable(on=True):
+    check(lib().mv_profile_enable(1 if on else 0), "profile_enable")
+
+
+def profile_query(kernel):
+    """(total device ms, launches) of `kernel` since profile_enable(True)."""
+    ms = ctypes.c_double(0)
+    n = ctypes.c_int(0)
+    check(lib().mv_profile_query(kernel.encode(), ctypes.byref(ms), ctypes.byref(n)), "profile_query")
+    return ms.value, n.value
+
+
+def window_params(semantics=AS_BUILT, **kw):
+    p = WindowParams()
+    lib().mv_window_params_default(ctypes.byref(p))
+    p.semantics = semantics
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def pose_params(semantics=AS_INTENDED, **kw):
+    p = PoseParams()
+    lib().mv_pose_params_default(ctypes.byref(p), semantics)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def track_params(semantics=AS_BUILT):
+    p = TrackParams()
+    lib().mv_track_params_default(ctypes.byref(p), semantics)
+    return p
+
+
+def scale_as_built(scale):
+    return float(lib().mv_scale_as_built(float(scale)))
+
+
+class Context:
+    """An mv_context on one device.  `stream` may be a torch.cuda.Stream."""
+
+    def __init__(self, device=0):
+        L = lib()
+        h = ctypes.c_void_p()
+        check(L.mv_context_create(device, ctypes.byref(h)), "mv_context_create")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib().mv_context_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream):
+        ptr = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+        check(lib().mv_context_set_stream(self.h, ptr), "set_stream")
+
+    def synchronize(self):
+        check(lib().mv_context_synchronize(self.h), "synchronize")
+
+    def reserve(self, batch, cap):
+        check(lib().mv_context_reserve(self.h, batch, cap), "reserve")
+
+    # ---------------- host-pointer calls (numpy) ----------------
+    def softmax_host(self, scale, semi):
+        semi = np.ascontiguousarray(semi, np.int8)
+        cells = semi.shape[0]
+        nv = ctypes.c_int(0)
+        mi = np.zeros(cells, np.int32)
+        pr = np.zeros(cells, np.float32)
+        check(lib().mv_softmax_host(self.h, float(scale), _np(semi), cells, ctypes.byref(nv), _np(mi), _np(pr)),
+              "softmax_host")
+        return nv.value, mi, pr
+
+    def top_n_host(self, scale, semi, N, cap=1000):
+        semi = np.ascontiguousarray(semi, np.int8)
+        ns = ctypes.c_int(0)
+        pa = np.zeros(N, np.int32)
+        ix = np.zeros(N, np.int32)
+        pr = np.zeros(N, np.float32)
+        st = lib().mv_top_n_host(self.h, float(scale), _np(semi), semi.shape[0], N, cap, ctypes.byref(ns), _np(pa),
+                                 _np(ix), _np(pr))
+        n = max(ns.value, 0)
+        return st, pa[:n].copy(), ix[:n].copy(), pr[:n].copy()
+
+    def window_match_host(self, params, rows, cols, desc0, max_idx0, probs0, desc1, patches1, indices1):
+        desc0 = np.ascontiguousarray(desc0, np.int8)
+        desc1 = np.ascontiguousarray(desc1, np.int8)
+        max_idx0 = np.ascontiguousarray(max_idx0, np.int32)
+        probs0 = np.ascontiguousarray(probs0, np.float32)
+        patches1 = np.ascontiguousarray(patches1, np.int32)
+        indices1 = np.ascontiguousarray(indices1, np.int32)
+        M = params.max_matches
+        p1 = np.zeros((M, 2), np.float32)
+        p2 = np.zeros((M, 2), np.float32)
+        q = np.zeros(M, np.int32)
+        nm = ctypes.c_int(0)
+        check(lib().mv_window_match_host(self.h, ctypes.byref(params), rows, cols, _np(desc0), _np(max_idx0),
+                                         _np(probs0), _np(desc1), len(patches1), _np(patches1), _np(indices1),
+                                         ctypes.byref(nm), _np(p1), _np(p2), _np(q)), "window_match_host")
+        n = nm.value
+        return p1[:n].copy(), p2[:n].copy(), q[:n].copy()
+
+    def ransac_stub_host(self, pts1, pts2, thresh=1.1):
+        pts1 = np.ascontiguousarray(pts1, np.float32)
+        pts2 = np.ascontiguousarray(pts2, np.float32)
+        n = pts1.shape[0]
+        E = np.zeros(9, np.float32)
+        inl = np.zeros(max(n, 1000), np.int32)
+        ni = ctypes.c_int(0)
+        check(lib().mv_ransac_stub_host(self.h, n, _np(pts1), _np(pts2), float(thresh), _np(E), _np(inl),
+                                        ctypes.byref(ni)), "ransac_stub_host")
+        return E.reshape(3, 3), inl[:ni.value].copy(), ni.value
+
+    def recover_pose_host(self, E):
+        E = np.ascontiguousarray(E, np.float32).reshape(9)
+        R1 = np.zeros(9, np.float32)
+        R2 = np.zeros(9, np.float32)
+        t = np.zeros(3, np.float32)
+        check(lib().mv_recover_pose_host(self.h, _np(E), _np(R1), _np(R2), _np(t)), "recover_pose_host")
+        return R1.reshape(3, 3), R2.reshape(3, 3), t
+
+    def svd3_host(self, A):
+        A = np.ascontiguousarray(A, np.float32).reshape(9)
+        U = np.zeros(9, np.float32)
+        S = np.zeros(3, np.float32)
+        V = np.zeros(9, np.float32)
+        check(lib().mv_svd3_host(self.h, _np(A), _np(U), _np(S), _np(V)), "svd3_host")
+        return U.reshape(3, 3), S, V.reshape(3, 3)
+
+    def track_pair_host(self, params, rows, cols, f0, f1):
+        """f = dict(semi_scale, semi [cells,65] i8, desc [cells,256] i8)"""
+        s0 = np.ascontiguousarray(f0["semi"], np.int8)
+        d0 = np.ascontiguousarray(f0["desc"], np.int8)
+        s1 = np.ascontiguousarray(f1["semi"], np.int8)
+        d1 = np.ascontiguousarray(f1["desc"], np.int8)
+        M = params.window.max_matches
+        T = np.zeros((3, 4), np.float32)
+        p1 = np.zeros((M, 2), np.float32)
+        p2 = np.zeros((M, 2), np.float32)
+        nm = ctypes.c_int(0)
+        st = lib().mv_track_pair_host(self.h, ctypes.byref(params), rows, cols, float(f0["semi_scale"]), _np(s0),
+                                      _np(d0), float(f1["semi_scale"]), _np(s1), _np(d1), _np(T), ctypes.byref(nm),
+                                      _np(p1), _np(p2))
+        n = nm.value
+        return st, T, p1[:n].copy(), p2[:n].copy()
+
+    # ---------------- batched device calls (torch tensors on this device) ----------------
+    def softmax_batch(self, scales, semi, max_idx, probs, num_valid):
+        B, cells = semi.shape[0], semi.shape[1]
+        check(lib().mv_softmax_batch_dev(self.h, B, cells, _t(scales), _t(semi), _t(max_idx), _t(probs),
+                                         _t(num_valid)), "softmax_batch")
+
+    def top_n_select_batch(self, max_idx, probs, N, cap, num_sel, patches, indices, sel_probs, status):
+        B, cells = max_idx.shape[0], max_idx.shape[1]
+        check(lib().mv_top_n_select_batch_dev(self.h, B, cells, _t(max_idx), _t(probs), N, cap, _t(num_sel),
+                                              _t(patches), _t(indices), _t(sel_probs), _t(status)),
+              "top_n_select_batch")
+
+    def window_match_batch(self, params, rows, cols, desc0, max_idx0, probs0, desc1, num_sel, patches1, indices1,
+                           num_matches, points1, points2, query_of_match=None):
+        B, N = patches1.shape[0], patches1.shape[1]
+        check(lib().mv_window_match_batch_dev(self.h, ctypes.byref(params), B, rows, cols, _t(desc0), _t(max_idx0),
+                                              _t(probs0), _t(desc1), N, _t(num_sel), _t(patches1), _t(indices1),
+                                              _t(num_matches), _t(points1), _t(points2), _t(query_of_match)),
+              "window_match_batch")
+
+    def match_allpairs_f32(self, desc0, desc1, n0, n1, match_idx, match_score, thresh=0.8):
+        B, cap = desc0.shape[0], desc0.shape[1]
+        check(lib().mv_match_allpairs_f32_dev(self.h, B, cap, _t(n0), _t(n1), _t(desc0), _t(desc1), float(thresh),
+                                              _t(match_idx), _t(match_score)), "match_allpairs_f32")
+
+    def match_allpairs_i8(self, desc0, desc1, n0, n1, match_idx, match_dot):
+        B, cap = desc0.shape[0], desc0.shape[1]
+        check(lib().mv_match_allpairs_i8_dev(self.h, B, cap, _t(n0), _t(n1), _t(desc0), _t(desc1), _t(match_idx),
+                                             _t(match_dot)), "match_allpairs_i8")
+
+    def pose_batch(self, params, n, pts0, pts1, T, num_inliers, status):
+        B, cap = pts0.shape[0], pts0.shape[1]
+        check(lib().mv_pose_batch_dev(self.h, ctypes.byref(params), B, cap, _t(n), _t(pts0), _t(pts1), _t(T),
+                                      _t(num_inliers), _t(status)), "pose_batch")
+
+    def pose_from_matches(self, params, n0, match_idx, kp0, kp1, T, num_matches, num_inliers, status):
+        B, cap = kp0.shape[0], kp0.shape[1]
+        check(lib().mv_pose_from_matches_dev(self.h, ctypes.byref(params), B, cap, _t(n0), _t(match_idx), _t(kp0),
+                                             _t(kp1), _t(T), _t(num_matches), _t(num_inliers), _t(status)),
+              "pose_from_matches")

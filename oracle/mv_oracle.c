@@ -1,0 +1,597 @@
+/*
+ * mv_oracle.c -- CPU ORACLE (test infrastructure only).
+ *
+ * A clean-room C restatement of the reference's tracking hot path
+ * (rogerhh/maveric-slam @ 2025-01-17).  It is the CHECKER for the HIP product
+ * path: only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+ * may load it.  Nothing in maveric-slam_amd/ links or calls it.
+ *
+ * Pinning (see tests/test_oracle_pinning.py):
+ *   - softmax / top-N / ransac / recover_pose / svd are checked bit-for-bit
+ *     against the reference's own top_N.c + pnp_solver.c + svd.h compiled from
+ *     /root/reference by oracle/Makefile into oracle/_ref/libmv_ref.so;
+ *   - the gemmini matmul restatement against include/gemmini_functions_cpu.h
+ *     compiled the same way;
+ *   - the exact-softmax argmax against include/data/quantized/pair0_gt.h;
+ *   - the windowed match loop (src/tracking_main.c:103-194) cannot be built:
+ *     tracking_main.c includes quantized_pair0.h, which the reference does not
+ *     ship.  Its restatement is pinned through the pinned softmax/top-N stages
+ *     plus committed golden match lists (tests/golden/window_*.npz), i.e.
+ *     "partially pinned" -- see DESIGN.md section Oracle.
+ *
+ * Every arithmetic expression keeps the reference's evaluation order
+ * (float/double promotions included); compile with -ffp-contract=off.
+ */
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORC_EXPORT __attribute__((visibility("default")))
+
+/* ------------------------------------------------------------------------ */
+/* Approximate softmax and top-N                 (src/top_N.c:7-165)        */
+/* ------------------------------------------------------------------------ */
+#define ORC_TAYLOR_TERMS 5 /* top_N.c:7  (P) */
+
+/* F7 of SURVEY.md: tracking_main.c calls compute_softmax/compute_top_N without
+ * a prototype, so the float scale is promoted to double and the callee reads
+ * the low 32 bits of that double as its float argument (x86-64 SysV ABI). */
+ORC_EXPORT float orc_scale_as_built(float scale) {
+    double d = (double)scale;
+    uint64_t bits;
+    memcpy(&bits, &d, sizeof bits);
+    uint32_t lo = (uint32_t)(bits & 0xffffffffu);
+    float f;
+    memcpy(&f, &lo, sizeof f);
+    return f;
+}
+
+/* top_N.c:59-63 (and again :141-145): sp[i] = sp[i-1] * scale / i */
+static void orc_scale_poly(float scale, float sp[ORC_TAYLOR_TERMS]) {
+    sp[0] = 1.0f;
+    for (int i = 1; i < ORC_TAYLOR_TERMS; i++) sp[i] = sp[i - 1] * scale / (float)i;
+}
+
+/* top_N.c:12-20: 1 + sum_{i=1..4} sp[i] * x^i, x^i as an int */
+ORC_EXPORT float orc_approx_exp(const float *sp, int8_t x) {
+    float acc = 1.0f;
+    int32_t xp = x;
+    for (int i = 1; i < ORC_TAYLOR_TERMS; i++) {
+        acc += sp[i] * (float)xp;
+        if (i + 1 < ORC_TAYLOR_TERMS) xp *= x; /* the reference also forms x^5 (unused) */
+    }
+    return acc;
+}
+
+/* top_N.c:22-49 */
+static void orc_approx_softmax(const float *sp, const int8_t *row, int *max_index, float *max_prob) {
+    int best = 64;
+    float best_e = 0.0f;
+    float den = FLT_MIN;
+    for (int i = 0; i < 65; i++) {
+        if (row[i] < 0) continue;
+        float e = orc_approx_exp(sp, row[i]);
+        if (i != 64 && e > best_e) {
+            best_e = e;
+            best = i;
+        }
+        den += e;
+    }
+    *max_index = best;
+    *max_prob = best_e / den;
+}
+
+/* top_N.c:136-165.  `cells` generalises the hard-coded 1920. */
+ORC_EXPORT void orc_compute_softmax(float scale, const int8_t *semi, int cells, int *num_valid,
+                                    int *max_indices, float *probs) {
+    float sp[ORC_TAYLOR_TERMS];
+    orc_scale_poly(scale, sp);
+    for (int c = 0; c < cells; c++) {
+        int mi;
+        float pr;
+        orc_approx_softmax(sp, semi + (size_t)c * 65, &mi, &pr);
+        max_indices[c] = mi;
+        if (mi != 64) {
+            probs[c] = pr;
+            (*num_valid)++;
+        } else {
+            probs[c] = -1.0f;
+        }
+    }
+}
+
+/* top_N.c:53-134.  Returns 0, or -1 where the reference calls exit(1)
+ * (num_valid reaching `cap`, MAX_VALID_FEATURES=1000 at :51,91-94). */
+ORC_EXPORT int orc_compute_top_N(float scale, const int8_t *semi, int cells, int N, int cap,
+                                 int *num_selected, int *N_patches, int *N_indices, float *N_probs) {
+    float sp[ORC_TAYLOR_TERMS];
+    orc_scale_poly(scale, sp);
+    *num_selected = 0;
+    int *vp = (int *)malloc(sizeof(int) * (size_t)cap);
+    int *vi = (int *)malloc(sizeof(int) * (size_t)cap);
+    float *vpr = (float *)malloc(sizeof(float) * (size_t)cap);
+    float pmax = 0.0f, pmin = FLT_MAX;
+    int nv = 0, status = 0;
+    for (int c = 0; c < cells; c++) {
+        int mi = 64;
+        float pr = -1.0f;
+        orc_approx_softmax(sp, semi + (size_t)c * 65, &mi, &pr);
+        if (mi != 64 && (double)pr > 0.01) {
+            vp[nv] = c;
+            vi[nv] = mi;
+            vpr[nv] = pr;
+            if (pr > pmax) pmax = pr;
+            if (pr < pmin) pmin = pr;
+            nv++;
+            if (nv >= cap) {
+                status = -1;
+                goto done;
+            }
+        }
+    }
+    if (nv <= N) {
+        *num_selected = nv;
+        for (int k = 0; k < nv; k++) {
+            N_patches[k] = vp[k];
+            N_indices[k] = vi[k];
+            N_probs[k] = vpr[k];
+        }
+        goto done;
+    }
+    {
+        float split = (float)N / (float)nv;
+        float thr = pmax * split + pmin * (1 - split);
+        for (int k = 0; k < nv; k++) {
+            if (vpr[k] >= thr) {
+                N_patches[*num_selected] = vp[k];
+                N_indices[*num_selected] = vi[k];
+                N_probs[*num_selected] = vpr[k];
+                (*num_selected)++;
+                if (*num_selected >= N) break;
+            }
+        }
+    }
+done:
+    free(vp);
+    free(vi);
+    free(vpr);
+    return status;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Windowed int8 descriptor match              (src/tracking_main.c:18-194) */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    int shift_x, shift_y, radius; /* tracking_main.c:104-106 (4,4,4) */
+    int max_matches;              /* MAX_NUM_MATCH 150, :13 */
+    int as_built;                 /* 1: stale-norm / 64-dim / int32-wrap (F8); 0: exact cosine */
+} orc_window_params;
+
+static int32_t wrap_mul(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
+
+/* Returns the number of matches; points are [max_matches][2] (x, y) pixels.
+ * q_of_match (optional) receives the query slot i of each match. */
+ORC_EXPORT int orc_window_match(int rows, int cols, const int8_t *desc0, const int *max_idx0,
+                                const float *probs0, const int8_t *desc1, int nq, const int *patches1,
+                                const int *indices1, const orc_window_params *p, float *points1,
+                                float *points2, int *q_of_match, float *score_of_match) {
+    int nm = 0;
+    for (int i = 0; i < nq; i++) {
+        int patch1 = patches1[i];
+        int x1 = patch1 / rows, y1 = patch1 % rows; /* patch_to_grid, :59-62 */
+        const int8_t *q = desc1 + (size_t)patch1 * 256;
+        int found = 0, best_index = -1, bx = 0, by = 0;
+        float best = 0.0f;
+        int64_t bdot = 0, bn1 = 0; /* as-intended running best (exact rational) */
+        int xlo = x1 + p->shift_x - p->radius, xhi = x1 + p->shift_x + p->radius;
+        int ylo = y1 + p->shift_y - p->radius, yhi = y1 + p->shift_y + p->radius;
+        if (xlo < 0) xlo = 0;
+        if (xhi > cols - 1) xhi = cols - 1;
+        if (ylo < 0) ylo = 0;
+        if (yhi > rows - 1) yhi = rows - 1;
+        int32_t n1 = 0; /* :133, reset per query, latched by the first candidate */
+        for (int x0 = xlo; x0 <= xhi; x0++) {
+            for (int y0 = ylo; y0 <= yhi; y0++) {
+                int patch0 = x0 * rows + y0; /* grid_to_patch, :64-66 */
+                int idx0 = max_idx0[patch0];
+                if (idx0 == 64) continue;
+                if ((double)probs0[patch0] < 0.2) continue; /* :146 */
+                const int8_t *c = desc0 + (size_t)patch0 * 256;
+                if (p->as_built) {
+                    /* squared_dist(desc0, desc1, ...) :18-43 -- note the argument order:
+                     * its "desc1/norm1" is the CANDIDATE, "desc2/norm2" the query. */
+                    int32_t dot = 0, n2 = 0;
+                    if (n1 == 0) {
+                        for (int k = 0; k < 256; k++) {
+                            dot += c[k] * q[k];
+                            n1 += c[k] * c[k];
+                            n2 += q[k] * q[k];
+                        }
+                    } else {
+                        for (int k = 0; k < 64; k++) {
+                            dot += c[k] * q[k];
+                            n2 += q[k] * q[k];
+                        }
+                    }
+                    /* :154  (int)dot*dot / (float)(int)(n1*n2), both products wrap */
+                    float d = (float)wrap_mul(dot, dot) / (float)wrap_mul(n1, n2);
+                    if ((double)d > 0.9 * 0.9) { /* :155, MATCH_THRESHOLD^2 in double */
+                        if (!found || d > best) {
+                            found = 1;
+                            best_index = idx0;
+                            best = d;
+                            bx = x0;
+                            by = y0;
+                        }
+                    }
+                } else {
+                    int64_t dot = 0, na = 0, nb = 0;
+                    for (int k = 0; k < 256; k++) {
+                        dot += c[k] * q[k];
+                        na += c[k] * c[k];
+                        nb += q[k] * q[k];
+                    }
+                    if (dot <= 0 || na == 0 || nb == 0) continue;
+                    /* cos > 0.9  <=>  100 dot^2 > 81 na nb   (exact) */
+                    if ((unsigned __int128)(100 * dot * dot) <= (unsigned __int128)81 * (uint64_t)(na * nb))
+                        continue;
+                    /* strictly better: dot^2/na > bdot^2/bn1 */
+                    int better = !found ||
+                                 (unsigned __int128)(dot * dot) * (uint64_t)bn1 >
+                                     (unsigned __int128)(bdot * bdot) * (uint64_t)na;
+                    if (better) {
+                        found = 1;
+                        best_index = idx0;
+                        bdot = dot;
+                        bn1 = na;
+                        best = (float)((double)dot * (double)dot / ((double)na * (double)nb));
+                        bx = x0;
+                        by = y0;
+                    }
+                }
+            }
+        }
+        if (found && nm < p->max_matches) { /* :167-188 */
+            int idx1 = indices1[i];
+            points1[nm * 2 + 0] = (float)(bx * 8 + best_index % 8);
+            points1[nm * 2 + 1] = (float)(by * 8 + best_index / 8);
+            points2[nm * 2 + 0] = (float)(x1 * 8 + idx1 % 8);
+            points2[nm * 2 + 1] = (float)(y1 * 8 + idx1 / 8);
+            if (q_of_match) q_of_match[nm] = i;
+            if (score_of_match) score_of_match[nm] = best;
+            nm++;
+        }
+        if (nm >= p->max_matches) break; /* :190-192 */
+    }
+    return nm;
+}
+
+/* ------------------------------------------------------------------------ */
+/* McAdams et al. 3x3 SVD (TR1690, 2011)            (include/svd/svd.h)     */
+/* Restated with the same float/double evaluation order.                     */
+/* ------------------------------------------------------------------------ */
+static float orc_rsqrt(float x) { /* svd.h:37-48, one Newton step */
+    float h = 0.5f * x;
+    int32_t i;
+    memcpy(&i, &x, 4);
+    i = 0x5f375a82 - (i >> 1);
+    float y;
+    memcpy(&y, &i, 4);
+    return y * (1.5f - h * y * y);
+}
+
+static float orc_rsqrt2(float x) { /* svd.h:54-62, two Newton steps */
+    float h = 0.5f * x;
+    int32_t i;
+    memcpy(&i, &x, 4);
+    i = 0x5f37599e - (i >> 1);
+    float y;
+    memcpy(&y, &i, 4);
+    y = y * (1.5f - h * y * y);
+    return y * (1.5f - h * y * y);
+}
+
+/* Symmetric 3x3 stored as s[0]=s11 s[1]=s21 s[2]=s22 s[3]=s31 s[4]=s32 s[5]=s33;
+ * quaternion q = (x, y, z, w).  One Jacobi conjugation (svd.h:148-216). */
+static void orc_jacobi_step(int x, int y, int z, float s[6], float q[4]) {
+    float ch = 2 * (s[0] - s[2]), sh = s[1];
+    int take = 5.828427124 * sh * sh < (double)(ch * ch); /* gamma test in double */
+    float w = orc_rsqrt(ch * ch + sh * sh);
+    ch = take ? w * ch : (float)0.923879532;
+    sh = take ? w * sh : (float)0.3826834323;
+
+    float sc = ch * ch + sh * sh;
+    float a = (ch * ch - sh * sh) / sc;
+    float b = (2 * sh * ch) / sc;
+    float t11 = s[0], t21 = s[1], t22 = s[2], t31 = s[3], t32 = s[4], t33 = s[5];
+    float n11 = a * (a * t11 + b * t21) + b * (a * t21 + b * t22);
+    float n21 = a * (-b * t11 + a * t21) + b * (-b * t21 + a * t22);
+    float n22 = -b * (-b * t11 + a * t21) + a * (-b * t21 + a * t22);
+    float n31 = a * t31 + b * t32;
+    float n32 = -b * t31 + a * t32;
+    float n33 = t33;
+
+    float tq[3] = {q[0] * sh, q[1] * sh, q[2] * sh};
+    sh *= q[3];
+    q[0] *= ch;
+    q[1] *= ch;
+    q[2] *= ch;
+    q[3] *= ch;
+    q[z] += sh;
+    q[3] -= tq[z];
+    q[x] += tq[y];
+    q[y] -= tq[x];
+
+    /* cyclic relabel for the next pair */
+    s[0] = n22;
+    s[1] = n32;
+    s[2] = n33;
+    s[3] = n21;
+    s[4] = n31;
+    s[5] = n11;
+}
+
+static void orc_qr_givens(float a1, float a2, float *ch, float *sh) { /* svd.h:277-291 */
+    float eps = (float)1e-6;
+    float r2 = a1 * a1 + a2 * a2;
+    float rho = r2 * orc_rsqrt2(r2);
+    float s = rho > eps ? a2 : 0;
+    float c = fabsf(a1) + fmaxf(rho, eps);
+    if (a1 < 0) {
+        float t = s;
+        s = c;
+        c = t;
+    }
+    float w = orc_rsqrt(c * c + s * s);
+    *ch = c * w;
+    *sh = s * w;
+}
+
+/* A, U, V row-major 3x3; S the diagonal of R.  Mirrors svd() (svd.h:358-405)
+ * and call_svd()'s outputs (pnp_solver.c:8-25): the third output is V, not V^T. */
+ORC_EXPORT void orc_svd3(const float *A, float *U, float *S, float *V) {
+    float a[3][3];
+    for (int i = 0; i < 9; i++) a[i / 3][i % 3] = A[i];
+    /* A^T A, each entry summed k = 0,1,2 left to right (multAtB, :105-120) */
+    float m[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) m[i][j] = a[0][i] * a[0][j] + a[1][i] * a[1][j] + a[2][i] * a[2][j];
+    float s[6] = {m[0][0], m[1][0], m[1][1], m[2][0], m[2][1], m[2][2]};
+    float q[4] = {0, 0, 0, 1};
+    for (int sweep = 0; sweep < 4; sweep++) { /* jacobiEigenanlysis, :226-244 */
+        orc_jacobi_step(0, 1, 2, s, q);
+        orc_jacobi_step(1, 2, 0, s, q);
+        orc_jacobi_step(2, 0, 1, s, q);
+    }
+    /* quaternion -> V (quatToMat3, :122-146) */
+    float qx = q[0], qy = q[1], qz = q[2], qw = q[3];
+    float xx = qx * qx, yy = qy * qy, zz = qz * qz, xz = qx * qz, xy = qx * qy, yz = qy * qz;
+    float wx = qw * qx, wy = qw * qy, wz = qw * qz;
+    float v[3][3] = {{1 - 2 * (yy + zz), 2 * (xy - wz), 2 * (xz + wy)},
+                     {2 * (xy + wz), 1 - 2 * (xx + zz), 2 * (yz - wx)},
+                     {2 * (xz - wy), 2 * (yz + wx), 1 - 2 * (xx + yy)}};
+    /* B = A V (multAB, :86-102) */
+    float bm[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) bm[i][j] = a[i][0] * v[0][j] + a[i][1] * v[1][j] + a[i][2] * v[2][j];
+    /* sort columns by descending norm with sign-flipping swaps (:247-274) */
+    float rho[3];
+    for (int j = 0; j < 3; j++) rho[j] = bm[0][j] * bm[0][j] + bm[1][j] * bm[1][j] + bm[2][j] * bm[2][j];
+    static const int pairs[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+    for (int pidx = 0; pidx < 3; pidx++) {
+        int c0 = pairs[pidx][0], c1 = pairs[pidx][1];
+        if (rho[c0] < rho[c1]) {
+            for (int r = 0; r < 3; r++) {
+                float t = -bm[r][c0];
+                bm[r][c0] = bm[r][c1];
+                bm[r][c1] = t;
+                t = -v[r][c0];
+                v[r][c0] = v[r][c1];
+                v[r][c1] = t;
+            }
+            if (pidx < 2) {
+                float t = rho[c0];
+                rho[c0] = rho[c1];
+                rho[c1] = t;
+            }
+        }
+    }
+    /* QR by three Givens rotations (QRDecomposition, :294-356) */
+    float ch1, sh1, ch2, sh2, ch3, sh3, ga, gb;
+    float r[3][3];
+    orc_qr_givens(bm[0][0], bm[1][0], &ch1, &sh1);
+    ga = 1 - 2 * sh1 * sh1;
+    gb = 2 * ch1 * sh1;
+    for (int j = 0; j < 3; j++) {
+        r[0][j] = ga * bm[0][j] + gb * bm[1][j];
+        r[1][j] = -gb * bm[0][j] + ga * bm[1][j];
+        r[2][j] = bm[2][j];
+    }
+    orc_qr_givens(r[0][0], r[2][0], &ch2, &sh2);
+    ga = 1 - 2 * sh2 * sh2;
+    gb = 2 * ch2 * sh2;
+    for (int j = 0; j < 3; j++) {
+        float top = ga * r[0][j] + gb * r[2][j];
+        float bot = -gb * r[0][j] + ga * r[2][j];
+        bm[0][j] = top;
+        bm[1][j] = r[1][j];
+        bm[2][j] = bot;
+    }
+    orc_qr_givens(bm[1][1], bm[2][1], &ch3, &sh3);
+    ga = 1 - 2 * sh3 * sh3;
+    gb = 2 * ch3 * sh3;
+    for (int j = 0; j < 3; j++) {
+        r[0][j] = bm[0][j];
+        r[1][j] = ga * bm[1][j] + gb * bm[2][j];
+        r[2][j] = -gb * bm[1][j] + ga * bm[2][j];
+    }
+    float p1 = sh1 * sh1, p2 = sh2 * sh2, p3 = sh3 * sh3;
+    U[0] = (-1 + 2 * p1) * (-1 + 2 * p2);
+    U[1] = 4 * ch2 * ch3 * (-1 + 2 * p1) * sh2 * sh3 + 2 * ch1 * sh1 * (-1 + 2 * p3);
+    U[2] = 4 * ch1 * ch3 * sh1 * sh3 - 2 * ch2 * (-1 + 2 * p1) * sh2 * (-1 + 2 * p3);
+    U[3] = 2 * ch1 * sh1 * (1 - 2 * p2);
+    U[4] = -8 * ch1 * ch2 * ch3 * sh1 * sh2 * sh3 + (-1 + 2 * p1) * (-1 + 2 * p3);
+    U[5] = -2 * ch3 * sh3 + 4 * sh1 * (ch3 * sh1 * sh3 + ch1 * ch2 * sh2 * (-1 + 2 * p3));
+    U[6] = 2 * ch2 * sh2;
+    U[7] = 2 * ch3 * (1 - 2 * p2) * sh3;
+    U[8] = (-1 + 2 * p2) * (-1 + 2 * p3);
+    S[0] = r[0][0];
+    S[1] = r[1][1];
+    S[2] = r[2][2];
+    for (int i = 0; i < 9; i++) V[i] = v[i / 3][i % 3];
+}
+
+/* ------------------------------------------------------------------------ */
+/* Pose: stub essential-matrix RANSAC + pose recovery (src/pnp_solver.c)    */
+/* ------------------------------------------------------------------------ */
+ORC_EXPORT void orc_normalize_points(int n, const float *pts, const float *K, float *out) { /* :28-34 */
+    for (int i = 0; i < n; i++) {
+        out[2 * i + 0] = (pts[2 * i + 0] - K[2]) / K[0];
+        out[2 * i + 1] = (pts[2 * i + 1] - K[5]) / K[4];
+    }
+}
+
+ORC_EXPORT float orc_reprojection_error(const float *p1, const float *p2, const float *E) { /* :89-105 */
+    float h1[3] = {p1[0], p1[1], 1.0f}, h2[3] = {p2[0], p2[1], 1.0f};
+    float err = 0;
+    for (int i = 0; i < 3; i++) {
+        float t = E[3 * i + 0] * h1[0] + E[3 * i + 1] * h1[1] + E[3 * i + 2] * h1[2];
+        float d = t - h2[i];
+        err += d * d;
+    }
+    return err;
+}
+
+/* :110-165 with the stubbed solve of :36-86 (E == I whatever the sample).
+ * The 8 sample indices per iteration are drawn with libc rand() exactly as
+ * the reference does, so the caller's rand() stream advances identically.
+ * Returns -1 for n <= 0 (the reference divides by zero, :123). */
+ORC_EXPORT int orc_ransac_essential_matrix(int n, const float *pts1, const float *pts2, const float *K,
+                                           int iters, float thr, float *best_E, int *best_inliers,
+                                           int *num_inliers) {
+    (void)K;
+    if (n <= 0) return -1;
+    int best = 0;
+    int *inl = (int *)malloc(sizeof(int) * 1000);
+    for (int it = 0; it < iters; it++) {
+        for (int s = 0; s < 8; s++) (void)(rand() % n);
+        float E[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+        int cnt = 0;
+        for (int i = 0; i < n; i++) {
+            float e = orc_reprojection_error(pts1 + 2 * i, pts2 + 2 * i, E);
+            if (e < thr && cnt < 1000) inl[cnt++] = i;
+        }
+        if (cnt > best || cnt == 1000) {
+            best = cnt;
+            *num_inliers = cnt;
+            memcpy(best_E, E, sizeof E);
+            memcpy(best_inliers, inl, sizeof(int) * (size_t)cnt);
+        }
+    }
+    free(inl);
+    return 0;
+}
+
+/* :168-194: R1 = U W, R2 = U W^T, t = U[:,2] */
+ORC_EXPORT void orc_recover_pose(const float *E, float *R1, float *R2, float *t) {
+    float U[9], S[3], V[9];
+    orc_svd3(E, U, S, V);
+    static const float W[9] = {0, -1, 0, 1, 0, 0, 0, 0, 1};
+    static const float Wt[9] = {0, 1, 0, -1, 0, 0, 0, 0, 1};
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            R1[3 * i + j] = U[3 * i + 0] * W[j] + U[3 * i + 1] * W[3 + j] + U[3 * i + 2] * W[6 + j];
+            R2[3 * i + j] = U[3 * i + 0] * Wt[j] + U[3 * i + 1] * Wt[3 + j] + U[3 * i + 2] * Wt[6 + j];
+        }
+    for (int i = 0; i < 3; i++) t[i] = U[3 * i + 2];
+}
+
+/* ------------------------------------------------------------------------ */
+/* All-pairs fp32 match (python/pairwise_pnp.py:635-659) on the             */
+/* gemmini_functions_cpu.h:14-56 summation order (k = 0..K-1, mul then add) */
+/* ------------------------------------------------------------------------ */
+ORC_EXPORT void orc_matmul_nt(int I, int J, int Kd, const float *A, const float *B, float *C) {
+    for (int i = 0; i < I; i++)
+        for (int j = 0; j < J; j++) {
+            float acc = C[(size_t)i * J + j];
+            const float *a = A + (size_t)i * Kd, *b = B + (size_t)j * Kd;
+            for (int k = 0; k < Kd; k++) acc += a[k] * b[k];
+            C[(size_t)i * J + j] = acc;
+        }
+}
+
+/* First strict maximum over j of the exact score, kept only if > thresh
+ * (double compare).  idx = -1 where no j qualifies. */
+ORC_EXPORT void orc_allpairs_f32(const float *d0, int n0, const float *d1, int n1, int dim, double thresh,
+                                 int *idx, float *score) {
+    for (int i = 0; i < n0; i++) {
+        const float *a = d0 + (size_t)i * dim;
+        int best = -1;
+        float bs = 0.0f;
+        for (int j = 0; j < n1; j++) {
+            const float *b = d1 + (size_t)j * dim;
+            float s = 0.0f;
+            for (int k = 0; k < dim; k++) s += a[k] * b[k];
+            if ((double)s > thresh && s > bs) {
+                bs = s;
+                best = j;
+            }
+        }
+        idx[i] = best;
+        score[i] = best >= 0 ? bs : 0.0f;
+    }
+}
+
+/* Row-argmax over a precomputed score matrix (the gemmini baseline's epilogue). */
+ORC_EXPORT void orc_row_argmax(const float *S, int n0, int n1, double thresh, int *idx, float *score) {
+    for (int i = 0; i < n0; i++) {
+        int best = -1;
+        float bs = 0.0f;
+        for (int j = 0; j < n1; j++) {
+            float s = S[(size_t)i * n1 + j];
+            if ((double)s > thresh && s > bs) {
+                bs = s;
+                best = j;
+            }
+        }
+        idx[i] = best;
+        score[i] = best >= 0 ? bs : 0.0f;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* All-pairs int8 match (exact cosine, as-intended squared_dist semantics)  */
+/* ------------------------------------------------------------------------ */
+ORC_EXPORT void orc_allpairs_i8(const int8_t *d0, int n0, const int8_t *d1, int n1, int *idx, int *dot_out) {
+    int64_t *nb = (int64_t *)malloc(sizeof(int64_t) * (size_t)(n1 > 0 ? n1 : 1));
+    for (int j = 0; j < n1; j++) {
+        int64_t s = 0;
+        for (int k = 0; k < 256; k++) s += d1[(size_t)j * 256 + k] * d1[(size_t)j * 256 + k];
+        nb[j] = s;
+    }
+    for (int i = 0; i < n0; i++) {
+        const int8_t *a = d0 + (size_t)i * 256;
+        int64_t na = 0;
+        for (int k = 0; k < 256; k++) na += a[k] * a[k];
+        int best = -1;
+        int64_t bd = 0, bn = 1;
+        for (int j = 0; j < n1; j++) {
+            const int8_t *b = d1 + (size_t)j * 256;
+            int64_t dot = 0;
+            for (int k = 0; k < 256; k++) dot += a[k] * b[k];
+            if (dot <= 0 || na == 0 || nb[j] == 0) continue;
+            if ((unsigned __int128)(100 * dot * dot) <= (unsigned __int128)81 * (uint64_t)(na * nb[j])) continue;
+            if (best < 0 || (unsigned __int128)(dot * dot) * (uint64_t)bn >
+                                (unsigned __int128)(bd * bd) * (uint64_t)nb[j]) {
+                best = j;
+                bd = dot;
+                bn = nb[j];
+            }
+        }
+        idx[i] = best;
+        dot_out[i] = best >= 0 ? (int)bd : 0;
+    }
+    free(nb);
+}

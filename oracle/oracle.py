@@ -1,0 +1,220 @@
+"""ctypes front-end to the CPU ORACLE (oracle/liboracle.so) and, when built,
+to the reference's own code compiled by oracle/Makefile (oracle/_ref/libmv_ref.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, never by the product package (maveric-slam_amd/).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liboracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libmv_ref.so")
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+_D = ctypes.c_double
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            build()
+        L = ctypes.CDLL(ORACLE_SO)
+        L.orc_scale_as_built.restype = _F
+        L.orc_scale_as_built.argtypes = [_F]
+        L.orc_approx_exp.restype = _F
+        L.orc_compute_softmax.argtypes = [_F, _P, _I, _P, _P, _P]
+        L.orc_compute_top_N.restype = _I
+        L.orc_compute_top_N.argtypes = [_F, _P, _I, _I, _I, _P, _P, _P, _P]
+        L.orc_window_match.restype = _I
+        L.orc_window_match.argtypes = [_I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P]
+        L.orc_svd3.argtypes = [_P, _P, _P, _P]
+        L.orc_normalize_points.argtypes = [_I, _P, _P, _P]
+        L.orc_reprojection_error.restype = _F
+        L.orc_reprojection_error.argtypes = [_P, _P, _P]
+        L.orc_ransac_essential_matrix.restype = _I
+        L.orc_ransac_essential_matrix.argtypes = [_I, _P, _P, _P, _I, _F, _P, _P, _P]
+        L.orc_recover_pose.argtypes = [_P, _P, _P, _P]
+        L.orc_matmul_nt.argtypes = [_I, _I, _I, _P, _P, _P]
+        L.orc_allpairs_f32.argtypes = [_P, _I, _P, _I, _I, _D, _P, _P]
+        L.orc_row_argmax.argtypes = [_P, _I, _I, _D, _P, _P]
+        L.orc_allpairs_i8.argtypes = [_P, _I, _P, _I, _P, _P]
+        _lib = L
+    return _lib
+
+
+def ref_available():
+    return os.path.exists(REF_SO)
+
+
+_ref = None
+
+
+def ref():
+    """The reference's own top_N.c / pnp_solver.c / svd.h / gemmini matmul."""
+    global _ref
+    if _ref is None:
+        R = ctypes.CDLL(REF_SO)
+        R.compute_softmax.argtypes = [_F, _P, _P, _P, _P]
+        R.compute_top_N.argtypes = [_F, _P, _I, _P, _P, _P, _P]
+        R.normalize_points.argtypes = [_I, _P, _P, _P]
+        R.compute_reprojection_error.restype = _F
+        R.compute_reprojection_error.argtypes = [_P, _P, _P]
+        R.ransac_essential_matrix.argtypes = [_I, _P, _P, _P, _I, _F, _P, _P, _P]
+        R.recover_pose_from_essential_matrix.argtypes = [_P, _P, _P, _P]
+        R.call_svd.argtypes = [_P, _P, _P, _P]
+        R.ref_matmul_nt.argtypes = [_I, _I, _I, _P, _P, _P]
+        _ref = R
+    return _ref
+
+
+# --------------------------------------------------------------------------
+# numpy-level helpers
+# --------------------------------------------------------------------------
+def scale_as_built(scale):
+    return float(lib().orc_scale_as_built(float(scale)))
+
+
+def compute_softmax(scale, semi):
+    semi = np.ascontiguousarray(semi, dtype=np.int8)
+    cells = semi.shape[0]
+    nv = ctypes.c_int(0)
+    mi = np.zeros(cells, np.int32)
+    pr = np.zeros(cells, np.float32)
+    lib().orc_compute_softmax(float(scale), _ptr(semi), cells, ctypes.byref(nv), _ptr(mi), _ptr(pr))
+    return nv.value, mi, pr
+
+
+def compute_top_N(scale, semi, N, cap=1000):
+    semi = np.ascontiguousarray(semi, dtype=np.int8)
+    ns = ctypes.c_int(0)
+    pa = np.zeros(max(N, 1), np.int32)
+    ix = np.zeros(max(N, 1), np.int32)
+    pr = np.zeros(max(N, 1), np.float32)
+    st = lib().orc_compute_top_N(float(scale), _ptr(semi), semi.shape[0], N, cap, ctypes.byref(ns),
+                                 _ptr(pa), _ptr(ix), _ptr(pr))
+    n = ns.value
+    return st, pa[:n].copy(), ix[:n].copy(), pr[:n].copy()
+
+
+class WindowParams(ctypes.Structure):
+    _fields_ = [("shift_x", _I), ("shift_y", _I), ("radius", _I), ("max_matches", _I), ("as_built", _I)]
+
+
+def window_match(rows, cols, desc0, max_idx0, probs0, desc1, patches1, indices1, as_built=True,
+                 shift=(4, 4), radius=4, max_matches=150):
+    desc0 = np.ascontiguousarray(desc0, np.int8)
+    desc1 = np.ascontiguousarray(desc1, np.int8)
+    max_idx0 = np.ascontiguousarray(max_idx0, np.int32)
+    probs0 = np.ascontiguousarray(probs0, np.float32)
+    patches1 = np.ascontiguousarray(patches1, np.int32)
+    indices1 = np.ascontiguousarray(indices1, np.int32)
+    p = WindowParams(shift[0], shift[1], radius, max_matches, 1 if as_built else 0)
+    cap = max(max_matches, 1)
+    p1 = np.zeros((cap, 2), np.float32)
+    p2 = np.zeros((cap, 2), np.float32)
+    q = np.zeros(cap, np.int32)
+    sc = np.zeros(cap, np.float32)
+    n = lib().orc_window_match(rows, cols, _ptr(desc0), _ptr(max_idx0), _ptr(probs0), _ptr(desc1),
+                               len(patches1), _ptr(patches1), _ptr(indices1), ctypes.byref(p), _ptr(p1),
+                               _ptr(p2), _ptr(q), _ptr(sc))
+    return p1[:n].copy(), p2[:n].copy(), q[:n].copy(), sc[:n].copy()
+
+
+def track_window(frame0, frame1, as_built=True, N=100, shift=(4, 4), radius=4, max_matches=150, cap=1000):
+    """The whole tracking_main.c:84-194 front half on one pair.
+    frame = dict(rows, cols (grid), semi[cells,65] i8, desc[cells,256] i8, semi_scale)."""
+    s0, s1 = float(frame0["semi_scale"]), float(frame1["semi_scale"])
+    if as_built:
+        s0, s1 = scale_as_built(s0), scale_as_built(s1)
+    _, mi0, pr0 = compute_softmax(s0, frame0["semi"])
+    st, pa, ix, pr = compute_top_N(s1, frame1["semi"], N, cap)
+    if st != 0:
+        raise RuntimeError("top-N capacity exceeded")
+    p1, p2, q, sc = window_match(frame0["rows"], frame0["cols"], frame0["desc"], mi0, pr0, frame1["desc"],
+                                 pa, ix, as_built, shift, radius, max_matches)
+    return dict(max_idx0=mi0, probs0=pr0, patches1=pa, indices1=ix, probs1=pr, points1=p1, points2=p2,
+                query=q, score=sc)
+
+
+def svd3(A):
+    A = np.ascontiguousarray(A, np.float32).reshape(9)
+    U = np.zeros(9, np.float32)
+    S = np.zeros(3, np.float32)
+    V = np.zeros(9, np.float32)
+    lib().orc_svd3(_ptr(A), _ptr(U), _ptr(S), _ptr(V))
+    return U.reshape(3, 3), S, V.reshape(3, 3)
+
+
+def recover_pose(E):
+    E = np.ascontiguousarray(E, np.float32).reshape(9)
+    R1 = np.zeros(9, np.float32)
+    R2 = np.zeros(9, np.float32)
+    t = np.zeros(3, np.float32)
+    lib().orc_recover_pose(_ptr(E), _ptr(R1), _ptr(R2), _ptr(t))
+    return R1.reshape(3, 3), R2.reshape(3, 3), t
+
+
+def ransac_essential_matrix(pts1, pts2, K, iters=10, thr=1.1):
+    pts1 = np.ascontiguousarray(pts1, np.float32)
+    pts2 = np.ascontiguousarray(pts2, np.float32)
+    K = np.ascontiguousarray(K, np.float32)
+    n = pts1.shape[0]
+    E = np.zeros(9, np.float32)
+    inl = np.zeros(max(n, 1000), np.int32)
+    ni = ctypes.c_int(-1)
+    st = lib().orc_ransac_essential_matrix(n, _ptr(pts1), _ptr(pts2), _ptr(K), iters, thr, _ptr(E), _ptr(inl),
+                                           ctypes.byref(ni))
+    return st, E.reshape(3, 3), inl[:max(ni.value, 0)].copy(), ni.value
+
+
+def allpairs_f32(d0, d1, thresh=0.8):
+    d0 = np.ascontiguousarray(d0, np.float32)
+    d1 = np.ascontiguousarray(d1, np.float32)
+    idx = np.zeros(d0.shape[0], np.int32)
+    sc = np.zeros(d0.shape[0], np.float32)
+    lib().orc_allpairs_f32(_ptr(d0), d0.shape[0], _ptr(d1), d1.shape[0], d0.shape[1], float(thresh), _ptr(idx),
+                           _ptr(sc))
+    return idx, sc
+
+
+def matmul_nt(A, B):
+    A = np.ascontiguousarray(A, np.float32)
+    B = np.ascontiguousarray(B, np.float32)
+    C = np.zeros((A.shape[0], B.shape[0]), np.float32)
+    lib().orc_matmul_nt(A.shape[0], B.shape[0], A.shape[1], _ptr(A), _ptr(B), _ptr(C))
+    return C
+
+
+def row_argmax(S, thresh=0.8):
+    S = np.ascontiguousarray(S, np.float32)
+    idx = np.zeros(S.shape[0], np.int32)
+    sc = np.zeros(S.shape[0], np.float32)
+    lib().orc_row_argmax(_ptr(S), S.shape[0], S.shape[1], float(thresh), _ptr(idx), _ptr(sc))
+    return idx, sc
+
+
+def allpairs_i8(d0, d1):
+    d0 = np.ascontiguousarray(d0, np.int8)
+    d1 = np.ascontiguousarray(d1, np.int8)
+    idx = np.zeros(d0.shape[0], np.int32)
+    dot = np.zeros(d0.shape[0], np.int32)
+    lib().orc_allpairs_i8(_ptr(d0), d0.shape[0], _ptr(d1), d1.shape[0], _ptr(idx), _ptr(dot))
+    return idx, dot

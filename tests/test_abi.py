@@ -1,0 +1,96 @@
+"""CPU: the C-ABI library builds for gfx950, loads, and exports every function
+declared in include/*.h; without a device it fails loudly (no CPU fallback)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INCLUDE = os.path.join(ROOT, "include")
+
+
+def declared_functions():
+    names = set()
+    for h in sorted(os.listdir(INCLUDE)):
+        if not h.endswith(".h"):
+            continue
+        src = open(os.path.join(INCLUDE, h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        src = re.sub(r"//[^\n]*", "", src)
+        src = re.sub(r"static inline[^{]*\{.*?\n\}", "", src, flags=re.S)  # frame_create (header-only)
+        src = re.sub(r"typedef[^;]*\{[^}]*\}[^;]*;", "", src, flags=re.S)
+        for m in re.finditer(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\(([^;{)]*(?:\([^)]*\)[^;{)]*)*)\)\s*;", src):
+            name = m.group(1)
+            if name in ("if", "for", "while", "return", "sizeof"):
+                continue
+            names.add(name)
+    return names
+
+
+def test_headers_declare_the_reference_api():
+    names = declared_functions()
+    for ref_name in ("compute_top_N", "compute_softmax", "normalize_points", "compute_essential_matrix",
+                     "compute_reprojection_error", "ransac_essential_matrix", "recover_pose_from_essential_matrix",
+                     "track"):
+        assert ref_name in names
+    assert "mv_match_allpairs_f32_dev" in names and len(names) > 30
+
+
+def test_library_exports_every_declared_symbol():
+    import mvtrack
+
+    path = mvtrack.LIB_PATH
+    if not os.path.exists(path):
+        mvtrack.build()
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = declared_functions() - exported
+    assert not missing, "declared but not exported: %s" % sorted(missing)
+    extra = {s for s in exported if not (s.startswith("mv_") or s in declared_functions())}
+    assert not extra, "unexpected exports: %s" % sorted(extra)
+    L = mvtrack.lib()  # dlopen works without a GPU
+    assert L.mv_version() == 100
+
+
+def test_library_targets_gfx950_only():
+    import re as _re
+
+    import mvtrack
+
+    data = open(mvtrack.LIB_PATH, "rb").read()
+    targets = set(_re.findall(rb"amdgcn-amd-amdhsa--(gfx[0-9a-z]+)", data))
+    assert targets == {b"gfx950"}, targets
+
+
+def test_no_device_fails_loudly(capfd):
+    import mvtrack
+
+    L = mvtrack.lib()
+    if L.mv_device_count() > 0:
+        pytest.skip("a device is present: covered by the gpu tests")
+    assert L.mv_default_context() is None
+    h = ctypes.c_void_p()
+    assert L.mv_context_create(0, ctypes.byref(h)) == mvtrack.MV_ERR_NO_DEVICE
+    import numpy as np
+
+    semi = np.zeros((1920, 65), np.int8)
+    ns = ctypes.c_int(123)
+    buf = np.zeros(100, np.int32)
+    pr = np.zeros(100, np.float32)
+    L.compute_top_N(0.3, semi.ctypes.data_as(ctypes.c_void_p), 100, ctypes.byref(ns),
+                    buf.ctypes.data_as(ctypes.c_void_p), buf.ctypes.data_as(ctypes.c_void_p),
+                    pr.ctypes.data_as(ctypes.c_void_p))
+    assert ns.value == -1
+    assert "no HIP device" in capfd.readouterr().err
+
+
+def test_frame_header_compiles_as_c(tmp_path):
+    src = tmp_path / "t.c"
+    src.write_text('#include "frame.h"\n#include "top_N.h"\n#include "pnp_solver.h"\n#include "tracking.h"\n'
+                   '#include "maveric_hip.h"\nint main(void){Frame f; frame_create(1,2,3,0,4,5,.5f,0,.5f,0,&f);'
+                   'return f.feature_cols == 5 ? 0 : 1;}\n')
+    exe = tmp_path / "t"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", INCLUDE, str(src), "-o", str(exe)], check=True)
+    assert subprocess.run([str(exe)]).returncode == 0

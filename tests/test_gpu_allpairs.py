@@ -1,0 +1,158 @@
+"""GPU parity: all-pairs descriptor match (python/pairwise_pnp.py:635-659 semantics on the
+gemmini_functions_cpu.h summation order) -- fp32 MFMA screen + exact re-score must give the
+oracle's indices AND scores bit-for-bit; int8 MFMA path integer-exact."""
+import numpy as np
+import pytest
+
+import synth
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.int32)
+
+
+def run_f32(ctx, torch, pairs, cap=None, thresh=0.8):
+    """pairs: list of (d0 [n0,256], d1 [n1,256]) float32"""
+    B = len(pairs)
+    cap = cap or max(max(a.shape[0], b.shape[0]) for a, b in pairs)
+    D0 = np.zeros((B, cap, 256), np.float32)
+    D1 = np.zeros((B, cap, 256), np.float32)
+    n0 = np.zeros(B, np.int32)
+    n1 = np.zeros(B, np.int32)
+    rng = np.random.default_rng(0)
+    for b, (a, c) in enumerate(pairs):
+        D0[b] = rng.standard_normal((cap, 256)).astype(np.float32) * 7  # garbage beyond n must not matter
+        D1[b] = rng.standard_normal((cap, 256)).astype(np.float32) * 7
+        D0[b, :a.shape[0]] = a
+        D1[b, :c.shape[0]] = c
+        n0[b], n1[b] = a.shape[0], c.shape[0]
+    dev = torch.device("cuda:0")
+    t = lambda x: torch.from_numpy(x).to(dev)  # noqa: E731
+    idx = torch.full((B, cap), -7, dtype=torch.int32, device=dev)
+    sc = torch.zeros((B, cap), dtype=torch.float32, device=dev)
+    ctx.set_stream(torch.cuda.current_stream())
+    ctx.match_allpairs_f32(t(D0), t(D1), t(n0), t(n1), idx, sc, thresh)
+    torch.cuda.synchronize()
+    ctx.set_stream(None)
+    return idx.cpu().numpy(), sc.cpu().numpy()
+
+
+@pytest.mark.parametrize("name", ["pair0", "pair10"])
+def test_allpairs_f32_reference_fixtures(ctx, orc, torch_cuda, name):
+    d = load_golden("tracking_%s.npz" % name)
+    exp = load_golden("expected_outputs.npz")
+    idx, sc = run_f32(ctx, torch_cuda, [(d["image0_desc"], d["image1_desc"])])
+    n0 = d["image0_desc"].shape[0]
+    assert (idx[0, :n0] == exp["ap_%s_idx" % name]).all()
+    assert (bits(sc[0, :n0]) == bits(exp["ap_%s_score" % name])).all()
+    assert (idx[0, n0:] == -1).all()
+
+
+def test_allpairs_f32_full_size_synthetic(ctx, orc, torch_cuda):
+    """BASELINE config 2: 1024 x 1024 x 256 fp32, checked against the oracle on 2 pairs."""
+    pairs = []
+    for s in range(2):
+        p = synth.synth_pair_f32(s)
+        pairs.append((p["desc0"], p["desc1"]))
+    idx, sc = run_f32(ctx, torch_cuda, pairs)
+    for b, (a, c) in enumerate(pairs):
+        i2, s2 = orc.allpairs_f32(a, c, 0.8)
+        assert (idx[b] == i2).all() and (bits(sc[b]) == bits(s2)).all()
+        assert (i2 >= 0).sum() > 500
+
+
+def test_allpairs_f32_ragged_batch(ctx, orc, torch_cuda):
+    rng = np.random.default_rng(4)
+    shapes = [(1, 1), (1, 300), (129, 1), (127, 129), (300, 257), (0, 40), (40, 0), (511, 513), (128, 128)]
+    pairs = []
+    for k, (a, b) in enumerate(shapes):
+        p = synth.synth_pair_f32(50 + k, n=max(a, 1), n1=max(b, 1), noise=0.25)
+        pairs.append((p["desc0"][:a], p["desc1"][:b]))
+    idx, sc = run_f32(ctx, torch_cuda, pairs, cap=640)
+    for b, (a, c) in enumerate(pairs):
+        if a.shape[0] == 0:
+            continue
+        if c.shape[0] == 0:
+            assert (idx[b, :a.shape[0]] == -1).all()
+            continue
+        i2, s2 = orc.allpairs_f32(a, c, 0.8)
+        assert (idx[b, :a.shape[0]] == i2).all() and (bits(sc[b, :a.shape[0]]) == bits(s2)).all()
+
+
+def test_allpairs_f32_ties_and_near_ties(ctx, orc, torch_cuda):
+    """duplicate and rounding-level-perturbed columns force the exact re-score / ambiguous-tile path."""
+    rng = np.random.default_rng(8)
+    a = rng.standard_normal((300, 256)).astype(np.float32)
+    a /= np.linalg.norm(a, axis=1, keepdims=True)
+    b = a[rng.permutation(300)].copy()
+    b += 0.01 * rng.standard_normal(b.shape).astype(np.float32)
+    b /= np.linalg.norm(b, axis=1, keepdims=True)
+    b = np.concatenate([b, b[:40], b[:40] * np.float32(1 + 2 ** -23), b[50:60] * np.float32(1 - 2 ** -24)])
+    b[400:410] = b[5]  # many identical columns in one tile and across tiles
+    b = b[rng.permutation(b.shape[0])]
+    idx, sc = run_f32(ctx, torch_cuda, [(a, b)])
+    i2, s2 = orc.allpairs_f32(a, b, 0.8)
+    assert (idx[0, :300] == i2).all() and (bits(sc[0, :300]) == bits(s2)).all()
+
+
+def test_allpairs_f32_threshold_edges(ctx, orc, torch_cuda):
+    rng = np.random.default_rng(2)
+    a = rng.standard_normal((64, 256)).astype(np.float32)
+    a /= np.linalg.norm(a, axis=1, keepdims=True)
+    b = a.copy()
+    for thr in (0.8, 0.999999, 1.0, -1.0, 0.0):
+        idx, sc = run_f32(ctx, torch_cuda, [(a, b)], thresh=thr)
+        i2, s2 = orc.allpairs_f32(a, b, thr)
+        assert (idx[0, :64] == i2).all() and (bits(sc[0, :64]) == bits(s2)).all()
+
+
+def run_i8(ctx, torch, pairs, cap=None):
+    B = len(pairs)
+    cap = cap or max(max(a.shape[0], b.shape[0]) for a, b in pairs)
+    D0 = np.zeros((B, cap, 256), np.int8)
+    D1 = np.zeros((B, cap, 256), np.int8)
+    n0 = np.zeros(B, np.int32)
+    n1 = np.zeros(B, np.int32)
+    for b, (a, c) in enumerate(pairs):
+        D0[b, :a.shape[0]] = a
+        D1[b, :c.shape[0]] = c
+        n0[b], n1[b] = a.shape[0], c.shape[0]
+    dev = torch.device("cuda:0")
+    t = lambda x: torch.from_numpy(x).to(dev)  # noqa: E731
+    idx = torch.full((B, cap), -7, dtype=torch.int32, device=dev)
+    dot = torch.zeros((B, cap), dtype=torch.int32, device=dev)
+    ctx.set_stream(torch.cuda.current_stream())
+    ctx.match_allpairs_i8(t(D0), t(D1), t(n0), t(n1), idx, dot)
+    torch.cuda.synchronize()
+    ctx.set_stream(None)
+    return idx.cpu().numpy(), dot.cpu().numpy()
+
+
+def test_allpairs_i8_full_size(ctx, orc, torch_cuda):
+    """BASELINE config 5: 2048 kp x 256 int8 per frame."""
+    a, b = synth.synth_pair_i8(0)
+    idx, dot = run_i8(ctx, torch_cuda, [(a, b)])
+    i2, d2 = orc.allpairs_i8(a, b)
+    assert (idx[0] == i2).all() and (dot[0] == d2).all()
+    assert (i2 >= 0).sum() > 1000
+
+
+def test_allpairs_i8_ragged_and_degenerate(ctx, orc, torch_cuda):
+    rng = np.random.default_rng(6)
+    pairs = []
+    for k, (na, nb) in enumerate([(1, 1), (130, 257), (300, 129), (7, 1000)]):
+        a, b = synth.synth_pair_i8(10 + k, n=max(na, nb))
+        a, b = a[:na].copy(), b[:nb].copy()
+        if k == 1:
+            a[3] = 0  # zero query
+            b[:20] = b[20]  # duplicated columns: first index must win
+        if k == 3:
+            b[5] = a[2] * 2 // 2
+        pairs.append((a, b))
+    idx, dot = run_i8(ctx, torch_cuda, pairs, cap=1024)
+    for b, (a, c) in enumerate(pairs):
+        i2, d2 = orc.allpairs_i8(a, c)
+        assert (idx[b, :a.shape[0]] == i2).all() and (dot[b, :a.shape[0]] == d2).all()
