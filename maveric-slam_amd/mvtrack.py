@@ -68,6 +68,13 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             build()
+        # PyTorch-ROCm bundles its own libamdhip64 (same SONAME, different file name in
+        # its NEEDED entries).  Load it first so this library binds to the SAME HIP
+        # runtime; loading ours first would make torch pull in a second runtime copy.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         sig = {
             "mv_version": (_I, []),
