@@ -14,7 +14,9 @@
 //   4. E = U diag(s1,s2,s3) V^T (double Jacobi on E^T E), the four (R, t)
 //      candidates R = U W V^T / U W^T V^T, t = +-u3, cheirality vote by
 //      triangulated depth over the inliers (block reduction);
-//   5. Gauss-Newton on the inliers: residual r_i = (x2^T [t]x R x1) / s_i,
+//   5. Gauss-Newton: residual r_i = (x2^T [t]x R x1) / s_i (Sampson), inliers
+//      re-selected each iteration at min(thr, 3 rms) so outliers that fell inside
+//      the RANSAC band drop out (exact data converges to machine precision),
 //      per-correspondence Jacobian d r / d(omega, tangent(t)) (5 dof),
 //      J^T J and J^T r assembled with wave64 shuffle reductions + LDS
 //      (the [J|r]^T[J|r] pattern of src/local_bundle_adjustment.c:161-176),
@@ -214,15 +216,6 @@ __device__ void rodrigues(const double w[3], double R[3][3]) {
         }
 }
 
-__device__ __forceinline__ double block_sum(double v, double *red) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    return red[0] + red[1] + red[2] + red[3];
-}
-
 __device__ __forceinline__ int block_sum_i(int v, int *red) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -252,7 +245,6 @@ __global__ __launch_bounds__(NT) void k_pose_ransac(PoseArgs a, const int *__res
     __shared__ int wsum[4];
     __shared__ int s_best[2];
     __shared__ float s_E[9];
-    __shared__ double red[4];
     __shared__ double s_pose[12];  // R (9) + t (3)
     const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int n_in = min(nv[b], a.cap);
@@ -421,12 +413,20 @@ __global__ __launch_bounds__(NT) void k_pose_ransac(PoseArgs a, const int *__res
     }
     __syncthreads();
 
-    // ---- 5. Gauss-Newton on the inliers ----
-    __shared__ double s_basis[6];
+    // ---- 5. Gauss-Newton, inliers re-selected every iteration with the current
+    //         model: |r_i| < th_k, th_0 = thr, th_{k+1} = min(thr, max(3 rms_k, 0.01 px))
+    //         (removes outliers that fell inside the RANSAC band; noisy data keeps thr) ----
+    __shared__ double s_red[4][22];
+    __shared__ double s_th;
+    if (t == 0) s_th = sqrt((double)a.thr2);
+    __syncthreads();
+    const double th_max = sqrt((double)a.thr2);
+    const double th_min = 0.01 * th_max;
     for (int it = 0; it < a.refine_iters; it++) {
         double R[9], tv[3];
         for (int i = 0; i < 9; i++) R[i] = s_pose[i];
         for (int i = 0; i < 3; i++) tv[i] = s_pose[9 + i];
+        const double th = s_th;
         // tangent basis of the unit sphere at t
         D3 tt = {{tv[0], tv[1], tv[2]}};
         D3 ax = fabs(tv[0]) < 0.57 ? D3{{1, 0, 0}} : (fabs(tv[1]) < 0.57 ? D3{{0, 1, 0}} : D3{{0, 0, 1}});
@@ -434,40 +434,55 @@ __global__ __launch_bounds__(NT) void k_pose_ransac(PoseArgs a, const int *__res
         const double nb1 = sqrt(dot3(b1, b1));
         for (int i = 0; i < 3; i++) b1.v[i] /= nb1;
         D3 b2 = cross(tt, b1);
-        double JtJ[15], Jtr[5];
-        for (int k = 0; k < 15; k++) JtJ[k] = 0;
-        for (int k = 0; k < 5; k++) Jtr[k] = 0;
+        double acc[22];  // J^T J (15, upper), J^T r (5), sum r^2, count
+#pragma unroll
+        for (int k = 0; k < 22; k++) acc[k] = 0;
         for (int i = t; i < n; i += NT) {
             const float4 p = P[i];
-            if (!sampson_inlier(E, p, a.thr2)) continue;
             D3 x1 = {{p.x, p.y, 1.0}}, x2 = {{p.z, p.w, 1.0}};
             D3 q = {{R[0] * x1.v[0] + R[1] * x1.v[1] + R[2], R[3] * x1.v[0] + R[4] * x1.v[1] + R[5],
                      R[6] * x1.v[0] + R[7] * x1.v[1] + R[8]}};
-            D3 x2t = cross(x2, tt);       // e = (x2 x t) . (R x1)
+            D3 x2t = cross(x2, tt);  // e = x2^T [t]x R x1 = (x2 x t) . (R x1)
             const double e = dot3(x2t, q);
-            // Sampson weight from the current E = [t]x R
-            D3 Ex1 = cross(tt, q);        // E x1
-            double Etx2[3];               // E^T x2 = R^T (x2 x t) ... = R^T [t]x^T x2
-            for (int c = 0; c < 3; c++) Etx2[c] = R[0 * 3 + c] * x2t.v[0] + R[1 * 3 + c] * x2t.v[1] + R[2 * 3 + c] * x2t.v[2];
+            D3 Ex1 = cross(tt, q);   // E x1
+            double Etx2[3];          // E^T x2 = R^T (x2 x t)
+            for (int c = 0; c < 3; c++)
+                Etx2[c] = R[0 * 3 + c] * x2t.v[0] + R[1 * 3 + c] * x2t.v[1] + R[2 * 3 + c] * x2t.v[2];
             const double s2 = Ex1.v[0] * Ex1.v[0] + Ex1.v[1] * Ex1.v[1] + Etx2[0] * Etx2[0] + Etx2[1] * Etx2[1];
             if (!(s2 > 0)) continue;
             const double inv = 1.0 / sqrt(s2);
-            D3 dw = cross(q, x2t);        // d e / d omega   (R <- exp(omega) R)
-            D3 dt = cross(q, x2);         // d e / d t
-            double J[5] = {dw.v[0] * inv, dw.v[1] * inv, dw.v[2] * inv, dot3(dt, b1) * inv, dot3(dt, b2) * inv};
-            const double r = e * inv;
+            const double r = e * inv;  // Sampson distance (weight frozen at the current model)
+            if (!(fabs(r) < th)) continue;
+            D3 dw = cross(q, x2t);   // d e / d omega   (R <- exp(omega) R)
+            D3 dt = cross(q, x2);    // d e / d t
+            const double J[5] = {dw.v[0] * inv, dw.v[1] * inv, dw.v[2] * inv, dot3(dt, b1) * inv,
+                                 dot3(dt, b2) * inv};
             int k = 0;
 #pragma unroll
             for (int u = 0; u < 5; u++) {
 #pragma unroll
-                for (int v = u; v < 5; v++) JtJ[k++] += J[u] * J[v];
-                Jtr[u] += J[u] * r;
+                for (int v = u; v < 5; v++) acc[k++] += J[u] * J[v];
             }
+#pragma unroll
+            for (int u = 0; u < 5; u++) acc[15 + u] += J[u] * r;
+            acc[20] += r * r;
+            acc[21] += 1.0;
         }
-        double H[15], g[5];
-        for (int k = 0; k < 15; k++) H[k] = block_sum(JtJ[k], red);
-        for (int k = 0; k < 5; k++) g[k] = block_sum(Jtr[k], red);
+        // one block reduction of all 22 sums: wave shuffles, then 4 partials in LDS
+#pragma unroll
+        for (int k = 0; k < 22; k++) {
+            double v = acc[k];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            if (lane == 0) s_red[w][k] = v;
+        }
+        __syncthreads();
         if (t == 0) {
+            double H[15], g[5];
+            for (int k = 0; k < 15; k++) H[k] = s_red[0][k] + s_red[1][k] + s_red[2][k] + s_red[3][k];
+            for (int k = 0; k < 5; k++) g[k] = s_red[0][15 + k] + s_red[1][15 + k] + s_red[2][15 + k] + s_red[3][15 + k];
+            const double r2 = s_red[0][20] + s_red[1][20] + s_red[2][20] + s_red[3][20];
+            const double cnt = s_red[0][21] + s_red[1][21] + s_red[2][21] + s_red[3][21];
             // (H + lambda diag H) d = -g, Cholesky
             double A[5][5];
             int k = 0;
@@ -479,32 +494,32 @@ __global__ __launch_bounds__(NT) void k_pose_ransac(PoseArgs a, const int *__res
                 }
             for (int u = 0; u < 5; u++) A[u][u] = A[u][u] * (1.0 + 1e-9) + 1e-300;
             double L[5][5] = {};
-            bool ok = true;
+            bool ok = cnt >= 5;
             for (int i = 0; i < 5 && ok; i++)
                 for (int j = 0; j <= i; j++) {
-                    double s = A[i][j];
-                    for (int m = 0; m < j; m++) s -= L[i][m] * L[j][m];
+                    double sum = A[i][j];
+                    for (int m = 0; m < j; m++) sum -= L[i][m] * L[j][m];
                     if (i == j) {
-                        if (!(s > 0)) {
+                        if (!(sum > 0)) {
                             ok = false;
                             break;
                         }
-                        L[i][i] = sqrt(s);
+                        L[i][i] = sqrt(sum);
                     } else {
-                        L[i][j] = s / L[j][j];
+                        L[i][j] = sum / L[j][j];
                     }
                 }
             if (ok) {
                 double y[5], d[5];
                 for (int i = 0; i < 5; i++) {
-                    double s = -g[i];
-                    for (int m = 0; m < i; m++) s -= L[i][m] * y[m];
-                    y[i] = s / L[i][i];
+                    double sum = -g[i];
+                    for (int m = 0; m < i; m++) sum -= L[i][m] * y[m];
+                    y[i] = sum / L[i][i];
                 }
                 for (int i = 4; i >= 0; i--) {
-                    double s = y[i];
-                    for (int m = i + 1; m < 5; m++) s -= L[m][i] * d[m];
-                    d[i] = s / L[i][i];
+                    double sum = y[i];
+                    for (int m = i + 1; m < 5; m++) sum -= L[m][i] * d[m];
+                    d[i] = sum / L[i][i];
                 }
                 double dR[3][3], Rn[3][3];
                 rodrigues(d, dR);
@@ -516,11 +531,11 @@ __global__ __launch_bounds__(NT) void k_pose_ransac(PoseArgs a, const int *__res
                 const double nt = sqrt(tn[0] * tn[0] + tn[1] * tn[1] + tn[2] * tn[2]);
                 for (int i = 0; i < 9; i++) s_pose[i] = Rn[i / 3][i % 3];
                 for (int i = 0; i < 3; i++) s_pose[9 + i] = tn[i] / nt;
+                s_th = fmin(th_max, fmax(3.0 * sqrt(r2 / cnt), th_min));
             }
         }
         __syncthreads();
     }
-    (void)s_basis;
     if (t < 12) {
         const int r = t / 4, c = t % 4;
         To[t] = (float)(c < 3 ? s_pose[r * 3 + c] : s_pose[9 + r]);
