@@ -8,9 +8,9 @@
 //      builds the 8x9 design matrix in the reference's column order
 //      (pnp_solver.c:42-50), and takes its null vector from a Householder QR
 //      of A^T (backward stable, no pivoting, static register indexing);
-//      hypotheses are scored by Sampson distance < (thr_px / f)^2 over all
+//      hypotheses are MSAC-scored: sum of min(Sampson^2, (thr_px / f)^2) over all
 //      correspondences (LDS broadcast reads);
-//   3. block argmax (most inliers, lowest hypothesis id) -> E;
+//   3. block argmin (lowest cost, lowest hypothesis id) -> E;
 //   4. E = U diag(s1,s2,s3) V^T (double Jacobi on E^T E), the four (R, t)
 //      candidates R = U W V^T / U W^T V^T, t = +-u3, cheirality vote by
 //      triangulated depth over the inliers (block reduction);
@@ -110,6 +110,22 @@ __device__ __forceinline__ bool sampson_inlier(const float e[9], float4 p, float
     const float num = x2 * ex0 + y2 * ex1 + ex2;
     const float den = ex0 * ex0 + ex1 * ex1 + etx0 * etx0 + etx1 * etx1;
     return num * num < thr2 * den;
+}
+
+// MSAC cost of one correspondence: min(Sampson^2, thr^2) (fast reciprocal: the
+// cost only has to be deterministic, not correctly rounded)
+__device__ __forceinline__ float msac_cost(const float e[9], float4 p, float thr2, int &inl) {
+    const float x1 = p.x, y1 = p.y, x2 = p.z, y2 = p.w;
+    const float ex0 = e[0] * x1 + e[1] * y1 + e[2];
+    const float ex1 = e[3] * x1 + e[4] * y1 + e[5];
+    const float ex2 = e[6] * x1 + e[7] * y1 + e[8];
+    const float etx0 = e[0] * x2 + e[3] * y2 + e[6];
+    const float etx1 = e[1] * x2 + e[4] * y2 + e[7];
+    const float num = x2 * ex0 + y2 * ex1 + ex2;
+    const float den = ex0 * ex0 + ex1 * ex1 + etx0 * etx0 + etx1 * etx1;
+    const bool in = num * num < thr2 * den;
+    inl += in ? 1 : 0;
+    return in ? num * num * __builtin_amdgcn_rcpf(den) : thr2;
 }
 
 // ---- small double linear algebra (one lane) ----
@@ -293,7 +309,10 @@ __global__ __launch_bounds__(NT) void k_pose_ransac(PoseArgs a, const int *__res
         return;
     }
 
-    // ---- 2. hypotheses ----
+    // ---- 2. hypotheses, MSAC-scored (sum of min(Sampson^2, thr^2); plain inlier
+    //         counting cannot separate an outlier-contaminated 8-point solution that
+    //         still explains every inlier within the band -- near-pure forward motion) ----
+    float best_cost = __builtin_inff();
     int best_cnt = -1, best_h = 0x7fffffff;
     float best_e[9];
     for (int h = t; h < a.hypotheses; h += NT) {
@@ -317,27 +336,30 @@ __global__ __launch_bounds__(NT) void k_pose_ransac(PoseArgs a, const int *__res
         float e[9];
         if (!eight_point(P, idx, e)) continue;
         int c = 0;
-        for (int i = 0; i < n; i++) c += sampson_inlier(e, P[i], a.thr2) ? 1 : 0;
-        if (c > best_cnt || (c == best_cnt && h < best_h)) {
+        float cost = 0.f;
+        for (int i = 0; i < n; i++) cost += msac_cost(e, P[i], a.thr2, c);
+        if (cost < best_cost || (cost == best_cost && h < best_h)) {
+            best_cost = cost;
             best_cnt = c;
             best_h = h;
 #pragma unroll
             for (int r = 0; r < 9; r++) best_e[r] = e[r];
         }
     }
-    // ---- 3. block argmax (count desc, hypothesis id asc) ----
-    long long key = best_cnt < 0 ? -1 : ((long long)best_cnt << 32) | (unsigned)(0x7fffffff - best_h);
+    // ---- 3. block argmin (cost asc, hypothesis id asc); cost >= 0 so its bits order as uint ----
+    unsigned long long key = best_cnt < 0 ? ~0ull
+                                          : ((unsigned long long)__float_as_uint(best_cost) << 32) | (unsigned)best_h;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-        long long k2 = __shfl_xor(key, o, 64);
-        key = k2 > key ? k2 : key;
+        unsigned long long k2 = __shfl_xor(key, o, 64);
+        key = k2 < key ? k2 : key;
     }
-    __shared__ long long s_key[4];
+    __shared__ unsigned long long s_key[4];
     if (lane == 0) s_key[w] = key;
     __syncthreads();
-    long long bk = s_key[0];
-    for (int k = 1; k < 4; k++) bk = s_key[k] > bk ? s_key[k] : bk;
-    if (bk < 0) {
+    unsigned long long bk = s_key[0];
+    for (int k = 1; k < 4; k++) bk = s_key[k] < bk ? s_key[k] : bk;
+    if (bk == ~0ull) {
         if (t < 12) To[t] = (t % 4 == t / 4) ? 1.f : 0.f;
         if (t == 0) {
             num_inliers[b] = 0;
@@ -346,7 +368,7 @@ __global__ __launch_bounds__(NT) void k_pose_ransac(PoseArgs a, const int *__res
         }
         return;
     }
-    const int win_h = 0x7fffffff - (int)(bk & 0xffffffff);
+    const int win_h = (int)(bk & 0xffffffff);
     if (best_cnt >= 0 && best_h == win_h) {
         for (int r = 0; r < 9; r++) s_E[r] = best_e[r];
         s_best[0] = best_cnt;

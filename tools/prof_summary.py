@@ -11,6 +11,13 @@ import sys
 out, tag, args = sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else ""
 
 
+def short_name(name):
+    name = name.replace("(anonymous namespace)::", "")
+    if name.startswith("void "):
+        name = name[5:]
+    return name.split("(")[0].split("<")[0].split("::")[-1].strip()
+
+
 def rows(pattern):
     res = []
     for f in glob.glob(os.path.join(out, pattern), recursive=True):
@@ -23,13 +30,13 @@ stats = rows("trace/**/*kernel_stats.csv")
 summary = {"tag": tag, "bench_args": args, "kernels": {}}
 for r in stats:
     name = r.get("Name", r.get("KernelName", "?"))
-    short = name.split("(")[0].split("::")[-1].strip()
+    short = short_name(name)
     summary["kernels"][short] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                                  "total_ns": float(r["TotalDurationNs"]), "pct": float(r.get("Percentage", 0))}
 for C in ("FETCH_SIZE", "WRITE_SIZE"):
     per = {}
     for r in rows("pmc_%s/**/*counter_collection.csv" % C):
-        name = r.get("Kernel_Name", r.get("KernelName", "?")).split("(")[0].split("::")[-1].strip()
+        name = short_name(r.get("Kernel_Name", r.get("KernelName", "?")))
         if r.get("Counter_Name", C) != C:
             continue
         per.setdefault(name, []).append(float(r["Counter_Value"]))
