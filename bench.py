@@ -46,6 +46,44 @@ def parse():
     return ap.parse_args()
 
 
+def pair_seed(rank, b):
+    """Seed of pair b on `rank`: ranks draw disjoint pairs (pair id = rank * 2^20 + b)."""
+    return 1000 + rank * (1 << 20) + b
+
+
+def timed_loop(step, steps, warmup, sync, barrier):
+    """warmup untimed steps, then EXACTLY `steps` steps bracketed by barrier + device sync."""
+    for _ in range(warmup):
+        step()
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    barrier()
+    return time.perf_counter() - t0
+
+
+def max_over_ranks(torch, dist, x, device):
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return x
+    e = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(e, op=dist.ReduceOp.MAX)
+    return float(e.item())
+
+
+def gather_checksums(torch, dist, values, device):
+    """All-gather a small per-rank result vector (validation only, outside the timed region)."""
+    t = torch.as_tensor(values, dtype=torch.float64, device=device)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [t.cpu()]
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [o.cpu() for o in out]
+
+
 def gen_batch(torch, dev, B, n, seed):
     """B synthetic KITTI-shape pairs (synth.synth_pair_f32 semantics; descriptors drawn on the GPU)."""
     import synth
@@ -149,7 +187,7 @@ def main():
     dev = torch.device("cuda", local)
     B, n = args.batch, args.kp
 
-    d0, d1, kp0, kp1 = gen_batch(torch, dev, B, n, seed=1000 + rank * 7919)
+    d0, d1, kp0, kp1 = gen_batch(torch, dev, B, n, seed=pair_seed(rank, 0))
     nn_ = torch.full((B,), n, dtype=torch.int32, device=dev)
     idx = torch.empty((B, n), dtype=torch.int32, device=dev)
     score = torch.empty((B, n), dtype=torch.float32, device=dev)
@@ -172,26 +210,17 @@ def main():
         ctx.match_allpairs_f32(d0, d1, nn_, nn_, idx, score, 0.8)
         ctx.pose_from_matches(pose_p, nn_, idx, kp0, kp1, T, nmatch, ninl, status)
 
+    mvtrack.profile_enable(False)
+    sync = torch.cuda.synchronize
+    barrier = dist.barrier if world > 1 else (lambda: None)
+
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    mvtrack.profile_enable(True)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
+    sync()
+    mvtrack.profile_enable(True)  # records only the timed steps
+    elapsed = timed_loop(step, args.steps, 0, sync, barrier)
     mvtrack.profile_enable(False)
-    elapsed = t1 - t0
-    if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+    elapsed = max_over_ranks(torch, dist, elapsed, dev)
     k_ms, k_n = mvtrack.profile_query("k_ap_screen")
     r_ms, r_n = mvtrack.profile_query("k_ap_resolve")
     p_ms, p_n = mvtrack.profile_query("k_pose_ransac")
@@ -211,6 +240,7 @@ def main():
         err = np.abs(R - synth.T_785_786[None, :, :3]).max(axis=(1, 2))
         assert ok == B and float(err.max()) < 1e-3, "pose failed: ok=%d max|dR|=%g" % (ok, err.max())
 
+    sums = gather_checksums(torch, dist, [float(nmatch.sum().item()), float(ok)], dev)
     pairs_total = B * args.steps * world
     value = pairs_total / elapsed
     flops_pair = 2.0 * n * n * KD
@@ -250,7 +280,8 @@ def main():
         "stages_ms_per_step": {"k_ap_screen": round(k_ms / max(k_n, 1), 4),
                                "k_ap_resolve": round(r_ms / max(r_n, 1), 4),
                                "k_pose_ransac": round(p_ms / max(p_n, 1), 4)},
-        "checked_pairs": checked, "pose_ok": ok,
+        "checked_pairs": checked, "pose_ok": int(sum(float(x[1]) for x in sums)),
+        "matches_per_pair": round(sum(float(x[0]) for x in sums) / (B * world), 1),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, n)
