@@ -117,6 +117,22 @@ def gen_batch(torch, dev, B, n, seed):
     return d0.contiguous(), d1, torch.from_numpy(kp0).to(dev), torch.from_numpy(kp1).to(dev)
 
 
+def pmc_traffic(kernel, B, n):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/r*_summary.json, written by tools/profile.sh) taken at the same batch/kp."""
+    import glob
+
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        k = d.get("kernels", {}).get(kernel, {})
+        if d.get("batch") == B and d.get("kp") == n and "hbm_bytes_per_launch" in k:
+            return k["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
+    return None, None
+
+
 def cpu_baseline(seconds, n):
     """gemmini_functions_cpu.h matmul (C += A.B^T, sequential k) + row argmax + as-built stub
     pose, on host threads (ctypes releases the GIL).  'reference' when the reference's own
@@ -246,15 +262,7 @@ def main():
     flops_pair = 2.0 * n * n * KD
     screen_avg_s = (k_ms / max(k_n, 1)) * 1e-3
     achieved = flops_pair * B / screen_avg_s / 1e12
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_k_ap_screen.json")
-    if os.path.exists(pmc_path):
-        try:
-            pmc = json.load(open(pmc_path))
-            if pmc.get("batch") == B and pmc.get("kp") == n:
-                traffic = pmc.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic, traffic_src = pmc_traffic("k_ap_screen", B, n)
     out = {
         "metric": "tracked frame-pairs/sec (match+PnP), 1024kp x 256-D KITTI shape",
         "value": round(value, 2),
@@ -275,7 +283,9 @@ def main():
                    "parallelism": "pairs sharded one process per GPU (dp%d), no collective" % world},
         "roofline": {"bound": "mfma", "kernel": "k_ap_screen", "achieved": round(achieved, 2),
                      "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
-                     "traffic": traffic, "algorithmic_flops_per_launch": flops_pair * B,
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "algorithmic_flops_per_launch": flops_pair * B,
+                     "algorithmic_bytes_per_launch": 2 * n * KD * 4 * B,
                      "avg_launch_ms": round(screen_avg_s * 1e3, 4), "launches": k_n},
         "stages_ms_per_step": {"k_ap_screen": round(k_ms / max(k_n, 1), 4),
                                "k_ap_resolve": round(r_ms / max(r_n, 1), 4),

@@ -27,7 +27,13 @@ def rows(pattern):
 
 
 stats = rows("trace/**/*kernel_stats.csv")
-summary = {"tag": tag, "bench_args": args, "kernels": {}}
+def argval(flag, default):
+    toks = args.split()
+    return int(toks[toks.index(flag) + 1]) if flag in toks else default
+
+
+summary = {"tag": tag, "bench_args": args, "batch": argval("--batch", 256), "kp": argval("--kp", 1024),
+           "kernels": {}}
 for r in stats:
     name = r.get("Name", r.get("KernelName", "?"))
     short = short_name(name)
