@@ -11,7 +11,7 @@ with the pose of the metric's "match+PnP".  Pairs are independent: with --gpus N
 (one process per GPU, torch.distributed) processes its own B pairs -- weak scaling, no
 data-path collective.  value = pairs processed by all ranks / max-over-ranks wall time.
 
-Extra fields: roofline of the dominant kernel (k_ap_screen, FP32 MFMA bound), measured with
+Extra fields: roofline of the dominant kernel (k_ap_match, FP32 MFMA bound), measured with
 HIP events on the launch stream inside the timed region; cpu_baseline = the gemmini matmul
 + row argmax (+ as-built stub pose) on host cores (rank 0, N = 1 only).
 """
@@ -237,8 +237,7 @@ def main():
     elapsed = timed_loop(step, args.steps, 0, sync, barrier)
     mvtrack.profile_enable(False)
     elapsed = max_over_ranks(torch, dist, elapsed, dev)
-    k_ms, k_n = mvtrack.profile_query("k_ap_screen")
-    r_ms, r_n = mvtrack.profile_query("k_ap_resolve")
+    k_ms, k_n = mvtrack.profile_query("k_ap_match")
     p_ms, p_n = mvtrack.profile_query("k_pose_ransac")
 
     # correctness of the timed outputs on a few pairs (outside the timed region)
@@ -262,7 +261,7 @@ def main():
     flops_pair = 2.0 * n * n * KD
     screen_avg_s = (k_ms / max(k_n, 1)) * 1e-3
     achieved = flops_pair * B / screen_avg_s / 1e12
-    traffic, traffic_src = pmc_traffic("k_ap_screen", B, n)
+    traffic, traffic_src = pmc_traffic("k_ap_match", B, n)
     out = {
         "metric": "tracked frame-pairs/sec (match+PnP), 1024kp x 256-D KITTI shape",
         "value": round(value, 2),
@@ -281,14 +280,13 @@ def main():
                                % (n, n), "pairs_per_gpu_per_step": B, "kp": n, "dim": KD,
                    "pose": "8-point RANSAC %d hyp + cheirality + 10 GN iters" % args.hypotheses,
                    "parallelism": "pairs sharded one process per GPU (dp%d), no collective" % world},
-        "roofline": {"bound": "mfma", "kernel": "k_ap_screen", "achieved": round(achieved, 2),
+        "roofline": {"bound": "mfma", "kernel": "k_ap_match", "achieved": round(achieved, 2),
                      "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
                      "algorithmic_flops_per_launch": flops_pair * B,
                      "algorithmic_bytes_per_launch": 2 * n * KD * 4 * B,
                      "avg_launch_ms": round(screen_avg_s * 1e3, 4), "launches": k_n},
-        "stages_ms_per_step": {"k_ap_screen": round(k_ms / max(k_n, 1), 4),
-                               "k_ap_resolve": round(r_ms / max(r_n, 1), 4),
+        "stages_ms_per_step": {"k_ap_match": round(k_ms / max(k_n, 1), 4),
                                "k_pose_ransac": round(p_ms / max(p_n, 1), 4)},
         "checked_pairs": checked, "pose_ok": int(sum(float(x[1]) for x in sums)),
         "matches_per_pair": round(sum(float(x[0]) for x in sums) / (B * world), 1),

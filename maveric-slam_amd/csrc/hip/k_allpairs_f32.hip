@@ -1,44 +1,48 @@
 // k_allpairs_f32.hip -- all-pairs fp32 descriptor match (python/pairwise_pnp.py:635-659)
 // with the gemmini_functions_cpu.h:14-56 summation order as the exact score.
 //
-// Two kernels per launch:
-//   k_ap_screen   S = D0 . D1^T with v_mfma_f32_32x32x2_f32 (exact f32 FMA chain,
-//                 k permuted), 128x128 tile per 256-thread block, K = 256 staged
-//                 through LDS in BK = 32 slices; epilogue reduces every row of the
-//                 tile to (max1, idx1, max2) and also publishes max_j |d1_j|^2.
-//   k_ap_resolve  one lane per query row: M = max over tiles, rounding bound
-//                 delta = 2 gamma_256 |a| max|b| (both the MFMA chain and the
-//                 sequential sum are within gamma_256 sum|a_k b_k| of the real
-//                 dot), then an EXACT sequential re-score (v_mul_f32 + v_add_f32,
-//                 k = 0..255) of every column whose screen score is >= M - 2 delta
-//                 -- that set provably contains every possible maximiser -- and
-//                 the reference's rule: first j with the maximum, kept when > thresh.
-// Bound: the screen is FP32-MFMA bound (2*256 FLOP per score, 157 TF/s chip);
-// per pair 2*1024*1024*256 = 536.9 MFLOP on 2 x 1 MiB of descriptors.
+// k_ap_match: ONE kernel per batch.  A 256-thread block owns 128 query rows of one pair and
+// sweeps ALL column tiles of the other frame:
+//   * S = D0 . D1^T on v_mfma_f32_32x32x2_f32 (exact f32 FMA chain, k permuted), 4 waves
+//     in 2x2, 64x64 per wave (4 accumulators of 32x32);
+//   * K = 256 streamed in 32-wide slices through a DOUBLE-BUFFERED padded LDS tile (row
+//     stride 144 B: conflict-free ds_read_b128), register-staged, one barrier per slice;
+//   * after each 128-column tile every lane folds its accumulators into a lane-local
+//     running (max1, idx1, max2) per row -- no LDS epilogue per tile;
+//   * |a_i|^2 and max_j |b_j|^2 are accumulated from the staged slices;
+//   * at the end: cross-lane / cross-wave merge of the triples, then the EXACT re-score in
+//     the reference order (v_mul_f32 + v_add_f32, k = 0..255) of the screen maximiser.
+//     Rounding bound: both the MFMA chain and the sequential sum are within
+//     gamma_256 * sum|a_k b_k| <= gamma_256 |a| |b| of the real dot, so every possible
+//     maximiser has a screen score >= M - 2 delta, delta = 2 gamma_256 |a| max|b|.  When
+//     the runner-up is inside that window the row is AMBIGUOUS and one wave re-scores all
+//     of its columns exactly (slow path: only near-duplicate descriptors trigger it).
+//   Result = the reference's rule: the first j with the maximum exact score, kept when
+//   (double)score > thresh and score > 0 (max_score starts at 0, pairwise_pnp.py:644).
+// Bound: FP32 MFMA (157.3 TF/s); per pair 2 * n0 * n1 * 256 FLOP = 536.9 MFLOP at 1024^2
+// on 2 x 1 MiB of descriptors.
 #include <math.h>
 
 #include "mv_internal.hpp"
 
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 32, KD = 256;
-constexpr int LDK = BK + 4;        // padded staging row: 144 B -> conflict-free ds_read_b128
-constexpr int LDC = BM + 4;        // transposed score tile Ct[col][row]
-constexpr int STAGE_FLOATS = 2 * BM * LDK;
-constexpr int C_FLOATS = BN * LDC;
-constexpr int LDS_FLOATS = STAGE_FLOATS > C_FLOATS ? STAGE_FLOATS : C_FLOATS;
+constexpr int BM = 128, BN = 128, BK = 32, KD = 256, KS = KD / BK;
+constexpr int LDK = BK + 4;            // padded staging row (floats): 144 B
+constexpr int TILE_FLOATS = BM * LDK;  // one A or B slice
+// LDS map (a single array, byte offsets)
+constexpr int OFF_STAGE = 0;                          // [2 buf][A, B][128][36] f32
+constexpr int STAGE_BYTES = 2 * 2 * TILE_FLOATS * 4;  // 73,728
+constexpr int OFF_ANORM = STAGE_BYTES;                // [128] f32 |a_i|^2
+constexpr int OFF_TRIP = OFF_ANORM + BM * 4;          // [2 wc][128] {m1, i1, m2}
+constexpr int OFF_AMB = OFF_TRIP + 2 * BM * 12;       // [128] i32 ambiguous rows
+constexpr int OFF_MISC = OFF_AMB + BM * 4;            // [4] f32 per-wave max|b|^2, [4] i32 #ambiguous
+constexpr int LDS_BYTES = OFF_MISC + 32;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-struct Partial {
-    float max1;
-    int idx1;
-    float max2;
-    float pad;
-};
-
-__device__ __forceinline__ void triple_push(float v, int j, float &m1, int &i1, float &m2) {
-    if (v > m1) {
+__device__ __forceinline__ void push(float v, int j, float &m1, int &i1, float &m2) {
+    if (v > m1 || (v == m1 && j < i1)) {
         m2 = m1;
         m1 = v;
         i1 = j;
@@ -47,101 +51,161 @@ __device__ __forceinline__ void triple_push(float v, int j, float &m1, int &i1, 
     }
 }
 
-// XCD-aware bijective remap: blocks b and b+8 share an XCD (dispatch is
-// round-robin); give each XCD a contiguous run of logical tiles so the 64
-// tiles of one pair (2 MiB of descriptors) share one 4 MiB L2.  Speed only.
+// order-independent merge of two (max1, idx1, max2) triples
+__device__ __forceinline__ void merge(float &m1, int &i1, float &m2, float o1, int oi, float o2) {
+    if (o1 > m1 || (o1 == m1 && oi < i1)) {
+        m2 = fmaxf(o2, m1);
+        m1 = o1;
+        i1 = oi;
+    } else {
+        m2 = fmaxf(m2, o1);
+    }
+}
+
+__device__ __forceinline__ float sum8(float v) {  // sum over the 8 lanes that share a staged row
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 4, 64);
+    return v;
+}
+
+// XCD-aware bijective remap: blocks b and b+8 share an XCD (round-robin dispatch); give
+// each XCD a contiguous run of logical blocks so a pair's row tiles share one L2.  Speed only.
 __device__ __forceinline__ int xcd_remap(int b, int total) {
     const int q = total / 8, r = total % 8, x = b % 8;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-__global__ __launch_bounds__(256, 2) void k_ap_screen(int tiles_r, int tiles_c, int cap,
-                                                      const int *__restrict__ n0v, const int *__restrict__ n1v,
-                                                      const float *__restrict__ desc0,
-                                                      const float *__restrict__ desc1, Partial *__restrict__ part,
-                                                      unsigned *__restrict__ bmax2) {
-    __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
-    float *As = lds;
-    float *Bs = lds + BM * LDK;
+// the reference's score: s = 0; s = s + a[k]*b[k], k = 0..255 (no FMA: -ffp-contract=off)
+__device__ __forceinline__ float exact_dot(const float *__restrict__ a, const float *__restrict__ b) {
+    float s = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < KD; k += 4) {
+        const float4 x = *reinterpret_cast<const float4 *>(a + k);
+        const float4 y = *reinterpret_cast<const float4 *>(b + k);
+        s = __fadd_rn(s, __fmul_rn(x.x, y.x));
+        s = __fadd_rn(s, __fmul_rn(x.y, y.y));
+        s = __fadd_rn(s, __fmul_rn(x.z, y.z));
+        s = __fadd_rn(s, __fmul_rn(x.w, y.w));
+    }
+    return s;
+}
 
-    const int per_pair = tiles_r * tiles_c;
+__global__ __launch_bounds__(256, 2) void k_ap_match(int tiles_r, int cap, const int *__restrict__ n0v,
+                                                     const int *__restrict__ n1v, const float *__restrict__ desc0,
+                                                     const float *__restrict__ desc1, double thresh,
+                                                     int *__restrict__ match_idx, float *__restrict__ match_score) {
+    __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+    float *stage = reinterpret_cast<float *>(lds + OFF_STAGE);
+    float *anorm2 = reinterpret_cast<float *>(lds + OFF_ANORM);
+    float *trip = reinterpret_cast<float *>(lds + OFF_TRIP);
+    int *amb = reinterpret_cast<int *>(lds + OFF_AMB);
+    float *misc = reinterpret_cast<float *>(lds + OFF_MISC);
+    int *namb_p = reinterpret_cast<int *>(lds + OFF_MISC) + 4;
+
     const int L = xcd_remap(blockIdx.x, gridDim.x);
-    const int pair = L / per_pair;
-    const int tile = L % per_pair;
-    const int tr = tile / tiles_c, tc = tile % tiles_c;
+    const int pair = L / tiles_r, tr = L % tiles_r;
     const int n0 = n0v[pair], n1 = n1v[pair];
-    if (tr * BM >= n0 || tc * BN >= n1) return;
-
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int wr = w >> 1, wc = w & 1;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
+    const int row0 = tr * BM;
+    if (row0 >= n0) return;
+    int *oidx = match_idx + (size_t)pair * cap + row0;
+    float *oscore = match_score + (size_t)pair * cap + row0;
+    if (n1 <= 0) {
+        if (t < BM && row0 + t < n0) {
+            oidx[t] = -1;
+            oscore[t] = 0.f;
+        }
+        return;
+    }
     const float *A = desc0 + (size_t)pair * cap * KD;
     const float *B = desc1 + (size_t)pair * cap * KD;
+    const int nsteps = ((n1 + BN - 1) / BN) * KS;
 
-    // staging map: element idx = it*256 + t -> row idx/8, float4 column idx%8
+    // staging map: slice element idx = it*256 + t -> row it*32 + t/8, float4 column t%8
     const int srow = t >> 3, sc4 = t & 7;
-    // one staged row per it = 0..3: rows it*32 + srow (named registers, no arrays)
-    const int ao0 = min(tr * BM + 0 * 32 + srow, n0 - 1) * KD + sc4 * 4;
-    const int ao1 = min(tr * BM + 1 * 32 + srow, n0 - 1) * KD + sc4 * 4;
-    const int ao2 = min(tr * BM + 2 * 32 + srow, n0 - 1) * KD + sc4 * 4;
-    const int ao3 = min(tr * BM + 3 * 32 + srow, n0 - 1) * KD + sc4 * 4;
-    const int bo0 = min(tc * BN + 0 * 32 + srow, n1 - 1) * KD + sc4 * 4;
-    const int bo1 = min(tc * BN + 1 * 32 + srow, n1 - 1) * KD + sc4 * 4;
-    const int bo2 = min(tc * BN + 2 * 32 + srow, n1 - 1) * KD + sc4 * 4;
-    const int bo3 = min(tc * BN + 3 * 32 + srow, n1 - 1) * KD + sc4 * 4;
+    const int ao0 = min(row0 + 0 * 32 + srow, n0 - 1) * KD + sc4 * 4;
+    const int ao1 = min(row0 + 1 * 32 + srow, n0 - 1) * KD + sc4 * 4;
+    const int ao2 = min(row0 + 2 * 32 + srow, n0 - 1) * KD + sc4 * 4;
+    const int ao3 = min(row0 + 3 * 32 + srow, n0 - 1) * KD + sc4 * 4;
     float4 ra0, ra1, ra2, ra3, rb0, rb1, rb2, rb3;
-    float bsq0 = 0.f, bsq1 = 0.f, bsq2 = 0.f, bsq3 = 0.f;
-#define AP_GLOAD(kt)                                                                   \
-    do {                                                                               \
-        ra0 = *reinterpret_cast<const float4 *>(A + ao0 + (kt) * BK);                 \
-        ra1 = *reinterpret_cast<const float4 *>(A + ao1 + (kt) * BK);                 \
-        ra2 = *reinterpret_cast<const float4 *>(A + ao2 + (kt) * BK);                 \
-        ra3 = *reinterpret_cast<const float4 *>(A + ao3 + (kt) * BK);                 \
-        rb0 = *reinterpret_cast<const float4 *>(B + bo0 + (kt) * BK);                 \
-        rb1 = *reinterpret_cast<const float4 *>(B + bo1 + (kt) * BK);                 \
-        rb2 = *reinterpret_cast<const float4 *>(B + bo2 + (kt) * BK);                 \
-        rb3 = *reinterpret_cast<const float4 *>(B + bo3 + (kt) * BK);                 \
+    float asq0 = 0.f, asq1 = 0.f, asq2 = 0.f, asq3 = 0.f;
+    float bsq0 = 0.f, bsq1 = 0.f, bsq2 = 0.f, bsq3 = 0.f, bmax = 0.f;
+
+#define AP_GLOAD(g)                                                                                   \
+    do {                                                                                              \
+        const int ks_ = (g) % KS, bb_ = ((g) / KS) * BN + srow;                                       \
+        ra0 = *reinterpret_cast<const float4 *>(A + ao0 + ks_ * BK);                                 \
+        ra1 = *reinterpret_cast<const float4 *>(A + ao1 + ks_ * BK);                                 \
+        ra2 = *reinterpret_cast<const float4 *>(A + ao2 + ks_ * BK);                                 \
+        ra3 = *reinterpret_cast<const float4 *>(A + ao3 + ks_ * BK);                                 \
+        rb0 = *reinterpret_cast<const float4 *>(B + min(bb_ + 0, n1 - 1) * KD + sc4 * 4 + ks_ * BK);  \
+        rb1 = *reinterpret_cast<const float4 *>(B + min(bb_ + 32, n1 - 1) * KD + sc4 * 4 + ks_ * BK); \
+        rb2 = *reinterpret_cast<const float4 *>(B + min(bb_ + 64, n1 - 1) * KD + sc4 * 4 + ks_ * BK); \
+        rb3 = *reinterpret_cast<const float4 *>(B + min(bb_ + 96, n1 - 1) * KD + sc4 * 4 + ks_ * BK); \
     } while (0)
-#define AP_ST1(it, ra, rb, bsq)                                                        \
-    do {                                                                               \
-        *reinterpret_cast<float4 *>(As + ((it) * 32 + srow) * LDK + sc4 * 4) = ra;    \
-        *reinterpret_cast<float4 *>(Bs + ((it) * 32 + srow) * LDK + sc4 * 4) = rb;    \
-        bsq += rb.x * rb.x + rb.y * rb.y + rb.z * rb.z + rb.w * rb.w;                 \
-    } while (0)
-#define AP_LSTORE()                                                                    \
-    do {                                                                               \
-        AP_ST1(0, ra0, rb0, bsq0);                                                     \
-        AP_ST1(1, ra1, rb1, bsq1);                                                     \
-        AP_ST1(2, ra2, rb2, bsq2);                                                     \
-        AP_ST1(3, ra3, rb3, bsq3);                                                     \
+#define SQ4(v) (v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w)
+#define AP_LSTORE(buf, g)                                                                             \
+    do {                                                                                              \
+        float *As_ = stage + (buf) * 2 * TILE_FLOATS;                                                 \
+        float *Bs_ = As_ + TILE_FLOATS;                                                               \
+        *reinterpret_cast<float4 *>(As_ + (0 * 32 + srow) * LDK + sc4 * 4) = ra0;                    \
+        *reinterpret_cast<float4 *>(As_ + (1 * 32 + srow) * LDK + sc4 * 4) = ra1;                    \
+        *reinterpret_cast<float4 *>(As_ + (2 * 32 + srow) * LDK + sc4 * 4) = ra2;                    \
+        *reinterpret_cast<float4 *>(As_ + (3 * 32 + srow) * LDK + sc4 * 4) = ra3;                    \
+        *reinterpret_cast<float4 *>(Bs_ + (0 * 32 + srow) * LDK + sc4 * 4) = rb0;                    \
+        *reinterpret_cast<float4 *>(Bs_ + (1 * 32 + srow) * LDK + sc4 * 4) = rb1;                    \
+        *reinterpret_cast<float4 *>(Bs_ + (2 * 32 + srow) * LDK + sc4 * 4) = rb2;                    \
+        *reinterpret_cast<float4 *>(Bs_ + (3 * 32 + srow) * LDK + sc4 * 4) = rb3;                    \
+        if ((g) < KS) {                                                                               \
+            asq0 += SQ4(ra0);                                                                         \
+            asq1 += SQ4(ra1);                                                                         \
+            asq2 += SQ4(ra2);                                                                         \
+            asq3 += SQ4(ra3);                                                                         \
+        }                                                                                             \
+        bsq0 += SQ4(rb0);                                                                             \
+        bsq1 += SQ4(rb1);                                                                             \
+        bsq2 += SQ4(rb2);                                                                             \
+        bsq3 += SQ4(rb3);                                                                             \
     } while (0)
 
     f32x16 acc[2][2];
 #pragma unroll
-    for (int i = 0; i < 2; i++)
+    for (int m = 0; m < 2; m++)
 #pragma unroll
-        for (int j = 0; j < 2; j++)
+        for (int n = 0; n < 2; n++)
 #pragma unroll
-            for (int g = 0; g < 16; g++) acc[i][j][g] = 0.f;
+            for (int q = 0; q < 16; q++) acc[m][n][q] = 0.f;
+    // running triples, one per row (m, q) of this lane's half, over this lane's columns
+    float m1[2][16], m2[2][16];
+    int i1[2][16];
+#pragma unroll
+    for (int m = 0; m < 2; m++)
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            m1[m][q] = -__builtin_inff();
+            m2[m][q] = -__builtin_inff();
+            i1[m][q] = 0x7fffffff;
+        }
 
     // fragment read map (k permuted: lane half h takes k = h*16 + s at MFMA step s)
     const int fr = lane & 31, fh = lane >> 5;
-    const float *a_frag = As + (wr * 64 + fr) * LDK + fh * 16;
-    const float *b_frag = Bs + (wc * 64 + fr) * LDK + fh * 16;
+    const int a_off = (wr * 64 + fr) * LDK + fh * 16;
+    const int b_off = TILE_FLOATS + (wc * 64 + fr) * LDK + fh * 16;
 
     AP_GLOAD(0);
-    AP_LSTORE();
+    AP_LSTORE(0, 0);
     __syncthreads();
-    constexpr int KT = KD / BK;
-    for (int kt = 0; kt < KT; kt++) {
-        if (kt + 1 < KT) {
-            AP_GLOAD(kt + 1);
-        }
+    for (int g = 0; g < nsteps; g++) {
+        const int cur = g & 1;
+        if (g + 1 < nsteps) AP_GLOAD(g + 1);
+        const float *base = stage + cur * 2 * TILE_FLOATS;
 #pragma unroll
-        for (int v = 0; v < 4; v++) {  // 4 k-steps of 2 per ds_read_b128
-            const float4 a0 = *reinterpret_cast<const float4 *>(a_frag + v * 4);
-            const float4 a1 = *reinterpret_cast<const float4 *>(a_frag + 32 * LDK + v * 4);
-            const float4 b0 = *reinterpret_cast<const float4 *>(b_frag + v * 4);
-            const float4 b1 = *reinterpret_cast<const float4 *>(b_frag + 32 * LDK + v * 4);
+        for (int v = 0; v < 4; v++) {  // 4 float4 fragment reads = 4 k-steps of 2
+            const float4 a0 = *reinterpret_cast<const float4 *>(base + a_off + v * 4);
+            const float4 a1 = *reinterpret_cast<const float4 *>(base + a_off + 32 * LDK + v * 4);
+            const float4 b0 = *reinterpret_cast<const float4 *>(base + b_off + v * 4);
+            const float4 b1 = *reinterpret_cast<const float4 *>(base + b_off + 32 * LDK + v * 4);
             const float av[2][4] = {{a0.x, a0.y, a0.z, a0.w}, {a1.x, a1.y, a1.z, a1.w}};
             const float bv[2][4] = {{b0.x, b0.y, b0.z, b0.w}, {b1.x, b1.y, b1.z, b1.w}};
 #pragma unroll
@@ -152,153 +216,129 @@ __global__ __launch_bounds__(256, 2) void k_ap_screen(int tiles_r, int tiles_c, 
                     for (int n = 0; n < 2; n++)
                         acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m][s], bv[n][s], acc[m][n], 0, 0, 0);
         }
-        __syncthreads();
-        if (kt + 1 < KT) {
-            AP_LSTORE();
-            __syncthreads();
-        }
-    }
-
-#undef AP_GLOAD
-#undef AP_ST1
-#undef AP_LSTORE
-    // ---- max |b_j|^2 over this tile's columns (8 lanes share a staged row) ----
-    float bm = 0.f;
+        if ((g % KS) == KS - 1) {
+            // column tile done: fold the accumulators into the lane-local triples
+            const int tc = g / KS;
 #pragma unroll
-    for (int it = 0; it < 4; it++) {
-        float v = it == 0 ? bsq0 : it == 1 ? bsq1 : it == 2 ? bsq2 : bsq3;
-        v += __shfl_xor(v, 1, 64);
-        v += __shfl_xor(v, 2, 64);
-        v += __shfl_xor(v, 4, 64);
-        bm = fmaxf(bm, v);
-    }
+            for (int n = 0; n < 2; n++) {
+                const int col = tc * BN + wc * 64 + n * 32 + fr;
+                const bool ok = col < n1;
 #pragma unroll
-    for (int o = 8; o < 64; o <<= 1) bm = fmaxf(bm, __shfl_xor(bm, o, 64));
-    if (tr == 0 && lane == 0) atomicMax(&bmax2[pair], __float_as_uint(bm));
-
-    // ---- scores -> LDS, transposed: Ct[col][row] (C/D map: col = lane&31,
-    //      row = (g&3) + 8*(g>>2) + 4*(lane>>5)) ----
-    float *Ct = lds;
+                for (int m = 0; m < 2; m++)
 #pragma unroll
-    for (int m = 0; m < 2; m++)
-#pragma unroll
-        for (int n = 0; n < 2; n++)
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int col = wc * 64 + n * 32 + fr;
-                const int row = wr * 64 + m * 32 + 8 * q + 4 * fh;
-                float4 v = make_float4(acc[m][n][4 * q + 0], acc[m][n][4 * q + 1], acc[m][n][4 * q + 2],
-                                       acc[m][n][4 * q + 3]);
-                *reinterpret_cast<float4 *>(Ct + col * LDC + row) = v;
+                    for (int q = 0; q < 16; q++) {
+                        if (ok) push(acc[m][n][q], col, m1[m][q], i1[m][q], m2[m][q]);
+                        acc[m][n][q] = 0.f;
+                    }
             }
-    __syncthreads();
-
-    // ---- per-row (max1, idx1, max2) over the tile's valid columns ----
-    const int r = t & (BM - 1), half = t >> 7;
-    const int cvalid = min(BN, n1 - tc * BN);
-    float m1 = -__builtin_inff(), m2 = -__builtin_inff();
-    int i1 = -1;
-    const int cb = half * 64, ce = min(cb + 64, cvalid);
-    for (int c = cb; c < ce; c++) triple_push(Ct[c * LDC + r], tc * BN + c, m1, i1, m2);
-    __syncthreads();
-    float *mx = lds;  // reuse: [128] m1, [128] i1, [128] m2 of the upper half
-    if (half == 1) {
-        mx[r] = m1;
-        reinterpret_cast<int *>(mx)[BM + r] = i1;
-        mx[2 * BM + r] = m2;
-    }
-    __syncthreads();
-    if (half == 0) {
-        const float u1 = mx[r], u2 = mx[2 * BM + r];
-        const int ui = reinterpret_cast<int *>(mx)[BM + r];
-        if (u1 > m1) {
-            m2 = fmaxf(m1, u2);
-            m1 = u1;
-            i1 = ui;
-        } else {
-            m2 = fmaxf(m2, u1);
-        }
-        const int grow = tr * BM + r;
-        if (grow < n0) {
-            Partial p;
-            p.max1 = m1;
-            p.idx1 = i1;
-            p.max2 = m2;
-            p.pad = 0.f;
-            part[((size_t)pair * cap + grow) * tiles_c + tc] = p;
-        }
-    }
-}
-
-// exact score in the reference order: s = 0; s = s + a[k]*b[k], k = 0..255
-__device__ __forceinline__ float exact_dot(const float *__restrict__ a, const float *__restrict__ b) {
-    float s = 0.f;
-#pragma unroll 4
-    for (int k = 0; k < KD; k += 4) {
-        float4 x = *reinterpret_cast<const float4 *>(a + k);
-        float4 y = *reinterpret_cast<const float4 *>(b + k);
-        s = __fadd_rn(s, __fmul_rn(x.x, y.x));
-        s = __fadd_rn(s, __fmul_rn(x.y, y.y));
-        s = __fadd_rn(s, __fmul_rn(x.z, y.z));
-        s = __fadd_rn(s, __fmul_rn(x.w, y.w));
-    }
-    return s;
-}
-
-__global__ __launch_bounds__(256) void k_ap_resolve(int tiles_c, int cap, const int *__restrict__ n0v,
-                                                    const int *__restrict__ n1v, const float *__restrict__ desc0,
-                                                    const float *__restrict__ desc1,
-                                                    const Partial *__restrict__ part,
-                                                    const unsigned *__restrict__ bmax2, double thresh,
-                                                    int *__restrict__ match_idx, float *__restrict__ match_score) {
-    const int pair = blockIdx.y;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= cap) return;
-    const int n0 = n0v[pair], n1 = n1v[pair];
-    int best = -1;
-    float bs = 0.f;
-    if (i < n0 && n1 > 0) {
-        const float *a = desc0 + ((size_t)pair * cap + i) * KD;
-        const float *B = desc1 + (size_t)pair * cap * KD;
-        const Partial *p = part + ((size_t)pair * cap + i) * tiles_c;
-        const int tiles = (n1 + BN - 1) / BN;
-        float M = -__builtin_inff();
-        for (int tt = 0; tt < tiles; tt++) M = fmaxf(M, p[tt].max1);
-        float na2 = 0.f;
-        for (int k = 0; k < KD; k += 4) {
-            float4 x = *reinterpret_cast<const float4 *>(a + k);
-            na2 += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
-        }
-        const double u = 5.9604644775390625e-08;  // 2^-24
-        const double gamma = KD * u / (1.0 - KD * u);
-        const double nb = sqrt((double)__uint_as_float(bmax2[pair]));
-        const double delta = 2.0 * gamma * sqrt((double)na2) * nb * 1.01 + 1e-30;
-        if ((double)M + delta > thresh) {
-            const double win = (double)M - 2.0 * delta;
-            for (int tt = 0; tt < tiles; tt++) {
-                const Partial q = p[tt];
-                if ((double)q.max2 >= win) {  // ambiguous tile: re-score all of its columns
-                    const int je = min(tt * BN + BN, n1);
-                    for (int j = tt * BN; j < je; j++) {
-                        float e = exact_dot(a, B + (size_t)j * KD);
-                        if ((double)e > thresh && e > bs) {
-                            bs = e;
-                            best = j;
-                        }
-                    }
-                } else if ((double)q.max1 >= win) {
-                    const int j = q.idx1;
-                    float e = exact_dot(a, B + (size_t)j * KD);
-                    if ((double)e > thresh && e > bs) {
-                        bs = e;
-                        best = j;
-                    }
+            // this tile's rows of D1 are complete: max |b_j|^2 (clamped rows are real rows)
+            bmax = fmaxf(bmax, fmaxf(fmaxf(sum8(bsq0), sum8(bsq1)), fmaxf(sum8(bsq2), sum8(bsq3))));
+            bsq0 = bsq1 = bsq2 = bsq3 = 0.f;
+            if (tc == 0) {
+                const float a0 = sum8(asq0), a1 = sum8(asq1), a2 = sum8(asq2), a3 = sum8(asq3);
+                if (sc4 == 0) {
+                    anorm2[0 * 32 + srow] = a0;
+                    anorm2[1 * 32 + srow] = a1;
+                    anorm2[2 * 32 + srow] = a2;
+                    anorm2[3 * 32 + srow] = a3;
                 }
             }
         }
+        if (g + 1 < nsteps) AP_LSTORE(cur ^ 1, g + 1);
+        __syncthreads();
     }
-    match_idx[(size_t)pair * cap + i] = best;
-    match_score[(size_t)pair * cap + i] = best >= 0 ? bs : 0.f;
+#undef AP_GLOAD
+#undef AP_LSTORE
+#undef SQ4
+
+    // ---- merge the triples: across the 32 lanes of each half, then across the 2 column waves ----
+#pragma unroll
+    for (int m = 0; m < 2; m++)
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            float a1 = m1[m][q], a2 = m2[m][q];
+            int ai = i1[m][q];
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) {
+                const float b1 = __shfl_xor(a1, o, 64), b2 = __shfl_xor(a2, o, 64);
+                const int bi = __shfl_xor(ai, o, 64);
+                merge(a1, ai, a2, b1, bi, b2);
+            }
+            if (fr == 0) {
+                const int row = wr * 64 + m * 32 + (q & 3) + 8 * (q >> 2) + 4 * fh;
+                float *tp = trip + (wc * BM + row) * 3;
+                tp[0] = a1;
+                reinterpret_cast<int *>(tp)[1] = ai;
+                tp[2] = a2;
+            }
+        }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) bmax = fmaxf(bmax, __shfl_xor(bmax, o, 64));
+    if (lane == 0) misc[w] = bmax;
+    if (t == 0) *namb_p = 0;
+    __syncthreads();
+    const float bmax2 = fmaxf(fmaxf(misc[0], misc[1]), fmaxf(misc[2], misc[3]));
+
+    // ---- exact re-score, fast path: the screen maximiser is the only possible maximiser ----
+    const double u = 5.9604644775390625e-08;  // 2^-24
+    const double gamma = KD * u / (1.0 - KD * u);
+    const double nb = sqrt((double)bmax2);
+    if (t < BM && row0 + t < n0) {
+        const float *tp0 = trip + t * 3, *tp1 = trip + (BM + t) * 3;
+        float M = tp0[0], M2 = tp0[2];
+        int I = reinterpret_cast<const int *>(tp0)[1];
+        merge(M, I, M2, tp1[0], reinterpret_cast<const int *>(tp1)[1], tp1[2]);
+        const double delta = 2.0 * gamma * sqrt((double)anorm2[t]) * nb * 1.01 + 1e-30;
+        int best = -1;
+        float bs = 0.f;
+        bool ambiguous = false;
+        if ((double)M + delta > thresh) {
+            if ((double)M2 >= (double)M - 2.0 * delta) {
+                ambiguous = true;
+                amb[atomicAdd(namb_p, 1)] = t;
+            } else {
+                const float e = exact_dot(A + (size_t)(row0 + t) * KD, B + (size_t)I * KD);
+                if ((double)e > thresh && e > 0.f) {
+                    bs = e;
+                    best = I;
+                }
+            }
+        }
+        if (!ambiguous) {
+            oidx[t] = best;
+            oscore[t] = best >= 0 ? bs : 0.f;
+        }
+    }
+    __syncthreads();
+    // ---- slow path: one wave re-scores every column of an ambiguous row exactly ----
+    const int namb = *namb_p;
+    for (int k = w; k < namb; k += 4) {
+        const int r = amb[k];
+        const float *a = A + (size_t)(row0 + r) * KD;
+        int best = 0x7fffffff;
+        float bs = -__builtin_inff();
+        for (int j = lane; j < n1; j += 64) {
+            const float e = exact_dot(a, B + (size_t)j * KD);
+            if (e > bs) {  // j ascending per lane: strict > keeps the first
+                bs = e;
+                best = j;
+            }
+        }
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const float ob = __shfl_xor(bs, o, 64);
+            const int oj = __shfl_xor(best, o, 64);
+            if (ob > bs || (ob == bs && oj < best)) {
+                bs = ob;
+                best = oj;
+            }
+        }
+        if (lane == 0) {
+            const bool keep = (double)bs > thresh && bs > 0.f;
+            oidx[r] = keep ? best : -1;
+            oscore[r] = keep ? bs : 0.f;
+        }
+    }
 }
 
 }  // namespace
@@ -306,30 +346,23 @@ __global__ __launch_bounds__(256) void k_ap_resolve(int tiles_c, int cap, const 
 namespace mv {
 
 size_t allpairs_f32_scratch_bytes(int batch, int cap) {
-    const int tiles_c = (cap + BN - 1) / BN;
-    return align_up(sizeof(Partial) * (size_t)batch * cap * tiles_c, 256) + align_up(sizeof(unsigned) * batch, 256);
+    (void)batch;
+    (void)cap;
+    return 256;
 }
 
 int launch_allpairs_f32(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
                         const float *desc0, const float *desc1, double thresh, int *match_idx,
                         float *match_score) {
-    MV_REQUIRE(batch > 0 && cap > 0 && n0 && n1 && desc0 && desc1 && match_idx && match_score && scratch);
+    (void)scratch;
+    MV_REQUIRE(batch > 0 && cap > 0 && n0 && n1 && desc0 && desc1 && match_idx && match_score);
     MV_REQUIRE(((uintptr_t)desc0 & 15) == 0 && ((uintptr_t)desc1 & 15) == 0);
-    const int tiles_r = (cap + BM - 1) / BM, tiles_c = (cap + BN - 1) / BN;
-    Partial *part = (Partial *)scratch;
-    unsigned *bmax2 =
-        (unsigned *)((char *)scratch + align_up(sizeof(Partial) * (size_t)batch * cap * tiles_c, 256));
-    MV_HIP_TRY(hipMemsetAsync(bmax2, 0, sizeof(unsigned) * batch, s));
-    const long blocks = (long)batch * tiles_r * tiles_c;
+    const int tiles_r = (cap + BM - 1) / BM;
+    const long blocks = (long)batch * tiles_r;
     MV_REQUIRE(blocks < (1l << 31));
-    MV_PROF_BEGIN(s, "k_ap_screen");
-    hipLaunchKernelGGL(k_ap_screen, dim3((unsigned)blocks), dim3(256), 0, s, tiles_r, tiles_c, cap, n0, n1, desc0,
-                       desc1, part, bmax2);
-    MV_PROF_END(s);
-    MV_LAUNCH_CHECK();
-    MV_PROF_BEGIN(s, "k_ap_resolve");
-    hipLaunchKernelGGL(k_ap_resolve, dim3((cap + 255) / 256, batch), dim3(256), 0, s, tiles_c, cap, n0, n1, desc0,
-                       desc1, part, bmax2, thresh, match_idx, match_score);
+    MV_PROF_BEGIN(s, "k_ap_match");
+    hipLaunchKernelGGL(k_ap_match, dim3((unsigned)blocks), dim3(256), 0, s, tiles_r, cap, n0, n1, desc0, desc1,
+                       thresh, match_idx, match_score);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     return MV_OK;
@@ -342,8 +375,6 @@ extern "C" int mv_match_allpairs_f32_dev(mv_context *ctx, int batch, int cap, co
                                          float *match_score) {
     MV_REQUIRE(ctx != nullptr);
     MV_HIP_TRY(hipSetDevice(ctx->device));
-    void *scr = mv::scratch(ctx, mv::allpairs_f32_scratch_bytes(batch, cap));
-    if (!scr) return MV_ERR_OUT_OF_MEMORY;
-    return mv::launch_allpairs_f32(ctx->stream, scr, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
+    return mv::launch_allpairs_f32(ctx->stream, nullptr, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
                                    match_score);
 }
