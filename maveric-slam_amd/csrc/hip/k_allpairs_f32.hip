@@ -5,11 +5,13 @@
 // sweeps ALL column tiles of the other frame:
 //   * S = D0 . D1^T on v_mfma_f32_32x32x2_f32 (exact f32 FMA chain, k permuted), 4 waves
 //     in 2x2, 64x64 per wave (4 accumulators of 32x32);
-//   * K = 256 streamed in 32-wide slices through a DOUBLE-BUFFERED padded LDS tile (row
-//     stride 144 B: conflict-free ds_read_b128), register-staged, one barrier per slice;
+//   * K = 256 streamed in 32-wide slices into a DOUBLE-BUFFERED LDS image by
+//     global_load_lds (HBM/L2 -> LDS DMA, no staging VGPRs); the image is XOR-swizzled by
+//     16-B chunk (chunk ^ ((row >> 1) & 7)) on the SOURCE address and on the read, which
+//     makes the 16-lane ds_read_b128 groups conflict-free; one barrier per slice;
 //   * after each 128-column tile every lane folds its accumulators into a lane-local
 //     running (max1, idx1, max2) per row -- no LDS epilogue per tile;
-//   * |a_i|^2 and max_j |b_j|^2 are accumulated from the staged slices;
+//   * |a_i|^2 and max_j |b_j|^2 are accumulated from the MFMA operand fragments;
 //   * at the end: cross-lane / cross-wave merge of the triples, then the EXACT re-score in
 //     the reference order (v_mul_f32 + v_add_f32, k = 0..255) of the screen maximiser.
 //     Rounding bound: both the MFMA chain and the sequential sum are within
@@ -28,11 +30,10 @@
 namespace {
 
 constexpr int BM = 128, BN = 128, BK = 32, KD = 256, KS = KD / BK;
-constexpr int LDK = BK + 4;            // padded staging row (floats): 144 B
-constexpr int TILE_FLOATS = BM * LDK;  // one A or B slice
-// LDS map (a single array, byte offsets)
-constexpr int OFF_STAGE = 0;                          // [2 buf][A, B][128][36] f32
-constexpr int STAGE_BYTES = 2 * 2 * TILE_FLOATS * 4;  // 73,728
+constexpr int TILE_FLOATS = BM * BK;  // one A or B slice: 128 rows x 128 B, swizzled
+// LDS map (a single array -- a second __shared__ object can de-pipeline glds -- byte offsets)
+constexpr int OFF_STAGE = 0;                          // [2 buf][A, B][128][32] f32
+constexpr int STAGE_BYTES = 2 * 2 * TILE_FLOATS * 4;  // 65,536
 constexpr int OFF_ANORM = STAGE_BYTES;                // [128] f32 |a_i|^2
 constexpr int OFF_TRIP = OFF_ANORM + BM * 4;          // [2 wc][128] {m1, i1, m2}
 constexpr int OFF_AMB = OFF_TRIP + 2 * BM * 12;       // [128] i32 ambiguous rows
@@ -41,14 +42,24 @@ constexpr int LDS_BYTES = OFF_MISC + 32;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-__device__ __forceinline__ void push(float v, int j, float &m1, int &i1, float &m2) {
-    if (v > m1 || (v == m1 && j < i1)) {
-        m2 = m1;
-        m1 = v;
-        i1 = j;
-    } else if (v > m2) {
-        m2 = v;
-    }
+// 16-B-per-lane HBM/L2 -> LDS DMA (global_load_lds_dwordx4): LDS destination = M0 (wave-
+// uniform byte address) + lane * 16.  Issued from inline asm on purpose: the compiler
+// cannot tell the two LDS buffers apart and would otherwise drain the DMA (vmcnt(0))
+// before the first ds_read of the OTHER buffer; the kernel counts vmcnt itself.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void glds16(const void *gsrc, unsigned lds_byte) {
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(lds_byte) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+// branch-free (selects only): push value v of column j into the triple when `ok`
+__device__ __forceinline__ void push(bool ok, float v, int j, float &m1, int &i1, float &m2) {
+    const bool top = ok && (v > m1 || (v == m1 && j < i1));
+    const float lo = ok ? fmaxf(m2, v) : m2;
+    m2 = top ? m1 : lo;
+    m1 = top ? v : m1;
+    i1 = top ? j : i1;
 }
 
 // order-independent merge of two (max1, idx1, max2) triples
@@ -96,7 +107,7 @@ __global__ __launch_bounds__(256, 2) void k_ap_match(int tiles_r, int cap, const
                                                      const float *__restrict__ desc1, double thresh,
                                                      int *__restrict__ match_idx, float *__restrict__ match_score) {
     __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
-    float *stage = reinterpret_cast<float *>(lds + OFF_STAGE);
+    float *stage_lds = reinterpret_cast<float *>(lds + OFF_STAGE);
     float *anorm2 = reinterpret_cast<float *>(lds + OFF_ANORM);
     float *trip = reinterpret_cast<float *>(lds + OFF_TRIP);
     int *amb = reinterpret_cast<int *>(lds + OFF_AMB);
@@ -108,66 +119,40 @@ __global__ __launch_bounds__(256, 2) void k_ap_match(int tiles_r, int cap, const
     const int n0 = n0v[pair], n1 = n1v[pair];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
     const int row0 = tr * BM;
-    if (row0 >= n0) return;
     int *oidx = match_idx + (size_t)pair * cap + row0;
     float *oscore = match_score + (size_t)pair * cap + row0;
-    if (n1 <= 0) {
-        if (t < BM && row0 + t < n0) {
-            oidx[t] = -1;
-            oscore[t] = 0.f;
-        }
-        return;
+    // rows in [n0, cap) report "no match"
+    if (t < BM && row0 + t < cap && (row0 + t >= n0 || n1 <= 0)) {
+        oidx[t] = -1;
+        oscore[t] = 0.f;
     }
+    if (row0 >= n0 || n1 <= 0) return;
     const float *A = desc0 + (size_t)pair * cap * KD;
     const float *B = desc1 + (size_t)pair * cap * KD;
     const int nsteps = ((n1 + BN - 1) / BN) * KS;
 
-    // staging map: slice element idx = it*256 + t -> row it*32 + t/8, float4 column t%8
-    const int srow = t >> 3, sc4 = t & 7;
-    const int ao0 = min(row0 + 0 * 32 + srow, n0 - 1) * KD + sc4 * 4;
-    const int ao1 = min(row0 + 1 * 32 + srow, n0 - 1) * KD + sc4 * 4;
-    const int ao2 = min(row0 + 2 * 32 + srow, n0 - 1) * KD + sc4 * 4;
-    const int ao3 = min(row0 + 3 * 32 + srow, n0 - 1) * KD + sc4 * 4;
-    float4 ra0, ra1, ra2, ra3, rb0, rb1, rb2, rb3;
-    float asq0 = 0.f, asq1 = 0.f, asq2 = 0.f, asq3 = 0.f;
-    float bsq0 = 0.f, bsq1 = 0.f, bsq2 = 0.f, bsq3 = 0.f, bmax = 0.f;
-
-#define AP_GLOAD(g)                                                                                   \
-    do {                                                                                              \
-        const int ks_ = (g) % KS, bb_ = ((g) / KS) * BN + srow;                                       \
-        ra0 = *reinterpret_cast<const float4 *>(A + ao0 + ks_ * BK);                                 \
-        ra1 = *reinterpret_cast<const float4 *>(A + ao1 + ks_ * BK);                                 \
-        ra2 = *reinterpret_cast<const float4 *>(A + ao2 + ks_ * BK);                                 \
-        ra3 = *reinterpret_cast<const float4 *>(A + ao3 + ks_ * BK);                                 \
-        rb0 = *reinterpret_cast<const float4 *>(B + min(bb_ + 0, n1 - 1) * KD + sc4 * 4 + ks_ * BK);  \
-        rb1 = *reinterpret_cast<const float4 *>(B + min(bb_ + 32, n1 - 1) * KD + sc4 * 4 + ks_ * BK); \
-        rb2 = *reinterpret_cast<const float4 *>(B + min(bb_ + 64, n1 - 1) * KD + sc4 * 4 + ks_ * BK); \
-        rb3 = *reinterpret_cast<const float4 *>(B + min(bb_ + 96, n1 - 1) * KD + sc4 * 4 + ks_ * BK); \
-    } while (0)
-#define SQ4(v) (v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w)
-#define AP_LSTORE(buf, g)                                                                             \
-    do {                                                                                              \
-        float *As_ = stage + (buf) * 2 * TILE_FLOATS;                                                 \
-        float *Bs_ = As_ + TILE_FLOATS;                                                               \
-        *reinterpret_cast<float4 *>(As_ + (0 * 32 + srow) * LDK + sc4 * 4) = ra0;                    \
-        *reinterpret_cast<float4 *>(As_ + (1 * 32 + srow) * LDK + sc4 * 4) = ra1;                    \
-        *reinterpret_cast<float4 *>(As_ + (2 * 32 + srow) * LDK + sc4 * 4) = ra2;                    \
-        *reinterpret_cast<float4 *>(As_ + (3 * 32 + srow) * LDK + sc4 * 4) = ra3;                    \
-        *reinterpret_cast<float4 *>(Bs_ + (0 * 32 + srow) * LDK + sc4 * 4) = rb0;                    \
-        *reinterpret_cast<float4 *>(Bs_ + (1 * 32 + srow) * LDK + sc4 * 4) = rb1;                    \
-        *reinterpret_cast<float4 *>(Bs_ + (2 * 32 + srow) * LDK + sc4 * 4) = rb2;                    \
-        *reinterpret_cast<float4 *>(Bs_ + (3 * 32 + srow) * LDK + sc4 * 4) = rb3;                    \
-        if ((g) < KS) {                                                                               \
-            asq0 += SQ4(ra0);                                                                         \
-            asq1 += SQ4(ra1);                                                                         \
-            asq2 += SQ4(ra2);                                                                         \
-            asq3 += SQ4(ra3);                                                                         \
-        }                                                                                             \
-        bsq0 += SQ4(rb0);                                                                             \
-        bsq1 += SQ4(rb1);                                                                             \
-        bsq2 += SQ4(rb2);                                                                             \
-        bsq3 += SQ4(rb3);                                                                             \
-    } while (0)
+    // DMA map: wave w fills rows w*32 .. w*32+31 of a slice, 8 rows (1 KiB) per instruction;
+    // lane l lands at LDS row (l >> 3), chunk position l & 7, and fetches the global chunk
+    // (l & 7) ^ ((row >> 1) & 7) of that row (source-side swizzle, lane-linear LDS writes).
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    const int drow = lane >> 3;
+    float asq0 = 0.f, asq1 = 0.f, bsq0 = 0.f, bsq1 = 0.f, bmax = 0.f;
+    const unsigned lds_base =
+        (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char *)(lds + OFF_STAGE);
+    auto stage = [&](int buf, int gs) {
+        const int ks = gs % KS, crow0 = (gs / KS) * BN;
+        const unsigned bufa = lds_base + (unsigned)(buf * 2 * TILE_FLOATS) * 4u;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int row = wu * 32 + i * 8 + drow;
+            const int c = (lane & 7) ^ ((row >> 1) & 7);
+            const float *sa = A + (size_t)min(row0 + row, n0 - 1) * KD + ks * BK + c * 4;
+            const float *sb = B + (size_t)min(crow0 + row, n1 - 1) * KD + ks * BK + c * 4;
+            const unsigned dst = bufa + (unsigned)((wu * 32 + i * 8) * BK) * 4u;
+            glds16(sa, dst);
+            glds16(sb, dst + TILE_FLOATS * 4u);
+        }
+    };
 
     f32x16 acc[2][2];
 #pragma unroll
@@ -188,24 +173,32 @@ __global__ __launch_bounds__(256, 2) void k_ap_match(int tiles_r, int cap, const
             i1[m][q] = 0x7fffffff;
         }
 
-    // fragment read map (k permuted: lane half h takes k = h*16 + s at MFMA step s)
+    // fragment read map (k permuted: lane half h takes k = h*16 + s at MFMA step s, i.e.
+    // chunk h*4 + s/4 of its row); rows +32 share the swizzle ((row >> 1) & 7 unchanged)
     const int fr = lane & 31, fh = lane >> 5;
-    const int a_off = (wr * 64 + fr) * LDK + fh * 16;
-    const int b_off = TILE_FLOATS + (wc * 64 + fr) * LDK + fh * 16;
+    const int ra = wr * 64 + fr, rb = wc * 64 + fr;
+    const int swa = (ra >> 1) & 7, swb = (rb >> 1) & 7;
+    int offa[4], offb[4];
+#pragma unroll
+    for (int v = 0; v < 4; v++) {
+        offa[v] = ra * BK + (((fh * 4 + v) ^ swa) * 4);
+        offb[v] = TILE_FLOATS + rb * BK + (((fh * 4 + v) ^ swb) * 4);
+    }
+    const bool a_norms = wc == 0, b_norms = wr == 0;  // wave-uniform: one wave per row set
 
-    AP_GLOAD(0);
-    AP_LSTORE(0, 0);
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int g = 0; g < nsteps; g++) {
         const int cur = g & 1;
-        if (g + 1 < nsteps) AP_GLOAD(g + 1);
-        const float *base = stage + cur * 2 * TILE_FLOATS;
+        if (g + 1 < nsteps) stage(cur ^ 1, g + 1);  // DMA of the next slice overlaps the MFMAs
+        const float *base = stage_lds + cur * 2 * TILE_FLOATS;
 #pragma unroll
         for (int v = 0; v < 4; v++) {  // 4 float4 fragment reads = 4 k-steps of 2
-            const float4 a0 = *reinterpret_cast<const float4 *>(base + a_off + v * 4);
-            const float4 a1 = *reinterpret_cast<const float4 *>(base + a_off + 32 * LDK + v * 4);
-            const float4 b0 = *reinterpret_cast<const float4 *>(base + b_off + v * 4);
-            const float4 b1 = *reinterpret_cast<const float4 *>(base + b_off + 32 * LDK + v * 4);
+            const float4 a0 = *reinterpret_cast<const float4 *>(base + offa[v]);
+            const float4 a1 = *reinterpret_cast<const float4 *>(base + offa[v] + 32 * BK);
+            const float4 b0 = *reinterpret_cast<const float4 *>(base + offb[v]);
+            const float4 b1 = *reinterpret_cast<const float4 *>(base + offb[v] + 32 * BK);
             const float av[2][4] = {{a0.x, a0.y, a0.z, a0.w}, {a1.x, a1.y, a1.z, a1.w}};
             const float bv[2][4] = {{b0.x, b0.y, b0.z, b0.w}, {b1.x, b1.y, b1.z, b1.w}};
 #pragma unroll
@@ -215,6 +208,15 @@ __global__ __launch_bounds__(256, 2) void k_ap_match(int tiles_r, int cap, const
 #pragma unroll
                     for (int n = 0; n < 2; n++)
                         acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m][s], bv[n][s], acc[m][n], 0, 0, 0);
+            // norms for the rounding bound only (any summation order is fine here)
+            if (a_norms && g < KS) {
+                asq0 = fmaf(a0.x, a0.x, fmaf(a0.y, a0.y, fmaf(a0.z, a0.z, fmaf(a0.w, a0.w, asq0))));
+                asq1 = fmaf(a1.x, a1.x, fmaf(a1.y, a1.y, fmaf(a1.z, a1.z, fmaf(a1.w, a1.w, asq1))));
+            }
+            if (b_norms) {
+                bsq0 = fmaf(b0.x, b0.x, fmaf(b0.y, b0.y, fmaf(b0.z, b0.z, fmaf(b0.w, b0.w, bsq0))));
+                bsq1 = fmaf(b1.x, b1.x, fmaf(b1.y, b1.y, fmaf(b1.z, b1.z, fmaf(b1.w, b1.w, bsq1))));
+            }
         }
         if ((g % KS) == KS - 1) {
             // column tile done: fold the accumulators into the lane-local triples
@@ -227,29 +229,27 @@ __global__ __launch_bounds__(256, 2) void k_ap_match(int tiles_r, int cap, const
                 for (int m = 0; m < 2; m++)
 #pragma unroll
                     for (int q = 0; q < 16; q++) {
-                        if (ok) push(acc[m][n][q], col, m1[m][q], i1[m][q], m2[m][q]);
+                        push(ok, acc[m][n][q], col, m1[m][q], i1[m][q], m2[m][q]);
                         acc[m][n][q] = 0.f;
                     }
             }
-            // this tile's rows of D1 are complete: max |b_j|^2 (clamped rows are real rows)
-            bmax = fmaxf(bmax, fmaxf(fmaxf(sum8(bsq0), sum8(bsq1)), fmaxf(sum8(bsq2), sum8(bsq3))));
-            bsq0 = bsq1 = bsq2 = bsq3 = 0.f;
-            if (tc == 0) {
-                const float a0 = sum8(asq0), a1 = sum8(asq1), a2 = sum8(asq2), a3 = sum8(asq3);
-                if (sc4 == 0) {
-                    anorm2[0 * 32 + srow] = a0;
-                    anorm2[1 * 32 + srow] = a1;
-                    anorm2[2 * 32 + srow] = a2;
-                    anorm2[3 * 32 + srow] = a3;
+            if (b_norms) {  // |b_col|^2: the two lane halves hold the two k halves
+                const float c0 = bsq0 + __shfl_xor(bsq0, 32, 64), c1 = bsq1 + __shfl_xor(bsq1, 32, 64);
+                const int col0 = tc * BN + wc * 64 + fr;
+                bmax = fmaxf(bmax, fmaxf(col0 < n1 ? c0 : 0.f, col0 + 32 < n1 ? c1 : 0.f));
+                bsq0 = bsq1 = 0.f;
+            }
+            if (a_norms && tc == 0) {
+                const float r0 = asq0 + __shfl_xor(asq0, 32, 64), r1 = asq1 + __shfl_xor(asq1, 32, 64);
+                if (fh == 0) {
+                    anorm2[ra] = r0;
+                    anorm2[ra + 32] = r1;
                 }
             }
         }
-        if (g + 1 < nsteps) AP_LSTORE(cur ^ 1, g + 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next slice has landed
         __syncthreads();
     }
-#undef AP_GLOAD
-#undef AP_LSTORE
-#undef SQ4
 
     // ---- merge the triples: across the 32 lanes of each half, then across the 2 column waves ----
 #pragma unroll
