@@ -1,17 +1,18 @@
 // k_allpairs_f32.hip -- all-pairs fp32 descriptor match (python/pairwise_pnp.py:635-659)
 // with the gemmini_functions_cpu.h:14-56 summation order as the exact score.
 //
-// k_ap_match: ONE kernel per batch.  A 256-thread block owns 128 query rows of one pair and
-// sweeps ALL column tiles of the other frame:
-//   * S = D0 . D1^T on v_mfma_f32_32x32x2_f32 (exact f32 FMA chain, k permuted), 4 waves
-//     in 2x2, 64x64 per wave (4 accumulators of 32x32);
+// k_ap_match: ONE kernel per batch.  A 512-thread block (8 waves: 4 row groups x 2 column
+// groups) owns 128 query rows of one pair and sweeps ALL column tiles of the other frame:
+//   * S = D0 . D1^T on v_mfma_f32_32x32x2_f32 (exact f32 FMA chain, k permuted); each wave
+//     computes 32 rows x 64 columns of a 128-column tile (2 accumulators of 32x32);
 //   * K = 256 streamed in 32-wide slices into a DOUBLE-BUFFERED LDS image by
-//     global_load_lds (HBM/L2 -> LDS DMA, no staging VGPRs); the image is XOR-swizzled by
-//     16-B chunk (chunk ^ ((row >> 1) & 7)) on the SOURCE address and on the read, which
-//     makes the 16-lane ds_read_b128 groups conflict-free; one barrier per slice;
-//   * after each 128-column tile every lane folds its accumulators into a lane-local
-//     running (max1, idx1, max2) per row -- no LDS epilogue per tile;
-//   * |a_i|^2 and max_j |b_j|^2 are accumulated from the MFMA operand fragments;
+//     global_load_lds (HBM/L2 -> LDS DMA, no staging VGPRs, issued from inline asm with
+//     immediate K offsets so the compiler does not drain it before unrelated ds_reads);
+//     the image is XOR-swizzled by 16-B chunk (chunk ^ ((row >> 1) & 7)) on the SOURCE
+//     address and on the read -> conflict-free ds_read_b128; one barrier per slice;
+//   * after each column tile every lane folds its accumulators into a lane-local running
+//     (max1, idx1, max2) per row (selects only) -- no per-tile LDS epilogue;
+//   * |a_i|^2 and max_j |b_j|^2 from each thread's own DMA'd chunks (bound only);
 //   * at the end: cross-lane / cross-wave merge of the triples, then the EXACT re-score in
 //     the reference order (v_mul_f32 + v_add_f32, k = 0..255) of the screen maximiser.
 //     Rounding bound: both the MFMA chain and the sequential sum are within
@@ -25,41 +26,53 @@
 // on 2 x 1 MiB of descriptors.
 #include <math.h>
 
+#include <utility>
+
 #include "mv_internal.hpp"
 
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 32, KD = 256, KS = KD / BK;
+constexpr int BM = 128, BN = 128, BK = 32, KD = 256, KS = KD / BK, NT = 512;
 constexpr int TILE_FLOATS = BM * BK;  // one A or B slice: 128 rows x 128 B, swizzled
-// LDS map (a single array -- a second __shared__ object can de-pipeline glds -- byte offsets)
+// LDS map (ONE array -- a second __shared__ object can de-pipeline the DMA), byte offsets
 constexpr int OFF_STAGE = 0;                          // [2 buf][A, B][128][32] f32
 constexpr int STAGE_BYTES = 2 * 2 * TILE_FLOATS * 4;  // 65,536
 constexpr int OFF_ANORM = STAGE_BYTES;                // [128] f32 |a_i|^2
 constexpr int OFF_TRIP = OFF_ANORM + BM * 4;          // [2 wc][128] {m1, i1, m2}
 constexpr int OFF_AMB = OFF_TRIP + 2 * BM * 12;       // [128] i32 ambiguous rows
-constexpr int OFF_MISC = OFF_AMB + BM * 4;            // [4] f32 per-wave max|b|^2, [4] i32 #ambiguous
-constexpr int LDS_BYTES = OFF_MISC + 32;
+constexpr int OFF_MISC = OFF_AMB + BM * 4;            // [8] f32 per-wave max|b|^2, [1] i32 #ambiguous
+constexpr int LDS_BYTES = OFF_MISC + 48;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-// 16-B-per-lane HBM/L2 -> LDS DMA (global_load_lds_dwordx4): LDS destination = M0 (wave-
-// uniform byte address) + lane * 16.  Issued from inline asm on purpose: the compiler
-// cannot tell the two LDS buffers apart and would otherwise drain the DMA (vmcnt(0))
-// before the first ds_read of the OTHER buffer; the kernel counts vmcnt itself.
+template <class F, int... I>
+__device__ __forceinline__ void static_for(F &&f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+
+// 16-B-per-lane HBM/L2 -> LDS DMA (global_load_lds_dwordx4, SADDR form): source = SGPR
+// base + 32-bit VGPR byte offset; LDS destination = M0 (wave-uniform byte address) + lane *
+// 16.  No instruction offset: it would displace the LDS destination as well.  The slice's
+// K offset goes into the scalar base instead (one s_add per load, no VALU).
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
-__device__ __forceinline__ void glds16(const void *gsrc, unsigned lds_byte) {
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(lds_byte) : "memory", "m0");
+__device__ __forceinline__ void glds16(const void *sbase, unsigned voff, unsigned lds_byte) {
+    asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds_byte)
+                 : "memory", "m0");
 }
 #pragma clang diagnostic pop
 
-// branch-free (selects only): push value v of column j into the triple when `ok`
-__device__ __forceinline__ void push(bool ok, float v, int j, float &m1, int &i1, float &m2) {
-    const bool top = ok && (v > m1 || (v == m1 && j < i1));
-    const float lo = ok ? fmaxf(m2, v) : m2;
-    m2 = top ? m1 : lo;
-    m1 = top ? v : m1;
-    i1 = top ? j : i1;
+// Fold one tile's two columns of a row (v0 at column j, v1 at j + 32; -inf past n1) into the
+// running triple.  Earlier tiles hold smaller column indices, so a tie never replaces
+// (strict >); within the pair the lower column wins a tie.  Selects only.
+__device__ __forceinline__ void fold2(float v0, float v1, int j, float &m1, int &i1, float &m2) {
+    const bool hi = v1 > v0;
+    const float t1 = fmaxf(v0, v1), t2 = fminf(v0, v1);
+    const int tj = hi ? j + 32 : j;
+    const bool top = t1 > m1;
+    m2 = top ? fmaxf(m1, t2) : fmaxf(m2, t1);
+    m1 = top ? t1 : m1;
+    i1 = top ? tj : i1;
 }
 
 // order-independent merge of two (max1, idx1, max2) triples
@@ -71,13 +84,6 @@ __device__ __forceinline__ void merge(float &m1, int &i1, float &m2, float o1, i
     } else {
         m2 = fmaxf(m2, o1);
     }
-}
-
-__device__ __forceinline__ float sum8(float v) {  // sum over the 8 lanes that share a staged row
-    v += __shfl_xor(v, 1, 64);
-    v += __shfl_xor(v, 2, 64);
-    v += __shfl_xor(v, 4, 64);
-    return v;
 }
 
 // XCD-aware bijective remap: blocks b and b+8 share an XCD (round-robin dispatch); give
@@ -102,17 +108,28 @@ __device__ __forceinline__ float exact_dot(const float *__restrict__ a, const fl
     return s;
 }
 
-__global__ __launch_bounds__(256, 2) void k_ap_match(int tiles_r, int cap, const int *__restrict__ n0v,
-                                                     const int *__restrict__ n1v, const float *__restrict__ desc0,
-                                                     const float *__restrict__ desc1, double thresh,
-                                                     int *__restrict__ match_idx, float *__restrict__ match_score) {
+__device__ __forceinline__ float sum8(float v) {  // over the 8 lanes (l & 7) of a DMA row
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 4, 64);
+    return v;
+}
+
+__device__ __forceinline__ float nrm4(float4 x, float acc) {
+    return fmaf(x.x, x.x, fmaf(x.y, x.y, fmaf(x.z, x.z, fmaf(x.w, x.w, acc))));
+}
+
+__global__ __launch_bounds__(NT, 2) void k_ap_match(int tiles_r, int cap, const int *__restrict__ n0v,
+                                                    const int *__restrict__ n1v, const float *__restrict__ desc0,
+                                                    const float *__restrict__ desc1, double thresh,
+                                                    int *__restrict__ match_idx, float *__restrict__ match_score) {
     __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
-    float *stage_lds = reinterpret_cast<float *>(lds + OFF_STAGE);
+    const float *stage_lds = reinterpret_cast<const float *>(lds + OFF_STAGE);
     float *anorm2 = reinterpret_cast<float *>(lds + OFF_ANORM);
     float *trip = reinterpret_cast<float *>(lds + OFF_TRIP);
     int *amb = reinterpret_cast<int *>(lds + OFF_AMB);
     float *misc = reinterpret_cast<float *>(lds + OFF_MISC);
-    int *namb_p = reinterpret_cast<int *>(lds + OFF_MISC) + 4;
+    int *namb_p = reinterpret_cast<int *>(lds + OFF_MISC) + 8;
 
     const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int pair = L / tiles_r, tr = L % tiles_r;
@@ -129,155 +146,167 @@ __global__ __launch_bounds__(256, 2) void k_ap_match(int tiles_r, int cap, const
     if (row0 >= n0 || n1 <= 0) return;
     const float *A = desc0 + (size_t)pair * cap * KD;
     const float *B = desc1 + (size_t)pair * cap * KD;
-    const int nsteps = ((n1 + BN - 1) / BN) * KS;
+    const int ntc = (n1 + BN - 1) / BN;
 
-    // DMA map: wave w fills rows w*32 .. w*32+31 of a slice, 8 rows (1 KiB) per instruction;
-    // lane l lands at LDS row (l >> 3), chunk position l & 7, and fetches the global chunk
-    // (l & 7) ^ ((row >> 1) & 7) of that row (source-side swizzle, lane-linear LDS writes).
+    // ---- DMA map: wave w fills rows w*16 .. w*16+15 of each slice (A and B), 8 rows
+    //      (1 KiB) per instruction; lane l lands at row (l >> 3), chunk position l & 7 and
+    //      fetches global chunk (l & 7) ^ ((row >> 1) & 7) of that row ----
     const int wu = __builtin_amdgcn_readfirstlane(w);
-    const int drow = lane >> 3;
-    float asq0 = 0.f, asq1 = 0.f, bsq0 = 0.f, bsq1 = 0.f, bmax = 0.f;
-    const unsigned lds_base =
-        (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char *)(lds + OFF_STAGE);
-    auto stage = [&](int buf, int gs) {
-        const int ks = gs % KS, crow0 = (gs / KS) * BN;
-        const unsigned bufa = lds_base + (unsigned)(buf * 2 * TILE_FLOATS) * 4u;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int row = wu * 32 + i * 8 + drow;
-            const int c = (lane & 7) ^ ((row >> 1) & 7);
-            const float *sa = A + (size_t)min(row0 + row, n0 - 1) * KD + ks * BK + c * 4;
-            const float *sb = B + (size_t)min(crow0 + row, n1 - 1) * KD + ks * BK + c * 4;
-            const unsigned dst = bufa + (unsigned)((wu * 32 + i * 8) * BK) * 4u;
-            glds16(sa, dst);
-            glds16(sb, dst + TILE_FLOATS * 4u);
-        }
-    };
+    const int dr0 = wu * 16 + (lane >> 3), dr1 = dr0 + 8;
+    const int dc0 = ((lane & 7) ^ ((dr0 >> 1) & 7)) * 4, dc1 = ((lane & 7) ^ ((dr1 >> 1) & 7)) * 4;
+    // per-lane source byte offsets (rows clamped into [0, n)); A's stay fixed, B's advance per tile
+    const unsigned oA0 = (unsigned)(min(row0 + dr0, n0 - 1) * KD + dc0) * 4u;
+    const unsigned oA1 = (unsigned)(min(row0 + dr1, n0 - 1) * KD + dc1) * 4u;
+    unsigned oB0 = (unsigned)(min(dr0, n1 - 1) * KD + dc0) * 4u;
+    unsigned oB1 = (unsigned)(min(dr1, n1 - 1) * KD + dc1) * 4u;
+    const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char *)(lds + OFF_STAGE);
+    const unsigned dst_w = lds_base + (unsigned)(wu * 16 * BK * 4);
+#define AP_STAGE(BUF, KSI)                                                                   \
+    do {                                                                                     \
+        const unsigned d_ = dst_w + (unsigned)((BUF) * 2 * TILE_FLOATS * 4);                 \
+        const float *sa_ = A + (KSI) * BK, *sb_ = B + (KSI) * BK;                            \
+        glds16(sa_, oA0, d_);                                                                \
+        glds16(sa_, oA1, d_ + 8 * BK * 4);                                                   \
+        glds16(sb_, oB0, d_ + TILE_FLOATS * 4);                                              \
+        glds16(sb_, oB1, d_ + TILE_FLOATS * 4 + 8 * BK * 4);                                 \
+    } while (0)
 
-    f32x16 acc[2][2];
-#pragma unroll
-    for (int m = 0; m < 2; m++)
-#pragma unroll
-        for (int n = 0; n < 2; n++)
-#pragma unroll
-            for (int q = 0; q < 16; q++) acc[m][n][q] = 0.f;
-    // running triples, one per row (m, q) of this lane's half, over this lane's columns
-    float m1[2][16], m2[2][16];
-    int i1[2][16];
-#pragma unroll
-    for (int m = 0; m < 2; m++)
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-            m1[m][q] = -__builtin_inff();
-            m2[m][q] = -__builtin_inff();
-            i1[m][q] = 0x7fffffff;
-        }
-
-    // fragment read map (k permuted: lane half h takes k = h*16 + s at MFMA step s, i.e.
-    // chunk h*4 + s/4 of its row); rows +32 share the swizzle ((row >> 1) & 7 unchanged)
+    // ---- fragment read map: lane half h takes k = h*16 + s at MFMA step s (chunk h*4 + s/4)
     const int fr = lane & 31, fh = lane >> 5;
-    const int ra = wr * 64 + fr, rb = wc * 64 + fr;
+    const int ra = wr * 32 + fr, rb = wc * 64 + fr;  // rb + 32 has the same swizzle
     const int swa = (ra >> 1) & 7, swb = (rb >> 1) & 7;
-    int offa[4], offb[4];
-#pragma unroll
-    for (int v = 0; v < 4; v++) {
-        offa[v] = ra * BK + (((fh * 4 + v) ^ swa) * 4);
-        offb[v] = TILE_FLOATS + rb * BK + (((fh * 4 + v) ^ swb) * 4);
-    }
-    const bool a_norms = wc == 0, b_norms = wr == 0;  // wave-uniform: one wave per row set
+    const int offa = ra * BK, offb = TILE_FLOATS + rb * BK;
 
-    stage(0, 0);
+    f32x16 acc0, acc1;
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        acc0[q] = 0.f;
+        acc1[q] = 0.f;
+    }
+    float m1[16], m2[16];
+    int i1[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        m1[q] = -__builtin_inff();
+        m2[q] = -__builtin_inff();
+        i1[q] = 0x7fffffff;
+    }
+    float asq0 = 0.f, asq1 = 0.f, bsq0 = 0.f, bsq1 = 0.f, bmax = 0.f;
+    const int nro0 = dr0 * BK + (lane & 7) * 4, nro1 = dr1 * BK + (lane & 7) * 4;  // own chunks
+
+#define AP_SLICE(ks)                                                                          \
+    do {                                                                                      \
+        constexpr int cur = (ks) & 1; /* KS is even: slice ks of a tile lives in buffer ks & 1 */ \
+ /* DMA of the next slice (the next tile's slice 0 after the last) overlaps the MFMAs */ \
+            if constexpr ((ks) + 1 < KS) { \
+                AP_STAGE(cur ^ 1, ks + 1); \
+            } else { \
+                if (!last_tile) { \
+                    oB0 = (unsigned)(min((tc + 1) * BN + dr0, n1 - 1) * KD + dc0) * 4u; \
+                    oB1 = (unsigned)(min((tc + 1) * BN + dr1, n1 - 1) * KD + dc1) * 4u; \
+                    AP_STAGE(cur ^ 1, 0); \
+                } \
+            } \
+            const float *base = stage_lds + cur * 2 * TILE_FLOATS; \
+            { /* norms for the rounding bound, from this thread's own DMA'd chunks */ \
+                const float4 nb0 = *reinterpret_cast<const float4 *>(base + TILE_FLOATS + nro0); \
+                const float4 nb1 = *reinterpret_cast<const float4 *>(base + TILE_FLOATS + nro1); \
+                bsq0 = nrm4(nb0, bsq0); \
+                bsq1 = nrm4(nb1, bsq1); \
+                if (tc == 0) { \
+                    const float4 na0 = *reinterpret_cast<const float4 *>(base + nro0); \
+                    const float4 na1 = *reinterpret_cast<const float4 *>(base + nro1); \
+                    asq0 = nrm4(na0, asq0); \
+                    asq1 = nrm4(na1, asq1); \
+                } \
+            } \
+_Pragma("unroll") \
+            for (int v = 0; v < 4; v++) { /* 3 float4 fragment reads feed 8 MFMAs (4 k-steps x 2 n) */ \
+                const float4 a = *reinterpret_cast<const float4 *>(base + offa + (((fh * 4 + v) ^ swa) * 4)); \
+                const float4 b0 = *reinterpret_cast<const float4 *>(base + offb + (((fh * 4 + v) ^ swb) * 4)); \
+                const float4 b1 = \
+                    *reinterpret_cast<const float4 *>(base + offb + 32 * BK + (((fh * 4 + v) ^ swb) * 4)); \
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b0.x, acc0, 0, 0, 0); \
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b1.x, acc1, 0, 0, 0); \
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b0.y, acc0, 0, 0, 0); \
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b1.y, acc1, 0, 0, 0); \
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b0.z, acc0, 0, 0, 0); \
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b1.z, acc1, 0, 0, 0); \
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b0.w, acc0, 0, 0, 0); \
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b1.w, acc1, 0, 0, 0); \
+            } \
+            if constexpr ((ks) == KS - 1) { \
+ /* column tile done: fold the accumulators into the lane-local triples */ \
+                const int col = tc * BN + wc * 64 + fr; \
+                const float lo0 = col < n1 ? 0.f : -__builtin_inff(); /* + 0 keeps, + -inf drops */ \
+                const float lo1 = col + 32 < n1 ? 0.f : -__builtin_inff(); \
+_Pragma("unroll") \
+                for (int q = 0; q < 16; q++) { \
+                    fold2(acc0[q] + lo0, acc1[q] + lo1, col, m1[q], i1[q], m2[q]); \
+                    acc0[q] = 0.f; \
+                    acc1[q] = 0.f; \
+                } \
+                { /* row norms: the 8 lanes (l & 7) of a DMA row hold its 8 chunks */ \
+                    const float c0 = sum8(bsq0), c1 = sum8(bsq1); \
+                    bmax = fmaxf(bmax, fmaxf(tc * BN + dr0 < n1 ? c0 : 0.f, tc * BN + dr1 < n1 ? c1 : 0.f)); \
+                    bsq0 = bsq1 = 0.f; \
+                    if (tc == 0) { \
+                        const float r0 = sum8(asq0), r1 = sum8(asq1); \
+                        if ((lane & 7) == 0) { \
+                            anorm2[dr0] = r0; \
+                            anorm2[dr1] = r1; \
+                        } \
+                    } \
+                } \
+            } \
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* the next slice has landed */ \
+            __syncthreads(); \
+    } while (0)
+
+    AP_STAGE(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int g = 0; g < nsteps; g++) {
-        const int cur = g & 1;
-        if (g + 1 < nsteps) stage(cur ^ 1, g + 1);  // DMA of the next slice overlaps the MFMAs
-        const float *base = stage_lds + cur * 2 * TILE_FLOATS;
-#pragma unroll
-        for (int v = 0; v < 4; v++) {  // 4 float4 fragment reads = 4 k-steps of 2
-            const float4 a0 = *reinterpret_cast<const float4 *>(base + offa[v]);
-            const float4 a1 = *reinterpret_cast<const float4 *>(base + offa[v] + 32 * BK);
-            const float4 b0 = *reinterpret_cast<const float4 *>(base + offb[v]);
-            const float4 b1 = *reinterpret_cast<const float4 *>(base + offb[v] + 32 * BK);
-            const float av[2][4] = {{a0.x, a0.y, a0.z, a0.w}, {a1.x, a1.y, a1.z, a1.w}};
-            const float bv[2][4] = {{b0.x, b0.y, b0.z, b0.w}, {b1.x, b1.y, b1.z, b1.w}};
-#pragma unroll
-            for (int s = 0; s < 4; s++)
-#pragma unroll
-                for (int m = 0; m < 2; m++)
-#pragma unroll
-                    for (int n = 0; n < 2; n++)
-                        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m][s], bv[n][s], acc[m][n], 0, 0, 0);
-            // norms for the rounding bound only (any summation order is fine here)
-            if (a_norms && g < KS) {
-                asq0 = fmaf(a0.x, a0.x, fmaf(a0.y, a0.y, fmaf(a0.z, a0.z, fmaf(a0.w, a0.w, asq0))));
-                asq1 = fmaf(a1.x, a1.x, fmaf(a1.y, a1.y, fmaf(a1.z, a1.z, fmaf(a1.w, a1.w, asq1))));
-            }
-            if (b_norms) {
-                bsq0 = fmaf(b0.x, b0.x, fmaf(b0.y, b0.y, fmaf(b0.z, b0.z, fmaf(b0.w, b0.w, bsq0))));
-                bsq1 = fmaf(b1.x, b1.x, fmaf(b1.y, b1.y, fmaf(b1.z, b1.z, fmaf(b1.w, b1.w, bsq1))));
-            }
-        }
-        if ((g % KS) == KS - 1) {
-            // column tile done: fold the accumulators into the lane-local triples
-            const int tc = g / KS;
-#pragma unroll
-            for (int n = 0; n < 2; n++) {
-                const int col = tc * BN + wc * 64 + n * 32 + fr;
-                const bool ok = col < n1;
-#pragma unroll
-                for (int m = 0; m < 2; m++)
-#pragma unroll
-                    for (int q = 0; q < 16; q++) {
-                        push(ok, acc[m][n][q], col, m1[m][q], i1[m][q], m2[m][q]);
-                        acc[m][n][q] = 0.f;
-                    }
-            }
-            if (b_norms) {  // |b_col|^2: the two lane halves hold the two k halves
-                const float c0 = bsq0 + __shfl_xor(bsq0, 32, 64), c1 = bsq1 + __shfl_xor(bsq1, 32, 64);
-                const int col0 = tc * BN + wc * 64 + fr;
-                bmax = fmaxf(bmax, fmaxf(col0 < n1 ? c0 : 0.f, col0 + 32 < n1 ? c1 : 0.f));
-                bsq0 = bsq1 = 0.f;
-            }
-            if (a_norms && tc == 0) {
-                const float r0 = asq0 + __shfl_xor(asq0, 32, 64), r1 = asq1 + __shfl_xor(asq1, 32, 64);
-                if (fh == 0) {
-                    anorm2[ra] = r0;
-                    anorm2[ra + 32] = r1;
-                }
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next slice has landed
-        __syncthreads();
+    for (int tc = 0; tc < ntc; tc++) {
+        const bool last_tile = tc + 1 == ntc;
+        AP_SLICE(0);
+        AP_SLICE(1);
+        AP_SLICE(2);
+        AP_SLICE(3);
+        AP_SLICE(4);
+        AP_SLICE(5);
+        AP_SLICE(6);
+        AP_SLICE(7);
     }
+#undef AP_STAGE
+#undef AP_SLICE
 
     // ---- merge the triples: across the 32 lanes of each half, then across the 2 column waves ----
 #pragma unroll
-    for (int m = 0; m < 2; m++)
+    for (int q = 0; q < 16; q++) {
+        float a1 = m1[q], a2 = m2[q];
+        int ai = i1[q];
 #pragma unroll
-        for (int q = 0; q < 16; q++) {
-            float a1 = m1[m][q], a2 = m2[m][q];
-            int ai = i1[m][q];
-#pragma unroll
-            for (int o = 1; o < 32; o <<= 1) {
-                const float b1 = __shfl_xor(a1, o, 64), b2 = __shfl_xor(a2, o, 64);
-                const int bi = __shfl_xor(ai, o, 64);
-                merge(a1, ai, a2, b1, bi, b2);
-            }
-            if (fr == 0) {
-                const int row = wr * 64 + m * 32 + (q & 3) + 8 * (q >> 2) + 4 * fh;
-                float *tp = trip + (wc * BM + row) * 3;
-                tp[0] = a1;
-                reinterpret_cast<int *>(tp)[1] = ai;
-                tp[2] = a2;
-            }
+        for (int o = 1; o < 32; o <<= 1) {
+            const float b1 = __shfl_xor(a1, o, 64), b2 = __shfl_xor(a2, o, 64);
+            const int bi = __shfl_xor(ai, o, 64);
+            merge(a1, ai, a2, b1, bi, b2);
         }
+        if (fr == 0) {
+            const int row = wr * 32 + (q & 3) + 8 * (q >> 2) + 4 * fh;  // 32x32 C/D row map
+            float *tp = trip + (wc * BM + row) * 3;
+            tp[0] = a1;
+            reinterpret_cast<int *>(tp)[1] = ai;
+            tp[2] = a2;
+        }
+    }
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) bmax = fmaxf(bmax, __shfl_xor(bmax, o, 64));
     if (lane == 0) misc[w] = bmax;
     if (t == 0) *namb_p = 0;
     __syncthreads();
-    const float bmax2 = fmaxf(fmaxf(misc[0], misc[1]), fmaxf(misc[2], misc[3]));
+    float bmax2 = misc[0];
+#pragma unroll
+    for (int k = 1; k < 8; k++) bmax2 = fmaxf(bmax2, misc[k]);
 
     // ---- exact re-score, fast path: the screen maximiser is the only possible maximiser ----
     const double u = 5.9604644775390625e-08;  // 2^-24
@@ -312,7 +341,7 @@ __global__ __launch_bounds__(256, 2) void k_ap_match(int tiles_r, int cap, const
     __syncthreads();
     // ---- slow path: one wave re-scores every column of an ambiguous row exactly ----
     const int namb = *namb_p;
-    for (int k = w; k < namb; k += 4) {
+    for (int k = w; k < namb; k += NT / 64) {
         const int r = amb[k];
         const float *a = A + (size_t)(row0 + r) * KD;
         int best = 0x7fffffff;
@@ -360,9 +389,10 @@ int launch_allpairs_f32(hipStream_t s, void *scratch, int batch, int cap, const 
     const int tiles_r = (cap + BM - 1) / BM;
     const long blocks = (long)batch * tiles_r;
     MV_REQUIRE(blocks < (1l << 31));
+    MV_REQUIRE(cap <= (1 << 21));  // per-lane DMA source offsets are 32-bit byte offsets into a pair
     MV_PROF_BEGIN(s, "k_ap_match");
-    hipLaunchKernelGGL(k_ap_match, dim3((unsigned)blocks), dim3(256), 0, s, tiles_r, cap, n0, n1, desc0, desc1,
-                       thresh, match_idx, match_score);
+    hipLaunchKernelGGL(k_ap_match, dim3((unsigned)blocks), dim3(NT), 0, s, tiles_r, cap, n0, n1, desc0, desc1, thresh,
+                       match_idx, match_score);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     return MV_OK;

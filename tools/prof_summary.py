@@ -39,17 +39,21 @@ for r in stats:
     short = short_name(name)
     summary["kernels"][short] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                                  "total_ns": float(r["TotalDurationNs"]), "pct": float(r.get("Percentage", 0))}
-for C in ("FETCH_SIZE", "WRITE_SIZE"):
-    per = {}
-    for r in rows("pmc_%s/**/*counter_collection.csv" % C):
-        name = short_name(r.get("Kernel_Name", r.get("KernelName", "?")))
-        if r.get("Counter_Name", C) != C:
-            continue
-        per.setdefault(name, []).append(float(r["Counter_Value"]))
-    for k, v in per.items():
-        summary["kernels"].setdefault(k, {})[C + "_KB_avg"] = sum(v) / len(v)
+per = {}
+for r in rows("pmc_*/**/*counter_collection.csv"):
+    name = short_name(r.get("Kernel_Name", r.get("KernelName", "?")))
+    per.setdefault((name, r["Counter_Name"]), []).append(float(r["Counter_Value"]))
+for (k, c), v in per.items():
+    key = c + "_KB_avg" if c in ("FETCH_SIZE", "WRITE_SIZE") else c + "_avg"
+    summary["kernels"].setdefault(k, {})[key] = sum(v) / len(v)
 for k, v in summary["kernels"].items():
     if "FETCH_SIZE_KB_avg" in v or "WRITE_SIZE_KB_avg" in v:
         v["hbm_bytes_per_launch"] = 2 * v.get("FETCH_SIZE_KB_avg", 0) * 1024 + v.get("WRITE_SIZE_KB_avg", 0) * 1024
+for k, v in summary["kernels"].items():
+    if "GRBM_GUI_ACTIVE_avg" in v and "avg_ns" in v:
+        v["effective_clock_GHz"] = v["GRBM_GUI_ACTIVE_avg"] / 8 / v["avg_ns"]
+    if "SQ_VALU_MFMA_BUSY_CYCLES_avg" in v and "GRBM_GUI_ACTIVE_avg" in v:
+        # MFMA busy cycles summed over SIMDs (1024) vs GPU-active cycles (summed over 8 XCDs)
+        v["mfma_busy_frac"] = v["SQ_VALU_MFMA_BUSY_CYCLES_avg"] / (1024 * v["GRBM_GUI_ACTIVE_avg"] / 8)
 json.dump(summary, open(os.path.join(out, "summary_%s.json" % tag), "w"), indent=1)
 print(json.dumps(summary, indent=1))
