@@ -1,32 +1,34 @@
 // k_allpairs_f32.hip -- all-pairs fp32 descriptor match (python/pairwise_pnp.py:635-659)
 // with the gemmini_functions_cpu.h:14-56 summation order as the exact score.
 //
-// Two kernels per batch:
-//   k_ap_split  one pass over both frames: every fp32 descriptor a becomes a bf16 pair
-//               (a_hi = bf16(a), a_lo = bf16(a - a_hi)) stored SLICE-INTERLEAVED
-//               ([hi k0..k0+31 | lo k0..k0+31] per 32-wide k slice, 1 KiB per row, the
-//               same bytes as the fp32 row) and |a|^2.  HBM-bound: 4 B read + 4 B written
-//               per element.
-//   k_ap_match  a 512-thread block (8 waves: 4 row groups x 2 column groups) owns 128 query
-//               rows of one pair and sweeps ALL column tiles of the other frame:
-//     * screen S ~= D0 . D1^T as a_hi b_hi + a_hi b_lo + a_lo b_hi on
-//       v_mfma_f32_32x32x16_bf16 (3 bf16 products per fp32 product: 3/16 of the fp32-MFMA
-//       cycles), each wave 32 rows x 64 columns of a 128-column tile;
-//     * k streamed in 32-wide slices through a NBUF-deep LDS ring filled by
+// Two kernels per batch (plus a 4-byte-per-pair memset):
+//   k_ap_split  one pass over both frames: every fp32 descriptor row becomes an fp16 row of
+//               2^14 * a (round to nearest even; 512 B per row) and |a|^2.  A pair whose
+//               values leave |a_k| < 2 (or are not finite) is flagged: all of its rows take the
+//               exact slow path, so the fp16 range never has to be trusted.  HBM-bound: 4 B read
+//               + 2 B written per element.
+//   k_ap_match  a 512-thread block (8 waves, 2 per SIMD, 32 rows each) owns 256 query rows of
+//               one pair and sweeps ALL column tiles of the other frame:
+//     * the wave's 32 rows x 256 k of A (fp16, 64 VGPRs) are loaded ONCE into registers;
+//       only B streams (512 B per column per block);
+//     * screen S ~= D0 . D1^T on v_mfma_f32_32x32x16_f16 (exact fp16 products, fp32
+//       accumulation), each wave 32 rows x 128 columns of a tile (4 accumulators);
+//     * k streamed in 64-wide slices (128 B per row) through a NBUF-deep LDS ring filled by
 //       global_load_lds (HBM/L2 -> LDS DMA, no staging VGPRs, issued NBUF-1 slices ahead),
 //       XOR-swizzled by 16-B chunk (chunk ^ ((row >> 1) & 7)) on the SOURCE address and on
 //       the read -> conflict-free ds_read_b128; one barrier per slice;
 //     * after each column tile every lane folds its accumulators into a lane-local running
 //       (max1, idx1, max2) per row (selects only);
-//     * at the end: cross-lane / cross-wave merge of the triples, then the EXACT re-score in
-//       the reference order (v_mul_f32 + v_add_f32, k = 0..255, fp32 inputs) of the screen
-//       maximiser.
+//     * at the end: cross-lane merge of the triples, then the EXACT re-score in the reference
+//       order (v_mul_f32 + v_add_f32, k = 0..255, fp32 inputs) of the screen maximiser.
 //   Why the result is exact (bit-identical to the reference): with d_j the real dot product,
-//   s_j the screen and e_j the reference's sequential fp32 sum,
-//     |s_j - d_j| <= ds = (3.1 * 2^-16 + 1.02 gamma_768(2^-23)) |a| max|b|
-//       (split residuals and the dropped a_lo b_lo term; 768 fp32 accumulations inside the
-//        MFMA bounded with unit roundoff 2^-23, i.e. even for truncating adders),
-//     |e_j - d_j| <= de = gamma_256(2^-24) |a| |b|.
+//   s_j the screen (unscaled by 2^-28) and e_j the reference's sequential fp32 sum,
+//     |s_j - d_j| <= ds = (2^-10 + 2^-22 + 1.01 gamma_256(2^-23)) |a| B
+//                         + 1.001 * 2^-24 (|a| + B) + 2^-48,          B = max_j |b_j|
+//       (fp16 rounding 2^-11 per operand; values below the fp16 normal range, 2^-28 in
+//        original units, bounded as if flushed; sum |x_k| <= 16 |x|; 256 fp32 accumulations
+//        inside the MFMA bounded with unit roundoff 2^-23, i.e. even for truncating adders),
+//     |e_j - d_j| <= de = gamma_256(2^-24) |a| B.
 //   Any column whose exact score can reach the screen maximiser's has s_j >= M - 2(ds + de).
 //   If the runner-up screen value is below that window, the screen maximiser IS the
 //   reference's maximiser (ties included) and one exact dot decides the threshold; otherwise
@@ -34,42 +36,68 @@
 //   only rows that can pass the threshold and have a near-equal runner-up reach it).
 //   Result = the reference's rule: the first j with the maximum exact score, kept when
 //   (double)score > thresh and score > 0 (max_score starts at 0, pairwise_pnp.py:644).
-// Bound: BF16 MFMA.  Per pair 2 * n0 * n1 * 256 algorithmic FLOP (536.9 MFLOP at 1024^2),
-// executed as 3x that on the bf16 pipe: peak 2.5 PF / 3 = 833 TF/s fp32-equivalent.
+// Bound: FP16 MFMA.  Per pair 2 * n0 * n1 * 256 algorithmic FLOP (536.9 MFLOP at 1024^2);
+// dense fp16 MFMA peak 2.5 PF/s.
 #include <math.h>
 
 #include "mv_internal.hpp"
 
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 32, KD = 256, KS = KD / BK, NT = 512, NBUF = 4;
-constexpr int ROW_BYTES = 2 * KD * 2;            // split row: 256 hi + 256 lo bf16 = 1 KiB
-constexpr int SL_ROW = BK * 2 * 2;               // one row of one slice: 32 hi + 32 lo = 128 B
-constexpr int SL_BYTES = BM * SL_ROW;            // one operand slice (A or B): 16 KiB
-constexpr int BUF_BYTES = 2 * SL_BYTES;          // A + B
-static_assert(KS % NBUF == 0, "ring slots must be compile-time per slice");
+constexpr int BM = 256, BN = 128, BK = 64, KD = 256, KS = KD / BK, NT = 512, NW = NT / 64, RW = BM / NW;
+#ifndef AP_NBUF
+#define AP_NBUF 4
+#endif
+constexpr int NBUF = AP_NBUF;
+// timing experiments only (wrong results): drop the DMA waits / barriers / MFMAs / DMAs
+#ifndef AP_EXP_NOWAIT
+#define AP_EXP_NOWAIT 0
+#endif
+#ifndef AP_EXP_NOBAR
+#define AP_EXP_NOBAR 0
+#endif
+#ifndef AP_EXP_NOMFMA
+#define AP_EXP_NOMFMA 0
+#endif
+#ifndef AP_EXP_NODMA
+#define AP_EXP_NODMA 0
+#endif
+constexpr int ROW_BYTES = KD * 2;                // fp16 row: 512 B
+constexpr int SL_ROW = BK * 2;                   // one row of one slice: 64 fp16 = 128 B
+constexpr int SL_BYTES = BN * SL_ROW;            // one B slice: 16 KiB
+constexpr int DMA_PER_SLICE = BN / 8 / NW;       // 1-KiB DMA instructions per wave per slice
+constexpr float SCALE = 16384.f;                 // 2^14: |a_k| < 2 -> |2^14 a_k| < 2^15 < 65504
+static_assert(KS % NBUF == 0 || NBUF % KS == 0, "ring slots must be compile-time per slice");
+static_assert(RW == 32 && DMA_PER_SLICE == 2, "one wave per 32 rows (32x32 MFMA), 2 DMA per slice");
 // LDS map (ONE array -- a second __shared__ object can de-pipeline the DMA), byte offsets
-constexpr int OFF_STAGE = 0;                     // [NBUF][A, B][128 rows][128 B]
-constexpr int OFF_TRIP = NBUF * BUF_BYTES;       // [2 wc][128] {m1, i1, m2}
-constexpr int OFF_AMB = OFF_TRIP + 2 * BM * 12;  // [128] i32 ambiguous rows
-constexpr int OFF_MISC = OFF_AMB + BM * 4;       // [8] f32 per-wave max|b|^2, [1] i32 #ambiguous
-constexpr int LDS_BYTES = OFF_MISC + 48;
+constexpr int OFF_STAGE = 0;                     // [NBUF][128 B rows][128 B]
+constexpr int OFF_TRIP = NBUF * SL_BYTES;        // [256] {m1, i1, m2}
+constexpr int OFF_AMB = OFF_TRIP + BM * 12;      // [256] i32 ambiguous rows
+constexpr int OFF_MISC = OFF_AMB + BM * 4;       // [NW] f32 per-wave max|b|^2, [1] i32 #ambiguous
+constexpr int LDS_BYTES = OFF_MISC + 4 * NW + 16;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
 // 16-B-per-lane HBM/L2 -> LDS DMA (global_load_lds_dwordx4, SADDR form): source = SGPR
 // base + 32-bit VGPR byte offset; LDS destination = M0 (wave-uniform byte address) + lane *
-// 16.  No instruction offset: it would displace the LDS destination as well.  The slice's
-// K offset goes into the scalar base instead (one s_add per load, no VALU).
-#pragma clang diagnostic push
+// 16.  No instruction offset: it would displace the LDS destination as well.  The constant
+// K offset (KOFF) and LDS offset (DOFF) are added INSIDE the asm, so the compiler cannot
+// hoist one address per slice into long-lived registers.
+// (the m0 clobber warning fires at template instantiation: ignored for the whole file)
 #pragma clang diagnostic ignored "-Winline-asm"
+template <int KOFF, int DOFF>
 __device__ __forceinline__ void glds16(const void *sbase, unsigned voff, unsigned lds_byte) {
-    asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds_byte)
-                 : "memory", "m0");
+    unsigned tmp;
+    asm volatile(
+        "v_add_u32 %0, %4, %1\n\t"
+        "s_add_u32 m0, %3, %5\n\t"
+        "global_load_lds_dwordx4 %0, %2"
+        : "=&v"(tmp)
+        : "v"(voff), "s"(sbase), "s"(lds_byte), "i"(KOFF), "i"(DOFF)
+        : "memory", "m0", "scc");
 }
-#pragma clang diagnostic pop
 
 // s_waitcnt on vmcnt only (expcnt / lgkmcnt left at their no-wait maxima)
 template <int N>
@@ -78,17 +106,34 @@ __device__ __forceinline__ void wait_vm() {
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-// Fold one tile's two columns of a row (v0 at column j, v1 at j + 32; -inf past n1) into the
-// running triple.  Earlier tiles hold smaller column indices, so a tie never replaces
-// (strict >); within the pair the lower column wins a tie.  Selects only.
-__device__ __forceinline__ void fold2(float v0, float v1, int j, float &m1, int &i1, float &m2) {
-    const bool hi = v1 > v0;
-    const float t1 = fmaxf(v0, v1), t2 = fminf(v0, v1);
-    const int tj = hi ? j + 32 : j;
-    const bool top = t1 > m1;
-    m2 = top ? fmaxf(m1, t2) : fmaxf(m2, t1);
-    m1 = top ? t1 : m1;
-    i1 = top ? tj : i1;
+// max / min as v_med3_f32 against -/+inf: no NaN-quieting v_max(x, x) in front (inputs are
+// MFMA results, never NaN for finite descriptors)
+__device__ __forceinline__ float vmax(float a, float b) { return __builtin_amdgcn_fmed3f(a, b, __builtin_inff()); }
+__device__ __forceinline__ float vmin(float a, float b) { return __builtin_amdgcn_fmed3f(a, b, -__builtin_inff()); }
+
+// Top-2 of a set of columns: largest value m1 at column i (lowest column on a tie) and the
+// second largest value m2 (equal to m1 on a tie).  Min/max/select only.
+struct Top2 {
+    float m1, m2;
+    int i;
+};
+__device__ __forceinline__ Top2 leaf2(float va, int ca, float vb, int cb) {  // ca < cb
+    int i = vb > va ? cb : ca;
+    asm volatile("" : "+v"(i));  // materialise: keeps later updates selects, not branches
+    return {vmax(va, vb), vmin(va, vb), i};
+}
+__device__ __forceinline__ Top2 join2(const Top2 &x, const Top2 &y) {  // x's columns < y's columns
+    const bool up = y.m1 > x.m1;
+    return {vmax(x.m1, y.m1), vmax(vmin(x.m1, y.m1), vmax(x.m2, y.m2)), up ? y.i : x.i};
+}
+// Fold one row's 4 values of a tile (columns j + 32 c, c = 0..3; -inf past n1) into the running
+// triple; an earlier tile's column is kept on a tie (strict >).
+__device__ __forceinline__ void fold4(float v0, float v1, float v2, float v3, int j, float &m1, int &i1,
+                                      float &m2) {
+    const Top2 t = join2(leaf2(v0, j, v1, j + 32), leaf2(v2, j + 64, v3, j + 96));
+    m2 = vmax(vmin(m1, t.m1), vmax(m2, t.m2));
+    i1 = t.m1 > m1 ? t.i : i1;
+    m1 = vmax(m1, t.m1);
 }
 
 // order-independent merge of two (max1, idx1, max2) triples
@@ -124,17 +169,12 @@ __device__ __forceinline__ float exact_dot(const float *__restrict__ a, const fl
     return s;
 }
 
-__device__ __forceinline__ unsigned pack_bf16(float x, float y) {
-    const bf16x2 v = {(__bf16)x, (__bf16)y};  // v_cvt_pk_bf16_f32 (round to nearest even)
-    return __builtin_bit_cast(unsigned, v);
-}
-
 // ---- k_ap_split: one wave per descriptor row (rows >= n are never read downstream) ----
 __global__ __launch_bounds__(256) void k_ap_split(int batch, int cap, const int *__restrict__ n0v,
                                                   const int *__restrict__ n1v, const float *__restrict__ desc0,
-                                                  const float *__restrict__ desc1, char *__restrict__ split0,
-                                                  char *__restrict__ split1, float *__restrict__ nrm0,
-                                                  float *__restrict__ nrm1) {
+                                                  const float *__restrict__ desc1, char *__restrict__ h0,
+                                                  char *__restrict__ h1, float *__restrict__ nrm0,
+                                                  float *__restrict__ nrm1, int *__restrict__ bad) {
     const long R = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
     const long per_frame = (long)batch * cap;
     if (R >= 2 * per_frame) return;
@@ -144,15 +184,11 @@ __global__ __launch_bounds__(256) void k_ap_split(int batch, int cap, const int 
     if (r >= (frame ? n1v : n0v)[pair]) return;
     const int lane = threadIdx.x & 63;
     const float4 v = *reinterpret_cast<const float4 *>((frame ? desc1 : desc0) + fr * KD + lane * 4);
-    const unsigned h01 = pack_bf16(v.x, v.y), h23 = pack_bf16(v.z, v.w);
-    // a - a_hi is exact in f32 (a_hi is within 2^-8 of a); then rounded to bf16
-    const float hx = __uint_as_float(h01 << 16), hy = __uint_as_float(h01 & 0xffff0000u);
-    const float hz = __uint_as_float(h23 << 16), hw = __uint_as_float(h23 & 0xffff0000u);
-    const unsigned l01 = pack_bf16(v.x - hx, v.y - hy), l23 = pack_bf16(v.z - hz, v.w - hw);
-    // element k = 4 lane .. 4 lane + 3 sits in slice lane / 8 at position (lane & 7) * 4
-    char *row = (frame ? split1 : split0) + fr * ROW_BYTES + (lane >> 3) * SL_ROW + (lane & 7) * 8;
-    *reinterpret_cast<uint2 *>(row) = make_uint2(h01, h23);
-    *reinterpret_cast<uint2 *>(row + BK * 2) = make_uint2(l01, l23);
+    const bool ok = fabsf(v.x) < 2.f && fabsf(v.y) < 2.f && fabsf(v.z) < 2.f && fabsf(v.w) < 2.f;  // NaN: false
+    if (__builtin_amdgcn_ballot_w64(!ok) != 0 && lane == 0) bad[pair] = 1;
+    const f16x4 h = {(_Float16)(v.x * SCALE), (_Float16)(v.y * SCALE), (_Float16)(v.z * SCALE),
+                     (_Float16)(v.w * SCALE)};  // exact power-of-two scale, then RNE to fp16
+    *reinterpret_cast<f16x4 *>((frame ? h1 : h0) + fr * ROW_BYTES + lane * 8) = h;
     float q = fmaf(v.x, v.x, fmaf(v.y, v.y, fmaf(v.z, v.z, v.w * v.w)));
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) q += __shfl_xor(q, o, 64);
@@ -161,22 +197,21 @@ __global__ __launch_bounds__(256) void k_ap_split(int batch, int cap, const int 
 
 __global__ __launch_bounds__(NT, 1) void k_ap_match(int tiles_r, int cap, const int *__restrict__ n0v,
                                                     const int *__restrict__ n1v, const float *__restrict__ desc0,
-                                                    const float *__restrict__ desc1,
-                                                    const char *__restrict__ split0,
-                                                    const char *__restrict__ split1,
-                                                    const float *__restrict__ nrm0,
-                                                    const float *__restrict__ nrm1, double thresh,
-                                                    int *__restrict__ match_idx, float *__restrict__ match_score) {
+                                                    const float *__restrict__ desc1, const char *__restrict__ h0,
+                                                    const char *__restrict__ h1, const float *__restrict__ nrm0,
+                                                    const float *__restrict__ nrm1, const int *__restrict__ bad,
+                                                    double thresh, int *__restrict__ match_idx,
+                                                    float *__restrict__ match_score) {
     __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
     float *trip = reinterpret_cast<float *>(lds + OFF_TRIP);
     int *amb = reinterpret_cast<int *>(lds + OFF_AMB);
     float *misc = reinterpret_cast<float *>(lds + OFF_MISC);
-    int *namb_p = reinterpret_cast<int *>(lds + OFF_MISC) + 8;
+    int *namb_p = reinterpret_cast<int *>(lds + OFF_MISC) + NW;
 
     const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int pair = L / tiles_r, tr = L % tiles_r;
     const int n0 = n0v[pair], n1 = n1v[pair];
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int row0 = tr * BM;
     int *oidx = match_idx + (size_t)pair * cap + row0;
     float *oscore = match_score + (size_t)pair * cap + row0;
@@ -186,46 +221,43 @@ __global__ __launch_bounds__(NT, 1) void k_ap_match(int tiles_r, int cap, const 
         oscore[t] = 0.f;
     }
     if (row0 >= n0 || n1 <= 0) return;
-    const char *SA = split0 + (size_t)pair * cap * ROW_BYTES;
-    const char *SB = split1 + (size_t)pair * cap * ROW_BYTES;
-    const int ntc = (n1 + BN - 1) / BN;
+    const bool flagged = bad[pair] != 0;
+    const char *SA = h0 + (size_t)pair * cap * ROW_BYTES;
+    const char *SB = h1 + (size_t)pair * cap * ROW_BYTES;
+    const int ntc = flagged ? 0 : (n1 + BN - 1) / BN;  // a flagged pair skips the screen
 
-    // ---- DMA map: wave w fills rows w*16 .. w*16+15 of each slice (A and B), 8 rows
-    //      (1 KiB) per instruction; lane l lands at row (l >> 3), chunk position l & 7 and
-    //      fetches source chunk (l & 7) ^ ((row >> 1) & 7) of that row ----
+    // ---- B DMA map: wave w fills rows w*16 .. w*16+15 of each slice, 8 rows (1 KiB) per
+    //      instruction; lane l lands at row (l >> 3), chunk position l & 7 and fetches
+    //      source chunk (l & 7) ^ ((row >> 1) & 7) of that row ----
     const int wu = __builtin_amdgcn_readfirstlane(w);
-    const int dr0 = wu * 16 + (lane >> 3), dr1 = dr0 + 8;
-    const int dc0 = ((lane & 7) ^ ((dr0 >> 1) & 7)) * 16, dc1 = ((lane & 7) ^ ((dr1 >> 1) & 7)) * 16;
-    // per-lane source byte offsets (rows clamped into [0, n)); A's stay fixed, B's advance per tile
-    const unsigned oA0 = (unsigned)min(row0 + dr0, n0 - 1) * ROW_BYTES + dc0;
-    const unsigned oA1 = (unsigned)min(row0 + dr1, n0 - 1) * ROW_BYTES + dc1;
-    unsigned oB0 = (unsigned)min(dr0, n1 - 1) * ROW_BYTES + dc0;
-    unsigned oB1 = (unsigned)min(dr1, n1 - 1) * ROW_BYTES + dc1;
+    const int dr = wu * 16 + (lane >> 3);
+    // ((dr + 8) >> 1) & 7 = ((dr >> 1) & 7) ^ 4
+    const unsigned dcb = (unsigned)((lane & 7) ^ ((dr >> 1) & 7)) * 16, dcb4 = dcb ^ 64u;
+    unsigned oB0 = (unsigned)min(dr, n1 - 1) * ROW_BYTES + dcb;
+    unsigned oB1 = (unsigned)min(dr + 8, n1 - 1) * ROW_BYTES + dcb4;
     const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char *)(lds + OFF_STAGE);
     const unsigned dst_w = lds_base + (unsigned)(wu * 16 * SL_ROW);
 #define AP_STAGE(BUF, KSI)                                                                   \
     do {                                                                                     \
-        const unsigned d_ = dst_w + (unsigned)((BUF) * BUF_BYTES);                           \
-        const char *sa_ = SA + (KSI) * SL_ROW, *sb_ = SB + (KSI) * SL_ROW;                   \
-        glds16(sa_, oA0, d_);                                                                \
-        glds16(sa_, oA1, d_ + 8 * SL_ROW);                                                   \
-        glds16(sb_, oB0, d_ + SL_BYTES);                                                     \
-        glds16(sb_, oB1, d_ + SL_BYTES + 8 * SL_ROW);                                        \
+        glds16<(KSI) * SL_ROW, (BUF) * SL_BYTES>(SB, oB0, dst_w);                            \
+        glds16<(KSI) * SL_ROW, (BUF) * SL_BYTES + 8 * SL_ROW>(SB, oB1, dst_w);               \
     } while (0)
 
-    // ---- fragment read map: at k16 step s of a slice, lane half h holds k = s*16 + h*8 .. +7:
-    //      hi chunk s*2 + h, lo chunk 4 + s*2 + h of the 128-B slice row ----
+    // ---- fragment map (v_mfma_f32_32x32x16_f16): lane l holds row/column l & 31 and
+    //      k = 16 s + 8 (l >> 5) .. +7 at k16 step s, i.e. chunk 2 (s % 4) + (l >> 5) of slice
+    //      s / 4.  A (this wave's 32 rows x 256 k: 64 VGPRs) stays in registers.
     const int fr = lane & 31, fh = lane >> 5;
-    const int ra = wr * 32 + fr, rb = wc * 64 + fr;  // rb + 32 has the same swizzle
-    const int swa = (ra >> 1) & 7, swb = (rb >> 1) & 7;
-    const int offa = ra * SL_ROW, offb = SL_BYTES + rb * SL_ROW;
-
-    f32x16 acc0, acc1;
+    f16x8 aF[KD / 16];
+    {
+        const char *arow = SA + (size_t)min(row0 + w * RW + fr, n0 - 1) * ROW_BYTES + fh * 16;
 #pragma unroll
-    for (int q = 0; q < 16; q++) {
-        acc0[q] = 0.f;
-        acc1[q] = 0.f;
+        for (int s = 0; s < KD / 16; s++) aF[s] = *reinterpret_cast<const f16x8 *>(arow + s * 32);
     }
+    const int swb = (fr >> 1) & 7;  // rows 32 c + fr share it
+    const int offb = fr * SL_ROW;
+
+    const f32x16 zero16 = {};
+    f32x16 acc0 = zero16, acc1 = zero16, acc2 = zero16, acc3 = zero16;
     float m1[16], m2[16];
     int i1[16];
 #pragma unroll
@@ -238,79 +270,86 @@ __global__ __launch_bounds__(NT, 1) void k_ap_match(int tiles_r, int cap, const 
     // Ring schedule: global slice g = tc*KS + ks lives in slot g % NBUF = ks % NBUF.  At slice
     // g the block issues slice g + NBUF - 1 into the slot read at g - 1 (freed by that
     // slice's barrier), computes slice g, then waits until slice g + 1 has landed: the DMA
-    // groups issued after it (4 instructions each) may stay in flight.
+    // groups issued after it (DMA_PER_SLICE instructions each) may stay in flight.
+#define AP_MF(ACC, CG, S, FIRST)                                                              \
+    do {                                                                                      \
+        const f16x8 b_ = *reinterpret_cast<const f16x8 *>(                                    \
+            base + offb + (CG) * 32 * SL_ROW + (((2 * (S) + fh) ^ swb) * 16));                \
+        ACC = __builtin_amdgcn_mfma_f32_32x32x16_f16(aF[kk_ + (S)], b_, (FIRST) ? zero16 : ACC, 0, 0, 0); \
+    } while (0)
 #define AP_SLICE(ks)                                                                          \
     do {                                                                                      \
         constexpr int nx = (ks) + NBUF - 1; /* slice issued now, counted from this tile */    \
-        if constexpr (nx < KS) {                                                              \
+        if (AP_EXP_NODMA) {                                                                   \
+        } else if constexpr (nx < KS) {                                                       \
             AP_STAGE(nx % NBUF, nx);                                                          \
-        } else if (!last_tile) {                                                              \
-            if constexpr (nx == KS) { /* first slice of the next column tile */               \
-                oB0 = (unsigned)min((tc + 1) * BN + dr0, n1 - 1) * ROW_BYTES + dc0;           \
-                oB1 = (unsigned)min((tc + 1) * BN + dr1, n1 - 1) * ROW_BYTES + dc1;           \
+        } else if (tc + nx / KS < ntc) {                                                      \
+            if constexpr (nx % KS == 0) { /* first slice of a later column tile */            \
+                const int nb_ = (tc + nx / KS) * BN + dr;                                     \
+                oB0 = (unsigned)min(nb_, n1 - 1) * ROW_BYTES + dcb;                           \
+                oB1 = (unsigned)min(nb_ + 8, n1 - 1) * ROW_BYTES + dcb4;                      \
             }                                                                                 \
-            AP_STAGE(nx % NBUF, nx - KS);                                                     \
+            AP_STAGE(nx % NBUF, nx % KS);                                                     \
         }                                                                                     \
-        const char *base = lds + OFF_STAGE + ((ks) % NBUF) * BUF_BYTES;                       \
-        _Pragma("unroll") for (int st = 0; st < 2; st++) {                                    \
-            const int ch = st * 2 + fh;                                                       \
-            const bf16x8 ah = *reinterpret_cast<const bf16x8 *>(base + offa + ((ch ^ swa) * 16));       \
-            const bf16x8 al = *reinterpret_cast<const bf16x8 *>(base + offa + (((ch + 4) ^ swa) * 16)); \
-            const bf16x8 b0h = *reinterpret_cast<const bf16x8 *>(base + offb + ((ch ^ swb) * 16));      \
-            const bf16x8 b0l = *reinterpret_cast<const bf16x8 *>(base + offb + (((ch + 4) ^ swb) * 16)); \
-            const bf16x8 b1h = *reinterpret_cast<const bf16x8 *>(base + offb + 32 * SL_ROW + ((ch ^ swb) * 16)); \
-            const bf16x8 b1l =                                                                \
-                *reinterpret_cast<const bf16x8 *>(base + offb + 32 * SL_ROW + (((ch + 4) ^ swb) * 16)); \
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b0h, acc0, 0, 0, 0);           \
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b1h, acc1, 0, 0, 0);           \
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b0l, acc0, 0, 0, 0);           \
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, b1l, acc1, 0, 0, 0);           \
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, b0h, acc0, 0, 0, 0);           \
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, b1h, acc1, 0, 0, 0);           \
+        const char *base = lds + OFF_STAGE + ((ks) % NBUF) * SL_BYTES;                        \
+        constexpr int kk_ = (ks) * 4; /* first k16 step of this slice */                      \
+        if (!AP_EXP_NOMFMA) {                                                                 \
+            _Pragma("unroll") for (int s_ = 0; s_ < 4; s_++) {                                \
+                AP_MF(acc0, 0, s_, (ks) == 0 && s_ == 0);                                     \
+                AP_MF(acc1, 1, s_, (ks) == 0 && s_ == 0);                                     \
+                AP_MF(acc2, 2, s_, (ks) == 0 && s_ == 0);                                     \
+                AP_MF(acc3, 3, s_, (ks) == 0 && s_ == 0);                                     \
+            }                                                                                 \
         }                                                                                     \
         if constexpr ((ks) == KS - 1) { /* column tile done: fold into the lane triples */    \
-            const int col = tc * BN + wc * 64 + fr;                                           \
-            const float lo0 = col < n1 ? 0.f : -__builtin_inff(); /* + 0 keeps, + -inf drops */ \
-            const float lo1 = col + 32 < n1 ? 0.f : -__builtin_inff();                        \
-            _Pragma("unroll") for (int q = 0; q < 16; q++) {                                  \
-                fold2(acc0[q] + lo0, acc1[q] + lo1, col, m1[q], i1[q], m2[q]);                \
-                acc0[q] = 0.f;                                                                \
-                acc1[q] = 0.f;                                                                \
+            const int col = tc * BN + fr;                                                     \
+            if (tc + 1 == ntc) { /* only the last tile can reach past n1: + 0 keeps, + -inf drops */ \
+                const float lo0 = col < n1 ? 0.f : -__builtin_inff();                         \
+                const float lo1 = col + 32 < n1 ? 0.f : -__builtin_inff();                    \
+                const float lo2 = col + 64 < n1 ? 0.f : -__builtin_inff();                    \
+                const float lo3 = col + 96 < n1 ? 0.f : -__builtin_inff();                    \
+                _Pragma("unroll") for (int q = 0; q < 16; q++) {                              \
+                    acc0[q] += lo0;                                                           \
+                    acc1[q] += lo1;                                                           \
+                    acc2[q] += lo2;                                                           \
+                    acc3[q] += lo3;                                                           \
+                }                                                                             \
             }                                                                                 \
+            _Pragma("unroll") for (int q = 0; q < 16; q++)                                    \
+                fold4(acc0[q], acc1[q], acc2[q], acc3[q], col, m1[q], i1[q], m2[q]);          \
         }                                                                                     \
         /* slice g + 1 must have landed: in flight after it are the groups of slices */       \
-        /* g + 2 .. g + NBUF - 1, all issued unless past the block's last slice */           \
-        if (!last_tile) {                                                                     \
-            wait_vm<4 * (NBUF - 2)>();                                                        \
+        /* g + 2 .. g + NBUF - 1 that exist (the block's last slice is ntc*KS - 1) */        \
+        if (AP_EXP_NOWAIT) {                                                                  \
+        } else if (tc + (nx + 0) / KS < ntc) { /* every slice up to g + NBUF - 1 was issued */ \
+            wait_vm<DMA_PER_SLICE * (NBUF - 2)>();                                            \
         } else {                                                                              \
-            constexpr int fl = (KS - 2 - (ks)) < (NBUF - 2) ? (KS - 2 - (ks)) : (NBUF - 2);  \
-            wait_vm<4 * (fl > 0 ? fl : 0)>();                                                 \
+            wait_vm<0>(); /* tail of the sweep: drain */                                      \
         }                                                                                     \
-        __syncthreads();                                                                      \
+        if (!AP_EXP_NOBAR) __syncthreads();                                                   \
     } while (0)
 
-    // prologue: slices 0 .. NBUF-2 of tile 0, then wait for slice 0
+    // prologue: slices 0 .. NBUF-2 (of tile 0, and tile 1 when KS < NBUF - 1)
     static_assert(NBUF == 4, "prologue issues NBUF - 1 = 3 slices");
-    AP_STAGE(0, 0);
-    AP_STAGE(1, 1);
-    AP_STAGE(2, 2);
-    wait_vm<4 * (NBUF - 2)>();
+    static_assert(KS == 4, "prologue slices 0..2 all belong to tile 0");
+    if (ntc > 0) {
+        AP_STAGE(0, 0);
+        AP_STAGE(1, 1);
+        AP_STAGE(2, 2);
+    }
+    wait_vm<0>();
     __syncthreads();
     for (int tc = 0; tc < ntc; tc++) {
-        const bool last_tile = tc + 1 == ntc;
         AP_SLICE(0);
         AP_SLICE(1);
         AP_SLICE(2);
         AP_SLICE(3);
-        AP_SLICE(4);
-        AP_SLICE(5);
-        AP_SLICE(6);
-        AP_SLICE(7);
     }
 #undef AP_STAGE
 #undef AP_SLICE
+#undef AP_MF
 
-    // ---- merge the triples: across the 32 lanes of each half, then across the 2 column waves ----
+    // ---- merge the triples across the 32 lanes (columns) that share a row ----
 #pragma unroll
     for (int q = 0; q < 16; q++) {
         float a1 = m1[q], a2 = m2[q];
@@ -322,8 +361,8 @@ __global__ __launch_bounds__(NT, 1) void k_ap_match(int tiles_r, int cap, const 
             merge(a1, ai, a2, b1, bi, b2);
         }
         if (fr == 0) {
-            const int row = wr * 32 + (q & 3) + 8 * (q >> 2) + 4 * fh;  // 32x32 C/D row map
-            float *tp = trip + (wc * BM + row) * 3;
+            const int row = w * RW + (q & 3) + 8 * (q >> 2) + 4 * fh;  // 32x32 C/D row map
+            float *tp = trip + row * 3;
             tp[0] = a1;
             reinterpret_cast<int *>(tp)[1] = ai;
             tp[2] = a2;
@@ -340,29 +379,31 @@ __global__ __launch_bounds__(NT, 1) void k_ap_match(int tiles_r, int cap, const 
     __syncthreads();
     float bmax2 = misc[0];
 #pragma unroll
-    for (int k = 1; k < 8; k++) bmax2 = fmaxf(bmax2, misc[k]);
+    for (int k = 1; k < NW; k++) bmax2 = fmaxf(bmax2, misc[k]);
 
     // ---- exact re-score, fast path: the screen maximiser is the only possible maximiser ----
     const float *A = desc0 + (size_t)pair * cap * KD;
     const float *B = desc1 + (size_t)pair * cap * KD;
     const double u24 = 5.9604644775390625e-08, u23 = 2 * u24;
     const double gam_e = KD * u24 / (1.0 - KD * u24);
-    const double gam_s = 3 * KD * u23 / (1.0 - 3 * KD * u23);
-    const double coef = 3.1 * 1.52587890625e-05 + 1.02 * gam_s + gam_e;  // ds + de per |a| max|b|
-    const double nb = sqrt((double)bmax2);
+    const double gam_s = KD * u23 / (1.0 - KD * u23);
+    const double rel = 9.765625e-04 + 2.384185791015625e-07 + 1.01 * gam_s + gam_e;  // 2^-10 + 2^-22 + ...
+    const double Bn = sqrt((double)bmax2);
     if (t < BM && row0 + t < n0) {
-        const float *tp0 = trip + t * 3, *tp1 = trip + (BM + t) * 3;
-        float M = tp0[0], M2 = tp0[2];
-        int I = reinterpret_cast<const int *>(tp0)[1];
-        merge(M, I, M2, tp1[0], reinterpret_cast<const int *>(tp1)[1], tp1[2]);
-        const double delta = coef * sqrt((double)nrm0[(size_t)pair * cap + row0 + t]) * nb * 1.01 + 1e-30;
+        const float *tp = trip + t * 3;
+        const float M = tp[0], M2 = tp[2];
+        const int I = reinterpret_cast<const int *>(tp)[1];
+        const double an = sqrt((double)nrm0[(size_t)pair * cap + row0 + t]);
+        const double delta =
+            (rel * an * Bn + 1.001 * 5.9604644775390625e-08 * (an + Bn) + 3.552713678800501e-15) * 1.01 + 1e-30;
+        const double Ms = (double)M * 3.725290298461914e-09;  // screen / 2^28
+        const double M2s = (double)M2 * 3.725290298461914e-09;
         int best = -1;
         float bs = 0.f;
-        bool ambiguous = false;
-        if ((double)M + delta > thresh) {
-            if ((double)M2 >= (double)M - 2.0 * delta) {
+        bool ambiguous = flagged;
+        if (!flagged && Ms + delta > thresh) {
+            if (M2s >= Ms - 2.0 * delta) {
                 ambiguous = true;
-                amb[atomicAdd(namb_p, 1)] = t;
             } else {
                 const float e = exact_dot(A + (size_t)(row0 + t) * KD, B + (size_t)I * KD);
                 if ((double)e > thresh && e > 0.f) {
@@ -371,7 +412,9 @@ __global__ __launch_bounds__(NT, 1) void k_ap_match(int tiles_r, int cap, const 
                 }
             }
         }
-        if (!ambiguous) {
+        if (ambiguous) {
+            amb[atomicAdd(namb_p, 1)] = t;
+        } else {
             oidx[t] = best;
             oscore[t] = best >= 0 ? bs : 0.f;
         }
@@ -379,7 +422,7 @@ __global__ __launch_bounds__(NT, 1) void k_ap_match(int tiles_r, int cap, const 
     __syncthreads();
     // ---- slow path: one wave re-scores every column of an ambiguous row exactly ----
     const int namb = *namb_p;
-    for (int k = w; k < namb; k += NT / 64) {
+    for (int k = w; k < namb; k += NW) {
         const int r = amb[k];
         const float *a = A + (size_t)(row0 + r) * KD;
         int best = 0x7fffffff;
@@ -412,10 +455,10 @@ __global__ __launch_bounds__(NT, 1) void k_ap_match(int tiles_r, int cap, const 
 
 namespace mv {
 
-// scratch: split0 | split1 (batch * cap * 1 KiB each) | nrm0 | nrm1 (batch * cap f32 each)
+// scratch: h0 | h1 (batch * cap * 512 B each) | nrm0 | nrm1 (batch * cap f32 each) | bad (batch i32)
 size_t allpairs_f32_scratch_bytes(int batch, int cap) {
     const size_t rows = (size_t)batch * cap;
-    return 2 * rows * ROW_BYTES + 2 * align_up(rows * 4, 256);
+    return 2 * rows * ROW_BYTES + 2 * align_up(rows * 4, 256) + align_up((size_t)batch * 4, 256);
 }
 
 int launch_allpairs_f32(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
@@ -426,21 +469,23 @@ int launch_allpairs_f32(hipStream_t s, void *scratch, int batch, int cap, const 
     const int tiles_r = (cap + BM - 1) / BM;
     const long blocks = (long)batch * tiles_r;
     MV_REQUIRE(blocks < (1l << 31));
-    MV_REQUIRE(cap <= (1 << 21));  // per-lane DMA source offsets are 32-bit byte offsets into a pair
+    MV_REQUIRE(cap <= (1 << 22));  // per-lane DMA source offsets are 32-bit byte offsets into a pair
     const size_t rows = (size_t)batch * cap;
-    char *split0 = (char *)scratch, *split1 = split0 + rows * ROW_BYTES;
-    float *nrm0 = (float *)(split1 + rows * ROW_BYTES);
+    char *h0 = (char *)scratch, *h1 = h0 + rows * ROW_BYTES;
+    float *nrm0 = (float *)(h1 + rows * ROW_BYTES);
     float *nrm1 = (float *)((char *)nrm0 + align_up(rows * 4, 256));
+    int *bad = (int *)((char *)nrm1 + align_up(rows * 4, 256));
     const long split_blocks = (long)((2 * rows + 3) / 4);
     MV_REQUIRE(split_blocks < (1l << 31));
+    MV_HIP_TRY(hipMemsetAsync(bad, 0, (size_t)batch * 4, s));
     MV_PROF_BEGIN(s, "k_ap_split");
     hipLaunchKernelGGL(k_ap_split, dim3((unsigned)split_blocks), dim3(256), 0, s, batch, cap, n0, n1, desc0, desc1,
-                       split0, split1, nrm0, nrm1);
+                       h0, h1, nrm0, nrm1, bad);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     MV_PROF_BEGIN(s, "k_ap_match");
-    hipLaunchKernelGGL(k_ap_match, dim3((unsigned)blocks), dim3(NT), 0, s, tiles_r, cap, n0, n1, desc0, desc1,
-                       split0, split1, nrm0, nrm1, thresh, match_idx, match_score);
+    hipLaunchKernelGGL(k_ap_match, dim3((unsigned)blocks), dim3(NT), 0, s, tiles_r, cap, n0, n1, desc0, desc1, h0,
+                       h1, nrm0, nrm1, bad, thresh, match_idx, match_score);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     return MV_OK;

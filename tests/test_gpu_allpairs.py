@@ -1,6 +1,6 @@
 """GPU parity: all-pairs descriptor match (python/pairwise_pnp.py:635-659 semantics on the
-gemmini_functions_cpu.h summation order) -- fp32 MFMA screen + exact re-score must give the
-oracle's indices AND scores bit-for-bit; int8 MFMA path integer-exact."""
+gemmini_functions_cpu.h summation order) -- fp16 MFMA screen + exact fp32 re-score must give
+the oracle's indices AND scores bit-for-bit; int8 MFMA path integer-exact."""
 import numpy as np
 import pytest
 
@@ -107,6 +107,31 @@ def test_allpairs_f32_threshold_edges(ctx, orc, torch_cuda):
         idx, sc = run_f32(ctx, torch_cuda, [(a, b)], thresh=thr)
         i2, s2 = orc.allpairs_f32(a, b, thr)
         assert (idx[0, :64] == i2).all() and (bits(sc[0, :64]) == bits(s2)).all()
+
+
+def test_allpairs_f32_out_of_screen_range(ctx, orc, torch_cuda):
+    """The fp16 screen only takes |x| < 2: unnormalised, huge, tiny, NaN and mixed-scale
+    descriptors must still give the reference's answer (flagged pairs / wide windows route
+    rows through the exact re-score)."""
+    rng = np.random.default_rng(11)
+    pairs = []
+    for scale0, scale1 in ((5.0, 1.0), (1.0, 3e4), (1e-6, 1.0), (1e-20, 1e-20), (1.0, 1.0)):
+        a = rng.standard_normal((96, 256)).astype(np.float32)
+        a /= np.linalg.norm(a, axis=1, keepdims=True)
+        b = a[rng.permutation(96)][:80] + 0.05 * rng.standard_normal((80, 256)).astype(np.float32)
+        b /= np.linalg.norm(b, axis=1, keepdims=True)
+        pairs.append(((a * np.float32(scale0)).astype(np.float32), (b * np.float32(scale1)).astype(np.float32)))
+    a, b = pairs[-1]
+    b = b.copy()
+    b[7, 3] = np.nan  # a NaN column: never the maximiser in the reference's comparisons
+    b[9, :] *= np.float32(2.5)  # one column outside the fp16 range flags the whole pair
+    pairs[-1] = (a, b)
+    for thr in (0.8, 0.0):
+        idx, sc = run_f32(ctx, torch_cuda, pairs, thresh=thr)
+        for k, (a, b) in enumerate(pairs):
+            i2, s2 = orc.allpairs_f32(a, b, thr)
+            assert (idx[k, :a.shape[0]] == i2).all(), k
+            assert (bits(sc[k, :a.shape[0]]) == bits(s2)).all(), k
 
 
 def run_i8(ctx, torch, pairs, cap=None):
