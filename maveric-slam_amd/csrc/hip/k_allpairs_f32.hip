@@ -7,8 +7,9 @@
 //               values leave |a_k| < 2 (or are not finite) is flagged: all of its rows take the
 //               exact slow path, so the fp16 range never has to be trusted.  HBM-bound: 4 B read
 //               + 2 B written per element.
-//   k_ap_match  a 512-thread block (8 waves, 2 per SIMD, 32 rows each) owns 256 query rows of
-//               one pair and sweeps ALL column tiles of the other frame:
+//   k_ap_match  a 256-thread block (4 waves, one per SIMD, 32 rows each; two blocks per CU run
+//               out of phase, so one block's A load / fold overlaps the other's MFMAs) owns
+//               128 query rows of one pair and sweeps ALL column tiles of the other frame:
 //     * the wave's 32 rows x 256 k of A (fp16, 64 VGPRs) are loaded ONCE into registers;
 //       only B streams (512 B per column per block);
 //     * screen S ~= D0 . D1^T on v_mfma_f32_32x32x16_f16 (exact fp16 products, fp32
@@ -44,11 +45,8 @@
 
 namespace {
 
-constexpr int BM = 256, BN = 128, BK = 64, KD = 256, KS = KD / BK, NT = 512, NW = NT / 64, RW = BM / NW;
-#ifndef AP_NBUF
-#define AP_NBUF 4
-#endif
-constexpr int NBUF = AP_NBUF;
+constexpr int BM = 128, BN = 64, BK = 128, KD = 256, KS = KD / BK, NT = 256, NW = NT / 64, RW = BM / NW;
+constexpr int NBUF = 4;  // ring slots: two column tiles of KS = 2 slices
 // timing experiments only (wrong results): drop the DMA waits / barriers / MFMAs / DMAs
 #ifndef AP_EXP_NOWAIT
 #define AP_EXP_NOWAIT 0
@@ -59,20 +57,30 @@ constexpr int NBUF = AP_NBUF;
 #ifndef AP_EXP_NOMFMA
 #define AP_EXP_NOMFMA 0
 #endif
+#ifndef AP_EXP_NOEXACT
+#define AP_EXP_NOEXACT 0
+#endif
+#ifndef AP_EXP_NOALOAD
+#define AP_EXP_NOALOAD 0
+#endif
+#ifndef AP_EXP_NOFOLD
+#define AP_EXP_NOFOLD 0
+#endif
 #ifndef AP_EXP_NODMA
 #define AP_EXP_NODMA 0
 #endif
 constexpr int ROW_BYTES = KD * 2;                // fp16 row: 512 B
-constexpr int SL_ROW = BK * 2;                   // one row of one slice: 64 fp16 = 128 B
+constexpr int SL_ROW = BK * 2;                   // one row of one slice: 128 fp16 = 256 B = 16 chunks
 constexpr int SL_BYTES = BN * SL_ROW;            // one B slice: 16 KiB
-constexpr int DMA_PER_SLICE = BN / 8 / NW;       // 1-KiB DMA instructions per wave per slice
+constexpr int DMA_PER_SLICE = SL_BYTES / 1024 / NW;  // 1-KiB DMA instructions per wave per slice
 constexpr float SCALE = 16384.f;                 // 2^14: |a_k| < 2 -> |2^14 a_k| < 2^15 < 65504
-static_assert(KS % NBUF == 0 || NBUF % KS == 0, "ring slots must be compile-time per slice");
-static_assert(RW == 32 && DMA_PER_SLICE == 2, "one wave per 32 rows (32x32 MFMA), 2 DMA per slice");
+static_assert(KS == 2 && NBUF == 2 * KS, "the loop body covers two column tiles = NBUF slices");
+static_assert(RW == 32 && DMA_PER_SLICE == 4, "one wave per 32 rows (32x32 MFMA), 4 DMA per slice");
 // LDS map (ONE array -- a second __shared__ object can de-pipeline the DMA), byte offsets
-constexpr int OFF_STAGE = 0;                     // [NBUF][128 B rows][128 B]
+constexpr int OFF_STAGE = 0;                     // [NBUF][64 B rows][256 B]
 constexpr int OFF_TRIP = NBUF * SL_BYTES;        // [256] {m1, i1, m2}
-constexpr int OFF_AMB = OFF_TRIP + BM * 12;      // [256] i32 ambiguous rows
+constexpr int OFF_ANRM = OFF_TRIP + BM * 12;     // [256] f32 |a|^2 (< 0: row outside the fp16 range)
+constexpr int OFF_AMB = OFF_ANRM + BM * 4;       // [256] i32 ambiguous rows
 constexpr int OFF_MISC = OFF_AMB + BM * 4;       // [NW] f32 per-wave max|b|^2, [1] i32 #ambiguous
 constexpr int LDS_BYTES = OFF_MISC + 4 * NW + 16;
 
@@ -126,6 +134,15 @@ __device__ __forceinline__ Top2 join2(const Top2 &x, const Top2 &y) {  // x's co
     const bool up = y.m1 > x.m1;
     return {vmax(x.m1, y.m1), vmax(vmin(x.m1, y.m1), vmax(x.m2, y.m2)), up ? y.i : x.i};
 }
+// Fold one row's 2 values of a tile (columns j, j + 32; -inf past n1) into the running triple;
+// an earlier tile's column is kept on a tie (strict >).
+__device__ __forceinline__ void fold2(float v0, float v1, int j, float &m1, int &i1, float &m2) {
+    const Top2 t = leaf2(v0, j, v1, j + 32);
+    m2 = vmax(vmin(m1, t.m1), vmax(m2, t.m2));
+    i1 = t.m1 > m1 ? t.i : i1;
+    m1 = vmax(m1, t.m1);
+}
+
 // Fold one row's 4 values of a tile (columns j + 32 c, c = 0..3; -inf past n1) into the running
 // triple; an earlier tile's column is kept on a tie (strict >).
 __device__ __forceinline__ void fold4(float v0, float v1, float v2, float v3, int j, float &m1, int &i1,
@@ -169,41 +186,36 @@ __device__ __forceinline__ float exact_dot(const float *__restrict__ a, const fl
     return s;
 }
 
-// ---- k_ap_split: one wave per descriptor row (rows >= n are never read downstream) ----
-__global__ __launch_bounds__(256) void k_ap_split(int batch, int cap, const int *__restrict__ n0v,
-                                                  const int *__restrict__ n1v, const float *__restrict__ desc0,
-                                                  const float *__restrict__ desc1, char *__restrict__ h0,
-                                                  char *__restrict__ h1, float *__restrict__ nrm0,
+// ---- k_ap_split: frame 1 only, one wave per descriptor row (rows >= n1 are never read) ----
+__global__ __launch_bounds__(256) void k_ap_split(int batch, int cap, const int *__restrict__ n1v,
+                                                  const float *__restrict__ desc1, char *__restrict__ h1,
                                                   float *__restrict__ nrm1, int *__restrict__ bad) {
     const long R = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const long per_frame = (long)batch * cap;
-    if (R >= 2 * per_frame) return;
-    const int frame = R >= per_frame;
-    const long fr = frame ? R - per_frame : R;
-    const int pair = (int)(fr / cap), r = (int)(fr % cap);
-    if (r >= (frame ? n1v : n0v)[pair]) return;
+    if (R >= (long)batch * cap) return;
+    const int pair = (int)(R / cap), r = (int)(R % cap);
+    if (r >= n1v[pair]) return;
     const int lane = threadIdx.x & 63;
-    const float4 v = *reinterpret_cast<const float4 *>((frame ? desc1 : desc0) + fr * KD + lane * 4);
+    const float4 v = *reinterpret_cast<const float4 *>(desc1 + R * KD + lane * 4);
     const bool ok = fabsf(v.x) < 2.f && fabsf(v.y) < 2.f && fabsf(v.z) < 2.f && fabsf(v.w) < 2.f;  // NaN: false
     if (__builtin_amdgcn_ballot_w64(!ok) != 0 && lane == 0) bad[pair] = 1;
     const f16x4 h = {(_Float16)(v.x * SCALE), (_Float16)(v.y * SCALE), (_Float16)(v.z * SCALE),
                      (_Float16)(v.w * SCALE)};  // exact power-of-two scale, then RNE to fp16
-    *reinterpret_cast<f16x4 *>((frame ? h1 : h0) + fr * ROW_BYTES + lane * 8) = h;
+    *reinterpret_cast<f16x4 *>(h1 + R * ROW_BYTES + lane * 8) = h;
     float q = fmaf(v.x, v.x, fmaf(v.y, v.y, fmaf(v.z, v.z, v.w * v.w)));
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) q += __shfl_xor(q, o, 64);
-    if (lane == 0) (frame ? nrm1 : nrm0)[fr] = q;
+    if (lane == 0) nrm1[R] = q;
 }
 
-__global__ __launch_bounds__(NT, 1) void k_ap_match(int tiles_r, int cap, const int *__restrict__ n0v,
+__global__ __launch_bounds__(NT, 2) void k_ap_match(int tiles_r, int cap, const int *__restrict__ n0v,
                                                     const int *__restrict__ n1v, const float *__restrict__ desc0,
-                                                    const float *__restrict__ desc1, const char *__restrict__ h0,
-                                                    const char *__restrict__ h1, const float *__restrict__ nrm0,
+                                                    const float *__restrict__ desc1, const char *__restrict__ h1,
                                                     const float *__restrict__ nrm1, const int *__restrict__ bad,
                                                     double thresh, int *__restrict__ match_idx,
                                                     float *__restrict__ match_score) {
     __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
     float *trip = reinterpret_cast<float *>(lds + OFF_TRIP);
+    float *anrm = reinterpret_cast<float *>(lds + OFF_ANRM);
     int *amb = reinterpret_cast<int *>(lds + OFF_AMB);
     float *misc = reinterpret_cast<float *>(lds + OFF_MISC);
     int *namb_p = reinterpret_cast<int *>(lds + OFF_MISC) + NW;
@@ -222,42 +234,80 @@ __global__ __launch_bounds__(NT, 1) void k_ap_match(int tiles_r, int cap, const 
     }
     if (row0 >= n0 || n1 <= 0) return;
     const bool flagged = bad[pair] != 0;
-    const char *SA = h0 + (size_t)pair * cap * ROW_BYTES;
     const char *SB = h1 + (size_t)pair * cap * ROW_BYTES;
+    const float *A = desc0 + (size_t)pair * cap * KD;
+    const float *B = desc1 + (size_t)pair * cap * KD;
     const int ntc = flagged ? 0 : (n1 + BN - 1) / BN;  // a flagged pair skips the screen
 
-    // ---- B DMA map: wave w fills rows w*16 .. w*16+15 of each slice, 8 rows (1 KiB) per
-    //      instruction; lane l lands at row (l >> 3), chunk position l & 7 and fetches
-    //      source chunk (l & 7) ^ ((row >> 1) & 7) of that row ----
-    const int wu = __builtin_amdgcn_readfirstlane(w);
-    const int dr = wu * 16 + (lane >> 3);
-    // ((dr + 8) >> 1) & 7 = ((dr >> 1) & 7) ^ 4
-    const unsigned dcb = (unsigned)((lane & 7) ^ ((dr >> 1) & 7)) * 16, dcb4 = dcb ^ 64u;
-    unsigned oB0 = (unsigned)min(dr, n1 - 1) * ROW_BYTES + dcb;
-    unsigned oB1 = (unsigned)min(dr + 8, n1 - 1) * ROW_BYTES + dcb4;
-    const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char *)(lds + OFF_STAGE);
-    const unsigned dst_w = lds_base + (unsigned)(wu * 16 * SL_ROW);
-#define AP_STAGE(BUF, KSI)                                                                   \
-    do {                                                                                     \
-        glds16<(KSI) * SL_ROW, (BUF) * SL_BYTES>(SB, oB0, dst_w);                            \
-        glds16<(KSI) * SL_ROW, (BUF) * SL_BYTES + 8 * SL_ROW>(SB, oB1, dst_w);               \
-    } while (0)
-
-    // ---- fragment map (v_mfma_f32_32x32x16_f16): lane l holds row/column l & 31 and
-    //      k = 16 s + 8 (l >> 5) .. +7 at k16 step s, i.e. chunk 2 (s % 4) + (l >> 5) of slice
-    //      s / 4.  A (this wave's 32 rows x 256 k: 64 VGPRs) stays in registers.
+    // ---- A: this wave's 32 rows x 256 k, fp32 -> 2^14-scaled fp16 straight into registers
+    //      (v_mfma_f32_32x32x16_f16 A operand: lane l holds row l & 31, k = 16 s + 8 (l >> 5)
+    //      .. +7 at k16 step s).  |a|^2 and the fp16 range check come along. ----
     const int fr = lane & 31, fh = lane >> 5;
     f16x8 aF[KD / 16];
     {
-        const char *arow = SA + (size_t)min(row0 + w * RW + fr, n0 - 1) * ROW_BYTES + fh * 16;
+        const float *arow = A + (size_t)min(row0 + w * RW + fr, n0 - 1) * KD + fh * 8;
+        float4 xs[KD / 8];  // all 32 loads in flight at once, then convert
 #pragma unroll
-        for (int s = 0; s < KD / 16; s++) aF[s] = *reinterpret_cast<const f16x8 *>(arow + s * 32);
+        for (int s = 0; s < KD / 16; s++) {
+            if (AP_EXP_NOALOAD) {
+                xs[2 * s] = make_float4(0.01f * s, 0.f, 0.f, 0.f);
+                xs[2 * s + 1] = xs[2 * s];
+            } else {
+                xs[2 * s] = *reinterpret_cast<const float4 *>(arow + s * 16);
+                xs[2 * s + 1] = *reinterpret_cast<const float4 *>(arow + s * 16 + 4);
+            }
+        }
+        float q = 0.f;
+        int out = 0;  // any |a_k| >= 2 or NaN (comparisons with NaN are false)
+#pragma unroll
+        for (int s = 0; s < KD / 16; s++) {
+            const float4 x = xs[2 * s], y = xs[2 * s + 1];
+            out |= (int)!(fabsf(x.x) < 2.f) | (int)!(fabsf(x.y) < 2.f) | (int)!(fabsf(x.z) < 2.f) | (int)!(fabsf(x.w) < 2.f) |
+                   (int)!(fabsf(y.x) < 2.f) | (int)!(fabsf(y.y) < 2.f) | (int)!(fabsf(y.z) < 2.f) | (int)!(fabsf(y.w) < 2.f);
+            q = fmaf(x.x, x.x, fmaf(x.y, x.y, fmaf(x.z, x.z, fmaf(x.w, x.w, q))));
+            q = fmaf(y.x, y.x, fmaf(y.y, y.y, fmaf(y.z, y.z, fmaf(y.w, y.w, q))));
+            aF[s] = f16x8{(_Float16)(x.x * SCALE), (_Float16)(x.y * SCALE), (_Float16)(x.z * SCALE),
+                          (_Float16)(x.w * SCALE), (_Float16)(y.x * SCALE), (_Float16)(y.y * SCALE),
+                          (_Float16)(y.z * SCALE), (_Float16)(y.w * SCALE)};
+        }
+        q += __shfl_xor(q, 32, 64);
+        out |= __shfl_xor(out, 32, 64);
+        if (fh == 0) anrm[w * RW + fr] = out ? -1.f : q;
     }
-    const int swb = (fr >> 1) & 7;  // rows 32 c + fr share it
-    const int offb = fr * SL_ROW;
+
+    // ---- B DMA map: wave w fills rows w*16 .. w*16+15 of each slice, 4 rows (1 KiB) per
+    //      instruction; lane l lands at row (l >> 4), chunk position l & 15 and fetches
+    //      source chunk (l & 15) ^ (row & 15) of that row (256-B rows: 16 chunks) ----
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    const int dr = wu * 16 + (lane >> 4);  // (dr & 15) < 4, so (dr + 4 g) & 15 = (dr & 15) ^ 4 g
+    const unsigned dcb = (unsigned)((lane & 15) ^ (dr & 15)) * 16;
+    unsigned oB0, oB1, oB2, oB3;
+    const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char *)(lds + OFF_STAGE);
+    const unsigned dst_w = lds_base + (unsigned)(wu * 16 * SL_ROW);
+#define AP_STAGE(SLOT, KSI)                                                                  \
+    do {                                                                                     \
+        glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES>(SB, oB0, dst_w);                           \
+        glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES + 4 * SL_ROW>(SB, oB1, dst_w);              \
+        glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES + 8 * SL_ROW>(SB, oB2, dst_w);              \
+        glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES + 12 * SL_ROW>(SB, oB3, dst_w);             \
+    } while (0)
+#define AP_TILE_OFFSETS(TC)                                                                  \
+    do {                                                                                     \
+        const int nb_ = (TC) * BN + dr;                                                      \
+        oB0 = (unsigned)min(nb_, n1 - 1) * ROW_BYTES + dcb;                                  \
+        oB1 = (unsigned)min(nb_ + 4, n1 - 1) * ROW_BYTES + (dcb ^ 64u);                      \
+        oB2 = (unsigned)min(nb_ + 8, n1 - 1) * ROW_BYTES + (dcb ^ 128u);                     \
+        oB3 = (unsigned)min(nb_ + 12, n1 - 1) * ROW_BYTES + (dcb ^ 192u);                    \
+    } while (0)
+    AP_TILE_OFFSETS(0);
+
+    // ---- B fragment map: column block c (0, 1) of a tile, lane l reads row 32 c + (l & 31)
+    //      at chunk (2 s + (l >> 5)) ^ (row & 15) for k16 step s of the slice ----
+    const int rdb = fr * SL_ROW;
+    const int xsw = fh ^ (fr & 15);  // chunk(2 s + fh) ^ (fr & 15) = 2 s ^ xsw
 
     const f32x16 zero16 = {};
-    f32x16 acc0 = zero16, acc1 = zero16, acc2 = zero16, acc3 = zero16;
+    f32x16 acc0 = zero16, acc1 = zero16;
     float m1[16], m2[16];
     int i1[16];
 #pragma unroll
@@ -267,61 +317,50 @@ __global__ __launch_bounds__(NT, 1) void k_ap_match(int tiles_r, int cap, const 
         i1[q] = 0x7fffffff;
     }
 
-    // Ring schedule: global slice g = tc*KS + ks lives in slot g % NBUF = ks % NBUF.  At slice
-    // g the block issues slice g + NBUF - 1 into the slot read at g - 1 (freed by that
-    // slice's barrier), computes slice g, then waits until slice g + 1 has landed: the DMA
-    // groups issued after it (DMA_PER_SLICE instructions each) may stay in flight.
-#define AP_MF(ACC, CG, S, FIRST)                                                              \
+    // Ring schedule: the loop body covers tiles T and T+1 = slices g = 2T .. 2T+3 in slots
+    // J = 0..3.  At slot J the block issues slice g + 3 (tile T + (J+3)/2, k-slice (J+3)%2)
+    // into slot (J+3)%4 -- the slot read at g - 1, freed by that slice's barrier -- computes
+    // slot J, then waits until slice g + 1 has landed (the two later groups may stay in flight).
+#define AP_SLOT(J)                                                                            \
     do {                                                                                      \
-        const f16x8 b_ = *reinterpret_cast<const f16x8 *>(                                    \
-            base + offb + (CG) * 32 * SL_ROW + (((2 * (S) + fh) ^ swb) * 16));                \
-        ACC = __builtin_amdgcn_mfma_f32_32x32x16_f16(aF[kk_ + (S)], b_, (FIRST) ? zero16 : ACC, 0, 0, 0); \
-    } while (0)
-#define AP_SLICE(ks)                                                                          \
-    do {                                                                                      \
-        constexpr int nx = (ks) + NBUF - 1; /* slice issued now, counted from this tile */    \
-        if (AP_EXP_NODMA) {                                                                   \
-        } else if constexpr (nx < KS) {                                                       \
-            AP_STAGE(nx % NBUF, nx);                                                          \
-        } else if (tc + nx / KS < ntc) {                                                      \
-            if constexpr (nx % KS == 0) { /* first slice of a later column tile */            \
-                const int nb_ = (tc + nx / KS) * BN + dr;                                     \
-                oB0 = (unsigned)min(nb_, n1 - 1) * ROW_BYTES + dcb;                           \
-                oB1 = (unsigned)min(nb_ + 8, n1 - 1) * ROW_BYTES + dcb4;                      \
-            }                                                                                 \
+        constexpr int nx = (J) + NBUF - 1;                                                    \
+        const int ntile = T + nx / KS; /* tile of the slice issued now */                     \
+        if (!AP_EXP_NODMA && ntile < ntc) {                                                   \
+            if constexpr (nx % KS == 0) AP_TILE_OFFSETS(ntile);                               \
             AP_STAGE(nx % NBUF, nx % KS);                                                     \
         }                                                                                     \
-        const char *base = lds + OFF_STAGE + ((ks) % NBUF) * SL_BYTES;                        \
-        constexpr int kk_ = (ks) * 4; /* first k16 step of this slice */                      \
-        if (!AP_EXP_NOMFMA) {                                                                 \
-            _Pragma("unroll") for (int s_ = 0; s_ < 4; s_++) {                                \
-                AP_MF(acc0, 0, s_, (ks) == 0 && s_ == 0);                                     \
-                AP_MF(acc1, 1, s_, (ks) == 0 && s_ == 0);                                     \
-                AP_MF(acc2, 2, s_, (ks) == 0 && s_ == 0);                                     \
-                AP_MF(acc3, 3, s_, (ks) == 0 && s_ == 0);                                     \
+        const int tc = T + (J) / KS;                                                          \
+        const char *base = lds + OFF_STAGE + (J) * SL_BYTES + rdb;                            \
+        if (!AP_EXP_NOMFMA) { /* all 16 fragment reads first, then the MFMAs (counted waits) */ \
+            f16x8 b0_[BK / 16], b1_[BK / 16];                                                 \
+            _Pragma("unroll") for (int s_ = 0; s_ < BK / 16; s_++) {                          \
+                const int ch_ = ((2 * s_) ^ xsw) * 16;                                        \
+                b0_[s_] = *reinterpret_cast<const f16x8 *>(base + ch_);                       \
+                b1_[s_] = *reinterpret_cast<const f16x8 *>(base + 32 * SL_ROW + ch_);         \
+            }                                                                                 \
+            __builtin_amdgcn_sched_barrier(0);                                                \
+            _Pragma("unroll") for (int s_ = 0; s_ < BK / 16; s_++) {                          \
+                const f16x8 a_ = aF[((J) % KS) * (BK / 16) + s_];                             \
+                const bool z_ = (J) % KS == 0 && s_ == 0; /* a tile's first MFMA: C = 0 */    \
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_, b0_[s_], z_ ? zero16 : acc0, 0, 0, 0); \
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_, b1_[s_], z_ ? zero16 : acc1, 0, 0, 0); \
             }                                                                                 \
         }                                                                                     \
-        if constexpr ((ks) == KS - 1) { /* column tile done: fold into the lane triples */    \
+        if constexpr ((J) % KS == KS - 1) { /* column tile done: fold into the lane triples */ \
             const int col = tc * BN + fr;                                                     \
             if (tc + 1 == ntc) { /* only the last tile can reach past n1: + 0 keeps, + -inf drops */ \
                 const float lo0 = col < n1 ? 0.f : -__builtin_inff();                         \
                 const float lo1 = col + 32 < n1 ? 0.f : -__builtin_inff();                    \
-                const float lo2 = col + 64 < n1 ? 0.f : -__builtin_inff();                    \
-                const float lo3 = col + 96 < n1 ? 0.f : -__builtin_inff();                    \
                 _Pragma("unroll") for (int q = 0; q < 16; q++) {                              \
                     acc0[q] += lo0;                                                           \
                     acc1[q] += lo1;                                                           \
-                    acc2[q] += lo2;                                                           \
-                    acc3[q] += lo3;                                                           \
                 }                                                                             \
             }                                                                                 \
-            _Pragma("unroll") for (int q = 0; q < 16; q++)                                    \
-                fold4(acc0[q], acc1[q], acc2[q], acc3[q], col, m1[q], i1[q], m2[q]);          \
+            if (!AP_EXP_NOFOLD)                                                               \
+                _Pragma("unroll") for (int q = 0; q < 16; q++) fold2(acc0[q], acc1[q], col, m1[q], i1[q], m2[q]); \
         }                                                                                     \
-        /* slice g + 1 must have landed: in flight after it are the groups of slices */       \
-        /* g + 2 .. g + NBUF - 1 that exist (the block's last slice is ntc*KS - 1) */        \
         if (AP_EXP_NOWAIT) {                                                                  \
-        } else if (tc + (nx + 0) / KS < ntc) { /* every slice up to g + NBUF - 1 was issued */ \
+        } else if (ntile < ntc) {                                                             \
             wait_vm<DMA_PER_SLICE * (NBUF - 2)>();                                            \
         } else {                                                                              \
             wait_vm<0>(); /* tail of the sweep: drain */                                      \
@@ -329,25 +368,28 @@ __global__ __launch_bounds__(NT, 1) void k_ap_match(int tiles_r, int cap, const 
         if (!AP_EXP_NOBAR) __syncthreads();                                                   \
     } while (0)
 
-    // prologue: slices 0 .. NBUF-2 (of tile 0, and tile 1 when KS < NBUF - 1)
-    static_assert(NBUF == 4, "prologue issues NBUF - 1 = 3 slices");
-    static_assert(KS == 4, "prologue slices 0..2 all belong to tile 0");
+    // prologue: slices 0, 1, 2 (tile 0 both k-slices, tile 1 k-slice 0) behind the A loads
     if (ntc > 0) {
         AP_STAGE(0, 0);
         AP_STAGE(1, 1);
-        AP_STAGE(2, 2);
+        if (ntc > 1) {
+            AP_TILE_OFFSETS(1);
+            AP_STAGE(2, 0);
+        }
     }
     wait_vm<0>();
     __syncthreads();
-    for (int tc = 0; tc < ntc; tc++) {
-        AP_SLICE(0);
-        AP_SLICE(1);
-        AP_SLICE(2);
-        AP_SLICE(3);
+    for (int T = 0; T < ntc; T += 2) {
+        AP_SLOT(0);
+        AP_SLOT(1);
+        if (T + 1 < ntc) {
+            AP_SLOT(2);
+            AP_SLOT(3);
+        }
     }
 #undef AP_STAGE
-#undef AP_SLICE
-#undef AP_MF
+#undef AP_SLOT
+#undef AP_TILE_OFFSETS
 
     // ---- merge the triples across the 32 lanes (columns) that share a row ----
 #pragma unroll
@@ -382,8 +424,6 @@ __global__ __launch_bounds__(NT, 1) void k_ap_match(int tiles_r, int cap, const 
     for (int k = 1; k < NW; k++) bmax2 = fmaxf(bmax2, misc[k]);
 
     // ---- exact re-score, fast path: the screen maximiser is the only possible maximiser ----
-    const float *A = desc0 + (size_t)pair * cap * KD;
-    const float *B = desc1 + (size_t)pair * cap * KD;
     const double u24 = 5.9604644775390625e-08, u23 = 2 * u24;
     const double gam_e = KD * u24 / (1.0 - KD * u24);
     const double gam_s = KD * u23 / (1.0 - KD * u23);
@@ -393,19 +433,20 @@ __global__ __launch_bounds__(NT, 1) void k_ap_match(int tiles_r, int cap, const 
         const float *tp = trip + t * 3;
         const float M = tp[0], M2 = tp[2];
         const int I = reinterpret_cast<const int *>(tp)[1];
-        const double an = sqrt((double)nrm0[(size_t)pair * cap + row0 + t]);
+        const float an2 = anrm[t];
+        const double an = sqrt(fmax((double)an2, 0.0));
         const double delta =
             (rel * an * Bn + 1.001 * 5.9604644775390625e-08 * (an + Bn) + 3.552713678800501e-15) * 1.01 + 1e-30;
         const double Ms = (double)M * 3.725290298461914e-09;  // screen / 2^28
         const double M2s = (double)M2 * 3.725290298461914e-09;
         int best = -1;
         float bs = 0.f;
-        bool ambiguous = flagged;
-        if (!flagged && Ms + delta > thresh) {
+        bool ambiguous = flagged || an2 < 0.f;  // outside the fp16 screen's range: exact path
+        if (!ambiguous && Ms + delta > thresh) {
             if (M2s >= Ms - 2.0 * delta) {
                 ambiguous = true;
             } else {
-                const float e = exact_dot(A + (size_t)(row0 + t) * KD, B + (size_t)I * KD);
+                const float e = AP_EXP_NOEXACT ? M : exact_dot(A + (size_t)(row0 + t) * KD, B + (size_t)I * KD);
                 if ((double)e > thresh && e > 0.f) {
                     bs = e;
                     best = I;
@@ -455,10 +496,10 @@ __global__ __launch_bounds__(NT, 1) void k_ap_match(int tiles_r, int cap, const 
 
 namespace mv {
 
-// scratch: h0 | h1 (batch * cap * 512 B each) | nrm0 | nrm1 (batch * cap f32 each) | bad (batch i32)
+// scratch: h1 (batch * cap * 512 B) | nrm1 (batch * cap f32) | bad (batch i32)
 size_t allpairs_f32_scratch_bytes(int batch, int cap) {
     const size_t rows = (size_t)batch * cap;
-    return 2 * rows * ROW_BYTES + 2 * align_up(rows * 4, 256) + align_up((size_t)batch * 4, 256);
+    return rows * ROW_BYTES + align_up(rows * 4, 256) + align_up((size_t)batch * 4, 256);
 }
 
 int launch_allpairs_f32(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
@@ -471,21 +512,20 @@ int launch_allpairs_f32(hipStream_t s, void *scratch, int batch, int cap, const 
     MV_REQUIRE(blocks < (1l << 31));
     MV_REQUIRE(cap <= (1 << 22));  // per-lane DMA source offsets are 32-bit byte offsets into a pair
     const size_t rows = (size_t)batch * cap;
-    char *h0 = (char *)scratch, *h1 = h0 + rows * ROW_BYTES;
-    float *nrm0 = (float *)(h1 + rows * ROW_BYTES);
-    float *nrm1 = (float *)((char *)nrm0 + align_up(rows * 4, 256));
+    char *h1 = (char *)scratch;
+    float *nrm1 = (float *)(h1 + rows * ROW_BYTES);
     int *bad = (int *)((char *)nrm1 + align_up(rows * 4, 256));
-    const long split_blocks = (long)((2 * rows + 3) / 4);
+    const long split_blocks = (long)((rows + 3) / 4);
     MV_REQUIRE(split_blocks < (1l << 31));
     MV_HIP_TRY(hipMemsetAsync(bad, 0, (size_t)batch * 4, s));
     MV_PROF_BEGIN(s, "k_ap_split");
-    hipLaunchKernelGGL(k_ap_split, dim3((unsigned)split_blocks), dim3(256), 0, s, batch, cap, n0, n1, desc0, desc1,
-                       h0, h1, nrm0, nrm1, bad);
+    hipLaunchKernelGGL(k_ap_split, dim3((unsigned)split_blocks), dim3(256), 0, s, batch, cap, n1, desc1, h1, nrm1,
+                       bad);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     MV_PROF_BEGIN(s, "k_ap_match");
-    hipLaunchKernelGGL(k_ap_match, dim3((unsigned)blocks), dim3(NT), 0, s, tiles_r, cap, n0, n1, desc0, desc1, h0,
-                       h1, nrm0, nrm1, bad, thresh, match_idx, match_score);
+    hipLaunchKernelGGL(k_ap_match, dim3((unsigned)blocks), dim3(NT), 0, s, tiles_r, cap, n0, n1, desc0, desc1, h1,
+                       nrm1, bad, thresh, match_idx, match_score);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     return MV_OK;
