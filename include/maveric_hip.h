@@ -131,7 +131,7 @@ typedef struct {
     int semantics;         /* MV_AS_BUILT: stub RANSAC (E = I) + McAdams pose; MV_AS_INTENDED: below */
     int hypotheses;        /* RANSAC 8-point hypotheses per pair (as-built: iterations, 10) */
     float inlier_thresh;   /* as-built: ||E p1 - p2||^2 threshold (1.1); as-intended: Sampson, pixels */
-    int refine_iters;      /* Gauss-Newton iterations on the inliers */
+    int refine_iters;      /* maximum Gauss-Newton iterations on the inliers (stops at convergence) */
     unsigned long long seed;
 } mv_pose_params;
 void mv_pose_params_default(mv_pose_params *p, int semantics);

@@ -8,9 +8,10 @@
 //      builds the 8x9 design matrix in the reference's column order
 //      (pnp_solver.c:42-50), and takes its null vector from a Householder QR
 //      of A^T (backward stable, no pivoting, static register indexing);
-//      hypotheses are MSAC-scored: sum of min(Sampson^2, (thr_px / f)^2) over all
-//      correspondences (LDS broadcast reads);
-//   3. block argmin (lowest cost, lowest hypothesis id) -> E;
+//      hypotheses are MSAC-scored (sum of min(Sampson^2, (thr_px / f)^2)) on an evenly
+//      strided subset of 128 correspondences (LDS broadcast reads);
+//   3. preemption: the 2 best of each wave survive and are MSAC-scored on ALL
+//      correspondences by the whole block; lowest (cost, hypothesis id) -> E;
 //   4. E = U diag(s1,s2,s3) V^T (double Jacobi on E^T E), the four (R, t)
 //      candidates R = U W V^T / U W^T V^T, t = +-u3, cheirality vote by
 //      triangulated depth over the inliers (block reduction);
@@ -21,7 +22,9 @@
 //      J^T J and J^T r assembled with wave64 shuffle reductions + LDS
 //      (the [J|r]^T[J|r] pattern of src/local_bundle_adjustment.c:161-176),
 //      5x5 LM-damped Cholesky solve in one lane, R <- exp(omega) R,
-//      t <- normalise(t + B d).
+//      t <- normalise(t + B d).  The Gauss-Newton state, the per-correspondence terms, the
+//      22 sums and the solve are float (the output is float).  Stops early once the step is below 1e-7 and the
+//      inlier band is unchanged (refine_iters is the maximum).
 // Output T = [R | t] with x1 ~ R x0 + t, |t| = 1 (the OpenCV recoverPose convention).
 #include <math.h>
 
@@ -30,6 +33,28 @@
 namespace {
 
 constexpr int NT = 256;
+// timing experiments only (wrong results): skip the GN per-point pass / reduction / solve
+#ifndef PE_NOPOINTS
+#define PE_NOPOINTS 0
+#endif
+#ifndef PE_NORED
+#define PE_NORED 0
+#endif
+#ifndef PE_TRACE
+#define PE_TRACE 0  // printf per-phase clock64() deltas of block 0 (timing experiments only)
+#endif
+#ifndef PE_NODECOMP
+#define PE_NODECOMP 0
+#endif
+#ifndef PE_NOSCORE
+#define PE_NOSCORE 0
+#endif
+#ifndef PE_NOHYP
+#define PE_NOHYP 0
+#endif
+#ifndef PE_NOSOLVE
+#define PE_NOSOLVE 0
+#endif
 constexpr int MAXP = 4096;  // correspondences per pair held in LDS (float4 each)
 
 __device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
@@ -213,14 +238,52 @@ __device__ void essential_uv(const double E[9], double U[3][3], double V[3][3]) 
     }
 }
 
+// float forms for the Gauss-Newton update (one lane per iteration: latency, not throughput)
+__device__ __forceinline__ void tangent_basis_f(const float *t, float *b) {
+    const float ax[3] = {fabsf(t[0]) < 0.57f ? 1.f : 0.f,
+                         fabsf(t[0]) < 0.57f ? 0.f : (fabsf(t[1]) < 0.57f ? 1.f : 0.f),
+                         fabsf(t[0]) < 0.57f || fabsf(t[1]) < 0.57f ? 0.f : 1.f};
+    float b1[3] = {t[1] * ax[2] - t[2] * ax[1], t[2] * ax[0] - t[0] * ax[2], t[0] * ax[1] - t[1] * ax[0]};
+    const float r = 1.f / sqrtf(b1[0] * b1[0] + b1[1] * b1[1] + b1[2] * b1[2]);
+    b1[0] *= r;
+    b1[1] *= r;
+    b1[2] *= r;
+    b[0] = b1[0];
+    b[1] = b1[1];
+    b[2] = b1[2];
+    b[3] = t[1] * b1[2] - t[2] * b1[1];
+    b[4] = t[2] * b1[0] - t[0] * b1[2];
+    b[5] = t[0] * b1[1] - t[1] * b1[0];
+}
+__device__ __forceinline__ void rodrigues_f(const float w[3], float R[3][3]) {
+    const float th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    float a, b;
+    if (th2 < 1e-2f) {  // |theta| < 0.1: Taylor to theta^6 (remainder < 3e-11)
+        a = 1.f - th2 / 6.f * (1.f - th2 / 20.f * (1.f - th2 / 42.f));
+        b = 0.5f * (1.f - th2 / 12.f * (1.f - th2 / 30.f * (1.f - th2 / 56.f)));
+    } else {
+        const float th = sqrtf(th2);
+        a = sinf(th) / th;
+        b = (1.f - cosf(th)) / th2;
+    }
+    const float K[3][3] = {{0, -w[2], w[1]}, {w[2], 0, -w[0]}, {-w[1], w[0], 0}};
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const float kk = K[i][0] * K[0][j] + K[i][1] * K[1][j] + K[i][2] * K[2][j];
+            R[i][j] = (i == j ? 1.f : 0.f) + a * K[i][j] + b * kk;
+        }
+}
+
 __device__ void rodrigues(const double w[3], double R[3][3]) {
     const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
-    const double th = sqrt(th2);
     double a, b;
-    if (th < 1e-8) {
-        a = 1.0 - th2 / 6.0;
-        b = 0.5 - th2 / 24.0;
+    if (th2 < 2.5e-3) {  // |theta| < 0.05: Taylor to theta^8 (remainder < 3e-21), no transcendentals
+        a = 1.0 - th2 / 6.0 * (1.0 - th2 / 20.0 * (1.0 - th2 / 42.0 * (1.0 - th2 / 72.0)));
+        b = 0.5 * (1.0 - th2 / 12.0 * (1.0 - th2 / 30.0 * (1.0 - th2 / 56.0 * (1.0 - th2 / 90.0))));
     } else {
+        const double th = sqrt(th2);
         a = sin(th) / th;
         b = (1.0 - cos(th)) / th2;
     }
@@ -264,6 +327,7 @@ __global__ __launch_bounds__(NT) void k_pose_ransac(PoseArgs a, const int *__res
     __shared__ double s_pose[12];  // R (9) + t (3)
     const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int n_in = min(nv[b], a.cap);
+    const long long tk0 = PE_TRACE ? clock64() : 0;
 
     // ---- 1. compaction (query order) + normalisation ----
     const int per = (n_in + NT - 1) / NT;
@@ -309,11 +373,18 @@ __global__ __launch_bounds__(NT) void k_pose_ransac(PoseArgs a, const int *__res
         return;
     }
 
-    // ---- 2. hypotheses, MSAC-scored (sum of min(Sampson^2, thr^2); plain inlier
-    //         counting cannot separate an outlier-contaminated 8-point solution that
-    //         still explains every inlier within the band -- near-pure forward motion) ----
+    const long long tk1 = PE_TRACE ? clock64() : 0;
+    // ---- 2. hypotheses, preemptively MSAC-scored (sum of min(Sampson^2, thr^2); plain
+    //         inlier counting cannot separate an outlier-contaminated 8-point solution that
+    //         still explains every inlier within the band -- near-pure forward motion).
+    //         Every hypothesis is scored on an evenly strided subset of PRE_M
+    //         correspondences; the SURV best of each wave survive (preemptive RANSAC,
+    //         Nister 2003) and are re-scored on all correspondences cooperatively. ----
+    constexpr int PRE_M = 128, SURV = 2, NS = 4 * SURV;
+    const int m = min(n, PRE_M);
+    const unsigned step16 = ((unsigned)n << 16) / (unsigned)m;  // subset point k: (k * step16) >> 16 < n
     float best_cost = __builtin_inff();
-    int best_cnt = -1, best_h = 0x7fffffff;
+    int best_h = 0x7fffffff;
     float best_e[9];
     for (int h = t; h < a.hypotheses; h += NT) {
         int idx[8];
@@ -334,32 +405,106 @@ __global__ __launch_bounds__(NT) void k_pose_ransac(PoseArgs a, const int *__res
         }
         if (drawn < 8) continue;
         float e[9];
-        if (!eight_point(P, idx, e)) continue;
+        if (PE_NOHYP) {
+            for (int r = 0; r < 9; r++) e[r] = P[idx[r & 7]].x + r;
+        } else if (!eight_point(P, idx, e)) {
+            continue;
+        }
         int c = 0;
         float cost = 0.f;
-        for (int i = 0; i < n; i++) cost += msac_cost(e, P[i], a.thr2, c);
+        int k = 0;
+        for (; k + 4 <= (PE_NOSCORE ? 0 : m); k += 4) {  // 4 LDS broadcast reads in flight per step
+            const float4 p0 = P[(k * step16) >> 16], p1 = P[((k + 1) * step16) >> 16];
+            const float4 p2 = P[((k + 2) * step16) >> 16], p3 = P[((k + 3) * step16) >> 16];
+            cost += msac_cost(e, p0, a.thr2, c);
+            cost += msac_cost(e, p1, a.thr2, c);
+            cost += msac_cost(e, p2, a.thr2, c);
+            cost += msac_cost(e, p3, a.thr2, c);
+        }
+        for (; k < (PE_NOSCORE ? 0 : m); k++) cost += msac_cost(e, P[(k * step16) >> 16], a.thr2, c);
         if (cost < best_cost || (cost == best_cost && h < best_h)) {
             best_cost = cost;
-            best_cnt = c;
             best_h = h;
 #pragma unroll
             for (int r = 0; r < 9; r++) best_e[r] = e[r];
         }
     }
-    // ---- 3. block argmin (cost asc, hypothesis id asc); cost >= 0 so its bits order as uint ----
-    unsigned long long key = best_cnt < 0 ? ~0ull
-                                          : ((unsigned long long)__float_as_uint(best_cost) << 32) | (unsigned)best_h;
+    const long long tk2 = PE_TRACE ? clock64() : 0;
+    // ---- 3. survivors: the SURV lowest (partial cost, hypothesis id) keys of each wave (cost
+    //         >= 0, so its bits order as uint), then full MSAC of the NS survivors ----
+    __shared__ int s_sh[NS];
+    __shared__ float s_sE[NS][9];
+    {
+        unsigned long long key = best_h == 0x7fffffff
+                                     ? ~0ull
+                                     : ((unsigned long long)__float_as_uint(best_cost) << 32) | (unsigned)best_h;
+        for (int r = 0; r < SURV; r++) {
+            unsigned long long k = key;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        unsigned long long k2 = __shfl_xor(key, o, 64);
-        key = k2 < key ? k2 : key;
+            for (int o = 32; o > 0; o >>= 1) {
+                const unsigned long long k2 = __shfl_xor(k, o, 64);
+                k = k2 < k ? k2 : k;
+            }
+            if (k == ~0ull) {
+                if (lane == 0) s_sh[w * SURV + r] = -1;
+            } else if (key == k) {  // the owner (keys are unique: hypothesis ids differ)
+                s_sh[w * SURV + r] = best_h;
+#pragma unroll
+                for (int q = 0; q < 9; q++) s_sE[w * SURV + r][q] = best_e[q];
+                key = ~0ull;
+            }
+        }
     }
-    __shared__ unsigned long long s_key[4];
-    if (lane == 0) s_key[w] = key;
     __syncthreads();
-    unsigned long long bk = s_key[0];
-    for (int k = 1; k < 4; k++) bk = s_key[k] < bk ? s_key[k] : bk;
-    if (bk == ~0ull) {
+    float cs[NS];
+    int cn[NS];
+#pragma unroll
+    for (int sv = 0; sv < NS; sv++) {
+        cs[sv] = 0.f;
+        cn[sv] = 0;
+        if (s_sh[sv] < 0) continue;
+        float e[9];
+#pragma unroll
+        for (int q = 0; q < 9; q++) e[q] = s_sE[sv][q];
+        for (int i = t; i < n; i += NT) cs[sv] += msac_cost(e, P[i], a.thr2, cn[sv]);
+    }
+    __shared__ float s_red2[4][2 * NS];
+    {
+        float v[2 * NS];
+#pragma unroll
+        for (int sv = 0; sv < NS; sv++) {
+            v[sv] = cs[sv];
+            v[NS + sv] = (float)cn[sv];
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+            for (int k = 0; k < 2 * NS; k++) v[k] += __shfl_xor(v[k], o, 64);
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < 2 * NS; k++) s_red2[w][k] = v[k];
+        }
+    }
+    __syncthreads();
+    if (t == 0) {
+        int bs = -1;
+        float bc = 0.f;
+        for (int sv = 0; sv < NS; sv++) {
+            if (s_sh[sv] < 0) continue;
+            const float c = s_red2[0][sv] + s_red2[1][sv] + s_red2[2][sv] + s_red2[3][sv];
+            if (bs < 0 || c < bc || (c == bc && s_sh[sv] < s_sh[bs])) {
+                bs = sv;
+                bc = c;
+            }
+        }
+        s_best[0] = bs < 0 ? -1
+                           : (int)(s_red2[0][NS + bs] + s_red2[1][NS + bs] + s_red2[2][NS + bs] + s_red2[3][NS + bs]);
+        if (bs >= 0)
+            for (int r = 0; r < 9; r++) s_E[r] = s_sE[bs][r];
+    }
+    __syncthreads();
+    if (s_best[0] < 0) {
         if (t < 12) To[t] = (t % 4 == t / 4) ? 1.f : 0.f;
         if (t == 0) {
             num_inliers[b] = 0;
@@ -368,22 +513,22 @@ __global__ __launch_bounds__(NT) void k_pose_ransac(PoseArgs a, const int *__res
         }
         return;
     }
-    const int win_h = (int)(bk & 0xffffffff);
-    if (best_cnt >= 0 && best_h == win_h) {
-        for (int r = 0; r < 9; r++) s_E[r] = best_e[r];
-        s_best[0] = best_cnt;
-    }
-    __syncthreads();
     float E[9];
     for (int r = 0; r < 9; r++) E[r] = s_E[r];
     const int ninl = s_best[0];
 
+    const long long tk3 = PE_TRACE ? clock64() : 0;
     // ---- 4. decomposition + cheirality ----
     __shared__ double s_cand[4][12];
     if (t == 0) {
         double Ed[9], U[3][3], V[3][3];
         for (int r = 0; r < 9; r++) Ed[r] = E[r];
-        essential_uv(Ed, U, V);
+        if (PE_NODECOMP) {
+            for (int i = 0; i < 3; i++)
+                for (int j = 0; j < 3; j++) U[i][j] = V[i][j] = i == j;
+        } else {
+            essential_uv(Ed, U, V);
+        }
         const double W[3][3] = {{0, -1, 0}, {1, 0, 0}, {0, 0, 1}};
         for (int c = 0; c < 4; c++) {
             double R[3][3];
@@ -421,6 +566,7 @@ __global__ __launch_bounds__(NT) void k_pose_ransac(PoseArgs a, const int *__res
             votes[c] += (z1 > 0 && z2 > 0) ? 1 : 0;
         }
     }
+    const long long tk4 = PE_TRACE ? clock64() : 0;
     __shared__ int s_votes[4];
     for (int c = 0; c < 4; c++) {
         int v = block_sum_i(votes[c], wsum);
@@ -435,50 +581,61 @@ __global__ __launch_bounds__(NT) void k_pose_ransac(PoseArgs a, const int *__res
     }
     __syncthreads();
 
+    const long long tk5 = PE_TRACE ? clock64() : 0;
     // ---- 5. Gauss-Newton, inliers re-selected every iteration with the current
     //         model: |r_i| < th_k, th_0 = thr, th_{k+1} = min(thr, max(3 rms_k, 0.01 px))
     //         (removes outliers that fell inside the RANSAC band; noisy data keeps thr) ----
-    __shared__ double s_red[4][22];
+    __shared__ float s_red[4][22];
     __shared__ double s_th;
-    if (t == 0) s_th = sqrt((double)a.thr2);
+    __shared__ int s_done;
+    __shared__ float s_basis[6];
+    __shared__ float s_pf[12];  // R (9) + t (3): the Gauss-Newton state
+    if (t == 0) {
+        s_th = sqrt((double)a.thr2);
+        s_done = 0;
+        for (int i = 0; i < 12; i++) s_pf[i] = (float)s_pose[i];
+        tangent_basis_f(s_pf + 9, s_basis);
+    }
     __syncthreads();
     const double th_max = sqrt((double)a.thr2);
     const double th_min = 0.01 * th_max;
     for (int it = 0; it < a.refine_iters; it++) {
-        double R[9], tv[3];
-        for (int i = 0; i < 9; i++) R[i] = s_pose[i];
-        for (int i = 0; i < 3; i++) tv[i] = s_pose[9 + i];
-        const double th = s_th;
-        // tangent basis of the unit sphere at t
-        D3 tt = {{tv[0], tv[1], tv[2]}};
-        D3 ax = fabs(tv[0]) < 0.57 ? D3{{1, 0, 0}} : (fabs(tv[1]) < 0.57 ? D3{{0, 1, 0}} : D3{{0, 0, 1}});
-        D3 b1 = cross(tt, ax);
-        const double nb1 = sqrt(dot3(b1, b1));
-        for (int i = 0; i < 3; i++) b1.v[i] /= nb1;
-        D3 b2 = cross(tt, b1);
-        double acc[22];  // J^T J (15, upper), J^T r (5), sum r^2, count
+        // the pose lives in double (LDS); the per-correspondence Jacobian and the 22 sums are
+        // float (the fixed point is set by the float residual, ~1e-7 of a unit vector)
+        float R[9], tv[3];
+        for (int i = 0; i < 9; i++) R[i] = s_pf[i];
+        for (int i = 0; i < 3; i++) tv[i] = s_pf[9 + i];
+        const float th = (float)s_th;
+        const float b1f[3] = {s_basis[0], s_basis[1], s_basis[2]};  // tangent basis at t
+        const float b2f[3] = {s_basis[3], s_basis[4], s_basis[5]};
+        float acc[22];  // J^T J (15, upper), J^T r (5), sum r^2, count
 #pragma unroll
-        for (int k = 0; k < 22; k++) acc[k] = 0;
-        for (int i = t; i < n; i += NT) {
+        for (int k = 0; k < 22; k++) acc[k] = 0.f;
+        for (int i = t; i < (PE_NOPOINTS ? 0 : n); i += NT) {
             const float4 p = P[i];
-            D3 x1 = {{p.x, p.y, 1.0}}, x2 = {{p.z, p.w, 1.0}};
-            D3 q = {{R[0] * x1.v[0] + R[1] * x1.v[1] + R[2], R[3] * x1.v[0] + R[4] * x1.v[1] + R[5],
-                     R[6] * x1.v[0] + R[7] * x1.v[1] + R[8]}};
-            D3 x2t = cross(x2, tt);  // e = x2^T [t]x R x1 = (x2 x t) . (R x1)
-            const double e = dot3(x2t, q);
-            D3 Ex1 = cross(tt, q);   // E x1
-            double Etx2[3];          // E^T x2 = R^T (x2 x t)
-            for (int c = 0; c < 3; c++)
-                Etx2[c] = R[0 * 3 + c] * x2t.v[0] + R[1 * 3 + c] * x2t.v[1] + R[2 * 3 + c] * x2t.v[2];
-            const double s2 = Ex1.v[0] * Ex1.v[0] + Ex1.v[1] * Ex1.v[1] + Etx2[0] * Etx2[0] + Etx2[1] * Etx2[1];
-            if (!(s2 > 0)) continue;
-            const double inv = 1.0 / sqrt(s2);
-            const double r = e * inv;  // Sampson distance (weight frozen at the current model)
-            if (!(fabs(r) < th)) continue;
-            D3 dw = cross(q, x2t);   // d e / d omega   (R <- exp(omega) R)
-            D3 dt = cross(q, x2);    // d e / d t
-            const double J[5] = {dw.v[0] * inv, dw.v[1] * inv, dw.v[2] * inv, dot3(dt, b1) * inv,
-                                 dot3(dt, b2) * inv};
+            const float x1[3] = {p.x, p.y, 1.f}, x2[3] = {p.z, p.w, 1.f};
+            const float q[3] = {R[0] * x1[0] + R[1] * x1[1] + R[2], R[3] * x1[0] + R[4] * x1[1] + R[5],
+                                R[6] * x1[0] + R[7] * x1[1] + R[8]};
+            // e = x2^T [t]x R x1 = (x2 x t) . (R x1)
+            const float x2t[3] = {x2[1] * tv[2] - x2[2] * tv[1], x2[2] * tv[0] - x2[0] * tv[2],
+                                  x2[0] * tv[1] - x2[1] * tv[0]};
+            const float e = x2t[0] * q[0] + x2t[1] * q[1] + x2t[2] * q[2];
+            const float Ex1[2] = {tv[1] * q[2] - tv[2] * q[1], tv[2] * q[0] - tv[0] * q[2]};  // (E x1)_{0,1}
+            float Etx2[2];  // (E^T x2)_{0,1} = (R^T (x2 x t))_{0,1}
+            for (int c = 0; c < 2; c++) Etx2[c] = R[c] * x2t[0] + R[3 + c] * x2t[1] + R[6 + c] * x2t[2];
+            const float s2 = Ex1[0] * Ex1[0] + Ex1[1] * Ex1[1] + Etx2[0] * Etx2[0] + Etx2[1] * Etx2[1];
+            if (!(s2 > 0.f)) continue;
+            const float inv = 1.f / sqrtf(s2);
+            const float r = e * inv;  // Sampson distance (weight frozen at the current model)
+            if (!(fabsf(r) < th)) continue;
+            // d e / d omega = q x (x2 x t)  (R <- exp(omega) R);  d e / d t = q x x2
+            const float dw[3] = {q[1] * x2t[2] - q[2] * x2t[1], q[2] * x2t[0] - q[0] * x2t[2],
+                                 q[0] * x2t[1] - q[1] * x2t[0]};
+            const float dt[3] = {q[1] * x2[2] - q[2] * x2[1], q[2] * x2[0] - q[0] * x2[2],
+                                 q[0] * x2[1] - q[1] * x2[0]};
+            const float J[5] = {dw[0] * inv, dw[1] * inv, dw[2] * inv,
+                                (dt[0] * b1f[0] + dt[1] * b1f[1] + dt[2] * b1f[2]) * inv,
+                                (dt[0] * b2f[0] + dt[1] * b2f[1] + dt[2] * b2f[2]) * inv};
             int k = 0;
 #pragma unroll
             for (int u = 0; u < 5; u++) {
@@ -488,79 +645,116 @@ __global__ __launch_bounds__(NT) void k_pose_ransac(PoseArgs a, const int *__res
 #pragma unroll
             for (int u = 0; u < 5; u++) acc[15 + u] += J[u] * r;
             acc[20] += r * r;
-            acc[21] += 1.0;
+            acc[21] += 1.f;
         }
         // one block reduction of all 22 sums: wave shuffles, then 4 partials in LDS
+        // (levels outer, sums inner: 22 independent shuffles in flight per level)
+        if (!PE_NORED) {
 #pragma unroll
-        for (int k = 0; k < 22; k++) {
-            double v = acc[k];
+            for (int o = 32; o > 0; o >>= 1) {
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-            if (lane == 0) s_red[w][k] = v;
+                for (int k = 0; k < 22; k++) acc[k] += __shfl_xor(acc[k], o, 64);
+            }
+        }
+        if (lane < 22) {
+            float v = acc[0];
+#pragma unroll
+            for (int k = 1; k < 22; k++) v = lane == k ? acc[k] : v;
+            s_red[w][lane] = v;
         }
         __syncthreads();
-        if (t == 0) {
-            double H[15], g[5];
+        if (t == 0 && !PE_NOSOLVE) {
+            float H[15], g[5];
             for (int k = 0; k < 15; k++) H[k] = s_red[0][k] + s_red[1][k] + s_red[2][k] + s_red[3][k];
             for (int k = 0; k < 5; k++) g[k] = s_red[0][15 + k] + s_red[1][15 + k] + s_red[2][15 + k] + s_red[3][15 + k];
-            const double r2 = s_red[0][20] + s_red[1][20] + s_red[2][20] + s_red[3][20];
-            const double cnt = s_red[0][21] + s_red[1][21] + s_red[2][21] + s_red[3][21];
-            // (H + lambda diag H) d = -g, Cholesky
-            double A[5][5];
-            int k = 0;
-            for (int u = 0; u < 5; u++)
-                for (int v = u; v < 5; v++) {
+            const float r2 = s_red[0][20] + s_red[1][20] + s_red[2][20] + s_red[3][20];
+            const float cnt = s_red[0][21] + s_red[1][21] + s_red[2][21] + s_red[3][21];
+            // (H + lambda diag H) d = -g: float Cholesky with one reciprocal per pivot (the
+            // step only has to be a descent direction; the pose itself stays double)
+            // every loop fully unrolled: static register indexing, no private (scratch) arrays
+            float A[5][5];
+#pragma unroll
+            for (int u = 0, k = 0; u < 5; u++)
+#pragma unroll
+                for (int v = u; v < 5; v++, k++) {
                     A[u][v] = H[k];
                     A[v][u] = H[k];
-                    k++;
                 }
-            for (int u = 0; u < 5; u++) A[u][u] = A[u][u] * (1.0 + 1e-9) + 1e-300;
-            double L[5][5] = {};
-            bool ok = cnt >= 5;
-            for (int i = 0; i < 5 && ok; i++)
+#pragma unroll
+            for (int u = 0; u < 5; u++) A[u][u] = A[u][u] * (1.0f + 1e-6f) + 1e-30f;
+            float L[5][5] = {}, rl[5] = {};
+            bool ok = cnt >= 5.f;
+#pragma unroll
+            for (int i = 0; i < 5; i++)
+#pragma unroll
                 for (int j = 0; j <= i; j++) {
-                    double sum = A[i][j];
+                    float sum = A[i][j];
+#pragma unroll
                     for (int m = 0; m < j; m++) sum -= L[i][m] * L[j][m];
                     if (i == j) {
-                        if (!(sum > 0)) {
-                            ok = false;
-                            break;
-                        }
-                        L[i][i] = sqrt(sum);
+                        ok = ok && sum > 0.f;
+                        L[i][i] = sqrtf(fmaxf(sum, 1e-30f));
+                        rl[i] = 1.f / L[i][i];
                     } else {
-                        L[i][j] = sum / L[j][j];
+                        L[i][j] = sum * rl[j];
                     }
                 }
             if (ok) {
-                double y[5], d[5];
+                float y[5];
+                double d[5];
+#pragma unroll
                 for (int i = 0; i < 5; i++) {
-                    double sum = -g[i];
+                    float sum = -g[i];
+#pragma unroll
                     for (int m = 0; m < i; m++) sum -= L[i][m] * y[m];
-                    y[i] = sum / L[i][i];
+                    y[i] = sum * rl[i];
                 }
+#pragma unroll
                 for (int i = 4; i >= 0; i--) {
-                    double sum = y[i];
-                    for (int m = i + 1; m < 5; m++) sum -= L[m][i] * d[m];
-                    d[i] = sum / L[i][i];
+                    float sum = y[i];
+#pragma unroll
+                    for (int m = i + 1; m < 5; m++) sum -= L[m][i] * (float)d[m];
+                    d[i] = sum * rl[i];
                 }
-                double dR[3][3], Rn[3][3];
-                rodrigues(d, dR);
+                float dR[3][3];
+                const float df[3] = {(float)d[0], (float)d[1], (float)d[2]};
+                rodrigues_f(df, dR);
+                float Rn[9], tn[3];
+#pragma unroll
                 for (int i = 0; i < 3; i++)
+#pragma unroll
                     for (int j = 0; j < 3; j++)
-                        Rn[i][j] = dR[i][0] * R[0 * 3 + j] + dR[i][1] * R[1 * 3 + j] + dR[i][2] * R[2 * 3 + j];
-                double tn[3];
-                for (int i = 0; i < 3; i++) tn[i] = tv[i] + d[3] * b1.v[i] + d[4] * b2.v[i];
-                const double nt = sqrt(tn[0] * tn[0] + tn[1] * tn[1] + tn[2] * tn[2]);
-                for (int i = 0; i < 9; i++) s_pose[i] = Rn[i / 3][i % 3];
-                for (int i = 0; i < 3; i++) s_pose[9 + i] = tn[i] / nt;
-                s_th = fmin(th_max, fmax(3.0 * sqrt(r2 / cnt), th_min));
+                        Rn[i * 3 + j] = dR[i][0] * s_pf[0 * 3 + j] + dR[i][1] * s_pf[1 * 3 + j] + dR[i][2] * s_pf[2 * 3 + j];
+#pragma unroll
+                for (int i = 0; i < 3; i++) tn[i] = s_pf[9 + i] + (float)d[3] * s_basis[i] + (float)d[4] * s_basis[3 + i];
+                const float rn = 1.f / sqrtf(tn[0] * tn[0] + tn[1] * tn[1] + tn[2] * tn[2]);
+#pragma unroll
+                for (int i = 0; i < 9; i++) s_pf[i] = Rn[i];
+#pragma unroll
+                for (int i = 0; i < 3; i++) s_pf[9 + i] = tn[i] * rn;
+                tangent_basis_f(s_pf + 9, s_basis);
+                const double th_new = fmin(th_max, fmax(3.0 * sqrt((double)r2 / cnt), th_min));
+                double dmax = 0;
+                for (int i = 0; i < 5; i++) dmax = fmax(dmax, fabs(d[i]));
+                // converged: the step is below the float residual's resolution and the
+                // inlier band no longer moves -- further iterations cannot change the pose
+                s_done = dmax < 1e-7 && (float)th_new == (float)s_th;
+                s_th = th_new;
+            } else {
+                s_done = 1;
             }
         }
         __syncthreads();
+        if (s_done) break;
     }
     if (t < 12) {
         const int r = t / 4, c = t % 4;
-        To[t] = (float)(c < 3 ? s_pose[r * 3 + c] : s_pose[9 + r]);
+        To[t] = c < 3 ? s_pf[r * 3 + c] : s_pf[9 + r];
+    }
+    if (PE_TRACE && b == 0 && t == 0) {
+        const long long tk6 = clock64();
+        printf("pose phases (clk): compact %lld hyp+score %lld argmin %lld decomp %lld cheir %lld gn %lld\n",
+               tk1 - tk0, tk2 - tk1, tk3 - tk2, tk4 - tk3, tk5 - tk4, tk6 - tk5);
     }
     if (t == 0) {
         num_inliers[b] = ninl;
