@@ -114,10 +114,24 @@ __device__ __forceinline__ void wait_vm() {
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-// max / min as v_med3_f32 against -/+inf: no NaN-quieting v_max(x, x) in front (inputs are
-// MFMA results, never NaN for finite descriptors)
-__device__ __forceinline__ float vmax(float a, float b) { return __builtin_amdgcn_fmed3f(a, b, __builtin_inff()); }
-__device__ __forceinline__ float vmin(float a, float b) { return __builtin_amdgcn_fmed3f(a, b, -__builtin_inff()); }
+// max / min straight from inline asm: the compiler otherwise quiets each operand (IEEE-mode
+// v_max_f32 x, x, x) before every min/max.  Screen values are never NaN for in-range
+// descriptors (out-of-range rows / pairs take the exact path).  Not volatile: freely scheduled.
+__device__ __forceinline__ float vmax(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float vmin(float a, float b) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 
 // Top-2 of a set of columns: largest value m1 at column i (lowest column on a tie) and the
 // second largest value m2 (equal to m1 on a tie).  Min/max/select only.
@@ -136,9 +150,9 @@ __device__ __forceinline__ Top2 join2(const Top2 &x, const Top2 &y) {  // x's co
 }
 // Fold one row's 2 values of a tile (columns j, j + 32; -inf past n1) into the running triple;
 // an earlier tile's column is kept on a tie (strict >).
-__device__ __forceinline__ void fold2(float v0, float v1, int j, float &m1, int &i1, float &m2) {
-    const Top2 t = leaf2(v0, j, v1, j + 32);
-    m2 = vmax(vmin(m1, t.m1), vmax(m2, t.m2));
+__device__ __forceinline__ void fold2(float v0, float v1, int j, int j32, float &m1, int &i1, float &m2) {
+    const Top2 t = leaf2(v0, j, v1, j32);
+    m2 = vmax3(vmin(m1, t.m1), m2, t.m2);
     i1 = t.m1 > m1 ? t.i : i1;
     m1 = vmax(m1, t.m1);
 }
@@ -171,17 +185,34 @@ __device__ __forceinline__ int xcd_remap(int b, int total) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-// the reference's score: s = 0; s = s + a[k]*b[k], k = 0..255 (no FMA: -ffp-contract=off)
+
 __device__ __forceinline__ float exact_dot(const float *__restrict__ a, const float *__restrict__ b) {
+    constexpr int U = 4;  // float4 per operand per batch
+    float4 xa[2][U], xb[2][U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        xa[0][u] = *reinterpret_cast<const float4 *>(a + 4 * u);
+        xb[0][u] = *reinterpret_cast<const float4 *>(b + 4 * u);
+    }
     float s = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < KD; k += 4) {
-        const float4 x = *reinterpret_cast<const float4 *>(a + k);
-        const float4 y = *reinterpret_cast<const float4 *>(b + k);
-        s = __fadd_rn(s, __fmul_rn(x.x, y.x));
-        s = __fadd_rn(s, __fmul_rn(x.y, y.y));
-        s = __fadd_rn(s, __fmul_rn(x.z, y.z));
-        s = __fadd_rn(s, __fmul_rn(x.w, y.w));
+#pragma unroll
+    for (int bt = 0; bt < KD / (4 * U); bt++) {
+        const int cur = bt & 1;
+        if (bt + 1 < KD / (4 * U)) {
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                xa[cur ^ 1][u] = *reinterpret_cast<const float4 *>(a + 4 * U * (bt + 1) + 4 * u);
+                xb[cur ^ 1][u] = *reinterpret_cast<const float4 *>(b + 4 * U * (bt + 1) + 4 * u);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const float4 x = xa[cur][u], y = xb[cur][u];
+            s = __fadd_rn(s, __fmul_rn(x.x, y.x));
+            s = __fadd_rn(s, __fmul_rn(x.y, y.y));
+            s = __fadd_rn(s, __fmul_rn(x.z, y.z));
+            s = __fadd_rn(s, __fmul_rn(x.w, y.w));
+        }
     }
     return s;
 }
@@ -307,7 +338,6 @@ __global__ __launch_bounds__(NT, 2) void k_ap_match(int tiles_r, int cap, const 
     const int xsw = fh ^ (fr & 15);  // chunk(2 s + fh) ^ (fr & 15) = 2 s ^ xsw
 
     const f32x16 zero16 = {};
-    f32x16 acc0 = zero16, acc1 = zero16;
     float m1[16], m2[16];
     int i1[16];
 #pragma unroll
@@ -321,7 +351,20 @@ __global__ __launch_bounds__(NT, 2) void k_ap_match(int tiles_r, int cap, const 
     // J = 0..3.  At slot J the block issues slice g + 3 (tile T + (J+3)/2, k-slice (J+3)%2)
     // into slot (J+3)%4 -- the slot read at g - 1, freed by that slice's barrier -- computes
     // slot J, then waits until slice g + 1 has landed (the two later groups may stay in flight).
-#define AP_SLOT(J)                                                                            \
+    // Tiles alternate between two accumulator pairs (A: even tiles, B: odd tiles); a tile is
+    // folded into the triples during the FIRST slot of the next tile, so the fold's VALU work
+    // interleaves with that slot's MFMAs.  The sweep's last tile (the only one that can reach
+    // past n1) is folded after the loop, with the -inf mask.
+    f32x16 accA0 = zero16, accA1 = zero16, accB0 = zero16, accB1 = zero16;
+#define AP_FOLD(X0, X1, TC)                                                                   \
+    do {                                                                                      \
+        const int col_ = (TC) * BN + fr, col32_ = col_ + 32;                                  \
+        if (!AP_EXP_NOFOLD)                                                                   \
+            _Pragma("unroll") for (int q = 0; q < 16; q++) fold2(X0[q], X1[q], col_, col32_, m1[q], i1[q], m2[q]); \
+        else /* timing experiment: keep the MFMAs live at 1/16 of the fold's VALU work */      \
+            fold2(X0[0] + X0[5] + X0[10] + X0[15], X1[0] + X1[5] + X1[10] + X1[15], col_, col32_, m1[0], i1[0], m2[0]); \
+    } while (0)
+#define AP_SLOT(J, C0, C1, F0, F1, FOLD)                                                      \
     do {                                                                                      \
         constexpr int nx = (J) + NBUF - 1;                                                    \
         const int ntile = T + nx / KS; /* tile of the slice issued now */                     \
@@ -329,36 +372,27 @@ __global__ __launch_bounds__(NT, 2) void k_ap_match(int tiles_r, int cap, const 
             if constexpr (nx % KS == 0) AP_TILE_OFFSETS(ntile);                               \
             AP_STAGE(nx % NBUF, nx % KS);                                                     \
         }                                                                                     \
-        const int tc = T + (J) / KS;                                                          \
         const char *base = lds + OFF_STAGE + (J) * SL_BYTES + rdb;                            \
-        if (!AP_EXP_NOMFMA) { /* all 16 fragment reads first, then the MFMAs (counted waits) */ \
+        if (!AP_EXP_NOMFMA) {                                                                 \
+            /* fragment reads run PF k16 steps ahead of the MFMAs (counted lgkm waits) */      \
+            constexpr int PF = 4;                                                             \
             f16x8 b0_[BK / 16], b1_[BK / 16];                                                 \
-            _Pragma("unroll") for (int s_ = 0; s_ < BK / 16; s_++) {                          \
-                const int ch_ = ((2 * s_) ^ xsw) * 16;                                        \
-                b0_[s_] = *reinterpret_cast<const f16x8 *>(base + ch_);                       \
-                b1_[s_] = *reinterpret_cast<const f16x8 *>(base + 32 * SL_ROW + ch_);         \
-            }                                                                                 \
-            __builtin_amdgcn_sched_barrier(0);                                                \
-            _Pragma("unroll") for (int s_ = 0; s_ < BK / 16; s_++) {                          \
-                const f16x8 a_ = aF[((J) % KS) * (BK / 16) + s_];                             \
-                const bool z_ = (J) % KS == 0 && s_ == 0; /* a tile's first MFMA: C = 0 */    \
-                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_, b0_[s_], z_ ? zero16 : acc0, 0, 0, 0); \
-                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_, b1_[s_], z_ ? zero16 : acc1, 0, 0, 0); \
-            }                                                                                 \
-        }                                                                                     \
-        if constexpr ((J) % KS == KS - 1) { /* column tile done: fold into the lane triples */ \
-            const int col = tc * BN + fr;                                                     \
-            if (tc + 1 == ntc) { /* only the last tile can reach past n1: + 0 keeps, + -inf drops */ \
-                const float lo0 = col < n1 ? 0.f : -__builtin_inff();                         \
-                const float lo1 = col + 32 < n1 ? 0.f : -__builtin_inff();                    \
-                _Pragma("unroll") for (int q = 0; q < 16; q++) {                              \
-                    acc0[q] += lo0;                                                           \
-                    acc1[q] += lo1;                                                           \
+            _Pragma("unroll") for (int s_ = 0; s_ < BK / 16 + PF; s_++) {                     \
+                if (s_ < BK / 16) {                                                           \
+                    const int ch_ = ((2 * s_) ^ xsw) * 16;                                    \
+                    b0_[s_] = *reinterpret_cast<const f16x8 *>(base + ch_);                   \
+                    b1_[s_] = *reinterpret_cast<const f16x8 *>(base + 32 * SL_ROW + ch_);     \
+                }                                                                             \
+                if (s_ >= PF) {                                                               \
+                    const int m_ = s_ - PF;                                                   \
+                    const f16x8 a_ = aF[((J) % KS) * (BK / 16) + m_];                         \
+                    const bool z_ = (J) % KS == 0 && m_ == 0; /* a tile's first MFMA: C = 0 */ \
+                    C0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_, b0_[m_], z_ ? zero16 : C0, 0, 0, 0); \
+                    C1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_, b1_[m_], z_ ? zero16 : C1, 0, 0, 0); \
                 }                                                                             \
             }                                                                                 \
-            if (!AP_EXP_NOFOLD)                                                               \
-                _Pragma("unroll") for (int q = 0; q < 16; q++) fold2(acc0[q], acc1[q], col, m1[q], i1[q], m2[q]); \
         }                                                                                     \
+        if (FOLD) AP_FOLD(F0, F1, T + (J) / KS - 1); /* previous tile, beside these MFMAs */  \
         if (AP_EXP_NOWAIT) {                                                                  \
         } else if (ntile < ntc) {                                                             \
             wait_vm<DMA_PER_SLICE * (NBUF - 2)>();                                            \
@@ -380,15 +414,29 @@ __global__ __launch_bounds__(NT, 2) void k_ap_match(int tiles_r, int cap, const 
     wait_vm<0>();
     __syncthreads();
     for (int T = 0; T < ntc; T += 2) {
-        AP_SLOT(0);
-        AP_SLOT(1);
+        AP_SLOT(0, accA0, accA1, accB0, accB1, T > 0);
+        AP_SLOT(1, accA0, accA1, accB0, accB1, false);
         if (T + 1 < ntc) {
-            AP_SLOT(2);
-            AP_SLOT(3);
+            AP_SLOT(2, accB0, accB1, accA0, accA1, true);
+            AP_SLOT(3, accB0, accB1, accA0, accA1, false);
         }
+    }
+    if (ntc > 0) {  // the last tile: mask columns past n1 (+ 0 keeps, + -inf drops), fold
+        const int tl = ntc - 1;
+        f32x16 x0 = (tl & 1) ? accB0 : accA0, x1 = (tl & 1) ? accB1 : accA1;
+        const int col = tl * BN + fr;
+        const float lo0 = col < n1 ? 0.f : -__builtin_inff();
+        const float lo1 = col + 32 < n1 ? 0.f : -__builtin_inff();
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            x0[q] += lo0;
+            x1[q] += lo1;
+        }
+        AP_FOLD(x0, x1, tl);
     }
 #undef AP_STAGE
 #undef AP_SLOT
+#undef AP_FOLD
 #undef AP_TILE_OFFSETS
 
     // ---- merge the triples across the 32 lanes (columns) that share a row ----
