@@ -223,9 +223,14 @@ def main():
     pose_p = mvtrack.pose_params(mvtrack.AS_INTENDED, fx=K[0, 0], fy=K[1, 1], cx=K[0, 2], cy=K[1, 2],
                                  hypotheses=args.hypotheses, inlier_thresh=1.0, refine_iters=10, seed=7)
 
+    # pipelined across steps: frame 1 of the next batch is staged (k_ap_split, auxiliary
+    # stream) while this batch's pose runs; every step still does all of its own work
     def step():
-        ctx.match_allpairs_f32(d0, d1, nn_, nn_, idx, score, 0.8)
+        ctx.match_allpairs_f32_run(d0, d1, nn_, nn_, idx, score, 0.8)
+        ctx.match_allpairs_f32_prepare(d1, nn_)  # the next step's batch
         ctx.pose_from_matches(pose_p, nn_, idx, kp0, kp1, T, nmatch, ninl, status)
+
+    ctx.match_allpairs_f32_prepare(d1, nn_)
 
     mvtrack.profile_enable(False)
     sync = torch.cuda.synchronize

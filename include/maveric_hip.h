@@ -112,12 +112,23 @@ float mv_scale_as_built(float scale); /* low 32 bits of (double)scale, SURVEY F7
 /* For every row i < n0[b] of desc0[b]: the FIRST j < n1[b] attaining the
  * maximum of the fp32 score s_ij = sum_k d0[i][k]*d1[j][k] (summed k = 0..255
  * sequentially, mul then add: the gemmini_functions_cpu.h:45-49 order), kept
- * when (double)s > thresh.  match_idx = -1 otherwise.  Bit-exact: an MFMA
- * screen plus an exact re-score of every candidate within the rounding bound.
- * Rows must be finite.  cap = row stride (keypoints per frame slot). */
+ * when (double)s > thresh and s > 0.  match_idx = -1 otherwise.  Bit-exact: an
+ * fp16 MFMA screen plus an exact re-score of every candidate within the
+ * rounding bound (rows with |x| >= 2 or non-finite values take the exact path).
+ * cap = row stride (keypoints per frame slot). */
 int mv_match_allpairs_f32_dev(mv_context *ctx, int batch, int cap, const int *n0, const int *n1,
                               const float *desc0, const float *desc1, double thresh, int *match_idx,
                               float *match_score);
+/* The same as two stages, for pipelining batches: prepare stages frame 1 (fp16 image,
+ * norms) on the context's auxiliary stream, ordered after everything issued so far on the
+ * context stream; run waits for it on the context stream and matches.  Issue
+ * prepare(next batch) right after run(this batch) and before the pose of this batch: the
+ * staging of the next batch then overlaps the pose.  run must be given exactly the
+ * (batch, cap, n1, desc1) of the last prepare. */
+int mv_match_allpairs_f32_prepare_dev(mv_context *ctx, int batch, int cap, const int *n1, const float *desc1);
+int mv_match_allpairs_f32_run_dev(mv_context *ctx, int batch, int cap, const int *n0, const int *n1,
+                                  const float *desc0, const float *desc1, double thresh, int *match_idx,
+                                  float *match_score);
 /* int8 descriptors: exact cosine (dot > 0, 100 dot^2 > 81 |a|^2 |b|^2, first
  * maximum of dot^2/|b|^2); integer-exact (MFMA i8). */
 int mv_match_allpairs_i8_dev(mv_context *ctx, int batch, int cap, const int *n0, const int *n1,

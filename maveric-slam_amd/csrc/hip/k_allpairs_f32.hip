@@ -550,30 +550,54 @@ size_t allpairs_f32_scratch_bytes(int batch, int cap) {
     return rows * ROW_BYTES + align_up(rows * 4, 256) + align_up((size_t)batch * 4, 256);
 }
 
-int launch_allpairs_f32(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
-                        const float *desc0, const float *desc1, double thresh, int *match_idx,
-                        float *match_score) {
+namespace {
+struct ApScratch {
+    char *h1;
+    float *nrm1;
+    int *bad;
+};
+ApScratch ap_scratch_map(void *scratch, int batch, int cap) {
+    const size_t rows = (size_t)batch * cap;
+    ApScratch m;
+    m.h1 = (char *)scratch;
+    m.nrm1 = (float *)(m.h1 + rows * ROW_BYTES);
+    m.bad = (int *)((char *)m.nrm1 + align_up(rows * 4, 256));
+    return m;
+}
+}  // namespace
+
+// frame 1 -> fp16 image + |b|^2 + per-pair range flag (k_ap_split)
+int launch_allpairs_f32_prepare(hipStream_t s, void *scratch, int batch, int cap, const int *n1,
+                                const float *desc1) {
+    MV_REQUIRE(batch > 0 && cap > 0 && n1 && desc1 && scratch);
+    MV_REQUIRE(((uintptr_t)desc1 & 15) == 0);
+    MV_REQUIRE(cap <= (1 << 22));  // per-lane DMA source offsets are 32-bit byte offsets into a pair
+    const size_t rows = (size_t)batch * cap;
+    const ApScratch m = ap_scratch_map(scratch, batch, cap);
+    const long split_blocks = (long)((rows + 3) / 4);
+    MV_REQUIRE(split_blocks < (1l << 31));
+    MV_HIP_TRY(hipMemsetAsync(m.bad, 0, (size_t)batch * 4, s));
+    MV_PROF_BEGIN(s, "k_ap_split");
+    hipLaunchKernelGGL(k_ap_split, dim3((unsigned)split_blocks), dim3(256), 0, s, batch, cap, n1, desc1, m.h1, m.nrm1,
+                       m.bad);
+    MV_PROF_END(s);
+    MV_LAUNCH_CHECK();
+    return MV_OK;
+}
+
+// the sweep + exact re-score (k_ap_match) over a prepared frame 1
+int launch_allpairs_f32_match(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
+                              const float *desc0, const float *desc1, double thresh, int *match_idx,
+                              float *match_score) {
     MV_REQUIRE(batch > 0 && cap > 0 && n0 && n1 && desc0 && desc1 && match_idx && match_score && scratch);
     MV_REQUIRE(((uintptr_t)desc0 & 15) == 0 && ((uintptr_t)desc1 & 15) == 0);
     const int tiles_r = (cap + BM - 1) / BM;
     const long blocks = (long)batch * tiles_r;
     MV_REQUIRE(blocks < (1l << 31));
-    MV_REQUIRE(cap <= (1 << 22));  // per-lane DMA source offsets are 32-bit byte offsets into a pair
-    const size_t rows = (size_t)batch * cap;
-    char *h1 = (char *)scratch;
-    float *nrm1 = (float *)(h1 + rows * ROW_BYTES);
-    int *bad = (int *)((char *)nrm1 + align_up(rows * 4, 256));
-    const long split_blocks = (long)((rows + 3) / 4);
-    MV_REQUIRE(split_blocks < (1l << 31));
-    MV_HIP_TRY(hipMemsetAsync(bad, 0, (size_t)batch * 4, s));
-    MV_PROF_BEGIN(s, "k_ap_split");
-    hipLaunchKernelGGL(k_ap_split, dim3((unsigned)split_blocks), dim3(256), 0, s, batch, cap, n1, desc1, h1, nrm1,
-                       bad);
-    MV_PROF_END(s);
-    MV_LAUNCH_CHECK();
+    const ApScratch m = ap_scratch_map(scratch, batch, cap);
     MV_PROF_BEGIN(s, "k_ap_match");
-    hipLaunchKernelGGL(k_ap_match, dim3((unsigned)blocks), dim3(NT), 0, s, tiles_r, cap, n0, n1, desc0, desc1, h1,
-                       nrm1, bad, thresh, match_idx, match_score);
+    hipLaunchKernelGGL(k_ap_match, dim3((unsigned)blocks), dim3(NT), 0, s, tiles_r, cap, n0, n1, desc0, desc1, m.h1,
+                       m.nrm1, m.bad, thresh, match_idx, match_score);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     return MV_OK;
@@ -581,13 +605,75 @@ int launch_allpairs_f32(hipStream_t s, void *scratch, int batch, int cap, const 
 
 }  // namespace mv
 
+namespace {
+void *ap_scratch(mv_context *ctx, size_t bytes) {
+    if (bytes <= ctx->ap_scratch_bytes) return ctx->ap_scratch;
+    if (ctx->ap_scratch) {
+        (void)hipDeviceSynchronize();  // growing: nothing may still use the old buffer
+        (void)hipFree(ctx->ap_scratch);
+        ctx->ap_scratch = nullptr;
+        ctx->ap_scratch_bytes = 0;
+    }
+    const size_t b = mv::align_up(bytes, 1 << 20);
+    if (hipMalloc(&ctx->ap_scratch, b) != hipSuccess) {
+        mv::set_error(MV_ERR_OUT_OF_MEMORY, "all-pairs scratch allocation of %zu bytes failed", b);
+        ctx->ap_scratch = nullptr;
+        return nullptr;
+    }
+    ctx->ap_scratch_bytes = b;
+    return ctx->ap_scratch;
+}
+}  // namespace
+
 extern "C" int mv_match_allpairs_f32_dev(mv_context *ctx, int batch, int cap, const int *n0, const int *n1,
                                          const float *desc0, const float *desc1, double thresh, int *match_idx,
                                          float *match_score) {
     MV_REQUIRE(ctx != nullptr && batch > 0 && cap > 0);
     MV_HIP_TRY(hipSetDevice(ctx->device));
-    void *scr = mv::scratch(ctx, mv::allpairs_f32_scratch_bytes(batch, cap));
+    void *scr = ap_scratch(ctx, mv::allpairs_f32_scratch_bytes(batch, cap));
     if (!scr) return MV_ERR_OUT_OF_MEMORY;
-    return mv::launch_allpairs_f32(ctx->stream, scr, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
-                                   match_score);
+    ctx->prep_desc1 = nullptr;  // the prepared image is overwritten
+    const int st = mv::launch_allpairs_f32_prepare(ctx->stream, scr, batch, cap, n1, desc1);
+    if (st != MV_OK) return st;
+    return mv::launch_allpairs_f32_match(ctx->stream, scr, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
+                                         match_score);
+}
+
+extern "C" int mv_match_allpairs_f32_prepare_dev(mv_context *ctx, int batch, int cap, const int *n1,
+                                                 const float *desc1) {
+    MV_REQUIRE(ctx != nullptr && batch > 0 && cap > 0 && n1 && desc1);
+    MV_HIP_TRY(hipSetDevice(ctx->device));
+    void *scr = ap_scratch(ctx, mv::allpairs_f32_scratch_bytes(batch, cap));
+    if (!scr) return MV_ERR_OUT_OF_MEMORY;
+    if (!ctx->aux_stream) {
+        MV_HIP_TRY(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
+        MV_HIP_TRY(hipEventCreateWithFlags(&ctx->ev_in, hipEventDisableTiming));
+        MV_HIP_TRY(hipEventCreateWithFlags(&ctx->ev_prep, hipEventDisableTiming));
+    }
+    // inputs (and the previous run's use of the scratch) as of this call on the context stream
+    MV_HIP_TRY(hipEventRecord(ctx->ev_in, ctx->stream));
+    MV_HIP_TRY(hipStreamWaitEvent(ctx->aux_stream, ctx->ev_in, 0));
+    const int st = mv::launch_allpairs_f32_prepare(ctx->aux_stream, scr, batch, cap, n1, desc1);
+    if (st != MV_OK) return st;
+    MV_HIP_TRY(hipEventRecord(ctx->ev_prep, ctx->aux_stream));
+    ctx->prep_batch = batch;
+    ctx->prep_cap = cap;
+    ctx->prep_n1 = n1;
+    ctx->prep_desc1 = desc1;
+    return MV_OK;
+}
+
+extern "C" int mv_match_allpairs_f32_run_dev(mv_context *ctx, int batch, int cap, const int *n0, const int *n1,
+                                             const float *desc0, const float *desc1, double thresh, int *match_idx,
+                                             float *match_score) {
+    MV_REQUIRE(ctx != nullptr);
+    if (!ctx->prep_desc1 || ctx->prep_batch != batch || ctx->prep_cap != cap || ctx->prep_n1 != n1 ||
+        ctx->prep_desc1 != desc1) {
+        mv::set_error(MV_ERR_INVALID_ARG, "mv_match_allpairs_f32_run_dev: no matching prepare for this batch");
+        return MV_ERR_INVALID_ARG;
+    }
+    MV_HIP_TRY(hipSetDevice(ctx->device));
+    MV_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_prep, 0));
+    return mv::launch_allpairs_f32_match(ctx->stream, ctx->ap_scratch, batch, cap, n0, n1, desc0, desc1, thresh,
+                                         match_idx, match_score);
 }

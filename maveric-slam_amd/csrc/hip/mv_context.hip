@@ -138,7 +138,14 @@ int mv_context_destroy(mv_context *ctx) {
     if (!ctx) return MV_OK;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->aux_stream) {
+        (void)hipStreamSynchronize(ctx->aux_stream);
+        (void)hipEventDestroy(ctx->ev_in);
+        (void)hipEventDestroy(ctx->ev_prep);
+        (void)hipStreamDestroy(ctx->aux_stream);
+    }
     if (ctx->scratch) (void)hipFree(ctx->scratch);
+    if (ctx->ap_scratch) (void)hipFree(ctx->ap_scratch);
     if (ctx->stage_dev) (void)hipFree(ctx->stage_dev);
     (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
@@ -161,9 +168,19 @@ int mv_context_synchronize(mv_context *ctx) {
 
 int mv_context_reserve(mv_context *ctx, int batch, int cap) {
     MV_REQUIRE(ctx != nullptr && batch > 0 && cap > 0);
-    size_t need = mv::allpairs_f32_scratch_bytes(batch, cap);
-    size_t b = mv::allpairs_i8_scratch_bytes(batch, cap);
-    if (b > need) need = b;
+    if (ctx->ap_scratch_bytes < mv::allpairs_f32_scratch_bytes(batch, cap)) {
+        if (ctx->ap_scratch) {
+            MV_HIP_TRY(hipDeviceSynchronize());
+            MV_HIP_TRY(hipFree(ctx->ap_scratch));
+            ctx->ap_scratch = nullptr;
+            ctx->ap_scratch_bytes = 0;
+        }
+        const size_t ab = mv::align_up(mv::allpairs_f32_scratch_bytes(batch, cap), 1 << 20);
+        if (hipMalloc(&ctx->ap_scratch, ab) != hipSuccess) return MV_ERR_OUT_OF_MEMORY;
+        ctx->ap_scratch_bytes = ab;
+    }
+    size_t need = mv::allpairs_i8_scratch_bytes(batch, cap);
+    size_t b;
     b = mv::pose_scratch_bytes(batch, cap);
     if (b > need) need = b;
     if (!mv::scratch(ctx, need)) return MV_ERR_OUT_OF_MEMORY;

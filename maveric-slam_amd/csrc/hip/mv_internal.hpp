@@ -15,6 +15,15 @@ struct mv_context {
     // small host<->device staging for the single-pair host entry points
     void *stage_dev;
     size_t stage_bytes;
+    // all-pairs fp32: its own scratch (frame-1 fp16 image, norms, range flags) so that a
+    // prepare of the next batch on aux_stream never races the pose kernels on `stream`
+    void *ap_scratch;
+    size_t ap_scratch_bytes;
+    hipStream_t aux_stream;  // created on first prepare
+    hipEvent_t ev_in, ev_prep;
+    int prep_batch, prep_cap;  // what the last prepare staged (run checks it)
+    const int *prep_n1;
+    const float *prep_desc1;
 };
 
 namespace mv {
@@ -75,9 +84,11 @@ int launch_softmax(hipStream_t s, int batch, int cells, const float *scales, con
 int launch_top_n_select(hipStream_t s, int batch, int cells, const int *max_idx, const float *probs, int N,
                         int cap, int *num_sel, int *patches, int *indices, float *sel_probs, int *status);
 size_t allpairs_f32_scratch_bytes(int batch, int cap);
-int launch_allpairs_f32(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
-                        const float *desc0, const float *desc1, double thresh, int *match_idx,
-                        float *match_score);
+int launch_allpairs_f32_prepare(hipStream_t s, void *scratch, int batch, int cap, const int *n1,
+                                const float *desc1);
+int launch_allpairs_f32_match(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
+                              const float *desc0, const float *desc1, double thresh, int *match_idx,
+                              float *match_score);
 size_t allpairs_i8_scratch_bytes(int batch, int cap);
 int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
                        const int8_t *desc0, const int8_t *desc1, int *match_idx, int *match_dot);

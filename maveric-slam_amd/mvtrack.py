@@ -103,6 +103,8 @@ def lib():
             "mv_window_match_batch_dev": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P,
                                                _P]),
             "mv_match_allpairs_f32_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _D, _P, _P]),
+            "mv_match_allpairs_f32_prepare_dev": (_I, [_P, _I, _I, _P, _P]),
+            "mv_match_allpairs_f32_run_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _D, _P, _P]),
             "mv_match_allpairs_i8_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P]),
             "mv_pose_batch_dev": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P]),
             "mv_pose_from_matches_dev": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
@@ -324,6 +326,17 @@ class Context:
         B, cap = desc0.shape[0], desc0.shape[1]
         check(lib().mv_match_allpairs_f32_dev(self.h, B, cap, _t(n0), _t(n1), _t(desc0), _t(desc1), float(thresh),
                                               _t(match_idx), _t(match_score)), "match_allpairs_f32")
+
+    def match_allpairs_f32_prepare(self, desc1, n1):
+        """Stage frame 1 of a batch on the auxiliary stream (see mv_match_allpairs_f32_prepare_dev)."""
+        B, cap = desc1.shape[0], desc1.shape[1]
+        check(lib().mv_match_allpairs_f32_prepare_dev(self.h, B, cap, _t(n1), _t(desc1)), "match_allpairs_f32_prepare")
+
+    def match_allpairs_f32_run(self, desc0, desc1, n0, n1, match_idx, match_score, thresh=0.8):
+        """Match a batch staged by match_allpairs_f32_prepare(desc1, n1)."""
+        B, cap = desc0.shape[0], desc0.shape[1]
+        check(lib().mv_match_allpairs_f32_run_dev(self.h, B, cap, _t(n0), _t(n1), _t(desc0), _t(desc1), float(thresh),
+                                                  _t(match_idx), _t(match_score)), "match_allpairs_f32_run")
 
     def match_allpairs_i8(self, desc0, desc1, n0, n1, match_idx, match_dot):
         B, cap = desc0.shape[0], desc0.shape[1]

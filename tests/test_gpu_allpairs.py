@@ -134,6 +134,40 @@ def test_allpairs_f32_out_of_screen_range(ctx, orc, torch_cuda):
             assert (bits(sc[k, :a.shape[0]]) == bits(s2)).all(), k
 
 
+def test_allpairs_f32_prepare_run_pipeline(ctx, orc, torch_cuda):
+    """prepare(next) issued between run(this) and the next run: identical to the one-call API;
+    run without its prepare is refused."""
+    torch = torch_cuda
+    dev = torch.device("cuda:0")
+    batches = []
+    for s in range(3):
+        p = synth.synth_pair_f32(70 + s, n=300, n1=280)
+        batches.append((torch.from_numpy(p["desc0"][None].copy()).to(dev),
+                        torch.from_numpy(np.ascontiguousarray(np.pad(p["desc1"], ((0, 20), (0, 0))))[None]).to(dev)))
+    n0 = torch.tensor([300], dtype=torch.int32, device=dev)
+    n1 = torch.tensor([280], dtype=torch.int32, device=dev)
+    ctx.set_stream(torch.cuda.current_stream())
+    outs = []
+    ctx.match_allpairs_f32_prepare(batches[0][1], n1)
+    for k, (a, b) in enumerate(batches):
+        idx = torch.full((1, 300), -7, dtype=torch.int32, device=dev)
+        sc = torch.zeros((1, 300), dtype=torch.float32, device=dev)
+        ctx.match_allpairs_f32_run(a, b, n0, n1, idx, sc, 0.8)
+        if k + 1 < len(batches):
+            ctx.match_allpairs_f32_prepare(batches[k + 1][1], n1)
+        outs.append((idx, sc))
+    torch.cuda.synchronize()
+    for (a, b), (idx, sc) in zip(batches, outs):
+        i2, s2 = orc.allpairs_f32(a[0].cpu().numpy(), b[0, :280].cpu().numpy(), 0.8)
+        assert (idx[0].cpu().numpy() == i2).all()
+        assert (bits(sc[0].cpu().numpy()) == bits(s2)).all()
+    import mvtrack
+    with pytest.raises(RuntimeError):  # batches[0] is not the staged batch any more
+        ctx.match_allpairs_f32_run(batches[0][0], batches[0][1], n0, n1, outs[0][0], outs[0][1], 0.8)
+    assert mvtrack.lib().mv_last_status() == mvtrack.MV_ERR_INVALID_ARG
+    ctx.set_stream(None)
+
+
 def run_i8(ctx, torch, pairs, cap=None):
     B = len(pairs)
     cap = cap or max(max(a.shape[0], b.shape[0]) for a, b in pairs)
