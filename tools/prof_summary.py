@@ -32,7 +32,7 @@ def argval(flag, default):
     return int(toks[toks.index(flag) + 1]) if flag in toks else default
 
 
-summary = {"tag": tag, "bench_args": args, "batch": argval("--batch", 256), "kp": argval("--kp", 1024),
+summary = {"tag": tag, "bench_args": args, "batch": argval("--batch", 1024), "kp": argval("--kp", 1024),
            "kernels": {}}
 for r in stats:
     name = r.get("Name", r.get("KernelName", "?"))
