@@ -41,6 +41,8 @@
 // dense fp16 MFMA peak 2.5 PF/s.
 #include <math.h>
 
+#include <algorithm>
+
 #include "mv_internal.hpp"
 
 namespace {
@@ -217,25 +219,44 @@ __device__ __forceinline__ float exact_dot(const float *__restrict__ a, const fl
     return s;
 }
 
-// ---- k_ap_split: frame 1 only, one wave per descriptor row (rows >= n1 are never read) ----
+// ---- k_ap_split: frame 1 only.  32 lanes per row, 8 consecutive floats per lane (two
+//      16-B loads, one 16-B store); a 256-thread block converts 8 rows per iteration and
+//      strides over the batch (rows >= n1 are never read downstream) ----
+constexpr int SPLIT_ROWS = 8;
 __global__ __launch_bounds__(256) void k_ap_split(int batch, int cap, const int *__restrict__ n1v,
                                                   const float *__restrict__ desc1, char *__restrict__ h1,
                                                   float *__restrict__ nrm1, int *__restrict__ bad) {
-    const long R = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (R >= (long)batch * cap) return;
-    const int pair = (int)(R / cap), r = (int)(R % cap);
-    if (r >= n1v[pair]) return;
-    const int lane = threadIdx.x & 63;
-    const float4 v = *reinterpret_cast<const float4 *>(desc1 + R * KD + lane * 4);
-    const bool ok = fabsf(v.x) < 2.f && fabsf(v.y) < 2.f && fabsf(v.z) < 2.f && fabsf(v.w) < 2.f;  // NaN: false
-    if (__builtin_amdgcn_ballot_w64(!ok) != 0 && lane == 0) bad[pair] = 1;
-    const f16x4 h = {(_Float16)(v.x * SCALE), (_Float16)(v.y * SCALE), (_Float16)(v.z * SCALE),
-                     (_Float16)(v.w * SCALE)};  // exact power-of-two scale, then RNE to fp16
-    *reinterpret_cast<f16x4 *>(h1 + R * ROW_BYTES + lane * 8) = h;
-    float q = fmaf(v.x, v.x, fmaf(v.y, v.y, fmaf(v.z, v.z, v.w * v.w)));
+    const long rows = (long)batch * cap;
+    const int sub = threadIdx.x & 31, rl = threadIdx.x >> 5;
+    for (long R0 = (long)blockIdx.x * SPLIT_ROWS; R0 < rows; R0 += (long)gridDim.x * SPLIT_ROWS) {
+        const long R = R0 + rl;
+        const int pair = (int)(R / cap), r = (int)(R % cap);
+        const bool live = R < rows && r < n1v[min(pair, batch - 1)];
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f), y = x;
+        if (live) {
+            const float *src = desc1 + R * KD + sub * 8;
+            typedef float f32x4v __attribute__((ext_vector_type(4)));
+            const f32x4v u = __builtin_nontemporal_load(reinterpret_cast<const f32x4v *>(src));
+            const f32x4v v = __builtin_nontemporal_load(reinterpret_cast<const f32x4v *>(src + 4));
+            x = make_float4(u[0], u[1], u[2], u[3]);
+            y = make_float4(v[0], v[1], v[2], v[3]);
+        }
+        const int out = (int)!(fabsf(x.x) < 2.f) | (int)!(fabsf(x.y) < 2.f) | (int)!(fabsf(x.z) < 2.f) |
+                        (int)!(fabsf(x.w) < 2.f) | (int)!(fabsf(y.x) < 2.f) | (int)!(fabsf(y.y) < 2.f) |
+                        (int)!(fabsf(y.z) < 2.f) | (int)!(fabsf(y.w) < 2.f);  // NaN: out of range
+        float q = fmaf(x.x, x.x, fmaf(x.y, x.y, fmaf(x.z, x.z, x.w * x.w)));
+        q = fmaf(y.x, y.x, fmaf(y.y, y.y, fmaf(y.z, y.z, fmaf(y.w, y.w, q))));
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) q += __shfl_xor(q, o, 64);
-    if (lane == 0) nrm1[R] = q;
+        for (int o = 1; o < 32; o <<= 1) q += __shfl_xor(q, o, 64);  // the row's 32 lanes
+        if (live) {
+            const f16x8 h = {(_Float16)(x.x * SCALE), (_Float16)(x.y * SCALE), (_Float16)(x.z * SCALE),
+                             (_Float16)(x.w * SCALE), (_Float16)(y.x * SCALE), (_Float16)(y.y * SCALE),
+                             (_Float16)(y.z * SCALE), (_Float16)(y.w * SCALE)};  // exact 2^14 scale, RNE
+            *reinterpret_cast<f16x8 *>(h1 + R * ROW_BYTES + sub * 16) = h;
+            if (out) bad[pair] = 1;
+            if (sub == 0) nrm1[R] = q;
+        }
+    }
 }
 
 __global__ __launch_bounds__(NT, 2) void k_ap_match(int tiles_r, int cap, const int *__restrict__ n0v,
@@ -574,8 +595,7 @@ int launch_allpairs_f32_prepare(hipStream_t s, void *scratch, int batch, int cap
     MV_REQUIRE(cap <= (1 << 22));  // per-lane DMA source offsets are 32-bit byte offsets into a pair
     const size_t rows = (size_t)batch * cap;
     const ApScratch m = ap_scratch_map(scratch, batch, cap);
-    const long split_blocks = (long)((rows + 3) / 4);
-    MV_REQUIRE(split_blocks < (1l << 31));
+    const long split_blocks = std::min<long>((long)((rows + SPLIT_ROWS - 1) / SPLIT_ROWS), 256l * 64);
     MV_HIP_TRY(hipMemsetAsync(m.bad, 0, (size_t)batch * 4, s));
     MV_PROF_BEGIN(s, "k_ap_split");
     hipLaunchKernelGGL(k_ap_split, dim3((unsigned)split_blocks), dim3(256), 0, s, batch, cap, n1, desc1, m.h1, m.nrm1,
