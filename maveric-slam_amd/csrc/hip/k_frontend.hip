@@ -11,6 +11,7 @@
 // no MFMA here (the window dot is 64..256 int8 MACs per candidate, v_dot4).
 #include "mv_internal.hpp"
 
+
 namespace {
 
 constexpr int kSemiC = 65;
@@ -38,14 +39,18 @@ __device__ __forceinline__ float approx_exp(const float sp[5], int x) {
 
 // ---------------------------------------------------------------------------
 // k_softmax: block = 256 consecutive (frame, cell) rows of 65 int8.
-// The 16,640-byte row block is staged into LDS with coalesced dword loads;
-// each lane then walks its own row (65 logits) in the reference order.
+// The 16,640-byte row block is staged into LDS with coalesced dword loads; each
+// lane then walks its own row (65 logits) in the reference order.  approx_exp
+// depends only on (scale, x) with x in 0..127, so the block first tabulates it for
+// the (at most two) frames it spans -- the same arithmetic, the same bits -- and
+// the row walk reads the table.  Row bytes come from aligned dword reads
+// (v_alignbyte) instead of 65 byte reads.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_softmax(int total_rows, int cells, const float *__restrict__ scales,
                                                  const int8_t *__restrict__ semi, int *__restrict__ max_idx,
                                                  float *__restrict__ probs, int *__restrict__ num_valid) {
-    __shared__ int lds32[256 * kSemiC / 4];
-    const int8_t *lds8 = reinterpret_cast<const int8_t *>(lds32);
+    __shared__ __attribute__((aligned(16))) int lds32[256 * kSemiC / 4 + 4];
+    __shared__ float lut[2][128];
     const int t = threadIdx.x;
     const long r0 = (long)blockIdx.x * 256;
     const int nrows = (int)min((long)256, (long)total_rows - r0);
@@ -55,29 +60,60 @@ __global__ __launch_bounds__(256) void k_softmax(int total_rows, int cells, cons
     for (int i = t; i < nbytes / 4; i += 256) lds32[i] = g32[i];
     for (int i = (nbytes / 4) * 4 + t; i < nbytes; i += 256)
         reinterpret_cast<int8_t *>(lds32)[i] = semi[base + i];
+    const int f_first = (int)(r0 / cells);
+    {  // approx_exp(x), x = 0..127, for frames f_first and f_first + 1 (top_N.c:12-20, 59-63)
+        const int f = f_first + (t >> 7), x = t & 127;
+        if ((long)f * cells < (long)total_rows) {
+            float sp[5];
+            scale_poly(scales[f], sp);
+            lut[t >> 7][x] = approx_exp(sp, x);
+        }
+    }
     __syncthreads();
     if (t >= nrows) return;
     const long r = r0 + t;
     const int frame = (int)(r / cells);
-    float sp[5];
-    scale_poly(scales[frame], sp);
-    const int8_t *row = lds8 + t * kSemiC;
+    const int fl = frame - f_first;  // < 2 whenever cells >= 256
+    float sp_own[5];
+    if (fl >= 2) scale_poly(scales[frame], sp_own);  // tiny frames: no table for this one
+    // the row's 65 bytes: 17 aligned dwords re-aligned to the row start, + the last byte
+    const int rb = t * kSemiC, o = rb & 3, d0 = rb >> 2;
     int best = 64;
     float best_e = 0.0f;
     float den = 1.17549435e-38f;  // FLT_MIN (top_N.c:30)
-    for (int i = 0; i < kSemiC; i++) {
-        int x = row[i];
-        if (x < 0) continue;
-        float e = approx_exp(sp, x);
-        if (i != 64 && e > best_e) {
-            best_e = e;
-            best = i;
+    unsigned w = (unsigned)lds32[d0];
+#pragma unroll
+    for (int j = 0; j < 17; j++) {
+        const unsigned wn = (unsigned)lds32[d0 + j + 1];
+        const unsigned u = __builtin_amdgcn_alignbyte(wn, w, o);  // bytes 4j .. 4j+3 of the row
+        w = wn;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const int i = 4 * j + b;
+            if (i >= kSemiC) break;
+            const int x = (int)(signed char)(u >> (8 * b));
+            if (x < 0) continue;
+            const float e = fl < 2 ? lut[fl][x] : approx_exp(sp_own, x);
+            if (i != 64 && e > best_e) {
+                best_e = e;
+                best = i;
+            }
+            den += e;
         }
-        den += e;
     }
     max_idx[r] = best;
     probs[r] = best != 64 ? best_e / den : -1.0f;
-    if (best != 64) atomicAdd(&num_valid[frame], 1);
+    // (*num_valid)++ per valid cell (top_N.c:160): one atomic per wave and frame, not per
+    // cell (per-cell atomics on one counter per frame serialise in L2)
+    const bool v = best != 64;
+    const int f0 = __shfl(frame, 0, 64);
+    const unsigned long long vm = __ballot(v);
+    if (__ballot(frame != f0) == 0) {  // the whole active wave is one frame (cells >= 64: common)
+        if ((threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1 && vm)
+            atomicAdd(&num_valid[f0], __popcll(vm));
+    } else if (v) {
+        atomicAdd(&num_valid[frame], 1);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -223,22 +259,6 @@ __device__ __forceinline__ int wave_sum(int v) {
     return v;
 }
 
-// dot and squared norm of 64 int8 (16 dwords) against q (16 dwords)
-__device__ __forceinline__ void dot64(const int4 *c, const int *q, int &dot, int &nrm) {
-#pragma unroll
-    for (int v = 0; v < 4; v++) {
-        int4 x = c[v];
-        dot = __builtin_amdgcn_sdot4(x.x, q[4 * v + 0], dot, false);
-        dot = __builtin_amdgcn_sdot4(x.y, q[4 * v + 1], dot, false);
-        dot = __builtin_amdgcn_sdot4(x.z, q[4 * v + 2], dot, false);
-        dot = __builtin_amdgcn_sdot4(x.w, q[4 * v + 3], dot, false);
-        nrm = __builtin_amdgcn_sdot4(x.x, x.x, nrm, false);
-        nrm = __builtin_amdgcn_sdot4(x.y, x.y, nrm, false);
-        nrm = __builtin_amdgcn_sdot4(x.z, x.z, nrm, false);
-        nrm = __builtin_amdgcn_sdot4(x.w, x.w, nrm, false);
-    }
-}
-
 // strict "a better than b" for as-intended (dot^2/na) with tie -> lower order
 __device__ __forceinline__ bool exact_better(long long da, long long na, int ka, long long db, long long nb,
                                              int kb) {
@@ -250,7 +270,186 @@ __device__ __forceinline__ bool exact_better(long long da, long long na, int ka,
     return ka < kb;
 }
 
-// one wave per query slot; 4 waves per block
+// Candidate source for the per-query evaluation: frame 0 straight from global memory (L2
+// serves the overlap of neighbouring windows).  An LDS-tiled variant (union of an 8x8 query
+// tile's windows DMA'd once) measured 2x slower at 14 % query density: see DESIGN.md.
+struct GlobalCands {
+    const int8_t *d0;  // this pair's frame-0 descriptors
+    const int *mi0;
+    const float *pr0;
+    int rows;
+    double prob_thr;
+    __device__ __forceinline__ bool valid(int, int, int p) const {
+        return mi0[p] != 64 && !((double)pr0[p] < prob_thr);
+    }
+    __device__ __forceinline__ int4 chunk(int x, int y, int j) const {
+        return reinterpret_cast<const int4 *>(d0 + ((long)x * rows + y) * kDescD)[j];
+    }
+    __device__ __forceinline__ int dword(int x, int y, int i) const {
+        return reinterpret_cast<const int *>(d0 + ((long)x * rows + y) * kDescD)[i];
+    }
+};
+// dot and squared norm of the first 64 int8 (4 chunks) against q (16 dwords)
+template <class CS>
+__device__ __forceinline__ void dot64c(const CS &C, int x, int y, const int *q, int &dot, int &nrm) {
+#pragma unroll
+    for (int v = 0; v < 4; v++) {
+        int4 c = C.chunk(x, y, v);
+        dot = __builtin_amdgcn_sdot4(c.x, q[4 * v + 0], dot, false);
+        dot = __builtin_amdgcn_sdot4(c.y, q[4 * v + 1], dot, false);
+        dot = __builtin_amdgcn_sdot4(c.z, q[4 * v + 2], dot, false);
+        dot = __builtin_amdgcn_sdot4(c.w, q[4 * v + 3], dot, false);
+        nrm = __builtin_amdgcn_sdot4(c.x, c.x, nrm, false);
+        nrm = __builtin_amdgcn_sdot4(c.y, c.y, nrm, false);
+        nrm = __builtin_amdgcn_sdot4(c.z, c.z, nrm, false);
+        nrm = __builtin_amdgcn_sdot4(c.w, c.w, nrm, false);
+    }
+}
+
+// One query (a whole wave): tracking_main.c:114-165 on the window of frame-1 cell (x1, y1).
+// Returns the result in every lane; best_patch is the frame-0 patch of the winner.
+template <class CS>
+__device__ __forceinline__ QueryResult eval_query(const WinArgs &a, const CS &C, const int8_t *qd, int x1, int y1,
+                                                  int lane, int &best_patch_out) {
+    QueryResult res = {0, 0, 0, -1, 0.0f};
+    // query: lane holds dword `lane` (bytes 4*lane .. 4*lane+3) for cooperative 256-D work,
+    // and every lane holds the first 64 bytes for the per-candidate 64-D dot.
+    const int qv = reinterpret_cast<const int *>(qd)[lane];
+    int q64[16];
+#pragma unroll
+    for (int v = 0; v < 16; v++) q64[v] = __shfl(qv, v, 64);
+    const int n2_256 = wave_sum(__builtin_amdgcn_sdot4(qv, qv, 0, false));
+    const int n2_64 = wave_sum(lane < 16 ? __builtin_amdgcn_sdot4(qv, qv, 0, false) : 0);
+    int xlo = max(x1 + a.shift_x - a.radius, 0), xhi = min(x1 + a.shift_x + a.radius, a.cols - 1);
+    int ylo = max(y1 + a.shift_y - a.radius, 0), yhi = min(y1 + a.shift_y + a.radius, a.rows - 1);
+    const int ny = yhi - ylo + 1;
+    const int ncand = (xhi >= xlo && yhi >= ylo) ? (xhi - xlo + 1) * ny : 0;
+
+    // as-built latch state (carried across 64-candidate chunks)
+    bool latched = false;
+    int n1f = 0;
+    // running best
+    float best_d = 0.0f;
+    int best_k = -1;
+    long long best_dot = 0, best_na = 1;
+    int best_patch = 0;
+
+    for (int base = 0; base < ncand; base += 64) {
+        const int k = base + lane;
+        int patch0 = 0;
+        bool valid = false;
+        if (k < ncand) {
+            const int x0 = xlo + k / ny, y0 = ylo + k % ny;
+            patch0 = x0 * a.rows + y0;
+            valid = C.valid(x0, y0, patch0);
+        }
+        const int cx0 = xlo + min(k, ncand - 1) / ny, cy0 = ylo + min(k, ncand - 1) % ny;
+        float d = __builtin_nanf("");
+        long long cdot = 0, cna = 0;
+        if (a.as_built) {
+            int dot_64 = 0, n1_64 = 0;
+            if (valid) dot64c(C, cx0, cy0, q64, dot_64, n1_64);
+            // resolve the latch: the first valid candidate (scan order) whose
+            // full 256-D norm is non-zero computes the full dot; candidates
+            // before it (all-zero descriptors) divide 0 by 0.
+            unsigned long long vm = __ballot(valid);
+            int f_lane = -1;   // lane of the latching candidate in this chunk
+            int dot_f = 0;
+            while (!latched && vm) {
+                const int l = __ffsll((long long)vm) - 1;
+                const int lx0 = __shfl(cx0, l, 64), ly0 = __shfl(cy0, l, 64);
+                const int cv = C.dword(lx0, ly0, lane);
+                const int full_n1 = wave_sum(__builtin_amdgcn_sdot4(cv, cv, 0, false));
+                const int full_dot = wave_sum(__builtin_amdgcn_sdot4(cv, qv, 0, false));
+                vm &= vm - 1;
+                if (full_n1 != 0) {
+                    latched = true;
+                    n1f = full_n1;
+                    f_lane = l;
+                    dot_f = full_dot;
+                } else if (lane == l) {
+                    d = (float)wrap_mul(full_dot, full_dot) / (float)wrap_mul(full_n1, n2_256);
+                }
+            }
+            if (valid) {
+                if (lane == f_lane) {
+                    d = (float)wrap_mul(dot_f, dot_f) / (float)wrap_mul(n1f, n2_256);
+                } else if (latched && (f_lane < 0 || lane > f_lane)) {
+                    d = (float)wrap_mul(dot_64, dot_64) / (float)wrap_mul(n1f, n2_64);
+                }
+            }
+            bool pass = valid && (double)d > a.thr_sq;
+            // first strict maximum in scan order: max d, ties -> smallest k
+            float bd = pass ? d : -__builtin_inff();
+            int bk = pass ? k : 0x7fffffff;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                float od = __shfl_xor(bd, o, 64);
+                int ok = __shfl_xor(bk, o, 64);
+                if (od > bd || (od == bd && ok < bk)) {
+                    bd = od;
+                    bk = ok;
+                }
+            }
+            if (bk != 0x7fffffff && (best_k < 0 || bd > best_d)) {
+                best_d = bd;
+                best_k = bk;
+                best_patch = __shfl(patch0, bk - base, 64);
+            }
+        } else {
+            int dot = 0, na = 0;
+            if (valid) {
+                const int4 *q4 = reinterpret_cast<const int4 *>(qd);  // wave-uniform address
+#pragma unroll
+                for (int v = 0; v < 16; v++) {
+                    int4 x = C.chunk(cx0, cy0, v), y = q4[v];
+                    dot = __builtin_amdgcn_sdot4(x.x, y.x, dot, false);
+                    dot = __builtin_amdgcn_sdot4(x.y, y.y, dot, false);
+                    dot = __builtin_amdgcn_sdot4(x.z, y.z, dot, false);
+                    dot = __builtin_amdgcn_sdot4(x.w, y.w, dot, false);
+                    na = __builtin_amdgcn_sdot4(x.x, x.x, na, false);
+                    na = __builtin_amdgcn_sdot4(x.y, x.y, na, false);
+                    na = __builtin_amdgcn_sdot4(x.z, x.z, na, false);
+                    na = __builtin_amdgcn_sdot4(x.w, x.w, na, false);
+                }
+            }
+            cdot = dot;
+            cna = na;
+            bool pass = valid && dot > 0 && na != 0 && n2_256 != 0 &&
+                        (unsigned __int128)(100ll * cdot * cdot) >
+                            (unsigned __int128)81 * (unsigned long long)(cna * (long long)n2_256);
+            long long bd = pass ? cdot : 0, bn = pass ? cna : 1;
+            int bk = pass ? k : -1;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                long long od = __shfl_xor(bd, o, 64), on = __shfl_xor(bn, o, 64);
+                int ok = __shfl_xor(bk, o, 64);
+                if (exact_better(od, on, ok, bd, bn, bk)) {
+                    bd = od;
+                    bn = on;
+                    bk = ok;
+                }
+            }
+            if (bk >= 0 && exact_better(bd, bn, bk, best_dot, best_na, best_k)) {
+                best_dot = bd;
+                best_na = bn;
+                best_k = bk;
+                best_d = (float)((double)bd * (double)bd / ((double)bn * (double)n2_256));
+                best_patch = __shfl(patch0, bk - base, 64);
+            }
+        }
+    }
+    if (best_k >= 0) {
+        res.found = 1;
+        res.bx = xlo + best_k / ny;
+        res.by = ylo + best_k % ny;
+        res.score = best_d;
+    }
+    best_patch_out = best_k >= 0 ? best_patch : -1;
+    return res;
+}
+
+// one wave per query slot; 4 waves per block; candidates straight from global memory
 __global__ __launch_bounds__(256) void k_window_eval(WinArgs a, const int8_t *__restrict__ desc0,
                                                      const int *__restrict__ max_idx0,
                                                      const float *__restrict__ probs0,
@@ -268,150 +467,15 @@ __global__ __launch_bounds__(256) void k_window_eval(WinArgs a, const int8_t *__
     if (qslot < nsel) {
         const int patch1 = __builtin_amdgcn_readfirstlane(patches1[(long)pair * a.N + qslot]);
         const int x1 = patch1 / a.rows, y1 = patch1 % a.rows;
-        const int8_t *qd = desc1 + ((long)pair * cells + patch1) * kDescD;
-        const int8_t *d0 = desc0 + (long)pair * cells * kDescD;
-        const int *mi0 = max_idx0 + (long)pair * cells;
-        const float *pr0 = probs0 + (long)pair * cells;
-        // query: lane holds dword `lane` (bytes 4*lane .. 4*lane+3) for cooperative 256-D work,
-        // and every lane holds the first 64 bytes for the per-candidate 64-D dot.
-        const int qv = reinterpret_cast<const int *>(qd)[lane];
-        int q64[16];
-#pragma unroll
-        for (int v = 0; v < 16; v++) q64[v] = __shfl(qv, v, 64);
-        const int n2_256 = wave_sum(__builtin_amdgcn_sdot4(qv, qv, 0, false));
-        const int n2_64 = wave_sum(lane < 16 ? __builtin_amdgcn_sdot4(qv, qv, 0, false) : 0);
-
-        int xlo = max(x1 + a.shift_x - a.radius, 0), xhi = min(x1 + a.shift_x + a.radius, a.cols - 1);
-        int ylo = max(y1 + a.shift_y - a.radius, 0), yhi = min(y1 + a.shift_y + a.radius, a.rows - 1);
-        const int ny = yhi - ylo + 1;
-        const int ncand = (xhi >= xlo && yhi >= ylo) ? (xhi - xlo + 1) * ny : 0;
-
-        // as-built latch state (carried across 64-candidate chunks)
-        bool latched = false;
-        int n1f = 0;
-        // running best
-        float best_d = 0.0f;
-        int best_k = -1;
-        long long best_dot = 0, best_na = 1;
-        int best_patch = 0;
-
-        for (int base = 0; base < ncand; base += 64) {
-            const int k = base + lane;
-            int patch0 = 0;
-            bool valid = false;
-            if (k < ncand) {
-                const int x0 = xlo + k / ny, y0 = ylo + k % ny;
-                patch0 = x0 * a.rows + y0;
-                valid = mi0[patch0] != 64 && !((double)pr0[patch0] < a.prob_thr);
-            }
-            const int4 *cd = reinterpret_cast<const int4 *>(d0 + (long)patch0 * kDescD);
-            float d = __builtin_nanf("");
-            long long cdot = 0, cna = 0;
-            if (a.as_built) {
-                int dot_64 = 0, n1_64 = 0;
-                if (valid) dot64(cd, q64, dot_64, n1_64);
-                // resolve the latch: the first valid candidate (scan order) whose
-                // full 256-D norm is non-zero computes the full dot; candidates
-                // before it (all-zero descriptors) divide 0 by 0.
-                unsigned long long vm = __ballot(valid);
-                int f_lane = -1;   // lane of the latching candidate in this chunk
-                int dot_f = 0;
-                while (!latched && vm) {
-                    const int l = __ffsll((long long)vm) - 1;
-                    const int p0 = __shfl(patch0, l, 64);
-                    const int cv = reinterpret_cast<const int *>(d0 + (long)p0 * kDescD)[lane];
-                    const int full_n1 = wave_sum(__builtin_amdgcn_sdot4(cv, cv, 0, false));
-                    const int full_dot = wave_sum(__builtin_amdgcn_sdot4(cv, qv, 0, false));
-                    vm &= vm - 1;
-                    if (full_n1 != 0) {
-                        latched = true;
-                        n1f = full_n1;
-                        f_lane = l;
-                        dot_f = full_dot;
-                    } else if (lane == l) {
-                        d = (float)wrap_mul(full_dot, full_dot) / (float)wrap_mul(full_n1, n2_256);
-                    }
-                }
-                if (valid) {
-                    if (lane == f_lane) {
-                        d = (float)wrap_mul(dot_f, dot_f) / (float)wrap_mul(n1f, n2_256);
-                    } else if (latched && (f_lane < 0 || lane > f_lane)) {
-                        d = (float)wrap_mul(dot_64, dot_64) / (float)wrap_mul(n1f, n2_64);
-                    }
-                }
-                bool pass = valid && (double)d > a.thr_sq;
-                // first strict maximum in scan order: max d, ties -> smallest k
-                float bd = pass ? d : -__builtin_inff();
-                int bk = pass ? k : 0x7fffffff;
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) {
-                    float od = __shfl_xor(bd, o, 64);
-                    int ok = __shfl_xor(bk, o, 64);
-                    if (od > bd || (od == bd && ok < bk)) {
-                        bd = od;
-                        bk = ok;
-                    }
-                }
-                if (bk != 0x7fffffff && (best_k < 0 || bd > best_d)) {
-                    best_d = bd;
-                    best_k = bk;
-                    best_patch = __shfl(patch0, bk - base, 64);
-                }
-            } else {
-                int dot = 0, na = 0;
-                if (valid) {
-                    const int4 *q4 = reinterpret_cast<const int4 *>(qd);  // wave-uniform address
-#pragma unroll
-                    for (int v = 0; v < 16; v++) {
-                        int4 x = cd[v], y = q4[v];
-                        dot = __builtin_amdgcn_sdot4(x.x, y.x, dot, false);
-                        dot = __builtin_amdgcn_sdot4(x.y, y.y, dot, false);
-                        dot = __builtin_amdgcn_sdot4(x.z, y.z, dot, false);
-                        dot = __builtin_amdgcn_sdot4(x.w, y.w, dot, false);
-                        na = __builtin_amdgcn_sdot4(x.x, x.x, na, false);
-                        na = __builtin_amdgcn_sdot4(x.y, x.y, na, false);
-                        na = __builtin_amdgcn_sdot4(x.z, x.z, na, false);
-                        na = __builtin_amdgcn_sdot4(x.w, x.w, na, false);
-                    }
-                }
-                cdot = dot;
-                cna = na;
-                bool pass = valid && dot > 0 && na != 0 && n2_256 != 0 &&
-                            (unsigned __int128)(100ll * cdot * cdot) >
-                                (unsigned __int128)81 * (unsigned long long)(cna * (long long)n2_256);
-                long long bd = pass ? cdot : 0, bn = pass ? cna : 1;
-                int bk = pass ? k : -1;
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) {
-                    long long od = __shfl_xor(bd, o, 64), on = __shfl_xor(bn, o, 64);
-                    int ok = __shfl_xor(bk, o, 64);
-                    if (exact_better(od, on, ok, bd, bn, bk)) {
-                        bd = od;
-                        bn = on;
-                        bk = ok;
-                    }
-                }
-                if (bk >= 0 && exact_better(bd, bn, bk, best_dot, best_na, best_k)) {
-                    best_dot = bd;
-                    best_na = bn;
-                    best_k = bk;
-                    best_d = (float)((double)bd * (double)bd / ((double)bn * (double)n2_256));
-                    best_patch = __shfl(patch0, bk - base, 64);
-                }
-            }
-        }
-        if (best_k >= 0) {
-            res.found = 1;
-            res.bx = xlo + best_k / ny;
-            res.by = ylo + best_k % ny;
-            res.best_index = mi0[best_patch];
-            res.score = best_d;
-        }
+        const GlobalCands C = {desc0 + (long)pair * cells * kDescD, max_idx0 + (long)pair * cells,
+                               probs0 + (long)pair * cells, a.rows, a.prob_thr};
+        int bp;
+        res = eval_query(a, C, desc1 + ((long)pair * cells + patch1) * kDescD, x1, y1, lane, bp);
+        if (bp >= 0) res.best_index = C.mi0[bp];
     }
     if (lane == 0) out[(long)pair * a.N + qslot] = res;
 }
 
-// query-ordered compaction, cap max_matches (tracking_main.c:167-192)
 __global__ __launch_bounds__(1024) void k_window_compact(int N, int rows, int max_matches,
                                                          const QueryResult *__restrict__ qr,
                                                          const int *__restrict__ num_sel,
@@ -471,8 +535,10 @@ int launch_softmax(hipStream_t s, int batch, int cells, const float *scales, con
 int launch_top_n_select(hipStream_t s, int batch, int cells, const int *max_idx, const float *probs, int N,
                         int cap, int *num_sel, int *patches, int *indices, float *sel_probs, int *status) {
     MV_REQUIRE(batch > 0 && cells > 0 && N > 0 && cap > 0);
+    MV_PROF_BEGIN(s, "k_top_n_select");
     hipLaunchKernelGGL(k_top_n_select, dim3(batch), dim3(1024), 0, s, cells, max_idx, probs, N, cap, num_sel,
                        patches, indices, sel_probs, status);
+    MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     return MV_OK;
 }
@@ -507,8 +573,10 @@ extern "C" int mv_window_match_batch_dev(mv_context *ctx, const mv_window_params
                        probs0, desc1, num_selected, patches1, qr);
     MV_PROF_END(ctx->stream);
     MV_LAUNCH_CHECK();
+    MV_PROF_BEGIN(ctx->stream, "k_window_compact");
     hipLaunchKernelGGL(k_window_compact, dim3(batch), dim3(1024), 0, ctx->stream, N, rows, p->max_matches, qr,
                        num_selected, patches1, indices1, num_matches, points1, points2, query_of_match);
+    MV_PROF_END(ctx->stream);
     MV_LAUNCH_CHECK();
     return MV_OK;
 }

@@ -1,0 +1,117 @@
+#!/usr/bin/env python3
+"""Windowed int8 tracking front-end (tracking_main.c:84-194) at the
+full-resolution KITTI grid: 47 x 155 = 7285 cells, N = 1024 top-N queries, 9 x 9 windows,
+B pairs per launch.  One step = softmax(frame 0) + softmax(frame 1) + top-N(frame 1) +
+windowed match, as-intended or as-built semantics.  Prints one JSON line with pairs/s, the
+per-kernel averages (HIP events) and the HBM-roofline fraction of the window kernel and of
+the whole front-end against SURVEY §8d's 4.69 MB algorithmic bytes per pair.  GPU only."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "maveric-slam_amd"), os.path.join(ROOT, "oracle")):
+    sys.path.insert(0, p)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import mvtrack  # noqa: E402
+import synth  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--distinct", type=int, default=8, help="distinct synthetic pairs tiled over the batch")
+    ap.add_argument("--as-built", action="store_true")
+    ap.add_argument("--check", type=int, default=2)
+    args = ap.parse_args()
+    B, rows, cols, N = args.batch, 47, 155, 1024
+    cells = rows * cols
+    dev = torch.device("cuda", 0)
+    pairs = [synth.synth_window_pair(500 + k, rows=rows, cols=cols) for k in range(args.distinct)]
+    pick = [b % args.distinct for b in range(B)]
+    semi0 = torch.from_numpy(np.stack([pairs[k][0]["semi"] for k in pick])).to(dev)
+    semi1 = torch.from_numpy(np.stack([pairs[k][1]["semi"] for k in pick])).to(dev)
+    desc0 = torch.from_numpy(np.stack([pairs[k][0]["desc"] for k in pick])).to(dev)
+    desc1 = torch.from_numpy(np.stack([pairs[k][1]["desc"] for k in pick])).to(dev)
+    built = args.as_built
+    s = [mvtrack.scale_as_built(pairs[k][0]["semi_scale"]) if built else float(pairs[k][0]["semi_scale"])
+         for k in pick]
+    sc = torch.tensor(s, dtype=torch.float32, device=dev)
+    mi0 = torch.empty((B, cells), dtype=torch.int32, device=dev)
+    pr0 = torch.empty((B, cells), dtype=torch.float32, device=dev)
+    mi1, pr1 = torch.empty_like(mi0), torch.empty_like(pr0)
+    nv0 = torch.empty(B, dtype=torch.int32, device=dev)
+    nv1 = torch.empty(B, dtype=torch.int32, device=dev)
+    ns, st = (torch.empty(B, dtype=torch.int32, device=dev) for _ in range(2))
+    pa, ix = (torch.empty((B, N), dtype=torch.int32, device=dev) for _ in range(2))
+    sp = torch.empty((B, N), dtype=torch.float32, device=dev)
+    M = 150  # tracking_main.c's match cap
+    nm = torch.empty(B, dtype=torch.int32, device=dev)
+    p1 = torch.empty((B, M, 2), dtype=torch.float32, device=dev)
+    p2 = torch.empty((B, M, 2), dtype=torch.float32, device=dev)
+    prm = mvtrack.window_params(mvtrack.AS_BUILT if built else mvtrack.AS_INTENDED, max_matches=M)
+    ctx = mvtrack.Context(0)
+    ctx.set_stream(torch.cuda.current_stream())
+
+    def step():
+        ctx.softmax_batch(sc, semi0, mi0, pr0, nv0)
+        ctx.softmax_batch(sc, semi1, mi1, pr1, nv1)
+        ctx.top_n_select_batch(mi1, pr1, N, cells, ns, pa, ix, sp, st)
+        ctx.window_match_batch(prm, rows, cols, desc0, mi0, pr0, desc1, ns, pa, ix, nm, p1, p2)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    mvtrack.profile_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    mvtrack.profile_enable(False)
+    stages = {}
+    for k in ("k_softmax", "k_top_n_select", "k_window_eval", "k_window_compact"):
+        ms, n = mvtrack.profile_query(k)
+        stages[k] = round(ms / max(n, 1), 4)
+    checked = 0
+    if args.check:
+        import oracle
+
+        orc = oracle
+        for b in range(min(args.check, B)):
+            f0, f1 = pairs[pick[b]]
+            r = orc.track_window(f0, f1, as_built=built, N=N, cap=cells, max_matches=M)
+            n = int(nm[b])
+            assert n == len(r["query"]), (n, len(r["query"]))
+            assert (p1[b, :n].cpu().numpy() == r["points1"]).all() and (p2[b, :n].cpu().numpy() == r["points2"]).all()
+            checked += 1
+    alg_bytes = 2 * cells * (256 + 65) + N * 8  # SURVEY §8d per pair
+    step_s = el / args.steps
+    win_s = stages["k_window_eval"] * 1e-3
+    out = {
+        "metric": "windowed int8 front-end pairs/sec (softmax x2 + top-N + window match), 7285 cells, N=1024",
+        "value": round(B / step_s, 1), "unit": "pairs/s", "batch": B, "steps": args.steps,
+        "ms_per_step": round(step_s * 1e3, 4), "semantics": "as-built" if built else "as-intended",
+        "stages_ms": stages, "queries_selected_avg": float(ns.float().mean()), "matches_avg": float(nm.float().mean()),
+        "hbm_roofline": {"algorithmic_bytes_per_pair": alg_bytes,
+                         "frontend_GBs": round(alg_bytes * B / step_s / 1e9, 1),
+                         "frontend_frac": round(alg_bytes * B / step_s / 1e9 / HBM_PEAK_GBS, 4),
+                         "window_kernel_bytes_per_pair": 2 * cells * 256 + cells * 8 + N * 8,
+                         "window_kernel_GBs": round((2 * cells * 256 + cells * 8 + N * 8) * B / win_s / 1e9, 1),
+                         "peak_GBs": HBM_PEAK_GBS},
+        "checked_pairs": checked,
+    }
+    print(json.dumps(out), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
