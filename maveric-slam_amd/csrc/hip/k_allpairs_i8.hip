@@ -268,9 +268,13 @@ int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const i
     p += align_up(4 * rows, 256);
     float *rnb = (float *)p;
     const int nblk = (int)((rows + 255) / 256);
+    MV_PROF_BEGIN(s, "k_i8_norms");
     hipLaunchKernelGGL(k_i8_norms, dim3(nblk), dim3(256), 0, s, (long)rows, desc0, na, (float *)nullptr);
+    MV_PROF_END(s);
     MV_LAUNCH_CHECK();
+    MV_PROF_BEGIN(s, "k_i8_norms");
     hipLaunchKernelGGL(k_i8_norms, dim3(nblk), dim3(256), 0, s, (long)rows, desc1, nb, rnb);
+    MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     const long blocks = (long)batch * tiles_r * tiles_c;
     MV_REQUIRE(blocks < (1l << 31));
@@ -279,8 +283,10 @@ int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const i
                        desc1, rnb, part);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
+    MV_PROF_BEGIN(s, "k_i8_resolve");
     hipLaunchKernelGGL(k_i8_resolve, dim3((cap + 255) / 256, batch), dim3(256), 0, s, tiles_c, cap, n0, n1, desc0,
                        desc1, na, nb, part, match_idx, match_dot);
+    MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     return MV_OK;
 }
