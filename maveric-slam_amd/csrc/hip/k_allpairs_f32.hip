@@ -47,7 +47,10 @@
 
 namespace {
 
-constexpr int BM = 128, BN = 64, BK = 128, KD = 256, KS = KD / BK, NT = 256, NW = NT / 64, RW = BM / NW;
+#ifndef AP_NW
+#define AP_NW 4  // waves per block (32 rows each): 4 -> two blocks per CU, 8 -> one
+#endif
+constexpr int NW = AP_NW, NT = 64 * NW, BM = 32 * NW, BN = 64, BK = 128, KD = 256, KS = KD / BK, RW = BM / NW;
 constexpr int NBUF = 4;  // ring slots: two column tiles of KS = 2 slices
 // timing experiments only (wrong results): drop the DMA waits / barriers / MFMAs / DMAs
 #ifndef AP_EXP_NOWAIT
@@ -77,7 +80,7 @@ constexpr int SL_BYTES = BN * SL_ROW;            // one B slice: 16 KiB
 constexpr int DMA_PER_SLICE = SL_BYTES / 1024 / NW;  // 1-KiB DMA instructions per wave per slice
 constexpr float SCALE = 16384.f;                 // 2^14: |a_k| < 2 -> |2^14 a_k| < 2^15 < 65504
 static_assert(KS == 2 && NBUF == 2 * KS, "the loop body covers two column tiles = NBUF slices");
-static_assert(RW == 32 && DMA_PER_SLICE == 4, "one wave per 32 rows (32x32 MFMA), 4 DMA per slice");
+static_assert(RW == 32 && (NW == 4 || NW == 8), "one wave per 32 rows (32x32 MFMA), 4 or 8 waves");
 // LDS map (ONE array -- a second __shared__ object can de-pipeline the DMA), byte offsets
 constexpr int OFF_STAGE = 0;                     // [NBUF][64 B rows][256 B]
 constexpr int OFF_TRIP = NBUF * SL_BYTES;        // [256] {m1, i1, m2}
@@ -259,7 +262,7 @@ __global__ __launch_bounds__(256) void k_ap_split(int batch, int cap, const int 
     }
 }
 
-__global__ __launch_bounds__(NT, 2) void k_ap_match(int tiles_r, int cap, const int *__restrict__ n0v,
+__global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, const int *__restrict__ n0v,
                                                     const int *__restrict__ n1v, const float *__restrict__ desc0,
                                                     const float *__restrict__ desc1, const char *__restrict__ h1,
                                                     const float *__restrict__ nrm1, const int *__restrict__ bad,
@@ -331,25 +334,26 @@ __global__ __launch_bounds__(NT, 2) void k_ap_match(int tiles_r, int cap, const 
     //      instruction; lane l lands at row (l >> 4), chunk position l & 15 and fetches
     //      source chunk (l & 15) ^ (row & 15) of that row (256-B rows: 16 chunks) ----
     const int wu = __builtin_amdgcn_readfirstlane(w);
-    const int dr = wu * 16 + (lane >> 4);  // (dr & 15) < 4, so (dr + 4 g) & 15 = (dr & 15) ^ 4 g
+    constexpr int RPW = BN / NW;  // slice rows each wave DMAs: 16 (4 waves) or 8 (8 waves)
+    const int dr = wu * RPW + (lane >> 4);  // (dr & 4) == 0, so (dr + 4 g) & 15 = (dr & 15) ^ 4 g
     const unsigned dcb = (unsigned)((lane & 15) ^ (dr & 15)) * 16;
-    unsigned oB0, oB1, oB2, oB3;
+    unsigned oB[RPW / 4];
     const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char *)(lds + OFF_STAGE);
-    const unsigned dst_w = lds_base + (unsigned)(wu * 16 * SL_ROW);
+    const unsigned dst_w = lds_base + (unsigned)(wu * RPW * SL_ROW);
 #define AP_STAGE(SLOT, KSI)                                                                  \
     do {                                                                                     \
-        glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES>(SB, oB0, dst_w);                           \
-        glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES + 4 * SL_ROW>(SB, oB1, dst_w);              \
-        glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES + 8 * SL_ROW>(SB, oB2, dst_w);              \
-        glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES + 12 * SL_ROW>(SB, oB3, dst_w);             \
+        glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES>(SB, oB[0], dst_w);                         \
+        glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES + 4 * SL_ROW>(SB, oB[1], dst_w);            \
+        if constexpr (RPW == 16) {                                                           \
+            glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES + 8 * SL_ROW>(SB, oB[RPW / 4 - 2], dst_w);  \
+            glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES + 12 * SL_ROW>(SB, oB[RPW / 4 - 1], dst_w); \
+        }                                                                                    \
     } while (0)
 #define AP_TILE_OFFSETS(TC)                                                                  \
     do {                                                                                     \
         const int nb_ = (TC) * BN + dr;                                                      \
-        oB0 = (unsigned)min(nb_, n1 - 1) * ROW_BYTES + dcb;                                  \
-        oB1 = (unsigned)min(nb_ + 4, n1 - 1) * ROW_BYTES + (dcb ^ 64u);                      \
-        oB2 = (unsigned)min(nb_ + 8, n1 - 1) * ROW_BYTES + (dcb ^ 128u);                     \
-        oB3 = (unsigned)min(nb_ + 12, n1 - 1) * ROW_BYTES + (dcb ^ 192u);                    \
+        _Pragma("unroll") for (int g_ = 0; g_ < RPW / 4; g_++)                               \
+            oB[g_] = (unsigned)min(nb_ + 4 * g_, n1 - 1) * ROW_BYTES + (dcb ^ (64u * g_));   \
     } while (0)
     AP_TILE_OFFSETS(0);
 
