@@ -223,42 +223,49 @@ __device__ __forceinline__ float exact_dot(const float *__restrict__ a, const fl
 }
 
 // ---- k_ap_split: frame 1 only.  32 lanes per row, 8 consecutive floats per lane (two
-//      16-B loads, one 16-B store); a 256-thread block converts 8 rows per iteration and
+//      16-B loads, one 16-B store); a 256-thread block converts 16 rows per iteration and
 //      strides over the batch (rows >= n1 are never read downstream) ----
-constexpr int SPLIT_ROWS = 8;
+constexpr int SPLIT_ROWS = 16;  // rows per block iteration: 8 row groups x 2
+__device__ __forceinline__ void split_row(long R, int live, int pair, int sub, const float4 &x, const float4 &y,
+                                          char *__restrict__ h1, float *__restrict__ nrm1, int *__restrict__ bad) {
+    const int out = (int)!(fabsf(x.x) < 2.f) | (int)!(fabsf(x.y) < 2.f) | (int)!(fabsf(x.z) < 2.f) |
+                    (int)!(fabsf(x.w) < 2.f) | (int)!(fabsf(y.x) < 2.f) | (int)!(fabsf(y.y) < 2.f) |
+                    (int)!(fabsf(y.z) < 2.f) | (int)!(fabsf(y.w) < 2.f);  // NaN: out of range
+    float q = fmaf(x.x, x.x, fmaf(x.y, x.y, fmaf(x.z, x.z, x.w * x.w)));
+    q = fmaf(y.x, y.x, fmaf(y.y, y.y, fmaf(y.z, y.z, fmaf(y.w, y.w, q))));
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) q += __shfl_xor(q, o, 64);  // the row's 32 lanes
+    if (live) {
+        const f16x8 h = {(_Float16)(x.x * SCALE), (_Float16)(x.y * SCALE), (_Float16)(x.z * SCALE),
+                         (_Float16)(x.w * SCALE), (_Float16)(y.x * SCALE), (_Float16)(y.y * SCALE),
+                         (_Float16)(y.z * SCALE), (_Float16)(y.w * SCALE)};  // exact 2^14 scale, RNE
+        *reinterpret_cast<f16x8 *>(h1 + R * ROW_BYTES + sub * 16) = h;
+        if (out) bad[pair] = 1;
+        if (sub == 0) nrm1[R] = q;
+    }
+}
 __global__ __launch_bounds__(256) void k_ap_split(int batch, int cap, const int *__restrict__ n1v,
                                                   const float *__restrict__ desc1, char *__restrict__ h1,
                                                   float *__restrict__ nrm1, int *__restrict__ bad) {
     const long rows = (long)batch * cap;
     const int sub = threadIdx.x & 31, rl = threadIdx.x >> 5;
+    typedef float f32x4v __attribute__((ext_vector_type(4)));
     for (long R0 = (long)blockIdx.x * SPLIT_ROWS; R0 < rows; R0 += (long)gridDim.x * SPLIT_ROWS) {
-        const long R = R0 + rl;
-        const int pair = (int)(R / cap), r = (int)(R % cap);
-        const bool live = R < rows && r < n1v[min(pair, batch - 1)];
-        float4 x = make_float4(0.f, 0.f, 0.f, 0.f), y = x;
-        if (live) {
-            const float *src = desc1 + R * KD + sub * 8;
-            typedef float f32x4v __attribute__((ext_vector_type(4)));
-            const f32x4v u = __builtin_nontemporal_load(reinterpret_cast<const f32x4v *>(src));
-            const f32x4v v = __builtin_nontemporal_load(reinterpret_cast<const f32x4v *>(src + 4));
-            x = make_float4(u[0], u[1], u[2], u[3]);
-            y = make_float4(v[0], v[1], v[2], v[3]);
-        }
-        const int out = (int)!(fabsf(x.x) < 2.f) | (int)!(fabsf(x.y) < 2.f) | (int)!(fabsf(x.z) < 2.f) |
-                        (int)!(fabsf(x.w) < 2.f) | (int)!(fabsf(y.x) < 2.f) | (int)!(fabsf(y.y) < 2.f) |
-                        (int)!(fabsf(y.z) < 2.f) | (int)!(fabsf(y.w) < 2.f);  // NaN: out of range
-        float q = fmaf(x.x, x.x, fmaf(x.y, x.y, fmaf(x.z, x.z, x.w * x.w)));
-        q = fmaf(y.x, y.x, fmaf(y.y, y.y, fmaf(y.z, y.z, fmaf(y.w, y.w, q))));
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) q += __shfl_xor(q, o, 64);  // the row's 32 lanes
-        if (live) {
-            const f16x8 h = {(_Float16)(x.x * SCALE), (_Float16)(x.y * SCALE), (_Float16)(x.z * SCALE),
-                             (_Float16)(x.w * SCALE), (_Float16)(y.x * SCALE), (_Float16)(y.y * SCALE),
-                             (_Float16)(y.z * SCALE), (_Float16)(y.w * SCALE)};  // exact 2^14 scale, RNE
-            *reinterpret_cast<f16x8 *>(h1 + R * ROW_BYTES + sub * 16) = h;
-            if (out) bad[pair] = 1;
-            if (sub == 0) nrm1[R] = q;
-        }
+        // two rows per lane group, all four 16-B loads issued before any use; rows past n1
+        // are inside the cap stride, so they are read unconditionally and only not stored
+        const long Ra = R0 + rl, Rb = R0 + 8 + rl;
+        const long ca = Ra < rows ? Ra : rows - 1, cb = Rb < rows ? Rb : rows - 1;
+        const f32x4v u0 = __builtin_nontemporal_load(reinterpret_cast<const f32x4v *>(desc1 + ca * KD + sub * 8));
+        const f32x4v v0 = __builtin_nontemporal_load(reinterpret_cast<const f32x4v *>(desc1 + ca * KD + sub * 8 + 4));
+        const f32x4v u1 = __builtin_nontemporal_load(reinterpret_cast<const f32x4v *>(desc1 + cb * KD + sub * 8));
+        const f32x4v v1 = __builtin_nontemporal_load(reinterpret_cast<const f32x4v *>(desc1 + cb * KD + sub * 8 + 4));
+        const int pa = (int)(ca / cap), pb = (int)(cb / cap);
+        const int la = Ra < rows && (int)(ca - (long)pa * cap) < n1v[pa];
+        const int lb = Rb < rows && (int)(cb - (long)pb * cap) < n1v[pb];
+        split_row(ca, la, pa, sub, make_float4(u0[0], u0[1], u0[2], u0[3]), make_float4(v0[0], v0[1], v0[2], v0[3]),
+                  h1, nrm1, bad);
+        split_row(cb, lb, pb, sub, make_float4(u1[0], u1[1], u1[2], u1[3]), make_float4(v1[0], v1[1], v1[2], v1[3]),
+                  h1, nrm1, bad);
     }
 }
 
