@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--check", type=int, default=1)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
     B, n, D = args.batch, args.kp, 256
     dev = torch.device("cuda", 0)
@@ -77,6 +78,29 @@ def main():
                              "peak_TOPS": I8_PEAK_TOPS,
                              "frac": round(ops / scr / 1e12 / I8_PEAK_TOPS, 4) if scr else None},
            "checked_pairs": checked}
+    if args.cpu_seconds > 0:  # the oracle's C restatement (exact cosine, sequential int MACs) on host threads
+        import concurrent.futures as cf
+
+        import oracle
+
+        a0, a1 = d0[0].cpu().numpy(), d1[0].cpu().numpy()
+        threads = max(1, min(16, os.cpu_count() or 1))
+        deadline = time.perf_counter() + args.cpu_seconds
+
+        def worker(_):
+            c = 0
+            while time.perf_counter() < deadline:
+                oracle.allpairs_i8(a0, a1)
+                c += 1
+            return c
+
+        t0 = time.perf_counter()
+        with cf.ThreadPoolExecutor(threads) as ex:
+            total = sum(ex.map(worker, range(threads)))
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(total / dt, 2), "unit": "pairs/s", "cores": threads, "kind": "port",
+                               "sample": "%d pairs of %dx%dx256 int8 in %.1f s on %d host threads"
+                                         % (total, n, n, dt, threads)}
     print(json.dumps(out), flush=True)
     ctx.close()
 

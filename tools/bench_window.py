@@ -23,6 +23,33 @@ import synth  # noqa: E402
 HBM_PEAK_GBS = 8000.0
 
 
+def cpu_baseline(pairs, built, N, cells, seconds):
+    """oracle/mv_oracle.c's restatement of tracking_main.c:84-194 (softmax, top-N, window
+    loop; the reference's own loop cannot be built here -- SURVEY F6) on host threads."""
+    import concurrent.futures as cf
+
+    import oracle
+
+    threads = max(1, min(16, os.cpu_count() or 1))
+    deadline = time.perf_counter() + seconds
+
+    def worker(k):
+        f0, f1 = pairs[k % len(pairs)]
+        done = 0
+        while time.perf_counter() < deadline:
+            oracle.track_window(f0, f1, as_built=built, N=N, cap=cells, max_matches=150)
+            done += 1
+        return done
+
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(threads) as ex:
+        total = sum(ex.map(worker, range(threads)))
+    dt = time.perf_counter() - t0
+    return {"value": round(total / dt, 1), "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": "%d pairs (%d cells, N=%d) through the oracle's C restatement in %.1f s on %d host threads"
+                      % (total, cells, N, dt, threads)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1024)
@@ -31,6 +58,7 @@ def main():
     ap.add_argument("--distinct", type=int, default=8, help="distinct synthetic pairs tiled over the batch")
     ap.add_argument("--as-built", action="store_true")
     ap.add_argument("--check", type=int, default=2)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
     B, rows, cols, N = args.batch, 47, 155, 1024
     cells = rows * cols
@@ -109,6 +137,8 @@ def main():
                          "peak_GBs": HBM_PEAK_GBS},
         "checked_pairs": checked,
     }
+    if args.cpu_seconds > 0:
+        out["cpu_baseline"] = cpu_baseline(pairs, built, N, cells, args.cpu_seconds)
     print(json.dumps(out), flush=True)
     ctx.close()
 
