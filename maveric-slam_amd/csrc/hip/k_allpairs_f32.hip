@@ -284,7 +284,7 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
 
     const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int pair = L / tiles_r, tr = L % tiles_r;
-    const int n0 = n0v[pair], n1 = n1v[pair];
+    const int n0 = min(max(n0v[pair], 0), cap), n1 = min(max(n1v[pair], 0), cap);
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int row0 = tr * BM;
     int *oidx = match_idx + (size_t)pair * cap + row0;

@@ -6,12 +6,12 @@
 // (cos > MATCH_THRESHOLD 0.9); the kept j is the FIRST maximiser of
 // dot^2 / |b|^2 (the cosine at fixed query).  Integer-exact.
 //
-//   k_i8_norms    |x|^2 of every row of both frames (v_dot4)
-//   k_i8_screen   D = A . B^T with v_mfma_i32_32x32x32_i8 (exact int32), 128x128
-//                 tile, the whole K = 256 panel staged once in LDS (2 x 32 KiB);
-//                 epilogue f = dot * rsqrt|b|^2 for dot > 0, per-row (max1, idx1, max2)
-//   k_i8_resolve  exact re-score of every candidate with f >= M (1 - 1e-5):
-//                 integer dot, u128 cross-multiplied comparison, exact threshold.
+//   k_i8_norms    |b|^2 and rsqrt|b|^2 of every frame-1 row (v_dot4)
+//   k_i8_match    D = A . B^T with v_mfma_i32_32x32x32_i8 (exact int32), A in
+//                 registers, B streamed through an LDS ring, fused per-row top-2 of
+//                 f = dot * rsqrt|b|^2, then the exact decision per row (one integer
+//                 dot + u128 threshold, or an exact re-score when the top-2 is within
+//                 1e-5).
 // Per pair at 2048 kp: 2 * 2048^2 * 256 = 2.147 GOP on 2 x 512 KiB; MFMA-int8 bound.
 #include <math.h>
 
@@ -19,22 +19,10 @@
 
 namespace {
 
-constexpr int BM = 128, BN = 128, KD = 256;
-constexpr int LDR = KD + 16;      // bytes per staged row (272 B: conflict-free ds_read_b128)
-constexpr int LDC = BM + 4;       // floats, transposed score tile
-constexpr int STAGE_BYTES = 2 * BM * LDR;
-constexpr int C_BYTES = BN * LDC * 4;
-constexpr int LDS_BYTES = STAGE_BYTES > C_BYTES ? STAGE_BYTES : C_BYTES;
+constexpr int KD = 256;
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
-
-struct Partial {
-    float max1;
-    int idx1;
-    float max2;
-    float pad;
-};
 
 __device__ __forceinline__ int xcd_remap(int b, int total) {
     const int q = total / 8, r = total % 8, x = b % 8;
@@ -59,131 +47,6 @@ __global__ __launch_bounds__(256) void k_i8_norms(long rows, const int8_t *__res
     if (rnrm) rnrm[r] = s > 0 ? 1.0f / sqrtf((float)s) : 0.f;
 }
 
-__global__ __launch_bounds__(256, 2) void k_i8_screen(int tiles_r, int tiles_c, int cap, const int *__restrict__ n0v,
-                                                      const int *__restrict__ n1v, const int8_t *__restrict__ desc0,
-                                                      const int8_t *__restrict__ desc1,
-                                                      const float *__restrict__ rnb, Partial *__restrict__ part) {
-    __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
-    char *As = lds;
-    char *Bs = lds + BM * LDR;
-    const int per_pair = tiles_r * tiles_c;
-    const int L = xcd_remap(blockIdx.x, gridDim.x);
-    const int pair = L / per_pair, tile = L % per_pair;
-    const int tr = tile / tiles_c, tc = tile % tiles_c;
-    const int n0 = n0v[pair], n1 = n1v[pair];
-    if (tr * BM >= n0 || tc * BN >= n1) return;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
-    const int8_t *A = desc0 + (size_t)pair * cap * KD;
-    const int8_t *B = desc1 + (size_t)pair * cap * KD;
-    // stage the full K panels: 128 rows x 256 B each, 16 lanes per row
-#pragma unroll
-    for (int it = 0; it < 8; it++) {
-        const int row = it * 16 + (t >> 4), ch = t & 15;
-        const int ra = min(tr * BM + row, n0 - 1), rb = min(tc * BN + row, n1 - 1);
-        int4 xa = *reinterpret_cast<const int4 *>(A + (size_t)ra * KD + ch * 16);
-        int4 xb = *reinterpret_cast<const int4 *>(B + (size_t)rb * KD + ch * 16);
-        *reinterpret_cast<int4 *>(As + row * LDR + ch * 16) = xa;
-        *reinterpret_cast<int4 *>(Bs + row * LDR + ch * 16) = xb;
-    }
-    __syncthreads();
-    i32x16 acc[2][2];
-#pragma unroll
-    for (int m = 0; m < 2; m++)
-#pragma unroll
-        for (int n = 0; n < 2; n++)
-#pragma unroll
-            for (int g = 0; g < 16; g++) acc[m][n][g] = 0;
-    const int fr = lane & 31, fh = lane >> 5;
-#pragma unroll
-    for (int kk = 0; kk < KD / 32; kk++) {
-        i32x4 a[2], b[2];
-#pragma unroll
-        for (int m = 0; m < 2; m++) {
-            a[m] = *reinterpret_cast<const i32x4 *>(As + (wr * 64 + m * 32 + fr) * LDR + kk * 32 + fh * 16);
-            b[m] = *reinterpret_cast<const i32x4 *>(Bs + (wc * 64 + m * 32 + fr) * LDR + kk * 32 + fh * 16);
-        }
-#pragma unroll
-        for (int m = 0; m < 2; m++)
-#pragma unroll
-            for (int n = 0; n < 2; n++) acc[m][n] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[m], b[n], acc[m][n], 0, 0, 0);
-    }
-    __syncthreads();
-    float *Ct = reinterpret_cast<float *>(lds);
-    const float *rb_pair = rnb + (size_t)pair * cap;
-#pragma unroll
-    for (int n = 0; n < 2; n++) {
-        const int col = wc * 64 + n * 32 + fr;
-        const int gcol = min(tc * BN + col, n1 - 1);
-        const float rn = rb_pair[gcol];
-#pragma unroll
-        for (int m = 0; m < 2; m++)
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int row = wr * 64 + m * 32 + 8 * q + 4 * fh;
-                float4 v;
-                int d0 = acc[m][n][4 * q + 0], d1 = acc[m][n][4 * q + 1], d2 = acc[m][n][4 * q + 2],
-                    d3 = acc[m][n][4 * q + 3];
-                v.x = d0 > 0 ? (float)d0 * rn : -__builtin_inff();
-                v.y = d1 > 0 ? (float)d1 * rn : -__builtin_inff();
-                v.z = d2 > 0 ? (float)d2 * rn : -__builtin_inff();
-                v.w = d3 > 0 ? (float)d3 * rn : -__builtin_inff();
-                *reinterpret_cast<float4 *>(Ct + col * LDC + row) = v;
-            }
-    }
-    __syncthreads();
-    const int r = t & (BM - 1), half = t >> 7;
-    const int cvalid = min(BN, n1 - tc * BN);
-    float m1 = -__builtin_inff(), m2 = -__builtin_inff();
-    int i1 = -1;
-    const int cb = half * 64, ce = min(cb + 64, cvalid);
-    for (int c = cb; c < ce; c++) {
-        const float v = Ct[c * LDC + r];
-        if (v > m1) {
-            m2 = m1;
-            m1 = v;
-            i1 = tc * BN + c;
-        } else if (v > m2) {
-            m2 = v;
-        }
-    }
-    __syncthreads();
-    float *mx = Ct;
-    if (half == 1) {
-        mx[r] = m1;
-        reinterpret_cast<int *>(mx)[BM + r] = i1;
-        mx[2 * BM + r] = m2;
-    }
-    __syncthreads();
-    if (half == 0) {
-        const float u1 = mx[r], u2 = mx[2 * BM + r];
-        const int ui = reinterpret_cast<int *>(mx)[BM + r];
-        if (u1 > m1) {
-            m2 = fmaxf(m1, u2);
-            m1 = u1;
-            i1 = ui;
-        } else {
-            m2 = fmaxf(m2, u1);
-        }
-        const int grow = tr * BM + r;
-        if (grow < n0) part[((size_t)pair * cap + grow) * tiles_c + tc] = Partial{m1, i1, m2, 0.f};
-    }
-}
-
-__device__ __forceinline__ int exact_dot_i8(const int8_t *a, const int8_t *b) {
-    const int4 *p = reinterpret_cast<const int4 *>(a);
-    const int4 *q = reinterpret_cast<const int4 *>(b);
-    int s = 0;
-#pragma unroll
-    for (int v = 0; v < 16; v++) {
-        int4 x = p[v], y = q[v];
-        s = __builtin_amdgcn_sdot4(x.x, y.x, s, false);
-        s = __builtin_amdgcn_sdot4(x.y, y.y, s, false);
-        s = __builtin_amdgcn_sdot4(x.z, y.z, s, false);
-        s = __builtin_amdgcn_sdot4(x.w, y.w, s, false);
-    }
-    return s;
-}
-
 // candidate (dot, nb, j) strictly better than current best?  max dot^2/nb, ties -> lower j
 __device__ __forceinline__ bool better(long long d, long long nb, int j, long long bd, long long bn, int bj) {
     if (bj < 0) return true;
@@ -192,55 +55,424 @@ __device__ __forceinline__ bool better(long long d, long long nb, int j, long lo
     return l > r || (l == r && j < bj);
 }
 
-__global__ __launch_bounds__(256) void k_i8_resolve(int tiles_c, int cap, const int *__restrict__ n0v,
-                                                    const int *__restrict__ n1v, const int8_t *__restrict__ desc0,
-                                                    const int8_t *__restrict__ desc1, const int *__restrict__ na_v,
-                                                    const int *__restrict__ nb_v, const Partial *__restrict__ part,
-                                                    int *__restrict__ match_idx, int *__restrict__ match_dot) {
-    const int pair = blockIdx.y;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= cap) return;
-    const int n0 = n0v[pair], n1 = n1v[pair];
-    int best = -1;
-    long long bd = 0, bn = 1;
-    if (i < n0 && n1 > 0) {
-        const long long na = na_v[(size_t)pair * cap + i];
-        const int8_t *a = desc0 + ((size_t)pair * cap + i) * KD;
-        const int8_t *B = desc1 + (size_t)pair * cap * KD;
-        const int *nb = nb_v + (size_t)pair * cap;
-        const Partial *p = part + ((size_t)pair * cap + i) * tiles_c;
-        const int tiles = (n1 + BN - 1) / BN;
-        float M = -__builtin_inff();
-        for (int tt = 0; tt < tiles; tt++) M = fmaxf(M, p[tt].max1);
-        if (na > 0 && M > 0.f) {
-            const float win = M * (1.0f - 1e-5f);
-            for (int tt = 0; tt < tiles; tt++) {
-                const Partial q = p[tt];
-                int jb = tt * BN, je = jb;
-                if (q.max2 >= win)
-                    je = min(jb + BN, n1);
-                else if (q.max1 >= win) {
-                    jb = q.idx1;
-                    je = jb + 1;
+// ---------------------------------------------------------------------------
+// k_i8_match: the fp16 kernel's structure on the int8 matrix cores.  A 256-thread
+// block (4 waves x 32 rows, two blocks per CU) owns 128 query rows of one pair; the
+// wave's 32 rows x 256 int8 live in 32 VGPRs; frame 1 streams in 64-column tiles
+// (16 KiB, the whole K) through a 4-slot LDS ring by global_load_lds (3 tiles in
+// flight), 16-B chunks XOR-swizzled by row.  v_mfma_i32_32x32x32_i8 gives the EXACT
+// integer dot; each tile is folded (beside the next tile's MFMAs) as
+// f = dot * rsqrt|b|^2 into a lane-local (max1, idx1, max2) per row.  f orders like
+// dot^2/|b|^2 for dot > 0 with a relative error < 3e-7, so when the runner-up is
+// below M (1 - 1e-5) the screen maximiser is the exact one and one integer dot +
+// the u128 threshold decide; otherwise one wave re-scores the row exactly.
+// ---------------------------------------------------------------------------
+// timing experiments only (wrong results): I8_EXP_NOFOLD folds 1 of 16 rows per lane,
+// I8_EXP_NOEXACT skips the per-row exact decision, I8_EXP_NODMA / NOBAR / NOMFMA drop the
+// tile DMA / the per-tile barrier / the matrix instructions
+#ifdef I8_EXP_NODMA
+#define I8_NODMA 1
+#else
+#define I8_NODMA 0
+#endif
+#ifdef I8_EXP_NOBAR
+#define I8_NOBAR 1
+#else
+#define I8_NOBAR 0
+#endif
+#ifdef I8_EXP_NOMFMA
+#define I8_NOMFMA 1
+#else
+#define I8_NOMFMA 0
+#endif
+#ifdef I8_EXP_NOFOLD
+#define I8_FOLD_ROWS 1
+#else
+#define I8_FOLD_ROWS 16
+#endif
+constexpr int M_NW = 4, M_NT = 64 * M_NW, M_BM = 32 * M_NW, M_BN = 64, M_NBUF = 4;
+constexpr int M_TILE = M_BN * KD;                 // 16 KiB: one column tile, whole K
+constexpr int M_SLOT = M_TILE + M_BN * 4;         // + the tile's 64 rsqrt|b|^2
+constexpr int M_OFF_TRIP = M_NBUF * M_SLOT;       // [BM] {m1, i1, m2}
+constexpr int M_OFF_NA = M_OFF_TRIP + M_BM * 12;  // [BM] i32 |a|^2
+constexpr int M_LDS = M_OFF_NA + M_BM * 4;
+
+#pragma clang diagnostic ignored "-Winline-asm"
+template <int KOFF, int DOFF>
+__device__ __forceinline__ void glds16_i8(const void *sbase, unsigned voff, unsigned lds_byte) {
+    unsigned tmp;
+    asm volatile(
+        "v_add_u32 %0, %4, %1\n\t"
+        "s_add_u32 m0, %3, %5\n\t"
+        "global_load_lds_dwordx4 %0, %2"
+        : "=&v"(tmp)
+        : "v"(voff), "s"(sbase), "s"(lds_byte), "i"(KOFF), "i"(DOFF)
+        : "memory", "m0", "scc");
+}
+template <int DOFF>
+__device__ __forceinline__ void glds4_i8(const void *sbase, unsigned voff, unsigned lds_byte) {
+    asm volatile(
+        "s_add_u32 m0, %2, %3\n\t"
+        "global_load_lds_dword %0, %1"
+        :
+        : "v"(voff), "s"(sbase), "s"(lds_byte), "i"(DOFF)
+        : "memory", "m0", "scc");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm_i8() {
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+// (f & keep) | tag in one instruction
+__device__ __forceinline__ float tag_i8(float f, unsigned keep, unsigned tag) {
+    float r;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(keep), "s"(tag));
+    return r;
+}
+// top-2 of {m1, m2, a, b} given m1 >= m2: m1' = max3(m1, a, b), m2' = max(m2, med3(m1, a, b))
+__device__ __forceinline__ void fold3_i8(float a, float b, float &m1, float &m2) {
+    float md;
+    asm("v_med3_f32 %0, %1, %2, %3" : "=v"(md) : "v"(m1), "v"(a), "v"(b));
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m1) : "v"(m1), "v"(a), "v"(b));
+    asm("v_max_f32 %0, %1, %2" : "=v"(m2) : "v"(m2), "v"(md));
+}
+
+__global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, const int *__restrict__ n0v,
+                                                      const int *__restrict__ n1v, const int8_t *__restrict__ desc0,
+                                                      const int8_t *__restrict__ desc1, const int *__restrict__ nb_v,
+                                                      const float *__restrict__ rnb_v, int *__restrict__ match_idx,
+                                                      int *__restrict__ match_dot) {
+    __shared__ __attribute__((aligned(16))) char lds[M_LDS];
+    float *trip = reinterpret_cast<float *>(lds + M_OFF_TRIP);
+    int *na_s = reinterpret_cast<int *>(lds + M_OFF_NA);
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int pair = L / tiles_r, tr = L % tiles_r;
+    const int n0 = min(max(n0v[pair], 0), cap), n1 = min(max(n1v[pair], 0), cap);
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int row0 = tr * M_BM;
+    int *oidx = match_idx + (size_t)pair * cap + row0;
+    int *odot = match_dot + (size_t)pair * cap + row0;
+    if (t < M_BM && row0 + t < cap && (row0 + t >= n0 || n1 <= 0)) {
+        oidx[t] = -1;
+        odot[t] = 0;
+    }
+    if (row0 >= n0 || n1 <= 0) return;
+    const int8_t *A = desc0 + (size_t)pair * cap * KD;
+    const int8_t *B = desc1 + (size_t)pair * cap * KD;
+    const float *rnb = rnb_v + (size_t)pair * cap;
+    const int *nb = nb_v + (size_t)pair * cap;
+    const int ntc = (n1 + M_BN - 1) / M_BN;
+
+    // ---- A: 32 rows x 256 int8 in 32 VGPRs (i8 MFMA A operand: lane l holds row l & 31,
+    //      k = 32 s + 16 (l >> 5) .. +15 at k32 step s); |a|^2 along the way ----
+    const int fr = lane & 31, fh = lane >> 5;
+    i32x4 aI[KD / 32];
+    int na_r;  // |a|^2 of row w*32 + fr
+    {
+        const int8_t *arow = A + (size_t)min(row0 + w * 32 + fr, n0 - 1) * KD + fh * 16;
+#pragma unroll
+        for (int s2 = 0; s2 < KD / 32; s2++) aI[s2] = *reinterpret_cast<const i32x4 *>(arow + s2 * 32);
+        int q = 0;
+#pragma unroll
+        for (int s2 = 0; s2 < KD / 32; s2++)
+#pragma unroll
+            for (int u = 0; u < 4; u++) q = __builtin_amdgcn_sdot4(aI[s2][u], aI[s2][u], q, false);
+        q += __shfl_xor(q, 32, 64);
+        if (fh == 0) na_s[w * 32 + fr] = q;
+        na_r = q;
+    }
+
+    // ---- B DMA: wave w fills rows w*16 .. +15 of a tile, 4 rows (1 KiB) per instruction;
+    //      lane l -> row (l >> 4), chunk position l & 15, source chunk (l & 15) ^ (row & 15) ----
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    const int dr = wu * 16 + (lane >> 4);
+    const unsigned dcb = (unsigned)((lane & 15) ^ (dr & 15)) * 16;
+    unsigned oB[4], oR;
+    const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char *)lds;
+    const unsigned dst_w = lds_base + (unsigned)(wu * 16 * KD);
+    // + every wave copies the tile's 64 rsqrt|b|^2 (identical bytes) so that all waves
+    //   count the same 5 loads per tile; compiler-visible loads here would make the
+    //   compiler's vmcnt waits drain the whole DMA ring
+#define I8_STAGE(SLOT)                                                                       \
+    do {                                                                                     \
+        glds16_i8<0, (SLOT) * M_SLOT>(B, oB[0], dst_w);                                      \
+        glds16_i8<0, (SLOT) * M_SLOT + 4 * KD>(B, oB[1], dst_w);                             \
+        glds16_i8<0, (SLOT) * M_SLOT + 8 * KD>(B, oB[2], dst_w);                             \
+        glds16_i8<0, (SLOT) * M_SLOT + 12 * KD>(B, oB[3], dst_w);                            \
+        glds4_i8<(SLOT) * M_SLOT + M_TILE>(rnb, oR, lds_base);                               \
+    } while (0)
+#define I8_OFFSETS(TC)                                                                       \
+    do {                                                                                     \
+        const int nb_ = (TC) * M_BN + dr;                                                    \
+        _Pragma("unroll") for (int g_ = 0; g_ < 4; g_++)                                     \
+            oB[g_] = (unsigned)min(nb_ + 4 * g_, n1 - 1) * KD + (dcb ^ (64u * g_));          \
+        oR = (unsigned)min((TC) * M_BN + lane, n1 - 1) * 4;                                  \
+    } while (0)
+    // B fragment: column block c (0, 1), lane row 32 c + fr, k32 step s: chunk (2 s + fh)
+    const int rdb = fr * KD;
+    const int xsw = fh ^ (fr & 15);  // chunk (2 s + fh) ^ (fr & 15) = 2 s ^ xsw
+
+    // Accumulators start at the bits of 2^23: the MFMA leaves t = 2^23 + dot as a float
+    // (exact for 0 <= dot <= 2^22; a negative dot gives 2^23 + dot/2, still below 2^23), so
+    // f = fma(t, r, -2^23 r) = RN(dot * r) in one instruction (2^23 r is exact).  The low tb
+    // bits of f are then replaced by the column tag 2 tc + half (the lane's column within the
+    // half is its own lane index): top-2 tracking needs no index registers.
+    const i32x16 zero16 = {};
+    i32x16 magic16;
+#pragma unroll
+    for (int q = 0; q < 16; q++) magic16[q] = 0x4B000000;
+    i32x16 accA0 = zero16, accA1 = zero16, accB0 = zero16, accB1 = zero16;
+    float m1[16], m2[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        m1[q] = -__builtin_inff();
+        m2[q] = -__builtin_inff();
+    }
+    const int tb = 2 * ntc <= 256 ? 8 : 32 - __builtin_clz(2 * ntc - 1);
+    const unsigned tkeep = ~((1u << tb) - 1u);
+    unsigned vkeep = tkeep;
+    asm volatile("" : "+v"(vkeep));  // a VGPR operand: v_and_or_b32 may read one SGPR only
+    // fold tile TC with its norms rp0/rp1 (read from the slot while it was current: the
+    // slot is being refilled by then); only the last tile has columns past n1
+    float rp0 = 0.f, rp1 = 0.f;
+#define I8_FOLD(X0, X1, TC, MASK)                                                            \
+    do {                                                                                     \
+        const int col_ = (TC) * M_BN + fr;                                                   \
+        float r0_ = rp0, r1_ = rp1;                                                          \
+        if (MASK) {                                                                          \
+            r0_ = col_ < n1 ? r0_ : 0.f;                                                     \
+            r1_ = col_ + 32 < n1 ? r1_ : 0.f;                                                \
+        }                                                                                    \
+        const float c0_ = -8388608.0f * r0_, c1_ = -8388608.0f * r1_;                        \
+        const unsigned g0_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)(TC)), g1_ = g0_ + 1u; \
+        _Pragma("unroll") for (int q = 0; q < I8_FOLD_ROWS; q++) {                           \
+            const float a_ = __builtin_fmaf(__int_as_float(X0[q]), r0_, c0_);                \
+            const float b_ = __builtin_fmaf(__int_as_float(X1[q]), r1_, c1_);                \
+            fold3_i8(tag_i8(a_, vkeep, g0_), tag_i8(b_, vkeep, g1_), m1[q], m2[q]);          \
+        }                                                                                    \
+    } while (0)
+    // ring: tile g lives in slot g % 4; at tile g issue tile g + 3 into the slot read at g - 1
+#define I8_SLOT(J, C0, C1, F0, F1, FOLD)                                                     \
+    do {                                                                                     \
+        const int tc = T + (J);                                                              \
+        const int ntile = tc + M_NBUF - 1;                                                   \
+        if (ntile < ntc) {                                                                   \
+            I8_OFFSETS(ntile);                                                               \
+            if (!I8_NODMA) I8_STAGE((J + M_NBUF - 1) % M_NBUF);                              \
+        }                                                                                    \
+        const char *base = lds + (J) * M_SLOT + rdb;                                         \
+        _Pragma("unroll") for (int h_ = 0; h_ < 2; h_++) { /* K halves: 32 fragment VGPRs */ \
+            i32x4 b0_[KD / 64], b1_[KD / 64];                                                \
+            _Pragma("unroll") for (int u_ = 0; u_ < KD / 64; u_++) {                         \
+                const int ch_ = ((2 * (4 * h_ + u_)) ^ xsw) * 16;                            \
+                b0_[u_] = *reinterpret_cast<const i32x4 *>(base + ch_);                      \
+                b1_[u_] = *reinterpret_cast<const i32x4 *>(base + 32 * KD + ch_);            \
+            }                                                                                \
+            _Pragma("unroll") for (int u_ = 0; u_ < KD / 64; u_++) {                         \
+                const int s_ = 4 * h_ + u_;                                                  \
+                if (I8_NOMFMA) {                                                             \
+                    C0[s_] ^= b0_[u_][0];                                                    \
+                    C1[s_] ^= b1_[u_][1];                                                    \
+                } else {                                                                     \
+                C0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[s_], b0_[u_], s_ == 0 ? magic16 : C0, 0, 0, 0); \
+                C1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[s_], b1_[u_], s_ == 0 ? magic16 : C1, 0, 0, 0); \
+                }                                                                            \
+            }                                                                                \
+            if (h_ == 0) asm volatile("" ::: "memory");                                      \
+        }                                                                                    \
+        if (FOLD) I8_FOLD(F0, F1, tc - 1, false); /* previous tile, beside these MFMAs */     \
+        {                                                                                    \
+            const float *rl_ = reinterpret_cast<const float *>(lds + (J) * M_SLOT + M_TILE); \
+            rp0 = rl_[fr];                                                                   \
+            rp1 = rl_[fr + 32];                                                              \
+        }                                                                                    \
+        if (ntile < ntc) {                                                                   \
+            wait_vm_i8<5 * (M_NBUF - 2)>();                                                  \
+        } else {                                                                             \
+            wait_vm_i8<0>();                                                                 \
+        }                                                                                    \
+        if (!I8_NOBAR) __syncthreads();                                                      \
+    } while (0)
+
+    // prologue: tiles 0, 1, 2
+    for (int g = 0; g < M_NBUF - 1 && g < ntc; g++) {
+        I8_OFFSETS(g);
+        if (g == 0) I8_STAGE(0);
+        if (g == 1) I8_STAGE(1);
+        if (g == 2) I8_STAGE(2);
+    }
+    wait_vm_i8<0>();
+    __syncthreads();
+    for (int T = 0; T < ntc; T += 4) {
+        I8_SLOT(0, accA0, accA1, accB0, accB1, T > 0);
+        if (T + 1 < ntc) I8_SLOT(1, accB0, accB1, accA0, accA1, true);
+        if (T + 2 < ntc) I8_SLOT(2, accA0, accA1, accB0, accB1, true);
+        if (T + 3 < ntc) I8_SLOT(3, accB0, accB1, accA0, accA1, true);
+    }
+    if (ntc > 0) {  // the last tile (masked past n1 inside the fold)
+        const int tl = ntc - 1;
+        if (tl & 1)
+            I8_FOLD(accB0, accB1, tl, true);
+        else
+            I8_FOLD(accA0, accA1, tl, true);
+    }
+#undef I8_STAGE
+#undef I8_OFFSETS
+#undef I8_FOLD
+#undef I8_SLOT
+
+    // ---- merge the lanes' (m1, m2) per row (32 lanes per row); lanes fr == 0 publish the
+    //      wave's own rows to LDS (read back by the same wave only: the epilogue has no
+    //      block barrier).  A row whose runner-up is inside the window lists its candidate
+    //      columns: the maximum of every lane whose maximum is inside (the lane's column is
+    //      its tag + its lane index).  If some lane holds TWO columns inside (its m2 too),
+    //      every column of every lane whose maximum is inside is a candidate ("deep" row) ----
+    // the tag moved each f by < 2^(tb-23) relative and the screen itself is within 2e-7 of
+    // dot/|b|: a column below M (1 - 2^(tb-21)) cannot be (or tie) the true maximiser
+    const float keep_frac = 1.0f - __builtin_ldexpf(1.0f, tb - 21);
+    int *clist = reinterpret_cast<int *>(lds);               // [BM][32] (the ring is free now)
+    int *ccount = clist + M_BM * 32;                         // [BM]; -1: deep
+    unsigned *lmask = reinterpret_cast<unsigned *>(ccount + M_BM);  // [BM] lanes inside (deep rows)
+    if (fh == 0) ccount[w * 32 + fr] = 0;
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        float a1 = m1[q], a2 = m2[q];
+        int ai = fr;  // the lane holding a1: its column within the tag's half
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+            const float b1 = __shfl_xor(a1, o, 64), b2 = __shfl_xor(a2, o, 64);
+            const int bi = __shfl_xor(ai, o, 64);
+            a2 = fmaxf(fmaxf(a2, b2), fminf(a1, b1));  // equal maxima land in a2: ambiguous
+            ai = b1 > a1 ? bi : ai;
+            a1 = fmaxf(a1, b1);
+        }
+        const int row = w * 32 + (q & 3) + 8 * (q >> 2) + 4 * fh;
+        if (fr == 0) {
+            const unsigned tag = __float_as_uint(a1) & ~tkeep;
+            float *tp = trip + row * 3;
+            tp[0] = a1;
+            reinterpret_cast<int *>(tp)[1] = (int)(tag >> 1) * M_BN + (int)(tag & 1) * 32 + ai;
+            tp[2] = a2;
+        }
+        const float lim = a1 * keep_frac;
+        if (a2 >= lim && a1 > 1e-30f) {  // uniform per half; inactive half reads 0 in ballots
+            const unsigned deep = (unsigned)(__ballot(m2[q] >= lim) >> (32 * fh));
+            const unsigned inside = (unsigned)(__ballot(m1[q] >= lim) >> (32 * fh));
+#ifdef I8_EXP_PRINT
+            if (fr == 0) printf("I8AMB pair %d row %d M %.9g M2 %.9g deep %x\n", pair, row0 + row, a1, a2, deep);
+#endif
+            if (deep) {
+                if (fr == 0) {
+                    ccount[row] = -1;
+                    lmask[row] = inside;
                 }
-                for (int j = jb; j < je; j++) {
-                    const long long d = exact_dot_i8(a, B + (size_t)j * KD);
-                    const long long nbj = nb[j];
-                    if (d <= 0 || nbj == 0) continue;
-                    if (better(d, nbj, j, bd, bn, best)) {
-                        best = j;
-                        bd = d;
-                        bn = nbj;
-                    }
-                }
+            } else if (m1[q] >= lim) {
+                const unsigned tag = __float_as_uint(m1[q]) & ~tkeep;
+                clist[row * 32 + __popc(inside & ((1u << fr) - 1u))] = (int)(tag >> 1) * M_BN + (int)(tag & 1) * 32 + fr;
+                if (fr == 31 - __builtin_clz(inside)) ccount[row] = __popc(inside);
             }
-            if (best >= 0 && !((unsigned __int128)(100ll * bd * bd) >
-                               (unsigned __int128)81 * (unsigned long long)(na * bn)))
-                best = -1;
         }
     }
-    match_idx[(size_t)pair * cap + i] = best;
-    match_dot[(size_t)pair * cap + i] = best >= 0 ? (int)bd : 0;
+
+    // ---- decide row w*32 + fr in its own two lanes (they hold its A halves in aI): exact
+    //      integer dots with the screen maximiser I, or with each listed candidate ----
+    unsigned deep_rows;
+    {
+        const int rl = w * 32 + fr;
+        const float *tp = trip + rl * 3;
+        const float M = tp[0], M2 = tp[2];
+        const int I = reinterpret_cast<const int *>(tp)[1];
+        const bool live = row0 + rl < n0;
+#ifdef I8_EXP_NOEXACT
+        const bool cand = false;
+#else
+        const bool cand = live && na_r > 0 && M > 1e-30f;  // else every dot <= 0 (tagged zeros are subnormal)
+#endif
+        const bool ambig = cand && M2 >= M * keep_frac;
+        const int nc = ambig ? ccount[rl] : (cand ? 1 : 0);
+        int bj = -1;
+        long long bd = 0, bn = 1;
+        for (int k = 0; k < nc; k++) {  // the row's two lanes run the same trip count
+            const int j = ambig ? clist[rl * 32 + k] : I;
+            const int8_t *brow = B + (size_t)j * KD + fh * 16;
+            i32x4 bv[KD / 32];
+#pragma unroll
+            for (int s2 = 0; s2 < KD / 32; s2++) bv[s2] = *reinterpret_cast<const i32x4 *>(brow + s2 * 32);
+            const long long nbj = nb[j];
+            int part = 0;
+#pragma unroll
+            for (int s2 = 0; s2 < KD / 32; s2++)
+#pragma unroll
+                for (int u = 0; u < 4; u++) part = __builtin_amdgcn_sdot4(aI[s2][u], bv[s2][u], part, false);
+            part += __shfl_xor(part, 32, 64);
+            if (part > 0 && nbj > 0 && better(part, nbj, j, bd, bn, bj)) {
+                bj = j;
+                bd = part;
+                bn = nbj;
+            }
+        }
+        if (fh == 0 && live && nc >= 0) {
+            const long long na = na_r;
+            const bool keep = bj >= 0 &&
+                              (unsigned __int128)(100ll * bd * bd) > (unsigned __int128)81 * (unsigned long long)(na * bn);
+            oidx[rl] = keep ? bj : -1;
+            odot[rl] = keep ? (int)bd : 0;
+        }
+        deep_rows = (unsigned)__ballot(fh == 0 && live && nc < 0);
+    }
+
+    // ---- deep rows (rare): the wave scores every column of every inside lane exactly,
+    //      one column per lane (lane l: column f + 32 (l + 64 i) of inside lane f) ----
+    while (deep_rows) {
+        const int rr = __builtin_ctz(deep_rows);
+        deep_rows &= deep_rows - 1;
+        const int rl = w * 32 + rr;
+#ifdef I8_EXP_PRINT
+        if (lane == 0) printf("I8DEEP pair %d row %d lanes %x\n", pair, row0 + rl, lmask[rl]);
+#endif
+        const i32x4 *arow = reinterpret_cast<const i32x4 *>(A + (size_t)(row0 + rl) * KD);
+        i32x4 av[KD / 16];
+#pragma unroll
+        for (int v = 0; v < KD / 16; v++) av[v] = arow[v];
+        int bj = -1;
+        long long bd = 0, bn = 1;
+        for (unsigned L = lmask[rl]; L; L &= L - 1) {
+            const int f = __builtin_ctz(L);
+            for (int j = f + 32 * lane; j < n1; j += 32 * 64) {
+                const i32x4 *brow = reinterpret_cast<const i32x4 *>(B + (size_t)j * KD);
+                i32x4 bv[KD / 16];
+#pragma unroll
+                for (int v = 0; v < KD / 16; v++) bv[v] = brow[v];
+                const long long nbj = nb[j];
+                int d = 0;
+#pragma unroll
+                for (int v = 0; v < KD / 16; v++)
+#pragma unroll
+                    for (int u = 0; u < 4; u++) d = __builtin_amdgcn_sdot4(av[v][u], bv[v][u], d, false);
+                if (d > 0 && nbj > 0 && better(d, nbj, j, bd, bn, bj)) {
+                    bj = j;
+                    bd = d;
+                    bn = nbj;
+                }
+            }
+        }
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const long long od = __shfl_xor(bd, o, 64), on = __shfl_xor(bn, o, 64);
+            const int oj = __shfl_xor(bj, o, 64);
+            if (oj >= 0 && better(od, on, oj, bd, bn, bj)) {
+                bj = oj;
+                bd = od;
+                bn = on;
+            }
+        }
+        if (lane == 0) {
+            const long long na = na_s[rl];
+            const bool keep = bj >= 0 &&
+                              (unsigned __int128)(100ll * bd * bd) > (unsigned __int128)81 * (unsigned long long)(na * bn);
+            oidx[rl] = keep ? bj : -1;
+            odot[rl] = keep ? (int)bd : 0;
+        }
+    }
 }
 
 }  // namespace
@@ -248,44 +480,29 @@ __global__ __launch_bounds__(256) void k_i8_resolve(int tiles_c, int cap, const 
 namespace mv {
 
 size_t allpairs_i8_scratch_bytes(int batch, int cap) {
-    const int tiles_c = (cap + BN - 1) / BN;
     const size_t rows = (size_t)batch * cap;
-    return align_up(sizeof(Partial) * rows * tiles_c, 256) + 3 * align_up(4 * rows, 256);
+    return 2 * align_up(4 * rows, 256);
 }
 
 int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
                        const int8_t *desc0, const int8_t *desc1, int *match_idx, int *match_dot) {
     MV_REQUIRE(batch > 0 && cap > 0 && n0 && n1 && desc0 && desc1 && match_idx && match_dot && scratch);
     MV_REQUIRE(((uintptr_t)desc0 & 15) == 0 && ((uintptr_t)desc1 & 15) == 0);
-    const int tiles_r = (cap + BM - 1) / BM, tiles_c = (cap + BN - 1) / BN;
     const size_t rows = (size_t)batch * cap;
-    char *p = (char *)scratch;
-    Partial *part = (Partial *)p;
-    p += align_up(sizeof(Partial) * rows * tiles_c, 256);
-    int *na = (int *)p;
-    p += align_up(4 * rows, 256);
-    int *nb = (int *)p;
-    p += align_up(4 * rows, 256);
-    float *rnb = (float *)p;
+    int *nb = (int *)scratch;
+    float *rnb = (float *)((char *)scratch + align_up(4 * rows, 256));
     const int nblk = (int)((rows + 255) / 256);
-    MV_PROF_BEGIN(s, "k_i8_norms");
-    hipLaunchKernelGGL(k_i8_norms, dim3(nblk), dim3(256), 0, s, (long)rows, desc0, na, (float *)nullptr);
-    MV_PROF_END(s);
-    MV_LAUNCH_CHECK();
     MV_PROF_BEGIN(s, "k_i8_norms");
     hipLaunchKernelGGL(k_i8_norms, dim3(nblk), dim3(256), 0, s, (long)rows, desc1, nb, rnb);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
-    const long blocks = (long)batch * tiles_r * tiles_c;
-    MV_REQUIRE(blocks < (1l << 31));
-    MV_PROF_BEGIN(s, "k_i8_screen");
-    hipLaunchKernelGGL(k_i8_screen, dim3((unsigned)blocks), dim3(256), 0, s, tiles_r, tiles_c, cap, n0, n1, desc0,
-                       desc1, rnb, part);
-    MV_PROF_END(s);
-    MV_LAUNCH_CHECK();
-    MV_PROF_BEGIN(s, "k_i8_resolve");
-    hipLaunchKernelGGL(k_i8_resolve, dim3((cap + 255) / 256, batch), dim3(256), 0, s, tiles_c, cap, n0, n1, desc0,
-                       desc1, na, nb, part, match_idx, match_dot);
+    const int tiles_m = (cap + M_BM - 1) / M_BM;
+    const long mblocks = (long)batch * tiles_m;
+    MV_REQUIRE(mblocks < (1l << 31));
+    MV_REQUIRE((long)cap * KD < (1l << 31));  // 32-bit DMA source offsets within a pair
+    MV_PROF_BEGIN(s, "k_i8_match");
+    hipLaunchKernelGGL(k_i8_match, dim3((unsigned)mblocks), dim3(M_NT), 0, s, tiles_m, cap, n0, n1, desc0, desc1, nb,
+                       rnb, match_idx, match_dot);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     return MV_OK;

@@ -168,7 +168,7 @@ def test_allpairs_f32_prepare_run_pipeline(ctx, orc, torch_cuda):
     ctx.set_stream(None)
 
 
-def run_i8(ctx, torch, pairs, cap=None):
+def run_i8(ctx, torch, pairs, cap=None, decoys=False):
     B = len(pairs)
     cap = cap or max(max(a.shape[0], b.shape[0]) for a, b in pairs)
     D0 = np.zeros((B, cap, 256), np.int8)
@@ -178,6 +178,8 @@ def run_i8(ctx, torch, pairs, cap=None):
     for b, (a, c) in enumerate(pairs):
         D0[b, :a.shape[0]] = a
         D1[b, :c.shape[0]] = c
+        if decoys:  # slots past n1 repeat the queries: they must never be matched
+            D1[b, c.shape[0]:] = np.resize(a, (cap - c.shape[0], 256))
         n0[b], n1[b] = a.shape[0], c.shape[0]
     dev = torch.device("cuda:0")
     t = lambda x: torch.from_numpy(x).to(dev)  # noqa: E731
@@ -215,3 +217,30 @@ def test_allpairs_i8_ragged_and_degenerate(ctx, orc, torch_cuda):
     for b, (a, c) in enumerate(pairs):
         i2, d2 = orc.allpairs_i8(a, c)
         assert (idx[b, :a.shape[0]] == i2).all() and (dot[b, :a.shape[0]] == d2).all()
+
+
+def test_allpairs_i8_ties_and_near_ties(ctx, orc, torch_cuda):
+    """Columns with equal or nearly equal dot^2/|b|^2 take the exact re-score:
+    b and b/2 tie exactly (first index wins), b and b + e_k differ in the 5th digit;
+    rows whose every dot is <= 0 never match; slots past n1 hold strong decoys."""
+    pairs = []
+    for k, (na, nb) in enumerate([(200, 300), (129, 65), (64, 1000)]):
+        a, b = synth.synth_pair_i8(40 + k, n=max(na, nb))
+        a, b = a[:na].copy(), b[:nb].copy()
+        m = nb // 4
+        b[:m] = (b[:m] // 2) * 2
+        b[nb // 2: nb // 2 + m] = b[:m] // 2          # exact ties with earlier columns
+        for j in range(m, min(m + 40, nb // 2 - 1), 2):  # near ties
+            b[j + 1] = b[j]
+            b[j + 1, j % 256] = np.clip(int(b[j, j % 256]) + 1, -127, 127)
+        if nb > 3 * 64:  # exact duplicates one tile apart: two candidates in one lane
+            b[m + 64: m + 80] = b[m: m + 16]
+        a[5] = 0
+        a[5, 0] = -1
+        b[:, 0] = np.abs(b[:, 0]) + 1                 # row 5: every dot < 0
+        pairs.append((a, b))
+    idx, dot = run_i8(ctx, torch_cuda, pairs, cap=1000, decoys=True)
+    for q, (a, c) in enumerate(pairs):
+        i2, d2 = orc.allpairs_i8(a, c)
+        assert (idx[q, :a.shape[0]] == i2).all() and (dot[q, :a.shape[0]] == d2).all()
+        assert i2[5] == -1 and (i2 >= 0).sum() > a.shape[0] // 8
