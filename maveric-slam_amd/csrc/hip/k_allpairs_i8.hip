@@ -90,11 +90,16 @@ __device__ __forceinline__ bool better(long long d, long long nb, int j, long lo
 #else
 #define I8_FOLD_ROWS 16
 #endif
+#ifdef I8_EXP_TRACE
+constexpr int I8_TRACE_BLOCKS = 8192;
+__device__ unsigned long long g_i8_trace[I8_TRACE_BLOCKS * 4 * 10];
+#endif
 constexpr int M_NW = 4, M_NT = 64 * M_NW, M_BM = 32 * M_NW, M_BN = 64, M_NBUF = 4;
 constexpr int M_TILE = M_BN * KD;                 // 16 KiB: one column tile, whole K
 constexpr int M_SLOT = M_TILE + M_BN * 4;         // + the tile's 64 rsqrt|b|^2
-constexpr int M_OFF_TRIP = M_NBUF * M_SLOT;       // [BM] {m1, i1, m2}
-constexpr int M_OFF_NA = M_OFF_TRIP + M_BM * 12;  // [BM] i32 |a|^2
+constexpr int M_OFF_NA = M_NBUF * M_SLOT;         // [BM] i32 |a|^2
+constexpr int MT_STRIDE = 32 * 8 + 16;            // epilogue transpose row: 32 (m1, m2) + pad
+static_assert(M_NW * 32 * MT_STRIDE + M_BM * 33 * 4 <= M_NBUF * M_SLOT, "epilogue fits the ring");
 constexpr int M_LDS = M_OFF_NA + M_BM * 4;
 
 #pragma clang diagnostic ignored "-Winline-asm"
@@ -142,8 +147,14 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
                                                       const float *__restrict__ rnb_v, int *__restrict__ match_idx,
                                                       int *__restrict__ match_dot) {
     __shared__ __attribute__((aligned(16))) char lds[M_LDS];
-    float *trip = reinterpret_cast<float *>(lds + M_OFF_TRIP);
     int *na_s = reinterpret_cast<int *>(lds + M_OFF_NA);
+#ifdef I8_EXP_TRACE
+#define I8_STAMP(K) do { __builtin_amdgcn_sched_barrier(0); ts_[K] = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
+    unsigned long long ts_[8];
+    I8_STAMP(0);
+#else
+#define I8_STAMP(K) do { } while (0)
+#endif
     const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int pair = L / tiles_r, tr = L % tiles_r;
     const int n0 = min(max(n0v[pair], 0), cap), n1 = min(max(n1v[pair], 0), cap);
@@ -180,6 +191,7 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
         if (fh == 0) na_s[w * 32 + fr] = q;
         na_r = q;
     }
+    I8_STAMP(1);
 
     // ---- B DMA: wave w fills rows w*16 .. +15 of a tile, 4 rows (1 KiB) per instruction;
     //      lane l -> row (l >> 4), chunk position l & 15, source chunk (l & 15) ^ (row & 15) ----
@@ -302,12 +314,14 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
     }
     wait_vm_i8<0>();
     __syncthreads();
+    I8_STAMP(2);
     for (int T = 0; T < ntc; T += 4) {
         I8_SLOT(0, accA0, accA1, accB0, accB1, T > 0);
         if (T + 1 < ntc) I8_SLOT(1, accB0, accB1, accA0, accA1, true);
         if (T + 2 < ntc) I8_SLOT(2, accA0, accA1, accB0, accB1, true);
         if (T + 3 < ntc) I8_SLOT(3, accB0, accB1, accA0, accA1, true);
     }
+    I8_STAMP(3);
     if (ntc > 0) {  // the last tile (masked past n1 inside the fold)
         const int tl = ntc - 1;
         if (tl & 1)
@@ -320,75 +334,96 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
 #undef I8_FOLD
 #undef I8_SLOT
 
-    // ---- merge the lanes' (m1, m2) per row (32 lanes per row); lanes fr == 0 publish the
-    //      wave's own rows to LDS (read back by the same wave only: the epilogue has no
-    //      block barrier).  A row whose runner-up is inside the window lists its candidate
-    //      columns: the maximum of every lane whose maximum is inside (the lane's column is
-    //      its tag + its lane index).  If some lane holds TWO columns inside (its m2 too),
-    //      every column of every lane whose maximum is inside is a candidate ("deep" row) ----
+    // ---- per row, merge the 32 lanes' (m1, m2): transposed through LDS (the ring is free
+    //      now; the wave reads back only what it wrote: no block barrier in the epilogue).
+    //      Row r of the wave gets its lanes' entries [r][e] (e = the lane = the column within
+    //      the tag's half); lane (fr, fh) folds entries 16 fh .. 16 fh + 15 of row fr, and the
+    //      two halves combine: lanes fr and fr + 32 end with row fr's (M, E, M2), which is
+    //      where the row's A halves are (aI) ----
     // the tag moved each f by < 2^(tb-23) relative and the screen itself is within 2e-7 of
     // dot/|b|: a column below M (1 - 2^(tb-21)) cannot be (or tie) the true maximiser
     const float keep_frac = 1.0f - __builtin_ldexpf(1.0f, tb - 21);
-    int *clist = reinterpret_cast<int *>(lds);               // [BM][32] (the ring is free now)
-    int *ccount = clist + M_BM * 32;                         // [BM]; -1: deep
-    unsigned *lmask = reinterpret_cast<unsigned *>(ccount + M_BM);  // [BM] lanes inside (deep rows)
-    if (fh == 0) ccount[w * 32 + fr] = 0;
+    char *mt = lds + w * 32 * MT_STRIDE;
 #pragma unroll
     for (int q = 0; q < 16; q++) {
-        float a1 = m1[q], a2 = m2[q];
-        int ai = fr;  // the lane holding a1: its column within the tag's half
+        const int r = (q & 3) + 8 * (q >> 2) + 4 * fh;
+        float2 v;
+        v.x = m1[q];
+        v.y = m2[q];
+        *reinterpret_cast<float2 *>(mt + r * MT_STRIDE + fr * 8) = v;
+    }
+    float e1[16], e2[16];
 #pragma unroll
-        for (int o = 1; o < 32; o <<= 1) {
-            const float b1 = __shfl_xor(a1, o, 64), b2 = __shfl_xor(a2, o, 64);
-            const int bi = __shfl_xor(ai, o, 64);
-            a2 = fmaxf(fmaxf(a2, b2), fminf(a1, b1));  // equal maxima land in a2: ambiguous
-            ai = b1 > a1 ? bi : ai;
-            a1 = fmaxf(a1, b1);
-        }
-        const int row = w * 32 + (q & 3) + 8 * (q >> 2) + 4 * fh;
-        if (fr == 0) {
-            const unsigned tag = __float_as_uint(a1) & ~tkeep;
-            float *tp = trip + row * 3;
-            tp[0] = a1;
-            reinterpret_cast<int *>(tp)[1] = (int)(tag >> 1) * M_BN + (int)(tag & 1) * 32 + ai;
-            tp[2] = a2;
-        }
-        const float lim = a1 * keep_frac;
-        if (a2 >= lim && a1 > 1e-30f) {  // uniform per half; inactive half reads 0 in ballots
-            const unsigned deep = (unsigned)(__ballot(m2[q] >= lim) >> (32 * fh));
-            const unsigned inside = (unsigned)(__ballot(m1[q] >= lim) >> (32 * fh));
-#ifdef I8_EXP_PRINT
-            if (fr == 0) printf("I8AMB pair %d row %d M %.9g M2 %.9g deep %x\n", pair, row0 + row, a1, a2, deep);
-#endif
-            if (deep) {
-                if (fr == 0) {
-                    ccount[row] = -1;
-                    lmask[row] = inside;
-                }
-            } else if (m1[q] >= lim) {
-                const unsigned tag = __float_as_uint(m1[q]) & ~tkeep;
-                clist[row * 32 + __popc(inside & ((1u << fr) - 1u))] = (int)(tag >> 1) * M_BN + (int)(tag & 1) * 32 + fr;
-                if (fr == 31 - __builtin_clz(inside)) ccount[row] = __popc(inside);
-            }
-        }
+    for (int i = 0; i < 8; i++) {
+        const float4 v = *reinterpret_cast<const float4 *>(mt + fr * MT_STRIDE + (fh * 16 + 2 * i) * 8);
+        e1[2 * i] = v.x;
+        e2[2 * i] = v.y;
+        e1[2 * i + 1] = v.z;
+        e2[2 * i + 1] = v.w;
+    }
+    float M = -__builtin_inff(), M2 = -__builtin_inff();
+    int E = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {  // equal maxima land in M2: ambiguous
+        M2 = fmaxf(fmaxf(M2, e2[i]), fminf(M, e1[i]));
+        E = e1[i] > M ? fh * 16 + i : E;
+        M = fmaxf(M, e1[i]);
+    }
+    {
+        const float oM = __shfl_xor(M, 32, 64), oM2 = __shfl_xor(M2, 32, 64);
+        const int oE = __shfl_xor(E, 32, 64);
+        M2 = fmaxf(fmaxf(M2, oM2), fminf(M, oM));
+        E = (oM > M || (oM == M && oE < E)) ? oE : E;
+        M = fmaxf(M, oM);
     }
 
-    // ---- decide row w*32 + fr in its own two lanes (they hold its A halves in aI): exact
-    //      integer dots with the screen maximiser I, or with each listed candidate ----
+    I8_STAMP(4);
+    // ---- decide row w*32 + fr in its own two lanes: exact integer dots with the screen
+    //      maximiser, or -- runner-up inside the window -- with the maximum of every entry
+    //      (lane) inside; if some entry holds TWO columns inside (its m2 too), every column of
+    //      every inside entry is a candidate ("deep" row, below) ----
+    int *clist = reinterpret_cast<int *>(lds + M_NW * 32 * MT_STRIDE);  // [BM][32]
+    unsigned *lmask = reinterpret_cast<unsigned *>(clist + M_BM * 32);  // [BM] deep rows' entries
     unsigned deep_rows;
     {
         const int rl = w * 32 + fr;
-        const float *tp = trip + rl * 3;
-        const float M = tp[0], M2 = tp[2];
-        const int I = reinterpret_cast<const int *>(tp)[1];
         const bool live = row0 + rl < n0;
 #ifdef I8_EXP_NOEXACT
         const bool cand = false;
 #else
         const bool cand = live && na_r > 0 && M > 1e-30f;  // else every dot <= 0 (tagged zeros are subnormal)
 #endif
-        const bool ambig = cand && M2 >= M * keep_frac;
-        const int nc = ambig ? ccount[rl] : (cand ? 1 : 0);
+        const float lim = M * keep_frac;
+        const bool ambig = cand && M2 >= lim;
+        int nc = cand ? 1 : 0;
+        if (ambig) {  // both lanes of the row take this branch
+            unsigned in1 = 0, in2 = 0;
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                in1 |= (e1[i] >= lim ? 1u : 0u) << i;
+                in2 |= (e2[i] >= lim ? 1u : 0u) << i;
+            }
+            const unsigned o1 = __shfl_xor(in1, 32, 64), o2 = __shfl_xor(in2, 32, 64);
+            const unsigned inside = fh ? (o1 | (in1 << 16)) : (in1 | (o1 << 16));
+            if (in2 | o2) {
+                nc = -1;
+                if (fh == 0) lmask[rl] = inside;
+            } else {
+                nc = __popc(inside);
+                int k = fh ? __popc(o1) : 0;
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    if (e1[i] >= lim) {
+                        const unsigned tag = __float_as_uint(e1[i]) & ~tkeep;
+                        clist[rl * 32 + k++] = (int)(tag >> 1) * M_BN + (int)(tag & 1) * 32 + fh * 16 + i;
+                    }
+            }
+#ifdef I8_EXP_PRINT
+            if (fh == 0) printf("I8AMB pair %d row %d M %.9g M2 %.9g nc %d\n", pair, row0 + rl, M, M2, nc);
+#endif
+        }
+        const unsigned tagM = __float_as_uint(M) & ~tkeep;
+        const int I = (int)(tagM >> 1) * M_BN + (int)(tagM & 1) * 32 + E;
         int bj = -1;
         long long bd = 0, bn = 1;
         for (int k = 0; k < nc; k++) {  // the row's two lanes run the same trip count
@@ -419,9 +454,11 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
         }
         deep_rows = (unsigned)__ballot(fh == 0 && live && nc < 0);
     }
+    I8_STAMP(5);
 
     // ---- deep rows (rare): the wave scores every column of every inside lane exactly,
     //      one column per lane (lane l: column f + 32 (l + 64 i) of inside lane f) ----
+    I8_STAMP(6);
     while (deep_rows) {
         const int rr = __builtin_ctz(deep_rows);
         deep_rows &= deep_rows - 1;
@@ -473,6 +510,15 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
             odot[rl] = keep ? (int)bd : 0;
         }
     }
+#ifdef I8_EXP_TRACE
+    I8_STAMP(7);
+    if (lane == 0 && blockIdx.x < I8_TRACE_BLOCKS) {
+        unsigned long long *o = g_i8_trace + ((size_t)blockIdx.x * M_NW + w) * 10;
+        for (int k = 0; k < 8; k++) o[k] = ts_[k];
+        o[8] = __smid();
+        o[9] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 }
 
 }  // namespace
@@ -518,3 +564,10 @@ extern "C" int mv_match_allpairs_i8_dev(mv_context *ctx, int batch, int cap, con
     if (!scr) return MV_ERR_OUT_OF_MEMORY;
     return mv::launch_allpairs_i8(ctx->stream, scr, batch, cap, n0, n1, desc0, desc1, match_idx, match_dot);
 }
+
+#ifdef I8_EXP_TRACE
+// timing experiment only: copy the per-(block, wave) phase stamps of the last launch
+extern "C" int mv_debug_i8_trace(void *host, long bytes) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_i8_trace), (size_t)bytes) == hipSuccess ? 0 : -3;
+}
+#endif
