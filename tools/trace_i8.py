@@ -52,3 +52,9 @@ o = sel[np.argsort(start[sel])]
 print("CU", cu, "timeline (start, end, dur) rel. to first start:")
 for b in o[:16]:
     print("  blk %5d  %9d %9d %9d" % (b, start[b] - start[o[0]], end[b] - start[o[0]], end[b] - start[b]))
+# shader clock: s_memtime (SCLK) against s_memrealtime (100 MHz) at block ends on this CU
+rt = tr[:, 0, 9]
+e7 = st[:, 0, 7]
+a, b = o[0], o[-1]
+if rt[b] != rt[a]:
+    print("SCLK over the CU's run: %.3f GHz" % ((e7[b] - e7[a]) / ((rt[b] - rt[a]) / 100e6) / 1e9))
