@@ -90,17 +90,26 @@ __device__ __forceinline__ bool better(long long d, long long nb, int j, long lo
 #else
 #define I8_FOLD_ROWS 16
 #endif
+#ifndef I8_PIPE
+#define I8_PIPE 0  // 1: fold group 1 of tile t beside group 0's MFMAs of tile t + 1 (spills)
+#endif
+#ifndef I8_KSTEP
+#define I8_KSTEP 2  // k32 steps of B fragments read per group (8 VGPRs each)
+#endif
 #ifdef I8_EXP_TRACE
 constexpr int I8_TRACE_BLOCKS = 8192;
 __device__ unsigned long long g_i8_trace[I8_TRACE_BLOCKS * 4 * 10];
 #endif
-constexpr int M_NW = 4, M_NT = 64 * M_NW, M_BM = 32 * M_NW, M_BN = 64, M_NBUF = 4;
+constexpr int M_NW = 4, M_NT = 64 * M_NW, M_RG = 2, M_BM = 32 * M_RG * M_NW, M_BN = 64, M_NBUF = 4;
 constexpr int M_TILE = M_BN * KD;                 // 16 KiB: one column tile, whole K
 constexpr int M_SLOT = M_TILE + M_BN * 4;         // + the tile's 64 rsqrt|b|^2
 constexpr int M_OFF_NA = M_NBUF * M_SLOT;         // [BM] i32 |a|^2
-constexpr int MT_STRIDE = 32 * 8 + 16;            // epilogue transpose row: 32 (m1, m2) + pad
-static_assert(M_NW * 32 * MT_STRIDE + M_BM * 33 * 4 <= M_NBUF * M_SLOT, "epilogue fits the ring");
 constexpr int M_LDS = M_OFF_NA + M_BM * 4;
+constexpr int MT_STRIDE = 32 * 8 + 16;            // epilogue transpose row: 32 (m1, m2) + pad
+constexpr int M_NCAND = 16;                       // listed candidates per row (more: deep row)
+constexpr int M_OFF_CL = M_NW * 32 * MT_STRIDE;   // epilogue, inside the ring: [BM][NCAND] candidates
+constexpr int M_OFF_LM = M_OFF_CL + M_BM * M_NCAND * 4;  // [BM] deep rows' inside entries
+static_assert(M_OFF_LM + M_BM * 4 <= M_NBUF * M_SLOT, "epilogue fits the ring");
 
 #pragma clang diagnostic ignored "-Winline-asm"
 template <int KOFF, int DOFF>
@@ -162,7 +171,7 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
     const int row0 = tr * M_BM;
     int *oidx = match_idx + (size_t)pair * cap + row0;
     int *odot = match_dot + (size_t)pair * cap + row0;
-    if (t < M_BM && row0 + t < cap && (row0 + t >= n0 || n1 <= 0)) {
+    if (row0 + t < cap && (row0 + t >= n0 || n1 <= 0)) {
         oidx[t] = -1;
         odot[t] = 0;
     }
@@ -173,23 +182,28 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
     const int *nb = nb_v + (size_t)pair * cap;
     const int ntc = (n1 + M_BN - 1) / M_BN;
 
-    // ---- A: 32 rows x 256 int8 in 32 VGPRs (i8 MFMA A operand: lane l holds row l & 31,
-    //      k = 32 s + 16 (l >> 5) .. +15 at k32 step s); |a|^2 along the way ----
+    // ---- A: the wave's 2 x 32 rows (w*64 + 32 g + fr) x 256 int8 in 64 VGPRs (i8 MFMA A
+    //      operand: lane l holds row l & 31, k = 32 s + 16 (l >> 5) .. +15 at k32 step s);
+    //      |a|^2 along the way ----
     const int fr = lane & 31, fh = lane >> 5;
-    i32x4 aI[KD / 32];
-    int na_r;  // |a|^2 of row w*32 + fr
-    {
-        const int8_t *arow = A + (size_t)min(row0 + w * 32 + fr, n0 - 1) * KD + fh * 16;
+    i32x4 aI[M_RG][KD / 32];
+    int na_r[M_RG];  // |a|^2 of row w*64 + 32 g + fr
 #pragma unroll
-        for (int s2 = 0; s2 < KD / 32; s2++) aI[s2] = *reinterpret_cast<const i32x4 *>(arow + s2 * 32);
+    for (int g = 0; g < M_RG; g++) {
+        const int8_t *arow = A + (size_t)min(row0 + w * 64 + g * 32 + fr, n0 - 1) * KD + fh * 16;
+#pragma unroll
+        for (int s2 = 0; s2 < KD / 32; s2++) aI[g][s2] = *reinterpret_cast<const i32x4 *>(arow + s2 * 32);
+    }
+#pragma unroll
+    for (int g = 0; g < M_RG; g++) {
         int q = 0;
 #pragma unroll
         for (int s2 = 0; s2 < KD / 32; s2++)
 #pragma unroll
-            for (int u = 0; u < 4; u++) q = __builtin_amdgcn_sdot4(aI[s2][u], aI[s2][u], q, false);
+            for (int u = 0; u < 4; u++) q = __builtin_amdgcn_sdot4(aI[g][s2][u], aI[g][s2][u], q, false);
         q += __shfl_xor(q, 32, 64);
-        if (fh == 0) na_s[w * 32 + fr] = q;
-        na_r = q;
+        if (fh == 0) na_s[w * 64 + g * 32 + fr] = q;
+        na_r[g] = q;
     }
     I8_STAMP(1);
 
@@ -228,42 +242,68 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
     // f = fma(t, r, -2^23 r) = RN(dot * r) in one instruction (2^23 r is exact).  The low tb
     // bits of f are then replaced by the column tag 2 tc + half (the lane's column within the
     // half is its own lane index): top-2 tracking needs no index registers.
-    const i32x16 zero16 = {};
     i32x16 magic16;
 #pragma unroll
     for (int q = 0; q < 16; q++) magic16[q] = 0x4B000000;
-    i32x16 accA0 = zero16, accA1 = zero16, accB0 = zero16, accB1 = zero16;
-    float m1[16], m2[16];
+    i32x16 acc[M_RG][2];
+    float m1[M_RG][16], m2[M_RG][16];
 #pragma unroll
-    for (int q = 0; q < 16; q++) {
-        m1[q] = -__builtin_inff();
-        m2[q] = -__builtin_inff();
-    }
+    for (int g = 0; g < M_RG; g++)
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            m1[g][q] = -__builtin_inff();
+            m2[g][q] = -__builtin_inff();
+        }
     const int tb = 2 * ntc <= 256 ? 8 : 32 - __builtin_clz(2 * ntc - 1);
     const unsigned tkeep = ~((1u << tb) - 1u);
     unsigned vkeep = tkeep;
     asm volatile("" : "+v"(vkeep));  // a VGPR operand: v_and_or_b32 may read one SGPR only
-    // fold tile TC with its norms rp0/rp1 (read from the slot while it was current: the
-    // slot is being refilled by then); only the last tile has columns past n1
-    float rp0 = 0.f, rp1 = 0.f;
-#define I8_FOLD(X0, X1, TC, MASK)                                                            \
+
+    // fold row group G of tile TC (norms R0/R1; only the last tile has columns past n1)
+#define I8_FOLD(G, TC, R0, R1)                                                               \
     do {                                                                                     \
-        const int col_ = (TC) * M_BN + fr;                                                   \
-        float r0_ = rp0, r1_ = rp1;                                                          \
-        if (MASK) {                                                                          \
-            r0_ = col_ < n1 ? r0_ : 0.f;                                                     \
-            r1_ = col_ + 32 < n1 ? r1_ : 0.f;                                                \
-        }                                                                                    \
-        const float c0_ = -8388608.0f * r0_, c1_ = -8388608.0f * r1_;                        \
+        const float c0_ = -8388608.0f * (R0), c1_ = -8388608.0f * (R1);                      \
         const unsigned g0_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)(TC)), g1_ = g0_ + 1u; \
         _Pragma("unroll") for (int q = 0; q < I8_FOLD_ROWS; q++) {                           \
-            const float a_ = __builtin_fmaf(__int_as_float(X0[q]), r0_, c0_);                \
-            const float b_ = __builtin_fmaf(__int_as_float(X1[q]), r1_, c1_);                \
-            fold3_i8(tag_i8(a_, vkeep, g0_), tag_i8(b_, vkeep, g1_), m1[q], m2[q]);          \
+            const float a_ = __builtin_fmaf(__int_as_float(acc[G][0][q]), (R0), c0_);        \
+            const float b_ = __builtin_fmaf(__int_as_float(acc[G][1][q]), (R1), c1_);        \
+            fold3_i8(tag_i8(a_, vkeep, g0_), tag_i8(b_, vkeep, g1_), m1[G][q], m2[G][q]);    \
         }                                                                                    \
     } while (0)
-    // ring: tile g lives in slot g % 4; at tile g issue tile g + 3 into the slot read at g - 1
-#define I8_SLOT(J, C0, C1, F0, F1, FOLD)                                                     \
+    // one row group's MFMAs over the whole K of the tile in slot J (fragments re-read per group)
+#define I8_MMA(J, G0, G1)                                                                    \
+    do {                                                                                     \
+        const char *base = lds + (J) * M_SLOT + rdb;                                         \
+        int xs_ = xsw;                                                                       \
+        asm volatile("" : "+v"(xs_)); /* per-use offsets: not 8 loop-invariant VGPRs */      \
+        _Pragma("unroll") for (int h_ = 0; h_ < KD / 32 / I8_KSTEP; h_++) {                  \
+            i32x4 b0_[I8_KSTEP], b1_[I8_KSTEP];                                              \
+            _Pragma("unroll") for (int u_ = 0; u_ < I8_KSTEP; u_++) {                        \
+                const int ch_ = ((2 * (I8_KSTEP * h_ + u_)) ^ xs_) * 16;                     \
+                b0_[u_] = *reinterpret_cast<const i32x4 *>(base + ch_);                      \
+                b1_[u_] = *reinterpret_cast<const i32x4 *>(base + 32 * KD + ch_);            \
+            }                                                                                \
+            _Pragma("unroll") for (int u_ = 0; u_ < I8_KSTEP; u_++) {                        \
+                const int s_ = I8_KSTEP * h_ + u_;                                           \
+                _Pragma("unroll") for (int G = (G0); G < (G1); G++) {                        \
+                    if (I8_NOMFMA) {                                                         \
+                        acc[G][0][s_] ^= b0_[u_][0];                                         \
+                        acc[G][1][s_] ^= b1_[u_][1];                                         \
+                    } else {                                                                 \
+                        acc[G][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][s_], b0_[u_], \
+                                                                          s_ == 0 ? magic16 : acc[G][0], 0, 0, 0); \
+                        acc[G][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][s_], b1_[u_], \
+                                                                          s_ == 0 ? magic16 : acc[G][1], 0, 0, 0); \
+                    }                                                                        \
+                }                                                                            \
+            }                                                                                \
+        }                                                                                    \
+    } while (0)
+    // ring: tile g lives in slot g % 4; at tile g issue tile g + 3 into the slot read at g - 1.
+    // Group 0's MFMAs run beside the fold of group 1 of the previous tile, group 1's beside
+    // the fold of group 0 of this tile.
+    float rp0 = 0.f, rp1 = 0.f;  // previous tile's norms
+#define I8_SLOT(J)                                                                           \
     do {                                                                                     \
         const int tc = T + (J);                                                              \
         const int ntile = tc + M_NBUF - 1;                                                   \
@@ -271,32 +311,24 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
             I8_OFFSETS(ntile);                                                               \
             if (!I8_NODMA) I8_STAGE((J + M_NBUF - 1) % M_NBUF);                              \
         }                                                                                    \
-        const char *base = lds + (J) * M_SLOT + rdb;                                         \
-        _Pragma("unroll") for (int h_ = 0; h_ < 2; h_++) { /* K halves: 32 fragment VGPRs */ \
-            i32x4 b0_[KD / 64], b1_[KD / 64];                                                \
-            _Pragma("unroll") for (int u_ = 0; u_ < KD / 64; u_++) {                         \
-                const int ch_ = ((2 * (4 * h_ + u_)) ^ xsw) * 16;                            \
-                b0_[u_] = *reinterpret_cast<const i32x4 *>(base + ch_);                      \
-                b1_[u_] = *reinterpret_cast<const i32x4 *>(base + 32 * KD + ch_);            \
-            }                                                                                \
-            _Pragma("unroll") for (int u_ = 0; u_ < KD / 64; u_++) {                         \
-                const int s_ = 4 * h_ + u_;                                                  \
-                if (I8_NOMFMA) {                                                             \
-                    C0[s_] ^= b0_[u_][0];                                                    \
-                    C1[s_] ^= b1_[u_][1];                                                    \
-                } else {                                                                     \
-                C0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[s_], b0_[u_], s_ == 0 ? magic16 : C0, 0, 0, 0); \
-                C1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[s_], b1_[u_], s_ == 0 ? magic16 : C1, 0, 0, 0); \
-                }                                                                            \
-            }                                                                                \
-            if (h_ == 0) asm volatile("" ::: "memory");                                      \
+        if (I8_PIPE) {                                                                       \
+            I8_MMA(J, 0, 1);                                                                 \
+            if (tc > 0) I8_FOLD(1, tc - 1, rp0, rp1);                                        \
+        } else {                                                                             \
+            I8_MMA(J, 0, M_RG);                                                              \
         }                                                                                    \
-        if (FOLD) I8_FOLD(F0, F1, tc - 1, false); /* previous tile, beside these MFMAs */     \
+        float r0_, r1_;                                                                      \
         {                                                                                    \
             const float *rl_ = reinterpret_cast<const float *>(lds + (J) * M_SLOT + M_TILE); \
-            rp0 = rl_[fr];                                                                   \
-            rp1 = rl_[fr + 32];                                                              \
+            const int col_ = tc * M_BN + fr;                                                 \
+            r0_ = col_ < n1 ? rl_[fr] : 0.f;                                                 \
+            r1_ = col_ + 32 < n1 ? rl_[fr + 32] : 0.f;                                       \
         }                                                                                    \
+        if (I8_PIPE) I8_MMA(J, 1, 2);                                                        \
+        I8_FOLD(0, tc, r0_, r1_);                                                            \
+        if (!I8_PIPE) I8_FOLD(1, tc, r0_, r1_);                                              \
+        rp0 = r0_;                                                                           \
+        rp1 = r1_;                                                                           \
         if (ntile < ntc) {                                                                   \
             wait_vm_i8<5 * (M_NBUF - 2)>();                                                  \
         } else {                                                                             \
@@ -316,82 +348,79 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
     __syncthreads();
     I8_STAMP(2);
     for (int T = 0; T < ntc; T += 4) {
-        I8_SLOT(0, accA0, accA1, accB0, accB1, T > 0);
-        if (T + 1 < ntc) I8_SLOT(1, accB0, accB1, accA0, accA1, true);
-        if (T + 2 < ntc) I8_SLOT(2, accA0, accA1, accB0, accB1, true);
-        if (T + 3 < ntc) I8_SLOT(3, accB0, accB1, accA0, accA1, true);
+        I8_SLOT(0);
+        if (T + 1 < ntc) I8_SLOT(1);
+        if (T + 2 < ntc) I8_SLOT(2);
+        if (T + 3 < ntc) I8_SLOT(3);
     }
     I8_STAMP(3);
-    if (ntc > 0) {  // the last tile (masked past n1 inside the fold)
-        const int tl = ntc - 1;
-        if (tl & 1)
-            I8_FOLD(accB0, accB1, tl, true);
-        else
-            I8_FOLD(accA0, accA1, tl, true);
-    }
+    if (I8_PIPE) I8_FOLD(1, ntc - 1, rp0, rp1);  // the last tile's group 1
 #undef I8_STAGE
 #undef I8_OFFSETS
 #undef I8_FOLD
+#undef I8_MMA
 #undef I8_SLOT
 
-    // ---- per row, merge the 32 lanes' (m1, m2): transposed through LDS (the ring is free
-    //      now; the wave reads back only what it wrote: no block barrier in the epilogue).
-    //      Row r of the wave gets its lanes' entries [r][e] (e = the lane = the column within
-    //      the tag's half); lane (fr, fh) folds entries 16 fh .. 16 fh + 15 of row fr, and the
-    //      two halves combine: lanes fr and fr + 32 end with row fr's (M, E, M2), which is
-    //      where the row's A halves are (aI) ----
     // the tag moved each f by < 2^(tb-23) relative and the screen itself is within 2e-7 of
     // dot/|b|: a column below M (1 - 2^(tb-21)) cannot be (or tie) the true maximiser
     const float keep_frac = 1.0f - __builtin_ldexpf(1.0f, tb - 21);
     char *mt = lds + w * 32 * MT_STRIDE;
+    int *clist = reinterpret_cast<int *>(lds + M_OFF_CL);      // [BM][NCAND]
+    unsigned *lmask = reinterpret_cast<unsigned *>(lds + M_OFF_LM);  // [BM] deep rows' entries
+    unsigned deep_rows[M_RG];
 #pragma unroll
-    for (int q = 0; q < 16; q++) {
-        const int r = (q & 3) + 8 * (q >> 2) + 4 * fh;
-        float2 v;
-        v.x = m1[q];
-        v.y = m2[q];
-        *reinterpret_cast<float2 *>(mt + r * MT_STRIDE + fr * 8) = v;
-    }
-    float e1[16], e2[16];
+    for (int g = 0; g < M_RG; g++) {
+        // ---- per row, merge the 32 lanes' (m1, m2): transposed through LDS (the ring is free
+        //      now; the wave reads back only what it wrote: no block barrier in the epilogue).
+        //      Row r of the group gets its lanes' entries [r][e] (e = the lane = the column
+        //      within the tag's half); lane (fr, fh) folds entries 16 fh .. +15 of row fr, and
+        //      the two halves combine: lanes fr and fr + 32 end with row fr's (M, E, M2),
+        //      which is where the row's A halves are (aI[g]) ----
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const float4 v = *reinterpret_cast<const float4 *>(mt + fr * MT_STRIDE + (fh * 16 + 2 * i) * 8);
-        e1[2 * i] = v.x;
-        e2[2 * i] = v.y;
-        e1[2 * i + 1] = v.z;
-        e2[2 * i + 1] = v.w;
-    }
-    float M = -__builtin_inff(), M2 = -__builtin_inff();
-    int E = 0;
+        for (int q = 0; q < 16; q++) {
+            const int r = (q & 3) + 8 * (q >> 2) + 4 * fh;
+            float2 v;
+            v.x = m1[g][q];
+            v.y = m2[g][q];
+            *reinterpret_cast<float2 *>(mt + r * MT_STRIDE + fr * 8) = v;
+        }
+        float e1[16], e2[16];
 #pragma unroll
-    for (int i = 0; i < 16; i++) {  // equal maxima land in M2: ambiguous
-        M2 = fmaxf(fmaxf(M2, e2[i]), fminf(M, e1[i]));
-        E = e1[i] > M ? fh * 16 + i : E;
-        M = fmaxf(M, e1[i]);
-    }
-    {
-        const float oM = __shfl_xor(M, 32, 64), oM2 = __shfl_xor(M2, 32, 64);
-        const int oE = __shfl_xor(E, 32, 64);
-        M2 = fmaxf(fmaxf(M2, oM2), fminf(M, oM));
-        E = (oM > M || (oM == M && oE < E)) ? oE : E;
-        M = fmaxf(M, oM);
-    }
+        for (int i = 0; i < 8; i++) {
+            const float4 v = *reinterpret_cast<const float4 *>(mt + fr * MT_STRIDE + (fh * 16 + 2 * i) * 8);
+            e1[2 * i] = v.x;
+            e2[2 * i] = v.y;
+            e1[2 * i + 1] = v.z;
+            e2[2 * i + 1] = v.w;
+        }
+        float M = -__builtin_inff(), M2 = -__builtin_inff();
+        int E = 0;
+#pragma unroll
+        for (int i = 0; i < 16; i++) {  // equal maxima land in M2: ambiguous
+            M2 = fmaxf(fmaxf(M2, e2[i]), fminf(M, e1[i]));
+            E = e1[i] > M ? fh * 16 + i : E;
+            M = fmaxf(M, e1[i]);
+        }
+        {
+            const float oM = __shfl_xor(M, 32, 64), oM2 = __shfl_xor(M2, 32, 64);
+            const int oE = __shfl_xor(E, 32, 64);
+            M2 = fmaxf(fmaxf(M2, oM2), fminf(M, oM));
+            E = (oM > M || (oM == M && oE < E)) ? oE : E;
+            M = fmaxf(M, oM);
+        }
+        if (g == 0) I8_STAMP(4);
 
-    I8_STAMP(4);
-    // ---- decide row w*32 + fr in its own two lanes: exact integer dots with the screen
-    //      maximiser, or -- runner-up inside the window -- with the maximum of every entry
-    //      (lane) inside; if some entry holds TWO columns inside (its m2 too), every column of
-    //      every inside entry is a candidate ("deep" row, below) ----
-    int *clist = reinterpret_cast<int *>(lds + M_NW * 32 * MT_STRIDE);  // [BM][32]
-    unsigned *lmask = reinterpret_cast<unsigned *>(clist + M_BM * 32);  // [BM] deep rows' entries
-    unsigned deep_rows;
-    {
-        const int rl = w * 32 + fr;
+        // ---- decide the row in its own two lanes: exact integer dots with the screen
+        //      maximiser, or -- runner-up inside the window -- with the maximum of every entry
+        //      (lane) inside; if some entry holds TWO columns inside (its m2 too), or more than
+        //      NCAND entries are inside, every column of every inside entry is a candidate
+        //      ("deep" row, below) ----
+        const int rl = w * 64 + g * 32 + fr;
         const bool live = row0 + rl < n0;
 #ifdef I8_EXP_NOEXACT
         const bool cand = false;
 #else
-        const bool cand = live && na_r > 0 && M > 1e-30f;  // else every dot <= 0 (tagged zeros are subnormal)
+        const bool cand = live && na_r[g] > 0 && M > 1e-30f;  // else every dot <= 0 (tagged zeros are subnormal)
 #endif
         const float lim = M * keep_frac;
         const bool ambig = cand && M2 >= lim;
@@ -405,7 +434,7 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
             }
             const unsigned o1 = __shfl_xor(in1, 32, 64), o2 = __shfl_xor(in2, 32, 64);
             const unsigned inside = fh ? (o1 | (in1 << 16)) : (in1 | (o1 << 16));
-            if (in2 | o2) {
+            if ((in2 | o2) || __popc(inside) > M_NCAND) {
                 nc = -1;
                 if (fh == 0) lmask[rl] = inside;
             } else {
@@ -415,7 +444,7 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
                 for (int i = 0; i < 16; i++)
                     if (e1[i] >= lim) {
                         const unsigned tag = __float_as_uint(e1[i]) & ~tkeep;
-                        clist[rl * 32 + k++] = (int)(tag >> 1) * M_BN + (int)(tag & 1) * 32 + fh * 16 + i;
+                        clist[rl * M_NCAND + k++] = (int)(tag >> 1) * M_BN + (int)(tag & 1) * 32 + fh * 16 + i;
                     }
             }
 #ifdef I8_EXP_PRINT
@@ -427,7 +456,7 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
         int bj = -1;
         long long bd = 0, bn = 1;
         for (int k = 0; k < nc; k++) {  // the row's two lanes run the same trip count
-            const int j = ambig ? clist[rl * 32 + k] : I;
+            const int j = ambig ? clist[rl * M_NCAND + k] : I;
             const int8_t *brow = B + (size_t)j * KD + fh * 16;
             i32x4 bv[KD / 32];
 #pragma unroll
@@ -437,7 +466,7 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
 #pragma unroll
             for (int s2 = 0; s2 < KD / 32; s2++)
 #pragma unroll
-                for (int u = 0; u < 4; u++) part = __builtin_amdgcn_sdot4(aI[s2][u], bv[s2][u], part, false);
+                for (int u = 0; u < 4; u++) part = __builtin_amdgcn_sdot4(aI[g][s2][u], bv[s2][u], part, false);
             part += __shfl_xor(part, 32, 64);
             if (part > 0 && nbj > 0 && better(part, nbj, j, bd, bn, bj)) {
                 bj = j;
@@ -446,70 +475,70 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
             }
         }
         if (fh == 0 && live && nc >= 0) {
-            const long long na = na_r;
+            const long long na = na_r[g];
             const bool keep = bj >= 0 &&
                               (unsigned __int128)(100ll * bd * bd) > (unsigned __int128)81 * (unsigned long long)(na * bn);
             oidx[rl] = keep ? bj : -1;
             odot[rl] = keep ? (int)bd : 0;
         }
-        deep_rows = (unsigned)__ballot(fh == 0 && live && nc < 0);
+        deep_rows[g] = (unsigned)__ballot(fh == 0 && live && nc < 0);
     }
     I8_STAMP(5);
 
-    // ---- deep rows (rare): the wave scores every column of every inside lane exactly,
-    //      one column per lane (lane l: column f + 32 (l + 64 i) of inside lane f) ----
+    // ---- deep rows (rare): the wave scores every column of every inside entry exactly,
+    //      one column per lane (lane l: column f + 32 (l + 64 i) of inside entry f) ----
     I8_STAMP(6);
-    while (deep_rows) {
-        const int rr = __builtin_ctz(deep_rows);
-        deep_rows &= deep_rows - 1;
-        const int rl = w * 32 + rr;
+#pragma unroll
+    for (int g = 0; g < M_RG; g++)
+        for (unsigned dm = deep_rows[g]; dm; dm &= dm - 1) {
+            const int rl = w * 64 + g * 32 + __builtin_ctz(dm);
 #ifdef I8_EXP_PRINT
-        if (lane == 0) printf("I8DEEP pair %d row %d lanes %x\n", pair, row0 + rl, lmask[rl]);
+            if (lane == 0) printf("I8DEEP pair %d row %d lanes %x\n", pair, row0 + rl, lmask[rl]);
 #endif
-        const i32x4 *arow = reinterpret_cast<const i32x4 *>(A + (size_t)(row0 + rl) * KD);
-        i32x4 av[KD / 16];
+            const i32x4 *arow = reinterpret_cast<const i32x4 *>(A + (size_t)(row0 + rl) * KD);
+            i32x4 av[KD / 16];
 #pragma unroll
-        for (int v = 0; v < KD / 16; v++) av[v] = arow[v];
-        int bj = -1;
-        long long bd = 0, bn = 1;
-        for (unsigned L = lmask[rl]; L; L &= L - 1) {
-            const int f = __builtin_ctz(L);
-            for (int j = f + 32 * lane; j < n1; j += 32 * 64) {
-                const i32x4 *brow = reinterpret_cast<const i32x4 *>(B + (size_t)j * KD);
-                i32x4 bv[KD / 16];
+            for (int v = 0; v < KD / 16; v++) av[v] = arow[v];
+            int bj = -1;
+            long long bd = 0, bn = 1;
+            for (unsigned Lm = lmask[rl]; Lm; Lm &= Lm - 1) {
+                const int f = __builtin_ctz(Lm);
+                for (int j = f + 32 * lane; j < n1; j += 32 * 64) {
+                    const i32x4 *brow = reinterpret_cast<const i32x4 *>(B + (size_t)j * KD);
+                    i32x4 bv[KD / 16];
 #pragma unroll
-                for (int v = 0; v < KD / 16; v++) bv[v] = brow[v];
-                const long long nbj = nb[j];
-                int d = 0;
+                    for (int v = 0; v < KD / 16; v++) bv[v] = brow[v];
+                    const long long nbj = nb[j];
+                    int d = 0;
 #pragma unroll
-                for (int v = 0; v < KD / 16; v++)
+                    for (int v = 0; v < KD / 16; v++)
 #pragma unroll
-                    for (int u = 0; u < 4; u++) d = __builtin_amdgcn_sdot4(av[v][u], bv[v][u], d, false);
-                if (d > 0 && nbj > 0 && better(d, nbj, j, bd, bn, bj)) {
-                    bj = j;
-                    bd = d;
-                    bn = nbj;
+                        for (int u = 0; u < 4; u++) d = __builtin_amdgcn_sdot4(av[v][u], bv[v][u], d, false);
+                    if (d > 0 && nbj > 0 && better(d, nbj, j, bd, bn, bj)) {
+                        bj = j;
+                        bd = d;
+                        bn = nbj;
+                    }
                 }
             }
-        }
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const long long od = __shfl_xor(bd, o, 64), on = __shfl_xor(bn, o, 64);
-            const int oj = __shfl_xor(bj, o, 64);
-            if (oj >= 0 && better(od, on, oj, bd, bn, bj)) {
-                bj = oj;
-                bd = od;
-                bn = on;
+            for (int o = 1; o < 64; o <<= 1) {
+                const long long od = __shfl_xor(bd, o, 64), on = __shfl_xor(bn, o, 64);
+                const int oj = __shfl_xor(bj, o, 64);
+                if (oj >= 0 && better(od, on, oj, bd, bn, bj)) {
+                    bj = oj;
+                    bd = od;
+                    bn = on;
+                }
+            }
+            if (lane == 0) {
+                const long long na = na_s[rl];
+                const bool keep = bj >= 0 &&
+                                  (unsigned __int128)(100ll * bd * bd) > (unsigned __int128)81 * (unsigned long long)(na * bn);
+                oidx[rl] = keep ? bj : -1;
+                odot[rl] = keep ? (int)bd : 0;
             }
         }
-        if (lane == 0) {
-            const long long na = na_s[rl];
-            const bool keep = bj >= 0 &&
-                              (unsigned __int128)(100ll * bd * bd) > (unsigned __int128)81 * (unsigned long long)(na * bn);
-            oidx[rl] = keep ? bj : -1;
-            odot[rl] = keep ? (int)bd : 0;
-        }
-    }
 #ifdef I8_EXP_TRACE
     I8_STAMP(7);
     if (lane == 0 && blockIdx.x < I8_TRACE_BLOCKS) {
