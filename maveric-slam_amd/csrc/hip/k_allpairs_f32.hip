@@ -83,11 +83,15 @@ static_assert(KS == 2 && NBUF == 2 * KS, "the loop body covers two column tiles 
 static_assert(RW == 32 && (NW == 4 || NW == 8), "one wave per 32 rows (32x32 MFMA), 4 or 8 waves");
 // LDS map (ONE array -- a second __shared__ object can de-pipeline the DMA), byte offsets
 constexpr int OFF_STAGE = 0;                     // [NBUF][64 B rows][256 B]
-constexpr int OFF_TRIP = NBUF * SL_BYTES;        // [256] {m1, i1, m2}
-constexpr int OFF_ANRM = OFF_TRIP + BM * 12;     // [256] f32 |a|^2 (< 0: row outside the fp16 range)
-constexpr int OFF_AMB = OFF_ANRM + BM * 4;       // [256] i32 ambiguous rows
-constexpr int OFF_MISC = OFF_AMB + BM * 4;       // [NW] f32 per-wave max|b|^2, [1] i32 #ambiguous
-constexpr int LDS_BYTES = OFF_MISC + 4 * NW + 16;
+constexpr int OFF_ANRM = NBUF * SL_BYTES;        // [BM] f32 |a|^2 (< 0: row outside the fp16 range)
+constexpr int OFF_MISC = OFF_ANRM + BM * 4;      // [NW] f32 per-wave max|b|^2
+constexpr int LDS_BYTES = OFF_MISC + 4 * NW;
+// epilogue, inside the (then free) ring
+constexpr int MT_STRIDE = 32 * 8 + 16;           // transpose row: 32 lanes' (m1, m2) + pad
+constexpr int NCAND = 16;                        // listed candidates per row (more: deep row)
+constexpr int OFF_CL = NW * 32 * MT_STRIDE;      // [BM][NCAND] candidate columns
+constexpr int OFF_LM = OFF_CL + BM * NCAND * 4;  // [BM] deep rows' inside lanes
+static_assert(OFF_LM + BM * 4 <= NBUF * SL_BYTES, "epilogue fits the ring");
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -119,68 +123,30 @@ __device__ __forceinline__ void wait_vm() {
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-// max / min straight from inline asm: the compiler otherwise quiets each operand (IEEE-mode
-// v_max_f32 x, x, x) before every min/max.  Screen values are never NaN for in-range
-// descriptors (out-of-range rows / pairs take the exact path).  Not volatile: freely scheduled.
-__device__ __forceinline__ float vmax(float a, float b) {
+// (f & keep) | tag in one instruction (keep in a VGPR: one SGPR operand only)
+__device__ __forceinline__ float tagf(float f, unsigned keep, unsigned tag) {
     float r;
-    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(keep), "s"(tag));
     return r;
 }
-__device__ __forceinline__ float vmin(float a, float b) {
-    float r;
-    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ float vmax3(float a, float b, float c) {
-    float r;
-    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
+// top-2 of {m1, m2, a, b} given m1 >= m2: m1' = max3(m1, a, b), m2' = max(m2, med3(m1, a, b))
+__device__ __forceinline__ void fold3(float a, float b, float &m1, float &m2) {
+    float md;
+    asm("v_med3_f32 %0, %1, %2, %3" : "=v"(md) : "v"(m1), "v"(a), "v"(b));
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m1) : "v"(m1), "v"(a), "v"(b));
+    asm("v_max_f32 %0, %1, %2" : "=v"(m2) : "v"(m2), "v"(md));
 }
 
-// Top-2 of a set of columns: largest value m1 at column i (lowest column on a tie) and the
-// second largest value m2 (equal to m1 on a tie).  Min/max/select only.
-struct Top2 {
-    float m1, m2;
-    int i;
-};
-__device__ __forceinline__ Top2 leaf2(float va, int ca, float vb, int cb) {  // ca < cb
-    int i = vb > va ? cb : ca;
-    asm volatile("" : "+v"(i));  // materialise: keeps later updates selects, not branches
-    return {vmax(va, vb), vmin(va, vb), i};
+// xor-shuffles within 32 lanes by ds_swizzle (immediate pattern: no lane-address VGPRs)
+template <int M>
+__device__ __forceinline__ float swz_xor(float v) {
+    static_assert(M >= 0 && M < 32, "ds_swizzle bit mode stays within 32 lanes");
+    return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), (M << 10) | 0x1F));
 }
-__device__ __forceinline__ Top2 join2(const Top2 &x, const Top2 &y) {  // x's columns < y's columns
-    const bool up = y.m1 > x.m1;
-    return {vmax(x.m1, y.m1), vmax(vmin(x.m1, y.m1), vmax(x.m2, y.m2)), up ? y.i : x.i};
-}
-// Fold one row's 2 values of a tile (columns j, j + 32; -inf past n1) into the running triple;
-// an earlier tile's column is kept on a tie (strict >).
-__device__ __forceinline__ void fold2(float v0, float v1, int j, int j32, float &m1, int &i1, float &m2) {
-    const Top2 t = leaf2(v0, j, v1, j32);
-    m2 = vmax3(vmin(m1, t.m1), m2, t.m2);
-    i1 = t.m1 > m1 ? t.i : i1;
-    m1 = vmax(m1, t.m1);
-}
-
-// Fold one row's 4 values of a tile (columns j + 32 c, c = 0..3; -inf past n1) into the running
-// triple; an earlier tile's column is kept on a tie (strict >).
-__device__ __forceinline__ void fold4(float v0, float v1, float v2, float v3, int j, float &m1, int &i1,
-                                      float &m2) {
-    const Top2 t = join2(leaf2(v0, j, v1, j + 32), leaf2(v2, j + 64, v3, j + 96));
-    m2 = vmax(vmin(m1, t.m1), vmax(m2, t.m2));
-    i1 = t.m1 > m1 ? t.i : i1;
-    m1 = vmax(m1, t.m1);
-}
-
-// order-independent merge of two (max1, idx1, max2) triples
-__device__ __forceinline__ void merge(float &m1, int &i1, float &m2, float o1, int oi, float o2) {
-    if (o1 > m1 || (o1 == m1 && oi < i1)) {
-        m2 = fmaxf(o2, m1);
-        m1 = o1;
-        i1 = oi;
-    } else {
-        m2 = fmaxf(m2, o1);
-    }
+template <int M>
+__device__ __forceinline__ int swz_xor(int v) {
+    static_assert(M >= 0 && M < 32, "ds_swizzle bit mode stays within 32 lanes");
+    return __builtin_amdgcn_ds_swizzle(v, (M << 10) | 0x1F);
 }
 
 // XCD-aware bijective remap: blocks b and b+8 share an XCD (round-robin dispatch); give
@@ -276,11 +242,8 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
                                                     double thresh, int *__restrict__ match_idx,
                                                     float *__restrict__ match_score) {
     __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
-    float *trip = reinterpret_cast<float *>(lds + OFF_TRIP);
     float *anrm = reinterpret_cast<float *>(lds + OFF_ANRM);
-    int *amb = reinterpret_cast<int *>(lds + OFF_AMB);
     float *misc = reinterpret_cast<float *>(lds + OFF_MISC);
-    int *namb_p = reinterpret_cast<int *>(lds + OFF_MISC) + NW;
 
     const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int pair = L / tiles_r, tr = L % tiles_r;
@@ -300,6 +263,22 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
     const float *A = desc0 + (size_t)pair * cap * KD;
     const float *B = desc1 + (size_t)pair * cap * KD;
     const int ntc = flagged ? 0 : (n1 + BN - 1) / BN;  // a flagged pair skips the screen
+
+    // max_j |b_j|^2 over the pair's valid columns (from k_ap_split), published by the
+    // prologue barrier
+    {
+        const float *nb2 = nrm1 + (size_t)pair * cap;
+        float bmax = 0.f;
+        for (int j = t; j < n1; j += NT) bmax = fmaxf(bmax, nb2[j]);
+        bmax = fmaxf(bmax, swz_xor<1>(bmax));
+        bmax = fmaxf(bmax, swz_xor<2>(bmax));
+        bmax = fmaxf(bmax, swz_xor<4>(bmax));
+        bmax = fmaxf(bmax, swz_xor<8>(bmax));
+        bmax = fmaxf(bmax, swz_xor<16>(bmax));
+        bmax = fmaxf(__builtin_amdgcn_readlane(__float_as_int(bmax), 0) == 0 ? 0.f : __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bmax), 0)),
+                     __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bmax), 32)));
+        if (lane == 0) misc[w] = bmax;
+    }
 
     // ---- A: this wave's 32 rows x 256 k, fp32 -> 2^14-scaled fp16 straight into registers
     //      (v_mfma_f32_32x32x16_f16 A operand: lane l holds row l & 31, k = 16 s + 8 (l >> 5)
@@ -369,32 +348,38 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
     const int rdb = fr * SL_ROW;
     const int xsw = fh ^ (fr & 15);  // chunk(2 s + fh) ^ (fr & 15) = 2 s ^ xsw
 
+    // ---- running per-row top-2 (m1, m2) of TAGGED screen values: the low tb bits of each
+    //      value are replaced by its column's tag 2 tc + half (the lane's own index gives the
+    //      column within the half), so the fold needs no index registers ----
     const f32x16 zero16 = {};
     float m1[16], m2[16];
-    int i1[16];
 #pragma unroll
     for (int q = 0; q < 16; q++) {
         m1[q] = -__builtin_inff();
         m2[q] = -__builtin_inff();
-        i1[q] = 0x7fffffff;
     }
+    const int tb = 2 * ntc <= 256 ? 8 : 32 - __builtin_clz(2 * ntc - 1);
+    const unsigned tkeep = ~((1u << tb) - 1u);
+    unsigned vkeep = tkeep;
+    asm volatile("" : "+v"(vkeep));
 
     // Ring schedule: the loop body covers tiles T and T+1 = slices g = 2T .. 2T+3 in slots
     // J = 0..3.  At slot J the block issues slice g + 3 (tile T + (J+3)/2, k-slice (J+3)%2)
     // into slot (J+3)%4 -- the slot read at g - 1, freed by that slice's barrier -- computes
     // slot J, then waits until slice g + 1 has landed (the two later groups may stay in flight).
     // Tiles alternate between two accumulator pairs (A: even tiles, B: odd tiles); a tile is
-    // folded into the triples during the FIRST slot of the next tile, so the fold's VALU work
-    // interleaves with that slot's MFMAs.  The sweep's last tile (the only one that can reach
-    // past n1) is folded after the loop, with the -inf mask.
+    // folded during the FIRST slot of the next tile, so the fold's VALU work interleaves with
+    // that slot's MFMAs.  The sweep's last tile (the only one that can reach past n1) is
+    // folded after the loop, masked.
     f32x16 accA0 = zero16, accA1 = zero16, accB0 = zero16, accB1 = zero16;
 #define AP_FOLD(X0, X1, TC)                                                                   \
     do {                                                                                      \
-        const int col_ = (TC) * BN + fr, col32_ = col_ + 32;                                  \
+        const unsigned g0_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)(TC)), g1_ = g0_ + 1u; \
         if (!AP_EXP_NOFOLD)                                                                   \
-            _Pragma("unroll") for (int q = 0; q < 16; q++) fold2(X0[q], X1[q], col_, col32_, m1[q], i1[q], m2[q]); \
+            _Pragma("unroll") for (int q = 0; q < 16; q++)                                    \
+                fold3(tagf(X0[q], vkeep, g0_), tagf(X1[q], vkeep, g1_), m1[q], m2[q]);        \
         else /* timing experiment: keep the MFMAs live at 1/16 of the fold's VALU work */      \
-            fold2(X0[0] + X0[5] + X0[10] + X0[15], X1[0] + X1[5] + X1[10] + X1[15], col_, col32_, m1[0], i1[0], m2[0]); \
+            fold3(X0[0] + X0[5] + X0[10] + X0[15], X1[0] + X1[5] + X1[10] + X1[15], m1[0], m2[0]); \
     } while (0)
 #define AP_SLOT(J, C0, C1, F0, F1, FOLD)                                                      \
     do {                                                                                      \
@@ -445,6 +430,9 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
     }
     wait_vm<0>();
     __syncthreads();
+    float bmax2 = misc[0];
+#pragma unroll
+    for (int k = 1; k < NW; k++) bmax2 = fmaxf(bmax2, misc[k]);
     for (int T = 0; T < ntc; T += 2) {
         AP_SLOT(0, accA0, accA1, accB0, accB1, T > 0);
         AP_SLOT(1, accA0, accA1, accB0, accB1, false);
@@ -453,12 +441,12 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
             AP_SLOT(3, accB0, accB1, accA0, accA1, false);
         }
     }
-    if (ntc > 0) {  // the last tile: mask columns past n1 (+ 0 keeps, + -inf drops), fold
+    if (ntc > 0) {  // the last tile: columns past n1 pushed to a finite -3e38 (a tag keeps it finite)
         const int tl = ntc - 1;
         f32x16 x0 = (tl & 1) ? accB0 : accA0, x1 = (tl & 1) ? accB1 : accA1;
         const int col = tl * BN + fr;
-        const float lo0 = col < n1 ? 0.f : -__builtin_inff();
-        const float lo1 = col + 32 < n1 ? 0.f : -__builtin_inff();
+        const float lo0 = col < n1 ? 0.f : -3.0e38f;
+        const float lo1 = col + 32 < n1 ? 0.f : -3.0e38f;
 #pragma unroll
         for (int q = 0; q < 16; q++) {
             x0[q] += lo0;
@@ -471,103 +459,175 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
 #undef AP_FOLD
 #undef AP_TILE_OFFSETS
 
-    // ---- merge the triples across the 32 lanes (columns) that share a row ----
+    // ---- per row, merge the 32 lanes' (m1, m2): transposed through LDS (the ring is free;
+    //      the wave reads back only what it wrote: the epilogue has no block barrier).  Row r
+    //      gets its lanes' entries [r][e] (e = the lane = the column within the tag's half);
+    //      lane (fr, fh) folds entries 16 fh .. +15 of row fr and the halves combine: lanes
+    //      fr and fr + 32 end with row fr's (M, E, M2) ----
+    char *mt = lds + w * 32 * MT_STRIDE;
 #pragma unroll
     for (int q = 0; q < 16; q++) {
-        float a1 = m1[q], a2 = m2[q];
-        int ai = i1[q];
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) {
-            const float b1 = __shfl_xor(a1, o, 64), b2 = __shfl_xor(a2, o, 64);
-            const int bi = __shfl_xor(ai, o, 64);
-            merge(a1, ai, a2, b1, bi, b2);
-        }
-        if (fr == 0) {
-            const int row = w * RW + (q & 3) + 8 * (q >> 2) + 4 * fh;  // 32x32 C/D row map
-            float *tp = trip + row * 3;
-            tp[0] = a1;
-            reinterpret_cast<int *>(tp)[1] = ai;
-            tp[2] = a2;
-        }
+        const int r = (q & 3) + 8 * (q >> 2) + 4 * fh;  // 32x32 C/D row map
+        float2 v;
+        v.x = m1[q];
+        v.y = m2[q];
+        *reinterpret_cast<float2 *>(mt + r * MT_STRIDE + fr * 8) = v;
     }
-    // max_j |b_j|^2 over the pair's valid columns (from k_ap_split)
-    const float *nb2 = nrm1 + (size_t)pair * cap;
-    float bmax = 0.f;
-    for (int j = t; j < n1; j += NT) bmax = fmaxf(bmax, nb2[j]);
+    float e1[16], e2[16];
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) bmax = fmaxf(bmax, __shfl_xor(bmax, o, 64));
-    if (lane == 0) misc[w] = bmax;
-    if (t == 0) *namb_p = 0;
-    __syncthreads();
-    float bmax2 = misc[0];
+    for (int i = 0; i < 8; i++) {
+        const float4 v = *reinterpret_cast<const float4 *>(mt + fr * MT_STRIDE + (fh * 16 + 2 * i) * 8);
+        e1[2 * i] = v.x;
+        e2[2 * i] = v.y;
+        e1[2 * i + 1] = v.z;
+        e2[2 * i + 1] = v.w;
+    }
+    float M = -__builtin_inff(), M2 = -__builtin_inff();
+    int E = 0;
 #pragma unroll
-    for (int k = 1; k < NW; k++) bmax2 = fmaxf(bmax2, misc[k]);
+    for (int i = 0; i < 16; i++) {  // equal maxima land in M2: ambiguous
+        M2 = fmaxf(fmaxf(M2, e2[i]), fminf(M, e1[i]));
+        E = e1[i] > M ? fh * 16 + i : E;
+        M = fmaxf(M, e1[i]);
+    }
+    {
+        const float oM = __shfl_xor(M, 32, 64), oM2 = __shfl_xor(M2, 32, 64);
+        const int oE = __shfl_xor(E, 32, 64);
+        M2 = fmaxf(fmaxf(M2, oM2), fminf(M, oM));
+        E = (oM > M || (oM == M && oE < E)) ? oE : E;
+        M = fmaxf(M, oM);
+    }
 
-    // ---- exact re-score, fast path: the screen maximiser is the only possible maximiser ----
+    // ---- decide row w*32 + fr in its two lanes.  Window (unscaled): delta bounds screen vs
+    //      exact score per column; a tag moves a value by < rho |value|, rho = 2^(tb-23), so
+    //      dp = delta + 2.2 rho (|M| + 2 delta) bounds |tagged screen - exact| for every column
+    //      that can compete with the maximiser.  Ms + dp <= thresh: no column can pass; a
+    //      runner-up below Ms - 2 dp: the screen maximiser I is the reference's maximiser (ties
+    //      included) and one exact dot decides; otherwise the columns inside the window are
+    //      listed (each lane's maximum) and scored exactly; a lane with TWO values inside (its
+    //      m2 too), more than NCAND lanes inside, a row outside the fp16 range or a flagged
+    //      pair takes the wave-wide exact scan ("wide" rows, below). ----
+    int *clist = reinterpret_cast<int *>(lds + OFF_CL);
+    unsigned *lmask = reinterpret_cast<unsigned *>(lds + OFF_LM);
     const double u24 = 5.9604644775390625e-08, u23 = 2 * u24;
     const double gam_e = KD * u24 / (1.0 - KD * u24);
     const double gam_s = KD * u23 / (1.0 - KD * u23);
     const double rel = 9.765625e-04 + 2.384185791015625e-07 + 1.01 * gam_s + gam_e;  // 2^-10 + 2^-22 + ...
     const double Bn = sqrt((double)bmax2);
-    if (t < BM && row0 + t < n0) {
-        const float *tp = trip + t * 3;
-        const float M = tp[0], M2 = tp[2];
-        const int I = reinterpret_cast<const int *>(tp)[1];
-        const float an2 = anrm[t];
+    const double rho = ldexp(1.0, tb - 23);
+    const int rl = w * RW + fr;
+    const bool live = row0 + rl < n0;
+    const float an2 = anrm[rl];
+    const bool full = flagged || an2 < 0.f;  // outside the fp16 screen's range: exact scan
+    const float *arow = A + (size_t)(row0 + rl) * KD;
+    float bs = -__builtin_inff();
+    int bj = 0x7fffffff;
+    bool wide = live && full;
+    if (wide && fh == 0) lmask[rl] = 0xffffffffu;
+    if (live && !full) {
         const double an = sqrt(fmax((double)an2, 0.0));
         const double delta =
             (rel * an * Bn + 1.001 * 5.9604644775390625e-08 * (an + Bn) + 3.552713678800501e-15) * 1.01 + 1e-30;
         const double Ms = (double)M * 3.725290298461914e-09;  // screen / 2^28
         const double M2s = (double)M2 * 3.725290298461914e-09;
-        int best = -1;
-        float bs = 0.f;
-        bool ambiguous = flagged || an2 < 0.f;  // outside the fp16 screen's range: exact path
-        if (!ambiguous && Ms + delta > thresh) {
-            if (M2s >= Ms - 2.0 * delta) {
-                ambiguous = true;
-            } else {
-                const float e = AP_EXP_NOEXACT ? M : exact_dot(A + (size_t)(row0 + t) * KD, B + (size_t)I * KD);
-                if ((double)e > thresh && e > 0.f) {
-                    bs = e;
-                    best = I;
+        const double dp = delta + 2.2 * rho * (fabs(Ms) + 2.0 * delta);
+        if (Ms + dp > thresh) {
+            if (M2s < Ms - 2.0 * dp) {
+                if (fh == 0) {
+                    const unsigned tg = __float_as_uint(M) & ~tkeep;
+                    const int I = (int)(tg >> 1) * BN + (int)(tg & 1) * 32 + E;
+                    bs = AP_EXP_NOEXACT ? M : exact_dot(arow, B + (size_t)I * KD);
+                    bj = I;
+                }
+            } else {  // both lanes of the row take this branch
+                const double lim = (Ms - 2.0 * dp) * 268435456.0;
+                unsigned in1 = 0, in2 = 0;
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    in1 |= ((double)e1[i] >= lim ? 1u : 0u) << i;
+                    in2 |= ((double)e2[i] >= lim ? 1u : 0u) << i;
+                }
+                const unsigned o1 = __shfl_xor(in1, 32, 64), o2 = __shfl_xor(in2, 32, 64);
+                const unsigned inside = fh ? (o1 | (in1 << 16)) : (in1 | (o1 << 16));
+                if ((in2 | o2) || __popc(inside) > NCAND) {
+                    wide = true;
+                    if (fh == 0) lmask[rl] = inside;
+                } else {
+                    int k = fh ? __popc(o1) : 0;
+#pragma unroll
+                    for (int i = 0; i < 16; i++)
+                        if ((double)e1[i] >= lim) {
+                            const unsigned tg = __float_as_uint(e1[i]) & ~tkeep;
+                            clist[rl * NCAND + k++] = (int)(tg >> 1) * BN + (int)(tg & 1) * 32 + fh * 16 + i;
+                        }
+                    const int nc = __popc(inside);
+                    for (int c = fh; c < nc; c += 2) {  // the row's two lanes split the list
+                        const int j = clist[rl * NCAND + c];
+                        const float *ap = arow;
+                        asm volatile("" : "+v"(ap));  // keep the A row's loads inside the loop
+                        const float e = exact_dot(ap, B + (size_t)j * KD);
+                        if (e > bs || (e == bs && j < bj)) {
+                            bs = e;
+                            bj = j;
+                        }
+                    }
                 }
             }
         }
-        if (ambiguous) {
-            amb[atomicAdd(namb_p, 1)] = t;
-        } else {
-            oidx[t] = best;
-            oscore[t] = best >= 0 ? bs : 0.f;
+    }
+    {
+        const float ob = __shfl_xor(bs, 32, 64);
+        const int oj = __shfl_xor(bj, 32, 64);
+        if (ob > bs || (ob == bs && oj < bj)) {
+            bs = ob;
+            bj = oj;
         }
     }
-    __syncthreads();
-    // ---- slow path: one wave re-scores every column of an ambiguous row exactly ----
-    const int namb = *namb_p;
-    for (int k = w; k < namb; k += NW) {
-        const int r = amb[k];
+    if (fh == 0 && live && !wide) {
+        const bool keep = bj != 0x7fffffff && (double)bs > thresh && bs > 0.f;
+        oidx[rl] = keep ? bj : -1;
+        oscore[rl] = keep ? bs : 0.f;
+    }
+
+    // ---- wide rows (rare): the wave scores every column of every listed lane exactly, one
+    //      column per lane at a time (lane l: columns f + 32 (l + 64 i) of inside lane f) ----
+    for (unsigned dm = (unsigned)__ballot(fh == 0 && wide); dm; dm &= dm - 1) {
+        const int r = w * RW + __builtin_ctz(dm);
         const float *a = A + (size_t)(row0 + r) * KD;
-        int best = 0x7fffffff;
-        float bs = -__builtin_inff();
-        for (int j = lane; j < n1; j += 64) {
-            const float e = exact_dot(a, B + (size_t)j * KD);
-            if (e > bs) {  // j ascending per lane: strict > keeps the first
-                bs = e;
-                best = j;
+        float ws = -__builtin_inff();
+        int wj = 0x7fffffff;
+        for (unsigned Lm = lmask[r]; Lm; Lm &= Lm - 1) {
+            const int f = __builtin_ctz(Lm);
+            for (int j = f + 32 * lane; j < n1; j += 32 * 64) {
+                const float *ap = a;
+                asm volatile("" : "+v"(ap));  // keep the A row's loads inside the loop
+                const float e = exact_dot(ap, B + (size_t)j * KD);
+                if (e > ws || (e == ws && j < wj)) {
+                    ws = e;
+                    wj = j;
+                }
             }
         }
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const float ob = __shfl_xor(bs, o, 64);
-            const int oj = __shfl_xor(best, o, 64);
-            if (ob > bs || (ob == bs && oj < best)) {
-                bs = ob;
-                best = oj;
-            }
-        }
+#define AP_WRED(O)                                                                           \
+        do {                                                                                 \
+            const float ob = O == 32 ? __shfl_xor(ws, 32, 64) : swz_xor<O & 31>(ws);         \
+            const int oj = O == 32 ? __shfl_xor(wj, 32, 64) : swz_xor<O & 31>(wj);           \
+            if (ob > ws || (ob == ws && oj < wj)) {                                          \
+                ws = ob;                                                                     \
+                wj = oj;                                                                     \
+            }                                                                                \
+        } while (0)
+        AP_WRED(1);
+        AP_WRED(2);
+        AP_WRED(4);
+        AP_WRED(8);
+        AP_WRED(16);
+        AP_WRED(32);
+#undef AP_WRED
         if (lane == 0) {
-            const bool keep = (double)bs > thresh && bs > 0.f;
-            oidx[r] = keep ? best : -1;
-            oscore[r] = keep ? bs : 0.f;
+            const bool keep = wj != 0x7fffffff && (double)ws > thresh && ws > 0.f;
+            oidx[r] = keep ? wj : -1;
+            oscore[r] = keep ? ws : 0.f;
         }
     }
 }
