@@ -157,28 +157,25 @@ __device__ __forceinline__ int xcd_remap(int b, int total) {
 }
 
 
+// The reference's sequential fp32 dot (mul then add, k = 0..255).  Latency-bound: loads go
+// out EXACT_U float4 per operand at a time (EXACT_U = 16: four round trips per dot).
+#ifndef EXACT_U
+#define EXACT_U 16
+#endif
 __device__ __forceinline__ float exact_dot(const float *__restrict__ a, const float *__restrict__ b) {
-    constexpr int U = 4;  // float4 per operand per batch
-    float4 xa[2][U], xb[2][U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-        xa[0][u] = *reinterpret_cast<const float4 *>(a + 4 * u);
-        xb[0][u] = *reinterpret_cast<const float4 *>(b + 4 * u);
-    }
+    constexpr int U = EXACT_U;
     float s = 0.f;
 #pragma unroll
     for (int bt = 0; bt < KD / (4 * U); bt++) {
-        const int cur = bt & 1;
-        if (bt + 1 < KD / (4 * U)) {
+        float4 xa[U], xb[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                xa[cur ^ 1][u] = *reinterpret_cast<const float4 *>(a + 4 * U * (bt + 1) + 4 * u);
-                xb[cur ^ 1][u] = *reinterpret_cast<const float4 *>(b + 4 * U * (bt + 1) + 4 * u);
-            }
+        for (int u = 0; u < U; u++) {
+            xa[u] = *reinterpret_cast<const float4 *>(a + 4 * U * bt + 4 * u);
+            xb[u] = *reinterpret_cast<const float4 *>(b + 4 * U * bt + 4 * u);
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const float4 x = xa[cur][u], y = xb[cur][u];
+            const float4 x = xa[u], y = xb[u];
             s = __fadd_rn(s, __fmul_rn(x.x, y.x));
             s = __fadd_rn(s, __fmul_rn(x.y, y.y));
             s = __fadd_rn(s, __fmul_rn(x.z, y.z));
@@ -524,7 +521,7 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
     int bj = 0x7fffffff;
     bool wide = live && full;
     if (wide && fh == 0) lmask[rl] = 0xffffffffu;
-    if (live && !full) {
+    if (live && !full && !AP_EXP_NOFOLD) {  // (the NOFOLD experiment leaves untagged values)
         const double an = sqrt(fmax((double)an2, 0.0));
         const double delta =
             (rel * an * Bn + 1.001 * 5.9604644775390625e-08 * (an + Bn) + 3.552713678800501e-15) * 1.01 + 1e-30;
@@ -533,19 +530,25 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
         const double dp = delta + 2.2 * rho * (fabs(Ms) + 2.0 * delta);
         if (Ms + dp > thresh) {
             if (M2s < Ms - 2.0 * dp) {
-                if (fh == 0) {
-                    const unsigned tg = __float_as_uint(M) & ~tkeep;
-                    const int I = (int)(tg >> 1) * BN + (int)(tg & 1) * 32 + E;
+                const unsigned tg = __float_as_uint(M) & ~tkeep;
+                const int I = (int)(tg >> 1) * BN + (int)(tg & 1) * 32 + E;
+                if (I >= n1) {  // cannot happen for a tagged in-range maximum; never read past n1
+                    wide = true;
+                    if (fh == 0) lmask[rl] = 0xffffffffu;
+                } else if (fh == 0) {
                     bs = AP_EXP_NOEXACT ? M : exact_dot(arow, B + (size_t)I * KD);
                     bj = I;
                 }
             } else {  // both lanes of the row take this branch
                 const double lim = (Ms - 2.0 * dp) * 268435456.0;
+                // padding columns (past n1: the last tile's -3e38) are never candidates; a
+                // padding entry's m2 can only be padding too
+                const float pad_hi = -1.0e38f;
                 unsigned in1 = 0, in2 = 0;
 #pragma unroll
                 for (int i = 0; i < 16; i++) {
-                    in1 |= ((double)e1[i] >= lim ? 1u : 0u) << i;
-                    in2 |= ((double)e2[i] >= lim ? 1u : 0u) << i;
+                    in1 |= ((double)e1[i] >= lim && e1[i] > pad_hi ? 1u : 0u) << i;
+                    in2 |= ((double)e2[i] >= lim && e2[i] > pad_hi ? 1u : 0u) << i;
                 }
                 const unsigned o1 = __shfl_xor(in1, 32, 64), o2 = __shfl_xor(in2, 32, 64);
                 const unsigned inside = fh ? (o1 | (in1 << 16)) : (in1 | (o1 << 16));
@@ -556,7 +559,7 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
                     int k = fh ? __popc(o1) : 0;
 #pragma unroll
                     for (int i = 0; i < 16; i++)
-                        if ((double)e1[i] >= lim) {
+                        if ((in1 >> i) & 1u) {
                             const unsigned tg = __float_as_uint(e1[i]) & ~tkeep;
                             clist[rl * NCAND + k++] = (int)(tg >> 1) * BN + (int)(tg & 1) * 32 + fh * 16 + i;
                         }
