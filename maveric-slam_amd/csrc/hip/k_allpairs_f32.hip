@@ -185,50 +185,57 @@ __device__ __forceinline__ float exact_dot(const float *__restrict__ a, const fl
     return s;
 }
 
-// ---- k_ap_split: frame 1 only.  32 lanes per row, 8 consecutive floats per lane (two
-//      16-B loads, one 16-B store); a 256-thread block converts 16 rows per iteration and
-//      strides over the batch (rows >= n1 are never read downstream) ----
-constexpr int SPLIT_ROWS = 16;  // rows per block iteration: 8 row groups x 2
-__device__ __forceinline__ void split_row(long R, int live, int pair, int sub, const float4 &x, const float4 &y,
-                                          char *__restrict__ h1, float *__restrict__ nrm1, int *__restrict__ bad) {
-    const int out = (int)!(fabsf(x.x) < 2.f) | (int)!(fabsf(x.y) < 2.f) | (int)!(fabsf(x.z) < 2.f) |
-                    (int)!(fabsf(x.w) < 2.f) | (int)!(fabsf(y.x) < 2.f) | (int)!(fabsf(y.y) < 2.f) |
-                    (int)!(fabsf(y.z) < 2.f) | (int)!(fabsf(y.w) < 2.f);  // NaN: out of range
-    float q = fmaf(x.x, x.x, fmaf(x.y, x.y, fmaf(x.z, x.z, x.w * x.w)));
-    q = fmaf(y.x, y.x, fmaf(y.y, y.y, fmaf(y.z, y.z, fmaf(y.w, y.w, q))));
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) q += __shfl_xor(q, o, 64);  // the row's 32 lanes
-    if (live) {
-        const f16x8 h = {(_Float16)(x.x * SCALE), (_Float16)(x.y * SCALE), (_Float16)(x.z * SCALE),
-                         (_Float16)(x.w * SCALE), (_Float16)(y.x * SCALE), (_Float16)(y.y * SCALE),
-                         (_Float16)(y.z * SCALE), (_Float16)(y.w * SCALE)};  // exact 2^14 scale, RNE
-        *reinterpret_cast<f16x8 *>(h1 + R * ROW_BYTES + sub * 16) = h;
-        if (out) bad[pair] = 1;
-        if (sub == 0) nrm1[R] = q;
-    }
-}
+// ---- k_ap_split: frame 1 only.  32 lanes per row: lane l converts floats 4l .. 4l+3 and
+//      128 + 4l .. +3 (each load instruction reads 512 contiguous bytes of two rows; each
+//      8-B store writes 256 contiguous bytes); SPLIT_RPG rows per lane group per iteration,
+//      all loads issued first; a 256-thread block strides over the batch (rows >= n1 are
+//      never read downstream) ----
+#ifndef SPLIT_RPG
+#define SPLIT_RPG 4
+#endif
+constexpr int SPLIT_ROWS = 8 * SPLIT_RPG;  // rows per block iteration: 8 row groups x SPLIT_RPG
+typedef float f32x4v __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void k_ap_split(int batch, int cap, const int *__restrict__ n1v,
                                                   const float *__restrict__ desc1, char *__restrict__ h1,
                                                   float *__restrict__ nrm1, int *__restrict__ bad) {
     const long rows = (long)batch * cap;
-    const int sub = threadIdx.x & 31, rl = threadIdx.x >> 5;
-    typedef float f32x4v __attribute__((ext_vector_type(4)));
+    const int sub = threadIdx.x & 31, rg = threadIdx.x >> 5;
     for (long R0 = (long)blockIdx.x * SPLIT_ROWS; R0 < rows; R0 += (long)gridDim.x * SPLIT_ROWS) {
-        // two rows per lane group, all four 16-B loads issued before any use; rows past n1
-        // are inside the cap stride, so they are read unconditionally and only not stored
-        const long Ra = R0 + rl, Rb = R0 + 8 + rl;
-        const long ca = Ra < rows ? Ra : rows - 1, cb = Rb < rows ? Rb : rows - 1;
-        const f32x4v u0 = __builtin_nontemporal_load(reinterpret_cast<const f32x4v *>(desc1 + ca * KD + sub * 8));
-        const f32x4v v0 = __builtin_nontemporal_load(reinterpret_cast<const f32x4v *>(desc1 + ca * KD + sub * 8 + 4));
-        const f32x4v u1 = __builtin_nontemporal_load(reinterpret_cast<const f32x4v *>(desc1 + cb * KD + sub * 8));
-        const f32x4v v1 = __builtin_nontemporal_load(reinterpret_cast<const f32x4v *>(desc1 + cb * KD + sub * 8 + 4));
-        const int pa = (int)(ca / cap), pb = (int)(cb / cap);
-        const int la = Ra < rows && (int)(ca - (long)pa * cap) < n1v[pa];
-        const int lb = Rb < rows && (int)(cb - (long)pb * cap) < n1v[pb];
-        split_row(ca, la, pa, sub, make_float4(u0[0], u0[1], u0[2], u0[3]), make_float4(v0[0], v0[1], v0[2], v0[3]),
-                  h1, nrm1, bad);
-        split_row(cb, lb, pb, sub, make_float4(u1[0], u1[1], u1[2], u1[3]), make_float4(v1[0], v1[1], v1[2], v1[3]),
-                  h1, nrm1, bad);
+        f32x4v lo[SPLIT_RPG], hi[SPLIT_RPG];
+        long c[SPLIT_RPG];
+#pragma unroll
+        for (int r = 0; r < SPLIT_RPG; r++) {  // rows past n1 lie inside the cap stride: read, never stored
+            const long R = R0 + 8 * r + rg;
+            c[r] = R < rows ? R : rows - 1;
+            lo[r] = __builtin_nontemporal_load(reinterpret_cast<const f32x4v *>(desc1 + c[r] * KD + 4 * sub));
+            hi[r] = __builtin_nontemporal_load(reinterpret_cast<const f32x4v *>(desc1 + c[r] * KD + 128 + 4 * sub));
+        }
+#pragma unroll
+        for (int r = 0; r < SPLIT_RPG; r++) {
+            const long R = R0 + 8 * r + rg;
+            const f32x4v x = lo[r], y = hi[r];
+            const int out = (int)!(fabsf(x[0]) < 2.f) | (int)!(fabsf(x[1]) < 2.f) | (int)!(fabsf(x[2]) < 2.f) |
+                            (int)!(fabsf(x[3]) < 2.f) | (int)!(fabsf(y[0]) < 2.f) | (int)!(fabsf(y[1]) < 2.f) |
+                            (int)!(fabsf(y[2]) < 2.f) | (int)!(fabsf(y[3]) < 2.f);  // NaN: out of range
+            float q = fmaf(x[0], x[0], fmaf(x[1], x[1], fmaf(x[2], x[2], x[3] * x[3])));
+            q = fmaf(y[0], y[0], fmaf(y[1], y[1], fmaf(y[2], y[2], fmaf(y[3], y[3], q))));
+            q += swz_xor<1>(q);
+            q += swz_xor<2>(q);
+            q += swz_xor<4>(q);
+            q += swz_xor<8>(q);
+            q += swz_xor<16>(q);  // the row's 32 lanes
+            const int pair = (int)(c[r] / cap);
+            if (R < rows && (int)(c[r] - (long)pair * cap) < n1v[pair]) {
+                const f16x4 hx = {(_Float16)(x[0] * SCALE), (_Float16)(x[1] * SCALE), (_Float16)(x[2] * SCALE),
+                                  (_Float16)(x[3] * SCALE)};  // exact 2^14 scale, RNE
+                const f16x4 hy = {(_Float16)(y[0] * SCALE), (_Float16)(y[1] * SCALE), (_Float16)(y[2] * SCALE),
+                                  (_Float16)(y[3] * SCALE)};
+                *reinterpret_cast<f16x4 *>(h1 + R * ROW_BYTES + 8 * sub) = hx;
+                *reinterpret_cast<f16x4 *>(h1 + R * ROW_BYTES + 256 + 8 * sub) = hy;
+                if (out) bad[pair] = 1;
+                if (sub == 0) nrm1[R] = q;
+            }
+        }
     }
 }
 

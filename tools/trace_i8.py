@@ -26,7 +26,7 @@ ctx.reserve(B, n)
 for _ in range(3):
     ctx.match_allpairs_i8(d0, d1, nn_, nn_, idx, dot)
 torch.cuda.synchronize()
-nblk = B * (n // 128)
+nblk = B * ((n + 255) // 256)  # k_i8_match: 256 rows per block
 buf = np.zeros(nblk * 4 * 10, np.uint64)
 lib = mvtrack.lib()
 lib.mv_debug_i8_trace.argtypes = [ctypes.c_void_p, ctypes.c_long]
