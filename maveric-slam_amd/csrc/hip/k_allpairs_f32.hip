@@ -74,6 +74,10 @@ constexpr int NBUF = 4;  // ring slots: two column tiles of KS = 2 slices
 #ifndef AP_EXP_NODMA
 #define AP_EXP_NODMA 0
 #endif
+#ifdef AP_EXP_TRACE
+constexpr int AP_TRACE_BLOCKS = 16384;
+__device__ unsigned long long g_ap_trace[AP_TRACE_BLOCKS * 4 * 10];
+#endif
 constexpr int ROW_BYTES = KD * 2;                // fp16 row: 512 B
 constexpr int SL_ROW = BK * 2;                   // one row of one slice: 128 fp16 = 256 B = 16 chunks
 constexpr int SL_BYTES = BN * SL_ROW;            // one B slice: 16 KiB
@@ -81,17 +85,19 @@ constexpr int DMA_PER_SLICE = SL_BYTES / 1024 / NW;  // 1-KiB DMA instructions p
 constexpr float SCALE = 16384.f;                 // 2^14: |a_k| < 2 -> |2^14 a_k| < 2^15 < 65504
 static_assert(KS == 2 && NBUF == 2 * KS, "the loop body covers two column tiles = NBUF slices");
 static_assert(RW == 32 && (NW == 4 || NW == 8), "one wave per 32 rows (32x32 MFMA), 4 or 8 waves");
-// LDS map (ONE array -- a second __shared__ object can de-pipeline the DMA), byte offsets
+// LDS map (ONE array -- a second __shared__ object can de-pipeline the DMA), byte offsets.
+// The epilogue reuses the region of the (then free) ring.
+constexpr int MT_STRIDE = 32 * 8 + 16;           // transpose row: 32 lanes' (m1, m2) + pad
+constexpr int NCAND = 16;                        // listed candidates per row (more: wide row)
+constexpr int OFF_CL = NW * 32 * MT_STRIDE;      // [BM][NCAND] candidate columns
+constexpr int OFF_LM = OFF_CL + BM * NCAND * 4;  // [BM] wide rows' inside lanes
+constexpr int EPI_BYTES = OFF_LM + BM * 4;
 constexpr int OFF_STAGE = 0;                     // [NBUF][64 B rows][256 B]
-constexpr int OFF_ANRM = NBUF * SL_BYTES;        // [BM] f32 |a|^2 (< 0: row outside the fp16 range)
+constexpr int RING_BYTES = NBUF * SL_BYTES > EPI_BYTES ? NBUF * SL_BYTES : EPI_BYTES;
+constexpr int OFF_ANRM = RING_BYTES;             // [BM] f32 |a|^2 (< 0: row outside the fp16 range)
 constexpr int OFF_MISC = OFF_ANRM + BM * 4;      // [NW] f32 per-wave max|b|^2
 constexpr int LDS_BYTES = OFF_MISC + 4 * NW;
-// epilogue, inside the (then free) ring
-constexpr int MT_STRIDE = 32 * 8 + 16;           // transpose row: 32 lanes' (m1, m2) + pad
-constexpr int NCAND = 16;                        // listed candidates per row (more: deep row)
-constexpr int OFF_CL = NW * 32 * MT_STRIDE;      // [BM][NCAND] candidate columns
-constexpr int OFF_LM = OFF_CL + BM * NCAND * 4;  // [BM] deep rows' inside lanes
-static_assert(OFF_LM + BM * 4 <= NBUF * SL_BYTES, "epilogue fits the ring");
+static_assert(LDS_BYTES * (8 / NW) <= 160 * 1024, "LDS per CU");
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -249,6 +255,13 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
     float *anrm = reinterpret_cast<float *>(lds + OFF_ANRM);
     float *misc = reinterpret_cast<float *>(lds + OFF_MISC);
 
+#ifdef AP_EXP_TRACE
+#define AP_STAMP(K) do { __builtin_amdgcn_sched_barrier(0); ts_[K] = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
+    unsigned long long ts_[8];
+    AP_STAMP(0);
+#else
+#define AP_STAMP(K) do { } while (0)
+#endif
     const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int pair = L / tiles_r, tr = L % tiles_r;
     const int n0 = min(max(n0v[pair], 0), cap), n1 = min(max(n1v[pair], 0), cap);
@@ -284,6 +297,42 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
         if (lane == 0) misc[w] = bmax;
     }
 
+    // ---- B DMA map: wave w fills rows w*16 .. w*16+15 of each slice, 4 rows (1 KiB) per
+    //      instruction; lane l lands at row (l >> 4), chunk position l & 15 and fetches
+    //      source chunk (l & 15) ^ (row & 15) of that row (256-B rows: 16 chunks) ----
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    constexpr int RPW = BN / NW;  // slice rows each wave DMAs: 16 (4 waves) or 8 (8 waves)
+    const int dr = wu * RPW + (lane >> 4);  // (dr & 4) == 0, so (dr + 4 g) & 15 = (dr & 15) ^ 4 g
+    const unsigned dcb = (unsigned)((lane & 15) ^ (dr & 15)) * 16;
+    unsigned oB[RPW / 4];
+    const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char *)(lds + OFF_STAGE);
+    const unsigned dst_w = lds_base + (unsigned)(wu * RPW * SL_ROW);
+#define AP_STAGE(SLOT, KSI)                                                                  \
+    do {                                                                                     \
+        glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES>(SB, oB[0], dst_w);                         \
+        glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES + 4 * SL_ROW>(SB, oB[1], dst_w);            \
+        if constexpr (RPW == 16) {                                                           \
+            glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES + 8 * SL_ROW>(SB, oB[RPW / 4 - 2], dst_w);  \
+            glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES + 12 * SL_ROW>(SB, oB[RPW / 4 - 1], dst_w); \
+        }                                                                                    \
+    } while (0)
+#define AP_TILE_OFFSETS(TC)                                                                  \
+    do {                                                                                     \
+        const int nb_ = (TC) * BN + dr;                                                      \
+        _Pragma("unroll") for (int g_ = 0; g_ < RPW / 4; g_++)                               \
+            oB[g_] = (unsigned)min(nb_ + 4 * g_, n1 - 1) * ROW_BYTES + (dcb ^ (64u * g_));   \
+    } while (0)
+    AP_TILE_OFFSETS(0);
+    // prologue: slices 0, 1, 2 (tile 0 both k-slices, tile 1 k-slice 0), issued before the A
+    // rows are read so that both latencies overlap
+    if (ntc > 0) {
+        AP_STAGE(0, 0);
+        AP_STAGE(1, 1);
+        if (ntc > 1) {
+            AP_TILE_OFFSETS(1);
+            AP_STAGE(2, 0);
+        }
+    }
     // ---- A: this wave's 32 rows x 256 k, fp32 -> 2^14-scaled fp16 straight into registers
     //      (v_mfma_f32_32x32x16_f16 A operand: lane l holds row l & 31, k = 16 s + 8 (l >> 5)
     //      .. +7 at k16 step s).  |a|^2 and the fp16 range check come along. ----
@@ -320,32 +369,7 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
         if (fh == 0) anrm[w * RW + fr] = out ? -1.f : q;
     }
 
-    // ---- B DMA map: wave w fills rows w*16 .. w*16+15 of each slice, 4 rows (1 KiB) per
-    //      instruction; lane l lands at row (l >> 4), chunk position l & 15 and fetches
-    //      source chunk (l & 15) ^ (row & 15) of that row (256-B rows: 16 chunks) ----
-    const int wu = __builtin_amdgcn_readfirstlane(w);
-    constexpr int RPW = BN / NW;  // slice rows each wave DMAs: 16 (4 waves) or 8 (8 waves)
-    const int dr = wu * RPW + (lane >> 4);  // (dr & 4) == 0, so (dr + 4 g) & 15 = (dr & 15) ^ 4 g
-    const unsigned dcb = (unsigned)((lane & 15) ^ (dr & 15)) * 16;
-    unsigned oB[RPW / 4];
-    const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char *)(lds + OFF_STAGE);
-    const unsigned dst_w = lds_base + (unsigned)(wu * RPW * SL_ROW);
-#define AP_STAGE(SLOT, KSI)                                                                  \
-    do {                                                                                     \
-        glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES>(SB, oB[0], dst_w);                         \
-        glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES + 4 * SL_ROW>(SB, oB[1], dst_w);            \
-        if constexpr (RPW == 16) {                                                           \
-            glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES + 8 * SL_ROW>(SB, oB[RPW / 4 - 2], dst_w);  \
-            glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES + 12 * SL_ROW>(SB, oB[RPW / 4 - 1], dst_w); \
-        }                                                                                    \
-    } while (0)
-#define AP_TILE_OFFSETS(TC)                                                                  \
-    do {                                                                                     \
-        const int nb_ = (TC) * BN + dr;                                                      \
-        _Pragma("unroll") for (int g_ = 0; g_ < RPW / 4; g_++)                               \
-            oB[g_] = (unsigned)min(nb_ + 4 * g_, n1 - 1) * ROW_BYTES + (dcb ^ (64u * g_));   \
-    } while (0)
-    AP_TILE_OFFSETS(0);
+    AP_STAMP(1);
 
     // ---- B fragment map: column block c (0, 1) of a tile, lane l reads row 32 c + (l & 31)
     //      at chunk (2 s + (l >> 5)) ^ (row & 15) for k16 step s of the slice ----
@@ -423,17 +447,9 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
         if (!AP_EXP_NOBAR) __syncthreads();                                                   \
     } while (0)
 
-    // prologue: slices 0, 1, 2 (tile 0 both k-slices, tile 1 k-slice 0) behind the A loads
-    if (ntc > 0) {
-        AP_STAGE(0, 0);
-        AP_STAGE(1, 1);
-        if (ntc > 1) {
-            AP_TILE_OFFSETS(1);
-            AP_STAGE(2, 0);
-        }
-    }
     wait_vm<0>();
     __syncthreads();
+    AP_STAMP(2);
     float bmax2 = misc[0];
 #pragma unroll
     for (int k = 1; k < NW; k++) bmax2 = fmaxf(bmax2, misc[k]);
@@ -445,6 +461,7 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
             AP_SLOT(3, accB0, accB1, accA0, accA1, false);
         }
     }
+    AP_STAMP(3);
     if (ntc > 0) {  // the last tile: columns past n1 pushed to a finite -3e38 (a tag keeps it finite)
         const int tl = ntc - 1;
         f32x16 x0 = (tl & 1) ? accB0 : accA0, x1 = (tl & 1) ? accB1 : accA1;
@@ -502,6 +519,7 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
         M = fmaxf(M, oM);
     }
 
+    AP_STAMP(4);
     // ---- decide row w*32 + fr in its two lanes.  Window (unscaled): delta bounds screen vs
     //      exact score per column; a tag moves a value by < rho |value|, rho = 2^(tb-23), so
     //      dp = delta + 2.2 rho (|M| + 2 delta) bounds |tagged screen - exact| for every column
@@ -599,6 +617,7 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
         oscore[rl] = keep ? bs : 0.f;
     }
 
+    AP_STAMP(5);
     // ---- wide rows (rare): the wave scores every column of every listed lane exactly, one
     //      column per lane at a time (lane l: columns f + 32 (l + 64 i) of inside lane f) ----
     for (unsigned dm = (unsigned)__ballot(fh == 0 && wide); dm; dm &= dm - 1) {
@@ -640,6 +659,16 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
             oscore[r] = keep ? ws : 0.f;
         }
     }
+#ifdef AP_EXP_TRACE
+    AP_STAMP(6);
+    AP_STAMP(7);
+    if (lane == 0 && blockIdx.x < AP_TRACE_BLOCKS) {
+        unsigned long long *o = g_ap_trace + ((size_t)blockIdx.x * NW + w) * 10;
+        for (int k = 0; k < 8; k++) o[k] = ts_[k];
+        o[8] = __smid();
+        o[9] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 }
 
 }  // namespace
@@ -778,3 +807,10 @@ extern "C" int mv_match_allpairs_f32_run_dev(mv_context *ctx, int batch, int cap
     return mv::launch_allpairs_f32_match(ctx->stream, ctx->ap_scratch, batch, cap, n0, n1, desc0, desc1, thresh,
                                          match_idx, match_score);
 }
+
+#ifdef AP_EXP_TRACE
+// timing experiment only: per-(block, wave) phase stamps of the last k_ap_match launch
+extern "C" int mv_debug_ap_trace(void *host, long bytes) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ap_trace), (size_t)bytes) == hipSuccess ? 0 : -3;
+}
+#endif

@@ -7,13 +7,13 @@ mkdir -p gpurun_out
 IFS=';' read -ra VS <<< "${VARIANTS:-}"
 i=0
 for V in "${VS[@]}"; do
-  touch maveric-slam_amd/csrc/hip/k_allpairs_i8.hip
-  make -s -C maveric-slam_amd/csrc -j16 EXTRA="-DI8_EXP_TRACE $V" > gpurun_out/tv_$i.build 2>&1 || { echo "build failed: $V"; exit 2; }
-  timeout -k 10 200 python tools/trace_i8.py > gpurun_out/tv_$i.log 2>&1
+  touch maveric-slam_amd/csrc/hip/${VFILE:-k_allpairs_i8}.hip
+  make -s -C maveric-slam_amd/csrc -j16 EXTRA="${TRACE_FLAG:--DI8_EXP_TRACE} $V" > gpurun_out/tv_$i.build 2>&1 || { echo "build failed: $V"; exit 2; }
+  timeout -k 10 200 python ${TRACE:-tools/trace_i8.py} > gpurun_out/tv_$i.log 2>&1
   rc=$?
-  echo "[$V] rc=$rc $(grep -E 'loop per tile' gpurun_out/tv_$i.log) $(grep -E '^  loop ' gpurun_out/tv_$i.log)"
+  echo "[$V] rc=$rc $(grep -E "per (64-col )?tile" gpurun_out/tv_$i.log) $(grep -E "^  (loop|sweep) " gpurun_out/tv_$i.log)"
   [ $rc -eq 0 ] || exit $rc
   i=$((i+1))
 done
-touch maveric-slam_amd/csrc/hip/k_allpairs_i8.hip
+touch maveric-slam_amd/csrc/hip/${VFILE:-k_allpairs_i8}.hip
 make -s -C maveric-slam_amd/csrc -j16 > /dev/null 2>&1
