@@ -288,6 +288,7 @@ struct GlobalCands {
     __device__ __forceinline__ int dword(int x, int y, int i) const {
         return reinterpret_cast<const int *>(d0 + ((long)x * rows + y) * kDescD)[i];
     }
+    __device__ __forceinline__ const int8_t *row(int x, int y) const { return d0 + ((long)x * rows + y) * kDescD; }
 };
 // dot and squared norm of the first 64 int8 (4 chunks) against q (16 dwords)
 template <class CS>
@@ -449,6 +450,98 @@ __device__ __forceinline__ QueryResult eval_query(const WinArgs &a, const CS &C,
     return res;
 }
 
+// As-intended query (tracking_main.c:114-165 with the exact cosine), latency-shaped: the
+// validity of up to 128 window candidates is read at once (two per lane), the valid ones are
+// compacted into a wave-local LDS list, and every valid candidate is scored by 4 lanes (64 B
+// each, the query's matching 64 B held in registers): two dependent global round trips per
+// query for up to 16 valid candidates, instead of validity -> descriptor per 64-candidate chunk.
+template <class CS>
+__device__ __forceinline__ QueryResult eval_query_intended(const WinArgs &a, const CS &C, const int8_t *qd, int x1,
+                                                           int y1, int lane, int *lst, int &best_patch_out) {
+    QueryResult res = {0, 0, 0, -1, 0.0f};
+    const int q4 = lane & 3, cslot = lane >> 2;
+    const int qv = reinterpret_cast<const int *>(qd)[lane];
+    int4 qa[4];
+#pragma unroll
+    for (int v = 0; v < 4; v++) qa[v] = reinterpret_cast<const int4 *>(qd + 64 * q4)[v];
+    const int n2_256 = wave_sum(__builtin_amdgcn_sdot4(qv, qv, 0, false));
+    const int xlo = max(x1 + a.shift_x - a.radius, 0), xhi = min(x1 + a.shift_x + a.radius, a.cols - 1);
+    const int ylo = max(y1 + a.shift_y - a.radius, 0), yhi = min(y1 + a.shift_y + a.radius, a.rows - 1);
+    const int ny = yhi - ylo + 1;
+    const int ncand = (xhi >= xlo && yhi >= ylo) ? (xhi - xlo + 1) * ny : 0;
+    const unsigned long long lower = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    long long best_dot = 0, best_na = 1;
+    int best_k = -1;
+    for (int vb = 0; vb < ncand; vb += 128) {
+        const int k0 = vb + lane, k1 = vb + 64 + lane;
+        const int kk0 = min(k0, ncand - 1), kk1 = min(k1, ncand - 1);
+        const int x0a = xlo + kk0 / ny, y0a = ylo + kk0 % ny, x0b = xlo + kk1 / ny, y0b = ylo + kk1 % ny;
+        const bool va = C.valid(x0a, y0a, x0a * a.rows + y0a), vbb = C.valid(x0b, y0b, x0b * a.rows + y0b);
+        const bool v0 = k0 < ncand && va, v1 = k1 < ncand && vbb;
+        const unsigned long long b0 = __ballot(v0), b1 = __ballot(v1);
+        const int n0c = __popcll(b0), nv = n0c + __popcll(b1);
+        if (v0) lst[__popcll(b0 & lower)] = k0;  // scan order
+        if (v1) lst[n0c + __popcll(b1 & lower)] = k1;
+        for (int c0 = 0; c0 < nv; c0 += 16) {
+            const int c = c0 + cslot;
+            int dot = 0, na = 0, k = -1;
+            if (c < nv) {
+                k = lst[c];
+                const int4 *cp = reinterpret_cast<const int4 *>(C.row(xlo + k / ny, ylo + k % ny) + 64 * q4);
+                int4 x[4];
+#pragma unroll
+                for (int v = 0; v < 4; v++) x[v] = cp[v];
+#pragma unroll
+                for (int v = 0; v < 4; v++) {
+                    dot = __builtin_amdgcn_sdot4(x[v].x, qa[v].x, dot, false);
+                    dot = __builtin_amdgcn_sdot4(x[v].y, qa[v].y, dot, false);
+                    dot = __builtin_amdgcn_sdot4(x[v].z, qa[v].z, dot, false);
+                    dot = __builtin_amdgcn_sdot4(x[v].w, qa[v].w, dot, false);
+                    na = __builtin_amdgcn_sdot4(x[v].x, x[v].x, na, false);
+                    na = __builtin_amdgcn_sdot4(x[v].y, x[v].y, na, false);
+                    na = __builtin_amdgcn_sdot4(x[v].z, x[v].z, na, false);
+                    na = __builtin_amdgcn_sdot4(x[v].w, x[v].w, na, false);
+                }
+            }
+            dot += __shfl_xor(dot, 1, 64);
+            dot += __shfl_xor(dot, 2, 64);
+            na += __shfl_xor(na, 1, 64);
+            na += __shfl_xor(na, 2, 64);
+            const long long cdot = dot, cna = na;
+            const bool pass = q4 == 0 && c < nv && dot > 0 && na != 0 && n2_256 != 0 &&
+                              (unsigned __int128)(100ll * cdot * cdot) >
+                                  (unsigned __int128)81 * (unsigned long long)(cna * (long long)n2_256);
+            long long bd = pass ? cdot : 0, bn = pass ? cna : 1;
+            int bk = pass ? k : -1;
+#pragma unroll
+            for (int o = 4; o < 64; o <<= 1) {  // the 16 scoring lanes (q4 == 0)
+                const long long od = __shfl_xor(bd, o, 64), on = __shfl_xor(bn, o, 64);
+                const int ok = __shfl_xor(bk, o, 64);
+                if (exact_better(od, on, ok, bd, bn, bk)) {
+                    bd = od;
+                    bn = on;
+                    bk = ok;
+                }
+            }
+            if (bk >= 0 && exact_better(bd, bn, bk, best_dot, best_na, best_k)) {
+                best_dot = bd;
+                best_na = bn;
+                best_k = bk;
+            }
+        }
+    }
+    if (best_k >= 0) {
+        res.found = 1;
+        res.bx = xlo + best_k / ny;
+        res.by = ylo + best_k % ny;
+        res.score = (float)((double)best_dot * (double)best_dot / ((double)best_na * (double)n2_256));
+        best_patch_out = res.bx * a.rows + res.by;
+    } else {
+        best_patch_out = -1;
+    }
+    return res;
+}
+
 // one wave per query slot; 4 waves per block; candidates straight from global memory
 __global__ __launch_bounds__(256) void k_window_eval(WinArgs a, const int8_t *__restrict__ desc0,
                                                      const int *__restrict__ max_idx0,
@@ -457,6 +550,7 @@ __global__ __launch_bounds__(256) void k_window_eval(WinArgs a, const int8_t *__
                                                      const int *__restrict__ num_sel,
                                                      const int *__restrict__ patches1,
                                                      QueryResult *__restrict__ out) {
+    __shared__ int lst_s[4][128];
     const int lane = threadIdx.x & 63;
     const int qslot = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int pair = blockIdx.y;
@@ -470,7 +564,11 @@ __global__ __launch_bounds__(256) void k_window_eval(WinArgs a, const int8_t *__
         const GlobalCands C = {desc0 + (long)pair * cells * kDescD, max_idx0 + (long)pair * cells,
                                probs0 + (long)pair * cells, a.rows, a.prob_thr};
         int bp;
-        res = eval_query(a, C, desc1 + ((long)pair * cells + patch1) * kDescD, x1, y1, lane, bp);
+        const int8_t *qd = desc1 + ((long)pair * cells + patch1) * kDescD;
+        if (a.as_built)
+            res = eval_query(a, C, qd, x1, y1, lane, bp);
+        else
+            res = eval_query_intended(a, C, qd, x1, y1, lane, lst_s[threadIdx.x >> 6], bp);
         if (bp >= 0) res.best_index = C.mi0[bp];
     }
     if (lane == 0) out[(long)pair * a.N + qslot] = res;
