@@ -44,8 +44,6 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", type=int, default=2, help="pairs verified against the oracle after timing")
-    ap.add_argument("--pose-stream", type=int, default=1,
-                    help="1: the pose of batch k runs on a side stream beside the match of batch k + 1")
     return ap.parse_args()
 
 
@@ -208,14 +206,12 @@ def main():
 
     d0, d1, kp0, kp1 = gen_batch(torch, dev, B, n, seed=pair_seed(rank, 0))
     nn_ = torch.full((B,), n, dtype=torch.int32, device=dev)
-    # two output sets: the pose of step k (side stream) still reads set k % 2 while the match
-    # of step k + 1 writes the other one
-    idx2 = [torch.empty((B, n), dtype=torch.int32, device=dev) for _ in range(2)]
-    score2 = [torch.empty((B, n), dtype=torch.float32, device=dev) for _ in range(2)]
-    T2 = [torch.empty((B, 3, 4), dtype=torch.float32, device=dev) for _ in range(2)]
-    nmatch2 = [torch.empty(B, dtype=torch.int32, device=dev) for _ in range(2)]
-    ninl2 = [torch.empty(B, dtype=torch.int32, device=dev) for _ in range(2)]
-    status2 = [torch.empty(B, dtype=torch.int32, device=dev) for _ in range(2)]
+    idx = torch.empty((B, n), dtype=torch.int32, device=dev)
+    score = torch.empty((B, n), dtype=torch.float32, device=dev)
+    T = torch.empty((B, 3, 4), dtype=torch.float32, device=dev)
+    nmatch = torch.empty(B, dtype=torch.int32, device=dev)
+    ninl = torch.empty(B, dtype=torch.int32, device=dev)
+    status = torch.empty(B, dtype=torch.int32, device=dev)
 
     ctx = mvtrack.Context(local)
     stream = torch.cuda.current_stream()
@@ -227,32 +223,12 @@ def main():
     pose_p = mvtrack.pose_params(mvtrack.AS_INTENDED, fx=K[0, 0], fy=K[1, 1], cx=K[0, 2], cy=K[1, 2],
                                  hypotheses=args.hypotheses, inlier_thresh=1.0, refine_iters=10, seed=7)
 
-    # pipelined across steps, three streams: the match of batch k (context stream), the
-    # staging of batch k + 1 (k_ap_split, the context's auxiliary stream) and the pose of
-    # batch k (a side stream, after the match of k); every step still does all of its own work
-    pose_stream = torch.cuda.Stream(device=dev)
-    ev_match = [torch.cuda.Event() for _ in range(2)]
-    ev_pose = [torch.cuda.Event() for _ in range(2)]
-    posed = [False, False]
-    k_step = [0]
-
+    # pipelined across steps: frame 1 of the next batch is staged (k_ap_split, auxiliary
+    # stream) while this batch's pose runs; every step still does all of its own work
     def step():
-        k = k_step[0] & 1
-        if posed[k]:
-            stream.wait_event(ev_pose[k])  # pose k-2 has read set k
-        ctx.match_allpairs_f32_run(d0, d1, nn_, nn_, idx2[k], score2[k], 0.8)
+        ctx.match_allpairs_f32_run(d0, d1, nn_, nn_, idx, score, 0.8)
         ctx.match_allpairs_f32_prepare(d1, nn_)  # the next step's batch
-        if args.pose_stream:
-            ev_match[k].record(stream)
-            pose_stream.wait_event(ev_match[k])
-            ctx.set_stream(pose_stream)
-            ctx.pose_from_matches(pose_p, nn_, idx2[k], kp0, kp1, T2[k], nmatch2[k], ninl2[k], status2[k])
-            ctx.set_stream(stream)
-            ev_pose[k].record(pose_stream)
-            posed[k] = True
-        else:
-            ctx.pose_from_matches(pose_p, nn_, idx2[k], kp0, kp1, T2[k], nmatch2[k], ninl2[k], status2[k])
-        k_step[0] += 1
+        ctx.pose_from_matches(pose_p, nn_, idx, kp0, kp1, T, nmatch, ninl, status)
 
     ctx.match_allpairs_f32_prepare(d1, nn_)
 
@@ -271,9 +247,7 @@ def main():
     s_ms, s_n = mvtrack.profile_query("k_ap_split")
     p_ms, p_n = mvtrack.profile_query("k_pose_ransac")
 
-    # correctness of the timed outputs on a few pairs (outside the timed region): the last step's set
-    last = (k_step[0] - 1) & 1
-    idx, T, nmatch, status = idx2[last], T2[last], nmatch2[last], status2[last]
+    # correctness of the timed outputs on a few pairs (outside the timed region)
     ok = int((status == 0).sum().item())
     checked = 0
     if args.check > 0:

@@ -675,13 +675,11 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
 
 namespace mv {
 
-// scratch: two slots (prepare of batch k+1 overlaps the run of batch k), each
-// h1 (batch * cap * 512 B) | nrm1 (batch * cap f32) | bad (batch i32)
-static size_t ap_slot_bytes(int batch, int cap) {
+// scratch: h1 (batch * cap * 512 B) | nrm1 (batch * cap f32) | bad (batch i32)
+size_t allpairs_f32_scratch_bytes(int batch, int cap) {
     const size_t rows = (size_t)batch * cap;
-    return align_up(rows * ROW_BYTES + align_up(rows * 4, 256) + align_up((size_t)batch * 4, 256), 1 << 16);
+    return rows * ROW_BYTES + align_up(rows * 4, 256) + align_up((size_t)batch * 4, 256);
 }
-size_t allpairs_f32_scratch_bytes(int batch, int cap) { return 2 * ap_slot_bytes(batch, cap); }
 
 namespace {
 struct ApScratch {
@@ -689,10 +687,10 @@ struct ApScratch {
     float *nrm1;
     int *bad;
 };
-ApScratch ap_scratch_map(void *scratch, int batch, int cap, int slot) {
+ApScratch ap_scratch_map(void *scratch, int batch, int cap) {
     const size_t rows = (size_t)batch * cap;
     ApScratch m;
-    m.h1 = (char *)scratch + (size_t)slot * ap_slot_bytes(batch, cap);
+    m.h1 = (char *)scratch;
     m.nrm1 = (float *)(m.h1 + rows * ROW_BYTES);
     m.bad = (int *)((char *)m.nrm1 + align_up(rows * 4, 256));
     return m;
@@ -700,13 +698,13 @@ ApScratch ap_scratch_map(void *scratch, int batch, int cap, int slot) {
 }  // namespace
 
 // frame 1 -> fp16 image + |b|^2 + per-pair range flag (k_ap_split)
-int launch_allpairs_f32_prepare(hipStream_t s, void *scratch, int slot, int batch, int cap, const int *n1,
+int launch_allpairs_f32_prepare(hipStream_t s, void *scratch, int batch, int cap, const int *n1,
                                 const float *desc1) {
     MV_REQUIRE(batch > 0 && cap > 0 && n1 && desc1 && scratch);
     MV_REQUIRE(((uintptr_t)desc1 & 15) == 0);
     MV_REQUIRE(cap <= (1 << 22));  // per-lane DMA source offsets are 32-bit byte offsets into a pair
     const size_t rows = (size_t)batch * cap;
-    const ApScratch m = ap_scratch_map(scratch, batch, cap, slot);
+    const ApScratch m = ap_scratch_map(scratch, batch, cap);
     const long split_blocks = std::min<long>((long)((rows + SPLIT_ROWS - 1) / SPLIT_ROWS), 256l * 64);
     MV_HIP_TRY(hipMemsetAsync(m.bad, 0, (size_t)batch * 4, s));
     MV_PROF_BEGIN(s, "k_ap_split");
@@ -718,15 +716,15 @@ int launch_allpairs_f32_prepare(hipStream_t s, void *scratch, int slot, int batc
 }
 
 // the sweep + exact re-score (k_ap_match) over a prepared frame 1
-int launch_allpairs_f32_match(hipStream_t s, void *scratch, int slot, int batch, int cap, const int *n0,
-                              const int *n1, const float *desc0, const float *desc1, double thresh, int *match_idx,
+int launch_allpairs_f32_match(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
+                              const float *desc0, const float *desc1, double thresh, int *match_idx,
                               float *match_score) {
     MV_REQUIRE(batch > 0 && cap > 0 && n0 && n1 && desc0 && desc1 && match_idx && match_score && scratch);
     MV_REQUIRE(((uintptr_t)desc0 & 15) == 0 && ((uintptr_t)desc1 & 15) == 0);
     const int tiles_r = (cap + BM - 1) / BM;
     const long blocks = (long)batch * tiles_r;
     MV_REQUIRE(blocks < (1l << 31));
-    const ApScratch m = ap_scratch_map(scratch, batch, cap, slot);
+    const ApScratch m = ap_scratch_map(scratch, batch, cap);
     MV_PROF_BEGIN(s, "k_ap_match");
     hipLaunchKernelGGL(k_ap_match, dim3((unsigned)blocks), dim3(NT), 0, s, tiles_r, cap, n0, n1, desc0, desc1, m.h1,
                        m.nrm1, m.bad, thresh, match_idx, match_score);
@@ -757,16 +755,6 @@ void *ap_scratch(mv_context *ctx, size_t bytes) {
 }
 }  // namespace
 
-static int ap_ensure_aux(mv_context *ctx) {
-    if (!ctx->aux_stream) {
-        MV_HIP_TRY(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
-        MV_HIP_TRY(hipEventCreateWithFlags(&ctx->ev_in, hipEventDisableTiming));
-        MV_HIP_TRY(hipEventCreateWithFlags(&ctx->ev_prep, hipEventDisableTiming));
-        MV_HIP_TRY(hipEventCreateWithFlags(&ctx->ev_pre, hipEventDisableTiming));
-    }
-    return MV_OK;
-}
-
 extern "C" int mv_match_allpairs_f32_dev(mv_context *ctx, int batch, int cap, const int *n0, const int *n1,
                                          const float *desc0, const float *desc1, double thresh, int *match_idx,
                                          float *match_score) {
@@ -774,13 +762,10 @@ extern "C" int mv_match_allpairs_f32_dev(mv_context *ctx, int batch, int cap, co
     MV_HIP_TRY(hipSetDevice(ctx->device));
     void *scr = ap_scratch(ctx, mv::allpairs_f32_scratch_bytes(batch, cap));
     if (!scr) return MV_ERR_OUT_OF_MEMORY;
-    // one-shot: slot 0 on the context stream, after any prepare still in flight on the
-    // auxiliary stream (it may be writing slot 0)
-    if (ctx->aux_stream) MV_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_prep, 0));
-    ctx->prep_desc1 = nullptr;  // the prepared images are not trusted any more
-    const int st = mv::launch_allpairs_f32_prepare(ctx->stream, scr, 0, batch, cap, n1, desc1);
+    ctx->prep_desc1 = nullptr;  // the prepared image is overwritten
+    const int st = mv::launch_allpairs_f32_prepare(ctx->stream, scr, batch, cap, n1, desc1);
     if (st != MV_OK) return st;
-    return mv::launch_allpairs_f32_match(ctx->stream, scr, 0, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
+    return mv::launch_allpairs_f32_match(ctx->stream, scr, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
                                          match_score);
 }
 
@@ -788,28 +773,19 @@ extern "C" int mv_match_allpairs_f32_prepare_dev(mv_context *ctx, int batch, int
                                                  const float *desc1) {
     MV_REQUIRE(ctx != nullptr && batch > 0 && cap > 0 && n1 && desc1);
     MV_HIP_TRY(hipSetDevice(ctx->device));
-    const bool had = ctx->ap_scratch != nullptr;
     void *scr = ap_scratch(ctx, mv::allpairs_f32_scratch_bytes(batch, cap));
     if (!scr) return MV_ERR_OUT_OF_MEMORY;
-    if (!had || scr != ctx->ap_scratch) ctx->prep_desc1 = nullptr;
-    const int e = ap_ensure_aux(ctx);
-    if (e != MV_OK) return e;
-    // Ordering: after the work issued on the context stream before the most recent run (if a
-    // run came after the previous prepare), else after everything issued so far.  The slot
-    // written now was last read by the run before that most recent run, so it is free.
-    if (ctx->run_since_prep) {
-        MV_HIP_TRY(hipStreamWaitEvent(ctx->aux_stream, ctx->ev_pre, 0));
-    } else {
-        MV_HIP_TRY(hipEventRecord(ctx->ev_in, ctx->stream));
-        MV_HIP_TRY(hipStreamWaitEvent(ctx->aux_stream, ctx->ev_in, 0));
+    if (!ctx->aux_stream) {
+        MV_HIP_TRY(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
+        MV_HIP_TRY(hipEventCreateWithFlags(&ctx->ev_in, hipEventDisableTiming));
+        MV_HIP_TRY(hipEventCreateWithFlags(&ctx->ev_prep, hipEventDisableTiming));
     }
-    const int slot = (int)(ctx->prep_count & 1u);
-    const int st = mv::launch_allpairs_f32_prepare(ctx->aux_stream, scr, slot, batch, cap, n1, desc1);
+    // inputs (and the previous run's use of the scratch) as of this call on the context stream
+    MV_HIP_TRY(hipEventRecord(ctx->ev_in, ctx->stream));
+    MV_HIP_TRY(hipStreamWaitEvent(ctx->aux_stream, ctx->ev_in, 0));
+    const int st = mv::launch_allpairs_f32_prepare(ctx->aux_stream, scr, batch, cap, n1, desc1);
     if (st != MV_OK) return st;
     MV_HIP_TRY(hipEventRecord(ctx->ev_prep, ctx->aux_stream));
-    ctx->prep_count++;
-    ctx->prep_slot = slot;
-    ctx->run_since_prep = 0;
     ctx->prep_batch = batch;
     ctx->prep_cap = cap;
     ctx->prep_n1 = n1;
@@ -827,11 +803,9 @@ extern "C" int mv_match_allpairs_f32_run_dev(mv_context *ctx, int batch, int cap
         return MV_ERR_INVALID_ARG;
     }
     MV_HIP_TRY(hipSetDevice(ctx->device));
-    MV_HIP_TRY(hipEventRecord(ctx->ev_pre, ctx->stream));
-    ctx->run_since_prep = 1;
     MV_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_prep, 0));
-    return mv::launch_allpairs_f32_match(ctx->stream, ctx->ap_scratch, ctx->prep_slot, batch, cap, n0, n1, desc0, desc1,
-                                         thresh, match_idx, match_score);
+    return mv::launch_allpairs_f32_match(ctx->stream, ctx->ap_scratch, batch, cap, n0, n1, desc0, desc1, thresh,
+                                         match_idx, match_score);
 }
 
 #ifdef AP_EXP_TRACE

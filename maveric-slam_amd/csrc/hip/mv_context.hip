@@ -142,7 +142,6 @@ int mv_context_destroy(mv_context *ctx) {
         (void)hipStreamSynchronize(ctx->aux_stream);
         (void)hipEventDestroy(ctx->ev_in);
         (void)hipEventDestroy(ctx->ev_prep);
-        (void)hipEventDestroy(ctx->ev_pre);
         (void)hipStreamDestroy(ctx->aux_stream);
     }
     if (ctx->scratch) (void)hipFree(ctx->scratch);

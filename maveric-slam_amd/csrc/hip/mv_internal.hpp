@@ -21,13 +21,6 @@ struct mv_context {
     size_t ap_scratch_bytes;
     hipStream_t aux_stream;  // created on first prepare
     hipEvent_t ev_in, ev_prep;
-    // pipelining: two prepared-image slots alternate; ev_pre is recorded on `stream` just
-    // before each run launch, and a prepare issued after a run waits only for it (so the
-    // prepare of batch k+1 overlaps the run of batch k, whose slot it does not touch)
-    hipEvent_t ev_pre;
-    int run_since_prep;
-    int prep_slot;             // slot of the last prepare (the next run reads it)
-    unsigned prep_count;
     int prep_batch, prep_cap;  // what the last prepare staged (run checks it)
     const int *prep_n1;
     const float *prep_desc1;
@@ -91,10 +84,10 @@ int launch_softmax(hipStream_t s, int batch, int cells, const float *scales, con
 int launch_top_n_select(hipStream_t s, int batch, int cells, const int *max_idx, const float *probs, int N,
                         int cap, int *num_sel, int *patches, int *indices, float *sel_probs, int *status);
 size_t allpairs_f32_scratch_bytes(int batch, int cap);
-int launch_allpairs_f32_prepare(hipStream_t s, void *scratch, int slot, int batch, int cap, const int *n1,
+int launch_allpairs_f32_prepare(hipStream_t s, void *scratch, int batch, int cap, const int *n1,
                                 const float *desc1);
-int launch_allpairs_f32_match(hipStream_t s, void *scratch, int slot, int batch, int cap, const int *n0,
-                              const int *n1, const float *desc0, const float *desc1, double thresh, int *match_idx,
+int launch_allpairs_f32_match(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
+                              const float *desc0, const float *desc1, double thresh, int *match_idx,
                               float *match_score);
 size_t allpairs_i8_scratch_bytes(int batch, int cap);
 int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
