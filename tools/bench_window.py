@@ -45,7 +45,16 @@ def cpu_baseline(pairs, built, N, cells, seconds):
     with cf.ThreadPoolExecutor(threads) as ex:
         total = sum(ex.map(worker, range(threads)))
     dt = time.perf_counter() - t0
+    # one core (1 core and all cores)
+    f0, f1 = pairs[0]
+    t1 = time.perf_counter()
+    one = 0
+    while time.perf_counter() - t1 < min(2.0, seconds / 4):
+        oracle.track_window(f0, f1, as_built=built, N=N, cap=cells, max_matches=150)
+        one += 1
+    us1 = (time.perf_counter() - t1) / one * 1e6
     return {"value": round(total / dt, 1), "unit": "pairs/s", "cores": threads, "kind": "port",
+            "us_per_pair_1core": round(us1, 1),
             "sample": "%d pairs (%d cells, N=%d) through the oracle's C restatement in %.1f s on %d host threads"
                       % (total, cells, N, dt, threads)}
 
@@ -59,8 +68,12 @@ def main():
     ap.add_argument("--as-built", action="store_true")
     ap.add_argument("--check", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--grid", choices=["kitti", "quantized"], default="kitti",
+                    help="kitti: 47x155 cells, N=1024 (full-res KITTI); quantized: the reference's own "
+                         "24x80-cell quantized frame, N=100 (SURVEY 8(d) C0; tracking_main.c:13-14)")
     args = ap.parse_args()
-    B, rows, cols, N = args.batch, 47, 155, 1024
+    rows, cols, N = (47, 155, 1024) if args.grid == "kitti" else (24, 80, 100)
+    B = args.batch
     cells = rows * cols
     dev = torch.device("cuda", 0)
     pairs = [synth.synth_window_pair(500 + k, rows=rows, cols=cols) for k in range(args.distinct)]
@@ -125,15 +138,18 @@ def main():
     step_s = el / args.steps
     win_s = stages["k_window_eval"] * 1e-3
     out = {
-        "metric": "windowed int8 front-end pairs/sec (softmax x2 + top-N + window match), 7285 cells, N=1024",
+        "metric": "windowed int8 front-end pairs/sec (softmax x2 + top-N + window match), %d cells, N=%d"
+                  % (cells, N),
         "value": round(B / step_s, 1), "unit": "pairs/s", "batch": B, "steps": args.steps,
         "ms_per_step": round(step_s * 1e3, 4), "semantics": "as-built" if built else "as-intended",
         "stages_ms": stages, "queries_selected_avg": float(ns.float().mean()), "matches_avg": float(nm.float().mean()),
         "hbm_roofline": {"algorithmic_bytes_per_pair": alg_bytes,
                          "frontend_GBs": round(alg_bytes * B / step_s / 1e9, 1),
                          "frontend_frac": round(alg_bytes * B / step_s / 1e9 / HBM_PEAK_GBS, 4),
-                         "window_kernel_bytes_per_pair": 2 * cells * 256 + cells * 8 + N * 8,
-                         "window_kernel_GBs": round((2 * cells * 256 + cells * 8 + N * 8) * B / win_s / 1e9, 1),
+                         # frame-0 descriptors + validity (every window cell at most once), the
+                         # N query descriptors of frame 1, the per-query results
+                         "window_kernel_bytes_per_pair": cells * (256 + 8) + N * (256 + 4 + 20),
+                         "window_kernel_GBs": round((cells * (256 + 8) + N * (256 + 4 + 20)) * B / win_s / 1e9, 1),
                          "peak_GBs": HBM_PEAK_GBS},
         "checked_pairs": checked,
     }
