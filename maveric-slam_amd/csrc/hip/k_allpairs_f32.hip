@@ -400,15 +400,17 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
     // that slot's MFMAs.  The sweep's last tile (the only one that can reach past n1) is
     // folded after the loop, masked.
     f32x16 accA0 = zero16, accA1 = zero16, accB0 = zero16, accB1 = zero16;
-#define AP_FOLD(X0, X1, TC)                                                                   \
+    // fold rows [Q0, Q1) of tile TC's accumulators
+#define AP_FOLD_ROWS(X0, X1, TC, Q0, Q1)                                                      \
     do {                                                                                      \
         const unsigned g0_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)(TC)), g1_ = g0_ + 1u; \
         if (!AP_EXP_NOFOLD)                                                                   \
-            _Pragma("unroll") for (int q = 0; q < 16; q++)                                    \
+            _Pragma("unroll") for (int q = (Q0); q < (Q1); q++)                               \
                 fold3(tagf(X0[q], vkeep, g0_), tagf(X1[q], vkeep, g1_), m1[q], m2[q]);        \
-        else /* timing experiment: keep the MFMAs live at 1/16 of the fold's VALU work */      \
+        else if ((Q0) == 0) /* timing experiment: keep the MFMAs live at 1/16 of the work */   \
             fold3(X0[0] + X0[5] + X0[10] + X0[15], X1[0] + X1[5] + X1[10] + X1[15], m1[0], m2[0]); \
     } while (0)
+#define AP_FOLD(X0, X1, TC) AP_FOLD_ROWS(X0, X1, TC, 0, 16)
 #define AP_SLOT(J, C0, C1, F0, F1, FOLD)                                                      \
     do {                                                                                      \
         constexpr int nx = (J) + NBUF - 1;                                                    \
@@ -437,7 +439,8 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
                 }                                                                             \
             }                                                                                 \
         }                                                                                     \
-        if (FOLD) AP_FOLD(F0, F1, T + (J) / KS - 1); /* previous tile, beside these MFMAs */  \
+        /* the previous tile's fold, half of its rows beside each k-slice's MFMAs */          \
+        if (FOLD) AP_FOLD_ROWS(F0, F1, T + (J) / KS - 1, 8 * ((J) % KS), 8 * ((J) % KS) + 8);  \
         if (AP_EXP_NOWAIT) {                                                                  \
         } else if (ntile < ntc) {                                                             \
             wait_vm<DMA_PER_SLICE * (NBUF - 2)>();                                            \
@@ -455,10 +458,10 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
     for (int k = 1; k < NW; k++) bmax2 = fmaxf(bmax2, misc[k]);
     for (int T = 0; T < ntc; T += 2) {
         AP_SLOT(0, accA0, accA1, accB0, accB1, T > 0);
-        AP_SLOT(1, accA0, accA1, accB0, accB1, false);
+        AP_SLOT(1, accA0, accA1, accB0, accB1, T > 0);
         if (T + 1 < ntc) {
             AP_SLOT(2, accB0, accB1, accA0, accA1, true);
-            AP_SLOT(3, accB0, accB1, accA0, accA1, false);
+            AP_SLOT(3, accB0, accB1, accA0, accA1, true);
         }
     }
     AP_STAMP(3);
@@ -478,6 +481,7 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
 #undef AP_STAGE
 #undef AP_SLOT
 #undef AP_FOLD
+#undef AP_FOLD_ROWS
 #undef AP_TILE_OFFSETS
 
     // ---- per row, merge the 32 lanes' (m1, m2): transposed through LDS (the ring is free;
