@@ -247,7 +247,7 @@ struct WinArgs {
 };
 
 struct QueryResult {  // one per (pair, query slot), consumed by k_window_compact
-    int found, bx, by, best_index;
+    int found, bx, by, best_patch;  // best_patch: frame-0 patch of the winner (compact reads its index)
     float score;
 };
 
@@ -569,9 +569,564 @@ __global__ __launch_bounds__(256) void k_window_eval(WinArgs a, const int8_t *__
             res = eval_query(a, C, qd, x1, y1, lane, bp);
         else
             res = eval_query_intended(a, C, qd, x1, y1, lane, lst_s[threadIdx.x >> 6], bp);
-        if (bp >= 0) res.best_index = C.mi0[bp];
+        res.best_patch = bp;
     }
     if (lane == 0) out[(long)pair * a.N + qslot] = res;
+}
+
+// ---------------------------------------------------------------------------
+// Window match, fast path (rows <= 64, window <= kWinList cells): the default at both the
+// reference's 24x80 grid and the 47x155 KITTI grid.
+//
+// k_window_mask: one 64-bit word per frame-0 grid column, bit y set when cell (x, y) is a
+// candidate (tracking_main.c:121-125: index != 64 and !(prob < 0.2), double compare).  A
+// column's cells are contiguous (p = x*rows + y), so one wave ballots one column.
+//
+// k_window_query: one wave walks kQPW consecutive top-N queries (patch order, so the windows
+// of a wave overlap in L1/L2).  Per query the wave reads the masks of the window's columns
+// (one word per lane), builds the scan-ordered candidate list in LDS, and loads the
+// descriptors of up to 32 candidates at once -- while the next query's masks and query row
+// are already in flight.  Blocks are remapped so that all blocks of a pair run on one XCD
+// (dispatch is round-robin over the 8 XCDs): the pair's frame-0 descriptors stream from one L2.
+// ---------------------------------------------------------------------------
+constexpr int kQPW = 8;        // queries per wave
+constexpr int kWinList = 256;  // candidate-list capacity per wave (window cells)
+
+__global__ __launch_bounds__(256) void k_window_mask(long total_cols, int rows, const int *__restrict__ mi0,
+                                                     const float *__restrict__ pr0, double prob_thr,
+                                                     unsigned long long *__restrict__ masks) {
+    const long col = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (col >= total_cols) return;
+    const int y = threadIdx.x & 63;
+    bool v = false;
+    if (y < rows) {
+        const long p = col * rows + y;
+        v = mi0[p] != 64 && !((double)pr0[p] < prob_thr);
+    }
+    const unsigned long long m = __ballot(v);
+    if (y == 0) masks[col] = m;
+}
+
+struct QueryPrefetch {
+    int patch1, ncol, ny, origin;  // origin: frame-0 cell (xlo, ylo) of the window
+    unsigned long long bits;       // lane j < ncol: candidate rows of window column j (bit = y - ylo)
+    int4 q[4];                     // query bytes: as-intended 32*(lane&7) .. +31 (q[0..1]); as-built 0 .. 63
+    int qv;                        // query dword `lane`
+};
+
+template <bool kBuilt>
+__device__ __forceinline__ QueryPrefetch window_prefetch(const WinArgs &a, const unsigned long long *mk,
+                                                         const int8_t *d1, int patch1, int lane) {
+    QueryPrefetch f;
+    f.patch1 = patch1;
+    f.bits = 0;
+    f.ncol = 0;
+    f.ny = 1;
+    f.origin = 0;
+    if (patch1 < 0) return f;
+    const int x1 = patch1 / a.rows, y1 = patch1 % a.rows;
+    const int xlo = max(x1 + a.shift_x - a.radius, 0), xhi = min(x1 + a.shift_x + a.radius, a.cols - 1);
+    const int ylo = max(y1 + a.shift_y - a.radius, 0), yhi = min(y1 + a.shift_y + a.radius, a.rows - 1);
+    f.origin = xlo * a.rows + ylo;
+    if (xhi >= xlo && yhi >= ylo) {
+        f.ncol = xhi - xlo + 1;
+        f.ny = yhi - ylo + 1;
+        if (lane < f.ncol) {
+            const unsigned long long keep = f.ny == 64 ? ~0ull : ((1ull << f.ny) - 1);
+            f.bits = (mk[xlo + lane] >> ylo) & keep;
+        }
+    }
+    const int8_t *qd = d1 + (long)patch1 * kDescD;
+    if (kBuilt) {
+        const int4 *qp = reinterpret_cast<const int4 *>(qd);
+#pragma unroll
+        for (int v = 0; v < 4; v++) f.q[v] = qp[v];
+    } else {
+        const int4 *qp = reinterpret_cast<const int4 *>(qd + 32 * (lane & 7));
+        f.q[0] = qp[0];
+        f.q[1] = qp[1];
+    }
+    f.qv = reinterpret_cast<const int *>(qd)[lane];
+    return f;
+}
+
+// Scan-ordered candidate list of the prefetched window.  An entry is the candidate's cell
+// offset from the window origin (column*rows + row offset): increasing in scan order (x outer,
+// y inner), and origin + entry addresses the descriptor without a division.
+__device__ __forceinline__ int window_list(const QueryPrefetch &f, int lane, int rows, int *lst) {
+    const int cnt = __popcll(f.bits);
+    int incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    const int nv = __shfl(incl, 63, 64);
+    int pos = incl - cnt;
+    unsigned long long b = f.bits;
+    const int colbase = lane * rows;
+    while (b) {
+        const int yb = __ffsll((long long)b) - 1;
+        b &= b - 1;
+        lst[pos++] = colbase + yb;
+    }
+    return nv;
+}
+
+__device__ __forceinline__ void dot_x4(const int4 *x, const int4 *q, int nv4, int &dot, int &na) {
+#pragma unroll
+    for (int v = 0; v < 4; v++) {
+        if (v >= nv4) break;
+        dot = __builtin_amdgcn_sdot4(x[v].x, q[v].x, dot, false);
+        dot = __builtin_amdgcn_sdot4(x[v].y, q[v].y, dot, false);
+        dot = __builtin_amdgcn_sdot4(x[v].z, q[v].z, dot, false);
+        dot = __builtin_amdgcn_sdot4(x[v].w, q[v].w, dot, false);
+        na = __builtin_amdgcn_sdot4(x[v].x, x[v].x, na, false);
+        na = __builtin_amdgcn_sdot4(x[v].y, x[v].y, na, false);
+        na = __builtin_amdgcn_sdot4(x[v].z, x[v].z, na, false);
+        na = __builtin_amdgcn_sdot4(x[v].w, x[v].w, na, false);
+    }
+}
+
+// a * b for a < 2^45, b < 2^32 as (hi, lo32): two v_mad_u64_u32, exact
+__device__ __forceinline__ void mul45x32(unsigned long long a, unsigned b, unsigned long long &hi, unsigned &lo) {
+    const unsigned long long p0 = (unsigned long long)(unsigned)a * b;
+    hi = (unsigned long long)(unsigned)(a >> 32) * b + (p0 >> 32);
+    lo = (unsigned)p0;
+}
+
+// exact "candidate a beats b" for the as-intended score dot^2/na (dot > 0, |dot|, na < 2^23:
+// 256 products of int8), ties -> lower scan position; k < 0 = none
+__device__ __forceinline__ bool better_i32(int da, int na, int ka, int db, int nb, int kb) {
+    if (ka < 0) return false;
+    if (kb < 0) return true;
+    unsigned long long lh, rh;
+    unsigned ll, rl;
+    mul45x32((unsigned long long)((long long)da * da), (unsigned)nb, lh, ll);
+    mul45x32((unsigned long long)((long long)db * db), (unsigned)na, rh, rl);
+    if (lh != rh) return lh > rh;
+    if (ll != rl) return ll > rl;
+    return ka < kb;
+}
+
+// As-intended (exact cosine, tracking_main.c:114-165 as meant): 8 lanes per candidate (32 B
+// each), four candidates per lane group per round: 32 candidate rows in flight.
+__device__ __forceinline__ void query_intended(const int8_t *d0, const QueryPrefetch &f, int nv, const int *lst,
+                                               int lane, int n2, int &best_dot, int &best_na, int &best_k) {
+    const int q8 = lane & 7, cslot = lane >> 3;
+    const int8_t *wbase = d0 + (long)f.origin * kDescD + 32 * q8;
+    for (int c0 = 0; c0 < nv; c0 += 32) {
+        int k[4];
+        int4 x[4][2];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int c = c0 + 8 * u + cslot;
+            k[u] = c < nv ? lst[c] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (k[u] >= 0) {
+                const int4 *p = reinterpret_cast<const int4 *>(wbase + (long)k[u] * kDescD);
+                x[u][0] = p[0];
+                x[u][1] = p[1];
+            }
+        }
+        int bd = 0, bn = 1, bk = -1;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            int d = 0, n = 0;
+            if (k[u] >= 0) dot_x4(x[u], f.q, 2, d, n);
+            d += __shfl_xor(d, 1, 64);
+            n += __shfl_xor(n, 1, 64);
+            d += __shfl_xor(d, 2, 64);
+            n += __shfl_xor(n, 2, 64);
+            d += __shfl_xor(d, 4, 64);
+            n += __shfl_xor(n, 4, 64);
+            const bool pass = k[u] >= 0 && d > 0 && n != 0 && n2 != 0 &&
+                              (unsigned long long)(100ll * d * d) > 81ull * (unsigned long long)((long long)n * n2);
+            if (pass && better_i32(d, n, k[u], bd, bn, bk)) {
+                bd = d;
+                bn = n;
+                bk = k[u];
+            }
+        }
+#pragma unroll
+        for (int o = 8; o < 64; o <<= 1) {  // the 8 lane groups (every lane of a group agrees)
+            const int od = __shfl_xor(bd, o, 64), on = __shfl_xor(bn, o, 64), ok = __shfl_xor(bk, o, 64);
+            if (better_i32(od, on, ok, bd, bn, bk)) {
+                bd = od;
+                bn = on;
+                bk = ok;
+            }
+        }
+        if (bk >= 0 && better_i32(bd, bn, bk, best_dot, best_na, best_k)) {
+            best_dot = bd;
+            best_na = bn;
+            best_k = bk;
+        }
+    }
+}
+
+// As-built: the first candidate (scan order) with a non-zero 256-D norm latches
+// norm1 and is scored in 256-D; every later candidate is scored in 64-D against the stale
+// norm1 with int32-wrapped products, float division and a double compare; candidates before
+// the latch are all-zero descriptors (0/0 = NaN: never pass).  One lane per candidate.
+// Returns the winner's list position.
+__device__ __forceinline__ void query_built(const WinArgs &a, const int8_t *d0, const QueryPrefetch &f, int nv,
+                                            const int *lst, int lane, int &best_pos, float &best_d) {
+    const int8_t *wbase = d0 + (long)f.origin * kDescD;
+    const int n2_256 = wave_sum(__builtin_amdgcn_sdot4(f.qv, f.qv, 0, false));
+    int n2_64 = 0, unused = 0;
+    dot_x4(f.q, f.q, 4, n2_64, unused);
+    // latch: the first listed candidate whose full norm is non-zero (almost always the first)
+    int latch = -1, n1f = 0, dot_f = 0;
+    for (int j = 0; j < nv; j++) {
+        const int cv = reinterpret_cast<const int *>(wbase + (long)lst[j] * kDescD)[lane];
+        const int full_n1 = wave_sum(__builtin_amdgcn_sdot4(cv, cv, 0, false));
+        if (full_n1 != 0) {
+            latch = j;
+            n1f = full_n1;
+            dot_f = wave_sum(__builtin_amdgcn_sdot4(cv, f.qv, 0, false));
+            break;
+        }
+    }
+    if (latch < 0) return;
+    const int den64 = wrap_mul(n1f, n2_64);
+    {  // the latching candidate itself (256-D)
+        const float d = (float)wrap_mul(dot_f, dot_f) / (float)wrap_mul(n1f, n2_256);
+        if ((double)d > a.thr_sq) {
+            best_pos = latch;
+            best_d = d;
+        }
+    }
+    for (int c0 = latch + 1; c0 < nv; c0 += 64) {
+        const int c = c0 + lane;
+        float d = -__builtin_inff();
+        int pc = 0x7fffffff;
+        if (c < nv) {
+            const int4 *p = reinterpret_cast<const int4 *>(wbase + (long)lst[c] * kDescD);
+            int4 x[4];
+#pragma unroll
+            for (int v = 0; v < 4; v++) x[v] = p[v];
+            int dot = 0, nn = 0;
+            dot_x4(x, f.q, 4, dot, nn);
+            const float dd = (float)wrap_mul(dot, dot) / (float)den64;
+            if ((double)dd > a.thr_sq) {
+                d = dd;
+                pc = c;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {  // first strict maximum: max d, ties -> lowest position
+            const float od = __shfl_xor(d, o, 64);
+            const int oc = __shfl_xor(pc, o, 64);
+            if (od > d || (od == d && oc < pc)) {
+                d = od;
+                pc = oc;
+            }
+        }
+        if (pc != 0x7fffffff && (best_pos < 0 || d > best_d)) {
+            best_d = d;
+            best_pos = pc;
+        }
+    }
+}
+
+template <bool kBuilt>
+__global__ __launch_bounds__(256) void k_window_query(WinArgs a, int blocks_per_pair, int nblocks,
+                                                      const unsigned long long *__restrict__ masks,
+                                                      const int8_t *__restrict__ desc0,
+                                                      const int8_t *__restrict__ desc1,
+                                                      const int *__restrict__ num_sel,
+                                                      const int *__restrict__ patches1,
+                                                      QueryResult *__restrict__ out) {
+    __shared__ int lst_s[4][kWinList];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // XCD-aware remap: physical block b runs on XCD b % 8; give each XCD a contiguous run of
+    // logical blocks (whole pairs).  gridDim.x is a multiple of 8.
+    const int b = blockIdx.x, per_xcd = gridDim.x >> 3;
+    const int logical = (b & 7) * per_xcd + (b >> 3);
+    if (logical >= nblocks) return;
+    const int pair = logical / blocks_per_pair;
+    const int qbase = ((logical % blocks_per_pair) * 4 + w) * kQPW;
+    if (qbase >= a.N) return;  // wave-uniform; the kernel has no block barrier
+    const int nq = min(kQPW, a.N - qbase);
+    const int nsel = num_sel[pair];
+    const long cells = (long)a.rows * a.cols;
+    const int8_t *d0 = desc0 + pair * cells * kDescD;
+    const int8_t *d1 = desc1 + pair * cells * kDescD;
+    const unsigned long long *mk = masks + (long)pair * a.cols;
+    const int my_patch = (lane < nq && qbase + lane < nsel) ? patches1[(long)pair * a.N + qbase + lane] : -1;
+    int *lst = lst_s[w];
+    QueryResult mine = {0, 0, 0, -1, 0.0f};  // lane i: query qbase + i
+
+    QueryPrefetch cur = window_prefetch<kBuilt>(a, mk, d1, __shfl(my_patch, 0, 64), lane);
+    for (int i = 0; i < nq; i++) {
+        if (cur.patch1 < 0) break;  // queries past num_selected (patch order: all later ones too)
+        const QueryPrefetch nxt =
+            window_prefetch<kBuilt>(a, mk, d1, i + 1 < nq ? __shfl(my_patch, i + 1, 64) : -1, lane);
+        const int nv = window_list(cur, lane, a.rows, lst);
+        QueryResult res = {0, 0, 0, -1, 0.0f};
+        int entry = -1;
+        if (!kBuilt) {
+            int n2 = 0, unused = 0;
+            dot_x4(cur.q, cur.q, 2, n2, unused);
+            n2 += __shfl_xor(n2, 1, 64);
+            n2 += __shfl_xor(n2, 2, 64);
+            n2 += __shfl_xor(n2, 4, 64);
+            int bd = 0, bn = 1, bk = -1;
+            query_intended(d0, cur, nv, lst, lane, n2, bd, bn, bk);
+            if (bk >= 0) {
+                entry = bk;
+                res.score = (float)((double)bd * (double)bd / ((double)bn * (double)n2));
+            }
+        } else {
+            int bpos = -1;
+            float bdv = 0.0f;
+            query_built(a, d0, cur, nv, lst, lane, bpos, bdv);
+            if (bpos >= 0) {
+                entry = lst[bpos];
+                res.score = bdv;
+            }
+        }
+        if (entry >= 0) {
+            res.found = 1;
+            res.best_patch = cur.origin + entry;
+            res.bx = res.best_patch / a.rows;
+            res.by = res.best_patch % a.rows;
+        }
+        if (lane == i) mine = res;
+        cur = nxt;
+    }
+    if (lane < nq) out[(long)pair * a.N + qbase + lane] = mine;
+}
+
+// ---------------------------------------------------------------------------
+// Window match, tiled (as-intended; SURVEY 8(a) a7 with the exact cosine): one block per
+// (pair, band of kBandW frame-1 grid columns).  The band's queries are a contiguous run of
+// the top-N list (patch order), and every window of the band lies in the frame-0 columns
+// [X + sx - r, X + kBandW - 1 + sx + r]: their candidate cells (column masks) are staged into
+// LDS once, kChunk rows per pass (16-B chunks XOR-swizzled by row, |c|^2 and (x, y) beside
+// them).  Each wave owns 16 queries (A = 16 rows x 256 int8, 16 VGPRs, straight from HBM)
+// and sweeps every staged candidate with v_mfma_i32_16x16x64_i8 -- exact int32 dots, four
+// MFMAs per 16x16 tile; a tile element counts only when the candidate lies in the query's
+// window.  The pass test (100 dot^2 > 81 |c|^2 |q|^2) and the best (dot^2/|c|^2 compared
+// exactly, ties -> lower patch = earlier in the window scan) are integer; passing elements
+// are rare, so the exact update sits behind a branch the wave almost always skips.
+// A and B fragments use the same lane -> k map (lane l: bytes 64 s + 16 (l >> 4) .. +15 of
+// k-step s), so the dot is exact whatever k order the instruction uses; C/D: lane l holds
+// column l & 15, rows 4 (l >> 4) + j (cdna_hip_programming.md, gfx950 C/D map).
+// ---------------------------------------------------------------------------
+#ifndef WIN_BAND_W
+#define WIN_BAND_W 5
+#endif
+#ifndef WIN_CHUNK
+#define WIN_CHUNK 144
+#endif
+constexpr int kBandW = WIN_BAND_W;
+constexpr int kChunk = WIN_CHUNK;  // candidate rows staged per pass (multiple of 16)
+constexpr int kBandList = 960;     // band candidate-list capacity (host checks (kBandW + 2r) * rows)
+
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int kBandQ = 1024;  // top-N patches cached in LDS per block (more: read from global)
+
+__global__ __launch_bounds__(256) void k_window_tile(WinArgs a, int bands, int nblocks,
+                                                     const unsigned long long *__restrict__ masks,
+                                                     const int8_t *__restrict__ desc0,
+                                                     const int8_t *__restrict__ desc1,
+                                                     const int *__restrict__ num_sel,
+                                                     const int *__restrict__ patches1,
+                                                     QueryResult *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) int8_t cand_s[kChunk * kDescD];
+    __shared__ unsigned short list_s[kBandList];  // candidates, scan order, packed x * 64 + y
+    __shared__ unsigned short pp_s[kBandQ];  // the pair's top-N patches (host: cells <= 65536)
+    __shared__ int misc_s[4];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    // XCD-aware remap (gridDim.x is a multiple of 8): each XCD runs whole pairs
+    const int b = blockIdx.x, per_xcd = gridDim.x >> 3;
+    const int logical = (b & 7) * per_xcd + (b >> 3);
+    if (logical >= nblocks) return;  // block-uniform
+    const int pair = logical / bands, band = logical % bands;
+    const int R = a.rows, X = band * kBandW;
+    const long cells = (long)R * a.cols;
+    const int nsel = num_sel[pair];
+    const int *pp = patches1 + (long)pair * a.N;
+
+    // 1. (together) the window columns' masks and the top-N patches: the band's query run
+    //    [qa, qb) (patches ascend) and its scan-ordered candidate list
+    const int cx0 = max(X + a.shift_x - a.radius, 0);
+    const int cx1 = min(X + kBandW - 1 + a.shift_x + a.radius, a.cols - 1);
+    unsigned long long bits = 0;
+    if (w == 0 && lane <= cx1 - cx0) bits = masks[(long)pair * a.cols + cx0 + lane];
+    const int key0 = X * R, key1 = min(X + kBandW, a.cols) * R;
+    int c0 = 0, c1 = 0;
+    for (int q0 = 0; q0 < nsel; q0 += 1024) {  // four independent loads per thread per pass
+        int pv[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int q = q0 + 256 * u + t;
+            pv[u] = q < nsel ? pp[q] : 0x7fffffff;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int q = q0 + 256 * u + t;
+            if (q < kBandQ && q < nsel) pp_s[q] = pv[u];
+            c0 += pv[u] < key0;
+            c1 += pv[u] < key1;
+        }
+    }
+    c0 = wave_sum(c0);
+    c1 = wave_sum(c1);
+    if (t == 0) misc_s[0] = misc_s[1] = 0;
+    if (w == 0) {
+        const int cnt = __popcll(bits);
+        int incl = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) misc_s[2] = incl;
+        int pos = incl - cnt;
+        const int xy = (cx0 + lane) << 6;
+        while (bits) {
+            const int yb = __ffsll((long long)bits) - 1;
+            bits &= bits - 1;
+            list_s[pos++] = xy | yb;
+        }
+    }
+    __syncthreads();
+    if (lane == 0) {
+        atomicAdd(&misc_s[0], c0);
+        atomicAdd(&misc_s[1], c1);
+    }
+    __syncthreads();
+    const int qa = misc_s[0], nq = misc_s[1] - misc_s[0], ncand = misc_s[2];
+    if (nq <= 0) return;  // block-uniform; no barrier follows for anyone
+
+    const int8_t *d0 = desc0 + pair * cells * kDescD;
+    const int8_t *d1 = desc1 + pair * cells * kDescD;
+    const int n_mt = (nq + 15) >> 4, rounds = (n_mt + 3) >> 2;
+    const int n_chunks = (ncand + kChunk - 1) / kChunk;
+    const int h = lane >> 4, col = lane & 15;
+    const int r = a.radius;
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    for (int rd = 0; rd < rounds; rd++) {
+        const int mt = rd * 4 + w;
+        const bool active = mt < n_mt;
+        int bd[4], bn[4], bk[4], rn2[4], rcx[4], rcy[4];
+        i32x4_t A[4];
+        for (int ch = 0; ch < n_chunks; ch++) {
+            const int cbase = ch * kChunk, crows = min(kChunk, ncand - cbase);
+            if (rd == 0 || n_chunks > 1) {  // (one chunk: staged once for every round)
+                if (rd > 0 || ch > 0) __syncthreads();  // the previous chunk is consumed
+                // LDS DMA: wave w fills rows 4 i + (lane >> 4), i = w, w + 4, ...; lane l
+                // fetches 16-B chunk (l & 15) ^ (row & 15) into position l & 15 (swizzle)
+                for (int i = wu; i < (crows + 3) / 4; i += 4) {
+                    const int row = 4 * i + h;
+                    const int xy = list_s[cbase + min(row, crows - 1)];
+                    const int8_t *src =
+                        d0 + ((long)(xy >> 6) * R + (xy & 63)) * kDescD + ((col ^ (row & 15)) << 4);
+                    __builtin_amdgcn_global_load_lds(src, cand_s + i * 4 * kDescD, 16, 0, 0);
+                }
+            }
+            if (ch == 0) {  // this round's queries (A: row mt*16 + col, bytes 64 s + 16 h .. +15)
+                const int rowq = mt * 16 + col;
+                const bool rv = active && rowq < nq;
+                const int qp = rv ? (qa + rowq < kBandQ ? pp_s[qa + rowq] : pp[qa + rowq]) : 0;
+                const i32x4_t *qrow = reinterpret_cast<const i32x4_t *>(d1 + (long)qp * kDescD + 16 * h);
+#pragma unroll
+                for (int s2 = 0; s2 < 4; s2++) A[s2] = rv ? qrow[4 * s2] : i32x4_t{0, 0, 0, 0};
+                int n2 = 0;
+#pragma unroll
+                for (int s2 = 0; s2 < 4; s2++)
+#pragma unroll
+                    for (int u = 0; u < 4; u++) n2 = __builtin_amdgcn_sdot4(A[s2][u], A[s2][u], n2, false);
+                n2 += __shfl_xor(n2, 16, 64);
+                n2 += __shfl_xor(n2, 32, 64);
+                // window centre of row `col`; rows past nq get a centre no candidate is near
+                const int qcx = rv ? qp / R + a.shift_x : -(1 << 20), qcy = rv ? qp % R + a.shift_y : -(1 << 20);
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    rn2[j] = __shfl(n2, 4 * h + j, 64);
+                    rcx[j] = __shfl(qcx, 4 * h + j, 64);
+                    rcy[j] = __shfl(qcy, 4 * h + j, 64);
+                    bd[j] = 0;
+                    bn[j] = 1;
+                    bk[j] = -1;
+                }
+            }
+            if (rd == 0 || n_chunks > 1) {
+                __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed
+                __syncthreads();                // ... and every other wave's
+            }
+            if (!active) continue;
+            const int ntiles = (crows + 15) >> 4;
+            for (int nt = 0; nt < ntiles; nt++) {
+                const int cr = nt * 16 + col;  // this lane's candidate (C/D column)
+                const int8_t *brow = cand_s + cr * kDescD;
+                i32x4_t acc = {0, 0, 0, 0};
+                int cna = 0;
+#pragma unroll
+                for (int s2 = 0; s2 < 4; s2++) {
+                    const i32x4_t bf = *reinterpret_cast<const i32x4_t *>(brow + (((4 * s2 + h) ^ (cr & 15)) << 4));
+                    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[s2], bf, acc, 0, 0, 0);
+#pragma unroll
+                    for (int u = 0; u < 4; u++) cna = __builtin_amdgcn_sdot4(bf[u], bf[u], cna, false);
+                }
+                cna += __shfl_xor(cna, 16, 64);
+                cna += __shfl_xor(cna, 32, 64);
+                const bool cv = cr < crows;
+                const int cxy = cv ? list_s[cbase + cr] : (1 << 24);
+                const int cx = cxy >> 6, cy = cxy & 63;
+                const int cp = cx * R + cy;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int d = acc[j];
+                    const bool pass = cv && (unsigned)(cx - rcx[j] + r) <= (unsigned)(2 * r) &&
+                                      (unsigned)(cy - rcy[j] + r) <= (unsigned)(2 * r) && d > 0 &&
+                                      (unsigned long long)(100ll * d * d) >
+                                          81ull * (unsigned long long)((long long)cna * rn2[j]);
+                    if (pass && better_i32(d, cna, cp, bd[j], bn[j], bk[j])) {
+                        bd[j] = d;
+                        bn[j] = cna;
+                        bk[j] = cp;
+                    }
+                }
+            }
+        }
+        if (!active) continue;
+        // best of each row over its 16 columns (lanes 16 h .. 16 h + 15)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {
+                const int od = __shfl_xor(bd[j], o, 64), on = __shfl_xor(bn[j], o, 64), ok = __shfl_xor(bk[j], o, 64);
+                if (better_i32(od, on, ok, bd[j], bn[j], bk[j])) {
+                    bd[j] = od;
+                    bn[j] = on;
+                    bk[j] = ok;
+                }
+            }
+        }
+        if (col == 0) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int qi = mt * 16 + 4 * h + j;
+                if (qi >= nq) continue;
+                QueryResult res = {0, 0, 0, -1, 0.0f};
+                if (bk[j] >= 0) {
+                    res.found = 1;
+                    res.best_patch = bk[j];
+                    res.bx = bk[j] / R;
+                    res.by = bk[j] % R;
+                    res.score = (float)((double)bd[j] * (double)bd[j] / ((double)bn[j] * (double)rn2[j]));
+                }
+                out[(long)pair * a.N + qa + qi] = res;
+            }
+        }
+    }
 }
 
 __global__ __launch_bounds__(1024) void k_window_compact(int N, int rows, int max_matches,
@@ -579,6 +1134,7 @@ __global__ __launch_bounds__(1024) void k_window_compact(int N, int rows, int ma
                                                          const int *__restrict__ num_sel,
                                                          const int *__restrict__ patches1,
                                                          const int *__restrict__ indices1,
+                                                         const int *__restrict__ max_idx0, long cells,
                                                          int *__restrict__ num_matches, float *__restrict__ points1,
                                                          float *__restrict__ points2, int *__restrict__ qom) {
     __shared__ int wsum[16];
@@ -598,10 +1154,11 @@ __global__ __launch_bounds__(1024) void k_window_compact(int N, int rows, int ma
             const int x1 = patch1 / rows, y1 = patch1 % rows;
             const int idx1 = indices1[(long)pair * N + q];
             const QueryResult m = r[q];
+            const int best_index = max_idx0[(long)pair * cells + m.best_patch];  // image0 index of the winner
             float *p1 = points1 + ((long)pair * max_matches + k) * 2;
             float *p2 = points2 + ((long)pair * max_matches + k) * 2;
-            p1[0] = (float)(m.bx * 8 + m.best_index % 8);
-            p1[1] = (float)(m.by * 8 + m.best_index / 8);
+            p1[0] = (float)(m.bx * 8 + best_index % 8);
+            p1[1] = (float)(m.by * 8 + best_index / 8);
             p2[0] = (float)(x1 * 8 + idx1 % 8);
             p2[1] = (float)(y1 * 8 + idx1 / 8);
             if (qom) qom[(long)pair * max_matches + k] = q;
@@ -654,8 +1211,6 @@ extern "C" int mv_window_match_batch_dev(mv_context *ctx, const mv_window_params
     MV_REQUIRE(num_matches && points1 && points2);
     MV_REQUIRE(((uintptr_t)desc0 & 15) == 0 && ((uintptr_t)desc1 & 15) == 0);
     MV_HIP_TRY(hipSetDevice(ctx->device));
-    QueryResult *qr = (QueryResult *)mv::scratch(ctx, sizeof(QueryResult) * (size_t)batch * N);
-    if (!qr) return MV_ERR_OUT_OF_MEMORY;
     WinArgs a;
     a.rows = rows;
     a.cols = cols;
@@ -666,14 +1221,60 @@ extern "C" int mv_window_match_batch_dev(mv_context *ctx, const mv_window_params
     a.as_built = p->semantics == MV_AS_BUILT;
     a.thr_sq = p->match_thresh_sq;
     a.prob_thr = p->prob_thresh;
-    MV_PROF_BEGIN(ctx->stream, "k_window_eval");
-    hipLaunchKernelGGL(k_window_eval, dim3((N + 3) / 4, batch), dim3(256), 0, ctx->stream, a, desc0, max_idx0,
-                       probs0, desc1, num_selected, patches1, qr);
-    MV_PROF_END(ctx->stream);
-    MV_LAUNCH_CHECK();
+    const long cells = (long)rows * cols;
+    // fast path: one mask word per column and a window list that fits the wave's LDS slice
+    const int wside = 2 * p->radius + 1;
+    const bool fast = rows <= 64 && p->radius >= 0 && wside <= 64 && (long)wside * min(wside, rows) <= kWinList;
+    const size_t qr_bytes = mv::align_up(sizeof(QueryResult) * (size_t)batch * N, 256);
+    char *sc = (char *)mv::scratch(ctx, qr_bytes + (fast ? sizeof(unsigned long long) * (size_t)batch * cols : 0));
+    if (!sc) return MV_ERR_OUT_OF_MEMORY;
+    QueryResult *qr = (QueryResult *)sc;
+    if (fast) {
+        unsigned long long *masks = (unsigned long long *)(sc + qr_bytes);
+        const long tcols = (long)batch * cols;
+        MV_PROF_BEGIN(ctx->stream, "k_window_mask");
+        hipLaunchKernelGGL(k_window_mask, dim3((unsigned)((tcols + 3) / 4)), dim3(256), 0, ctx->stream, tcols, rows,
+                           max_idx0, probs0, a.prob_thr, masks);
+        MV_PROF_END(ctx->stream);
+        MV_LAUNCH_CHECK();
+        const bool tiled = !a.as_built && kBandW + 2 * p->radius <= 64 && cells <= 65536 && cols <= 1024 &&
+                           (long)(kBandW + 2 * p->radius) * rows <= kBandList;
+        if (tiled) {
+            const int bands = (cols + kBandW - 1) / kBandW;
+            const long nblk = (long)bands * batch;
+            MV_REQUIRE(nblk < (1l << 30));
+            const unsigned g = (unsigned)((nblk + 7) / 8 * 8);
+            MV_PROF_BEGIN(ctx->stream, "k_window_eval");
+            hipLaunchKernelGGL(k_window_tile, dim3(g), dim3(256), 0, ctx->stream, a, bands, (int)nblk, masks, desc0,
+                               desc1, num_selected, patches1, qr);
+            MV_PROF_END(ctx->stream);
+            MV_LAUNCH_CHECK();
+        } else {
+        const int bpp = (N + 4 * kQPW - 1) / (4 * kQPW);
+        const long nblocks = (long)bpp * batch;
+        MV_REQUIRE(nblocks < (1l << 30));
+        const unsigned grid = (unsigned)((nblocks + 7) / 8 * 8);
+        MV_PROF_BEGIN(ctx->stream, "k_window_eval");
+        if (a.as_built)
+            hipLaunchKernelGGL(k_window_query<true>, dim3(grid), dim3(256), 0, ctx->stream, a, bpp, (int)nblocks,
+                               masks, desc0, desc1, num_selected, patches1, qr);
+        else
+            hipLaunchKernelGGL(k_window_query<false>, dim3(grid), dim3(256), 0, ctx->stream, a, bpp, (int)nblocks,
+                               masks, desc0, desc1, num_selected, patches1, qr);
+        MV_PROF_END(ctx->stream);
+        MV_LAUNCH_CHECK();
+        }
+    } else {
+        MV_PROF_BEGIN(ctx->stream, "k_window_eval");
+        hipLaunchKernelGGL(k_window_eval, dim3((N + 3) / 4, batch), dim3(256), 0, ctx->stream, a, desc0, max_idx0,
+                           probs0, desc1, num_selected, patches1, qr);
+        MV_PROF_END(ctx->stream);
+        MV_LAUNCH_CHECK();
+    }
     MV_PROF_BEGIN(ctx->stream, "k_window_compact");
     hipLaunchKernelGGL(k_window_compact, dim3(batch), dim3(1024), 0, ctx->stream, N, rows, p->max_matches, qr,
-                       num_selected, patches1, indices1, num_matches, points1, points2, query_of_match);
+                       num_selected, patches1, indices1, max_idx0, cells, num_matches, points1, points2,
+                       query_of_match);
     MV_PROF_END(ctx->stream);
     MV_LAUNCH_CHECK();
     return MV_OK;
