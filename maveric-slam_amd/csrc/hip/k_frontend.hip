@@ -38,69 +38,96 @@ __device__ __forceinline__ float approx_exp(const float sp[5], int x) {
 }
 
 // ---------------------------------------------------------------------------
-// k_softmax: block = 256 consecutive (frame, cell) rows of 65 int8.
-// The 16,640-byte row block is staged into LDS with coalesced dword loads; each
-// lane then walks its own row (65 logits) in the reference order.  approx_exp
-// depends only on (scale, x) with x in 0..127, so the block first tabulates it for
-// the (at most two) frames it spans -- the same arithmetic, the same bits -- and
-// the row walk reads the table.  Row bytes come from aligned dword reads
-// (v_alignbyte) instead of 65 byte reads.
+// k_softmax: block = 256 consecutive (frame, cell) rows of 65 int8, staged into LDS by
+// LDS DMA (16,640 B per block, 16-B aligned).  The reference walks all 65 logits, skipping
+// the negative ones (top_N.c:29-41); here each lane first builds its row's 64-bit mask of
+// non-negative logits from 16 aligned dwords (sign bits, four logits per dword) and then
+// visits only those, in ascending order -- so the float sum and the strict-max updates
+// happen in exactly the reference's order -- computing approx_exp arithmetically (the same
+// expression, the same bits).  Logit 64 (the dustbin) is added last and never wins the max.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_softmax(int total_rows, int cells, const float *__restrict__ scales,
                                                  const int8_t *__restrict__ semi, int *__restrict__ max_idx,
                                                  float *__restrict__ probs, int *__restrict__ num_valid) {
     __shared__ __attribute__((aligned(16))) int lds32[256 * kSemiC / 4 + 4];
-    __shared__ float lut[2][128];
-    const int t = threadIdx.x;
+    __shared__ float sp_s[2][5];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const long r0 = (long)blockIdx.x * 256;
     const int nrows = (int)min((long)256, (long)total_rows - r0);
     const int nbytes = nrows * kSemiC;
-    const long base = r0 * kSemiC;  // multiple of 4 (256*65 = 16640)
-    const int *g32 = reinterpret_cast<const int *>(semi + base);
-    for (int i = t; i < nbytes / 4; i += 256) lds32[i] = g32[i];
-    for (int i = (nbytes / 4) * 4 + t; i < nbytes; i += 256)
-        reinterpret_cast<int8_t *>(lds32)[i] = semi[base + i];
+    const long base = r0 * kSemiC;  // multiple of 16 (256*65 = 16640)
+    if (nrows == 256) {
+        // 1040 16-B pieces: 4 per lane + 16 (wave 0, lanes 0..15)
+        const int8_t *src = semi + base;
+        char *dst = reinterpret_cast<char *>(lds32);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int piece = i * 256 + w * 64;  // this wave's 64 pieces of pass i
+            __builtin_amdgcn_global_load_lds(src + (long)(piece + lane) * 16, dst + piece * 16, 16, 0, 0);
+        }
+        if (w == 0 && lane < 16) __builtin_amdgcn_global_load_lds(src + (1024 + lane) * 16, dst + 1024 * 16, 16, 0, 0);
+    } else {
+        const int *g32 = reinterpret_cast<const int *>(semi + base);
+        for (int i = t; i < nbytes / 4; i += 256) lds32[i] = g32[i];
+        for (int i = (nbytes / 4) * 4 + t; i < nbytes; i += 256)
+            reinterpret_cast<int8_t *>(lds32)[i] = semi[base + i];
+    }
     const int f_first = (int)(r0 / cells);
-    {  // approx_exp(x), x = 0..127, for frames f_first and f_first + 1 (top_N.c:12-20, 59-63)
-        const int f = f_first + (t >> 7), x = t & 127;
+    if (t < 2) {  // the polynomial of the (at most two) frames the block spans (top_N.c:59-63)
+        const int f = f_first + t;
         if ((long)f * cells < (long)total_rows) {
             float sp[5];
             scale_poly(scales[f], sp);
-            lut[t >> 7][x] = approx_exp(sp, x);
+#pragma unroll
+            for (int i = 0; i < 5; i++) sp_s[t][i] = sp[i];
         }
     }
+    __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     if (t >= nrows) return;
     const long r = r0 + t;
     const int frame = (int)(r / cells);
     const int fl = frame - f_first;  // < 2 whenever cells >= 256
-    float sp_own[5];
-    if (fl >= 2) scale_poly(scales[frame], sp_own);  // tiny frames: no table for this one
-    // the row's 65 bytes: 17 aligned dwords re-aligned to the row start, + the last byte
+    float sp[5];
+    if (fl < 2) {
+#pragma unroll
+        for (int i = 0; i < 5; i++) sp[i] = sp_s[fl][i];
+    } else {
+        scale_poly(scales[frame], sp);  // tiny frames
+    }
+    // the row's 65 bytes: dwords re-aligned to the row start; mask of non-negative logits
     const int rb = t * kSemiC, o = rb & 3, d0 = rb >> 2;
+    unsigned mlo = 0, mhi = 0;
+    unsigned wv = (unsigned)lds32[d0];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const unsigned wn = (unsigned)lds32[d0 + j + 1];
+        const unsigned u = __builtin_amdgcn_alignbyte(wn, wv, o);  // bytes 4j .. 4j+3 of the row
+        wv = wn;
+        const unsigned nn = ~u & 0x80808080u;
+        const unsigned m4 = ((nn >> 7) | (nn >> 14) | (nn >> 21) | (nn >> 28)) & 0xFu;
+        if (j < 8)
+            mlo |= m4 << (4 * j);
+        else
+            mhi |= m4 << (4 * (j - 8));
+    }
+    const int8_t *row = reinterpret_cast<const int8_t *>(lds32) + rb;
     int best = 64;
     float best_e = 0.0f;
     float den = 1.17549435e-38f;  // FLT_MIN (top_N.c:30)
-    unsigned w = (unsigned)lds32[d0];
-#pragma unroll
-    for (int j = 0; j < 17; j++) {
-        const unsigned wn = (unsigned)lds32[d0 + j + 1];
-        const unsigned u = __builtin_amdgcn_alignbyte(wn, w, o);  // bytes 4j .. 4j+3 of the row
-        w = wn;
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            const int i = 4 * j + b;
-            if (i >= kSemiC) break;
-            const int x = (int)(signed char)(u >> (8 * b));
-            if (x < 0) continue;
-            const float e = fl < 2 ? lut[fl][x] : approx_exp(sp_own, x);
-            if (i != 64 && e > best_e) {
-                best_e = e;
-                best = i;
-            }
-            den += e;
+    unsigned long long m = ((unsigned long long)mhi << 32) | mlo;
+    while (m) {
+        const int i = __builtin_ctzll(m);
+        m &= m - 1;
+        const float e = approx_exp(sp, (int)row[i]);
+        if (e > best_e) {
+            best_e = e;
+            best = i;
         }
+        den += e;
     }
+    const int x64 = (int)row[64];
+    if (x64 >= 0) den += approx_exp(sp, x64);
     max_idx[r] = best;
     probs[r] = best != 64 ? best_e / den : -1.0f;
     // (*num_valid)++ per valid cell (top_N.c:160): one atomic per wave and frame, not per
