@@ -956,6 +956,32 @@ constexpr int kBandList = 960;     // band candidate-list capacity (host checks 
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
+// One 16x16 tile's elements (lane: candidate column; rows 4 h + j): window membership, the
+// as-intended pass test 100 dot^2 > 81 |c|^2 |q|^2 and the exact running best.  The pass
+// test is screened in fp32 (relative error < 2^-20 on both sides) and decided in 64-bit
+// integers only within that margin.
+__device__ __forceinline__ void window_fold(const i32x4_t &acc, bool cv, int cx, int cy, int cp, int cna, int r,
+                                            const int *rcx, const int *rcy, const int *rn2, int *bd, int *bn,
+                                            int *bk) {
+    const float fna81 = 81.0f * (float)cna;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int d = acc[j];
+        const bool in = cv && (unsigned)(cx - rcx[j] + r) <= (unsigned)(2 * r) &&
+                        (unsigned)(cy - rcy[j] + r) <= (unsigned)(2 * r) && d > 0;
+        const float fd = (float)d;
+        const float lhs = 100.0f * fd * fd, rhs = fna81 * (float)rn2[j];
+        bool pass = in && lhs > rhs * 1.000002f;
+        if (in && !pass && lhs >= rhs * 0.999998f)  // within the screen's margin: exact
+            pass = (unsigned long long)(100ll * d * d) > 81ull * (unsigned long long)((long long)cna * rn2[j]);
+        if (pass && better_i32(d, cna, cp, bd[j], bn[j], bk[j])) {
+            bd[j] = d;
+            bn[j] = cna;
+            bk[j] = cp;
+        }
+    }
+}
+
 constexpr int kBandQ = 1024;  // top-N patches cached in LDS per block (more: read from global)
 
 __global__ __launch_bounds__(256) void k_window_tile(WinArgs a, int bands, int nblocks,
@@ -1108,19 +1134,7 @@ __global__ __launch_bounds__(256) void k_window_tile(WinArgs a, int bands, int n
                 const int cxy = cv ? list_s[cbase + cr] : (1 << 24);
                 const int cx = cxy >> 6, cy = cxy & 63;
                 const int cp = cx * R + cy;
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int d = acc[j];
-                    const bool pass = cv && (unsigned)(cx - rcx[j] + r) <= (unsigned)(2 * r) &&
-                                      (unsigned)(cy - rcy[j] + r) <= (unsigned)(2 * r) && d > 0 &&
-                                      (unsigned long long)(100ll * d * d) >
-                                          81ull * (unsigned long long)((long long)cna * rn2[j]);
-                    if (pass && better_i32(d, cna, cp, bd[j], bn[j], bk[j])) {
-                        bd[j] = d;
-                        bn[j] = cna;
-                        bk[j] = cp;
-                    }
-                }
+                window_fold(acc, cv, cx, cy, cp, cna, r, rcx, rcy, rn2, bd, bn, bk);
             }
         }
         if (!active) continue;
@@ -1152,6 +1166,169 @@ __global__ __launch_bounds__(256) void k_window_tile(WinArgs a, int bands, int n
                 }
                 out[(long)pair * a.N + qa + qi] = res;
             }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Window match, per-wave MFMA (as-intended; the default): one wave owns 16 consecutive
+// top-N queries of a pair -- patch order, so they span a few grid columns -- and sweeps the
+// candidates of the union of their windows' columns (column masks -> scan-ordered list in the
+// wave's LDS slice) with v_mfma_i32_16x16x64_i8, B fragments gathered straight from L2/HBM one
+// 16-candidate tile ahead.  No block barrier and no shared staging: latency is hidden by
+// occupancy (waves are independent), the band-tiled kernel above being the shared-staging
+// alternative (WIN_TILED=1).  Epilogue as in k_window_tile.
+// ---------------------------------------------------------------------------
+constexpr int kWQ = 16;            // queries per wave
+
+constexpr int kWaveList = 512;     // candidate-list capacity per wave (more: several passes)
+
+__device__ __forceinline__ void load_bfrag(const int8_t *d0, int R, int xy, bool ok, int h, i32x4_t *bf) {
+    const i32x4_t *src = reinterpret_cast<const i32x4_t *>(d0 + ((long)(xy >> 6) * R + (xy & 63)) * kDescD + 16 * h);
+#pragma unroll
+    for (int s2 = 0; s2 < 4; s2++) bf[s2] = ok ? src[4 * s2] : i32x4_t{0, 0, 0, 0};
+}
+
+#ifndef WIN_WPE
+#define WIN_WPE 2
+#endif
+__global__ __launch_bounds__(256, WIN_WPE) void k_window_wave(WinArgs a, int blocks_per_pair, int nblocks,
+                                                     const unsigned long long *__restrict__ masks,
+                                                     const int8_t *__restrict__ desc0,
+                                                     const int8_t *__restrict__ desc1,
+                                                     const int *__restrict__ num_sel,
+                                                     const int *__restrict__ patches1,
+                                                     QueryResult *__restrict__ out) {
+    __shared__ unsigned short lst_s[4][kWaveList];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int b = blockIdx.x, per_xcd = gridDim.x >> 3;
+    const int logical = (b & 7) * per_xcd + (b >> 3);
+    if (logical >= nblocks) return;
+    const int pair = logical / blocks_per_pair;
+    const int q0 = ((logical % blocks_per_pair) * 4 + w) * kWQ;
+    const int nsel = min(num_sel[pair], a.N);
+    if (q0 >= nsel) return;  // wave-uniform; the kernel has no block barrier
+    const int nq = min(kWQ, nsel - q0);
+    const int R = a.rows, r = a.radius;
+    const long cells = (long)R * a.cols;
+    const int8_t *d0 = desc0 + pair * cells * kDescD;
+    const int8_t *d1 = desc1 + pair * cells * kDescD;
+    const int h = lane >> 4, col = lane & 15;
+    unsigned short *lst = lst_s[w];
+
+    // queries: row `col` = query q0 + col (A: bytes 64 s + 16 h .. +15)
+    const bool rv = col < nq;
+    const int qp = patches1[(long)pair * a.N + q0 + min(col, nq - 1)];
+    const int xfirst = __shfl(qp, 0, 64) / R, xlast = __shfl(qp, nq - 1, 64) / R;
+    const int cx0 = max(xfirst + a.shift_x - r, 0), cx1 = min(xlast + a.shift_x + r, a.cols - 1);
+    i32x4_t A[4];
+    {
+        const i32x4_t *qrow = reinterpret_cast<const i32x4_t *>(d1 + (long)qp * kDescD + 16 * h);
+#pragma unroll
+        for (int s2 = 0; s2 < 4; s2++) A[s2] = rv ? qrow[4 * s2] : i32x4_t{0, 0, 0, 0};
+    }
+    unsigned long long bits = 0;
+    if (cx0 + lane <= cx1 && lane < 64) bits = masks[(long)pair * a.cols + cx0 + lane];
+    int n2 = 0;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; s2++)
+#pragma unroll
+        for (int u = 0; u < 4; u++) n2 = __builtin_amdgcn_sdot4(A[s2][u], A[s2][u], n2, false);
+    n2 += __shfl_xor(n2, 16, 64);
+    n2 += __shfl_xor(n2, 32, 64);
+    const int qcx = rv ? qp / R + a.shift_x : -(1 << 20), qcy = rv ? qp % R + a.shift_y : -(1 << 20);
+    int rn2[4], rcx[4], rcy[4], bd[4], bn[4], bk[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        rn2[j] = __shfl(n2, 4 * h + j, 64);
+        rcx[j] = __shfl(qcx, 4 * h + j, 64);
+        rcy[j] = __shfl(qcy, 4 * h + j, 64);
+        bd[j] = 0;
+        bn[j] = 1;
+        bk[j] = -1;
+    }
+    // candidate list: columns cx0 .. cx1 (<= 64 when the 16 queries span <= 64 - 2r columns;
+    // wider spans take the column groups in turn), scan order, in passes of kWaveList
+    for (int cg = cx0; cg <= cx1; cg += 64) {
+        if (cg > cx0) bits = (cg + lane <= cx1) ? masks[(long)pair * a.cols + cg + lane] : 0ull;
+        const int cnt = __popcll(bits);
+        int incl = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        const int total = __shfl(incl, 63, 64);
+        for (int lb = 0; lb < total; lb += kWaveList) {
+            {
+                int pos = incl - cnt - lb;
+                unsigned long long bb = bits;
+                const int xy = (cg + lane) << 6;
+                while (bb && pos < kWaveList) {
+                    const int yb = __ffsll((long long)bb) - 1;
+                    bb &= bb - 1;
+                    if (pos >= 0) lst[pos] = (unsigned short)(xy | yb);
+                    pos++;
+                }
+            }
+            const int nc = min(kWaveList, total - lb);
+            const int ntiles = (nc + 15) >> 4;
+            i32x4_t bcur[4], bnxt[4];
+            int xycur = lst[min(col, nc - 1)];
+            load_bfrag(d0, R, xycur, col < nc, h, bcur);
+            for (int nt = 0; nt < ntiles; nt++) {  // B fragments one tile ahead
+                const int cr = nt * 16 + col;
+                const bool more = nt + 1 < ntiles;
+                const int xynxt = more ? lst[min(cr + 16, nc - 1)] : 0;
+                if (more) load_bfrag(d0, R, xynxt, cr + 16 < nc, h, bnxt);
+                i32x4_t acc = {0, 0, 0, 0};
+                int cna = 0;
+#pragma unroll
+                for (int s2 = 0; s2 < 4; s2++) {
+                    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[s2], bcur[s2], acc, 0, 0, 0);
+#pragma unroll
+                    for (int u = 0; u < 4; u++) cna = __builtin_amdgcn_sdot4(bcur[s2][u], bcur[s2][u], cna, false);
+                }
+                cna += __shfl_xor(cna, 16, 64);
+                cna += __shfl_xor(cna, 32, 64);
+                const bool cv = cr < nc;
+                const int cx = cv ? xycur >> 6 : (1 << 24), cy = xycur & 63;
+                const int cp = cx * R + cy;
+                window_fold(acc, cv, cx, cy, cp, cna, r, rcx, rcy, rn2, bd, bn, bk);
+                if (more) {
+#pragma unroll
+                    for (int s2 = 0; s2 < 4; s2++) bcur[s2] = bnxt[s2];
+                    xycur = xynxt;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            const int od = __shfl_xor(bd[j], o, 64), on = __shfl_xor(bn[j], o, 64), ok = __shfl_xor(bk[j], o, 64);
+            if (better_i32(od, on, ok, bd[j], bn[j], bk[j])) {
+                bd[j] = od;
+                bn[j] = on;
+                bk[j] = ok;
+            }
+        }
+    }
+    if (col == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int qi = 4 * h + j;
+            if (qi >= nq) continue;
+            QueryResult res = {0, 0, 0, -1, 0.0f};
+            if (bk[j] >= 0) {
+                res.found = 1;
+                res.best_patch = bk[j];
+                res.bx = bk[j] / R;
+                res.by = bk[j] % R;
+                res.score = (float)((double)bd[j] * (double)bd[j] / ((double)bn[j] * (double)rn2[j]));
+            }
+            out[(long)pair * a.N + q0 + qi] = res;
         }
     }
 }
@@ -1266,7 +1443,20 @@ extern "C" int mv_window_match_batch_dev(mv_context *ctx, const mv_window_params
         MV_LAUNCH_CHECK();
         const bool tiled = !a.as_built && kBandW + 2 * p->radius <= 64 && cells <= 65536 && cols <= 1024 &&
                            (long)(kBandW + 2 * p->radius) * rows <= kBandList;
-        if (tiled) {
+#ifndef WIN_TILED
+#define WIN_TILED 0
+#endif
+        if (tiled && !WIN_TILED) {
+            const int bpp = (N + 4 * kWQ - 1) / (4 * kWQ);
+            const long nblk = (long)bpp * batch;
+            MV_REQUIRE(nblk < (1l << 30));
+            const unsigned g = (unsigned)((nblk + 7) / 8 * 8);
+            MV_PROF_BEGIN(ctx->stream, "k_window_eval");
+            hipLaunchKernelGGL(k_window_wave, dim3(g), dim3(256), 0, ctx->stream, a, bpp, (int)nblk, masks, desc0,
+                               desc1, num_selected, patches1, qr);
+            MV_PROF_END(ctx->stream);
+            MV_LAUNCH_CHECK();
+        } else if (tiled) {
             const int bands = (cols + kBandW - 1) / kBandW;
             const long nblk = (long)bands * batch;
             MV_REQUIRE(nblk < (1l << 30));

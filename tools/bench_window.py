@@ -119,7 +119,7 @@ def main():
     el = time.perf_counter() - t0
     mvtrack.profile_enable(False)
     stages = {}
-    for k in ("k_softmax", "k_top_n_select", "k_window_eval", "k_window_compact"):
+    for k in ("k_softmax", "k_top_n_select", "k_window_mask", "k_window_eval", "k_window_compact"):
         ms, n = mvtrack.profile_query(k)
         stages[k] = round(ms / max(n, 1), 4)
     checked = 0
