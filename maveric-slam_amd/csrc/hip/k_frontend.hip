@@ -174,7 +174,10 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int *total, int *wsum
 }
 
 // k_top_n_select: one 1024-thread block per frame; thread t owns the
-// contiguous cells [t*per, (t+1)*per) so that scans preserve patch order.
+// contiguous cells [t*per, (t+1)*per) so that scans preserve patch order.  With PER > 0
+// (per <= PER, e.g. the 7285-cell KITTI grid) a thread's cells are read once, all loads
+// in flight together, and kept in registers for the three passes.
+template <int PER>
 __global__ __launch_bounds__(1024) void k_top_n_select(int cells, const int *__restrict__ max_idx,
                                                        const float *__restrict__ probs, int N, int cap,
                                                        int *__restrict__ num_sel, int *__restrict__ patches,
@@ -187,13 +190,38 @@ __global__ __launch_bounds__(1024) void k_top_n_select(int cells, const int *__r
     const int c0 = t * per, c1 = min(c0 + per, cells);
     const int *mi = max_idx + (long)f * cells;
     const float *pr = probs + (long)f * cells;
+    constexpr int NR = PER > 0 ? PER : 1;
+    int mi_r[NR];
+    float pr_r[NR];
+    if (PER > 0) {
+#pragma unroll
+        for (int k = 0; k < NR; k++) {
+            const int c = c0 + k;
+            mi_r[k] = c < c1 ? mi[c] : 64;
+            pr_r[k] = c < c1 ? pr[c] : 0.0f;
+        }
+    }
+    const int n = PER > 0 ? NR : c1 - c0;
+    // cell c0 + k: (index, prob); valid per top_N.c:71-73
+    auto cell = [&](int k, int &idx, float &p) {
+        if (PER > 0) {
+            idx = mi_r[k];
+            p = pr_r[k];
+        } else {
+            idx = mi[c0 + k];
+            p = pr[c0 + k];
+        }
+        return idx != 64 && (double)p > 0.01;
+    };
     int nv_local = 0;
     float pmax = 0.0f, pmin = 3.40282347e+38f;  // FLT_MAX
-    for (int c = c0; c < c1; c++) {
-        if (mi[c] != 64 && (double)pr[c] > 0.01) {
+    for (int k = 0; k < n; k++) {
+        int idx;
+        float p;
+        if (cell(k, idx, p)) {
             nv_local++;
-            pmax = fmaxf(pmax, pr[c]);
-            pmin = fminf(pmin, pr[c]);
+            pmax = fmaxf(pmax, p);
+            pmin = fminf(pmin, p);
         }
     }
     int nv;
@@ -229,11 +257,13 @@ __global__ __launch_bounds__(1024) void k_top_n_select(int cells, const int *__r
     }
     if (nv <= N) {
         int k = off;
-        for (int c = c0; c < c1; c++) {
-            if (mi[c] != 64 && (double)pr[c] > 0.01) {
-                op[k] = c;
-                oi[k] = mi[c];
-                opr[k] = pr[c];
+        for (int j = 0; j < n; j++) {
+            int idx;
+            float p;
+            if (cell(j, idx, p)) {
+                op[k] = c0 + j;
+                oi[k] = idx;
+                opr[k] = p;
                 k++;
             }
         }
@@ -246,15 +276,20 @@ __global__ __launch_bounds__(1024) void k_top_n_select(int cells, const int *__r
     const float split = (float)N / (float)nv;
     const float thr = pmax * split + pmin * (1 - split);
     int ns_local = 0;
-    for (int c = c0; c < c1; c++)
-        if (mi[c] != 64 && (double)pr[c] > 0.01 && pr[c] >= thr) ns_local++;
+    for (int j = 0; j < n; j++) {
+        int idx;
+        float p;
+        if (cell(j, idx, p) && p >= thr) ns_local++;
+    }
     int ns;
     int k = block_exclusive_scan<1024>(ns_local, &ns, wsum);
-    for (int c = c0; c < c1 && k < N; c++) {
-        if (mi[c] != 64 && (double)pr[c] > 0.01 && pr[c] >= thr) {
-            op[k] = c;
-            oi[k] = mi[c];
-            opr[k] = pr[c];
+    for (int j = 0; j < n; j++) {
+        int idx;
+        float p;
+        if (k < N && cell(j, idx, p) && p >= thr) {
+            op[k] = c0 + j;
+            oi[k] = idx;
+            opr[k] = p;
             k++;
         }
     }
@@ -1395,8 +1430,12 @@ int launch_top_n_select(hipStream_t s, int batch, int cells, const int *max_idx,
                         int cap, int *num_sel, int *patches, int *indices, float *sel_probs, int *status) {
     MV_REQUIRE(batch > 0 && cells > 0 && N > 0 && cap > 0);
     MV_PROF_BEGIN(s, "k_top_n_select");
-    hipLaunchKernelGGL(k_top_n_select, dim3(batch), dim3(1024), 0, s, cells, max_idx, probs, N, cap, num_sel,
-                       patches, indices, sel_probs, status);
+    if (cells <= 8 * 1024)
+        hipLaunchKernelGGL(k_top_n_select<8>, dim3(batch), dim3(1024), 0, s, cells, max_idx, probs, N, cap,
+                           num_sel, patches, indices, sel_probs, status);
+    else
+        hipLaunchKernelGGL(k_top_n_select<0>, dim3(batch), dim3(1024), 0, s, cells, max_idx, probs, N, cap,
+                           num_sel, patches, indices, sel_probs, status);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     return MV_OK;
