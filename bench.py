@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", type=int, default=2, help="pairs verified against the oracle after timing")
+    ap.add_argument("--window-steps", type=int, default=10,
+                    help="secondary line (N = 1 only): the windowed int8 front-end of tracking_main.c "
+                         "(tools/bench_window.py, 7285-cell KITTI grid, 1024 pairs); 0 = skip")
     return ap.parse_args()
 
 
@@ -303,6 +306,15 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, n)
+    if rank == 0 and world == 1 and args.window_steps > 0:
+        # north-star secondary: HBM roofline of the windowed match kernel, timed
+        # after (and outside) the headline measurement
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import bench_window
+
+        w, _ = bench_window.run(batch=1024, steps=args.window_steps, warmup=2, check=1)
+        out["window_frontend"] = {k: w[k] for k in ("metric", "value", "unit", "ms_per_step", "semantics",
+                                                     "stages_ms", "hbm_roofline", "checked_pairs")}
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -59,30 +59,18 @@ def cpu_baseline(pairs, built, N, cells, seconds):
                       % (total, cells, N, dt, threads)}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--batch", type=int, default=1024)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--distinct", type=int, default=8, help="distinct synthetic pairs tiled over the batch")
-    ap.add_argument("--as-built", action="store_true")
-    ap.add_argument("--check", type=int, default=2)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--grid", choices=["kitti", "quantized"], default="kitti",
-                    help="kitti: 47x155 cells, N=1024 (full-res KITTI); quantized: the reference's own "
-                         "24x80-cell quantized frame, N=100 (SURVEY 8(d) C0; tracking_main.c:13-14)")
-    args = ap.parse_args()
-    rows, cols, N = (47, 155, 1024) if args.grid == "kitti" else (24, 80, 100)
-    B = args.batch
+def run(batch=1024, steps=20, warmup=3, distinct=8, built=False, check=2, grid="kitti"):
+    """Time the windowed front-end; returns the JSON dict (without cpu_baseline) and the pairs."""
+    rows, cols, N = (47, 155, 1024) if grid == "kitti" else (24, 80, 100)
+    B = batch
     cells = rows * cols
     dev = torch.device("cuda", 0)
-    pairs = [synth.synth_window_pair(500 + k, rows=rows, cols=cols) for k in range(args.distinct)]
-    pick = [b % args.distinct for b in range(B)]
+    pairs = [synth.synth_window_pair(500 + k, rows=rows, cols=cols) for k in range(distinct)]
+    pick = [b % distinct for b in range(B)]
     semi0 = torch.from_numpy(np.stack([pairs[k][0]["semi"] for k in pick])).to(dev)
     semi1 = torch.from_numpy(np.stack([pairs[k][1]["semi"] for k in pick])).to(dev)
     desc0 = torch.from_numpy(np.stack([pairs[k][0]["desc"] for k in pick])).to(dev)
     desc1 = torch.from_numpy(np.stack([pairs[k][1]["desc"] for k in pick])).to(dev)
-    built = args.as_built
     s = [mvtrack.scale_as_built(pairs[k][0]["semi_scale"]) if built else float(pairs[k][0]["semi_scale"])
          for k in pick]
     sc = torch.tensor(s, dtype=torch.float32, device=dev)
@@ -108,12 +96,12 @@ def main():
         ctx.top_n_select_batch(mi1, pr1, N, cells, ns, pa, ix, sp, st)
         ctx.window_match_batch(prm, rows, cols, desc0, mi0, pr0, desc1, ns, pa, ix, nm, p1, p2)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     mvtrack.profile_enable(True)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
@@ -123,40 +111,61 @@ def main():
         ms, n = mvtrack.profile_query(k)
         stages[k] = round(ms / max(n, 1), 4)
     checked = 0
-    if args.check:
+    if check:
         import oracle
 
-        orc = oracle
-        for b in range(min(args.check, B)):
+        for b in range(min(check, B)):
             f0, f1 = pairs[pick[b]]
-            r = orc.track_window(f0, f1, as_built=built, N=N, cap=cells, max_matches=M)
+            r = oracle.track_window(f0, f1, as_built=built, N=N, cap=cells, max_matches=M)
             n = int(nm[b])
             assert n == len(r["query"]), (n, len(r["query"]))
             assert (p1[b, :n].cpu().numpy() == r["points1"]).all() and (p2[b, :n].cpu().numpy() == r["points2"]).all()
             checked += 1
-    alg_bytes = 2 * cells * (256 + 65) + N * 8  # SURVEY §8d per pair
-    step_s = el / args.steps
+    alg_bytes = 2 * cells * (256 + 65) + N * 8  # SURVEY 8d per pair
+    # window kernel: frame-0 descriptors + validity (every window cell at most once), the N
+    # query descriptors of frame 1, the per-query results
+    win_bytes = cells * (256 + 8) + N * (256 + 4 + 20)
+    step_s = el / steps
     win_s = stages["k_window_eval"] * 1e-3
     out = {
         "metric": "windowed int8 front-end pairs/sec (softmax x2 + top-N + window match), %d cells, N=%d"
                   % (cells, N),
-        "value": round(B / step_s, 1), "unit": "pairs/s", "batch": B, "steps": args.steps,
+        "value": round(B / step_s, 1), "unit": "pairs/s", "batch": B, "steps": steps,
         "ms_per_step": round(step_s * 1e3, 4), "semantics": "as-built" if built else "as-intended",
         "stages_ms": stages, "queries_selected_avg": float(ns.float().mean()), "matches_avg": float(nm.float().mean()),
         "hbm_roofline": {"algorithmic_bytes_per_pair": alg_bytes,
                          "frontend_GBs": round(alg_bytes * B / step_s / 1e9, 1),
                          "frontend_frac": round(alg_bytes * B / step_s / 1e9 / HBM_PEAK_GBS, 4),
-                         # frame-0 descriptors + validity (every window cell at most once), the
-                         # N query descriptors of frame 1, the per-query results
-                         "window_kernel_bytes_per_pair": cells * (256 + 8) + N * (256 + 4 + 20),
-                         "window_kernel_GBs": round((cells * (256 + 8) + N * (256 + 4 + 20)) * B / win_s / 1e9, 1),
+                         "window_kernel_bytes_per_pair": win_bytes,
+                         "window_kernel_GBs": round(win_bytes * B / win_s / 1e9, 1),
+                         "window_kernel_frac": round(win_bytes * B / win_s / 1e9 / HBM_PEAK_GBS, 4),
                          "peak_GBs": HBM_PEAK_GBS},
         "checked_pairs": checked,
     }
+    ctx.close()
+    return out, pairs
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--distinct", type=int, default=8, help="distinct synthetic pairs tiled over the batch")
+    ap.add_argument("--as-built", action="store_true")
+    ap.add_argument("--check", type=int, default=2)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--grid", choices=["kitti", "quantized"], default="kitti",
+                    help="kitti: 47x155 cells, N=1024 (full-res KITTI); quantized: the reference's own "
+                         "24x80-cell quantized frame, N=100 (SURVEY 8(d) C0; tracking_main.c:13-14)")
+    args = ap.parse_args()
+    out, pairs = run(args.batch, args.steps, args.warmup, args.distinct, args.as_built, args.check, args.grid)
+    built = args.as_built
+    rows, cols, N = (47, 155, 1024) if args.grid == "kitti" else (24, 80, 100)
+    cells = rows * cols
     if args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(pairs, built, N, cells, args.cpu_seconds)
     print(json.dumps(out), flush=True)
-    ctx.close()
 
 
 if __name__ == "__main__":
