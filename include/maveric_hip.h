@@ -115,7 +115,11 @@ float mv_scale_as_built(float scale); /* low 32 bits of (double)scale, SURVEY F7
  * when (double)s > thresh and s > 0.  match_idx = -1 otherwise.  Bit-exact: an
  * fp16 MFMA screen plus an exact re-score of every candidate within the
  * rounding bound (rows with |x| >= 2 or non-finite values take the exact path).
- * cap = row stride (keypoints per frame slot). */
+ * cap = row stride (keypoints per frame slot).
+ * match_score may be NULL: the reference keeps only the matched pairs
+ * (pairwise_pnp.py:649-657), so without a score output the exact re-score runs
+ * only where the rounding window does not already decide the row; match_idx is
+ * identical either way. */
 int mv_match_allpairs_f32_dev(mv_context *ctx, int batch, int cap, const int *n0, const int *n1,
                               const float *desc0, const float *desc1, double thresh, int *match_idx,
                               float *match_score);

@@ -71,6 +71,12 @@ constexpr int NBUF = 4;  // ring slots: two column tiles of KS = 2 slices
 #ifndef AP_EXP_NOFOLD
 #define AP_EXP_NOFOLD 0
 #endif
+#ifndef AP_SETPRIO
+#define AP_SETPRIO 0  // 1: raised wave priority while a slot's MFMAs and fold issue
+#endif
+#ifndef AP_DMA_SPREAD
+#define AP_DMA_SPREAD 0  // 1: the slot's DMA pieces issued between its k16 steps, not before them
+#endif
 #ifndef AP_EXP_NODMA
 #define AP_EXP_NODMA 0
 #endif
@@ -268,11 +274,11 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int row0 = tr * BM;
     int *oidx = match_idx + (size_t)pair * cap + row0;
-    float *oscore = match_score + (size_t)pair * cap + row0;
+    float *oscore = match_score ? match_score + (size_t)pair * cap + row0 : nullptr;  // null: indices only
     // rows in [n0, cap) report "no match"
     if (t < BM && row0 + t < cap && (row0 + t >= n0 || n1 <= 0)) {
         oidx[t] = -1;
-        oscore[t] = 0.f;
+        if (oscore) oscore[t] = 0.f;
     }
     if (row0 >= n0 || n1 <= 0) return;
     const bool flagged = bad[pair] != 0;
@@ -316,6 +322,8 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
             glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES + 12 * SL_ROW>(SB, oB[RPW / 4 - 1], dst_w); \
         }                                                                                    \
     } while (0)
+#define AP_STAGE_PIECE(SLOT, KSI, G)                                                         \
+    glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES + (G) * 4 * SL_ROW>(SB, oB[G], dst_w)
 #define AP_TILE_OFFSETS(TC)                                                                  \
     do {                                                                                     \
         const int nb_ = (TC) * BN + dr;                                                      \
@@ -415,11 +423,13 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
     do {                                                                                      \
         constexpr int nx = (J) + NBUF - 1;                                                    \
         const int ntile = T + nx / KS; /* tile of the slice issued now */                     \
-        if (!AP_EXP_NODMA && ntile < ntc) {                                                   \
+        const bool dma_ = !AP_EXP_NODMA && ntile < ntc;                                       \
+        if (dma_) {                                                                           \
             if constexpr (nx % KS == 0) AP_TILE_OFFSETS(ntile);                               \
-            AP_STAGE(nx % NBUF, nx % KS);                                                     \
+            if constexpr (!AP_DMA_SPREAD) AP_STAGE(nx % NBUF, nx % KS);                       \
         }                                                                                     \
         const char *base = lds + OFF_STAGE + (J) * SL_BYTES + rdb;                            \
+        if constexpr (AP_SETPRIO) __builtin_amdgcn_s_setprio(1);                              \
         if (!AP_EXP_NOMFMA) {                                                                 \
             /* fragment reads run PF k16 steps ahead of the MFMAs (counted lgkm waits) */      \
             constexpr int PF = 4;                                                             \
@@ -429,6 +439,13 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
                     const int ch_ = ((2 * s_) ^ xsw) * 16;                                    \
                     b0_[s_] = *reinterpret_cast<const f16x8 *>(base + ch_);                   \
                     b1_[s_] = *reinterpret_cast<const f16x8 *>(base + 32 * SL_ROW + ch_);     \
+                }                                                                             \
+                /* spread: one DMA piece after every other k16 step's fragment reads */         \
+                if constexpr (AP_DMA_SPREAD) if (dma_) {                                      \
+                    if (s_ == 1) AP_STAGE_PIECE(nx % NBUF, nx % KS, 0);                       \
+                    if (s_ == 3) AP_STAGE_PIECE(nx % NBUF, nx % KS, 1);                       \
+                    if (RPW == 16 && s_ == 5) AP_STAGE_PIECE(nx % NBUF, nx % KS, RPW / 4 - 2); \
+                    if (RPW == 16 && s_ == 7) AP_STAGE_PIECE(nx % NBUF, nx % KS, RPW / 4 - 1); \
                 }                                                                             \
                 if (s_ >= PF) {                                                               \
                     const int m_ = s_ - PF;                                                   \
@@ -441,6 +458,7 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
         }                                                                                     \
         /* the previous tile's fold, half of its rows beside each k-slice's MFMAs */          \
         if (FOLD) AP_FOLD_ROWS(F0, F1, T + (J) / KS - 1, 8 * ((J) % KS), 8 * ((J) % KS) + 8);  \
+        if constexpr (AP_SETPRIO) __builtin_amdgcn_s_setprio(0);                              \
         if (AP_EXP_NOWAIT) {                                                                  \
         } else if (ntile < ntc) {                                                             \
             wait_vm<DMA_PER_SLICE * (NBUF - 2)>();                                            \
@@ -479,6 +497,7 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
         AP_FOLD(x0, x1, tl);
     }
 #undef AP_STAGE
+#undef AP_STAGE_PIECE
 #undef AP_SLOT
 #undef AP_FOLD
 #undef AP_FOLD_ROWS
@@ -565,7 +584,11 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
                     wide = true;
                     if (fh == 0) lmask[rl] = 0xffffffffu;
                 } else if (fh == 0) {
-                    bs = AP_EXP_NOEXACT ? M : exact_dot(arow, B + (size_t)I * KD);
+                    // decision-only (no score output): when every exact score within the window
+                    // clears both tests, the maximiser's exact dot decides nothing -- skip it
+                    const bool sure = !oscore && Ms - dp > fmax(thresh, 0.0);
+                    // (Ms = M 2^-28 is exact in float, and Ms > thresh, Ms > 0: the keep test passes)
+                    bs = sure ? (float)Ms : AP_EXP_NOEXACT ? M : exact_dot(arow, B + (size_t)I * KD);
                     bj = I;
                 }
             } else {  // both lanes of the row take this branch
@@ -618,7 +641,7 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
     if (fh == 0 && live && !wide) {
         const bool keep = bj != 0x7fffffff && (double)bs > thresh && bs > 0.f;
         oidx[rl] = keep ? bj : -1;
-        oscore[rl] = keep ? bs : 0.f;
+        if (oscore) oscore[rl] = keep ? bs : 0.f;
     }
 
     AP_STAMP(5);
@@ -660,7 +683,7 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
         if (lane == 0) {
             const bool keep = wj != 0x7fffffff && (double)ws > thresh && ws > 0.f;
             oidx[r] = keep ? wj : -1;
-            oscore[r] = keep ? ws : 0.f;
+            if (oscore) oscore[r] = keep ? ws : 0.f;
         }
     }
 #ifdef AP_EXP_TRACE
@@ -723,7 +746,7 @@ int launch_allpairs_f32_prepare(hipStream_t s, void *scratch, int batch, int cap
 int launch_allpairs_f32_match(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
                               const float *desc0, const float *desc1, double thresh, int *match_idx,
                               float *match_score) {
-    MV_REQUIRE(batch > 0 && cap > 0 && n0 && n1 && desc0 && desc1 && match_idx && match_score && scratch);
+    MV_REQUIRE(batch > 0 && cap > 0 && n0 && n1 && desc0 && desc1 && match_idx && scratch);  // match_score optional
     MV_REQUIRE(((uintptr_t)desc0 & 15) == 0 && ((uintptr_t)desc1 & 15) == 0);
     const int tiles_r = (cap + BM - 1) / BM;
     const long blocks = (long)batch * tiles_r;

@@ -14,8 +14,9 @@ def bits(a):
     return np.ascontiguousarray(a, np.float32).view(np.int32)
 
 
-def run_f32(ctx, torch, pairs, cap=None, thresh=0.8):
-    """pairs: list of (d0 [n0,256], d1 [n1,256]) float32"""
+def run_f32(ctx, torch, pairs, cap=None, thresh=0.8, scores=True):
+    """pairs: list of (d0 [n0,256], d1 [n1,256]) float32; scores=False: indices only (the
+    score output pointer is NULL -- the decision-only mode)"""
     B = len(pairs)
     cap = cap or max(max(a.shape[0], b.shape[0]) for a, b in pairs)
     D0 = np.zeros((B, cap, 256), np.float32)
@@ -32,12 +33,12 @@ def run_f32(ctx, torch, pairs, cap=None, thresh=0.8):
     dev = torch.device("cuda:0")
     t = lambda x: torch.from_numpy(x).to(dev)  # noqa: E731
     idx = torch.full((B, cap), -7, dtype=torch.int32, device=dev)
-    sc = torch.zeros((B, cap), dtype=torch.float32, device=dev)
+    sc = torch.zeros((B, cap), dtype=torch.float32, device=dev) if scores else None
     ctx.set_stream(torch.cuda.current_stream())
     ctx.match_allpairs_f32(t(D0), t(D1), t(n0), t(n1), idx, sc, thresh)
     torch.cuda.synchronize()
     ctx.set_stream(None)
-    return idx.cpu().numpy(), sc.cpu().numpy()
+    return idx.cpu().numpy(), (sc.cpu().numpy() if scores else None)
 
 
 @pytest.mark.parametrize("name", ["pair0", "pair10"])
@@ -132,6 +133,39 @@ def test_allpairs_f32_out_of_screen_range(ctx, orc, torch_cuda):
             i2, s2 = orc.allpairs_f32(a, b, thr)
             assert (idx[k, :a.shape[0]] == i2).all(), k
             assert (bits(sc[k, :a.shape[0]]) == bits(s2)).all(), k
+
+
+def test_allpairs_f32_indices_only(ctx, orc, torch_cuda):
+    """match_score = NULL (what pairwise_pnp.py:639-659 keeps: the matched pairs, not the
+    score): the exact re-score is skipped where the window already decides, and the indices
+    must still equal the oracle's on every hard case -- full size, ties and near-ties,
+    threshold edges, out-of-range and ragged inputs."""
+    rng = np.random.default_rng(21)
+    cases = []
+    cases.append(([(p["desc0"], p["desc1"]) for p in (synth.synth_pair_f32(s) for s in range(2))], 0.8))
+    a = rng.standard_normal((300, 256)).astype(np.float32)
+    a /= np.linalg.norm(a, axis=1, keepdims=True)
+    b = a[rng.permutation(300)] + 0.01 * rng.standard_normal((300, 256)).astype(np.float32)
+    b /= np.linalg.norm(b, axis=1, keepdims=True)
+    b = np.concatenate([b, b[:40], b[:40] * np.float32(1 + 2 ** -23), b[50:60] * np.float32(1 - 2 ** -24)])
+    b = b[rng.permutation(b.shape[0])]
+    for thr in (0.8, 0.999999, 1.0, -1.0, 0.0):
+        cases.append(([(a, b), (a[:64], a[:64].copy())], thr))
+    odd = []
+    for scale0, scale1 in ((5.0, 1.0), (1.0, 3e4), (1e-6, 1.0), (1e-20, 1e-20)):
+        odd.append(((a[:96] * np.float32(scale0)).astype(np.float32), (b[:80] * np.float32(scale1)).astype(np.float32)))
+    for k, (x, y) in enumerate([(1, 300), (129, 1), (127, 129), (511, 513)]):
+        p = synth.synth_pair_f32(70 + k, n=x, n1=y, noise=0.25)
+        odd.append((p["desc0"], p["desc1"]))
+    cases.append((odd, 0.8))
+    for pairs, thr in cases:
+        idx, _ = run_f32(ctx, torch_cuda, pairs, thresh=thr, scores=False)
+        idx_s, _ = run_f32(ctx, torch_cuda, pairs, thresh=thr, scores=True)
+        for k, (x, y) in enumerate(pairs):
+            i2, _ = orc.allpairs_f32(x, y, thr)
+            assert (idx[k, :x.shape[0]] == i2).all(), (thr, k)
+            assert (idx[k, :x.shape[0]] == idx_s[k, :x.shape[0]]).all(), (thr, k)
+            assert (idx[k, x.shape[0]:] == -1).all()
 
 
 def test_allpairs_f32_prepare_run_pipeline(ctx, orc, torch_cuda):
