@@ -71,6 +71,9 @@ constexpr int NBUF = 4;  // ring slots: two column tiles of KS = 2 slices
 #ifndef AP_EXP_NOFOLD
 #define AP_EXP_NOFOLD 0
 #endif
+#ifndef AP_STAGGER
+#define AP_STAGGER 0  // > 0: first-generation second-slot blocks start this many 100-MHz ticks late
+#endif
 #ifndef AP_SETPRIO
 #define AP_SETPRIO 0  // 1: raised wave priority while a slot's MFMAs and fold issue
 #endif
@@ -207,7 +210,13 @@ __device__ __forceinline__ float exact_dot(const float *__restrict__ a, const fl
 #endif
 constexpr int SPLIT_ROWS = 8 * SPLIT_RPG;  // rows per block iteration: 8 row groups x SPLIT_RPG
 typedef float f32x4v __attribute__((ext_vector_type(4)));
-__global__ __launch_bounds__(256) void k_ap_split(int batch, int cap, const int *__restrict__ n1v,
+#ifndef SPLIT_WPE
+#define SPLIT_WPE 1  // minimum waves per SIMD the split is compiled for (8: <= 64 VGPRs)
+#endif
+#ifndef SPLIT_GRID
+#define SPLIT_GRID (256 * 64)  // grid-stride blocks at most
+#endif
+__global__ __launch_bounds__(256, SPLIT_WPE) void k_ap_split(int batch, int cap, const int *__restrict__ n1v,
                                                   const float *__restrict__ desc1, char *__restrict__ h1,
                                                   float *__restrict__ nrm1, int *__restrict__ bad) {
     const long rows = (long)batch * cap;
@@ -267,6 +276,15 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
     AP_STAMP(0);
 #else
 #define AP_STAMP(K) do { } while (0)
+#endif
+#if AP_STAGGER > 0
+    // blocks 256..511 (the second slot of every CU in the first dispatch generation) start
+    // AP_STAGGER ticks (100 MHz) late, so that co-resident blocks' A-load bursts alternate
+    // with each other's MFMA sweeps instead of coinciding generation after generation
+    if (blockIdx.x >= 256 && blockIdx.x < 512) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)AP_STAGGER) __builtin_amdgcn_s_sleep(8);
+    }
 #endif
     const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int pair = L / tiles_r, tr = L % tiles_r;
@@ -732,7 +750,7 @@ int launch_allpairs_f32_prepare(hipStream_t s, void *scratch, int batch, int cap
     MV_REQUIRE(cap <= (1 << 22));  // per-lane DMA source offsets are 32-bit byte offsets into a pair
     const size_t rows = (size_t)batch * cap;
     const ApScratch m = ap_scratch_map(scratch, batch, cap);
-    const long split_blocks = std::min<long>((long)((rows + SPLIT_ROWS - 1) / SPLIT_ROWS), 256l * 64);
+    const long split_blocks = std::min<long>((long)((rows + SPLIT_ROWS - 1) / SPLIT_ROWS), (long)SPLIT_GRID);
     MV_HIP_TRY(hipMemsetAsync(m.bad, 0, (size_t)batch * 4, s));
     MV_PROF_BEGIN(s, "k_ap_split");
     hipLaunchKernelGGL(k_ap_split, dim3((unsigned)split_blocks), dim3(256), 0, s, batch, cap, n1, desc1, m.h1, m.nrm1,

@@ -23,8 +23,9 @@ sc = torch.empty((B, n), dtype=torch.float32, device=dev)
 ctx = mvtrack.Context(0)
 ctx.set_stream(torch.cuda.current_stream())
 ctx.reserve(B, n)
+scores = os.environ.get("SCORES", "0") == "1"  # default: the bench's indices-only mode
 for _ in range(3):
-    ctx.match_allpairs_f32(d0, d1, nn_, nn_, idx, sc, 0.8)
+    ctx.match_allpairs_f32(d0, d1, nn_, nn_, idx, sc if scores else None, 0.8)
 torch.cuda.synchronize()
 nblk = B * (n // int(os.environ.get("BM", 128)))
 NWV = int(os.environ.get("NW", 4))
@@ -50,3 +51,13 @@ o = sel[np.argsort(start[sel])]
 rt = tr[:, 0, 9]
 if rt[o[-1]] != rt[o[0]]:
     print("SCLK over the CU's run: %.3f GHz" % ((end[o[-1]] - end[o[0]]) / ((rt[o[-1]] - rt[o[0]]) / 100e6) / 1e9))
+
+# timeline of the first CU: per block (wave 0) start / A converted / sweep done / end, in
+# thousands of cycles from the CU's first start -- co-resident blocks in or out of phase?
+t0 = start[o[0]]
+print("CU %d timeline (kcycles): start  A-done  sweep-done  end" % cu)
+for b in o[:12]:
+    print("  blk %6d  %7.1f %7.1f %7.1f %7.1f" % (b, (st[b, 0, 0] - t0) / 1e3, (st[b, 0, 1] - t0) / 1e3,
+                                                (st[b, 0, 3] - t0) / 1e3, (end[b] - t0) / 1e3))
+# chip-wide: fraction of wave-time spent in A-load
+print("A-load share of wave time: %.3f" % (d[:, :, 0].sum() / tot.sum()))
