@@ -35,7 +35,8 @@ typedef enum {
     MV_ERR_NO_DEVICE = -4,   /* no usable gfx950 device: the library never falls back to the CPU */
     MV_ERR_NO_POINTS = -5,   /* pose requested on an empty correspondence set */
     MV_ERR_OUT_OF_MEMORY = -6,
-    MV_ERR_DEGENERATE = -7   /* pose: no hypothesis with enough support */
+    MV_ERR_DEGENERATE = -7,  /* pose: no hypothesis with enough support */
+    MV_ERR_IO = -8           /* a file could not be read or written (trajectory.h) */
 } mv_status;
 
 typedef enum {

@@ -93,6 +93,7 @@ const char *mv_status_string(int s) {
         case MV_ERR_NO_POINTS: return "no correspondences";
         case MV_ERR_OUT_OF_MEMORY: return "out of device memory";
         case MV_ERR_DEGENERATE: return "degenerate pose";
+        case MV_ERR_IO: return "file I/O error";
         default: return "unknown status";
     }
 }

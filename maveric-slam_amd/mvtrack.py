@@ -24,6 +24,7 @@ MV_ERR_NO_DEVICE = -4
 MV_ERR_NO_POINTS = -5
 MV_ERR_OUT_OF_MEMORY = -6
 MV_ERR_DEGENERATE = -7
+MV_ERR_IO = -8
 AS_BUILT = 0
 AS_INTENDED = 1
 
@@ -120,6 +121,13 @@ def lib():
             "ransac_essential_matrix": (None, [_I, _P, _P, _P, _I, _F, _P, _P, _P]),
             "recover_pose_from_essential_matrix": (None, [_P, _P, _P, _P]),
             "track": (_I, [_P, _P, _I, _I, _I, _F, _P]),
+            "mv_trajectory_chain_dev": (_I, [_P, _I, _I, _P, _P, _P, _I, _P]),
+            "mv_trajectory_rebase_dev": (_I, [_P, _I, _I, _P, _I, _P]),
+            "mv_trajectory_chain_host": (_I, [_P, _I, _P, _P, _P, _I, _P]),
+            "mv_write_pose_txt": (_I, [ctypes.c_char_p, _P]),
+            "mv_write_trajectory_ply": (_I, [ctypes.c_char_p, _I, _P]),
+            "mv_read_transform_npy": (_I, [ctypes.c_char_p, _P]),
+            "mv_compute_trajectory": (_I, [_P, _I, _I, ctypes.c_char_p, ctypes.c_char_p, _I, ctypes.POINTER(_I)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -131,6 +139,58 @@ def lib():
 
 def _np(a):
     return a.ctypes.data_as(ctypes.c_void_p)
+
+
+# ---------------- trajectory (include/trajectory.h; python/compute_trajectory.py) ----------------
+CHAIN_AS_BUILT, CHAIN_COMPOSE = 0, 1
+
+
+def write_pose_txt(path, pose):
+    """np.savetxt(pose[:3, :], fmt='%.6f') (compute_trajectory.py:49-51), in C."""
+    p = np.ascontiguousarray(pose, np.float64).reshape(-1)[:12].copy()
+    check(lib().mv_write_pose_txt(os.fsencode(path), _np(p)), "write_pose_txt")
+
+
+def write_trajectory_ply(path, xyz):
+    """write_ply (compute_trajectory.py:6-43), in C."""
+    x = np.ascontiguousarray(xyz, np.float64).reshape(-1, 3)
+    check(lib().mv_write_trajectory_ply(os.fsencode(path), x.shape[0], _np(x)), "write_trajectory_ply")
+
+
+def read_transform_npy(path):
+    """A (3, 4) float64 .npy read by the library's C reader -> (status, [3, 4])."""
+    T = np.zeros(12, np.float64)
+    st = lib().mv_read_transform_npy(os.fsencode(path), _np(T))
+    return st, T.reshape(3, 4)
+
+
+def chain_sharded(chain_local, rebase, gather, rank, rel_local, mode):
+    """A sequence sharded over ranks in order (rank r holds transforms [k_r, k_{r+1})):
+    each rank chains its shard from the identity (chain_local(rel) -> poses [len+1, 3, 4]),
+    the ranks exchange their shard's end pose (gather(last) -> [world] list, rank order:
+    the RCCL all-gather on GPUs), every rank folds the ends of the ranks before it into its
+    start pose (host, world x 3x4) and re-bases its poses on it (rebase(poses, start)).
+    Returns this rank's poses [len+1, 3, 4]; its pose 0 is the previous rank's last pose."""
+    import numpy as _n
+
+    poses = chain_local(rel_local)
+    ends = gather(_n.asarray(poses[-1], _n.float64))
+    start = _n.eye(4)[:3].copy()
+    for r in range(rank):  # start <- end_r applied after start (the chain rule, k_rebase order)
+        E = _n.asarray(ends[r], _n.float64)
+        nxt = _n.zeros((3, 4))
+        for i in range(3):
+            for c in range(4):
+                v = E[i, 0] * start[0, c]
+                v = v + E[i, 1] * start[1, c]
+                v = v + E[i, 2] * start[2, c]
+                if c == 3:
+                    v = v + E[i, 3] if mode == CHAIN_COMPOSE else E[i, 3] + start[i, 3]
+                nxt[i, c] = v
+        start = nxt
+    if rank == 0:
+        return poses
+    return rebase(poses, start)
 
 
 def _t(x):
@@ -337,6 +397,35 @@ class Context:
         B, cap = desc0.shape[0], desc0.shape[1]
         check(lib().mv_match_allpairs_f32_run_dev(self.h, B, cap, _t(n0), _t(n1), _t(desc0), _t(desc1), float(thresh),
                                                   _t(match_idx), _t(match_score)), "match_allpairs_f32_run")
+
+    def trajectory_chain(self, rel, poses, present=None, start=None, mode=CHAIN_AS_BUILT):
+        """Device tensors: rel [B, len, 3, 4] float64 -> poses [B, len + 1, 3, 4] (k_chain)."""
+        B, n = rel.shape[0], rel.shape[1]
+        check(lib().mv_trajectory_chain_dev(self.h, B, n, _t(rel), _t(present), _t(start), int(mode), _t(poses)),
+              "trajectory_chain")
+
+    def trajectory_rebase(self, base, poses, mode=CHAIN_AS_BUILT):
+        """Device tensors: poses [B, len1, 3, 4] re-based on base [B, 3, 4] in place (k_rebase)."""
+        check(lib().mv_trajectory_rebase_dev(self.h, poses.shape[0], poses.shape[1], _t(base), int(mode), _t(poses)),
+              "trajectory_rebase")
+
+    def trajectory_chain_host(self, rel, present=None, start=None, mode=CHAIN_AS_BUILT):
+        """numpy: one sequence rel [len, 3, 4] float64 -> poses [len + 1, 3, 4] (on the GPU)."""
+        r = np.ascontiguousarray(rel, np.float64).reshape(-1, 12)
+        out = np.zeros((r.shape[0] + 1, 12), np.float64)
+        pr = None if present is None else np.ascontiguousarray(present, np.int32)
+        st = None if start is None else np.ascontiguousarray(start, np.float64).reshape(12)
+        check(lib().mv_trajectory_chain_host(self.h, r.shape[0], _np(r), None if pr is None else _np(pr),
+                                             None if st is None else _np(st), int(mode), _np(out)),
+              "trajectory_chain_host")
+        return out.reshape(-1, 3, 4)
+
+    def compute_trajectory(self, start_frame, end_frame, pose_dir, out_dir, mode=CHAIN_AS_BUILT):
+        """compute_trajectory.py main() with the chain on the GPU; returns poses written."""
+        n = ctypes.c_int(0)
+        check(lib().mv_compute_trajectory(self.h, int(start_frame), int(end_frame), os.fsencode(pose_dir),
+                                          os.fsencode(out_dir), int(mode), ctypes.byref(n)), "compute_trajectory")
+        return n.value
 
     def match_allpairs_i8(self, desc0, desc1, n0, n1, match_idx, match_dot):
         B, cap = desc0.shape[0], desc0.shape[1]

@@ -595,3 +595,44 @@ ORC_EXPORT void orc_allpairs_i8(const int8_t *d0, int n0, const int8_t *d1, int 
     }
     free(nb);
 }
+
+/* ---- trajectory chaining: python/compute_trajectory.py:53-90 (the loop body :73-79) ----
+ * poses [len + 1][12] float64, row-major [R | t].  mode 0 (as built, :76-77):
+ *   R <- transform[:3, :3] @ current_pose[:3, :3];  t <- transform[:3, 3] + current_pose[:3, 3]
+ * mode 1 (the commented-out composition that produced outputs/785/trajectory.ply, here the
+ * left product T_rel @ current_pose of the 4x4 matrices):  t <- R_rel t + t_rel.
+ * numpy's order on these shapes: sum over k = 0, 1, 2 left to right, mul then add (pinned by
+ * the committed PLY points, which this reproduces bit for bit).  present[k] == 0: the file was
+ * missing (:86-87), the pose carries over. */
+ORC_EXPORT void orc_trajectory_chain(int len, const double *rel, const int *present, const double *start, int mode,
+                                     double *poses) {
+    double cur[12];
+    for (int e = 0; e < 12; e++) cur[e] = start ? start[e] : ((e >> 2) == (e & 3) ? 1.0 : 0.0);
+    memcpy(poses, cur, sizeof cur);
+    for (int k = 0; k < len; k++) {
+        const double *T = rel + 12 * (size_t)k;
+        double nx[12];
+        if (present && !present[k]) {
+            memcpy(poses + 12 * (size_t)(k + 1), cur, sizeof cur);
+            continue;
+        }
+        for (int i = 0; i < 3; i++) {
+            for (int j = 0; j < 3; j++) {
+                double s = T[4 * i] * cur[j];
+                s = s + T[4 * i + 1] * cur[4 + j];
+                s = s + T[4 * i + 2] * cur[8 + j];
+                nx[4 * i + j] = s;
+            }
+            if (mode == 1) {
+                double s = T[4 * i] * cur[3];
+                s = s + T[4 * i + 1] * cur[7];
+                s = s + T[4 * i + 2] * cur[11];
+                nx[4 * i + 3] = s + T[4 * i + 3];
+            } else {
+                nx[4 * i + 3] = T[4 * i + 3] + cur[4 * i + 3];
+            }
+        }
+        memcpy(cur, nx, sizeof cur);
+        memcpy(poses + 12 * (size_t)(k + 1), cur, sizeof cur);
+    }
+}

@@ -56,6 +56,7 @@ def lib():
         L.orc_allpairs_f32.argtypes = [_P, _I, _P, _I, _I, _D, _P, _P]
         L.orc_row_argmax.argtypes = [_P, _I, _I, _D, _P, _P]
         L.orc_allpairs_i8.argtypes = [_P, _I, _P, _I, _P, _P]
+        L.orc_trajectory_chain.argtypes = [_I, _P, _P, _P, _I, _P]
         _lib = L
     return _lib
 
@@ -218,3 +219,16 @@ def allpairs_i8(d0, d1):
     dot = np.zeros(d0.shape[0], np.int32)
     lib().orc_allpairs_i8(_ptr(d0), d0.shape[0], _ptr(d1), d1.shape[0], _ptr(idx), _ptr(dot))
     return idx, dot
+
+
+def trajectory_chain(rel, present=None, start=None, mode=0):
+    """compute_trajectory.py:73-79 chain (mode 0 as built, 1 = T_rel @ pose): rel [len, 3, 4]
+    float64 -> poses [len + 1, 3, 4]."""
+    rel = np.ascontiguousarray(rel, np.float64).reshape(-1, 12)
+    n = rel.shape[0]
+    out = np.zeros((n + 1, 12), np.float64)
+    pr = None if present is None else np.ascontiguousarray(present, np.int32)
+    st = None if start is None else np.ascontiguousarray(start, np.float64).reshape(12)
+    lib().orc_trajectory_chain(n, _ptr(rel), None if pr is None else _ptr(pr), None if st is None else _ptr(st),
+                               int(mode), _ptr(out))
+    return out.reshape(n + 1, 3, 4)

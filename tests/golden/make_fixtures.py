@@ -13,6 +13,7 @@ Sources (paths relative to /root/reference):
   include/data/tracking/pair0/image0.h        full-res (376x1241) frame 0, 1002 keypoints
   outputs/transform_00078{5..9}_*.npy         3x4 float64 [R|t] from cv2.findEssentialMat+recoverPose
   outputs/00.txt                              KITTI seq 00 GT poses (3x4 per line)
+  outputs/785/*.pose.txt, *.ply               compute_trajectory.py outputs (file bytes)
 
 Float literals are parsed with libc strtof (direct decimal->binary32 rounding,
 exactly what the C compiler does for a `const float` initialiser).
@@ -124,6 +125,17 @@ def poses():
                         kitti00_gt=gt[keep].reshape(-1, 3, 4))
 
 
+def trajectory():
+    """The reference's committed compute_trajectory.py outputs for frames 785..789 (output
+    files, stored as bytes): five .pose.txt, the current script's PLY and the older one."""
+    d = os.path.join(REF, "outputs", "785")
+    out = {}
+    for f in sorted(os.listdir(d)):
+        key = f.replace("-", "_").replace(".", "_")
+        out[key] = np.frombuffer(open(os.path.join(d, f), "rb").read(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(OUT, "trajectory_785.npz"), **out)
+
+
 def main():
     if not os.path.isdir(REF):
         print("reference not present; fixtures are already committed", file=sys.stderr)
@@ -135,6 +147,7 @@ def main():
     tracking_pair("include/data/tracking/pair0/image0.h", "tracking_fullres_image0.npz",
                   frames=("image0",))
     poses()
+    trajectory()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

@@ -78,3 +78,78 @@ def test_two_rank_harness_gloo():
     assert not set(seeds0) & set(seeds1)  # disjoint shards
     assert sums0 == sums1 and [s[1] for s in sums0] == [0.0, 1.0]
     assert all(s[0] > 100 for s in sums0)  # every rank matched its pairs
+
+
+def _traj_worker(rank, world, port, q):
+    import sys
+
+    import torch
+    import torch.distributed as dist
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "oracle"), os.path.join(root, "maveric-slam_amd")):
+        sys.path.insert(0, p)
+    import mvtrack
+    import oracle
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = np.load(os.path.join(root, "tests", "golden", "poses.npz"))["transforms_785_790"]
+    rel = np.concatenate([g, g[::-1], g])  # 15 transforms, sharded 8 / 7 in order
+    cut = [0, 8, 15]
+    mine = rel[cut[rank]:cut[rank + 1]]
+
+    def gather(x):  # the RCCL all-gather of the shard end poses (gloo here)
+        t = torch.from_numpy(np.ascontiguousarray(x, np.float64))
+        out = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(out, t)
+        return [o.numpy() for o in out]
+
+    def rebase(poses, start):  # k_rebase's rule (host stand-in for the device kernel)
+        out = poses.copy()
+        for k in range(poses.shape[0]):
+            P = poses[k]
+            for i in range(3):
+                for c in range(4):
+                    v = P[i, 0] * start[0, c] + P[i, 1] * start[1, c] + P[i, 2] * start[2, c]
+                    if c == 3:
+                        v = v + P[i, 3] if mode == mvtrack.CHAIN_COMPOSE else P[i, 3] + start[i, 3]
+                    out[k, i, c] = v
+        return out
+
+    res = {}
+    for mode in (mvtrack.CHAIN_AS_BUILT, mvtrack.CHAIN_COMPOSE):
+        res[mode] = mvtrack.chain_sharded(lambda r: oracle.trajectory_chain(r, mode=mode), rebase, gather, rank,
+                                          mine, mode)
+    q.put((rank, res))
+    dist.destroy_process_group()
+
+
+def test_two_rank_sharded_trajectory_gloo():
+    """a sequence sharded over 2 ranks: local chains + all-gather of shard ends + re-base equal
+    the unsharded chain (within float64 rounding: re-association)."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    import oracle
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_traj_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g = np.load(os.path.join(root, "tests", "golden", "poses.npz"))["transforms_785_790"]
+    rel = np.concatenate([g, g[::-1], g])
+    for mode in (0, 1):
+        full = oracle.trajectory_chain(rel, mode=mode)
+        got = np.concatenate([out[0][mode], out[1][mode][1:]])
+        assert got.shape == full.shape
+        assert np.abs(got - full).max() < 1e-12
+        assert np.abs(out[1][mode][0] - out[0][mode][-1]).max() < 1e-12  # rank 1 starts where rank 0 ends
