@@ -122,3 +122,24 @@ def synth_window_pair(seed, rows=24, cols=80, shift=(4, 4), jitter=1, noise=4.0)
     f0 = dict(rows=rows, cols=cols, semi=semi0, desc=desc0, semi_scale=scale)
     f1 = dict(rows=rows, cols=cols, semi=semi1, desc=desc1.astype(np.int8), semi_scale=scale)
     return f0, f1
+
+
+def synth_superpoint_outputs(seed, Hc, Wc, p_corner=0.3, dustbin=7.0):
+    """Synthetic SuperPoint network outputs (what SuperPointNet.forward returns,
+    pairwise_pnp.py:197-199): semi [65, Hc, Wc] and coarse_desc [256, Hc, Wc] float32.
+    Logits ~ N(0, 1) with a dominant dustbin (channel 64, ~dustbin + N(0, 0.5)); a fraction
+    p_corner of cells carries one spiked channel (a corner, +U(6, 11)), so that at
+    conf_thresh 0.015 a few thousand pixels of a KITTI-size frame pass (as with real images).
+    Descriptors: N(0, 1) per channel, smooth enough across cells to make bilinear sampling
+    meaningful (a 2x2 box blur of white noise)."""
+    rng = np.random.default_rng(seed)
+    semi = rng.standard_normal((65, Hc, Wc)).astype(np.float32)
+    semi[64] = (dustbin + 0.5 * rng.standard_normal((Hc, Wc))).astype(np.float32)
+    spike = rng.random((Hc, Wc)) < p_corner
+    ch = rng.integers(0, 64, (Hc, Wc))
+    amp = rng.uniform(6.0, 11.0, (Hc, Wc)).astype(np.float32)
+    hh, ww = np.nonzero(spike)
+    semi[ch[hh, ww], hh, ww] += amp[hh, ww]
+    w = rng.standard_normal((256, Hc + 1, Wc + 1)).astype(np.float32)
+    desc = ((w[:, :-1, :-1] + w[:, 1:, :-1] + w[:, :-1, 1:] + w[:, 1:, 1:]) * np.float32(0.5)).astype(np.float32)
+    return semi, desc

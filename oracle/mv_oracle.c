@@ -636,3 +636,123 @@ ORC_EXPORT void orc_trajectory_chain(int len, const double *rel, const int *pres
         memcpy(poses + 12 * (size_t)(k + 1), cur, sizeof cur);
     }
 }
+
+/* ---- keypoint extraction: SuperPointFrontend.run after the network (python/pairwise_pnp.py:
+ * 197-257) and nms_fast (:116-179).  SURVEY §8(f)2.
+ * Heatmap (:204-220): dense = exp(semi) (float32; here the correctly rounded exp, numpy's
+ * SIMD expf is within ~1 ulp of it), den = sum_c dense[c] sequentially (numpy's axis-0
+ * reduction) + float32(1e-5), heat[hc*8 + i][wc*8 + j] = dense[i*8 + j] / den. */
+ORC_EXPORT void orc_kp_heatmap(const float *semi, int Hc, int Wc, float *heat) {
+    const size_t plane = (size_t)Hc * Wc;
+    const int Wh = Wc * 8;
+    for (int hc = 0; hc < Hc; hc++)
+        for (int wc = 0; wc < Wc; wc++) {
+            float e[65], den = 0.f;
+            for (int c = 0; c < 65; c++) {
+                e[c] = (float)exp((double)semi[c * plane + (size_t)hc * Wc + wc]);
+                den = den + e[c];
+            }
+            den = den + 1e-5f;
+            for (int c = 0; c < 64; c++) heat[(size_t)(hc * 8 + c / 8) * Wh + wc * 8 + c % 8] = e[c] / den;
+        }
+}
+
+typedef struct {
+    float conf;
+    int idx;  /* np.where order (row-major) */
+} orc_cand;
+static int cand_desc(const void *a, const void *b) { /* conf descending, then np.where order */
+    const orc_cand *x = (const orc_cand *)a, *y = (const orc_cand *)b;
+    if (x->conf != y->conf) return x->conf > y->conf ? -1 : 1;
+    return x->idx - y->idx;
+}
+static int cand_desc_rev(const void *a, const void *b) { /* conf descending, ties reversed */
+    const orc_cand *x = (const orc_cand *)a, *y = (const orc_cand *)b;
+    if (x->conf != y->conf) return x->conf > y->conf ? -1 : 1;
+    return y->idx - x->idx;
+}
+
+/* threshold (:222, float32 compare), nms_fast (greedy in descending confidence, ties in
+ * np.where order, (2d+1)^2 window on an HxW grid), survivors sorted by descending confidence
+ * (:229-231: argsort(-conf) then argsort(conf) reversed, so ties come out in REVERSED
+ * np.where order -- what numpy's sorts do on these sizes; they do not promise it), border
+ * removal (:233-237).  pts [cap][3] = (x, y, conf).  Returns the count, or -1 when more than `cap`
+ * candidates pass the threshold (nothing written). */
+ORC_EXPORT int orc_kp_select(const float *heat, int Hh, int Wh, int H, int W, float conf_thresh, int nms_dist,
+                             int border, int cap, float *pts) {
+    int nc = 0;
+    for (int i = 0; i < Hh * Wh; i++)
+        if (heat[i] >= conf_thresh) nc++;
+    if (nc > cap) return -1;
+    if (nc == 0) return 0;
+    orc_cand *c = (orc_cand *)malloc(sizeof(orc_cand) * (size_t)nc);
+    nc = 0;
+    for (int i = 0; i < Hh * Wh; i++)
+        if (heat[i] >= conf_thresh) {
+            c[nc].conf = heat[i];
+            c[nc].idx = i;
+            nc++;
+        }
+    qsort(c, (size_t)nc, sizeof(orc_cand), cand_desc);
+    const int pad = nms_dist, GW = W + 2 * pad, GH = H + 2 * pad;
+    signed char *grid = (signed char *)calloc((size_t)GW * GH, 1);
+    for (int k = 0; k < nc; k++) grid[(size_t)(c[k].idx / Wh + pad) * GW + c[k].idx % Wh + pad] = 1;
+    int nk = 0;
+    for (int k = 0; k < nc; k++) {
+        const int y = c[k].idx / Wh + pad, x = c[k].idx % Wh + pad;
+        if (grid[(size_t)y * GW + x] != 1) continue;
+        for (int yy = y - pad; yy <= y + pad; yy++)
+            for (int xx = x - pad; xx <= x + pad; xx++) grid[(size_t)yy * GW + xx] = 0;
+        grid[(size_t)y * GW + x] = -1;
+        c[nk++] = c[k]; /* kept, in descending order (ties: np.where order) */
+    }
+    qsort(c, (size_t)nk, sizeof(orc_cand), cand_desc_rev);
+    int n = 0;
+    for (int k = 0; k < nk; k++) {
+        const int y = c[k].idx / Wh, x = c[k].idx % Wh;
+        if (x < border || x >= W - border || y < border || y >= H - border) continue;
+        pts[3 * n] = (float)x;
+        pts[3 * n + 1] = (float)y;
+        pts[3 * n + 2] = c[k].conf;
+        n++;
+    }
+    free(grid);
+    free(c);
+    return n;
+}
+
+/* descriptor sampling (:240-254): torch grid_sample (bilinear, zeros padding,
+ * align_corners=False) as its CPU kernel evaluates it -- ix = fma(gx + 1, Wc/2, -0.5),
+ * weights from the floor distances, corners accumulated by an fma chain -- then L2
+ * normalisation over the 256 channels (numpy: sequential sum of squares, sqrt, divide).
+ * desc [256][Hc][Wc]; pts [n][3]; out [n][256]. */
+ORC_EXPORT void orc_kp_sample(const float *desc, int Hc, int Wc, int H, int W, int n, const float *pts, float *out) {
+    const size_t plane = (size_t)Hc * Wc;
+    for (int p = 0; p < n; p++) {
+        const float gx = (float)((double)pts[3 * p] / ((double)W / 2.) - 1.);
+        const float gy = (float)((double)pts[3 * p + 1] / ((double)H / 2.) - 1.);
+        const float ix = fmaf(gx + 1.f, (float)Wc / 2.f, -0.5f), iy = fmaf(gy + 1.f, (float)Hc / 2.f, -0.5f);
+        const float x0f = floorf(ix), y0f = floorf(iy);
+        const float w = ix - x0f, e = 1.f - w, nn = iy - y0f, s = 1.f - nn;
+        const float wnw = s * e, wne = s * w, wsw = nn * e, wse = nn * w;
+        const int x0 = (int)x0f, y0 = (int)y0f;
+        float *o = out + (size_t)p * 256;
+        for (int ch = 0; ch < 256; ch++) {
+            const float *D = desc + ch * plane;
+#define ORC_AT(yy, xx) (((xx) >= 0 && (xx) < Wc && (yy) >= 0 && (yy) < Hc) ? D[(size_t)(yy) * Wc + (xx)] : 0.f)
+            float v = ORC_AT(y0, x0) * wnw;
+            v = fmaf(ORC_AT(y0, x0 + 1), wne, v);
+            v = fmaf(ORC_AT(y0 + 1, x0), wsw, v);
+            v = fmaf(ORC_AT(y0 + 1, x0 + 1), wse, v);
+#undef ORC_AT
+            o[ch] = v;
+        }
+        float ss = 0.f;
+        for (int ch = 0; ch < 256; ch++) {
+            const float q = o[ch] * o[ch];
+            ss = ss + q;
+        }
+        const float nrm = sqrtf(ss);
+        for (int ch = 0; ch < 256; ch++) o[ch] = o[ch] / nrm;
+    }
+}

@@ -57,6 +57,10 @@ def lib():
         L.orc_row_argmax.argtypes = [_P, _I, _I, _D, _P, _P]
         L.orc_allpairs_i8.argtypes = [_P, _I, _P, _I, _P, _P]
         L.orc_trajectory_chain.argtypes = [_I, _P, _P, _P, _I, _P]
+        L.orc_kp_heatmap.argtypes = [_P, _I, _I, _P]
+        L.orc_kp_select.restype = _I
+        L.orc_kp_select.argtypes = [_P, _I, _I, _I, _I, _F, _I, _I, _I, _P]
+        L.orc_kp_sample.argtypes = [_P, _I, _I, _I, _I, _I, _P, _P]
         _lib = L
     return _lib
 
@@ -232,3 +236,38 @@ def trajectory_chain(rel, present=None, start=None, mode=0):
     lib().orc_trajectory_chain(n, _ptr(rel), None if pr is None else _ptr(pr), None if st is None else _ptr(st),
                                int(mode), _ptr(out))
     return out.reshape(n + 1, 3, 4)
+
+
+def kp_heatmap(semi):
+    """SuperPointFrontend.run softmax -> heatmap (pairwise_pnp.py:204-220): semi [65, Hc, Wc]."""
+    semi = np.ascontiguousarray(semi, np.float32)
+    Hc, Wc = semi.shape[1], semi.shape[2]
+    heat = np.zeros((Hc * 8, Wc * 8), np.float32)
+    lib().orc_kp_heatmap(_ptr(semi), Hc, Wc, _ptr(heat))
+    return heat
+
+
+def kp_select(heat, H, W, conf=0.015, nms_dist=4, border=4, cap=1 << 20):
+    """threshold + nms_fast + sort + border removal -> pts [n, 3] (x, y, conf) float32."""
+    heat = np.ascontiguousarray(heat, np.float32)
+    pts = np.zeros((min(cap, heat.size), 3), np.float32)
+    n = lib().orc_kp_select(_ptr(heat), heat.shape[0], heat.shape[1], H, W, conf, nms_dist, border,
+                            pts.shape[0], _ptr(pts))
+    assert n >= 0, "more than cap candidates"
+    return pts[:n].copy()
+
+
+def kp_sample(desc, H, W, pts):
+    """grid_sample + L2 normalise (pairwise_pnp.py:240-254): desc [256, Hc, Wc] -> [n, 256]."""
+    desc = np.ascontiguousarray(desc, np.float32)
+    pts = np.ascontiguousarray(pts, np.float32).reshape(-1, 3)
+    out = np.zeros((pts.shape[0], 256), np.float32)
+    if pts.shape[0]:
+        lib().orc_kp_sample(_ptr(desc), desc.shape[1], desc.shape[2], H, W, pts.shape[0], _ptr(pts), _ptr(out))
+    return out
+
+
+def keypoints(semi, desc, H, W, conf=0.015, nms_dist=4, border=4):
+    heat = kp_heatmap(semi)
+    pts = kp_select(heat, H, W, conf, nms_dist, border)
+    return pts, kp_sample(desc, H, W, pts), heat
