@@ -1,0 +1,397 @@
+// k_keypoints.hip -- keypoint extraction + descriptor sampling:
+// SuperPointFrontend.run after the network forward (python/pairwise_pnp.py:197-257) and
+// nms_fast (:116-179), batched over frames.  See include/keypoints.h.
+//
+//   k_kp_heat    thread per cell: 65 correctly rounded expf, the reference's sequential
+//                float32 sum + 1e-5, 64 quotients -> the cell's 8x8 heatmap block
+//   k_kp_nms     one 1024-thread block per frame:
+//                (a) candidates (heat >= thresh) compacted in row-major order (tiles of 1024
+//                    pixels, ballot + LDS offsets), pixel -> candidate grid;
+//                (b) the greedy NMS as a fixed point: a candidate is KEPT when every
+//                    higher-priority candidate in its (2d+1)^2 window is suppressed, and
+//                    SUPPRESSED as soon as one of them is kept (priority: confidence, then
+//                    row-major order -- the reference's visiting order).  Each round decides
+//                    at least the highest-priority undecided candidate, and the result is the
+//                    sequential greedy one (a candidate's fate depends only on higher ones);
+//                (c) border filter, then each survivor's output slot = the number of
+//                    survivors ranked before it (confidence descending, ties in reversed
+//                    row-major order), counted through LDS tiles -- no sort;
+//   k_kp_nhwc    coarse descriptors [256][Hc*Wc] -> [Hc*Wc][256] (LDS tiles), so that each
+//                bilinear corner is one contiguous 1 KiB row
+//   k_kp_sample  one wave per keypoint: torch grid_sample's CPU arithmetic (fma unnormalise,
+//                floor-distance weights, fma chain over the 4 corners), then the L2 norm with
+//                the reference's sequential sum of squares (numpy axis-0 reduce) in one lane.
+// Bound: k_kp_heat is FP64-exp / HBM bound (65 x 4 B in, 64 x 4 B out per cell); k_kp_nms is
+// latency-bound (one block per frame); k_kp_sample reads 4 KiB per keypoint from L2.
+#include <math.h>
+
+#include "keypoints.h"
+#include "mv_internal.hpp"
+
+namespace {
+
+constexpr int NMS_T = 1024;  // threads of the per-frame block
+
+struct KpScratch {
+    float *heat;        // [B][P] (when the caller does not keep it)
+    int *grid;          // [B][P] candidate id or -1
+    int *cpix;          // [B][P] candidate pixel (row-major heat index)
+    float *cconf;       // [B][P]
+    unsigned char *st;  // [B][P] 0 undecided, 1 kept, 2 suppressed
+    int *kept;          // [B][P] surviving candidate ids (unordered)
+    int *slot_pix;      // [B][cap] pixel of output slot
+    float *nhwc;        // [B][Hc*Wc][256]
+};
+
+size_t a256(size_t x) { return mv::align_up(x, 256); }
+
+size_t kp_scratch_bytes(int B, int Hc, int Wc, int cap) {
+    const size_t P = (size_t)Hc * Wc * 64;
+    return a256((size_t)B * P * 4) * 5 + a256((size_t)B * P) + a256((size_t)B * cap * 4) +
+           a256((size_t)B * Hc * Wc * 256 * 4);
+}
+
+KpScratch kp_scratch_map(char *base, int B, int Hc, int Wc, int cap) {
+    const size_t P = (size_t)Hc * Wc * 64;
+    KpScratch m;
+    size_t o = 0;
+    m.heat = (float *)(base + o);
+    o += a256((size_t)B * P * 4);
+    m.grid = (int *)(base + o);
+    o += a256((size_t)B * P * 4);
+    m.cpix = (int *)(base + o);
+    o += a256((size_t)B * P * 4);
+    m.cconf = (float *)(base + o);
+    o += a256((size_t)B * P * 4);
+    m.kept = (int *)(base + o);
+    o += a256((size_t)B * P * 4);
+    m.st = (unsigned char *)(base + o);
+    o += a256((size_t)B * P);
+    m.slot_pix = (int *)(base + o);
+    o += a256((size_t)B * cap * 4);
+    m.nhwc = (float *)(base + o);
+    return m;
+}
+
+__global__ __launch_bounds__(256) void k_kp_heat(long cells, int Hc, int Wc, const float *__restrict__ semi,
+                                                 float *__restrict__ heat) {
+    const long q = (long)blockIdx.x * 256 + threadIdx.x;
+    if (q >= cells) return;
+    const long plane = (long)Hc * Wc;
+    const long b = q / plane, cell = q % plane;
+    const int hc = (int)(cell / Wc), wc = (int)(cell % Wc);
+    const float *S = semi + b * 65 * plane + cell;
+    float e[65];
+    float den = 0.f;
+#pragma unroll
+    for (int c = 0; c < 65; c++) {
+        e[c] = (float)exp((double)S[c * plane]);  // correctly rounded float32 exp (double, rounded once)
+        den = __fadd_rn(den, e[c]);              // np.sum(dense, axis=0): channel by channel
+    }
+    den = __fadd_rn(den, 1e-5f);
+    const int Wh = Wc * 8;
+    float *H = heat + b * plane * 64 + (long)(hc * 8) * Wh + wc * 8;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        float4 lo, hi;
+        lo.x = __fdiv_rn(e[8 * i + 0], den);
+        lo.y = __fdiv_rn(e[8 * i + 1], den);
+        lo.z = __fdiv_rn(e[8 * i + 2], den);
+        lo.w = __fdiv_rn(e[8 * i + 3], den);
+        hi.x = __fdiv_rn(e[8 * i + 4], den);
+        hi.y = __fdiv_rn(e[8 * i + 5], den);
+        hi.z = __fdiv_rn(e[8 * i + 6], den);
+        hi.w = __fdiv_rn(e[8 * i + 7], den);
+        *reinterpret_cast<float4 *>(H + (long)i * Wh) = lo;
+        *reinterpret_cast<float4 *>(H + (long)i * Wh + 4) = hi;
+    }
+}
+
+// priority of candidate j over k: higher confidence, then earlier in row-major order
+__device__ __forceinline__ bool before(float cj, int j, float ck, int k) { return cj > ck || (cj == ck && j < k); }
+
+__global__ __launch_bounds__(NMS_T) void k_kp_nms(int Hh, int Wh, int H, int W, float thresh, int nms_dist,
+                                                  int border, int cap, const float *__restrict__ heat_all,
+                                                  int *__restrict__ grid_all, int *__restrict__ cpix_all,
+                                                  float *__restrict__ cconf_all, unsigned char *__restrict__ st_all,
+                                                  int *__restrict__ kept_all, int *__restrict__ slot_pix_all,
+                                                  int *__restrict__ num_kp, float *__restrict__ kp_out,
+                                                  float *__restrict__ conf_out, int *__restrict__ status) {
+    __shared__ int wsum[NMS_T / 64];
+    __shared__ int s_base, s_flag, s_nk;
+    __shared__ float t_conf[NMS_T];
+    __shared__ int t_pix[NMS_T];
+    const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const long P = (long)Hh * Wh;
+    const float *heat = heat_all + b * P;
+    int *grid = grid_all + b * P;
+    int *cpix = cpix_all + b * P;
+    float *cconf = cconf_all + b * P;
+    unsigned char *st = st_all + b * P;
+    int *kept = kept_all + b * P;
+    int *slot_pix = slot_pix_all + (long)b * cap;
+
+    // (a) row-major compaction of the candidates
+    if (t == 0) s_base = 0;
+    __syncthreads();
+    for (long p0 = 0; p0 < P; p0 += NMS_T) {
+        const long p = p0 + t;
+        const float h = p < P ? heat[p] : 0.f;
+        const bool c = p < P && h >= thresh;
+        const unsigned long long m = __ballot(c);
+        if (lane == 0) wsum[w] = __popcll(m);
+        __syncthreads();
+        int off = s_base;
+        for (int k = 0; k < w; k++) off += wsum[k];
+        if (p < P) {
+            if (c) {
+                const int id = off + __popcll(m & ((1ull << lane) - 1ull));
+                grid[p] = id;
+                cpix[id] = (int)p;
+                cconf[id] = h;
+                st[id] = 0;
+            } else {
+                grid[p] = -1;
+            }
+        }
+        __syncthreads();
+        if (t == 0)
+            for (int k = 0; k < NMS_T / 64; k++) s_base += wsum[k];
+        __syncthreads();
+    }
+    const int nc = s_base;
+
+    // (b) greedy NMS as a fixed point over rounds
+    const int d = nms_dist;
+    for (;;) {
+        if (t == 0) s_flag = 0;
+        __syncthreads();
+        int undecided = 0;
+        for (int k = t; k < nc; k += NMS_T) {
+            if (st[k] != 0) continue;
+            const int pk = cpix[k], yk = pk / Wh, xk = pk % Wh;
+            const float ck = cconf[k];
+            bool supp = false, blocked = false;
+            for (int yy = max(yk - d, 0); yy <= min(yk + d, Hh - 1) && !supp; yy++)
+                for (int xx = max(xk - d, 0); xx <= min(xk + d, Wh - 1); xx++) {
+                    const int j = grid[(long)yy * Wh + xx];
+                    if (j < 0 || j == k || !before(cconf[j], j, ck, k)) continue;
+                    const unsigned char sj = __atomic_load_n(&st[j], __ATOMIC_RELAXED);
+                    if (sj == 1) {
+                        supp = true;
+                        break;
+                    }
+                    if (sj == 0) blocked = true;
+                }
+            if (supp)
+                st[k] = 2;
+            else if (!blocked)
+                st[k] = 1;
+            else
+                undecided = 1;
+        }
+        if (undecided) s_flag = 1;
+        __syncthreads();
+        if (!s_flag) break;
+    }
+
+    // (c) survivors inside the border; slot = rank (confidence desc, ties reversed row-major)
+    if (t == 0) s_nk = 0;
+    __syncthreads();
+    for (int k = t; k < nc; k += NMS_T) {
+        if (st[k] != 1) continue;
+        const int p = cpix[k], y = p / Wh, x = p % Wh;
+        if (x < border || x >= W - border || y < border || y >= H - border) continue;
+        kept[atomicAdd(&s_nk, 1)] = k;
+    }
+    __syncthreads();
+    const int nk = s_nk;
+    for (int k0 = 0; k0 < nk; k0 += NMS_T) {
+        const int k = k0 + t;
+        const int my = k < nk ? kept[k] : 0;
+        const float cm = k < nk ? cconf[my] : 0.f;
+        const int pm = k < nk ? cpix[my] : 0;
+        int rank = 0;
+        for (int j0 = 0; j0 < nk; j0 += NMS_T) {
+            __syncthreads();
+            if (j0 + t < nk) {
+                const int j = kept[j0 + t];
+                t_conf[t] = cconf[j];
+                t_pix[t] = cpix[j];
+            }
+            __syncthreads();
+            const int lim = min(NMS_T, nk - j0);
+            for (int q = 0; q < lim; q++) {
+                const float cq = t_conf[q];
+                rank += (cq > cm || (cq == cm && t_pix[q] > pm)) ? 1 : 0;
+            }
+        }
+        if (k < nk && rank < cap) {
+            const long o = (long)b * cap + rank;
+            kp_out[2 * o] = (float)(pm % Wh);
+            kp_out[2 * o + 1] = (float)(pm / Wh);
+            conf_out[o] = cm;
+            slot_pix[rank] = pm;
+        }
+    }
+    if (t == 0) {
+        num_kp[b] = min(nk, cap);
+        status[b] = nk > cap ? MV_ERR_CAPACITY : MV_OK;
+    }
+}
+
+// [B][256][HW] -> [B][HW][256], 64 x 64 tiles
+__global__ __launch_bounds__(256) void k_kp_nhwc(int HW, const float *__restrict__ in, float *__restrict__ out) {
+    __shared__ float tile[64][65];
+    const int b = blockIdx.z, c0 = blockIdx.y * 64, p0 = blockIdx.x * 64;
+    const float *I = in + (long)b * 256 * HW;
+    float *O = out + (long)b * HW * 256;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int r = ty; r < 64; r += 4) {
+        const int p = p0 + tx;
+        tile[r][tx] = p < HW ? I[(long)(c0 + r) * HW + p] : 0.f;
+    }
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4) {
+        const int p = p0 + r;
+        if (p < HW) O[(long)p * 256 + c0 + tx] = tile[tx][r];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_kp_sample(int B, int cap, int Hc, int Wc, int H, int W, int Wh,
+                                                   const int *__restrict__ num_kp, const int *__restrict__ slot_pix,
+                                                   const float *__restrict__ nhwc, float *__restrict__ desc) {
+    __shared__ float sq[4][256];
+    __shared__ float nrm[4];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const long q = (long)blockIdx.x * 4 + wv;
+    if (q >= (long)B * cap) return;
+    const int b = (int)(q / cap), slot = (int)(q % cap);
+    if (slot >= num_kp[b]) return;  // wave-uniform
+    const int pix = slot_pix[q];
+    const double x = (double)(pix % Wh), y = (double)(pix / Wh);
+    const float gx = (float)(x / ((double)W / 2.) - 1.), gy = (float)(y / ((double)H / 2.) - 1.);
+    const float ix = fmaf(gx + 1.f, (float)Wc / 2.f, -0.5f), iy = fmaf(gy + 1.f, (float)Hc / 2.f, -0.5f);
+    const float x0f = floorf(ix), y0f = floorf(iy);
+    const float wx = ix - x0f, e = 1.f - wx, n = iy - y0f, s = 1.f - n;
+    const float wnw = s * e, wne = s * wx, wsw = n * e, wse = n * wx;
+    const int x0 = (int)x0f, y0 = (int)y0f;
+    const float *D = nhwc + (long)b * Hc * Wc * 256 + 4 * lane;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto at = [&](int yy, int xx) {
+        return (xx >= 0 && xx < Wc && yy >= 0 && yy < Hc) ? *reinterpret_cast<const float4 *>(D + ((long)yy * Wc + xx) * 256)
+                                                          : z;
+    };
+    const float4 a = at(y0, x0), bq = at(y0, x0 + 1), c = at(y0 + 1, x0), dd = at(y0 + 1, x0 + 1);
+    float v[4];
+    const float *A = &a.x, *Bv = &bq.x, *C = &c.x, *Dv = &dd.x;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        float r = __fmul_rn(A[i], wnw);
+        r = fmaf(Bv[i], wne, r);
+        r = fmaf(C[i], wsw, r);
+        r = fmaf(Dv[i], wse, r);
+        v[i] = r;
+        sq[wv][4 * lane + i] = __fmul_rn(r, r);
+    }
+    // wave-local LDS hand-off (waves of the block retire independently: no block barrier)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane == 0) {
+        float ss = 0.f;
+        for (int ch = 0; ch < 256; ch++) ss = __fadd_rn(ss, sq[wv][ch]);  // numpy's sequential axis-0 sum
+        nrm[wv] = __fsqrt_rn(ss);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const float m = nrm[wv];
+    float4 o;
+    o.x = __fdiv_rn(v[0], m);
+    o.y = __fdiv_rn(v[1], m);
+    o.z = __fdiv_rn(v[2], m);
+    o.w = __fdiv_rn(v[3], m);
+    *reinterpret_cast<float4 *>(desc + q * 256 + 4 * lane) = o;
+}
+
+}  // namespace
+
+extern "C" void mv_kp_params_default(mv_kp_params *p) {
+    if (!p) return;
+    p->conf_thresh = 0.015f;
+    p->nms_dist = 4;
+    p->border = 4;
+}
+
+extern "C" int mv_keypoints_dev(mv_context *ctx, const mv_kp_params *p, int batch, int Hc, int Wc, int H, int W,
+                                const float *semi, const float *coarse_desc, int cap, int *num_kp, float *kp,
+                                float *conf, float *desc, float *heat, int *status) {
+    MV_REQUIRE(ctx && p && batch > 0 && Hc > 0 && Wc > 0 && cap > 0 && semi && coarse_desc && num_kp && kp && conf &&
+               desc && status);
+    MV_REQUIRE(Hc * 8 <= H && Wc * 8 <= W && p->nms_dist >= 0 && p->border >= 0);
+    MV_REQUIRE((long)Hc * Wc * 64 < (1l << 30) && (long)batch * cap < (1l << 31));
+    MV_REQUIRE(((uintptr_t)coarse_desc & 3) == 0 && ((uintptr_t)desc & 15) == 0);
+    MV_HIP_TRY(hipSetDevice(ctx->device));
+    char *scr = (char *)mv::scratch(ctx, kp_scratch_bytes(batch, Hc, Wc, cap));
+    if (!scr) return MV_ERR_OUT_OF_MEMORY;
+    const KpScratch m = kp_scratch_map(scr, batch, Hc, Wc, cap);
+    float *hm = heat ? heat : m.heat;
+    hipStream_t s = ctx->stream;
+    const long cells = (long)batch * Hc * Wc;
+    MV_PROF_BEGIN(s, "k_kp_heat");
+    hipLaunchKernelGGL(k_kp_heat, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s, cells, Hc, Wc, semi, hm);
+    MV_PROF_END(s);
+    MV_LAUNCH_CHECK();
+    MV_PROF_BEGIN(s, "k_kp_nms");
+    hipLaunchKernelGGL(k_kp_nms, dim3((unsigned)batch), dim3(NMS_T), 0, s, Hc * 8, Wc * 8, H, W, p->conf_thresh,
+                       p->nms_dist, p->border, cap, hm, m.grid, m.cpix, m.cconf, m.st, m.kept, m.slot_pix, num_kp, kp,
+                       conf, status);
+    MV_PROF_END(s);
+    MV_LAUNCH_CHECK();
+    const int HW = Hc * Wc;
+    MV_PROF_BEGIN(s, "k_kp_nhwc");
+    hipLaunchKernelGGL(k_kp_nhwc, dim3((unsigned)((HW + 63) / 64), 4, (unsigned)batch), dim3(256), 0, s, HW,
+                       coarse_desc, m.nhwc);
+    MV_PROF_END(s);
+    MV_LAUNCH_CHECK();
+    const long waves = (long)batch * cap;
+    MV_PROF_BEGIN(s, "k_kp_sample");
+    hipLaunchKernelGGL(k_kp_sample, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, batch, cap, Hc, Wc, H, W,
+                       Wc * 8, num_kp, m.slot_pix, m.nhwc, desc);
+    MV_PROF_END(s);
+    MV_LAUNCH_CHECK();
+    return mv::set_status(MV_OK);
+}
+
+extern "C" int mv_keypoints_host(mv_context *ctx, const mv_kp_params *p, int Hc, int Wc, int H, int W,
+                                 const float *semi, const float *coarse_desc, int cap, int *num_kp, float *kp,
+                                 float *conf, float *desc) {
+    MV_REQUIRE(ctx && p && Hc > 0 && Wc > 0 && cap > 0 && semi && coarse_desc && num_kp && kp && conf && desc);
+    MV_HIP_TRY(hipSetDevice(ctx->device));
+    const size_t plane = (size_t)Hc * Wc;
+    const size_t bs = a256(65 * plane * 4), bd = a256(256 * plane * 4), bk = a256((size_t)cap * 8),
+                 bc = a256((size_t)cap * 4), bo = a256((size_t)cap * 1024);
+    char *d = (char *)mv::stage(ctx, bs + bd + bk + bc + bo + 512);
+    if (!d) return MV_ERR_OUT_OF_MEMORY;
+    float *d_semi = (float *)d, *d_desc = (float *)(d + bs), *d_kp = (float *)(d + bs + bd),
+          *d_conf = (float *)(d + bs + bd + bk), *d_out = (float *)(d + bs + bd + bk + bc);
+    int *d_n = (int *)(d + bs + bd + bk + bc + bo), *d_st = d_n + 64;
+    hipStream_t s = ctx->stream;
+    MV_HIP_TRY(hipMemcpyAsync(d_semi, semi, 65 * plane * 4, hipMemcpyHostToDevice, s));
+    MV_HIP_TRY(hipMemcpyAsync(d_desc, coarse_desc, 256 * plane * 4, hipMemcpyHostToDevice, s));
+    int st = mv_keypoints_dev(ctx, p, 1, Hc, Wc, H, W, d_semi, d_desc, cap, d_n, d_kp, d_conf, d_out, nullptr, d_st);
+    if (st != MV_OK) return st;
+    int n = 0, fst = 0;
+    MV_HIP_TRY(hipMemcpyAsync(&n, d_n, 4, hipMemcpyDeviceToHost, s));
+    MV_HIP_TRY(hipMemcpyAsync(&fst, d_st, 4, hipMemcpyDeviceToHost, s));
+    MV_HIP_TRY(hipStreamSynchronize(s));
+    if (n > 0) {
+        MV_HIP_TRY(hipMemcpyAsync(kp, d_kp, (size_t)n * 8, hipMemcpyDeviceToHost, s));
+        MV_HIP_TRY(hipMemcpyAsync(conf, d_conf, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+        MV_HIP_TRY(hipMemcpyAsync(desc, d_out, (size_t)n * 1024, hipMemcpyDeviceToHost, s));
+        MV_HIP_TRY(hipStreamSynchronize(s));
+    }
+    *num_kp = n;
+    return mv::set_status(fst);
+}

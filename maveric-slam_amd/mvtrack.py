@@ -48,6 +48,10 @@ class PoseParams(ctypes.Structure):
                 ("inlier_thresh", _F), ("refine_iters", _I), ("seed", ctypes.c_ulonglong)]
 
 
+class KpParams(ctypes.Structure):
+    _fields_ = [("conf_thresh", _F), ("nms_dist", _I), ("border", _I)]
+
+
 class TrackParams(ctypes.Structure):
     _fields_ = [("window", WindowParams), ("pose", PoseParams), ("top_n", _I), ("valid_cap", _I)]
 
@@ -121,6 +125,9 @@ def lib():
             "ransac_essential_matrix": (None, [_I, _P, _P, _P, _I, _F, _P, _P, _P]),
             "recover_pose_from_essential_matrix": (None, [_P, _P, _P, _P]),
             "track": (_I, [_P, _P, _I, _I, _I, _F, _P]),
+            "mv_kp_params_default": (None, [_P]),
+            "mv_keypoints_dev": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P]),
+            "mv_keypoints_host": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _I, _P, _P, _P, _P]),
             "mv_trajectory_chain_dev": (_I, [_P, _I, _I, _P, _P, _P, _I, _P]),
             "mv_trajectory_rebase_dev": (_I, [_P, _I, _I, _P, _I, _P]),
             "mv_trajectory_chain_host": (_I, [_P, _I, _P, _P, _P, _I, _P]),
@@ -139,6 +146,15 @@ def lib():
 
 def _np(a):
     return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def kp_params(**kw):
+    """mv_kp_params (conf_thresh 0.015, nms_dist 4, border 4 -- pairwise_pnp.py:589-591, :99)."""
+    p = KpParams()
+    lib().mv_kp_params_default(ctypes.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
 
 
 # ---------------- trajectory (include/trajectory.h; python/compute_trajectory.py) ----------------
@@ -397,6 +413,34 @@ class Context:
         B, cap = desc0.shape[0], desc0.shape[1]
         check(lib().mv_match_allpairs_f32_run_dev(self.h, B, cap, _t(n0), _t(n1), _t(desc0), _t(desc1), float(thresh),
                                                   _t(match_idx), _t(match_score)), "match_allpairs_f32_run")
+
+    def keypoints(self, semi, coarse_desc, H, W, num_kp, kp, conf, desc, status, heat=None, params=None):
+        """Device tensors: semi [B, 65, Hc, Wc], coarse_desc [B, 256, Hc, Wc] (network outputs)
+        -> num_kp [B], kp [B, cap, 2], conf [B, cap], desc [B, cap, 256], status [B]
+        (SuperPointFrontend.run after the forward; include/keypoints.h)."""
+        B, Hc, Wc = semi.shape[0], semi.shape[2], semi.shape[3]
+        p = params or kp_params()
+        check(lib().mv_keypoints_dev(self.h, ctypes.byref(p), B, Hc, Wc, int(H), int(W), _t(semi), _t(coarse_desc),
+                                     kp.shape[1], _t(num_kp), _t(kp), _t(conf), _t(desc), _t(heat), _t(status)),
+              "keypoints")
+
+    def keypoints_host(self, semi, coarse_desc, H, W, cap=4096, params=None):
+        """numpy, one frame: semi [65, Hc, Wc], coarse_desc [256, Hc, Wc] -> (pts [n, 3] (x, y,
+        conf), desc [n, 256], status)."""
+        semi = np.ascontiguousarray(semi, np.float32)
+        cd = np.ascontiguousarray(coarse_desc, np.float32)
+        Hc, Wc = semi.shape[1], semi.shape[2]
+        kp = np.zeros((cap, 2), np.float32)
+        conf = np.zeros(cap, np.float32)
+        desc = np.zeros((cap, 256), np.float32)
+        n = ctypes.c_int(0)
+        p = params or kp_params()
+        st = lib().mv_keypoints_host(self.h, ctypes.byref(p), Hc, Wc, int(H), int(W), _np(semi), _np(cd), cap,
+                                     ctypes.byref(n), _np(kp), _np(conf), _np(desc))
+        if st not in (MV_OK, MV_ERR_CAPACITY):
+            check(st, "keypoints_host")
+        k = n.value
+        return np.concatenate([kp[:k], conf[:k, None]], axis=1), desc[:k].copy(), st
 
     def trajectory_chain(self, rel, poses, present=None, start=None, mode=CHAIN_AS_BUILT):
         """Device tensors: rel [B, len, 3, 4] float64 -> poses [B, len + 1, 3, 4] (k_chain)."""

@@ -80,3 +80,81 @@ def test_oracle_edge_cases(orc):
     semi[0, 2, 4] = 60.0  # (32, 16)
     pts, _, _ = orc.keypoints(semi, np.ones((256, 6, 9), np.float32), 48, 72)
     assert sorted(map(tuple, pts[:, :2].tolist())) == [(16.0, 16.0), (32.0, 16.0)]
+
+
+# ------------------------------------------------------------------ GPU
+def _gpu_batch(ctx, torch, frames, H, W, cap, heat=False):
+    dev = torch.device("cuda:0")
+    semi = torch.from_numpy(np.stack([f[0] for f in frames])).to(dev)
+    cd = torch.from_numpy(np.stack([f[1] for f in frames])).to(dev)
+    B, Hc, Wc = semi.shape[0], semi.shape[2], semi.shape[3]
+    n = torch.zeros(B, dtype=torch.int32, device=dev)
+    kp = torch.zeros((B, cap, 2), dtype=torch.float32, device=dev)
+    conf = torch.zeros((B, cap), dtype=torch.float32, device=dev)
+    desc = torch.zeros((B, cap, 256), dtype=torch.float32, device=dev)
+    st = torch.zeros(B, dtype=torch.int32, device=dev)
+    hm = torch.zeros((B, Hc * 8, Wc * 8), dtype=torch.float32, device=dev) if heat else None
+    ctx.set_stream(torch.cuda.current_stream())
+    ctx.keypoints(semi, cd, H, W, n, kp, conf, desc, st, heat=hm)
+    torch.cuda.synchronize()
+    ctx.set_stream(None)
+    out = (n.cpu().numpy(), kp.cpu().numpy(), conf.cpu().numpy(), desc.cpu().numpy(), st.cpu().numpy())
+    return out + ((hm.cpu().numpy(),) if heat else ())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", CASES)
+def test_gpu_keypoints_bit_exact(ctx, orc, torch_cuda, name):
+    g, semi, desc, H, W = case(name)
+    pts, d, heat = orc.keypoints(semi, desc, H, W)
+    n, kp, conf, dd, st, hm = _gpu_batch(ctx, torch_cuda, [(semi, desc)], H, W, cap=4096, heat=True)
+    assert (hm[0].view(np.int32) == heat.view(np.int32)).all()
+    assert st[0] == 0 and n[0] == pts.shape[0]
+    k = n[0]
+    assert (kp[0, :k] == pts[:, :2]).all() and (conf[0, :k].view(np.int32) == pts[:, 2].view(np.int32)).all()
+    assert (dd[0, :k].view(np.int32) == d.view(np.int32)).all()
+    # and the reference's own code (correctly rounded exp) on the fixture columns
+    assert (kp[0, :k].T.astype(np.float64) == g[name + "_cr_pts"][:2]).all()
+
+
+@pytest.mark.gpu
+def test_gpu_keypoints_batch_cap_and_edges(ctx, orc, torch_cuda):
+    """a batch of KITTI-size frames with a cap below the survivor count (prefix + status), a
+    frame without candidates and a frame with one candidate."""
+    frames = [synth.synth_superpoint_outputs(30 + i, 47, 155) for i in range(3)]
+    empty = np.zeros((65, 47, 155), np.float32)
+    empty[64] = 40.0
+    one = empty.copy()
+    one[9, 20, 30] = 60.0
+    frames += [(empty, frames[0][1]), (one, frames[1][1])]
+    cap = 1024
+    n, kp, conf, dd, st = _gpu_batch(ctx, torch_cuda, frames, 376, 1241, cap)
+    for b, (s_, d_) in enumerate(frames):
+        pts, d, _ = orc.keypoints(s_, d_, 376, 1241)
+        k = min(cap, pts.shape[0])
+        assert n[b] == k and st[b] == (-2 if pts.shape[0] > cap else 0), b
+        assert (kp[b, :k] == pts[:k, :2]).all() and (conf[b, :k] == pts[:k, 2]).all(), b
+        assert (dd[b, :k].view(np.int32) == d[:k].view(np.int32)).all(), b
+    assert n[3] == 0 and n[4] == 1 and tuple(kp[4, 0]) == (30 * 8 + 1.0, 20 * 8 + 1.0)
+
+
+@pytest.mark.gpu
+def test_gpu_keypoints_feed_allpairs(ctx, orc, torch_cuda):
+    """image pair -> keypoints -> all-pairs match on the device, end to end against the oracle."""
+    torch = torch_cuda
+    s0, d0 = synth.synth_superpoint_outputs(41, 47, 155)
+    s1, d1 = s0.copy(), d0.copy()
+    s1[:, :, 1:], d1[:, :, 1:] = s0[:, :, :-1], d0[:, :, :-1]  # frame 1: shifted one cell right
+    n, kp, conf, dd, st = _gpu_batch(ctx, torch, [(s0, d0), (s1, d1)], 376, 1241, 1024)
+    dev = torch.device("cuda:0")
+    D0 = torch.from_numpy(dd[0:1].copy()).to(dev)
+    D1 = torch.from_numpy(dd[1:2].copy()).to(dev)
+    n0 = torch.tensor(n[0:1], dtype=torch.int32, device=dev)
+    n1 = torch.tensor(n[1:2], dtype=torch.int32, device=dev)
+    idx = torch.zeros((1, 1024), dtype=torch.int32, device=dev)
+    ctx.set_stream(torch.cuda.current_stream())
+    ctx.match_allpairs_f32(D0, D1, n0, n1, idx, None, 0.8)
+    torch.cuda.synchronize()
+    ctx.set_stream(None)
+    i2, _ = orc.allpairs_f32(dd[0, :n[0]], dd[1, :n[1]], 0.8)
+    assert (idx.cpu().numpy()[0, :n[0]] == i2).all() and (i2 >= 0).sum() > 100
