@@ -301,7 +301,7 @@ __global__ __launch_bounds__(256) void k_kp_sample(int B, int cap, int Hc, int W
     if (lane == 0) {
         float ss = 0.f;
         for (int ch = 0; ch < 256; ch++) ss = __fadd_rn(ss, sq[wv][ch]);  // numpy's sequential axis-0 sum
-        nrm[wv] = __fsqrt_rn(ss);
+        nrm[wv] = sqrtf(ss);  // IEEE sqrt (-fhip-fp32-correctly-rounded-divide-sqrt; __fsqrt_rn is the native one here)
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
