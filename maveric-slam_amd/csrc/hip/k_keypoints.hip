@@ -5,17 +5,17 @@
 //   k_kp_heat    thread per cell: 65 correctly rounded expf, the reference's sequential
 //                float32 sum + 1e-5, 64 quotients -> the cell's 8x8 heatmap block
 //   k_kp_nms     one 1024-thread block per frame:
-//                (a) candidates (heat >= thresh) compacted in row-major order (tiles of 1024
-//                    pixels, ballot + LDS offsets), pixel -> candidate grid;
+//                (a) candidates (heat >= thresh) compacted in row-major order (a contiguous
+//                    chunk of pixels per wave: ballot counts, one block scan, ballot writes);
 //                (b) the greedy NMS as a fixed point: a candidate is KEPT when every
 //                    higher-priority candidate in its (2d+1)^2 window is suppressed, and
 //                    SUPPRESSED as soon as one of them is kept (priority: confidence, then
 //                    row-major order -- the reference's visiting order).  Each round decides
 //                    at least the highest-priority undecided candidate, and the result is the
 //                    sequential greedy one (a candidate's fate depends only on higher ones);
-//                (c) border filter, then each survivor's output slot = the number of
-//                    survivors ranked before it (confidence descending, ties in reversed
-//                    row-major order), counted through LDS tiles -- no sort;
+//                (c) border filter, then the survivors in output order (confidence descending,
+//                    ties in reversed row-major order): a bitonic sort of 64-bit keys in LDS
+//                    (<= 4096 survivors) or, beyond, each one's rank counted through LDS tiles;
 //   k_kp_nhwc    coarse descriptors [256][Hc*Wc] -> [Hc*Wc][256] (LDS tiles), so that each
 //                bilinear corner is one contiguous 1 KiB row
 //   k_kp_sample  one wave per keypoint: torch grid_sample's CPU arithmetic (fma unnormalise,
@@ -31,13 +31,17 @@
 namespace {
 
 constexpr int NMS_T = 1024;  // threads of the per-frame block
+constexpr int HN = 8;        // listed higher-priority neighbours per candidate
+constexpr int SORT_N = 4096; // survivors sorted in LDS (more: ranked by counting)
+__host__ __device__ inline long hn_cands(long P) { return (P + 7) / 8; }  // candidates with a list (more: rescanned)
 
 struct KpScratch {
     float *heat;        // [B][P] (when the caller does not keep it)
-    int *grid;          // [B][P] candidate id or -1
+    int *hn;            // [B][HNC][HN] higher-priority neighbour pixels of candidate k < HNC
+    int *hc;            // [B][HNC] their count (HN + 1: more than HN, rescanned each round)
     int *cpix;          // [B][P] candidate pixel (row-major heat index)
     float *cconf;       // [B][P]
-    unsigned char *st;  // [B][P] 0 undecided, 1 kept, 2 suppressed
+    unsigned char *st;  // [B][P] by PIXEL: 0 undecided, 1 kept, 2 suppressed (candidates only)
     int *kept;          // [B][P] surviving candidate ids (unordered)
     int *slot_pix;      // [B][cap] pixel of output slot
     float *nhwc;        // [B][Hc*Wc][256]
@@ -47,8 +51,9 @@ size_t a256(size_t x) { return mv::align_up(x, 256); }
 
 size_t kp_scratch_bytes(int B, int Hc, int Wc, int cap) {
     const size_t P = (size_t)Hc * Wc * 64;
-    return a256((size_t)B * P * 4) * 5 + a256((size_t)B * P) + a256((size_t)B * cap * 4) +
-           a256((size_t)B * Hc * Wc * 256 * 4);
+    const size_t hnc = (size_t)hn_cands((long)P);
+    return a256((size_t)B * P * 4) * 4 + a256((size_t)B * hnc * HN * 4) + a256((size_t)B * hnc * 4) +
+           a256((size_t)B * P) + a256((size_t)B * cap * 4) + a256((size_t)B * Hc * Wc * 256 * 4);
 }
 
 KpScratch kp_scratch_map(char *base, int B, int Hc, int Wc, int cap) {
@@ -57,8 +62,11 @@ KpScratch kp_scratch_map(char *base, int B, int Hc, int Wc, int cap) {
     size_t o = 0;
     m.heat = (float *)(base + o);
     o += a256((size_t)B * P * 4);
-    m.grid = (int *)(base + o);
-    o += a256((size_t)B * P * 4);
+    const size_t hnc = (size_t)hn_cands((long)P);
+    m.hn = (int *)(base + o);
+    o += a256((size_t)B * hnc * HN * 4);
+    m.hc = (int *)(base + o);
+    o += a256((size_t)B * hnc * 4);
     m.cpix = (int *)(base + o);
     o += a256((size_t)B * P * 4);
     m.cconf = (float *)(base + o);
@@ -110,83 +118,186 @@ __global__ __launch_bounds__(256) void k_kp_heat(long cells, int Hc, int Wc, con
 // priority of candidate j over k: higher confidence, then earlier in row-major order
 __device__ __forceinline__ bool before(float cj, int j, float ck, int k) { return cj > ck || (cj == ck && j < k); }
 
+// the higher-priority candidates in the (2D+1)^2 window of pixel pk: all heat values loaded
+// first (independent loads), then tested; the first HN pixels go to out (if out).  Returns
+// the count.
+template <int D>
+__device__ int list_higher(const float *__restrict__ heat, int Hh, int Wh, float thresh, int pk, float ck,
+                           int *__restrict__ out) {
+    const int yk = pk / Wh, xk = pk % Wh;
+    float v[2 * D + 1][2 * D + 1];
+#pragma unroll
+    for (int dy = -D; dy <= D; dy++)
+#pragma unroll
+        for (int dx = -D; dx <= D; dx++) {
+            const int y = yk + dy, x = xk + dx;
+            v[dy + D][dx + D] = (y >= 0 && y < Hh && x >= 0 && x < Wh) ? heat[y * Wh + x] : __builtin_nanf("");
+        }
+    int cnt = 0;
+#pragma unroll
+    for (int dy = -D; dy <= D; dy++)
+#pragma unroll
+        for (int dx = -D; dx <= D; dx++) {
+            if (dy == 0 && dx == 0) continue;
+            const int pj = pk + dy * Wh + dx;
+            const float h = v[dy + D][dx + D];
+            if (h >= thresh && before(h, pj, ck, pk)) {
+                if (out && cnt < HN) out[cnt] = pj;
+                cnt++;
+            }
+        }
+    return cnt;
+}
+
+__device__ int list_higher_any(const float *__restrict__ heat, int Hh, int Wh, float thresh, int d, int pk, float ck,
+                               int *__restrict__ out) {
+    const int yk = pk / Wh, xk = pk % Wh;
+    int cnt = 0;
+    for (int y = max(yk - d, 0); y <= min(yk + d, Hh - 1); y++)
+        for (int x = max(xk - d, 0); x <= min(xk + d, Wh - 1); x++) {
+            const int pj = y * Wh + x;
+            const float h = heat[pj];
+            if (pj != pk && h >= thresh && before(h, pj, ck, pk)) {
+                if (out && cnt < HN) out[cnt] = pj;
+                cnt++;
+            }
+        }
+    return cnt;
+}
+
 __global__ __launch_bounds__(NMS_T) void k_kp_nms(int Hh, int Wh, int H, int W, float thresh, int nms_dist,
                                                   int border, int cap, const float *__restrict__ heat_all,
-                                                  int *__restrict__ grid_all, int *__restrict__ cpix_all,
+                                                  int *__restrict__ hn_all, int *__restrict__ hc_all,
+                                                  int *__restrict__ cpix_all,
                                                   float *__restrict__ cconf_all, unsigned char *__restrict__ st_all,
                                                   int *__restrict__ kept_all, int *__restrict__ slot_pix_all,
                                                   int *__restrict__ num_kp, float *__restrict__ kp_out,
                                                   float *__restrict__ conf_out, int *__restrict__ status) {
     __shared__ int wsum[NMS_T / 64];
     __shared__ int s_base, s_flag, s_nk;
-    __shared__ float t_conf[NMS_T];
-    __shared__ int t_pix[NMS_T];
+    __shared__ unsigned long long skey[SORT_N];  // bitonic keys (or the rank tiles)
     const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
     const long P = (long)Hh * Wh;
     const float *heat = heat_all + b * P;
-    int *grid = grid_all + b * P;
+    const long HNC = hn_cands(P);
+    int *hn = hn_all + b * HNC * HN;
+    int *hcnt = hc_all + b * HNC;
     int *cpix = cpix_all + b * P;
     float *cconf = cconf_all + b * P;
     unsigned char *st = st_all + b * P;
     int *kept = kept_all + b * P;
     int *slot_pix = slot_pix_all + (long)b * cap;
 
-    // (a) row-major compaction of the candidates
-    if (t == 0) s_base = 0;
+    // (a) row-major compaction of the candidates: wave w owns a contiguous chunk of pixels;
+    //     count (ballots, 4 groups of 64 pixels in flight), one block scan, then write
+    constexpr int NWV = NMS_T / 64;
+    const long cw = ((P + NWV * 256 - 1) / (NWV * 256)) * 256;  // pixels per wave, multiple of 256
+    const long q0 = min(P, (long)w * cw), q1 = min(P, q0 + cw);
+    int cntw = 0;
+    for (long p0 = q0; p0 < q1; p0 += 256) {
+        float h[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const long p = p0 + 64 * u + lane;
+            h[u] = p < q1 ? heat[p] : __builtin_nanf("");
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) cntw += __popcll(__ballot(h[u] >= thresh));
+    }
+    if (lane == 0) wsum[w] = cntw;
     __syncthreads();
-    for (long p0 = 0; p0 < P; p0 += NMS_T) {
-        const long p = p0 + t;
-        const float h = p < P ? heat[p] : 0.f;
-        const bool c = p < P && h >= thresh;
-        const unsigned long long m = __ballot(c);
-        if (lane == 0) wsum[w] = __popcll(m);
-        __syncthreads();
-        int off = s_base;
-        for (int k = 0; k < w; k++) off += wsum[k];
-        if (p < P) {
-            if (c) {
-                const int id = off + __popcll(m & ((1ull << lane) - 1ull));
-                grid[p] = id;
-                cpix[id] = (int)p;
-                cconf[id] = h;
-                st[id] = 0;
-            } else {
-                grid[p] = -1;
+    if (t == 0) {
+        int acc = 0;
+        for (int k = 0; k < NWV; k++) {
+            const int c = wsum[k];
+            wsum[k] = acc;
+            acc += c;
+        }
+        s_base = acc;
+    }
+    __syncthreads();
+    {
+        int off = wsum[w];
+        for (long p0 = q0; p0 < q1; p0 += 256) {
+            float h[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const long p = p0 + 64 * u + lane;
+                h[u] = p < q1 ? heat[p] : __builtin_nanf("");
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const bool c = h[u] >= thresh;
+                const unsigned long long m = __ballot(c);
+                if (c) {
+                    const long p = p0 + 64 * u + lane;
+                    const int id = off + __popcll(m & ((1ull << lane) - 1ull));
+                    cpix[id] = (int)p;
+                    cconf[id] = h[u];
+                    st[p] = 0;
+                }
+                off += __popcll(m);
             }
         }
-        __syncthreads();
-        if (t == 0)
-            for (int k = 0; k < NMS_T / 64; k++) s_base += wsum[k];
-        __syncthreads();
     }
     const int nc = s_base;
 
-    // (b) greedy NMS as a fixed point over rounds
+    // (b) greedy NMS as a fixed point over rounds.  Candidates and their priority are read
+    //     straight from the heatmap (a pixel is a candidate iff heat >= thresh; ids are
+    //     row-major, so pixel order is id order); states are kept per pixel.  Round 0 lists each
+    //     candidate's higher-priority neighbours (all (2d+1)^2 heat values loaded at once) and
+    //     keeps those without any; later rounds only read the listed neighbours' states.
     const int d = nms_dist;
+    __syncthreads();
+    for (int k = t; k < nc; k += NMS_T) {
+        const int pk = cpix[k];
+        const float ck = cconf[k];
+        int cnt = 0;
+        int *out = k < HNC ? hn + (long)k * HN : nullptr;
+        if (d == 4)
+            cnt = list_higher<4>(heat, Hh, Wh, thresh, pk, ck, out);
+        else
+            cnt = list_higher_any(heat, Hh, Wh, thresh, d, pk, ck, out);
+        if (k < HNC) hcnt[k] = cnt;  // > HN: the list is partial, rescanned each round
+        if (cnt == 0) st[pk] = 1;
+    }
     for (;;) {
         if (t == 0) s_flag = 0;
         __syncthreads();
         int undecided = 0;
         for (int k = t; k < nc; k += NMS_T) {
-            if (st[k] != 0) continue;
-            const int pk = cpix[k], yk = pk / Wh, xk = pk % Wh;
-            const float ck = cconf[k];
+            const int pk = cpix[k];
+            if (st[pk] != 0) continue;
             bool supp = false, blocked = false;
-            for (int yy = max(yk - d, 0); yy <= min(yk + d, Hh - 1) && !supp; yy++)
-                for (int xx = max(xk - d, 0); xx <= min(xk + d, Wh - 1); xx++) {
-                    const int j = grid[(long)yy * Wh + xx];
-                    if (j < 0 || j == k || !before(cconf[j], j, ck, k)) continue;
-                    const unsigned char sj = __atomic_load_n(&st[j], __ATOMIC_RELAXED);
-                    if (sj == 1) {
-                        supp = true;
-                        break;
-                    }
-                    if (sj == 0) blocked = true;
+            const int c = k < HNC ? hcnt[k] : HN + 1;
+            if (c <= HN) {
+                int q[HN];
+#pragma unroll
+                for (int i = 0; i < HN; i++) q[i] = i < c ? hn[(long)k * HN + i] : -1;
+#pragma unroll
+                for (int i = 0; i < HN; i++) {
+                    if (q[i] < 0) continue;
+                    const unsigned char sj = __atomic_load_n(&st[q[i]], __ATOMIC_RELAXED);
+                    supp |= sj == 1;
+                    blocked |= sj == 0;
                 }
+            } else {  // more than HN higher neighbours: rescan the window
+                const float ck = cconf[k];
+                const int yk = pk / Wh, xk = pk % Wh;
+                for (int yy = max(yk - d, 0); yy <= min(yk + d, Hh - 1); yy++)
+                    for (int xx = max(xk - d, 0); xx <= min(xk + d, Wh - 1); xx++) {
+                        const int pj = yy * Wh + xx;
+                        const float h = heat[pj];
+                        if (pj == pk || !(h >= thresh) || !before(h, pj, ck, pk)) continue;
+                        const unsigned char sj = __atomic_load_n(&st[pj], __ATOMIC_RELAXED);
+                        supp |= sj == 1;
+                        blocked |= sj == 0;
+                    }
+            }
             if (supp)
-                st[k] = 2;
+                st[pk] = 2;
             else if (!blocked)
-                st[k] = 1;
+                st[pk] = 1;
             else
                 undecided = 1;
         }
@@ -199,39 +310,80 @@ __global__ __launch_bounds__(NMS_T) void k_kp_nms(int Hh, int Wh, int H, int W, 
     if (t == 0) s_nk = 0;
     __syncthreads();
     for (int k = t; k < nc; k += NMS_T) {
-        if (st[k] != 1) continue;
         const int p = cpix[k], y = p / Wh, x = p % Wh;
+        if (st[p] != 1) continue;
         if (x < border || x >= W - border || y < border || y >= H - border) continue;
         kept[atomicAdd(&s_nk, 1)] = k;
     }
     __syncthreads();
     const int nk = s_nk;
-    for (int k0 = 0; k0 < nk; k0 += NMS_T) {
-        const int k = k0 + t;
-        const int my = k < nk ? kept[k] : 0;
-        const float cm = k < nk ? cconf[my] : 0.f;
-        const int pm = k < nk ? cpix[my] : 0;
-        int rank = 0;
-        for (int j0 = 0; j0 < nk; j0 += NMS_T) {
-            __syncthreads();
-            if (j0 + t < nk) {
-                const int j = kept[j0 + t];
-                t_conf[t] = cconf[j];
-                t_pix[t] = cpix[j];
+    if (nk <= SORT_N) {
+        // bitonic sort (descending) of (confidence bits << 32 | pixel): confidence descending,
+        // ties in reversed row-major order; heat >= 0, so the float bits order as integers
+        int n2 = 1;
+        while (n2 < nk) n2 <<= 1;
+        for (int k = t; k < n2; k += NMS_T) {
+            unsigned long long key = 0ull;
+            if (k < nk) {
+                const int j = kept[k];
+                key = ((unsigned long long)__float_as_uint(cconf[j]) << 32) | (unsigned)cpix[j];
             }
-            __syncthreads();
-            const int lim = min(NMS_T, nk - j0);
-            for (int q = 0; q < lim; q++) {
-                const float cq = t_conf[q];
-                rank += (cq > cm || (cq == cm && t_pix[q] > pm)) ? 1 : 0;
-            }
+            skey[k] = key;
         }
-        if (k < nk && rank < cap) {
-            const long o = (long)b * cap + rank;
+        __syncthreads();
+        for (int size = 2; size <= n2; size <<= 1)
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                for (int i = t; i < n2 / 2; i += NMS_T) {
+                    const int lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
+                    const bool desc = (lo & size) == 0;
+                    const unsigned long long x = skey[lo], y = skey[hi];
+                    if ((x < y) == desc) {
+                        skey[lo] = y;
+                        skey[hi] = x;
+                    }
+                }
+                __syncthreads();
+            }
+        for (int r = t; r < min(nk, cap); r += NMS_T) {
+            const unsigned long long key = skey[r];
+            const int pm = (int)(unsigned)(key & 0xffffffffu);
+            const long o = (long)b * cap + r;
             kp_out[2 * o] = (float)(pm % Wh);
             kp_out[2 * o + 1] = (float)(pm / Wh);
-            conf_out[o] = cm;
-            slot_pix[rank] = pm;
+            conf_out[o] = __uint_as_float((unsigned)(key >> 32));
+            slot_pix[r] = pm;
+        }
+    } else {
+        // many survivors: slot = number ranked before (LDS tiles of the survivor list)
+        float *t_conf = reinterpret_cast<float *>(skey);
+        int *t_pix = reinterpret_cast<int *>(skey) + NMS_T;
+        for (int k0 = 0; k0 < nk; k0 += NMS_T) {
+            const int k = k0 + t;
+            const int my = k < nk ? kept[k] : 0;
+            const float cm = k < nk ? cconf[my] : 0.f;
+            const int pm = k < nk ? cpix[my] : 0;
+            int rank = 0;
+            for (int j0 = 0; j0 < nk; j0 += NMS_T) {
+                __syncthreads();
+                if (j0 + t < nk) {
+                    const int j = kept[j0 + t];
+                    t_conf[t] = cconf[j];
+                    t_pix[t] = cpix[j];
+                }
+                __syncthreads();
+                const int lim = min(NMS_T, nk - j0);
+                for (int q = 0; q < lim; q++) {
+                    const float cq = t_conf[q];
+                    rank += (cq > cm || (cq == cm && t_pix[q] > pm)) ? 1 : 0;
+                }
+            }
+            if (k < nk && rank < cap) {
+                const long o = (long)b * cap + rank;
+                kp_out[2 * o] = (float)(pm % Wh);
+                kp_out[2 * o + 1] = (float)(pm / Wh);
+                conf_out[o] = cm;
+                slot_pix[rank] = pm;
+            }
         }
     }
     if (t == 0) {
@@ -345,7 +497,7 @@ extern "C" int mv_keypoints_dev(mv_context *ctx, const mv_kp_params *p, int batc
     MV_LAUNCH_CHECK();
     MV_PROF_BEGIN(s, "k_kp_nms");
     hipLaunchKernelGGL(k_kp_nms, dim3((unsigned)batch), dim3(NMS_T), 0, s, Hc * 8, Wc * 8, H, W, p->conf_thresh,
-                       p->nms_dist, p->border, cap, hm, m.grid, m.cpix, m.cconf, m.st, m.kept, m.slot_pix, num_kp, kp,
+                       p->nms_dist, p->border, cap, hm, m.hn, m.hc, m.cpix, m.cconf, m.st, m.kept, m.slot_pix, num_kp, kp,
                        conf, status);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
