@@ -134,6 +134,15 @@ int mv_match_allpairs_f32_prepare_dev(mv_context *ctx, int batch, int cap, const
 int mv_match_allpairs_f32_run_dev(mv_context *ctx, int batch, int cap, const int *n0, const int *n1,
                                   const float *desc0, const float *desc1, double thresh, int *match_idx,
                                   float *match_score);
+/* nn_match_two_way (pairwise_pnp.py:281-323): mutual nearest neighbours under the
+ * float32 distance sqrt(2 - 2 clip(s, -1, 1)) of the score s above (np.argmin: the first
+ * NaN, else the first minimum), kept when dist < (float)nn_thresh and the reverse nearest
+ * neighbour of the match is the row itself.  match_idx[b][i] = j or -1 (i < n0[b]);
+ * match_dist (may be NULL) = the kept distance.  nn_thresh < 0: MV_ERR_INVALID_ARG (the
+ * reference raises).  Runs the all-pairs match both ways (frame 0 then frame 1 staged). */
+int mv_match_two_way_f32_dev(mv_context *ctx, int batch, int cap, const int *n0, const int *n1,
+                             const float *desc0, const float *desc1, double nn_thresh, int *match_idx,
+                             float *match_dist);
 /* int8 descriptors: exact cosine (dot > 0, 100 dot^2 > 81 |a|^2 |b|^2, first
  * maximum of dot^2/|b|^2); integer-exact (MFMA i8). */
 int mv_match_allpairs_i8_dev(mv_context *ctx, int batch, int cap, const int *n0, const int *n1,

@@ -172,6 +172,22 @@ __device__ __forceinline__ int xcd_remap(int b, int total) {
 }
 
 
+// nn_match_two_way's distance (pairwise_pnp.py:303): sqrt(2 - 2 clip(dot, -1, 1)) in float32
+// (np.clip keeps NaN); IEEE sqrt
+__device__ __forceinline__ float dist_of(float e) {
+    const float c = e != e ? e : fminf(fmaxf(e, -1.f), 1.f);
+    return sqrtf(__fsub_rn(2.f, __fmul_rn(2.f, c)));
+}
+// is (v, j) a better candidate than (bv, bj)?  dmode 0: larger dot, ties to the smaller index
+// (NaN never wins: `score > max_score`); dmode 1: np.argmin -- the first NaN, else the smaller
+// distance, ties to the smaller index
+__device__ __forceinline__ bool better(int dmode, float v, int j, float bv, int bj) {
+    if (!dmode) return v > bv || (v == bv && j < bj);
+    const bool nv = v != v, nb = bv != bv;
+    if (nv || nb) return nv && (!nb || j < bj);
+    return v < bv || (v == bv && j < bj);
+}
+
 // The reference's sequential fp32 dot (mul then add, k = 0..255).  Latency-bound: loads go
 // out EXACT_U float4 per operand at a time (EXACT_U = 16: four round trips per dot).
 #ifndef EXACT_U
@@ -264,7 +280,7 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
                                                     const int *__restrict__ n1v, const float *__restrict__ desc0,
                                                     const float *__restrict__ desc1, const char *__restrict__ h1,
                                                     const float *__restrict__ nrm1, const int *__restrict__ bad,
-                                                    double thresh, int *__restrict__ match_idx,
+                                                    double thresh, int dmode, int *__restrict__ match_idx,
                                                     float *__restrict__ match_score) {
     __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
     float *anrm = reinterpret_cast<float *>(lds + OFF_ANRM);
@@ -583,9 +599,14 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
     const float an2 = anrm[rl];
     const bool full = flagged || an2 < 0.f;  // outside the fp16 screen's range: exact scan
     const float *arow = A + (size_t)(row0 + rl) * KD;
-    float bs = -__builtin_inff();
+    // dmode 0: maximum dot (first strict), kept above thresh and 0 (pairwise_pnp.py:639-651);
+    // dmode 1: minimum distance sqrt(2 - 2 clip(dot)) (nn_match_two_way, :302-306), no threshold
+    float bs = dmode ? __builtin_inff() : -__builtin_inff();
     int bj = 0x7fffffff;
     bool wide = live && full;
+    // dmode 1: distinct dots can round to one distance; columns within TIE of the maximiser's
+    // exact dot are treated as competitors (a distance tie needs |d1 - d2| of a few ulp)
+    const double tie = dmode ? 1e-5 : 0.0;
     if (wide && fh == 0) lmask[rl] = 0xffffffffu;
     if (live && !full && !AP_EXP_NOFOLD) {  // (the NOFOLD experiment leaves untagged values)
         const double an = sqrt(fmax((double)an2, 0.0));
@@ -595,7 +616,7 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
         const double M2s = (double)M2 * 3.725290298461914e-09;
         const double dp = delta + 2.2 * rho * (fabs(Ms) + 2.0 * delta);
         if (Ms + dp > thresh) {
-            if (M2s < Ms - 2.0 * dp) {
+            if (M2s < Ms - 2.0 * dp - tie) {
                 const unsigned tg = __float_as_uint(M) & ~tkeep;
                 const int I = (int)(tg >> 1) * BN + (int)(tg & 1) * 32 + E;
                 if (I >= n1) {  // cannot happen for a tagged in-range maximum; never read past n1
@@ -604,13 +625,14 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
                 } else if (fh == 0) {
                     // decision-only (no score output): when every exact score within the window
                     // clears both tests, the maximiser's exact dot decides nothing -- skip it
-                    const bool sure = !oscore && Ms - dp > fmax(thresh, 0.0);
+                    const bool sure = !oscore && (dmode || Ms - dp > fmax(thresh, 0.0));
                     // (Ms = M 2^-28 is exact in float, and Ms > thresh, Ms > 0: the keep test passes)
                     bs = sure ? (float)Ms : AP_EXP_NOEXACT ? M : exact_dot(arow, B + (size_t)I * KD);
+                    if (dmode) bs = sure ? 0.f : dist_of(bs);
                     bj = I;
                 }
             } else {  // both lanes of the row take this branch
-                const double lim = (Ms - 2.0 * dp) * 268435456.0;
+                const double lim = (Ms - 2.0 * dp - tie) * 268435456.0;
                 // padding columns (past n1: the last tile's -3e38) are never candidates; a
                 // padding entry's m2 can only be padding too
                 const float pad_hi = -1.0e38f;
@@ -639,8 +661,9 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
                         const float *ap = arow;
                         asm volatile("" : "+v"(ap));  // keep the A row's loads inside the loop
                         const float e = exact_dot(ap, B + (size_t)j * KD);
-                        if (e > bs || (e == bs && j < bj)) {
-                            bs = e;
+                        const float v = dmode ? dist_of(e) : e;
+                        if (better(dmode, v, j, bs, bj)) {
+                            bs = v;
                             bj = j;
                         }
                     }
@@ -651,13 +674,13 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
     {
         const float ob = __shfl_xor(bs, 32, 64);
         const int oj = __shfl_xor(bj, 32, 64);
-        if (ob > bs || (ob == bs && oj < bj)) {
+        if (better(dmode, ob, oj, bs, bj)) {
             bs = ob;
             bj = oj;
         }
     }
     if (fh == 0 && live && !wide) {
-        const bool keep = bj != 0x7fffffff && (double)bs > thresh && bs > 0.f;
+        const bool keep = bj != 0x7fffffff && (dmode || ((double)bs > thresh && bs > 0.f));
         oidx[rl] = keep ? bj : -1;
         if (oscore) oscore[rl] = keep ? bs : 0.f;
     }
@@ -668,7 +691,7 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
     for (unsigned dm = (unsigned)__ballot(fh == 0 && wide); dm; dm &= dm - 1) {
         const int r = w * RW + __builtin_ctz(dm);
         const float *a = A + (size_t)(row0 + r) * KD;
-        float ws = -__builtin_inff();
+        float ws = dmode ? __builtin_inff() : -__builtin_inff();
         int wj = 0x7fffffff;
         for (unsigned Lm = lmask[r]; Lm; Lm &= Lm - 1) {
             const int f = __builtin_ctz(Lm);
@@ -676,8 +699,9 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
                 const float *ap = a;
                 asm volatile("" : "+v"(ap));  // keep the A row's loads inside the loop
                 const float e = exact_dot(ap, B + (size_t)j * KD);
-                if (e > ws || (e == ws && j < wj)) {
-                    ws = e;
+                const float v = dmode ? dist_of(e) : e;
+                if (better(dmode, v, j, ws, wj)) {
+                    ws = v;
                     wj = j;
                 }
             }
@@ -686,7 +710,7 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
         do {                                                                                 \
             const float ob = O == 32 ? __shfl_xor(ws, 32, 64) : swz_xor<O & 31>(ws);         \
             const int oj = O == 32 ? __shfl_xor(wj, 32, 64) : swz_xor<O & 31>(wj);           \
-            if (ob > ws || (ob == ws && oj < wj)) {                                          \
+            if (better(dmode, ob, oj, ws, wj)) {                                             \
                 ws = ob;                                                                     \
                 wj = oj;                                                                     \
             }                                                                                \
@@ -699,7 +723,7 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
         AP_WRED(32);
 #undef AP_WRED
         if (lane == 0) {
-            const bool keep = wj != 0x7fffffff && (double)ws > thresh && ws > 0.f;
+            const bool keep = wj != 0x7fffffff && (dmode || ((double)ws > thresh && ws > 0.f));
             oidx[r] = keep ? wj : -1;
             if (oscore) oscore[r] = keep ? ws : 0.f;
         }
@@ -763,7 +787,7 @@ int launch_allpairs_f32_prepare(hipStream_t s, void *scratch, int batch, int cap
 // the sweep + exact re-score (k_ap_match) over a prepared frame 1
 int launch_allpairs_f32_match(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
                               const float *desc0, const float *desc1, double thresh, int *match_idx,
-                              float *match_score) {
+                              float *match_score, int dmode) {
     MV_REQUIRE(batch > 0 && cap > 0 && n0 && n1 && desc0 && desc1 && match_idx && scratch);  // match_score optional
     MV_REQUIRE(((uintptr_t)desc0 & 15) == 0 && ((uintptr_t)desc1 & 15) == 0);
     const int tiles_r = (cap + BM - 1) / BM;
@@ -772,7 +796,7 @@ int launch_allpairs_f32_match(hipStream_t s, void *scratch, int batch, int cap, 
     const ApScratch m = ap_scratch_map(scratch, batch, cap);
     MV_PROF_BEGIN(s, "k_ap_match");
     hipLaunchKernelGGL(k_ap_match, dim3((unsigned)blocks), dim3(NT), 0, s, tiles_r, cap, n0, n1, desc0, desc1, m.h1,
-                       m.nrm1, m.bad, thresh, match_idx, match_score);
+                       m.nrm1, m.bad, dmode ? -1e300 : thresh, dmode, match_idx, match_score);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     return MV_OK;
@@ -851,6 +875,59 @@ extern "C" int mv_match_allpairs_f32_run_dev(mv_context *ctx, int batch, int cap
     MV_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_prep, 0));
     return mv::launch_allpairs_f32_match(ctx->stream, ctx->ap_scratch, batch, cap, n0, n1, desc0, desc1, thresh,
                                          match_idx, match_score);
+}
+
+namespace {
+// nn_match_two_way's keep (pairwise_pnp.py:307-313): dist < nn_thresh (float32 compare) and
+// the reverse argmin of the match is the row itself
+__global__ __launch_bounds__(256) void k_two_way_keep(long total, int cap, const int *__restrict__ n0v,
+                                                      const int *__restrict__ n1v, const int *__restrict__ ridx,
+                                                      float nn_thresh, int *__restrict__ fidx,
+                                                      float *__restrict__ fdist, int keep_dist) {
+    const long q = (long)blockIdx.x * 256 + threadIdx.x;
+    if (q >= total) return;
+    const long b = q / cap;
+    const int i = (int)(q % cap);
+    const int n0 = min(max(n0v[b], 0), cap), n1 = min(max(n1v[b], 0), cap);
+    const int j = fidx[q];
+    const bool keep = i < n0 && j >= 0 && j < n1 && fdist[q] < nn_thresh && ridx[b * cap + j] == i;
+    fidx[q] = keep ? j : -1;
+    if (keep_dist && !keep) fdist[q] = 0.f;
+}
+}  // namespace
+
+extern "C" int mv_match_two_way_f32_dev(mv_context *ctx, int batch, int cap, const int *n0, const int *n1,
+                                        const float *desc0, const float *desc1, double nn_thresh, int *match_idx,
+                                        float *match_dist) {
+    MV_REQUIRE(ctx != nullptr && batch > 0 && cap > 0 && n0 && n1 && desc0 && desc1 && match_idx);
+    if (!(nn_thresh >= 0.0)) {
+        mv::set_error(MV_ERR_INVALID_ARG, "nn_match_two_way: nn_thresh should be non-negative");
+        return MV_ERR_INVALID_ARG;
+    }
+    MV_HIP_TRY(hipSetDevice(ctx->device));
+    void *scr = ap_scratch(ctx, mv::allpairs_f32_scratch_bytes(batch, cap));
+    if (!scr) return MV_ERR_OUT_OF_MEMORY;
+    ctx->prep_desc1 = nullptr;  // the prepared image is overwritten
+    const size_t nb = mv::align_up((size_t)batch * cap * 4, 256);
+    char *tmp = (char *)mv::scratch(ctx, 2 * nb);
+    if (!tmp) return MV_ERR_OUT_OF_MEMORY;
+    int *ridx = (int *)tmp;
+    float *fdist = match_dist ? match_dist : (float *)(tmp + nb);
+    hipStream_t s = ctx->stream;
+    // forward: rows of frame 0 against frame 1 (argmin distance + its exact distance)
+    int st = mv::launch_allpairs_f32_prepare(s, scr, batch, cap, n1, desc1);
+    if (st == MV_OK)
+        st = mv::launch_allpairs_f32_match(s, scr, batch, cap, n0, n1, desc0, desc1, 0.0, match_idx, fdist, 1);
+    // reverse: rows of frame 1 against frame 0 (indices only)
+    if (st == MV_OK) st = mv::launch_allpairs_f32_prepare(s, scr, batch, cap, n0, desc0);
+    if (st == MV_OK)
+        st = mv::launch_allpairs_f32_match(s, scr, batch, cap, n1, n0, desc1, desc0, 0.0, ridx, nullptr, 1);
+    if (st != MV_OK) return st;
+    const long total = (long)batch * cap;
+    hipLaunchKernelGGL(k_two_way_keep, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, total, cap, n0, n1,
+                       ridx, (float)nn_thresh, match_idx, fdist, match_dist ? 1 : 0);
+    MV_LAUNCH_CHECK();
+    return mv::set_status(MV_OK);
 }
 
 #ifdef AP_EXP_TRACE

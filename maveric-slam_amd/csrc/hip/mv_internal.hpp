@@ -88,7 +88,7 @@ int launch_allpairs_f32_prepare(hipStream_t s, void *scratch, int batch, int cap
                                 const float *desc1);
 int launch_allpairs_f32_match(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
                               const float *desc0, const float *desc1, double thresh, int *match_idx,
-                              float *match_score);
+                              float *match_score, int dmode = 0);
 size_t allpairs_i8_scratch_bytes(int batch, int cap);
 int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
                        const int8_t *desc0, const int8_t *desc1, int *match_idx, int *match_dot);

@@ -111,6 +111,7 @@ def lib():
             "mv_match_allpairs_f32_prepare_dev": (_I, [_P, _I, _I, _P, _P]),
             "mv_match_allpairs_f32_run_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _D, _P, _P]),
             "mv_match_allpairs_i8_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P]),
+            "mv_match_two_way_f32_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _D, _P, _P]),
             "mv_pose_batch_dev": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P]),
             "mv_pose_from_matches_dev": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
             "mv_ransac_stub_host": (_I, [_P, _I, _P, _P, _F, _P, _P, _P]),
@@ -470,6 +471,12 @@ class Context:
         check(lib().mv_compute_trajectory(self.h, int(start_frame), int(end_frame), os.fsencode(pose_dir),
                                           os.fsencode(out_dir), int(mode), ctypes.byref(n)), "compute_trajectory")
         return n.value
+
+    def match_two_way_f32(self, desc0, desc1, n0, n1, match_idx, match_dist=None, nn_thresh=0.7):
+        """nn_match_two_way (pairwise_pnp.py:281-323) on device tensors: match_idx [B, cap]."""
+        B, cap = desc0.shape[0], desc0.shape[1]
+        check(lib().mv_match_two_way_f32_dev(self.h, B, cap, _t(n0), _t(n1), _t(desc0), _t(desc1), float(nn_thresh),
+                                             _t(match_idx), _t(match_dist)), "match_two_way_f32")
 
     def match_allpairs_i8(self, desc0, desc1, n0, n1, match_idx, match_dot):
         B, cap = desc0.shape[0], desc0.shape[1]

@@ -756,3 +756,66 @@ ORC_EXPORT void orc_kp_sample(const float *desc, int Hc, int Wc, int H, int W, i
         for (int ch = 0; ch < 256; ch++) o[ch] = o[ch] / nrm;
     }
 }
+
+/* ---- nn_match_two_way: python/pairwise_pnp.py:281-323 ----
+ * dmat = desc1^T desc2 (here the sequential fp32 dot of orc_allpairs_f32 -- the reference's
+ * np.dot is BLAS, whose order differs by ulps), dist = sqrt(2 - 2 clip(dmat, -1, 1)) in
+ * float32, idx = argmin over columns (np.argmin: first NaN, else first minimum), kept when
+ * dist < (float)nn_thresh and argmin over rows of column idx is the row.  idx [n0] = j or -1,
+ * dist [n0] = the kept distance or 0.  Returns the number kept (-1: nn_thresh < 0). */
+static float orc_dist(float s) {
+    const float c = s != s ? s : (s < -1.f ? -1.f : (s > 1.f ? 1.f : s));
+    return sqrtf(2.f - 2.f * c);
+}
+static int orc_argmin_better(float v, int j, float bv, int bj) {
+    const int nv = v != v, nb = bv != bv;
+    if (nv || nb) return nv && (!nb || j < bj);
+    return v < bv || (v == bv && j < bj);
+}
+ORC_EXPORT int orc_two_way_f32(const float *d0, int n0, const float *d1, int n1, int dim, double nn_thresh, int *idx,
+                               float *dist) {
+    if (nn_thresh < 0.0) return -1;
+    for (int i = 0; i < n0; i++) {
+        idx[i] = -1;
+        dist[i] = 0.f;
+    }
+    if (n0 == 0 || n1 == 0) return 0;
+    float *D = (float *)malloc(sizeof(float) * (size_t)n0 * n1);
+    for (int i = 0; i < n0; i++)
+        for (int j = 0; j < n1; j++) {
+            const float *a = d0 + (size_t)i * dim, *b = d1 + (size_t)j * dim;
+            float s = 0.0f;
+            for (int k = 0; k < dim; k++) s += a[k] * b[k];
+            D[(size_t)i * n1 + j] = orc_dist(s);
+        }
+    int *rev = (int *)malloc(sizeof(int) * (size_t)n1);
+    for (int j = 0; j < n1; j++) {
+        int bi = -1;
+        float bv = INFINITY;
+        for (int i = 0; i < n0; i++)
+            if (bi < 0 || orc_argmin_better(D[(size_t)i * n1 + j], i, bv, bi)) {
+                bv = D[(size_t)i * n1 + j];
+                bi = i;
+            }
+        rev[j] = bi;
+    }
+    const float th = (float)nn_thresh;
+    int kept = 0;
+    for (int i = 0; i < n0; i++) {
+        int bj = -1;
+        float bv = INFINITY;
+        for (int j = 0; j < n1; j++)
+            if (bj < 0 || orc_argmin_better(D[(size_t)i * n1 + j], j, bv, bj)) {
+                bv = D[(size_t)i * n1 + j];
+                bj = j;
+            }
+        if (bv < th && rev[bj] == i) {
+            idx[i] = bj;
+            dist[i] = bv;
+            kept++;
+        }
+    }
+    free(rev);
+    free(D);
+    return kept;
+}

@@ -58,6 +58,8 @@ def lib():
         L.orc_allpairs_i8.argtypes = [_P, _I, _P, _I, _P, _P]
         L.orc_trajectory_chain.argtypes = [_I, _P, _P, _P, _I, _P]
         L.orc_kp_heatmap.argtypes = [_P, _I, _I, _P]
+        L.orc_two_way_f32.restype = _I
+        L.orc_two_way_f32.argtypes = [_P, _I, _P, _I, _I, _D, _P, _P]
         L.orc_kp_select.restype = _I
         L.orc_kp_select.argtypes = [_P, _I, _I, _I, _I, _F, _I, _I, _I, _P]
         L.orc_kp_sample.argtypes = [_P, _I, _I, _I, _I, _I, _P, _P]
@@ -271,3 +273,16 @@ def keypoints(semi, desc, H, W, conf=0.015, nms_dist=4, border=4):
     heat = kp_heatmap(semi)
     pts = kp_select(heat, H, W, conf, nms_dist, border)
     return pts, kp_sample(desc, H, W, pts), heat
+
+
+def two_way_f32(d0, d1, nn_thresh=0.7):
+    """nn_match_two_way (pairwise_pnp.py:281-323) on row-major descriptors [n, 256] ->
+    (idx [n0] (-1: no match), dist [n0])."""
+    d0 = np.ascontiguousarray(d0, np.float32)
+    d1 = np.ascontiguousarray(d1, np.float32)
+    idx = np.zeros(d0.shape[0], np.int32)
+    dist = np.zeros(d0.shape[0], np.float32)
+    k = lib().orc_two_way_f32(_ptr(d0), d0.shape[0], _ptr(d1), d1.shape[0], d0.shape[1], float(nn_thresh), _ptr(idx),
+                              _ptr(dist))
+    assert k >= 0, "nn_thresh < 0"
+    return idx, dist
