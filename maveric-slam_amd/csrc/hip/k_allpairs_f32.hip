@@ -227,7 +227,9 @@ __device__ __forceinline__ float exact_dot(const float *__restrict__ a, const fl
 constexpr int SPLIT_ROWS = 8 * SPLIT_RPG;  // rows per block iteration: 8 row groups x SPLIT_RPG
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 #ifndef SPLIT_WPE
-#define SPLIT_WPE 1  // minimum waves per SIMD the split is compiled for (8: <= 64 VGPRs)
+#define SPLIT_WPE 1  // 8 (with SPLIT_RPG 2: 46 VGPRs) lets split waves co-reside with two
+                     // k_ap_match waves; measured: 0.34 -> 0.44 ms beside the pose, and the
+                     // overlapped pipeline (bench --pipeline 2/3) only +2 %: not the default
 #endif
 #ifndef SPLIT_GRID
 #define SPLIT_GRID (256 * 64)  // grid-stride blocks at most
