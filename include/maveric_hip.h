@@ -94,6 +94,12 @@ int mv_window_match_host(mv_context *ctx, const mv_window_params *p, int rows, i
  * scale[B] are the EFFECTIVE scales (apply mv_scale_as_built() for MV_AS_BUILT). */
 int mv_softmax_batch_dev(mv_context *ctx, int batch, int cells, const float *scales, const int8_t *semi,
                          int *max_idx, float *probs, int *num_valid);
+/* Cell-level NMS of the int8 path (src/run_nms.c:65-155) on softmax outputs, in place:
+ * max_idx / probs [B][cells] (suppressed cells: index 64, prob 64 as in the reference);
+ * kp [B][cells][2] = the surviving cells' pixels (x, y) in patch order, num_kp [B].
+ * rows * cols <= 8192 (the walk holds a frame in LDS). */
+int mv_run_nms_batch_dev(mv_context *ctx, int batch, int rows, int cols, int *max_idx, float *probs, int *num_kp,
+                         float *kp);
 /* Batched top-N selection from softmax outputs (compute_top_N, top_N.c:53-134).
  * status[B] = 0 or MV_ERR_CAPACITY.  Outputs [B][N]. */
 int mv_top_n_select_batch_dev(mv_context *ctx, int batch, int cells, const int *max_idx, const float *probs,

@@ -80,6 +80,9 @@ constexpr int NBUF = 4;  // ring slots: two column tiles of KS = 2 slices
 #ifndef AP_DMA_SPREAD
 #define AP_DMA_SPREAD 0  // 1: the slot's DMA pieces issued between its k16 steps, not before them
 #endif
+#ifndef AP_EXP_ACOAL
+#define AP_EXP_ACOAL 0
+#endif
 #ifndef AP_EXP_NODMA
 #define AP_EXP_NODMA 0
 #endif
@@ -390,6 +393,10 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
             if (AP_EXP_NOALOAD) {
                 xs[2 * s] = make_float4(0.01f * s, 0.f, 0.f, 0.f);
                 xs[2 * s + 1] = xs[2 * s];
+            } else if (AP_EXP_ACOAL) {  // timing only: row-contiguous 1-KiB loads (wrong layout)
+                const float *rb = A + (size_t)min(row0 + w * RW + 2 * s, n0 - 1) * KD + 4 * lane;
+                xs[2 * s] = *reinterpret_cast<const float4 *>(rb);
+                xs[2 * s + 1] = *reinterpret_cast<const float4 *>(rb + (2 * s + 1 < RW ? KD : 0));
             } else {
                 xs[2 * s] = *reinterpret_cast<const float4 *>(arow + s * 16);
                 xs[2 * s + 1] = *reinterpret_cast<const float4 *>(arow + s * 16 + 4);

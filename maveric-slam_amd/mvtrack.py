@@ -112,6 +112,7 @@ def lib():
             "mv_match_allpairs_f32_run_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _D, _P, _P]),
             "mv_match_allpairs_i8_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P]),
             "mv_match_two_way_f32_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _D, _P, _P]),
+            "mv_run_nms_batch_dev": (_I, [_P, _I, _I, _I, _P, _P, _P, _P]),
             "mv_pose_batch_dev": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P]),
             "mv_pose_from_matches_dev": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
             "mv_ransac_stub_host": (_I, [_P, _I, _P, _P, _F, _P, _P, _P]),
@@ -384,6 +385,11 @@ class Context:
         B, cells = semi.shape[0], semi.shape[1]
         check(lib().mv_softmax_batch_dev(self.h, B, cells, _t(scales), _t(semi), _t(max_idx), _t(probs),
                                          _t(num_valid)), "softmax_batch")
+
+    def run_nms_batch(self, rows, cols, max_idx, probs, num_kp, kp):
+        """src/run_nms.c cell NMS on device tensors max_idx/probs [B, cells] (in place)."""
+        check(lib().mv_run_nms_batch_dev(self.h, max_idx.shape[0], rows, cols, _t(max_idx), _t(probs), _t(num_kp),
+                                         _t(kp)), "run_nms_batch")
 
     def top_n_select_batch(self, max_idx, probs, N, cap, num_sel, patches, indices, sel_probs, status):
         B, cells = max_idx.shape[0], max_idx.shape[1]

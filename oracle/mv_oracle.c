@@ -819,3 +819,75 @@ ORC_EXPORT int orc_two_way_f32(const float *d0, int n0, const float *d1, int n1,
     free(D);
     return kept;
 }
+
+/* ---- cell-level NMS of the int8 path: src/run_nms.c:65-155 (main after compute_softmax) ----
+ * For every grid corner (x_grid_i, y_grid_i), x in [0, cols], y in [0, rows] (x outer, :68-69),
+ * gather the (at most 4) cells around it whose keypoint lies in the quadrant next to the
+ * corner (:75-104: x_delta -1 needs patch_x >= 2, 0 needs patch_x < 6, likewise y), then
+ * repeatedly take the most probable (the first loop only over patches > 0, :108-114, then a
+ * second pass over patches >= 0 from that maximum, :118-123) and suppress the others within
+ * 4 px in x and y (< 4, :131) by setting their max_indices to 64 and probs to 64 (:133-134).
+ * max_idx / probs [cells] are modified in place (cell p = gx * rows + gy); kp [cells][2]
+ * receives the survivors' pixels in patch order (:147-155).  Returns their count. */
+ORC_EXPORT int orc_run_nms(int rows, int cols, int *max_idx, float *probs, float *kp) {
+    for (int xi = 0; xi <= cols; xi++)
+        for (int yi = 0; yi <= rows; yi++) {
+            int n = 0, pat[4], xs[4], ys[4];
+            float pr[4];
+            for (int xd = -1; xd <= 0; xd++) {
+                const int xg = xi + xd;
+                if (xg < 0 || xg >= cols) continue;
+                for (int yd = -1; yd <= 0; yd++) {
+                    const int yg = yi + yd;
+                    if (yg < 0 || yg >= rows) continue;
+                    const int p = xg * rows + yg, idx = max_idx[p];
+                    if (idx == 64) continue;
+                    const int px = idx % 8, py = idx / 8;
+                    if (xd == -1 && px < 2) continue;
+                    if (xd == 0 && px >= 6) continue;
+                    if (yd == -1 && py < 2) continue;
+                    if (yd == 0 && py >= 6) continue;
+                    pat[n] = p;
+                    pr[n] = probs[p];
+                    xs[n] = xg * 8 + px;
+                    ys[n] = yg * 8 + py;
+                    n++;
+                }
+            }
+            for (;;) {
+                float mp = 0;
+                int mi = -1;
+                for (int i = 0; i < n; i++)
+                    if (pat[i] > 0 && pr[i] > mp) {
+                        mp = pr[i];
+                        mi = i;
+                    }
+                if (mi == -1) break;
+                for (int i = 0; i < n; i++)
+                    if (pat[i] >= 0 && pr[i] > mp) {
+                        mp = pr[i];
+                        mi = i;
+                    }
+                for (int i = 0; i < n; i++) {
+                    if (i == mi || pat[i] < 0) continue;
+                    if (abs(xs[mi] - xs[i]) < 4 && abs(ys[mi] - ys[i]) < 4) {
+                        max_idx[pat[i]] = 64;
+                        probs[pat[i]] = 64;
+                        pat[i] = -1;
+                        pr[i] = -1;
+                    }
+                }
+                pr[mi] = -1;
+                pat[mi] = -1;
+            }
+        }
+    int nk = 0;
+    for (int p = 0; p < rows * cols; p++) {
+        const int idx = max_idx[p];
+        if (idx == 64) continue;
+        kp[2 * nk] = (float)((p / rows) * 8 + idx % 8);
+        kp[2 * nk + 1] = (float)((p % rows) * 8 + idx / 8);
+        nk++;
+    }
+    return nk;
+}

@@ -58,6 +58,8 @@ def lib():
         L.orc_allpairs_i8.argtypes = [_P, _I, _P, _I, _P, _P]
         L.orc_trajectory_chain.argtypes = [_I, _P, _P, _P, _I, _P]
         L.orc_kp_heatmap.argtypes = [_P, _I, _I, _P]
+        L.orc_run_nms.restype = _I
+        L.orc_run_nms.argtypes = [_I, _I, _P, _P, _P]
         L.orc_two_way_f32.restype = _I
         L.orc_two_way_f32.argtypes = [_P, _I, _P, _I, _I, _D, _P, _P]
         L.orc_kp_select.restype = _I
@@ -286,3 +288,12 @@ def two_way_f32(d0, d1, nn_thresh=0.7):
                               _ptr(dist))
     assert k >= 0, "nn_thresh < 0"
     return idx, dist
+
+
+def run_nms(rows, cols, max_idx, probs):
+    """src/run_nms.c:65-155 on compute_softmax outputs -> (max_idx', probs', kp [n, 2])."""
+    mi = np.ascontiguousarray(max_idx, np.int32).copy()
+    pr = np.ascontiguousarray(probs, np.float32).copy()
+    kp = np.zeros((rows * cols, 2), np.float32)
+    n = lib().orc_run_nms(rows, cols, _ptr(mi), _ptr(pr), _ptr(kp))
+    return mi, pr, kp[:n].copy()
