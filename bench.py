@@ -49,6 +49,8 @@ def parse():
                          "includes its neighbours, so the roofline line is only meaningful at 1)")
     ap.add_argument("--score-steps", type=int, default=10,
                     help="secondary: steps timed with the exact score materialised (0 = skip)")
+    ap.add_argument("--extra-steps", type=int, default=10,
+                    help="secondary lines at N = 1: int8 all-pairs (config 5) and keypoint extraction; 0 = skip")
     ap.add_argument("--check", type=int, default=2, help="pairs verified against the oracle after timing")
     ap.add_argument("--window-steps", type=int, default=10,
                     help="secondary line (N = 1 only): the windowed int8 front-end of tracking_main.c "
@@ -368,6 +370,19 @@ def main():
         w, _ = bench_window.run(batch=1024, steps=args.window_steps, warmup=2, check=1)
         out["window_frontend"] = {k: w[k] for k in ("metric", "value", "unit", "ms_per_step", "semantics",
                                                      "stages_ms", "hbm_roofline", "checked_pairs")}
+    if rank == 0 and world == 1 and args.extra_steps > 0:
+        # the other single-GPU configs beside the headline (not its value): BASELINE config 5
+        # (int8 all-pairs, 2048 kp) and SURVEY §8(f)2 keypoint extraction, timed after it
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import bench_i8
+        import bench_keypoints
+
+        r = bench_i8.run(batch=256, kp=2048, steps=args.extra_steps, warmup=2, check=1)
+        out["i8_allpairs"] = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "stages_ms",
+                                                  "mfma_roofline", "checked_pairs")}
+        r = bench_keypoints.run(batch=256, steps=args.extra_steps, warmup=2, check=1)
+        out["keypoints"] = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "stages_ms",
+                                               "hbm_roofline", "checked_frames")}
     if rank == 0:
         print(json.dumps(out), flush=True)
     for cx in ctxs:

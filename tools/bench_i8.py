@@ -29,6 +29,11 @@ def main():
     ap.add_argument("--check", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
+    print(json.dumps(run(args.batch, args.kp, args.steps, args.warmup, args.check, args.cpu_seconds)), flush=True)
+
+
+def run(batch=256, kp=2048, steps=20, warmup=3, check=1, cpu_seconds=0.0):
+    args = argparse.Namespace(batch=batch, kp=kp, steps=steps, warmup=warmup, check=check, cpu_seconds=cpu_seconds)
     B, n, D = args.batch, args.kp, 256
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev)
@@ -101,8 +106,8 @@ def main():
         out["cpu_baseline"] = {"value": round(total / dt, 2), "unit": "pairs/s", "cores": threads, "kind": "port",
                                "sample": "%d pairs of %dx%dx256 int8 in %.1f s on %d host threads"
                                          % (total, n, n, dt, threads)}
-    print(json.dumps(out), flush=True)
     ctx.close()
+    return out
 
 
 if __name__ == "__main__":
