@@ -113,6 +113,8 @@ def lib():
             "mv_match_allpairs_i8_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P]),
             "mv_match_two_way_f32_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _D, _P, _P]),
             "mv_run_nms_batch_dev": (_I, [_P, _I, _I, _I, _P, _P, _P, _P]),
+            "mv_projection_factors_dev": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+            "mv_pose_normal_equations_dev": (_I, [_P, _I, _P, _P, _P, _P, _P]),
             "mv_pose_batch_dev": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P]),
             "mv_pose_from_matches_dev": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
             "mv_ransac_stub_host": (_I, [_P, _I, _P, _P, _F, _P, _P, _P]),
@@ -385,6 +387,16 @@ class Context:
         B, cells = semi.shape[0], semi.shape[1]
         check(lib().mv_softmax_batch_dev(self.h, B, cells, _t(scales), _t(semi), _t(max_idx), _t(probs),
                                          _t(num_valid)), "softmax_batch")
+
+    def projection_factors(self, landmarks, poses, cameras, ldmk_id, pose_id, meas, err, J=None, H=None):
+        """Device tensors (include/factors.h): err [F, 2], J [F, 20], H [F, 100]."""
+        check(lib().mv_projection_factors_dev(self.h, ldmk_id.shape[0], _t(landmarks), _t(poses), _t(cameras),
+                                              _t(ldmk_id), _t(pose_id), _t(meas), _t(err), _t(J), _t(H)),
+              "projection_factors")
+
+    def pose_normal_equations(self, pose_offsets, J, HPP, g, ee):
+        check(lib().mv_pose_normal_equations_dev(self.h, pose_offsets.shape[0] - 1, _t(pose_offsets), _t(J), _t(HPP),
+                                                 _t(g), _t(ee)), "pose_normal_equations")
 
     def run_nms_batch(self, rows, cols, max_idx, probs, num_kp, kp):
         """src/run_nms.c cell NMS on device tensors max_idx/probs [B, cells] (in place)."""

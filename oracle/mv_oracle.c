@@ -891,3 +891,85 @@ ORC_EXPORT int orc_run_nms(int rows, int cols, int *max_idx, float *probs, float
     }
     return nk;
 }
+
+/* ---- projection factors: src/projection_factor.c:12-33 with src/types.c:3-73 (error), an
+ * analytic Jacobian (the reference has none), and the factor's [J|r]^T [J|r] in the
+ * local-BA layout of src/local_bundle_adjustment.c:161-169 (columns [landmark 3 | pose 6 |
+ * residual 1], matmul2's k order).  pose [7] = (qw, qx, qy, qz, tx, ty, tz); cam [4] =
+ * (fx, fy, cx, cy).  J [20] column-major 2 x 10: landmark, rotation (left perturbation
+ * omega: p' = p + omega x p), translation, residual; H [100] row-major 10 x 10. ---- */
+static void orc_qmul(const float *a, const float *b, float *o) { /* types.c:19-26 order */
+    o[0] = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+    o[1] = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+    o[2] = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+    o[3] = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+}
+ORC_EXPORT void orc_pf_linearize(int F, const float *ldmk, const float *pose, const int *lid, const int *pid,
+                                 const float *meas, const float *cam, float *err, float *J, float *H) {
+    for (int f = 0; f < F; f++) {
+        const float *X = ldmk + 3 * (size_t)lid[f], *T = pose + 7 * (size_t)pid[f], *K = cam + 4 * (size_t)pid[f];
+        const float vq[4] = {0.f, X[0], X[1], X[2]}, qc[4] = {T[0], -T[1], -T[2], -T[3]};
+        float qv[4], r[4];
+        orc_qmul(T, vq, qv);
+        orc_qmul(qv, qc, r); /* apply_rotation, types.c:63-68 */
+        const float px = r[1] + 1.f * T[4], py = r[2] + 1.f * T[5], pz = r[3] + 1.f * T[6];
+        const float ux = px / pz, uy = py / pz; /* project2d, projection_factor.c:12-17 */
+        const float ex = (ux * K[0] + K[2]) + -1.f * meas[2 * f], ey = (uy * K[1] + K[3]) + -1.f * meas[2 * f + 1];
+        err[2 * f] = ex;
+        err[2 * f + 1] = ey;
+        /* d e / d p_c */
+        const float iz = 1.f / pz;
+        const float d00 = K[0] * iz, d02 = -(K[0] * px) * iz * iz, d11 = K[1] * iz, d12 = -(K[1] * py) * iz * iz;
+        /* the linear map v -> q v q* (unnormalised q) */
+        const float w = T[0], x = T[1], y = T[2], z = T[3];
+        const float R[9] = {w * w + x * x - y * y - z * z, 2.f * (x * y - w * z), 2.f * (x * z + w * y),
+                            2.f * (x * y + w * z), w * w - x * x + y * y - z * z, 2.f * (y * z - w * x),
+                            2.f * (x * z - w * y), 2.f * (y * z + w * x), w * w - x * x - y * y + z * z};
+        /* -[p]x */
+        const float S[9] = {0.f, pz, -py, -pz, 0.f, px, py, -px, 0.f};
+        float *Jf = J + 20 * (size_t)f;
+        for (int c = 0; c < 3; c++) {
+            Jf[2 * c] = d00 * R[c] + d02 * R[6 + c];
+            Jf[2 * c + 1] = d11 * R[3 + c] + d12 * R[6 + c];
+            Jf[2 * (3 + c)] = d00 * S[c] + d02 * S[6 + c];
+            Jf[2 * (3 + c) + 1] = d11 * S[3 + c] + d12 * S[6 + c];
+        }
+        Jf[12] = d00;
+        Jf[13] = 0.f;
+        Jf[14] = 0.f;
+        Jf[15] = d11;
+        Jf[16] = d02;
+        Jf[17] = d12;
+        Jf[18] = ex;
+        Jf[19] = ey;
+        float *Hf = H + 100 * (size_t)f;
+        for (int i = 0; i < 10; i++)
+            for (int j = 0; j < 10; j++) {
+                float s = 0.f;
+                s += Jf[2 * i] * Jf[2 * j];
+                s += Jf[2 * i + 1] * Jf[2 * j + 1];
+                Hf[10 * i + j] = s;
+            }
+    }
+}
+
+/* Normal equations of each pose from its factors (pose-only refinement): the factors of pose
+ * p are [off[p], off[p+1]) and are accumulated in that order, as the local-BA scatter adds
+ * H_factor into the pose block one factor at a time (local_bundle_adjustment.c:184-200):
+ * HPP [P][36] (rows 3..8 x cols 3..8 of H), g [P][6] (rows 3..8, col 9), ee [P] (9, 9). */
+ORC_EXPORT void orc_pose_normal_equations(int P, const int *off, const float *H, float *HPP, float *g, float *ee) {
+    for (int p = 0; p < P; p++) {
+        float a[36] = {0}, b[6] = {0}, c = 0.f;
+        for (int f = off[p]; f < off[p + 1]; f++) {
+            const float *Hf = H + 100 * (size_t)f;
+            for (int i = 0; i < 6; i++) {
+                for (int j = 0; j < 6; j++) a[6 * i + j] = Hf[10 * (3 + i) + 3 + j] + a[6 * i + j];
+                b[i] = Hf[10 * (3 + i) + 9] + b[i];
+            }
+            c = Hf[99] + c;
+        }
+        memcpy(HPP + 36 * (size_t)p, a, sizeof a);
+        memcpy(g + 6 * (size_t)p, b, sizeof b);
+        ee[p] = c;
+    }
+}

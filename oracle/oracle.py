@@ -58,6 +58,8 @@ def lib():
         L.orc_allpairs_i8.argtypes = [_P, _I, _P, _I, _P, _P]
         L.orc_trajectory_chain.argtypes = [_I, _P, _P, _P, _I, _P]
         L.orc_kp_heatmap.argtypes = [_P, _I, _I, _P]
+        L.orc_pf_linearize.argtypes = [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P]
+        L.orc_pose_normal_equations.argtypes = [_I, _P, _P, _P, _P, _P]
         L.orc_run_nms.restype = _I
         L.orc_run_nms.argtypes = [_I, _I, _P, _P, _P]
         L.orc_two_way_f32.restype = _I
@@ -90,6 +92,8 @@ def ref():
         R.recover_pose_from_essential_matrix.argtypes = [_P, _P, _P, _P]
         R.call_svd.argtypes = [_P, _P, _P, _P]
         R.ref_matmul_nt.argtypes = [_I, _I, _I, _P, _P, _P]
+        R.ref_pf_error.argtypes = [_P, _P, _P, _P, _P]
+        R.ref_h_factor.argtypes = [_P, _P]
         _ref = R
     return _ref
 
@@ -297,3 +301,31 @@ def run_nms(rows, cols, max_idx, probs):
     kp = np.zeros((rows * cols, 2), np.float32)
     n = lib().orc_run_nms(rows, cols, _ptr(mi), _ptr(pr), _ptr(kp))
     return mi, pr, kp[:n].copy()
+
+
+def pf_linearize(ldmk, pose, lid, pid, meas, cam):
+    """projection factors -> (err [F, 2], J [F, 20] col-major 2x10, H [F, 100])."""
+    ldmk = np.ascontiguousarray(ldmk, np.float32)
+    pose = np.ascontiguousarray(pose, np.float32)
+    lid = np.ascontiguousarray(lid, np.int32)
+    pid = np.ascontiguousarray(pid, np.int32)
+    meas = np.ascontiguousarray(meas, np.float32)
+    cam = np.ascontiguousarray(cam, np.float32)
+    F = lid.shape[0]
+    err = np.zeros((F, 2), np.float32)
+    J = np.zeros((F, 20), np.float32)
+    H = np.zeros((F, 100), np.float32)
+    lib().orc_pf_linearize(F, _ptr(ldmk), _ptr(pose), _ptr(lid), _ptr(pid), _ptr(meas), _ptr(cam), _ptr(err),
+                           _ptr(J), _ptr(H))
+    return err, J, H
+
+
+def pose_normal_equations(off, H):
+    off = np.ascontiguousarray(off, np.int32)
+    H = np.ascontiguousarray(H, np.float32)
+    P = off.shape[0] - 1
+    HPP = np.zeros((P, 36), np.float32)
+    g = np.zeros((P, 6), np.float32)
+    ee = np.zeros(P, np.float32)
+    lib().orc_pose_normal_equations(P, _ptr(off), _ptr(H), _ptr(HPP), _ptr(g), _ptr(ee))
+    return HPP, g, ee
