@@ -71,6 +71,9 @@ constexpr int NBUF = 4;  // ring slots: two column tiles of KS = 2 slices
 #ifndef AP_EXP_NOFOLD
 #define AP_EXP_NOFOLD 0
 #endif
+#ifndef AP_AUX_PRIO
+#define AP_AUX_PRIO 0
+#endif
 #ifndef AP_STAGGER
 #define AP_STAGGER 0  // > 0: first-generation second-slot blocks start this many 100-MHz ticks late
 #endif
@@ -854,7 +857,15 @@ extern "C" int mv_match_allpairs_f32_prepare_dev(mv_context *ctx, int batch, int
     void *scr = ap_scratch(ctx, mv::allpairs_f32_scratch_bytes(batch, cap));
     if (!scr) return MV_ERR_OUT_OF_MEMORY;
     if (!ctx->aux_stream) {
+#if AP_AUX_PRIO
+        // the staging stream at the highest priority: its HBM-bound split then runs ahead of
+        // the latency-bound pose kernels it overlaps (timing switch, AP_AUX_PRIO=1)
+        int prio_lo = 0, prio_hi = 0;
+        MV_HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+        MV_HIP_TRY(hipStreamCreateWithPriority(&ctx->aux_stream, hipStreamNonBlocking, prio_hi));
+#else
         MV_HIP_TRY(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
+#endif
         MV_HIP_TRY(hipEventCreateWithFlags(&ctx->ev_in, hipEventDisableTiming));
         MV_HIP_TRY(hipEventCreateWithFlags(&ctx->ev_prep, hipEventDisableTiming));
     }
