@@ -31,6 +31,19 @@ int mv_projection_factors_dev(mv_context *ctx, int num_factors, const float *lan
 int mv_pose_normal_equations_dev(mv_context *ctx, int num_poses, const int *pose_offsets, const float *J,
                                  float *HPP, float *g, float *ee);
 
+/* The local-BA Schur back-end (src/local_bundle_adjustment.c:128-250) for `batch`
+ * independent windows of num_poses poses and num_ldmks landmarks (every landmark observed by
+ * every pose, as in the reference), chunk landmarks at a time: J [batch][ceil(L/chunk)]
+ * [num_poses * chunk][20] holds each chunk's factor blocks (2 x 10 column-major, [landmark |
+ * pose | residual]); factor (landmark i of the chunk, pose p) is entry p * i with
+ * MV_AS_BUILT (the reference's index, local_bundle_adjustment.c:158) and i * num_poses + p
+ * with MV_AS_INTENDED.  C [batch][S][S] (S = 6 num_poses + 1, column-major) is accumulated
+ * in place: the pose-pose Schur complement (plus the reference's residual row).  The
+ * reference's order throughout (bit-identical to its own functions).  LDS: 4 (100 + 9 chunk^2
+ * + 6 S chunk + S^2) bytes <= 64 KiB. */
+int mv_lba_schur_dev(mv_context *ctx, int batch, int num_poses, int num_ldmks, int chunk, int semantics,
+                     const float *J, float *C);
+
 #ifdef __cplusplus
 }
 #endif

@@ -115,6 +115,7 @@ def lib():
             "mv_run_nms_batch_dev": (_I, [_P, _I, _I, _I, _P, _P, _P, _P]),
             "mv_projection_factors_dev": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
             "mv_pose_normal_equations_dev": (_I, [_P, _I, _P, _P, _P, _P, _P]),
+            "mv_lba_schur_dev": (_I, [_P, _I, _I, _I, _I, _I, _P, _P]),
             "mv_pose_batch_dev": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P]),
             "mv_pose_from_matches_dev": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
             "mv_ransac_stub_host": (_I, [_P, _I, _P, _P, _F, _P, _P, _P]),
@@ -397,6 +398,11 @@ class Context:
     def pose_normal_equations(self, pose_offsets, J, HPP, g, ee):
         check(lib().mv_pose_normal_equations_dev(self.h, pose_offsets.shape[0] - 1, _t(pose_offsets), _t(J), _t(HPP),
                                                  _t(g), _t(ee)), "pose_normal_equations")
+
+    def lba_schur(self, num_poses, num_ldmks, chunk, J, C, semantics=AS_INTENDED):
+        """local-BA Schur back-end on device tensors J [B, chunks, P*chunk, 20], C [B, S*S]."""
+        check(lib().mv_lba_schur_dev(self.h, J.shape[0], num_poses, num_ldmks, chunk, int(semantics), _t(J), _t(C)),
+              "lba_schur")
 
     def run_nms_batch(self, rows, cols, max_idx, probs, num_kp, kp):
         """src/run_nms.c cell NMS on device tensors max_idx/probs [B, cells] (in place)."""

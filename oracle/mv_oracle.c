@@ -973,3 +973,77 @@ ORC_EXPORT void orc_pose_normal_equations(int P, const int *off, const float *H,
         ee[p] = c;
     }
 }
+
+/* ---- local BA Schur back-end: src/local_bundle_adjustment.c:128-250 (main), with its
+ * matrix_add (:35-44), invert_3x3 (:46-75), invert_block_diagonal_matrix (:77-83), the
+ * zeroing helpers and matmul2 (gemmini_functions_cpu.h:60-124).  For every chunk of LC
+ * landmarks: assemble A (block-diagonal 3x3 landmark blocks), B (pose x landmark, residual
+ * row) and C (pose x pose, residual row) from the factors' H = J^T J, invert A's blocks, and
+ * C -= B^T-side product (B A^-1) -- the Schur complement of the landmarks, accumulated in C
+ * chunk after chunk.  J [L / LC][P * LC][20]: each chunk's factor buffer (2 x 10 column-major,
+ * [landmark 3 | pose 6 | residual 1]); factor (landmark chunk_i, pose p) is buffer entry
+ * p * chunk_i as built (:158, the reference's index), chunk_i * P + p as intended.
+ * C [(6P+1)^2], column-major stride 6P+1, in/out (the reference starts from zeros). ---- */
+static void orc_madd(const float *A, float *C, int rows, int cols, int sA, int sC) { /* :35-44, alpha = beta = 1 */
+    for (int j = 0; j < cols; j++)
+        for (int i = 0; i < rows; i++) C[j * sC + i] = 1.f * A[j * sA + i] + 1.f * C[j * sC + i];
+}
+static void orc_inv3(float *m, int stride) { /* :46-75 */
+    float a[9], v[9];
+    for (int j = 0; j < 3; j++)
+        for (int i = 0; i < 3; i++) a[j * 3 + i] = m[j * stride + i];
+    const float det = a[0] * (a[4] * a[8] - a[5] * a[7]) - a[1] * (a[3] * a[8] - a[5] * a[6]) +
+                      a[2] * (a[3] * a[7] - a[4] * a[6]);
+    v[0] = (a[4] * a[8] - a[5] * a[7]) / det;
+    v[1] = (a[2] * a[7] - a[1] * a[8]) / det;
+    v[2] = (a[1] * a[5] - a[2] * a[4]) / det;
+    v[3] = (a[5] * a[6] - a[3] * a[8]) / det;
+    v[4] = (a[0] * a[8] - a[2] * a[6]) / det;
+    v[5] = (a[2] * a[3] - a[0] * a[5]) / det;
+    v[6] = (a[3] * a[7] - a[4] * a[6]) / det;
+    v[7] = (a[1] * a[6] - a[0] * a[7]) / det;
+    v[8] = (a[0] * a[4] - a[1] * a[3]) / det;
+    for (int j = 0; j < 3; j++)
+        for (int i = 0; i < 3; i++) m[j * stride + i] = v[j * 3 + i];
+}
+/* matmul2 with D == C (C = sD * C first), row-major strides as in gemmini_functions_cpu.h */
+static void orc_mm2(int I, int Jn, int K, const float *A, const float *B, float *C, int sA, int sB, int sC, float aS,
+                    float bS, float dS, int tA, int tB) {
+    const int sAi = tA ? 1 : sA, sAk = tA ? sA : 1, sBk = tB ? 1 : sB, sBj = tB ? sB : 1;
+    for (int i = 0; i < I; i++)
+        for (int j = 0; j < Jn; j++) C[i * sC + j] = dS * C[i * sC + j];
+    for (int i = 0; i < I; i++)
+        for (int j = 0; j < Jn; j++)
+            for (int k = 0; k < K; k++) C[i * sC + j] += aS * A[i * sAi + k * sAk] * bS * B[k * sBk + j * sBj];
+}
+ORC_EXPORT void orc_lba_schur(int P, int L, int LC, int as_built, const float *J, float *C) {
+    const int S = 6 * P + 1, TL = 3 * LC;
+    float *A = (float *)calloc((size_t)TL * TL, sizeof(float));
+    float *Bc = (float *)calloc((size_t)S * TL, sizeof(float));
+    float *BA = (float *)calloc((size_t)S * TL, sizeof(float));
+    float H[100] = {0}; /* (main's H_factor is uninitialised stack memory; +0 here) */
+    for (int c0 = 0, ch = 0; c0 < L; c0 += LC, ch++) {
+        for (int I = 0; I < TL; I += 3) /* zero_block_diagonal_matrix */
+            for (int i = 0; i < 3; i++)
+                for (int j = 0; j < 3; j++) A[(I + i) * TL + I + j] = 0;
+        memset(Bc, 0, sizeof(float) * (size_t)S * TL);
+        const float *Jc = J + (size_t)ch * P * LC * 20;
+        for (int ci = 0; ci < LC; ci++)
+            for (int p = 0; p < P; p++) {
+                const int pi = p * 6, li = ci * 3;
+                const float *Jf = Jc + 20 * (size_t)(as_built ? p * ci : ci * P + p);
+                orc_mm2(10, 10, 2, Jf, Jf, H, 2, 2, 10, 1.f, 1.f, 0.f, 0, 1);
+                orc_madd(H, A + li * (TL + 1), 3, 3, 10, TL);
+                orc_madd(H + 3, Bc + pi + li * S, 6, 3, 10, S);
+                orc_madd(H + 9, Bc + (li + 1) * S - 1, 1, 3, 10, S);
+                orc_madd(H + 33, C + pi * (S + 1), 6, 6, 10, S);
+                orc_madd(H + 39, C + (pi + 1) * S - 1, 1, 6, 10, S);
+            }
+        for (int I = 0; I < TL; I += 3) orc_inv3(A + I * TL + I, TL);
+        orc_mm2(TL, 6 * P, TL, A, Bc, BA, TL, S, S, 1.f, 1.f, 0.f, 0, 0);
+        orc_mm2(6 * P, 6 * P, TL, Bc, BA, C, S, S, S, -1.f, 1.f, 1.f, 1, 0);
+    }
+    free(A);
+    free(Bc);
+    free(BA);
+}

@@ -60,6 +60,7 @@ def lib():
         L.orc_kp_heatmap.argtypes = [_P, _I, _I, _P]
         L.orc_pf_linearize.argtypes = [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P]
         L.orc_pose_normal_equations.argtypes = [_I, _P, _P, _P, _P, _P]
+        L.orc_lba_schur.argtypes = [_I, _I, _I, _I, _P, _P]
         L.orc_run_nms.restype = _I
         L.orc_run_nms.argtypes = [_I, _I, _P, _P, _P]
         L.orc_two_way_f32.restype = _I
@@ -329,3 +330,38 @@ def pose_normal_equations(off, H):
     ee = np.zeros(P, np.float32)
     lib().orc_pose_normal_equations(P, _ptr(off), _ptr(H), _ptr(HPP), _ptr(g), _ptr(ee))
     return HPP, g, ee
+
+
+def lba_schur(P, L, LC, J, as_built=True, C=None):
+    """local_bundle_adjustment.c main's Schur loop: J [L/LC, P*LC, 20] -> C [(6P+1)^2] col-major."""
+    J = np.ascontiguousarray(J, np.float32)
+    S = 6 * P + 1
+    C = np.zeros(S * S, np.float32) if C is None else np.ascontiguousarray(C, np.float32).copy()
+    lib().orc_lba_schur(P, L, LC, 1 if as_built else 0, _ptr(J), _ptr(C))
+    return C
+
+
+def lba_reference_J(P, L, LC):
+    """the factor buffers main() uses: initialize_random_matrix(J, 2 P LC, 10) every chunk
+    (local_bundle_adjustment.c:89-95, :149-151): element (i, j) of the column-major
+    (2 P LC) x 10 matrix is i * 10 + j."""
+    rows = 2 * P * LC
+    m = np.zeros(rows * 10, np.float32)
+    for j in range(10):
+        for i in range(rows):
+            m[j * rows + i] = i * 10 + j
+    return np.tile(m.reshape(P * LC, 20)[None], (-(-L // LC), 1, 1))
+
+
+_ref_lba = None
+
+
+def ref_lba():
+    """the reference's local_bundle_adjustment.c functions driven through main's loop
+    (oracle/ref_lba_harness.c); build-container only."""
+    global _ref_lba
+    if _ref_lba is None:
+        R = ctypes.CDLL(os.path.join(HERE, "_ref", "libmv_ref_lba.so"))
+        R.ref_lba_schur_main.argtypes = [_I, _I, _I, _P]
+        _ref_lba = R
+    return _ref_lba
