@@ -83,6 +83,9 @@ constexpr int NBUF = 4;  // ring slots: two column tiles of KS = 2 slices
 #ifndef AP_DMA_SPREAD
 #define AP_DMA_SPREAD 0  // 1: the slot's DMA pieces issued between its k16 steps, not before them
 #endif
+#ifndef AP_EXP_MX
+#define AP_EXP_MX 0  // timing only: the sweep on MX-fp8 MFMAs (2x the FP16 rate), wrong results
+#endif
 #ifndef AP_EXP_ACOAL
 #define AP_EXP_ACOAL 0
 #endif
@@ -117,6 +120,7 @@ static_assert(LDS_BYTES * (8 / NW) <= 160 * 1024, "LDS per CU");
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef int v8i_t __attribute__((ext_vector_type(8)));
 
 // 16-B-per-lane HBM/L2 -> LDS DMA (global_load_lds_dwordx4, SADDR form): source = SGPR
 // base + 32-bit VGPR byte offset; LDS destination = M0 (wave-uniform byte address) + lane *
@@ -476,7 +480,23 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
         }                                                                                     \
         const char *base = lds + OFF_STAGE + (J) * SL_BYTES + rdb;                            \
         if constexpr (AP_SETPRIO) __builtin_amdgcn_s_setprio(1);                              \
-        if (!AP_EXP_NOMFMA) {                                                                 \
+        if (AP_EXP_MX) {                                                                      \
+            /* timing only: MX-fp8 MFMAs (K = 64, 32 B per lane) on the first slice of a tile */ \
+            if ((J) % KS == 0) {                                                              \
+                v8i_t b0m_[4], b1m_[4];                                                       \
+                _Pragma("unroll") for (int m_ = 0; m_ < 4; m_++) {                            \
+                    const int ch_ = ((4 * m_) ^ xsw) * 16;                                    \
+                    b0m_[m_] = *reinterpret_cast<const v8i_t *>(base + ch_);                  \
+                    b1m_[m_] = *reinterpret_cast<const v8i_t *>(base + 32 * SL_ROW + ch_);    \
+                }                                                                             \
+                _Pragma("unroll") for (int m_ = 0; m_ < 4; m_++) {                            \
+                    v8i_t a_;                                                                 \
+                    __builtin_memcpy(&a_, &aF[2 * m_], 32);                                   \
+                    C0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a_, b0m_[m_], m_ == 0 ? zero16 : C0, 0, 0, 0, 127, 0, 127); \
+                    C1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a_, b1m_[m_], m_ == 0 ? zero16 : C1, 0, 0, 0, 127, 0, 127); \
+                }                                                                             \
+            }                                                                                 \
+        } else if (!AP_EXP_NOMFMA) {                                                          \
             /* fragment reads run PF k16 steps ahead of the MFMAs (counted lgkm waits) */      \
             constexpr int PF = 4;                                                             \
             f16x8 b0_[BK / 16], b1_[BK / 16];                                                 \
