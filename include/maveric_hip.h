@@ -7,9 +7,19 @@
  *      context (device 0) with host pointers, synchronously.
  *   2. This header: an explicit context, a stream, and BATCHED entry points
  *      over device pointers for throughput mode (many independent frame-pairs
- *      per launch).  All *_dev functions are stream-ordered and asynchronous;
- *      they never allocate once mv_context_reserve() has covered the sizes, so
- *      they can be captured in a hipGraph.
+ *      per launch).  All *_dev functions are stream-ordered and asynchronous.
+ *      The all-pairs match (fp32, int8) and pose *_dev calls never allocate
+ *      once mv_context_reserve() has covered (batch, cap), so they can be
+ *      captured in a hipGraph; the window, keypoint and two-way calls size
+ *      their scratch on first use: run each once at its largest shape before
+ *      capturing it.
+ *
+ * Threading: a mv_context is NOT thread-safe -- give each host thread its own
+ * (or serialise the calls).  The default context behind the reference's API
+ * is per thread: every thread that calls compute_top_N, ransac_essential_matrix,
+ * track(), ... gets its own context (device 0, own stream and buffers), created
+ * on first use and destroyed when that thread exits.  mv_last_status() is
+ * per thread as well.
  *
  * Conventions: plain C types only; every function returns an mv_status
  * (0 = success, negative = error) unless documented otherwise; nothing ever
@@ -59,7 +69,7 @@ void *mv_context_stream(mv_context *ctx);
 int mv_context_synchronize(mv_context *ctx);
 /* Pre-size scratch for up to `batch` pairs of `cap` keypoints / cells. */
 int mv_context_reserve(mv_context *ctx, int batch, int cap);
-mv_context *mv_default_context(void); /* NULL (and a stderr message) without a device */
+mv_context *mv_default_context(void); /* the calling thread's; NULL (stderr once) without a device */
 
 /* Kernel profiler: while enabled, every kernel launch is bracketed by two
  * hipEvents recorded on its own stream (no synchronisation is added).

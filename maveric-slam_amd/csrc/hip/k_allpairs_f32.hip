@@ -844,6 +844,7 @@ void *ap_scratch(mv_context *ctx, size_t bytes) {
         (void)hipFree(ctx->ap_scratch);
         ctx->ap_scratch = nullptr;
         ctx->ap_scratch_bytes = 0;
+        ctx->prep_desc1 = nullptr;  // a prepared frame 1 lived in the freed buffer
     }
     const size_t b = mv::align_up(bytes, 1 << 20);
     if (hipMalloc(&ctx->ap_scratch, b) != hipSuccess) {

@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256) void k_pose_as_built(int cap, const int *__res
                                                        int *__restrict__ num_inliers, int *__restrict__ status) {
     __shared__ int wsum[4];
     const int b = blockIdx.x;
-    const int n = nv[b];
+    const int n = min(max(nv[b], 0), cap);  // as every batched kernel: never past the pair's slot
     const Mat3 E = identity3();
     const int per = (n + 255) / 256;
     const int i0 = threadIdx.x * per, i1 = min(i0 + per, n);
@@ -138,7 +138,7 @@ __global__ __launch_bounds__(256) void k_pose_as_built(int cap, const int *__res
         float x1 = pts0[((size_t)b * cap + i) * 2], y1 = pts0[((size_t)b * cap + i) * 2 + 1], x2, y2;
         if (match_idx) {
             const int j = match_idx[(size_t)b * cap + i];
-            if (j < 0) continue;
+            if ((unsigned)j >= (unsigned)cap) continue;  // -1 or out of range: no match
             x2 = kp1[((size_t)b * cap + j) * 2];
             y2 = kp1[((size_t)b * cap + j) * 2 + 1];
         } else {

@@ -326,14 +326,16 @@ __global__ __launch_bounds__(NT) void k_pose_ransac(PoseArgs a, const int *__res
     __shared__ float s_E[9];
     __shared__ double s_pose[12];  // R (9) + t (3)
     const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int n_in = min(nv[b], a.cap);
+    const int n_in = min(max(nv[b], 0), a.cap);
     const long long tk0 = PE_TRACE ? clock64() : 0;
 
     // ---- 1. compaction (query order) + normalisation ----
     const int per = (n_in + NT - 1) / NT;
     const int i0 = t * per, i1 = min(i0 + per, n_in);
     int cnt = 0;
-    for (int i = i0; i < i1; i++) cnt += (!match_idx || match_idx[(size_t)b * a.cap + i] >= 0) ? 1 : 0;
+    // a match index outside [0, cap) is "no match" (never dereferenced)
+    for (int i = i0; i < i1; i++)
+        cnt += (!match_idx || (unsigned)match_idx[(size_t)b * a.cap + i] < (unsigned)a.cap) ? 1 : 0;
     int x = cnt;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -350,7 +352,7 @@ __global__ __launch_bounds__(NT) void k_pose_ransac(PoseArgs a, const int *__res
         float x1 = pts0[((size_t)b * a.cap + i) * 2], y1 = pts0[((size_t)b * a.cap + i) * 2 + 1], x2, y2;
         if (match_idx) {
             const int j = match_idx[(size_t)b * a.cap + i];
-            if (j < 0) continue;
+            if ((unsigned)j >= (unsigned)a.cap) continue;
             x2 = kp1[((size_t)b * a.cap + j) * 2];
             y2 = kp1[((size_t)b * a.cap + j) * 2 + 1];
         } else {

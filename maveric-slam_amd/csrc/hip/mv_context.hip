@@ -9,22 +9,16 @@
 namespace {
 thread_local int g_last_status = MV_OK;
 thread_local char g_last_msg[512] = "";
-pthread_once_t g_default_once = PTHREAD_ONCE_INIT;
-mv_context *g_default = nullptr;
+// The default context is PER THREAD (the drop-in entry points keep the reference's
+// single-threaded signatures, so the context is implicit): each host thread gets its own
+// stream, staging and scratch, created on first use and destroyed when the thread exits
+// (the main thread's lives until process exit).
+pthread_once_t g_key_once = PTHREAD_ONCE_INIT;
+pthread_key_t g_ctx_key;
+bool g_no_device_reported = false;
 
-void create_default() {
-    int n = mv_device_count();
-    if (n <= 0) {
-        fprintf(stderr,
-                "maveric_hip: no HIP device visible -- this library has no CPU fallback "
-                "(hipGetDeviceCount = %d)\n", n);
-        return;
-    }
-    if (mv_context_create(0, &g_default) != MV_OK) {
-        fprintf(stderr, "maveric_hip: cannot create the default context: %s\n", g_last_msg);
-        g_default = nullptr;
-    }
-}
+void destroy_thread_context(void *p) { (void)mv_context_destroy(static_cast<mv_context *>(p)); }
+void make_key() { (void)pthread_key_create(&g_ctx_key, destroy_thread_context); }
 }  // namespace
 
 namespace mv {
@@ -45,7 +39,7 @@ int set_status(int status) {
 void *scratch(mv_context *ctx, size_t bytes) {
     if (bytes <= ctx->scratch_bytes) return ctx->scratch;
     if (ctx->scratch) {
-        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipDeviceSynchronize();  // the old buffer may be in use on any stream the context used
         (void)hipFree(ctx->scratch);
         ctx->scratch = nullptr;
         ctx->scratch_bytes = 0;
@@ -63,7 +57,7 @@ void *scratch(mv_context *ctx, size_t bytes) {
 void *stage(mv_context *ctx, size_t bytes) {
     if (bytes <= ctx->stage_bytes) return ctx->stage_dev;
     if (ctx->stage_dev) {
-        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipDeviceSynchronize();
         (void)hipFree(ctx->stage_dev);
         ctx->stage_dev = nullptr;
         ctx->stage_bytes = 0;
@@ -176,6 +170,7 @@ int mv_context_reserve(mv_context *ctx, int batch, int cap) {
             ctx->ap_scratch = nullptr;
             ctx->ap_scratch_bytes = 0;
         }
+        ctx->prep_desc1 = nullptr;  // a prepared frame 1 lived in the freed buffer
         const size_t ab = mv::align_up(mv::allpairs_f32_scratch_bytes(batch, cap), 1 << 20);
         if (hipMalloc(&ctx->ap_scratch, ab) != hipSuccess) return MV_ERR_OUT_OF_MEMORY;
         ctx->ap_scratch_bytes = ab;
@@ -189,9 +184,28 @@ int mv_context_reserve(mv_context *ctx, int batch, int cap) {
 }
 
 mv_context *mv_default_context(void) {
-    pthread_once(&g_default_once, create_default);
-    if (g_default) (void)hipSetDevice(g_default->device);
-    return g_default;
+    pthread_once(&g_key_once, make_key);
+    mv_context *c = static_cast<mv_context *>(pthread_getspecific(g_ctx_key));
+    if (c) {
+        (void)hipSetDevice(c->device);
+        return c;
+    }
+    const int n = mv_device_count();
+    if (n <= 0) {
+        if (!g_no_device_reported)
+            fprintf(stderr,
+                    "maveric_hip: no HIP device visible -- this library has no CPU fallback "
+                    "(hipGetDeviceCount = %d)\n", n);
+        g_no_device_reported = true;
+        mv::set_error(MV_ERR_NO_DEVICE, "no HIP device visible");
+        return nullptr;
+    }
+    if (mv_context_create(0, &c) != MV_OK) {
+        fprintf(stderr, "maveric_hip: cannot create the default context: %s\n", g_last_msg);
+        return nullptr;
+    }
+    (void)pthread_setspecific(g_ctx_key, c);
+    return c;
 }
 
 }  // extern "C"

@@ -194,3 +194,47 @@ def test_as_built_batched_pose_matches_stub(ctx, orc, torch_cuda):
         assert ni[b] == max(ni2, 0)
         assert (bits(T[b, :, :3]) == bits(exp["pose_built_R1"])).all()
         assert (bits(T[b, :, 3]) == bits(exp["pose_built_t"])).all()
+
+
+@pytest.mark.parametrize("semantics", ["built", "intended"])
+def test_pose_clamps_counts_and_match_indices(ctx, torch_cuda, semantics):
+    """n[b] > cap behaves as n[b] = cap (the pair's slot is never overrun, the last pair's
+    included) and match indices outside [0, cap) count as "no match" in both pose kernels."""
+    import mvtrack
+
+    torch = torch_cuda
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(11)
+    B, cap = 3, 64
+    sem = mvtrack.AS_BUILT if semantics == "built" else mvtrack.AS_INTENDED
+    prm = mvtrack.pose_params(sem)
+    P0 = rng.uniform(0, 640, (B, cap, 2)).astype(np.float32)
+    P1 = (P0 + rng.normal(0, 0.8, (B, cap, 2))).astype(np.float32)
+    T1, ni1, st1 = _pose_batch(ctx, torch, prm, P0, P1, np.array([cap + 50, cap, 1 << 20], np.int32))
+    T2, ni2, st2 = _pose_batch(ctx, torch, prm, P0, P1, np.full(B, cap, np.int32))
+    assert (bits(T1) == bits(T2)).all() and (ni1 == ni2).all() and (st1 == st2).all()
+
+    # pose from matches: out-of-range indices are dropped exactly like -1
+    idx = np.tile(np.arange(cap, dtype=np.int32), (B, 1))
+    bad = idx.copy()
+    bad[:, ::5] = cap + 7
+    bad[:, 1::7] = -9
+    good = idx.copy()
+    good[bad != idx] = -1
+
+    def run(mi):
+        T = torch.zeros((B, 3, 4), dtype=torch.float32, device=dev)
+        nm = torch.zeros(B, dtype=torch.int32, device=dev)
+        ni = torch.zeros(B, dtype=torch.int32, device=dev)
+        st = torch.full((B,), 99, dtype=torch.int32, device=dev)
+        ctx.set_stream(torch.cuda.current_stream())
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+        ctx.pose_from_matches(prm, t(np.full(B, cap, np.int32)), t(mi), t(P0), t(P1), T, nm, ni, st)
+        torch.cuda.synchronize()
+        ctx.set_stream(None)
+        return T.cpu().numpy(), nm.cpu().numpy(), ni.cpu().numpy(), st.cpu().numpy()
+
+    a, b = run(bad), run(good)
+    assert (a[1] == (good >= 0).sum(1)).all()
+    for x, y in zip(a, b):
+        assert (np.ascontiguousarray(x).view(np.int32) == np.ascontiguousarray(y).view(np.int32)).all()

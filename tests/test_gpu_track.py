@@ -78,3 +78,46 @@ def test_track_null_last_frame_is_identity(ctx):
     T = (ctypes.c_float * 12)()
     assert L.track(None, None, 4, 4, 9, ctypes.c_float(0.9), T) == 0
     assert np.allclose(np.array(T).reshape(3, 4), np.hstack([np.eye(3), np.zeros((3, 1))]))
+
+
+def test_dropin_threads_get_their_own_default_context(ctx, orc, image0):
+    """The reference's API runs on an implicit context; it is per thread, so concurrent
+    callers never share staging or scratch.  Four threads run track() and the
+    host window match on different pairs at once; every result equals the serial one."""
+    import threading
+
+    import mvtrack
+
+    L = mvtrack.lib()
+    L.mv_default_context.restype = ctypes.c_void_p
+    pairs = [(image0, image0)] + [synth.synth_window_pair(k) for k in (1, 2, 3)]
+    keep = []
+    frames = [(make_frame(a, keep), make_frame(b, keep)) for a, b in pairs]
+
+    def run_track(k):
+        T = (ctypes.c_float * 12)()
+        st = L.track(ctypes.byref(frames[k][0]), ctypes.byref(frames[k][1]), 4, 4, 9, ctypes.c_float(0.9), T)
+        return st, bits(np.array(T, np.float32))
+
+    serial = [run_track(k) for k in range(4)]
+    out, ctxs, errs = {}, {}, []
+    alive = threading.Barrier(4, timeout=120)  # all four contexts exist at once
+
+    def worker(k):
+        try:
+            ctxs[k] = L.mv_default_context()
+            for rep in range(5):
+                out[(k, rep)] = run_track(k)
+            alive.wait()
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not errs, errs
+    assert len(set(ctxs.values())) == 4 and L.mv_default_context() not in ctxs.values()
+    for (k, rep), (st, T) in out.items():
+        assert st == serial[k][0] and (T == serial[k][1]).all(), (k, rep)
