@@ -137,6 +137,14 @@ float mv_scale_as_built(float scale); /* low 32 bits of (double)scale, SURVEY F7
  * (pairwise_pnp.py:649-657), so without a score output the exact re-score runs
  * only where the rounding window does not already decide the row; match_idx is
  * identical either way. */
+/* How the all-pairs fp32 match screens its candidates before the exact fp32 re-score (the
+ * outputs are bit-identical either way): MV_SCREEN_I8 (default) quantises both frames per row
+ * to int8 and screens on the int8 matrix cores with a rigorous quantisation window;
+ * MV_SCREEN_F16 screens on fp16 MFMAs (2^14-scaled operands).  The environment variable
+ * MV_AP_SCREEN=f16 selects the fp16 screen for contexts created afterwards. */
+typedef enum { MV_SCREEN_I8 = 0, MV_SCREEN_F16 = 1 } mv_allpairs_screen;
+int mv_context_set_allpairs_screen(mv_context *ctx, int screen);
+int mv_context_allpairs_screen(mv_context *ctx);
 int mv_match_allpairs_f32_dev(mv_context *ctx, int batch, int cap, const int *n0, const int *n1,
                               const float *desc0, const float *desc1, double thresh, int *match_idx,
                               float *match_score);

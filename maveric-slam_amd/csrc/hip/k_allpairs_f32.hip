@@ -647,8 +647,15 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
         const double Ms = (double)M * 3.725290298461914e-09;  // screen / 2^28
         const double M2s = (double)M2 * 3.725290298461914e-09;
         const double dp = delta + 2.2 * rho * (fabs(Ms) + 2.0 * delta);
-        if (Ms + dp > thresh) {
-            if (M2s < Ms - 2.0 * dp - tie) {
+        // competitors: columns whose exact score can reach the maximiser's; for the distance
+        // (dmode 1) also every column that can clip to 1 with it (distance-0 ties), and a
+        // maximiser that can clip to -1 ties every column (all distances 2)
+        const double lo = dmode ? fmin(Ms - 2.0 * dp, 1.0 - dp) - tie : Ms - 2.0 * dp;
+        if (dmode && Ms - dp <= -1.0 + tie) {
+            wide = true;
+            if (fh == 0) lmask[rl] = 0xffffffffu;
+        } else if (Ms + dp > thresh) {
+            if (M2s < lo) {
                 const unsigned tg = __float_as_uint(M) & ~tkeep;
                 const int I = (int)(tg >> 1) * BN + (int)(tg & 1) * 32 + E;
                 if (I >= n1) {  // cannot happen for a tagged in-range maximum; never read past n1
@@ -664,7 +671,7 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
                     bj = I;
                 }
             } else {  // both lanes of the row take this branch
-                const double lim = (Ms - 2.0 * dp - tie) * 268435456.0;
+                const double lim = lo * 268435456.0;
                 // padding columns (past n1: the last tile's -3e38) are never candidates; a
                 // padding entry's m2 can only be padding too
                 const float pad_hi = -1.0e38f;
@@ -776,10 +783,12 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
 
 namespace mv {
 
-// scratch: h1 (batch * cap * 512 B) | nrm1 (batch * cap f32) | bad (batch i32)
+// scratch: h1 (batch * cap * 512 B) | nrm1 (batch * cap f32) | bad (batch i32); the int8
+// screen's layout (k_allpairs_q8.hip) shares the buffer: the size covers both
 size_t allpairs_f32_scratch_bytes(int batch, int cap) {
     const size_t rows = (size_t)batch * cap;
-    return rows * ROW_BYTES + align_up(rows * 4, 256) + align_up((size_t)batch * 4, 256);
+    const size_t f16 = rows * ROW_BYTES + align_up(rows * 4, 256) + align_up((size_t)batch * 4, 256);
+    return std::max(f16, allpairs_q8_scratch_bytes(batch, cap));
 }
 
 namespace {
@@ -857,6 +866,22 @@ void *ap_scratch(mv_context *ctx, size_t bytes) {
 }
 }  // namespace
 
+namespace {
+int ap_prepare(int screen, hipStream_t s, void *scr, int batch, int cap, const int *n1, const float *desc1) {
+    return screen == MV_SCREEN_F16 ? mv::launch_allpairs_f32_prepare(s, scr, batch, cap, n1, desc1)
+                                   : mv::launch_allpairs_q8_prepare(s, scr, batch, cap, n1, desc1);
+}
+int ap_match(int screen, hipStream_t s, void *scr, int batch, int cap, const int *n0, const int *n1,
+             const float *desc0, const float *desc1, double thresh, int *match_idx, float *match_score,
+             int dmode = 0) {
+    return screen == MV_SCREEN_F16
+               ? mv::launch_allpairs_f32_match(s, scr, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
+                                               match_score, dmode)
+               : mv::launch_allpairs_q8_match(s, scr, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
+                                              match_score, dmode);
+}
+}  // namespace
+
 extern "C" int mv_match_allpairs_f32_dev(mv_context *ctx, int batch, int cap, const int *n0, const int *n1,
                                          const float *desc0, const float *desc1, double thresh, int *match_idx,
                                          float *match_score) {
@@ -865,10 +890,10 @@ extern "C" int mv_match_allpairs_f32_dev(mv_context *ctx, int batch, int cap, co
     void *scr = ap_scratch(ctx, mv::allpairs_f32_scratch_bytes(batch, cap));
     if (!scr) return MV_ERR_OUT_OF_MEMORY;
     ctx->prep_desc1 = nullptr;  // the prepared image is overwritten
-    const int st = mv::launch_allpairs_f32_prepare(ctx->stream, scr, batch, cap, n1, desc1);
+    const int st = ap_prepare(ctx->ap_screen, ctx->stream, scr, batch, cap, n1, desc1);
     if (st != MV_OK) return st;
-    return mv::launch_allpairs_f32_match(ctx->stream, scr, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
-                                         match_score);
+    return ap_match(ctx->ap_screen, ctx->stream, scr, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
+                    match_score);
 }
 
 extern "C" int mv_match_allpairs_f32_prepare_dev(mv_context *ctx, int batch, int cap, const int *n1,
@@ -893,9 +918,10 @@ extern "C" int mv_match_allpairs_f32_prepare_dev(mv_context *ctx, int batch, int
     // inputs (and the previous run's use of the scratch) as of this call on the context stream
     MV_HIP_TRY(hipEventRecord(ctx->ev_in, ctx->stream));
     MV_HIP_TRY(hipStreamWaitEvent(ctx->aux_stream, ctx->ev_in, 0));
-    const int st = mv::launch_allpairs_f32_prepare(ctx->aux_stream, scr, batch, cap, n1, desc1);
+    const int st = ap_prepare(ctx->ap_screen, ctx->aux_stream, scr, batch, cap, n1, desc1);
     if (st != MV_OK) return st;
     MV_HIP_TRY(hipEventRecord(ctx->ev_prep, ctx->aux_stream));
+    ctx->prep_screen = ctx->ap_screen;
     ctx->prep_batch = batch;
     ctx->prep_cap = cap;
     ctx->prep_n1 = n1;
@@ -908,14 +934,14 @@ extern "C" int mv_match_allpairs_f32_run_dev(mv_context *ctx, int batch, int cap
                                              float *match_score) {
     MV_REQUIRE(ctx != nullptr);
     if (!ctx->prep_desc1 || ctx->prep_batch != batch || ctx->prep_cap != cap || ctx->prep_n1 != n1 ||
-        ctx->prep_desc1 != desc1) {
+        ctx->prep_desc1 != desc1 || ctx->prep_screen != ctx->ap_screen) {
         mv::set_error(MV_ERR_INVALID_ARG, "mv_match_allpairs_f32_run_dev: no matching prepare for this batch");
         return MV_ERR_INVALID_ARG;
     }
     MV_HIP_TRY(hipSetDevice(ctx->device));
     MV_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_prep, 0));
-    return mv::launch_allpairs_f32_match(ctx->stream, ctx->ap_scratch, batch, cap, n0, n1, desc0, desc1, thresh,
-                                         match_idx, match_score);
+    return ap_match(ctx->ap_screen, ctx->stream, ctx->ap_scratch, batch, cap, n0, n1, desc0, desc1, thresh,
+                    match_idx, match_score);
 }
 
 namespace {
@@ -956,13 +982,12 @@ extern "C" int mv_match_two_way_f32_dev(mv_context *ctx, int batch, int cap, con
     float *fdist = match_dist ? match_dist : (float *)(tmp + nb);
     hipStream_t s = ctx->stream;
     // forward: rows of frame 0 against frame 1 (argmin distance + its exact distance)
-    int st = mv::launch_allpairs_f32_prepare(s, scr, batch, cap, n1, desc1);
-    if (st == MV_OK)
-        st = mv::launch_allpairs_f32_match(s, scr, batch, cap, n0, n1, desc0, desc1, 0.0, match_idx, fdist, 1);
+    const int sc = ctx->ap_screen;
+    int st = ap_prepare(sc, s, scr, batch, cap, n1, desc1);
+    if (st == MV_OK) st = ap_match(sc, s, scr, batch, cap, n0, n1, desc0, desc1, 0.0, match_idx, fdist, 1);
     // reverse: rows of frame 1 against frame 0 (indices only)
-    if (st == MV_OK) st = mv::launch_allpairs_f32_prepare(s, scr, batch, cap, n0, desc0);
-    if (st == MV_OK)
-        st = mv::launch_allpairs_f32_match(s, scr, batch, cap, n1, n0, desc1, desc0, 0.0, ridx, nullptr, 1);
+    if (st == MV_OK) st = ap_prepare(sc, s, scr, batch, cap, n0, desc0);
+    if (st == MV_OK) st = ap_match(sc, s, scr, batch, cap, n1, n0, desc1, desc0, 0.0, ridx, nullptr, 1);
     if (st != MV_OK) return st;
     const long total = (long)batch * cap;
     hipLaunchKernelGGL(k_two_way_keep, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, total, cap, n0, n1,

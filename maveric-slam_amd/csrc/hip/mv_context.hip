@@ -2,6 +2,7 @@
 #include <pthread.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "mv_internal.hpp"
@@ -125,6 +126,8 @@ int mv_context_create(int device, mv_context **out) {
         return MV_ERR_HIP;
     }
     c->stream = c->own_stream;
+    const char *scr = getenv("MV_AP_SCREEN");
+    c->ap_screen = (scr && strcmp(scr, "f16") == 0) ? MV_SCREEN_F16 : MV_SCREEN_I8;
     *out = c;
     return mv::set_status(MV_OK);
 }
@@ -160,6 +163,14 @@ int mv_context_synchronize(mv_context *ctx) {
     MV_HIP_TRY(hipStreamSynchronize(ctx->stream));
     return MV_OK;
 }
+
+int mv_context_set_allpairs_screen(mv_context *ctx, int screen) {
+    MV_REQUIRE(ctx != nullptr && (screen == MV_SCREEN_I8 || screen == MV_SCREEN_F16));
+    ctx->ap_screen = screen;
+    return MV_OK;
+}
+
+int mv_context_allpairs_screen(mv_context *ctx) { return ctx ? ctx->ap_screen : MV_ERR_INVALID_ARG; }
 
 int mv_context_reserve(mv_context *ctx, int batch, int cap) {
     MV_REQUIRE(ctx != nullptr && batch > 0 && cap > 0);

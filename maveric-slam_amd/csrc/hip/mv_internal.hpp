@@ -24,6 +24,8 @@ struct mv_context {
     int prep_batch, prep_cap;  // what the last prepare staged (run checks it)
     const int *prep_n1;
     const float *prep_desc1;
+    int prep_screen;
+    int ap_screen;  // mv_allpairs_screen of the fp32 all-pairs match (0 = int8, the default)
 };
 
 namespace mv {
@@ -89,6 +91,12 @@ int launch_allpairs_f32_prepare(hipStream_t s, void *scratch, int batch, int cap
 int launch_allpairs_f32_match(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
                               const float *desc0, const float *desc1, double thresh, int *match_idx,
                               float *match_score, int dmode = 0);
+size_t allpairs_q8_scratch_bytes(int batch, int cap);
+int launch_allpairs_q8_prepare(hipStream_t s, void *scratch, int batch, int cap, const int *n1,
+                               const float *desc1);
+int launch_allpairs_q8_match(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
+                             const float *desc0, const float *desc1, double thresh, int *match_idx,
+                             float *match_score, int dmode = 0);
 size_t allpairs_i8_scratch_bytes(int batch, int cap);
 int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
                        const int8_t *desc0, const int8_t *desc1, int *match_idx, int *match_dot);

@@ -34,6 +34,9 @@ _F = ctypes.c_float
 _D = ctypes.c_double
 
 
+SCREENS = {"i8": 0, "f16": 1}  # mv_allpairs_screen
+
+
 class MVError(RuntimeError):
     pass
 
@@ -90,6 +93,8 @@ def lib():
             "mv_context_create": (_I, [_I, ctypes.POINTER(_P)]),
             "mv_context_destroy": (_I, [_P]),
             "mv_context_set_stream": (_I, [_P, _P]),
+            "mv_context_set_allpairs_screen": (_I, [_P, _I]),
+            "mv_context_allpairs_screen": (_I, [_P]),
             "mv_context_stream": (_P, [_P]),
             "mv_context_synchronize": (_I, [_P]),
             "mv_context_reserve": (_I, [_P, _I, _I]),
@@ -292,6 +297,13 @@ class Context:
     def set_stream(self, stream):
         ptr = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
         check(lib().mv_context_set_stream(self.h, ptr), "set_stream")
+
+    def set_allpairs_screen(self, screen):
+        """'i8' (default) or 'f16': how the fp32 all-pairs match screens before its exact re-score."""
+        check(lib().mv_context_set_allpairs_screen(self.h, SCREENS[screen]), "set_allpairs_screen")
+
+    def allpairs_screen(self):
+        return {v: k for k, v in SCREENS.items()}[lib().mv_context_allpairs_screen(self.h)]
 
     def synchronize(self):
         check(lib().mv_context_synchronize(self.h), "synchronize")

@@ -45,6 +45,14 @@ def ctx():
     c.close()
 
 
+@pytest.fixture(params=["i8", "f16"])
+def screen(request, ctx):
+    """both fp32 screens (int8 MFMA, the default, and fp16 MFMA) must give identical outputs"""
+    ctx.set_allpairs_screen(request.param)
+    yield request.param
+    ctx.set_allpairs_screen("i8")
+
+
 @pytest.fixture(scope="session")
 def torch_cuda():
     import torch

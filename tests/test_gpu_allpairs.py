@@ -42,7 +42,7 @@ def run_f32(ctx, torch, pairs, cap=None, thresh=0.8, scores=True):
 
 
 @pytest.mark.parametrize("name", ["pair0", "pair10"])
-def test_allpairs_f32_reference_fixtures(ctx, orc, torch_cuda, name):
+def test_allpairs_f32_reference_fixtures(ctx, screen, orc, torch_cuda, name):
     d = load_golden("tracking_%s.npz" % name)
     exp = load_golden("expected_outputs.npz")
     idx, sc = run_f32(ctx, torch_cuda, [(d["image0_desc"], d["image1_desc"])])
@@ -52,7 +52,7 @@ def test_allpairs_f32_reference_fixtures(ctx, orc, torch_cuda, name):
     assert (idx[0, n0:] == -1).all()
 
 
-def test_allpairs_f32_full_size_synthetic(ctx, orc, torch_cuda):
+def test_allpairs_f32_full_size_synthetic(ctx, screen, orc, torch_cuda):
     """BASELINE config 2: 1024 x 1024 x 256 fp32, checked against the oracle on 2 pairs."""
     pairs = []
     for s in range(2):
@@ -65,7 +65,7 @@ def test_allpairs_f32_full_size_synthetic(ctx, orc, torch_cuda):
         assert (i2 >= 0).sum() > 500
 
 
-def test_allpairs_f32_ragged_batch(ctx, orc, torch_cuda):
+def test_allpairs_f32_ragged_batch(ctx, screen, orc, torch_cuda):
     rng = np.random.default_rng(4)
     shapes = [(1, 1), (1, 300), (129, 1), (127, 129), (300, 257), (0, 40), (40, 0), (511, 513), (128, 128)]
     pairs = []
@@ -83,7 +83,7 @@ def test_allpairs_f32_ragged_batch(ctx, orc, torch_cuda):
         assert (idx[b, :a.shape[0]] == i2).all() and (bits(sc[b, :a.shape[0]]) == bits(s2)).all()
 
 
-def test_allpairs_f32_ties_and_near_ties(ctx, orc, torch_cuda):
+def test_allpairs_f32_ties_and_near_ties(ctx, screen, orc, torch_cuda):
     """duplicate and rounding-level-perturbed columns force the exact re-score / ambiguous-tile path."""
     rng = np.random.default_rng(8)
     a = rng.standard_normal((300, 256)).astype(np.float32)
@@ -99,7 +99,7 @@ def test_allpairs_f32_ties_and_near_ties(ctx, orc, torch_cuda):
     assert (idx[0, :300] == i2).all() and (bits(sc[0, :300]) == bits(s2)).all()
 
 
-def test_allpairs_f32_threshold_edges(ctx, orc, torch_cuda):
+def test_allpairs_f32_threshold_edges(ctx, screen, orc, torch_cuda):
     rng = np.random.default_rng(2)
     a = rng.standard_normal((64, 256)).astype(np.float32)
     a /= np.linalg.norm(a, axis=1, keepdims=True)
@@ -110,7 +110,7 @@ def test_allpairs_f32_threshold_edges(ctx, orc, torch_cuda):
         assert (idx[0, :64] == i2).all() and (bits(sc[0, :64]) == bits(s2)).all()
 
 
-def test_allpairs_f32_out_of_screen_range(ctx, orc, torch_cuda):
+def test_allpairs_f32_out_of_screen_range(ctx, screen, orc, torch_cuda):
     """The fp16 screen only takes |x| < 2: unnormalised, huge, tiny, NaN and mixed-scale
     descriptors must still give the reference's answer (flagged pairs / wide windows route
     rows through the exact re-score)."""
@@ -135,7 +135,7 @@ def test_allpairs_f32_out_of_screen_range(ctx, orc, torch_cuda):
             assert (bits(sc[k, :a.shape[0]]) == bits(s2)).all(), k
 
 
-def test_allpairs_f32_indices_only(ctx, orc, torch_cuda):
+def test_allpairs_f32_indices_only(ctx, screen, orc, torch_cuda):
     """match_score = NULL (what pairwise_pnp.py:639-659 keeps: the matched pairs, not the
     score): the exact re-score is skipped where the window already decides, and the indices
     must still equal the oracle's on every hard case -- full size, ties and near-ties,
@@ -168,7 +168,7 @@ def test_allpairs_f32_indices_only(ctx, orc, torch_cuda):
             assert (idx[k, x.shape[0]:] == -1).all()
 
 
-def test_allpairs_f32_prepare_run_pipeline(ctx, orc, torch_cuda):
+def test_allpairs_f32_prepare_run_pipeline(ctx, screen, orc, torch_cuda):
     """prepare(next) issued between run(this) and the next run: identical to the one-call API;
     run without its prepare is refused."""
     torch = torch_cuda
@@ -278,3 +278,55 @@ def test_allpairs_i8_ties_and_near_ties(ctx, orc, torch_cuda):
         i2, d2 = orc.allpairs_i8(a, c)
         assert (idx[q, :a.shape[0]] == i2).all() and (dot[q, :a.shape[0]] == d2).all()
         assert i2[5] == -1 and (i2 >= 0).sum() > a.shape[0] // 8
+
+
+def test_allpairs_f32_quantisation_stress(ctx, screen, orc, torch_cuda):
+    """Inputs aimed at the int8 screen's window (k_allpairs_q8.hip): rows of every scale up to
+    the 2^+-40 range limits and past them (exact path), spiky rows (one component carries the
+    norm: the rest quantise to 0), sparse and zero rows on both sides, anti-correlated rows
+    (every dot negative), and near-ties closer than one quantisation step."""
+    rng = np.random.default_rng(31)
+    n = 160
+
+    def unit(k):
+        x = rng.standard_normal((k, 256)).astype(np.float32)
+        return x / np.linalg.norm(x, axis=1, keepdims=True)
+
+    a = unit(n)
+    b = a[rng.permutation(n)] + 0.03 * rng.standard_normal((n, 256)).astype(np.float32)
+    b /= np.linalg.norm(b, axis=1, keepdims=True)
+    scales = np.float32(2.0) ** rng.integers(-45, 46, n).astype(np.float32)
+    a_s = (a * scales[:, None]).astype(np.float32)
+    b_s = (b * np.float32(2.0) ** rng.integers(-39, 40, n).astype(np.float32)[:, None]).astype(np.float32)
+    spiky = a.copy()
+    spiky[:40] *= np.float32(1e-4)
+    spiky[:40, 3] = 1.0
+    sparse = a.copy()
+    sparse[40:80, 16:] = 0.0
+    sparse[80:84] = 0.0  # zero query rows
+    bz = b.copy()
+    bz[10:14] = 0.0  # zero columns
+    near = a.copy()
+    near2 = np.concatenate([a, a + np.float32(1e-4) * unit(n)]).astype(np.float32)  # near-ties per row
+    pairs = [(a_s, b), (a, b_s), (spiky, b), (sparse, bz), (-a, b), (near, near2),
+             (a, np.concatenate([b, -b]))]
+    for thr in (0.8, 0.0, -1.0):
+        for scores in (True, False):
+            idx, sc = run_f32(ctx, torch_cuda, pairs, thresh=thr, scores=scores)
+            for k, (x, y) in enumerate(pairs):
+                i2, s2 = orc.allpairs_f32(x, y, thr)
+                assert (idx[k, :x.shape[0]] == i2).all(), (thr, k)
+                if scores:
+                    assert (bits(sc[k, :x.shape[0]]) == bits(s2)).all(), (thr, k)
+
+
+def test_allpairs_screen_selection(ctx):
+    import mvtrack
+
+    c = mvtrack.Context(0)
+    assert c.allpairs_screen() == "i8"  # the default
+    c.set_allpairs_screen("f16")
+    assert c.allpairs_screen() == "f16"
+    with pytest.raises(RuntimeError):
+        mvtrack.check(mvtrack.lib().mv_context_set_allpairs_screen(c.h, 7), "bad screen")
+    c.close()

@@ -72,7 +72,7 @@ def _gpu(ctx, torch, pairs, th, cap=None, dist=True):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("th", fx.THRESHOLDS)
-def test_gpu_two_way_fixtures(ctx, orc, torch_cuda, th):
+def test_gpu_two_way_fixtures(ctx, screen, orc, torch_cuda, th):
     inp = fx.inputs()
     names = ["pair0", "pair10", "synth0", "synth1"]
     for dist in (True, False):
@@ -88,7 +88,7 @@ def test_gpu_two_way_fixtures(ctx, orc, torch_cuda, th):
 
 
 @pytest.mark.gpu
-def test_gpu_two_way_hard_cases(ctx, orc, torch_cuda):
+def test_gpu_two_way_hard_cases(ctx, screen, orc, torch_cuda):
     """duplicated columns and rows (distance ties: first index wins both ways), dots above 1
     (clipped: distance 0 ties), a NaN column (flagged pair: np.argmin picks the first NaN),
     ragged and empty pairs, a 1024 x 1024 full-size pair."""
@@ -115,3 +115,21 @@ def test_gpu_two_way_hard_cases(ctx, orc, torch_cuda):
             assert (idx[k, :x.shape[0]] == i2).all(), (th, k)
             assert (dd[k, :x.shape[0]].view(np.int32) == d2.view(np.int32)).all(), (th, k)
             assert (idx[k, x.shape[0]:] == -1).all()
+
+
+@pytest.mark.gpu
+def test_gpu_two_way_clipped_far_above_one(ctx, screen, orc, torch_cuda):
+    """Unnormalised descriptors whose dots exceed 1 by far more than the screen window: every
+    such column clips to distance 0, so np.argmin takes the FIRST of them, not the largest dot."""
+    rng = np.random.default_rng(12)
+    a = rng.standard_normal((120, 256)).astype(np.float32)
+    a /= np.linalg.norm(a, axis=1, keepdims=True)
+    b = np.concatenate([a[rng.permutation(120)] * np.float32(1.3), a[:60] * np.float32(1.7),
+                        a[60:] * np.float32(0.999)]).astype(np.float32)
+    b = b[rng.permutation(b.shape[0])]
+    for th in (0.7, 2.0):
+        idx, dd = _gpu(ctx, torch_cuda, [(a, b), (b[:100], a)], th, cap=256)
+        for k, (x, y) in enumerate([(a, b), (b[:100], a)]):
+            i2, d2 = orc.two_way_f32(x, y, th)
+            assert (idx[k, :x.shape[0]] == i2).all(), (th, k)
+            assert (dd[k, :x.shape[0]].view(np.int32) == d2.view(np.int32)).all(), (th, k)
