@@ -40,6 +40,27 @@
 namespace {
 
 constexpr int KD = 256;
+// timing experiments only (wrong results): Q8_EXP_NOALOAD (A rows from registers, no global
+// loads), Q8_EXP_NOFOLD (one of 16 rows folded), Q8_EXP_NOMFMA (no matrix instructions)
+#ifndef Q8_EXP_NOALOAD
+#define Q8_EXP_NOALOAD 0
+#endif
+#ifndef Q8_EXP_NOFOLD
+#define Q8_EXP_NOFOLD 0
+#endif
+#ifndef Q8_EXP_NOMFMA
+#define Q8_EXP_NOMFMA 0
+#endif
+#ifdef Q8_EXP_TRACE
+constexpr int Q8_TRACE_BLOCKS = 8192;
+__device__ unsigned long long g_q8_trace[Q8_TRACE_BLOCKS * 4 * 10];
+#define Q8_STAMP(K) do { __builtin_amdgcn_sched_barrier(0); ts_[K] = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define Q8_STAMP(K) do { } while (0)
+#endif
+#ifndef Q8_STAGGER
+#define Q8_STAGGER 0  // > 0: first-generation second-slot blocks start this many 100-MHz ticks late
+#endif
 constexpr int Q_NW = 4, Q_NT = 64 * Q_NW, Q_RG = 2, Q_BM = 32 * Q_RG * Q_NW, Q_BN = 64, Q_NBUF = 4;
 constexpr int Q_TILE = Q_BN * KD;                  // 16 KiB: one int8 column tile, whole K
 constexpr int Q_SLOT = Q_TILE + Q_BN * 4;          // + the tile's 64 scales s_j
@@ -253,6 +274,16 @@ __global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, cons
                                                       float *__restrict__ match_score) {
     __shared__ __attribute__((aligned(16))) char lds[Q_LDS];
     float *misc = reinterpret_cast<float *>(lds + Q_OFF_MISC);
+#ifdef Q8_EXP_TRACE
+    unsigned long long ts_[8] = {};
+    Q8_STAMP(0);
+#endif
+#if Q8_STAGGER > 0
+    if (blockIdx.x >= 256 && blockIdx.x < 512) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)Q8_STAGGER) __builtin_amdgcn_s_sleep(8);
+    }
+#endif
     const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int pair = L / tiles_r, tr = L % tiles_r;
     const int n0 = min(max(n0v[pair], 0), cap), n1 = min(max(n1v[pair], 0), cap);
@@ -346,7 +377,9 @@ __global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, cons
 #pragma unroll
         for (int s2 = 0; s2 < KD / 32; s2++)
 #pragma unroll
-            for (int u = 0; u < 4; u++) xs[4 * s2 + u] = *reinterpret_cast<const float4 *>(arow + 32 * s2 + 4 * u);
+            for (int u = 0; u < 4; u++)
+                xs[4 * s2 + u] = Q8_EXP_NOALOAD ? make_float4(0.01f * (s2 + u) + 0.001f * fr, -0.02f, 0.03f, 0.f)
+                                                : *reinterpret_cast<const float4 *>(arow + 32 * s2 + 4 * u);
         float m = 0.f, qa = 0.f, qb = 0.f;
 #pragma unroll
         for (int v = 0; v < KD / 8; v++) {
@@ -378,6 +411,7 @@ __global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, cons
         __builtin_amdgcn_sched_barrier(0);  // one group's 128 floats in flight at a time
     }
 
+    Q8_STAMP(1);
     // B fragment: column block c (0, 1), lane row 32 c + fr, k32 step s: chunk (2 s + fh)
     const int rdb = fr * KD;
     const int xsw = fh ^ (fr & 15);  // chunk (2 s + fh) ^ (fr & 15) = 2 s ^ xsw
@@ -406,7 +440,7 @@ __global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, cons
 #define Q8_FOLD(G, TC, R0, R1, C0, C1)                                                       \
     do {                                                                                     \
         const unsigned g0_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)(TC)), g1_ = g0_ + 1u; \
-        _Pragma("unroll") for (int q = 0; q < 16; q++) {                                     \
+        _Pragma("unroll") for (int q = 0; q < (Q8_EXP_NOFOLD ? 1 : 16); q++) {               \
             const float a_ = __builtin_fmaf(__int_as_float(acc[G][0][q]), (R0), (C0));       \
             const float b_ = __builtin_fmaf(__int_as_float(acc[G][1][q]), (R1), (C1));       \
             fold3_q8(tag_q8(a_, vkeep, g0_), tag_q8(b_, vkeep, g1_), m1[G][q], m2[G][q]);    \
@@ -427,6 +461,11 @@ __global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, cons
             _Pragma("unroll") for (int u_ = 0; u_ < 2; u_++) {                               \
                 const int s_ = 2 * h_ + u_;                                                  \
                 _Pragma("unroll") for (int G = 0; G < Q_RG; G++) {                           \
+                    if (Q8_EXP_NOMFMA) {                                                     \
+                        acc[G][0][s_] ^= b0_[u_][0] + aI[G][s_][1];                          \
+                        acc[G][1][s_] ^= b1_[u_][1];                                         \
+                        continue;                                                            \
+                    }                                                                        \
                     acc[G][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][s_], b0_[u_],    \
                                                                       s_ == 0 ? magic16 : acc[G][0], 0, 0, 0); \
                     acc[G][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][s_], b1_[u_],    \
@@ -466,6 +505,7 @@ __global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, cons
 
     wait_vm_q8<0>();
     __syncthreads();
+    Q8_STAMP(2);
     float bmax2 = misc[0], emax2 = misc[Q_NW];
 #pragma unroll
     for (int k = 1; k < Q_NW; k++) {
@@ -478,6 +518,7 @@ __global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, cons
         if (T + 2 < ntc) Q8_SLOT(2);
         if (T + 3 < ntc) Q8_SLOT(3);
     }
+    Q8_STAMP(3);
 #undef Q8_STAGE
 #undef Q8_OFFSETS
 #undef Q8_FOLD
@@ -633,6 +674,7 @@ __global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, cons
         wide_rows[g] = (unsigned)__ballot(fh == 0 && wide);
     }
 
+    Q8_STAMP(4);
     // ---- wide rows (rare): the wave scores every column of every listed lane exactly, one
     //      column per lane at a time (lane l: columns f + 32 (l + 64 i) of inside lane f) ----
 #pragma unroll
@@ -677,6 +719,15 @@ __global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, cons
                 if (oscore) oscore[r] = keep ? ws : 0.f;
             }
         }
+#ifdef Q8_EXP_TRACE
+    Q8_STAMP(5);
+    if (lane == 0 && blockIdx.x < Q8_TRACE_BLOCKS) {
+        unsigned long long *o = g_q8_trace + ((size_t)blockIdx.x * Q_NW + w) * 10;
+        for (int k = 0; k < 6; k++) o[k] = ts_[k];
+        o[8] = __smid();
+        o[9] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 }
 
 }  // namespace
@@ -742,3 +793,10 @@ int launch_allpairs_q8_match(hipStream_t s, void *scratch, int batch, int cap, c
 }
 
 }  // namespace mv
+
+#ifdef Q8_EXP_TRACE
+// timing experiment only: per-(block, wave) phase stamps of the last k_q8_match launch
+extern "C" int mv_debug_q8_trace(void *host, long bytes) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_q8_trace), (size_t)bytes) == hipSuccess ? 0 : -3;
+}
+#endif
