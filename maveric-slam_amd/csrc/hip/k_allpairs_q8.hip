@@ -41,15 +41,15 @@ namespace {
 
 constexpr int KD = 256;
 // timing experiments only (wrong results): Q8_EXP_NOALOAD (A rows from registers, no global
-// loads), Q8_EXP_NOFOLD (one of 16 rows folded), Q8_EXP_NOMFMA (no matrix instructions)
+// loads), Q8_EXP_NOFOLD (one of 16 rows folded)
 #ifndef Q8_EXP_NOALOAD
 #define Q8_EXP_NOALOAD 0
 #endif
 #ifndef Q8_EXP_NOFOLD
 #define Q8_EXP_NOFOLD 0
 #endif
-#ifndef Q8_EXP_NOMFMA
-#define Q8_EXP_NOMFMA 0
+#ifndef Q8_PF
+#define Q8_PF 2  // k32 steps of B fragments read ahead of the MFMAs
 #endif
 #ifdef Q8_EXP_TRACE
 constexpr int Q8_TRACE_BLOCKS = 8192;
@@ -65,7 +65,8 @@ constexpr int Q_NW = 4, Q_NT = 64 * Q_NW, Q_RG = 2, Q_BM = 32 * Q_RG * Q_NW, Q_B
 constexpr int Q_TILE = Q_BN * KD;                  // 16 KiB: one int8 column tile, whole K
 constexpr int Q_SLOT = Q_TILE + Q_BN * 4;          // + the tile's 64 scales s_j
 constexpr int Q_OFF_MISC = Q_NBUF * Q_SLOT;        // [2][NW] f32 per-wave max |b|^2, |eps|^2
-constexpr int Q_LDS = Q_OFF_MISC + 2 * Q_NW * 4;
+constexpr int Q_OFF_ROW = Q_OFF_MISC + 2 * Q_NW * 4;  // [BM] float2 per row (|a|^2, s_a; s_a < 0: exact path)
+constexpr int Q_LDS = Q_OFF_ROW + 2 * 32 * Q_RG * Q_NW * 4;
 constexpr int MT_STRIDE = 32 * 8 + 16;             // epilogue transpose row: 32 (m1, m2) + pad
 constexpr int Q_NCAND = 16;                        // listed candidates per row (more: wide row)
 constexpr int Q_OFF_CL = Q_NW * 32 * MT_STRIDE;    // epilogue, inside the ring: [BM][NCAND]
@@ -131,6 +132,14 @@ __device__ __forceinline__ float swz_xor_q8(float v) {
 template <int M>
 __device__ __forceinline__ int swz_xor_q8(int v) {
     return __builtin_amdgcn_ds_swizzle(v, (M << 10) | 0x1F);
+}
+// D = 0x40800000 (the bits of 4.0) + A.B: the first k32 step of a chain, C as the inline
+// constant 4.0 (a builtin with a constant C operand gets it hoisted into 16 VGPRs).  The
+// chain's next MFMA reads D as SrcC with exact overlap (hardware forwarding, no wait states).
+__device__ __forceinline__ i32x16 mfma_i8_from4(i32x4 a, i32x4 b) {
+    i32x16 d;
+    asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, 4.0" : "=&v"(d) : "v"(a), "v"(b));
+    return d;
 }
 // four int8 RNE(x q) packed into a dword (byte i = element i): the magic sum's low byte is
 // the two's-complement integer
@@ -368,8 +377,8 @@ __global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, cons
     //      Per row: m = max |a_k|, q = RN(127 / m), s_a = RN(m / 127), |a|^2, the range check ----
     const int fr = lane & 31, fh = lane >> 5;
     i32x4 aI[Q_RG][KD / 32];
-    float an2[Q_RG], sa[Q_RG];
-    bool afull[Q_RG];
+    // per-row epilogue inputs go to LDS (not live in VGPRs across the sweep)
+    float2 *rowv = reinterpret_cast<float2 *>(lds + Q_OFF_ROW);
 #pragma unroll
     for (int g = 0; g < Q_RG; g++) {
         const float *arow = A + (size_t)min(row0 + w * 64 + g * 32 + fr, n0 - 1) * KD + fh * 16;
@@ -395,9 +404,8 @@ __global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, cons
         m = fmaxf(m, __shfl_xor(m, 32, 64));
         q2 += __shfl_xor(q2, 32, 64);
         const float q = m > 0.f ? 127.f / m : 0.f;
-        sa[g] = m / 127.f;
-        an2[g] = q2;
-        afull[g] = !(q2 <= FLT_MAX) || m < SCALE_LO || m > SCALE_HI;  // zero rows too: exact path
+        const bool afull = !(q2 <= FLT_MAX) || m < SCALE_LO || m > SCALE_HI;  // zero rows too: exact path
+        if (fh == 0) rowv[w * 64 + g * 32 + fr] = make_float2(q2, afull ? -1.f : m / 127.f);
 #pragma unroll
         for (int s2 = 0; s2 < KD / 32; s2++) {
             i32x4 r;
@@ -407,6 +415,7 @@ __global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, cons
                 r[u] = pack4_q8(x.x, x.y, x.z, x.w, q);
             }
             aI[g][s2] = r;
+            asm volatile("" : "+v"(aI[g][s2]));  // packed HERE: not sunk past the barrier
         }
         __builtin_amdgcn_sched_barrier(0);  // one group's 128 floats in flight at a time
     }
@@ -416,13 +425,11 @@ __global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, cons
     const int rdb = fr * KD;
     const int xsw = fh ^ (fr & 15);  // chunk (2 s + fh) ^ (fr & 15) = 2 s ^ xsw
 
-    // Accumulators start at the bits of 2^23: t = 2^23 + D as a float (exact for
-    // 0 <= D <= 2^22; |D| <= 127^2 * 256 < 2^22), so f = fma(t, s_j, -2^23 s_j) = RN(D s_j).
+    // Accumulators start at the bits of 4.0 (0x40800000, an inline constant of the MFMA's C
+    // operand: no registers): t = 4 + D 2^-21 as a float (|D| <= 127^2 * 256 < 2^22), so
+    // f = fma(t, 2^21 s_j, -2^23 s_j) = RN(D s_j) (the product is exact inside the fma).
     // Columns past n1 (last tile only) get s = 0 and the offset -3e38.  The low tb bits of f
     // are then replaced by the column tag 2 tc + half.
-    i32x16 magic16;
-#pragma unroll
-    for (int q = 0; q < 16; q++) magic16[q] = 0x4B000000;
     i32x16 acc[Q_RG][2];
     float m1[Q_RG][16], m2[Q_RG][16];
 #pragma unroll
@@ -432,49 +439,60 @@ __global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, cons
             m1[g][q] = -__builtin_inff();
             m2[g][q] = -__builtin_inff();
         }
+#pragma unroll
+    for (int q = 0; q < 16; q++) {  // "tile -1" of group 1, folded beside tile 0: -3e38, never a maximum
+        acc[1][0][q] = 0;
+        acc[1][1][q] = 0;
+    }
     const int tb = 2 * ntc <= 256 ? 8 : 32 - __builtin_clz(2 * ntc - 1);
     const unsigned tkeep = ~((1u << tb) - 1u);
     unsigned vkeep = tkeep;
     asm volatile("" : "+v"(vkeep));  // a VGPR operand: v_and_or_b32 may read one SGPR only
 
-#define Q8_FOLD(G, TC, R0, R1, C0, C1)                                                       \
+    // Software pipeline over the two 32-row groups: tile tc's MFMAs for group 0 issue beside
+    // the fold of group 1 of tile tc - 1, then tile tc's MFMAs for group 1 beside the fold of
+    // group 0 of tile tc.  Each wave thus always has independent VALU work between its MFMAs
+    // (the fold of one group never waits on the MFMAs in flight), with one accumulator set.
+    // The B fragments are read from LDS once per group (2 ds_read_b128 per MFMA pair).
+    // fold rows 2 S, 2 S + 1 of group FG (tile tags G0, G0 + 1; scales R, offsets C)
+#define Q8_FOLD2(FG, S, G0, R0, R1, C0, C1)                                                  \
     do {                                                                                     \
-        const unsigned g0_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)(TC)), g1_ = g0_ + 1u; \
-        _Pragma("unroll") for (int q = 0; q < (Q8_EXP_NOFOLD ? 1 : 16); q++) {               \
-            const float a_ = __builtin_fmaf(__int_as_float(acc[G][0][q]), (R0), (C0));       \
-            const float b_ = __builtin_fmaf(__int_as_float(acc[G][1][q]), (R1), (C1));       \
-            fold3_q8(tag_q8(a_, vkeep, g0_), tag_q8(b_, vkeep, g1_), m1[G][q], m2[G][q]);    \
+        _Pragma("unroll") for (int q = 2 * (S); q < 2 * (S) + 2; q++) {                      \
+            if (Q8_EXP_NOFOLD && q != 0) continue;                                           \
+            const float a_ = __builtin_fmaf(__int_as_float(acc[FG][0][q]), (R0), (C0));      \
+            const float b_ = __builtin_fmaf(__int_as_float(acc[FG][1][q]), (R1), (C1));      \
+            fold3_q8(tag_q8(a_, vkeep, (G0)), tag_q8(b_, vkeep, (G0) + 1u), m1[FG][q], m2[FG][q]); \
         }                                                                                    \
     } while (0)
-#define Q8_MMA(J)                                                                            \
+    // group G's MFMAs on slot J (fragments read PF k32 steps ahead), folding group FG meanwhile
+#define Q8_SEG(J, G, FG, G0, R0, R1, C0, C1)                                                 \
     do {                                                                                     \
+        constexpr int PF = Q8_PF;                                                            \
         const char *base = lds + (J) * Q_SLOT + rdb;                                         \
         int xs_ = xsw;                                                                       \
         asm volatile("" : "+v"(xs_)); /* per-use offsets: not 8 loop-invariant VGPRs */      \
-        _Pragma("unroll") for (int h_ = 0; h_ < KD / 64; h_++) {                             \
-            i32x4 b0_[2], b1_[2];                                                            \
-            _Pragma("unroll") for (int u_ = 0; u_ < 2; u_++) {                               \
-                const int ch_ = ((2 * (2 * h_ + u_)) ^ xs_) * 16;                            \
-                b0_[u_] = *reinterpret_cast<const i32x4 *>(base + ch_);                      \
-                b1_[u_] = *reinterpret_cast<const i32x4 *>(base + 32 * KD + ch_);            \
+        i32x4 b0_[KD / 32], b1_[KD / 32];                                                    \
+        _Pragma("unroll") for (int s_ = 0; s_ < KD / 32 + PF; s_++) {                        \
+            if (s_ < KD / 32) {                                                              \
+                const int ch_ = ((2 * s_) ^ xs_) * 16;                                       \
+                b0_[s_] = *reinterpret_cast<const i32x4 *>(base + ch_);                      \
+                b1_[s_] = *reinterpret_cast<const i32x4 *>(base + 32 * KD + ch_);            \
             }                                                                                \
-            _Pragma("unroll") for (int u_ = 0; u_ < 2; u_++) {                               \
-                const int s_ = 2 * h_ + u_;                                                  \
-                _Pragma("unroll") for (int G = 0; G < Q_RG; G++) {                           \
-                    if (Q8_EXP_NOMFMA) {                                                     \
-                        acc[G][0][s_] ^= b0_[u_][0] + aI[G][s_][1];                          \
-                        acc[G][1][s_] ^= b1_[u_][1];                                         \
-                        continue;                                                            \
-                    }                                                                        \
-                    acc[G][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][s_], b0_[u_],    \
-                                                                      s_ == 0 ? magic16 : acc[G][0], 0, 0, 0); \
-                    acc[G][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][s_], b1_[u_],    \
-                                                                      s_ == 0 ? magic16 : acc[G][1], 0, 0, 0); \
+            if (s_ >= PF) {                                                                  \
+                const int m_ = s_ - PF;                                                      \
+                if (m_ == 0) {                                                               \
+                    acc[G][0] = mfma_i8_from4(aI[G][0], b0_[0]);                             \
+                    acc[G][1] = mfma_i8_from4(aI[G][0], b1_[0]);                             \
+                } else {                                                                     \
+                    acc[G][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b0_[m_], acc[G][0], 0, 0, 0); \
+                    acc[G][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b1_[m_], acc[G][1], 0, 0, 0); \
                 }                                                                            \
+                Q8_FOLD2(FG, m_, G0, R0, R1, C0, C1);                                        \
             }                                                                                \
         }                                                                                    \
     } while (0)
     // ring: tile g lives in slot g % 4; at tile g issue tile g + 3 into the slot read at g - 1
+    // (whose scales the previous tile left in pr*)
 #define Q8_SLOT(J)                                                                           \
     do {                                                                                     \
         const int tc = T + (J);                                                              \
@@ -483,18 +501,19 @@ __global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, cons
             Q8_OFFSETS(ntile);                                                               \
             Q8_STAGE((J + Q_NBUF - 1) % Q_NBUF);                                             \
         }                                                                                    \
-        Q8_MMA(J);                                                                           \
-        float r0_, r1_, c0_, c1_;                                                            \
+        const unsigned gp_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)max(tc - 1, 0));  \
+        Q8_SEG(J, 0, 1, gp_, pr0, pr1, pc0, pc1);                                            \
         {                                                                                    \
             const float *rl_ = reinterpret_cast<const float *>(lds + (J) * Q_SLOT + Q_TILE); \
             const int col_ = tc * Q_BN + fr;                                                 \
-            r0_ = col_ < n1 ? rl_[fr] : 0.f;                                                 \
-            r1_ = col_ + 32 < n1 ? rl_[fr + 32] : 0.f;                                       \
-            c0_ = col_ < n1 ? -8388608.0f * r0_ : -3.0e38f;                                  \
-            c1_ = col_ + 32 < n1 ? -8388608.0f * r1_ : -3.0e38f;                             \
+            const float s0_ = rl_[fr], s1_ = rl_[fr + 32];                                   \
+            pr0 = col_ < n1 ? 2097152.0f * s0_ : 0.f;                                        \
+            pr1 = col_ + 32 < n1 ? 2097152.0f * s1_ : 0.f;                                   \
+            pc0 = col_ < n1 ? -8388608.0f * s0_ : -3.0e38f;                                  \
+            pc1 = col_ + 32 < n1 ? -8388608.0f * s1_ : -3.0e38f;                             \
         }                                                                                    \
-        Q8_FOLD(0, tc, r0_, r1_, c0_, c1_);                                                  \
-        Q8_FOLD(1, tc, r0_, r1_, c0_, c1_);                                                  \
+        const unsigned gc_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)tc);              \
+        Q8_SEG(J, 1, 0, gc_, pr0, pr1, pc0, pc1);                                            \
         if (ntile < ntc) {                                                                   \
             wait_vm_q8<5 * (Q_NBUF - 2)>();                                                  \
         } else {                                                                             \
@@ -506,26 +525,32 @@ __global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, cons
     wait_vm_q8<0>();
     __syncthreads();
     Q8_STAMP(2);
-    float bmax2 = misc[0], emax2 = misc[Q_NW];
-#pragma unroll
-    for (int k = 1; k < Q_NW; k++) {
-        bmax2 = fmaxf(bmax2, misc[k]);
-        emax2 = fmaxf(emax2, misc[Q_NW + k]);
-    }
+    float pr0 = 0.f, pr1 = 0.f, pc0 = -3.0e38f, pc1 = -3.0e38f;  // scales of the tile before
     for (int T = 0; T < ntc; T += 4) {
         Q8_SLOT(0);
         if (T + 1 < ntc) Q8_SLOT(1);
         if (T + 2 < ntc) Q8_SLOT(2);
         if (T + 3 < ntc) Q8_SLOT(3);
     }
+    if (ntc > 0) {  // group 1 of the last tile
+        const unsigned gl_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)(ntc - 1));
+#pragma unroll
+        for (int s = 0; s < 8; s++) Q8_FOLD2(1, s, gl_, pr0, pr1, pc0, pc1);
+    }
     Q8_STAMP(3);
 #undef Q8_STAGE
 #undef Q8_OFFSETS
-#undef Q8_FOLD
-#undef Q8_MMA
+#undef Q8_FOLD2
+#undef Q8_SEG
 #undef Q8_SLOT
 
     // ---- epilogue (wave-local; the ring is free: the sweep's last barrier follows a full drain) ----
+    float bmax2 = misc[0], emax2 = misc[Q_NW];
+#pragma unroll
+    for (int k = 1; k < Q_NW; k++) {
+        bmax2 = fmaxf(bmax2, misc[k]);
+        emax2 = fmaxf(emax2, misc[Q_NW + k]);
+    }
     const double u24 = 5.9604644775390625e-08;
     const double gam_e = KD * u24 / (1.0 - KD * u24);
     const double Bn = sqrt((double)bmax2) * 1.0001, Eb = sqrt((double)emax2) * 1.0001 + 1e-30;
@@ -579,15 +604,16 @@ __global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, cons
         // ---- decide the row in its two lanes (the fp16 kernel's logic, quantisation window) ----
         const int rl = w * 64 + g * 32 + fr;
         const bool live = row0 + rl < n0;
-        const bool full = flagged || afull[g];
+        const float2 rv = rowv[rl];
+        const bool full = flagged || rv.y < 0.f;
         const float *arow = A + (size_t)(row0 + rl) * KD;
         float bs = dmode ? __builtin_inff() : -__builtin_inff();
         int bj = 0x7fffffff;
         bool wide = live && full;
         if (wide && fh == 0) lmask[rl] = 0xffffffffu;
         if (live && !full) {
-            const double s_a = (double)sa[g];
-            const double an = sqrt(fmax((double)an2[g], 0.0)) * 1.0001;
+            const double s_a = (double)rv.y;
+            const double an = sqrt(fmax((double)rv.x, 0.0)) * 1.0001;
             const double ea = 8.001 * s_a + 2.384185791015625e-07 * an;
             const double dq = (an * Eb + ea * Bn + ea * Eb) * 1.0001;
             const double delta = dq + u24 * (an * Bn + dq) * 1.01 + gam_e * an * Bn + 1e-30;
