@@ -45,10 +45,10 @@ def parse():
     ap.add_argument("--hypotheses", type=int, default=256)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pipeline", type=int, default=1,
-                    help="contexts (each with its own stream) taking the batches in turn; > 1 overlaps "
-                         "batches (measured +2-10 %% pairs/s, but each kernel's event-timed duration then "
-                         "includes its neighbours, so the roofline line is only meaningful at 1)")
+    ap.add_argument("--pipeline", type=int, default=2,
+                    help="contexts (each with its own stream) taking the batches in turn: one batch's pose "
+                         "overlaps the next batch's match.  The per-kernel durations (roofline, stages) "
+                         "come from a second loop on ONE context, where kernels do not overlap")
     ap.add_argument("--score-steps", type=int, default=10,
                     help="secondary: steps timed with the exact score materialised (0 = skip)")
     ap.add_argument("--extra-steps", type=int, default=10,
@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--screen", choices=("i8", "f16"), default="i8",
                     help="all-pairs screen (outputs identical): int8 MFMA (default) or fp16 MFMA")
     ap.add_argument("--check", type=int, default=2, help="pairs verified against the oracle after timing")
+    ap.add_argument("--unfused", action="store_true",
+                    help="int8 screen: stage the next batch with the separate k_q8_split on the auxiliary "
+                         "stream instead of inside k_q8_match (mv_match_allpairs_f32_run_prepare_dev)")
     ap.add_argument("--window-steps", type=int, default=10,
                     help="secondary line (N = 1 only): the windowed int8 front-end of tracking_main.c "
                          "(tools/bench_window.py, 7285-cell KITTI grid, 1024 pairs); 0 = skip")
@@ -259,12 +262,17 @@ def main():
     out_score = [None]
     turn = [0]
 
+    fused = args.screen == "i8" and not args.unfused
+
     def step():
         c = turn[0] % P
         turn[0] += 1
         cx = ctxs[c]
-        cx.match_allpairs_f32_run(d0, d1, nn_, nn_, idxs[c], out_score[0], 0.8)
-        cx.match_allpairs_f32_prepare(d1, nn_)  # this context's next batch
+        if fused:  # this batch's match + this context's next batch staged, one launch
+            cx.match_allpairs_f32_run_prepare(d0, d1, nn_, nn_, idxs[c], out_score[0], d1, nn_, 0.8)
+        else:
+            cx.match_allpairs_f32_run(d0, d1, nn_, nn_, idxs[c], out_score[0], 0.8)
+            cx.match_allpairs_f32_prepare(d1, nn_)  # this context's next batch
         cx.pose_from_matches(pose_p, nn_, idxs[c], kp0, kp1, Ts[c], nmatches[c], ninls[c], statuses[c])
 
     for cx in ctxs:
@@ -278,9 +286,15 @@ def main():
     elapsed = timed_loop(step, args.steps, args.warmup, sync, barrier)
     elapsed = max_over_ranks(torch, dist, elapsed, dev)
     # per-kernel durations for the roofline and the stage split: a second, profiled loop of
-    # the same steps (hipEvents on each kernel's own launch stream)
+    # the same steps on ONE context (hipEvents on each kernel's own launch stream; with P > 1
+    # the kernels of different contexts overlap and their event times would include each other)
+    def prof_step():
+        turn[0] = 0
+        step()
+
+    sync()
     mvtrack.profile_enable(True)
-    timed_loop(step, args.steps, 0, sync, barrier)
+    timed_loop(prof_step, args.steps, 0, sync, barrier)
     mvtrack.profile_enable(False)
     screen = ctxs[0].allpairs_screen()
     kmatch, ksplit = ("k_q8_match", "k_q8_split") if screen == "i8" else ("k_ap_match", "k_ap_split")
@@ -295,8 +309,9 @@ def main():
         for _ in range(2):
             step()
         sync()
-        mvtrack.profile_enable(True)
         el_s = max_over_ranks(torch, dist, timed_loop(step, args.score_steps, 0, sync, barrier), dev)
+        mvtrack.profile_enable(True)
+        timed_loop(prof_step, args.score_steps, 0, sync, barrier)
         mvtrack.profile_enable(False)
         ks_ms, ks_n = mvtrack.profile_query(kmatch)
         with_scores = {"value": round(B * args.score_steps * world / el_s, 2),
@@ -304,8 +319,11 @@ def main():
                        kmatch + "_ms": round(ks_ms / max(ks_n, 1), 4)}
         out_score[0] = None
         for c in range(P):  # leave idx from the headline mode
-            ctxs[c].match_allpairs_f32_run(d0, d1, nn_, nn_, idxs[c], None, 0.8)
-            ctxs[c].match_allpairs_f32_prepare(d1, nn_)
+            if fused:
+                ctxs[c].match_allpairs_f32_run_prepare(d0, d1, nn_, nn_, idxs[c], None, d1, nn_, 0.8)
+            else:
+                ctxs[c].match_allpairs_f32_run(d0, d1, nn_, nn_, idxs[c], None, 0.8)
+                ctxs[c].match_allpairs_f32_prepare(d1, nn_)
         sync()
 
     # correctness of the timed outputs on a few pairs (outside the timed region)
@@ -334,8 +352,9 @@ def main():
     traffic, traffic_src = pmc_traffic(kmatch, B, n)
     if screen == "i8":
         # k_q8_match reads frame 0 as fp32 (1 KiB per row) and frame 1's int8 image (256 B +
-        # a 4-B scale per row), writes 4 B per row; 2 n0 n1 256 int8 ops per pair
-        bytes_launch = B * n * (KD * 4 + KD + 4 + 4)
+        # a 4-B scale per row), writes 4 B per row; 2 n0 n1 256 int8 ops per pair.  Fused, it
+        # also stages the next batch's frame 1: 1 KiB read, 256 + 12 B written per row
+        bytes_launch = B * n * (KD * 4 + KD + 4 + 4) + (B * n * (KD * 4 + KD + 12) if fused else 0)
         peak_c, c_note = I8_PEAK_TOPS, ("algorithmic 2*n0*n1*256 ops per pair on v_mfma_i32_32x32x32_i8 (int8 "
                                         "screen with a rigorous quantisation window, exact fp32 re-score)")
     else:
@@ -378,6 +397,7 @@ def main():
                          algorithmic_ops_per_launch=flops_pair * B, algorithmic_bytes_per_launch=bytes_launch,
                          avg_launch_ms=round(screen_avg_s * 1e3, 4), launches=k_n),
         "screen": screen,
+        "staging": "fused into k_q8_match (next batch)" if fused else "k_q8_split on the auxiliary stream",
         "stages_ms_per_step": {ksplit: round(s_ms / max(s_n, 1), 4),
                                kmatch: round(k_ms / max(k_n, 1), 4),
                                "k_pose_ransac": round(p_ms / max(p_n, 1), 4)},

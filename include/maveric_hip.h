@@ -158,6 +158,15 @@ int mv_match_allpairs_f32_prepare_dev(mv_context *ctx, int batch, int cap, const
 int mv_match_allpairs_f32_run_dev(mv_context *ctx, int batch, int cap, const int *n0, const int *n1,
                                   const float *desc0, const float *desc1, double thresh, int *match_idx,
                                   float *match_score);
+/* run (this batch, prepared) + prepare (the next batch) in one call, both on the context
+ * stream: with the int8 screen ONE kernel matches this batch and stages the next batch's
+ * frame 1 into the context's second image (each workgroup takes a share of the next rows
+ * after its tile), so the pipelined step has no separate staging kernel or stream hand-off.
+ * Afterwards the next batch is the prepared one (call this again with it, or run_dev). */
+int mv_match_allpairs_f32_run_prepare_dev(mv_context *ctx, int batch, int cap, const int *n0, const int *n1,
+                                          const float *desc0, const float *desc1, double thresh, int *match_idx,
+                                          float *match_score, int next_batch, int next_cap, const int *next_n1,
+                                          const float *next_desc1);
 /* nn_match_two_way (pairwise_pnp.py:281-323): mutual nearest neighbours under the
  * float32 distance sqrt(2 - 2 clip(s, -1, 1)) of the score s above (np.argmin: the first
  * NaN, else the first minimum), kept when dist < (float)nn_thresh and the reverse nearest

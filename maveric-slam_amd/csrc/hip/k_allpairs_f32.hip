@@ -944,6 +944,60 @@ extern "C" int mv_match_allpairs_f32_run_dev(mv_context *ctx, int batch, int cap
                     match_idx, match_score);
 }
 
+extern "C" int mv_match_allpairs_f32_run_prepare_dev(mv_context *ctx, int batch, int cap, const int *n0,
+                                                     const int *n1, const float *desc0, const float *desc1,
+                                                     double thresh, int *match_idx, float *match_score,
+                                                     int next_batch, int next_cap, const int *next_n1,
+                                                     const float *next_desc1) {
+    MV_REQUIRE(ctx != nullptr && next_batch > 0 && next_cap > 0 && next_n1 && next_desc1);
+    if (!ctx->prep_desc1 || ctx->prep_batch != batch || ctx->prep_cap != cap || ctx->prep_n1 != n1 ||
+        ctx->prep_desc1 != desc1 || ctx->prep_screen != ctx->ap_screen) {
+        mv::set_error(MV_ERR_INVALID_ARG, "mv_match_allpairs_f32_run_prepare_dev: no matching prepare for this batch");
+        return MV_ERR_INVALID_ARG;
+    }
+    MV_HIP_TRY(hipSetDevice(ctx->device));
+    const size_t need = mv::allpairs_f32_scratch_bytes(next_batch, next_cap);
+    if (ctx->ap_scratch2_bytes < need) {
+        if (ctx->ap_scratch2) {
+            (void)hipDeviceSynchronize();  // growing: nothing may still use the old buffer
+            (void)hipFree(ctx->ap_scratch2);
+            ctx->ap_scratch2 = nullptr;
+            ctx->ap_scratch2_bytes = 0;
+        }
+        const size_t b = mv::align_up(need, 1 << 20);
+        if (hipMalloc(&ctx->ap_scratch2, b) != hipSuccess) {
+            mv::set_error(MV_ERR_OUT_OF_MEMORY, "all-pairs scratch allocation of %zu bytes failed", b);
+            return MV_ERR_OUT_OF_MEMORY;
+        }
+        ctx->ap_scratch2_bytes = b;
+    }
+    if (ctx->aux_stream) MV_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_prep, 0));
+    int st;
+    if (ctx->ap_screen == MV_SCREEN_I8) {
+        st = mv::launch_allpairs_q8_match_prepare(ctx->stream, ctx->ap_scratch, batch, cap, n0, n1, desc0, desc1,
+                                                  thresh, match_idx, match_score, 0, ctx->ap_scratch2, next_batch,
+                                                  next_cap, next_n1, next_desc1);
+    } else {  // the fp16 screen: the two kernels in stream order
+        st = ap_match(ctx->ap_screen, ctx->stream, ctx->ap_scratch, batch, cap, n0, n1, desc0, desc1, thresh,
+                      match_idx, match_score);
+        if (st == MV_OK)
+            st = ap_prepare(ctx->ap_screen, ctx->stream, ctx->ap_scratch2, next_batch, next_cap, next_n1, next_desc1);
+    }
+    if (st != MV_OK) return st;
+    // the next batch's image is now the prepared one
+    void *t = ctx->ap_scratch;
+    size_t tb = ctx->ap_scratch_bytes;
+    ctx->ap_scratch = ctx->ap_scratch2;
+    ctx->ap_scratch_bytes = ctx->ap_scratch2_bytes;
+    ctx->ap_scratch2 = t;
+    ctx->ap_scratch2_bytes = tb;
+    ctx->prep_batch = next_batch;
+    ctx->prep_cap = next_cap;
+    ctx->prep_n1 = next_n1;
+    ctx->prep_desc1 = next_desc1;
+    return mv::set_status(MV_OK);
+}
+
 namespace {
 // nn_match_two_way's keep (pairwise_pnp.py:307-313): dist < nn_thresh (float32 compare) and
 // the reverse argmin of the match is the row itself

@@ -200,81 +200,91 @@ __device__ __forceinline__ bool better_q8(int dmode, float v, int j, float bv, i
 #define QS_GRID (256 * 64)
 #endif
 constexpr int QS_ROWS = 16 * QS_RPG;
-__global__ __launch_bounds__(256) void k_q8_split(int batch, int cap, const int *__restrict__ n1v,
-                                                  const float *__restrict__ desc1, char *__restrict__ q1,
-                                                  float *__restrict__ s1, float *__restrict__ nb2,
-                                                  float *__restrict__ eb2, int *__restrict__ bad) {
-    const long rows = (long)batch * cap;
+#ifndef Q8_FUSE_HEAD
+#define Q8_FUSE_HEAD 0
+#endif
+// one pass: rows R0 + 16 r + (thread >> 4), r < QS_RPG, below `rows` (= batch * cap)
+__device__ __forceinline__ void q8_split_pass(long R0, long rows, int cap, const int *__restrict__ n1v,
+                                              const float *__restrict__ desc1, char *__restrict__ q1,
+                                              float *__restrict__ s1, float *__restrict__ nb2,
+                                              float *__restrict__ eb2, int *__restrict__ bad) {
     const int sub = threadIdx.x & 15, rg = threadIdx.x >> 4;
-    for (long R0 = (long)blockIdx.x * QS_ROWS; R0 < rows; R0 += (long)gridDim.x * QS_ROWS) {
-        f32x4v x[QS_RPG][4];
-        long c[QS_RPG];
+    f32x4v x[QS_RPG][4];
+    long c[QS_RPG];
 #pragma unroll
-        for (int r = 0; r < QS_RPG; r++) {
-            const long R = R0 + 16 * r + rg;
-            c[r] = R < rows ? R : rows - 1;
+    for (int r = 0; r < QS_RPG; r++) {
+        const long R = R0 + 16 * r + rg;
+        c[r] = R < rows ? R : rows - 1;
 #pragma unroll
-            for (int u = 0; u < 4; u++)
-                x[r][u] = __builtin_nontemporal_load(
-                    reinterpret_cast<const f32x4v *>(desc1 + c[r] * KD + 4 * (sub + 16 * u)));
+        for (int u = 0; u < 4; u++)
+            x[r][u] = __builtin_nontemporal_load(
+                reinterpret_cast<const f32x4v *>(desc1 + c[r] * KD + 4 * (sub + 16 * u)));
+    }
+#pragma unroll
+    for (int r = 0; r < QS_RPG; r++) {
+        const long R = R0 + 16 * r + rg;
+        float m = 0.f, q2 = 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            m = absmax3(m, x[r][u][0], x[r][u][1]);
+            m = absmax3(m, x[r][u][2], x[r][u][3]);
+#pragma unroll
+            for (int e = 0; e < 4; e++) q2 = __builtin_fmaf(x[r][u][e], x[r][u][e], q2);
         }
+        m = fmaxf(m, swz_xor_q8<1>(m));
+        m = fmaxf(m, swz_xor_q8<2>(m));
+        m = fmaxf(m, swz_xor_q8<4>(m));
+        m = fmaxf(m, swz_xor_q8<8>(m));
+        q2 += swz_xor_q8<1>(q2);
+        q2 += swz_xor_q8<2>(q2);
+        q2 += swz_xor_q8<4>(q2);
+        q2 += swz_xor_q8<8>(q2);
+        const float q = m > 0.f ? 127.f / m : 0.f;
+        const float s = m / 127.f;
+        int pk[4];
+        float e2 = 0.f;
 #pragma unroll
-        for (int r = 0; r < QS_RPG; r++) {
-            const long R = R0 + 16 * r + rg;
-            float m = 0.f, q2 = 0.f;
+        for (int u = 0; u < 4; u++) {
+            pk[u] = pack4_q8(x[r][u][0], x[r][u][1], x[r][u][2], x[r][u][3], q);
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                m = absmax3(m, x[r][u][0], x[r][u][1]);
-                m = absmax3(m, x[r][u][2], x[r][u][3]);
-#pragma unroll
-                for (int e = 0; e < 4; e++) q2 = __builtin_fmaf(x[r][u][e], x[r][u][e], q2);
+            for (int e = 0; e < 4; e++) {
+                const float v = __builtin_fmaf(x[r][u][e], q, MAGIC_RNE) - MAGIC_RNE;  // exact
+                const float ep = __builtin_fmaf(-v, s, x[r][u][e]);
+                e2 = __builtin_fmaf(ep, ep, e2);
             }
-            m = fmaxf(m, swz_xor_q8<1>(m));
-            m = fmaxf(m, swz_xor_q8<2>(m));
-            m = fmaxf(m, swz_xor_q8<4>(m));
-            m = fmaxf(m, swz_xor_q8<8>(m));
-            q2 += swz_xor_q8<1>(q2);
-            q2 += swz_xor_q8<2>(q2);
-            q2 += swz_xor_q8<4>(q2);
-            q2 += swz_xor_q8<8>(q2);
-            const float q = m > 0.f ? 127.f / m : 0.f;
-            const float s = m / 127.f;
-            int pk[4];
-            float e2 = 0.f;
+        }
+        e2 += swz_xor_q8<1>(e2);
+        e2 += swz_xor_q8<2>(e2);
+        e2 += swz_xor_q8<4>(e2);
+        e2 += swz_xor_q8<8>(e2);
+        // finite (|b|^2 propagates NaN / inf) and a representable scale (zero rows: s = 0,
+        // q = 0, every screen value of the column 0 -- exact, no flag needed)
+        const bool ok = q2 <= FLT_MAX && (m == 0.f || (m >= SCALE_LO && m <= SCALE_HI));
+        const int pair = (int)(c[r] / cap);
+        if (R < rows && (int)(c[r] - (long)pair * cap) < n1v[pair]) {
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                pk[u] = pack4_q8(x[r][u][0], x[r][u][1], x[r][u][2], x[r][u][3], q);
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    const float v = __builtin_fmaf(x[r][u][e], q, MAGIC_RNE) - MAGIC_RNE;  // exact
-                    const float ep = __builtin_fmaf(-v, s, x[r][u][e]);
-                    e2 = __builtin_fmaf(ep, ep, e2);
-                }
-            }
-            e2 += swz_xor_q8<1>(e2);
-            e2 += swz_xor_q8<2>(e2);
-            e2 += swz_xor_q8<4>(e2);
-            e2 += swz_xor_q8<8>(e2);
-            // finite (|b|^2 propagates NaN / inf) and a representable scale (zero rows: s = 0,
-            // q = 0, every screen value of the column 0 -- exact, no flag needed)
-            const bool ok = q2 <= FLT_MAX && (m == 0.f || (m >= SCALE_LO && m <= SCALE_HI));
-            const int pair = (int)(c[r] / cap);
-            if (R < rows && (int)(c[r] - (long)pair * cap) < n1v[pair]) {
-#pragma unroll
-                for (int u = 0; u < 4; u++) *reinterpret_cast<int *>(q1 + R * KD + 4 * (sub + 16 * u)) = pk[u];
-                if (!ok) bad[pair] = 1;
-                if (sub == 0) {
-                    s1[R] = s;
-                    nb2[R] = q2;
-                    eb2[R] = e2;
-                }
+            for (int u = 0; u < 4; u++) *reinterpret_cast<int *>(q1 + R * KD + 4 * (sub + 16 * u)) = pk[u];
+            if (!ok) bad[pair] = 1;
+            if (sub == 0) {
+                s1[R] = s;
+                nb2[R] = q2;
+                eb2[R] = e2;
             }
         }
     }
 }
 
+__global__ __launch_bounds__(256) void k_q8_split(int batch, int cap, const int *__restrict__ n1v,
+                                                  const float *__restrict__ desc1, char *__restrict__ q1,
+                                                  float *__restrict__ s1, float *__restrict__ nb2,
+                                                  float *__restrict__ eb2, int *__restrict__ bad) {
+    const long rows = (long)batch * cap;
+    for (long R0 = (long)blockIdx.x * QS_ROWS; R0 < rows; R0 += (long)gridDim.x * QS_ROWS)
+        q8_split_pass(R0, rows, cap, n1v, desc1, q1, s1, nb2, eb2, bad);
+}
+
 // ---- k_q8_match ----
-__global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, const int *__restrict__ n0v,
+__device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *__restrict__ n0v,
                                                       const int *__restrict__ n1v, const float *__restrict__ desc0,
                                                       const float *__restrict__ desc1, const char *__restrict__ q1,
                                                       const float *__restrict__ s1v, const float *__restrict__ nb2v,
@@ -756,6 +766,34 @@ __global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, cons
 #endif
 }
 
+
+// The match of one 256-row tile of one pair (q8_match_block), then -- when a next batch is
+// given (nrows > 0) -- this block's share of the next batch's frame-1 staging (the k_q8_split
+// passes, rows blockIdx * rpb .. +rpb): the separate staging kernel, its launch and its
+// stream hand-off leave the pipelined step; its HBM reads overlap the co-resident block's sweep.
+__global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, const int *__restrict__ n0v,
+                                                      const int *__restrict__ n1v, const float *__restrict__ desc0,
+                                                      const float *__restrict__ desc1, const char *__restrict__ q1,
+                                                      const float *__restrict__ s1v, const float *__restrict__ nb2v,
+                                                      const float *__restrict__ eb2v, const int *__restrict__ bad,
+                                                      double thresh, int dmode, int *__restrict__ match_idx,
+                                                      float *__restrict__ match_score, long nrows, int ncap,
+                                                      const int *__restrict__ nn1, const float *__restrict__ ndesc1,
+                                                      char *__restrict__ nq1, float *__restrict__ ns1,
+                                                      float *__restrict__ nnb2, float *__restrict__ neb2,
+                                                      int *__restrict__ nbad) {
+    const long rpb = ((nrows + gridDim.x - 1) / gridDim.x + QS_ROWS - 1) / QS_ROWS * QS_ROWS;
+    const long lo = (long)blockIdx.x * rpb, hi = min(lo + rpb, nrows);
+    if (Q8_FUSE_HEAD)  // timing switch: the staging share before the tile instead of after it
+        for (long R0 = lo; R0 < hi; R0 += QS_ROWS) q8_split_pass(R0, hi, ncap, nn1, ndesc1, nq1, ns1, nnb2, neb2, nbad);
+    q8_match_block(tiles_r, cap, n0v, n1v, desc0, desc1, q1, s1v, nb2v, eb2v, bad, thresh, dmode, match_idx,
+                   match_score);
+    if (!Q8_FUSE_HEAD && nrows > 0) {
+        __syncthreads();  // every wave is past its sweep (the tail needs no LDS)
+        for (long R0 = lo; R0 < hi; R0 += QS_ROWS) q8_split_pass(R0, hi, ncap, nn1, ndesc1, nq1, ns1, nnb2, neb2, nbad);
+    }
+}
+
 }  // namespace
 
 namespace mv {
@@ -800,9 +838,10 @@ int launch_allpairs_q8_prepare(hipStream_t s, void *scratch, int batch, int cap,
     return MV_OK;
 }
 
-int launch_allpairs_q8_match(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
-                             const float *desc0, const float *desc1, double thresh, int *match_idx,
-                             float *match_score, int dmode) {
+int launch_allpairs_q8_match_prepare(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
+                                     const float *desc0, const float *desc1, double thresh, int *match_idx,
+                                     float *match_score, int dmode, void *next_scratch, int next_batch,
+                                     int next_cap, const int *next_n1, const float *next_desc1) {
     MV_REQUIRE(batch > 0 && cap > 0 && n0 && n1 && desc0 && desc1 && match_idx && scratch);
     MV_REQUIRE(((uintptr_t)desc0 & 15) == 0 && ((uintptr_t)desc1 & 15) == 0);
     MV_REQUIRE((long)cap * KD < (1l << 31));
@@ -810,12 +849,30 @@ int launch_allpairs_q8_match(hipStream_t s, void *scratch, int batch, int cap, c
     const long blocks = (long)batch * tiles_r;
     MV_REQUIRE(blocks < (1l << 31));
     const Q8Scratch m = q8_map(scratch, batch, cap);
+    Q8Scratch nm = {};
+    long nrows = 0;
+    if (next_scratch) {
+        MV_REQUIRE(next_batch > 0 && next_cap > 0 && next_n1 && next_desc1 && next_scratch != scratch);
+        MV_REQUIRE(((uintptr_t)next_desc1 & 15) == 0);
+        MV_REQUIRE((long)next_cap * KD < (1l << 31));
+        nm = q8_map(next_scratch, next_batch, next_cap);
+        nrows = (long)next_batch * next_cap;
+        MV_HIP_TRY(hipMemsetAsync(nm.bad, 0, (size_t)next_batch * 4, s));
+    }
     MV_PROF_BEGIN(s, "k_q8_match");
     hipLaunchKernelGGL(k_q8_match, dim3((unsigned)blocks), dim3(Q_NT), 0, s, tiles_r, cap, n0, n1, desc0, desc1, m.q1,
-                       m.s1, m.nb2, m.eb2, m.bad, dmode ? -1e300 : thresh, dmode, match_idx, match_score);
+                       m.s1, m.nb2, m.eb2, m.bad, dmode ? -1e300 : thresh, dmode, match_idx, match_score, nrows,
+                       next_cap, next_n1, next_desc1, nm.q1, nm.s1, nm.nb2, nm.eb2, nm.bad);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     return MV_OK;
+}
+
+int launch_allpairs_q8_match(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
+                             const float *desc0, const float *desc1, double thresh, int *match_idx,
+                             float *match_score, int dmode) {
+    return launch_allpairs_q8_match_prepare(s, scratch, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
+                                            match_score, dmode, nullptr, 0, 0, nullptr, nullptr);
 }
 
 }  // namespace mv

@@ -144,6 +144,7 @@ int mv_context_destroy(mv_context *ctx) {
     }
     if (ctx->scratch) (void)hipFree(ctx->scratch);
     if (ctx->ap_scratch) (void)hipFree(ctx->ap_scratch);
+    if (ctx->ap_scratch2) (void)hipFree(ctx->ap_scratch2);
     if (ctx->stage_dev) (void)hipFree(ctx->stage_dev);
     (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
@@ -185,6 +186,17 @@ int mv_context_reserve(mv_context *ctx, int batch, int cap) {
         const size_t ab = mv::align_up(mv::allpairs_f32_scratch_bytes(batch, cap), 1 << 20);
         if (hipMalloc(&ctx->ap_scratch, ab) != hipSuccess) return MV_ERR_OUT_OF_MEMORY;
         ctx->ap_scratch_bytes = ab;
+    }
+    if (ctx->ap_scratch2_bytes < mv::allpairs_f32_scratch_bytes(batch, cap)) {  // run_prepare's second image
+        if (ctx->ap_scratch2) {
+            MV_HIP_TRY(hipDeviceSynchronize());
+            MV_HIP_TRY(hipFree(ctx->ap_scratch2));
+            ctx->ap_scratch2 = nullptr;
+            ctx->ap_scratch2_bytes = 0;
+        }
+        const size_t ab = mv::align_up(mv::allpairs_f32_scratch_bytes(batch, cap), 1 << 20);
+        if (hipMalloc(&ctx->ap_scratch2, ab) != hipSuccess) return MV_ERR_OUT_OF_MEMORY;
+        ctx->ap_scratch2_bytes = ab;
     }
     size_t need = mv::allpairs_i8_scratch_bytes(batch, cap);
     size_t b;

@@ -19,6 +19,8 @@ struct mv_context {
     // prepare of the next batch on aux_stream never races the pose kernels on `stream`
     void *ap_scratch;
     size_t ap_scratch_bytes;
+    void *ap_scratch2;  // the other image of run_prepare (swapped with ap_scratch per call)
+    size_t ap_scratch2_bytes;
     hipStream_t aux_stream;  // created on first prepare
     hipEvent_t ev_in, ev_prep;
     int prep_batch, prep_cap;  // what the last prepare staged (run checks it)
@@ -97,6 +99,11 @@ int launch_allpairs_q8_prepare(hipStream_t s, void *scratch, int batch, int cap,
 int launch_allpairs_q8_match(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
                              const float *desc0, const float *desc1, double thresh, int *match_idx,
                              float *match_score, int dmode = 0);
+// the match plus the next batch's frame-1 staging into next_scratch, in one launch
+int launch_allpairs_q8_match_prepare(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
+                                     const float *desc0, const float *desc1, double thresh, int *match_idx,
+                                     float *match_score, int dmode, void *next_scratch, int next_batch,
+                                     int next_cap, const int *next_n1, const float *next_desc1);
 size_t allpairs_i8_scratch_bytes(int batch, int cap);
 int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
                        const int8_t *desc0, const int8_t *desc1, int *match_idx, int *match_dot);

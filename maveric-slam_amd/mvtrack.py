@@ -115,6 +115,7 @@ def lib():
             "mv_match_allpairs_f32_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _D, _P, _P]),
             "mv_match_allpairs_f32_prepare_dev": (_I, [_P, _I, _I, _P, _P]),
             "mv_match_allpairs_f32_run_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _D, _P, _P]),
+            "mv_match_allpairs_f32_run_prepare_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _D, _P, _P, _I, _I, _P, _P]),
             "mv_match_allpairs_i8_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P]),
             "mv_match_two_way_f32_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _D, _P, _P]),
             "mv_run_nms_batch_dev": (_I, [_P, _I, _I, _I, _P, _P, _P, _P]),
@@ -450,6 +451,16 @@ class Context:
         B, cap = desc0.shape[0], desc0.shape[1]
         check(lib().mv_match_allpairs_f32_run_dev(self.h, B, cap, _t(n0), _t(n1), _t(desc0), _t(desc1), float(thresh),
                                                   _t(match_idx), _t(match_score)), "match_allpairs_f32_run")
+
+    def match_allpairs_f32_run_prepare(self, desc0, desc1, n0, n1, match_idx, match_score, next_desc1, next_n1,
+                                       thresh=0.8):
+        """Match the prepared batch (desc1, n1) and stage the next batch's frame 1 in the same
+        launch (mv_match_allpairs_f32_run_prepare_dev); the next batch is then the prepared one."""
+        B, cap = desc0.shape[0], desc0.shape[1]
+        nB, ncap = next_desc1.shape[0], next_desc1.shape[1]
+        check(lib().mv_match_allpairs_f32_run_prepare_dev(self.h, B, cap, _t(n0), _t(n1), _t(desc0), _t(desc1),
+                                                          float(thresh), _t(match_idx), _t(match_score), nB, ncap,
+                                                          _t(next_n1), _t(next_desc1)), "match_allpairs_f32_run_prepare")
 
     def keypoints(self, semi, coarse_desc, H, W, num_kp, kp, conf, desc, status, heat=None, params=None):
         """Device tensors: semi [B, 65, Hc, Wc], coarse_desc [B, 256, Hc, Wc] (network outputs)

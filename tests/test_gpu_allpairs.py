@@ -320,6 +320,82 @@ def test_allpairs_f32_quantisation_stress(ctx, screen, orc, torch_cuda):
                     assert (bits(sc[k, :x.shape[0]]) == bits(s2)).all(), (thr, k)
 
 
+def _batch_f32(torch, pairs, cap):
+    B = len(pairs)
+    D0 = np.zeros((B, cap, 256), np.float32)
+    D1 = np.zeros((B, cap, 256), np.float32)
+    n0 = np.zeros(B, np.int32)
+    n1 = np.zeros(B, np.int32)
+    rng = np.random.default_rng(B)
+    for b, (a, c) in enumerate(pairs):
+        D0[b] = rng.standard_normal((cap, 256)).astype(np.float32) * 7
+        D1[b] = rng.standard_normal((cap, 256)).astype(np.float32) * 7
+        D0[b, :a.shape[0]] = a
+        D1[b, :c.shape[0]] = c
+        n0[b], n1[b] = a.shape[0], c.shape[0]
+    dev = torch.device("cuda:0")
+    return [torch.from_numpy(x).to(dev) for x in (D0, D1, n0, n1)]
+
+
+def test_allpairs_f32_run_prepare_chain(ctx, screen, orc, torch_cuda):
+    """mv_match_allpairs_f32_run_prepare_dev: batch k is matched while batch k+1's frame 1 is
+    staged in the same launch (int8 screen) or right after (fp16); a chain of batches with
+    different sizes, ragged / empty / flagged pairs, scores and indices-only, must equal the
+    oracle batch by batch."""
+    torch = torch_cuda
+    rng = np.random.default_rng(91)
+    batches = []
+    for k, (B, cap) in enumerate(((3, 640), (5, 300), (2, 1024), (4, 512))):
+        pairs = []
+        for q in range(B):
+            a = int(rng.integers(0, cap + 1))
+            b = int(rng.integers(0, cap + 1))
+            p = synth.synth_pair_f32(700 + 10 * k + q, n=max(a, 1), n1=max(b, 1), noise=0.25)
+            pairs.append((p["desc0"][:a], p["desc1"][:b]))
+        if k == 1:
+            x, y = pairs[2]
+            if y.shape[0] > 3:
+                y = y.copy()
+                y[3, 0] = np.inf  # a flagged pair
+                pairs[2] = (x, y)
+        batches.append((pairs, cap, _batch_f32(torch, pairs, cap)))
+    ctx.set_stream(torch.cuda.current_stream())
+    try:
+        _, _, (D0, D1, N0, N1) = batches[0]
+        ctx.match_allpairs_f32_prepare(D1, N1)
+        for k, (pairs, cap, (D0, D1, N0, N1)) in enumerate(batches):
+            scores = k % 2 == 0
+            idx = torch.full((len(pairs), cap), -7, dtype=torch.int32, device=D0.device)
+            sc = torch.zeros((len(pairs), cap), dtype=torch.float32, device=D0.device) if scores else None
+            if k + 1 < len(batches):
+                _, _, (_, nD1, _, nN1) = batches[k + 1]
+                ctx.match_allpairs_f32_run_prepare(D0, D1, N0, N1, idx, sc, nD1, nN1)
+            else:
+                ctx.match_allpairs_f32_run(D0, D1, N0, N1, idx, sc, 0.8)
+            torch.cuda.synchronize()
+            idx = idx.cpu().numpy()
+            sc = sc.cpu().numpy() if scores else None
+            for q, (a, c) in enumerate(pairs):
+                n0 = a.shape[0]
+                assert (idx[q, n0:] == -1).all(), (k, q)
+                if n0 == 0:
+                    continue
+                if c.shape[0] == 0:
+                    assert (idx[q, :n0] == -1).all(), (k, q)
+                    continue
+                i2, s2 = orc.allpairs_f32(a, c, 0.8)
+                assert (idx[q, :n0] == i2).all(), (k, q)
+                if scores:
+                    assert (bits(sc[q, :n0]) == bits(s2)).all(), (k, q)
+        # the chain leaves the last batch prepared; a mismatched run is refused
+        with pytest.raises(RuntimeError):
+            _, cap, (D0, D1, N0, N1) = batches[0]
+            ctx.match_allpairs_f32_run(D0, D1, N0, N1, torch.empty((3, cap), dtype=torch.int32, device=D0.device),
+                                       None, 0.8)
+    finally:
+        ctx.set_stream(None)
+
+
 def test_allpairs_screen_selection(ctx):
     import mvtrack
 
