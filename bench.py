@@ -136,9 +136,10 @@ def gen_batch(torch, dev, B, n, seed):
     return d0.contiguous(), d1, torch.from_numpy(kp0).to(dev), torch.from_numpy(kp1).to(dev)
 
 
-def pmc_traffic(kernel, B, n):
+def pmc_traffic(kernel, B, n, fused=True):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
-    (profiles/r*_summary.json, written by tools/profile.sh) taken at the same batch/kp."""
+    (profiles/r*_summary.json, written by tools/profile.sh) taken at the same batch/kp and the
+    same staging mode (k_q8_match moves the next batch's frame 1 too when fused)."""
     import glob
 
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")), reverse=True):
@@ -147,6 +148,10 @@ def pmc_traffic(kernel, B, n):
         except Exception:
             continue
         k = d.get("kernels", {}).get(kernel, {})
+        if kernel == "k_q8_match" and ("--unfused" in d.get("bench_args", "")) == fused:
+            continue
+        if kernel == "k_q8_match" and fused and d.get("tag", "") < "r02b":  # profiled before the fusion
+            continue
         if d.get("batch") == B and d.get("kp") == n and "hbm_bytes_per_launch" in k:
             return k["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
     return None, None
@@ -349,7 +354,7 @@ def main():
     flops_pair = 2.0 * n * n * KD
     screen_avg_s = (k_ms / max(k_n, 1)) * 1e-3
     achieved = flops_pair * B / screen_avg_s / 1e12
-    traffic, traffic_src = pmc_traffic(kmatch, B, n)
+    traffic, traffic_src = pmc_traffic(kmatch, B, n, fused)
     if screen == "i8":
         # k_q8_match reads frame 0 as fp32 (1 KiB per row) and frame 1's int8 image (256 B +
         # a 4-B scale per row), writes 4 B per row; 2 n0 n1 256 int8 ops per pair.  Fused, it
