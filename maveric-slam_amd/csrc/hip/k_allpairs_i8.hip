@@ -57,19 +57,19 @@ __device__ __forceinline__ bool better(long long d, long long nb, int j, long lo
 
 // ---------------------------------------------------------------------------
 // k_i8_match: the fp16 kernel's structure on the int8 matrix cores.  A 256-thread
-// block (4 waves x 32 rows, two blocks per CU) owns 128 query rows of one pair; the
-// wave's 32 rows x 256 int8 live in 32 VGPRs; frame 1 streams in 64-column tiles
-// (16 KiB, the whole K) through a 4-slot LDS ring by global_load_lds (3 tiles in
-// flight), 16-B chunks XOR-swizzled by row.  v_mfma_i32_32x32x32_i8 gives the EXACT
-// integer dot; each tile is folded (beside the next tile's MFMAs) as
-// f = dot * rsqrt|b|^2 into a lane-local (max1, idx1, max2) per row.  f orders like
+// block (4 waves x 64 rows = two 32-row groups sharing each B fragment, two blocks per
+// CU) owns 256 query rows of one pair; the wave's rows x 256 int8 live in 64 VGPRs;
+// frame 1 streams in 64-column tiles (16 KiB, the whole K) through a 4-slot LDS ring by
+// global_load_lds (3 tiles in flight), 16-B chunks XOR-swizzled by row.
+// v_mfma_i32_32x32x32_i8 gives the EXACT integer dot; the two row groups are software-
+// pipelined (one group's MFMAs beside the other group's fold) and each value is folded as
+// f = dot * rsqrt|b|^2 into a lane-local tagged top-2 per row.  f orders like
 // dot^2/|b|^2 for dot > 0 with a relative error < 3e-7, so when the runner-up is
 // below M (1 - 1e-5) the screen maximiser is the exact one and one integer dot +
 // the u128 threshold decide; otherwise one wave re-scores the row exactly.
 // ---------------------------------------------------------------------------
-// timing experiments only (wrong results): I8_EXP_NOFOLD folds 1 of 16 rows per lane,
-// I8_EXP_NOEXACT skips the per-row exact decision, I8_EXP_NODMA / NOBAR / NOMFMA drop the
-// tile DMA / the per-tile barrier / the matrix instructions
+// timing experiments only (wrong results): I8_EXP_NOEXACT skips the per-row exact decision,
+// I8_EXP_NODMA / NOBAR drop the tile DMA / the per-tile barrier
 #ifdef I8_EXP_NODMA
 #define I8_NODMA 1
 #else
@@ -80,21 +80,8 @@ __device__ __forceinline__ bool better(long long d, long long nb, int j, long lo
 #else
 #define I8_NOBAR 0
 #endif
-#ifdef I8_EXP_NOMFMA
-#define I8_NOMFMA 1
-#else
-#define I8_NOMFMA 0
-#endif
-#ifdef I8_EXP_NOFOLD
-#define I8_FOLD_ROWS 1
-#else
-#define I8_FOLD_ROWS 16
-#endif
-#ifndef I8_PIPE
-#define I8_PIPE 0  // 1: fold group 1 of tile t beside group 0's MFMAs of tile t + 1 (spills)
-#endif
-#ifndef I8_KSTEP
-#define I8_KSTEP 2  // k32 steps of B fragments read per group (8 VGPRs each)
+#ifndef I8_PF
+#define I8_PF 2  // k32 steps of B fragments read ahead of the MFMAs
 #endif
 #ifdef I8_EXP_TRACE
 constexpr int I8_TRACE_BLOCKS = 8192;
@@ -150,6 +137,14 @@ __device__ __forceinline__ void fold3_i8(float a, float b, float &m1, float &m2)
     asm("v_max_f32 %0, %1, %2" : "=v"(m2) : "v"(m2), "v"(md));
 }
 
+// D = 0x40800000 (the bits of 4.0) + A.B: the first k32 step of a chain, C as the inline
+// constant 4.0 (a builtin with a constant C gets it hoisted into 16 VGPRs); the chain's next
+// MFMA reads D as SrcC with exact overlap (hardware forwarding, no wait states)
+__device__ __forceinline__ i32x16 mfma_i8_from4_m(i32x4 a, i32x4 b) {
+    i32x16 d;
+    asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, 4.0" : "=&v"(d) : "v"(a), "v"(b));
+    return d;
+}
 __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, const int *__restrict__ n0v,
                                                       const int *__restrict__ n1v, const int8_t *__restrict__ desc0,
                                                       const int8_t *__restrict__ desc1, const int *__restrict__ nb_v,
@@ -237,14 +232,12 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
     const int rdb = fr * KD;
     const int xsw = fh ^ (fr & 15);  // chunk (2 s + fh) ^ (fr & 15) = 2 s ^ xsw
 
-    // Accumulators start at the bits of 2^23: the MFMA leaves t = 2^23 + dot as a float
-    // (exact for 0 <= dot <= 2^22; a negative dot gives 2^23 + dot/2, still below 2^23), so
-    // f = fma(t, r, -2^23 r) = RN(dot * r) in one instruction (2^23 r is exact).  The low tb
-    // bits of f are then replaced by the column tag 2 tc + half (the lane's column within the
-    // half is its own lane index): top-2 tracking needs no index registers.
-    i32x16 magic16;
-#pragma unroll
-    for (int q = 0; q < 16; q++) magic16[q] = 0x4B000000;
+    // Accumulators start at the bits of 4.0 (0x40800000, the MFMA's inline C constant): the
+    // MFMA leaves t = 4 + dot 2^-21 as a float (exact for |dot| < 2^22; a negative dot gives
+    // 4 + dot 2^-22, still below 4), so f = fma(t, 2^21 r, -2^23 r) = RN(dot * r) in one
+    // instruction (the product is exact inside the fma).  The low tb bits of f are then
+    // replaced by the column tag 2 tc + half (the lane's column within the half is its own
+    // lane index): top-2 tracking needs no index registers.  Columns past n1 get r = 0 (f = 0).
     i32x16 acc[M_RG][2];
     float m1[M_RG][16], m2[M_RG][16];
 #pragma unroll
@@ -254,55 +247,57 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
             m1[g][q] = -__builtin_inff();
             m2[g][q] = -__builtin_inff();
         }
+#pragma unroll
+    for (int q = 0; q < 16; q++) {  // "tile -1" of group 1, folded beside tile 0: -3e38, never a maximum
+        acc[1][0][q] = 0;
+        acc[1][1][q] = 0;
+    }
     const int tb = 2 * ntc <= 256 ? 8 : 32 - __builtin_clz(2 * ntc - 1);
     const unsigned tkeep = ~((1u << tb) - 1u);
     unsigned vkeep = tkeep;
     asm volatile("" : "+v"(vkeep));  // a VGPR operand: v_and_or_b32 may read one SGPR only
 
-    // fold row group G of tile TC (norms R0/R1; only the last tile has columns past n1)
-#define I8_FOLD(G, TC, R0, R1)                                                               \
+    // Software pipeline over the two 32-row groups: tile tc's MFMAs for group 0 issue beside
+    // the fold of group 1 of tile tc - 1, then tile tc's MFMAs for group 1 beside the fold of
+    // group 0 of tile tc (fold rows 2 s, 2 s + 1 after k32 step s): one accumulator set, and
+    // the fold never waits on the MFMAs in flight.  B fragments are read per group.
+#define I8_FOLD2(FG, S, G0, R0, R1, C0, C1)                                                  \
     do {                                                                                     \
-        const float c0_ = -8388608.0f * (R0), c1_ = -8388608.0f * (R1);                      \
-        const unsigned g0_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)(TC)), g1_ = g0_ + 1u; \
-        _Pragma("unroll") for (int q = 0; q < I8_FOLD_ROWS; q++) {                           \
-            const float a_ = __builtin_fmaf(__int_as_float(acc[G][0][q]), (R0), c0_);        \
-            const float b_ = __builtin_fmaf(__int_as_float(acc[G][1][q]), (R1), c1_);        \
-            fold3_i8(tag_i8(a_, vkeep, g0_), tag_i8(b_, vkeep, g1_), m1[G][q], m2[G][q]);    \
+        _Pragma("unroll") for (int q = 2 * (S); q < 2 * (S) + 2; q++) {                      \
+            const float a_ = __builtin_fmaf(__int_as_float(acc[FG][0][q]), (R0), (C0));      \
+            const float b_ = __builtin_fmaf(__int_as_float(acc[FG][1][q]), (R1), (C1));      \
+            fold3_i8(tag_i8(a_, vkeep, (G0)), tag_i8(b_, vkeep, (G0) + 1u), m1[FG][q], m2[FG][q]); \
         }                                                                                    \
     } while (0)
-    // one row group's MFMAs over the whole K of the tile in slot J (fragments re-read per group)
-#define I8_MMA(J, G0, G1)                                                                    \
+#define I8_SEG(J, G, FG, G0, R0, R1, C0, C1)                                                 \
     do {                                                                                     \
+        constexpr int PF = I8_PF;                                                            \
         const char *base = lds + (J) * M_SLOT + rdb;                                         \
         int xs_ = xsw;                                                                       \
         asm volatile("" : "+v"(xs_)); /* per-use offsets: not 8 loop-invariant VGPRs */      \
-        _Pragma("unroll") for (int h_ = 0; h_ < KD / 32 / I8_KSTEP; h_++) {                  \
-            i32x4 b0_[I8_KSTEP], b1_[I8_KSTEP];                                              \
-            _Pragma("unroll") for (int u_ = 0; u_ < I8_KSTEP; u_++) {                        \
-                const int ch_ = ((2 * (I8_KSTEP * h_ + u_)) ^ xs_) * 16;                     \
-                b0_[u_] = *reinterpret_cast<const i32x4 *>(base + ch_);                      \
-                b1_[u_] = *reinterpret_cast<const i32x4 *>(base + 32 * KD + ch_);            \
+        i32x4 b0_[KD / 32], b1_[KD / 32];                                                    \
+        _Pragma("unroll") for (int s_ = 0; s_ < KD / 32 + PF; s_++) {                        \
+            if (s_ < KD / 32) {                                                              \
+                const int ch_ = ((2 * s_) ^ xs_) * 16;                                       \
+                b0_[s_] = *reinterpret_cast<const i32x4 *>(base + ch_);                      \
+                b1_[s_] = *reinterpret_cast<const i32x4 *>(base + 32 * KD + ch_);            \
             }                                                                                \
-            _Pragma("unroll") for (int u_ = 0; u_ < I8_KSTEP; u_++) {                        \
-                const int s_ = I8_KSTEP * h_ + u_;                                           \
-                _Pragma("unroll") for (int G = (G0); G < (G1); G++) {                        \
-                    if (I8_NOMFMA) {                                                         \
-                        acc[G][0][s_] ^= b0_[u_][0];                                         \
-                        acc[G][1][s_] ^= b1_[u_][1];                                         \
-                    } else {                                                                 \
-                        acc[G][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][s_], b0_[u_], \
-                                                                          s_ == 0 ? magic16 : acc[G][0], 0, 0, 0); \
-                        acc[G][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][s_], b1_[u_], \
-                                                                          s_ == 0 ? magic16 : acc[G][1], 0, 0, 0); \
-                    }                                                                        \
+            if (s_ >= PF) {                                                                  \
+                const int m_ = s_ - PF;                                                      \
+                if (m_ == 0) {                                                               \
+                    acc[G][0] = mfma_i8_from4_m(aI[G][0], b0_[0]);                           \
+                    acc[G][1] = mfma_i8_from4_m(aI[G][0], b1_[0]);                           \
+                } else {                                                                     \
+                    acc[G][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b0_[m_], acc[G][0], 0, 0, 0); \
+                    acc[G][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b1_[m_], acc[G][1], 0, 0, 0); \
                 }                                                                            \
+                I8_FOLD2(FG, m_, G0, R0, R1, C0, C1);                                        \
             }                                                                                \
         }                                                                                    \
     } while (0)
-    // ring: tile g lives in slot g % 4; at tile g issue tile g + 3 into the slot read at g - 1.
-    // Group 0's MFMAs run beside the fold of group 1 of the previous tile, group 1's beside
-    // the fold of group 0 of this tile.
-    float rp0 = 0.f, rp1 = 0.f;  // previous tile's norms
+    // ring: tile g lives in slot g % 4; at tile g issue tile g + 3 into the slot read at g - 1
+    // (whose norms the previous tile left in pr*/pc*)
+    float pr0 = 0.f, pr1 = 0.f, pc0 = -3.0e38f, pc1 = -3.0e38f;
 #define I8_SLOT(J)                                                                           \
     do {                                                                                     \
         const int tc = T + (J);                                                              \
@@ -311,24 +306,19 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
             I8_OFFSETS(ntile);                                                               \
             if (!I8_NODMA) I8_STAGE((J + M_NBUF - 1) % M_NBUF);                              \
         }                                                                                    \
-        if (I8_PIPE) {                                                                       \
-            I8_MMA(J, 0, 1);                                                                 \
-            if (tc > 0) I8_FOLD(1, tc - 1, rp0, rp1);                                        \
-        } else {                                                                             \
-            I8_MMA(J, 0, M_RG);                                                              \
-        }                                                                                    \
-        float r0_, r1_;                                                                      \
+        const unsigned gp_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)max(tc - 1, 0));  \
+        I8_SEG(J, 0, 1, gp_, pr0, pr1, pc0, pc1);                                            \
         {                                                                                    \
             const float *rl_ = reinterpret_cast<const float *>(lds + (J) * M_SLOT + M_TILE); \
             const int col_ = tc * M_BN + fr;                                                 \
-            r0_ = col_ < n1 ? rl_[fr] : 0.f;                                                 \
-            r1_ = col_ + 32 < n1 ? rl_[fr + 32] : 0.f;                                       \
+            const float s0_ = col_ < n1 ? rl_[fr] : 0.f, s1_ = col_ + 32 < n1 ? rl_[fr + 32] : 0.f; \
+            pr0 = 2097152.0f * s0_;                                                          \
+            pr1 = 2097152.0f * s1_;                                                          \
+            pc0 = -8388608.0f * s0_;                                                         \
+            pc1 = -8388608.0f * s1_;                                                         \
         }                                                                                    \
-        if (I8_PIPE) I8_MMA(J, 1, 2);                                                        \
-        I8_FOLD(0, tc, r0_, r1_);                                                            \
-        if (!I8_PIPE) I8_FOLD(1, tc, r0_, r1_);                                              \
-        rp0 = r0_;                                                                           \
-        rp1 = r1_;                                                                           \
+        const unsigned gc_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)tc);              \
+        I8_SEG(J, 1, 0, gc_, pr0, pr1, pc0, pc1);                                            \
         if (ntile < ntc) {                                                                   \
             wait_vm_i8<5 * (M_NBUF - 2)>();                                                  \
         } else {                                                                             \
@@ -354,11 +344,15 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
         if (T + 3 < ntc) I8_SLOT(3);
     }
     I8_STAMP(3);
-    if (I8_PIPE) I8_FOLD(1, ntc - 1, rp0, rp1);  // the last tile's group 1
+    {  // group 1 of the last tile
+        const unsigned gl_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)(ntc - 1));
+#pragma unroll
+        for (int s = 0; s < KD / 32; s++) I8_FOLD2(1, s, gl_, pr0, pr1, pc0, pc1);
+    }
 #undef I8_STAGE
 #undef I8_OFFSETS
-#undef I8_FOLD
-#undef I8_MMA
+#undef I8_FOLD2
+#undef I8_SEG
 #undef I8_SLOT
 
     // the tag moved each f by < 2^(tb-23) relative and the screen itself is within 2e-7 of

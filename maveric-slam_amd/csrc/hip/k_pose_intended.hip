@@ -52,6 +52,9 @@ constexpr int NT = 256;
 #ifndef PE_NOHYP
 #define PE_NOHYP 0
 #endif
+#ifndef PE_WAVES
+#define PE_WAVES 3  // waves per SIMD (4: <= 128 VGPRs, 51 spilled, no faster -- the kernel is VALU-bound)
+#endif
 #ifndef PE_NOSOLVE
 #define PE_NOSOLVE 0
 #endif
@@ -313,7 +316,7 @@ struct PoseArgs {
     unsigned long long seed;
 };
 
-__global__ __launch_bounds__(NT) void k_pose_ransac(PoseArgs a, const int *__restrict__ nv,
+__global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const int *__restrict__ nv,
                                                     const float *__restrict__ pts0,
                                                     const float *__restrict__ pts1,
                                                     const int *__restrict__ match_idx,
