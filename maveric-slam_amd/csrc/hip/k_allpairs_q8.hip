@@ -40,13 +40,12 @@
 namespace {
 
 constexpr int KD = 256;
-// timing experiments only (wrong results): Q8_EXP_NOALOAD (A rows from registers, no global
-// loads), Q8_EXP_NOFOLD (one of 16 rows folded)
-#ifndef Q8_EXP_NOALOAD
-#define Q8_EXP_NOALOAD 0
-#endif
+// timing experiments only (wrong results): Q8_EXP_NOFOLD (one of 16 rows folded)
 #ifndef Q8_EXP_NOFOLD
 #define Q8_EXP_NOFOLD 0
+#endif
+#ifndef Q8_QB
+#define Q8_QB 4  // row quads of frame 0 in flight per wave in the A phase (4 loads per lane each)
 #endif
 #ifndef Q8_PF
 #define Q8_PF 2  // k32 steps of B fragments read ahead of the MFMAs
@@ -374,60 +373,85 @@ __device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *
             oB[g_] = (unsigned)min(nb_ + 4 * g_, n1 - 1) * KD + (dcb ^ (64u * g_));          \
         oR = (unsigned)min((TC) * Q_BN + lane, n1 - 1) * 4;                                  \
     } while (0)
-    // prologue DMA: tiles 0, 1, 2 -- issued before the A rows are read so both latencies overlap
-    for (int g = 0; g < Q_NBUF - 1 && g < ntc; g++) {
+    // prologue DMA: tiles 0, 1 into slots 0, 1 -- issued before the A rows are read so both
+    // latencies overlap (slots 2, 3 hold the A images meanwhile; tile 2 follows the A phase)
+    for (int g = 0; g < 2 && g < ntc; g++) {
         Q8_OFFSETS(g);
         if (g == 0) Q8_STAGE(0);
         if (g == 1) Q8_STAGE(1);
-        if (g == 2) Q8_STAGE(2);
     }
 
-    // ---- A: the wave's 2 x 32 rows (w*64 + 32 g + fr), fp32 -> int8 in registers (i8 MFMA
-    //      A operand: lane l holds row l & 31, k = 32 s + 16 (l >> 5) .. +15 at k32 step s).
-    //      Per row: m = max |a_k|, q = RN(127 / m), s_a = RN(m / 127), |a|^2, the range check ----
+    // ---- A: the wave's 2 x 32 rows (w*64 + 32 g + i), fp32 -> int8.  Loaded COALESCED: 16
+    //      lanes per row, lane sub = lane & 15 holds floats 4 (sub + 16 u) .. +3 (u < 4), so every
+    //      load instruction reads 256 contiguous bytes of 4 rows.  Per row (a 16-lane
+    //      reduction): m = max |a_k|, q = RN(127 RN(1/m)), s_a = RN(m RN(1/127)) -- |1 - q s_a|
+    //      < 2^-21, the window's A term -- |a|^2 and the range check; the codes go to the wave's
+    //      row-major int8 image in LDS (ring slots 2-3, 16-B chunks swizzled by row) and come back
+    //      in the i8 MFMA A layout (lane l: row l & 31, k = 32 s + 16 (l >> 5) .. +15).  (Loading
+    //      the MFMA layout directly -- each lane its own row in 16-B pieces at 128-B stride --
+    //      asks the memory pipeline for every line four times.) ----
     const int fr = lane & 31, fh = lane >> 5;
     i32x4 aI[Q_RG][KD / 32];
     // per-row epilogue inputs go to LDS (not live in VGPRs across the sweep)
     float2 *rowv = reinterpret_cast<float2 *>(lds + Q_OFF_ROW);
+    {
+        char *img = lds + 2 * Q_SLOT + w * 32 * KD;  // 8 KiB per wave, one row group at a time
+        const int sub = lane & 15, rq = lane >> 4;
+        constexpr int QB = Q8_QB;  // row quads (4 QB loads per lane) in flight
 #pragma unroll
-    for (int g = 0; g < Q_RG; g++) {
-        const float *arow = A + (size_t)min(row0 + w * 64 + g * 32 + fr, n0 - 1) * KD + fh * 16;
-        float4 xs[KD / 8];  // 128 floats of the row, all loads in flight
+        for (int g = 0; g < Q_RG; g++) {
 #pragma unroll
-        for (int s2 = 0; s2 < KD / 32; s2++)
+            for (int qd0 = 0; qd0 < 8; qd0 += QB) {
+                f32x4v x[QB][4];
 #pragma unroll
-            for (int u = 0; u < 4; u++)
-                xs[4 * s2 + u] = Q8_EXP_NOALOAD ? make_float4(0.01f * (s2 + u) + 0.001f * fr, -0.02f, 0.03f, 0.f)
-                                                : *reinterpret_cast<const float4 *>(arow + 32 * s2 + 4 * u);
-        float m = 0.f, qa = 0.f, qb = 0.f;
+                for (int qd = 0; qd < QB; qd++) {
+                    const float *ar = A + (size_t)min(row0 + w * 64 + g * 32 + 4 * (qd0 + qd) + rq, n0 - 1) * KD;
 #pragma unroll
-        for (int v = 0; v < KD / 8; v++) {
-            const float4 x = xs[v];
-            m = absmax3(m, x.x, x.y);
-            m = absmax3(m, x.z, x.w);
-            qa = __builtin_fmaf(x.x, x.x, qa);
-            qb = __builtin_fmaf(x.y, x.y, qb);
-            qa = __builtin_fmaf(x.z, x.z, qa);
-            qb = __builtin_fmaf(x.w, x.w, qb);
-        }
-        float q2 = qa + qb;
-        m = fmaxf(m, __shfl_xor(m, 32, 64));
-        q2 += __shfl_xor(q2, 32, 64);
-        const float q = m > 0.f ? 127.f / m : 0.f;
-        const bool afull = !(q2 <= FLT_MAX) || m < SCALE_LO || m > SCALE_HI;  // zero rows too: exact path
-        if (fh == 0) rowv[w * 64 + g * 32 + fr] = make_float2(q2, afull ? -1.f : m / 127.f);
+                    for (int u = 0; u < 4; u++) x[qd][u] = *reinterpret_cast<const f32x4v *>(ar + 4 * (sub + 16 * u));
+                }
 #pragma unroll
-        for (int s2 = 0; s2 < KD / 32; s2++) {
-            i32x4 r;
+                for (int qd = 0; qd < QB; qd++) {
+                    const int r = 4 * (qd0 + qd) + rq;  // row within the group
+                    float m = 0.f, qa = 0.f, qb = 0.f;
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const float4 x = xs[4 * s2 + u];
-                r[u] = pack4_q8(x.x, x.y, x.z, x.w, q);
+                    for (int u = 0; u < 4; u++) {
+                        m = absmax3(m, x[qd][u][0], x[qd][u][1]);
+                        m = absmax3(m, x[qd][u][2], x[qd][u][3]);
+                        qa = __builtin_fmaf(x[qd][u][0], x[qd][u][0], qa);
+                        qb = __builtin_fmaf(x[qd][u][1], x[qd][u][1], qb);
+                        qa = __builtin_fmaf(x[qd][u][2], x[qd][u][2], qa);
+                        qb = __builtin_fmaf(x[qd][u][3], x[qd][u][3], qb);
+                    }
+                    float q2 = qa + qb;
+                    m = fmaxf(m, swz_xor_q8<1>(m));
+                    q2 += swz_xor_q8<1>(q2);
+                    m = fmaxf(m, swz_xor_q8<2>(m));
+                    q2 += swz_xor_q8<2>(q2);
+                    m = fmaxf(m, swz_xor_q8<4>(m));
+                    q2 += swz_xor_q8<4>(q2);
+                    m = fmaxf(m, swz_xor_q8<8>(m));
+                    q2 += swz_xor_q8<8>(q2);
+                    const float q = m > 0.f ? 127.f * __builtin_amdgcn_rcpf(m) : 0.f;
+                    const bool afull = !(q2 <= FLT_MAX) || m < SCALE_LO || m > SCALE_HI;  // zero rows too: exact path
+                    if (sub == 0) rowv[w * 64 + g * 32 + r] = make_float2(q2, afull ? -1.f : m * (1.f / 127.f));
+                    char *rowp = img + r * KD + 4 * (sub & 3);
+#pragma unroll
+                    for (int u = 0; u < 4; u++)  // k = 4 sub + 64 u: chunk (sub >> 2) + 4 u
+                        *reinterpret_cast<int *>(rowp + ((((sub >> 2) + 4 * u) ^ (r & 15)) << 4)) =
+                            pack4_q8(x[qd][u][0], x[qd][u][1], x[qd][u][2], x[qd][u][3], q);
+                }
             }
-            aI[g][s2] = r;
-            asm volatile("" : "+v"(aI[g][s2]));  // packed HERE: not sunk past the barrier
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own image writes
+#pragma unroll
+            for (int s2 = 0; s2 < KD / 32; s2++)
+                aI[g][s2] = *reinterpret_cast<const i32x4 *>(img + fr * KD + (((2 * s2 + fh) ^ (fr & 15)) << 4));
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // the reads complete before the next group's writes
         }
-        __builtin_amdgcn_sched_barrier(0);  // one group's 128 floats in flight at a time
+    }
+    __syncthreads();  // every wave's image is read: slot 2 takes tile 2
+    if (ntc > 2) {
+        Q8_OFFSETS(2);
+        Q8_STAGE(2);
     }
 
     Q8_STAMP(1);
@@ -532,7 +556,12 @@ __device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *
         __syncthreads();                                                                     \
     } while (0)
 
-    wait_vm_q8<0>();
+    // tile 0 landed (younger: tiles 1 and 2, 5 ops each)
+    if (ntc > 2) {
+        wait_vm_q8<10>();
+    } else {
+        wait_vm_q8<0>();
+    }
     __syncthreads();
     Q8_STAMP(2);
     float pr0 = 0.f, pr1 = 0.f, pc0 = -3.0e38f, pc1 = -3.0e38f;  // scales of the tile before
@@ -624,7 +653,7 @@ __device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *
         if (live && !full) {
             const double s_a = (double)rv.y;
             const double an = sqrt(fmax((double)rv.x, 0.0)) * 1.0001;
-            const double ea = 8.001 * s_a + 2.384185791015625e-07 * an;
+            const double ea = 8.001 * s_a + 4.76837158203125e-07 * an;  // |1 - q s_a| < 2^-21
             const double dq = (an * Eb + ea * Bn + ea * Eb) * 1.0001;
             const double delta = dq + u24 * (an * Bn + dq) * 1.01 + gam_e * an * Bn + 1e-30;
             const double Ms = (double)M * s_a;
