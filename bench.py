@@ -39,8 +39,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=1024,
-                    help="frame-pairs per GPU per step (one launch each; SURVEY §8d: >= 1000 pairs per launch)")
+    ap.add_argument("--batch", type=int, default=4096,
+                    help="frame-pairs per GPU per step (one launch each; SURVEY §8d: >= 1000 pairs per launch; "
+                         "1024 / 2048 / 4096 measured 1.32 / 1.42 / 1.46 M pairs/s: launch tails amortised)")
     ap.add_argument("--kp", type=int, default=1024, help="keypoints per frame")
     ap.add_argument("--hypotheses", type=int, default=256)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
