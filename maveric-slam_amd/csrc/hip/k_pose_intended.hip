@@ -12,7 +12,7 @@
 //      strided subset of 128 correspondences (LDS broadcast reads);
 //   3. preemption: the 2 best of each wave survive and are MSAC-scored on ALL
 //      correspondences by the whole block; lowest (cost, hypothesis id) -> E;
-//   4. E = U diag(s1,s2,s3) V^T (double Jacobi on E^T E), the four (R, t)
+//   4. E = U diag(s1,s2,s3) V^T (closed-form eigenvectors of E^T E), the four (R, t)
 //      candidates R = U W V^T / U W^T V^T, t = +-u3, cheirality vote by
 //      triangulated depth over the inliers (block reduction);
 //   5. Gauss-Newton: residual r_i = (x2^T [t]x R x1) / s_i (Sampson), inliers
@@ -29,6 +29,12 @@
 #include <math.h>
 
 #include "mv_internal.hpp"
+
+// This kernel is the as-INTENDED pose, checked against ground truth within a tolerance,
+// not bit-exact against the oracle: let every a * b + c contract to one FMA here (the
+// library's -ffp-contract=off exists for the bit-exact as-built paths).  Sampson scoring
+// drops from ~41 to ~26 VALU ops per (hypothesis, correspondence).
+#pragma clang fp contract(fast)
 
 namespace {
 
@@ -53,7 +59,7 @@ constexpr int NT = 256;
 #define PE_NOHYP 0
 #endif
 #ifndef PE_WAVES
-#define PE_WAVES 3  // waves per SIMD (4: <= 128 VGPRs, 51 spilled, no faster -- the kernel is VALU-bound)
+#define PE_WAVES 4  // waves per SIMD (4: 128 VGPRs, 13 spilled, 3% faster than 3 at 142)
 #endif
 #ifndef PE_NOSOLVE
 #define PE_NOSOLVE 0
@@ -156,81 +162,124 @@ __device__ __forceinline__ float msac_cost(const float e[9], float4 p, float thr
     return in ? num * num * __builtin_amdgcn_rcpf(den) : thr2;
 }
 
-// ---- small double linear algebra (one lane) ----
-struct D3 {
-    double v[3];
+// msac_cost of two correspondences at once on packed FP32 (v_pk_fma_f32 with the
+// hypothesis' coefficients splat): A = {x1 x1' y1 y1'}, B = {x2 x2' y2 y2'}, the
+// scoring subset's point-pair layout, so the operands need no register shuffling
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v msac_cost2(const float e[9], float4 A, float4 B, float thr2) {
+    const f2v x1 = {A.x, A.y}, y1 = {A.z, A.w}, x2 = {B.x, B.y}, y2 = {B.z, B.w};
+    const f2v ex0 = e[0] * x1 + (e[1] * y1 + e[2]);
+    const f2v ex1 = e[3] * x1 + (e[4] * y1 + e[5]);
+    const f2v ex2 = e[6] * x1 + (e[7] * y1 + e[8]);
+    const f2v etx0 = e[0] * x2 + (e[3] * y2 + e[6]);
+    const f2v etx1 = e[1] * x2 + (e[4] * y2 + e[7]);
+    const f2v num = x2 * ex0 + (y2 * ex1 + ex2);
+    const f2v den = ex0 * ex0 + ex1 * ex1 + etx0 * etx0 + etx1 * etx1;
+    const f2v nn = num * num, td = thr2 * den;
+    f2v r;
+    r.x = nn.x < td.x ? nn.x * __builtin_amdgcn_rcpf(den.x) : thr2;
+    r.y = nn.y < td.y ? nn.y * __builtin_amdgcn_rcpf(den.y) : thr2;
+    return r;
+}
+
+// ---- small 3-vector algebra ----
+template <typename T>
+struct V3 {
+    T v[3];
 };
-__device__ __forceinline__ D3 cross(const D3 &a, const D3 &b) {
+using F3 = V3<float>;
+template <typename T>
+__device__ __forceinline__ V3<T> cross(const V3<T> &a, const V3<T> &b) {
     return {{a.v[1] * b.v[2] - a.v[2] * b.v[1], a.v[2] * b.v[0] - a.v[0] * b.v[2], a.v[0] * b.v[1] - a.v[1] * b.v[0]}};
 }
-__device__ __forceinline__ double dot3(const D3 &a, const D3 &b) {
+template <typename T>
+__device__ __forceinline__ T dot3(const V3<T> &a, const V3<T> &b) {
     return a.v[0] * b.v[0] + a.v[1] * b.v[1] + a.v[2] * b.v[2];
 }
-
-// symmetric 3x3 eigen-decomposition by cyclic Jacobi (double); columns of V are eigenvectors
-__device__ void jacobi_eig3(double A[3][3], double V[3][3], double w[3]) {
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) V[i][j] = i == j ? 1.0 : 0.0;
-    for (int sweep = 0; sweep < 16; sweep++) {
-        const double off = A[0][1] * A[0][1] + A[0][2] * A[0][2] + A[1][2] * A[1][2];
-        if (off < 1e-60) break;
-        for (int p = 0; p < 2; p++)
-            for (int q = p + 1; q < 3; q++) {
-                if (fabs(A[p][q]) < 1e-300) continue;
-                const double theta = (A[q][q] - A[p][p]) / (2.0 * A[p][q]);
-                const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
-                for (int k = 0; k < 3; k++) {
-                    const double akp = A[k][p], akq = A[k][q];
-                    A[k][p] = c * akp - s * akq;
-                    A[k][q] = s * akp + c * akq;
-                }
-                for (int k = 0; k < 3; k++) {
-                    const double apk = A[p][k], aqk = A[q][k];
-                    A[p][k] = c * apk - s * aqk;
-                    A[q][k] = s * apk + c * aqk;
-                }
-                for (int k = 0; k < 3; k++) {
-                    const double vkp = V[k][p], vkq = V[k][q];
-                    V[k][p] = c * vkp - s * vkq;
-                    V[k][q] = s * vkp + c * vkq;
-                }
-            }
-    }
-    for (int i = 0; i < 3; i++) w[i] = A[i][i];
+__device__ __forceinline__ F3 scale3(const F3 &a, float s) { return {{a.v[0] * s, a.v[1] * s, a.v[2] * s}}; }
+__device__ __forceinline__ F3 mul_sym(const float A[3][3], const F3 &x) {
+    return {{A[0][0] * x.v[0] + A[0][1] * x.v[1] + A[0][2] * x.v[2],
+             A[1][0] * x.v[0] + A[1][1] * x.v[1] + A[1][2] * x.v[2],
+             A[2][0] * x.v[0] + A[2][1] * x.v[1] + A[2][2] * x.v[2]}};
 }
 
-// E (row-major double) -> U, V with E ~ U diag(1,1,0) V^T, det U = det V = +1
-__device__ void essential_uv(const double E[9], double U[3][3], double V[3][3]) {
-    double EtE[3][3];
+// The two leading eigenvectors (v1: largest eigenvalue) of the symmetric PSD 3x3 A, in
+// closed form and float (E is a float estimate; the Gauss-Newton stage refines the pose
+// in float from here).  Replaces a cyclic Jacobi in double, whose serial sweeps on one
+// lane cost ~17k of the block's ~133k cycles (this: ~3k, measured with PE_TRACE):
+//   - the smallest eigenvalue from the trigonometric solution of the characteristic
+//     cubic: for an essential matrix (l1 = l2, r = -1) l3 = q + 2p cos(pi - d) is flat
+//     in d, so the angle's rounding enters squared;
+//   - its eigenvector as the longest cross product of two rows of A - l3 I (rank 2: the
+//     gap to l2 is the leading singular value squared);
+//   - one exact Jacobi rotation of A restricted to the orthogonal complement.
+// When l1 ~ l2 the split of the complement is arbitrary, in any method, and the
+// candidate set {U W V^T, U W^T V^T} x {+-u3} does not depend on it (checked against
+// numpy.linalg.eigh on essential, noisy and degenerate E).
+__device__ void top2_eig3(const float A[3][3], F3 &v1, F3 &v2) {
+    const float p1 = A[0][1] * A[0][1] + A[0][2] * A[0][2] + A[1][2] * A[1][2];
+    const float q = (A[0][0] + A[1][1] + A[2][2]) * (1.f / 3.f);
+    const float d0 = A[0][0] - q, d1 = A[1][1] - q, d2 = A[2][2] - q;
+    const float p2 = (d0 * d0 + d1 * d1 + d2 * d2 + 2.f * p1) * (1.f / 6.f);
+    F3 v3 = {{0.f, 0.f, 1.f}};
+    if (p2 > 1e-30f) {
+        const float ip = __builtin_amdgcn_rsqf(p2), p = p2 * ip;
+        const float b00 = d0 * ip, b11 = d1 * ip, b22 = d2 * ip;
+        const float b01 = A[0][1] * ip, b02 = A[0][2] * ip, b12 = A[1][2] * ip;
+        float r = 0.5f * (b00 * (b11 * b22 - b12 * b12) - b01 * (b01 * b22 - b12 * b02) + b02 * (b01 * b12 - b11 * b02));
+        r = fminf(1.f, fmaxf(-1.f, r));
+        const float l3 = q + 2.f * p * cosf(acosf(r) * (1.f / 3.f) + 2.09439510f);
+        const F3 r0 = {{A[0][0] - l3, A[0][1], A[0][2]}};
+        const F3 r1 = {{A[1][0], A[1][1] - l3, A[1][2]}};
+        const F3 r2 = {{A[2][0], A[2][1], A[2][2] - l3}};
+        const F3 c0 = cross(r0, r1), c1 = cross(r0, r2), c2 = cross(r1, r2);
+        const float n0 = dot3(c0, c0), n1 = dot3(c1, c1), n2 = dot3(c2, c2);
+        const F3 c = (n0 >= n1 && n0 >= n2) ? c0 : (n1 >= n2 ? c1 : c2);
+        const float nc = fmaxf(fmaxf(n0, n1), n2);
+        if (nc > 1e-37f) v3 = scale3(c, __builtin_amdgcn_rsqf(nc));
+    }
+    // orthonormal basis (a, b) of the complement of v3
+    const float f0 = fabsf(v3.v[0]), f1 = fabsf(v3.v[1]), f2 = fabsf(v3.v[2]);
+    const int ax = (f0 <= f1 && f0 <= f2) ? 0 : (f1 <= f2 ? 1 : 2);
+    const F3 e = {{ax == 0 ? 1.f : 0.f, ax == 1 ? 1.f : 0.f, ax == 2 ? 1.f : 0.f}};
+    F3 a = cross(v3, e);
+    a = scale3(a, __builtin_amdgcn_rsqf(dot3(a, a)));
+    const F3 b = cross(v3, a);
+    const F3 Aa = mul_sym(A, a), Ab = mul_sym(A, b);
+    const float m00 = dot3(a, Aa), m11 = dot3(b, Ab), m01 = dot3(a, Ab);
+    float c = 1.f, s = 0.f;
+    if (fabsf(m01) > 1e-30f * fmaxf(fabsf(m00), fabsf(m11))) {
+        const float th = (m11 - m00) * __builtin_amdgcn_rcpf(2.f * m01);
+        const float t = copysignf(1.f, th) * __builtin_amdgcn_rcpf(fabsf(th) + sqrtf(th * th + 1.f));
+        c = __builtin_amdgcn_rsqf(t * t + 1.f);
+        s = t * c;
+    }
+    const F3 x = {{c * a.v[0] - s * b.v[0], c * a.v[1] - s * b.v[1], c * a.v[2] - s * b.v[2]}};
+    const F3 y = {{s * a.v[0] + c * b.v[0], s * a.v[1] + c * b.v[1], s * a.v[2] + c * b.v[2]}};
+    const bool sw = dot3(y, mul_sym(A, y)) > dot3(x, mul_sym(A, x));
+    v1 = sw ? y : x;
+    v2 = sw ? x : y;
+}
+
+// E (row-major) -> U, V with E ~ U diag(1,1,0) V^T, det U = det V = +1
+__device__ void essential_uv(const float E[9], float U[3][3], float V[3][3]) {
+    float EtE[3][3];
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++)
             EtE[i][j] = E[0 * 3 + i] * E[0 * 3 + j] + E[1 * 3 + i] * E[1 * 3 + j] + E[2 * 3 + i] * E[2 * 3 + j];
-    double Vr[3][3], w[3];
-    jacobi_eig3(EtE, Vr, w);
-    int o[3] = {0, 1, 2};  // sort descending
-    for (int a = 0; a < 3; a++)
-        for (int b = a + 1; b < 3; b++)
-            if (w[o[b]] > w[o[a]]) {
-                int t = o[a];
-                o[a] = o[b];
-                o[b] = t;
-            }
-    D3 v1 = {{Vr[0][o[0]], Vr[1][o[0]], Vr[2][o[0]]}};
-    D3 v2 = {{Vr[0][o[1]], Vr[1][o[1]], Vr[2][o[1]]}};
-    D3 v3 = cross(v1, v2);  // right-handed V
-    D3 u1, u2;
+    F3 v1, v2;
+    top2_eig3(EtE, v1, v2);
+    const F3 v3 = cross(v1, v2);  // right-handed V
+    F3 u1, u2;
     for (int i = 0; i < 3; i++) {
         u1.v[i] = E[i * 3 + 0] * v1.v[0] + E[i * 3 + 1] * v1.v[1] + E[i * 3 + 2] * v1.v[2];
         u2.v[i] = E[i * 3 + 0] * v2.v[0] + E[i * 3 + 1] * v2.v[1] + E[i * 3 + 2] * v2.v[2];
     }
-    double n1 = sqrt(dot3(u1, u1));
-    for (int i = 0; i < 3; i++) u1.v[i] /= n1;
-    const double d12 = dot3(u1, u2);  // re-orthogonalise
+    u1 = scale3(u1, __builtin_amdgcn_rsqf(dot3(u1, u1)));
+    const float d12 = dot3(u1, u2);  // re-orthogonalise
     for (int i = 0; i < 3; i++) u2.v[i] -= d12 * u1.v[i];
-    double n2 = sqrt(dot3(u2, u2));
-    for (int i = 0; i < 3; i++) u2.v[i] /= n2;
-    D3 u3 = cross(u1, u2);
+    u2 = scale3(u2, __builtin_amdgcn_rsqf(dot3(u2, u2)));
+    const F3 u3 = cross(u1, u2);
     for (int i = 0; i < 3; i++) {
         U[i][0] = u1.v[i];
         U[i][1] = u2.v[i];
@@ -279,25 +328,6 @@ __device__ __forceinline__ void rodrigues_f(const float w[3], float R[3][3]) {
         }
 }
 
-__device__ void rodrigues(const double w[3], double R[3][3]) {
-    const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
-    double a, b;
-    if (th2 < 2.5e-3) {  // |theta| < 0.05: Taylor to theta^8 (remainder < 3e-21), no transcendentals
-        a = 1.0 - th2 / 6.0 * (1.0 - th2 / 20.0 * (1.0 - th2 / 42.0 * (1.0 - th2 / 72.0)));
-        b = 0.5 * (1.0 - th2 / 12.0 * (1.0 - th2 / 30.0 * (1.0 - th2 / 56.0 * (1.0 - th2 / 90.0))));
-    } else {
-        const double th = sqrt(th2);
-        a = sin(th) / th;
-        b = (1.0 - cos(th)) / th2;
-    }
-    const double K[3][3] = {{0, -w[2], w[1]}, {w[2], 0, -w[0]}, {-w[1], w[0], 0}};
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) {
-            double kk = K[i][0] * K[0][j] + K[i][1] * K[1][j] + K[i][2] * K[2][j];
-            R[i][j] = (i == j ? 1.0 : 0.0) + a * K[i][j] + b * kk;
-        }
-}
-
 __device__ __forceinline__ int block_sum_i(int v, int *red) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -327,7 +357,7 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
     __shared__ int wsum[4];
     __shared__ int s_best[2];
     __shared__ float s_E[9];
-    __shared__ double s_pose[12];  // R (9) + t (3)
+    __shared__ float s_pose[12];  // R (9) + t (3)
     const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int n_in = min(max(nv[b], 0), a.cap);
     const long long tk0 = PE_TRACE ? clock64() : 0;
@@ -336,9 +366,39 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
     const int per = (n_in + NT - 1) / NT;
     const int i0 = t * per, i1 = min(i0 + per, n_in);
     int cnt = 0;
-    // a match index outside [0, cap) is "no match" (never dereferenced)
-    for (int i = i0; i < i1; i++)
-        cnt += (!match_idx || (unsigned)match_idx[(size_t)b * a.cap + i] < (unsigned)a.cap) ? 1 : 0;
+    // a match index outside [0, cap) is "no match" (never dereferenced).  Up to PF_PER
+    // entries per thread (cap <= 4 NT) are loaded, gathered and normalised here, before the
+    // scan, so their load latency overlaps it instead of costing a second dependent pass.
+    constexpr int PF_PER = 4;
+    float4 pf[PF_PER];
+    bool pok[PF_PER];
+    if (per <= PF_PER) {
+#pragma unroll
+        for (int q = 0; q < PF_PER; q++) {
+            const int i = i0 + q;
+            pok[q] = false;
+            pf[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (i >= i1) continue;
+            const size_t gi = (size_t)b * a.cap + i;
+            float x2, y2;
+            if (match_idx) {
+                const int j = match_idx[gi];
+                if ((unsigned)j >= (unsigned)a.cap) continue;
+                x2 = kp1[((size_t)b * a.cap + j) * 2];
+                y2 = kp1[((size_t)b * a.cap + j) * 2 + 1];
+            } else {
+                x2 = pts1[gi * 2];
+                y2 = pts1[gi * 2 + 1];
+            }
+            const float x1 = pts0[gi * 2], y1 = pts0[gi * 2 + 1];
+            pf[q] = make_float4((x1 - a.cx) / a.fx, (y1 - a.cy) / a.fy, (x2 - a.cx) / a.fx, (y2 - a.cy) / a.fy);
+            pok[q] = true;
+            cnt++;
+        }
+    } else {
+        for (int i = i0; i < i1; i++)
+            cnt += (!match_idx || (unsigned)match_idx[(size_t)b * a.cap + i] < (unsigned)a.cap) ? 1 : 0;
+    }
     int x = cnt;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -351,20 +411,29 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
     for (int k = 0; k < w; k++) off += wsum[k];
     const int n_all = wsum[0] + wsum[1] + wsum[2] + wsum[3];
     const int n = min(n_all, MAXP);
-    for (int i = i0; i < i1; i++) {
-        float x1 = pts0[((size_t)b * a.cap + i) * 2], y1 = pts0[((size_t)b * a.cap + i) * 2 + 1], x2, y2;
-        if (match_idx) {
-            const int j = match_idx[(size_t)b * a.cap + i];
-            if ((unsigned)j >= (unsigned)a.cap) continue;
-            x2 = kp1[((size_t)b * a.cap + j) * 2];
-            y2 = kp1[((size_t)b * a.cap + j) * 2 + 1];
-        } else {
-            x2 = pts1[((size_t)b * a.cap + i) * 2];
-            y2 = pts1[((size_t)b * a.cap + i) * 2 + 1];
+    if (per <= PF_PER) {
+#pragma unroll
+        for (int q = 0; q < PF_PER; q++) {
+            if (!pok[q]) continue;
+            if (off < MAXP) P[off] = pf[q];
+            off++;
         }
-        if (off < MAXP)
-            P[off] = make_float4((x1 - a.cx) / a.fx, (y1 - a.cy) / a.fy, (x2 - a.cx) / a.fx, (y2 - a.cy) / a.fy);
-        off++;
+    } else {
+        for (int i = i0; i < i1; i++) {
+            float x1 = pts0[((size_t)b * a.cap + i) * 2], y1 = pts0[((size_t)b * a.cap + i) * 2 + 1], x2, y2;
+            if (match_idx) {
+                const int j = match_idx[(size_t)b * a.cap + i];
+                if ((unsigned)j >= (unsigned)a.cap) continue;
+                x2 = kp1[((size_t)b * a.cap + j) * 2];
+                y2 = kp1[((size_t)b * a.cap + j) * 2 + 1];
+            } else {
+                x2 = pts1[((size_t)b * a.cap + i) * 2];
+                y2 = pts1[((size_t)b * a.cap + i) * 2 + 1];
+            }
+            if (off < MAXP)
+                P[off] = make_float4((x1 - a.cx) / a.fx, (y1 - a.cy) / a.fy, (x2 - a.cx) / a.fx, (y2 - a.cy) / a.fy);
+            off++;
+        }
     }
     __syncthreads();
     float *To = T + (size_t)b * 12;
@@ -388,6 +457,14 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
     constexpr int PRE_M = 128, SURV = 2, NS = 4 * SURV;
     const int m = min(n, PRE_M);
     const unsigned step16 = ((unsigned)n << 16) / (unsigned)m;  // subset point k: (k * step16) >> 16 < n
+    // the subset in point-pair layout (points 2k, 2k+1 of it in s_sub[k])
+    __shared__ float4 s_sub[PRE_M / 2][2];
+    if (t < m / 2) {
+        const float4 pa = P[((2 * t) * step16) >> 16], pb = P[((2 * t + 1) * step16) >> 16];
+        s_sub[t][0] = make_float4(pa.x, pb.x, pa.y, pb.y);
+        s_sub[t][1] = make_float4(pa.z, pb.z, pa.w, pb.w);
+    }
+    __syncthreads();
     float best_cost = __builtin_inff();
     int best_h = 0x7fffffff;
     float best_e[9];
@@ -415,18 +492,20 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
         } else if (!eight_point(P, idx, e)) {
             continue;
         }
-        int c = 0;
-        float cost = 0.f;
+        f2v acc = {0.f, 0.f};
+        const int m2 = PE_NOSCORE ? 0 : m / 2;
         int k = 0;
-        for (; k + 4 <= (PE_NOSCORE ? 0 : m); k += 4) {  // 4 LDS broadcast reads in flight per step
-            const float4 p0 = P[(k * step16) >> 16], p1 = P[((k + 1) * step16) >> 16];
-            const float4 p2 = P[((k + 2) * step16) >> 16], p3 = P[((k + 3) * step16) >> 16];
-            cost += msac_cost(e, p0, a.thr2, c);
-            cost += msac_cost(e, p1, a.thr2, c);
-            cost += msac_cost(e, p2, a.thr2, c);
-            cost += msac_cost(e, p3, a.thr2, c);
+        for (; k + 2 <= m2; k += 2) {  // 4 LDS broadcast reads in flight per step
+            const float4 A0 = s_sub[k][0], B0 = s_sub[k][1], A1 = s_sub[k + 1][0], B1 = s_sub[k + 1][1];
+            acc += msac_cost2(e, A0, B0, a.thr2);
+            acc += msac_cost2(e, A1, B1, a.thr2);
         }
-        for (; k < (PE_NOSCORE ? 0 : m); k++) cost += msac_cost(e, P[(k * step16) >> 16], a.thr2, c);
+        if (k < m2) acc += msac_cost2(e, s_sub[k][0], s_sub[k][1], a.thr2);
+        float cost = acc.x + acc.y;
+        if (!PE_NOSCORE && (m & 1)) {
+            int c = 0;
+            cost += msac_cost(e, P[((m - 1) * step16) >> 16], a.thr2, c);
+        }
         if (cost < best_cost || (cost == best_cost && h < best_h)) {
             best_cost = cost;
             best_h = h;
@@ -524,51 +603,69 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
 
     const long long tk3 = PE_TRACE ? clock64() : 0;
     // ---- 4. decomposition + cheirality ----
-    __shared__ double s_cand[4][12];
+    __shared__ float s_cand[4][12];
+    __shared__ float s_uv[2][3][3];
     if (t == 0) {
-        double Ed[9], U[3][3], V[3][3];
-        for (int r = 0; r < 9; r++) Ed[r] = E[r];
+        float U[3][3], V[3][3];
         if (PE_NODECOMP) {
             for (int i = 0; i < 3; i++)
                 for (int j = 0; j < 3; j++) U[i][j] = V[i][j] = i == j;
         } else {
-            essential_uv(Ed, U, V);
+            essential_uv(E, U, V);
         }
-        const double W[3][3] = {{0, -1, 0}, {1, 0, 0}, {0, 0, 1}};
-        for (int c = 0; c < 4; c++) {
-            double R[3][3];
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) {
+                s_uv[0][i][j] = U[i][j];
+                s_uv[1][i][j] = V[i][j];
+            }
+    }
+    __syncthreads();
+    if (t < 4) {  // candidate c = t, one lane each
+        const float W[3][3] = {{0, -1, 0}, {1, 0, 0}, {0, 0, 1}};
+        float U[3][3], V[3][3];
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) {
+                U[i][j] = s_uv[0][i][j];
+                V[i][j] = s_uv[1][i][j];
+            }
+        {
+            const int c = t;
+            float R[3][3];
             for (int i = 0; i < 3; i++)
                 for (int j = 0; j < 3; j++) {
-                    double s = 0;
+                    float s = 0;
                     for (int k = 0; k < 3; k++) {
-                        double uw = 0;
+                        float uw = 0;
                         for (int l = 0; l < 3; l++) uw += U[i][l] * (c < 2 ? W[l][k] : W[k][l]);
                         s += uw * V[j][k];
                     }
                     R[i][j] = s;
                 }
-            const double sg = (c & 1) ? -1.0 : 1.0;
+            const float sg = (c & 1) ? -1.f : 1.f;
             for (int i = 0; i < 9; i++) s_cand[c][i] = R[i / 3][i % 3];
             for (int i = 0; i < 3; i++) s_cand[c][9 + i] = sg * U[i][2];
         }
     }
     __syncthreads();
     int votes[4] = {0, 0, 0, 0};
-    for (int i = t; i < n; i += NT) {
-        const float4 p = P[i];
-        if (!sampson_inlier(E, p, a.thr2)) continue;
+    unsigned inl_mask = 0;  // bit k: correspondence t + k NT is a Sampson inlier of E (n <= 32 NT)
+    for (int i = t, k = 0; i < n; i += NT, k++)
+        inl_mask |= sampson_inlier(E, P[i], a.thr2) ? 1u << k : 0u;
 #pragma unroll
-        for (int c = 0; c < 4; c++) {
-            const double *C = s_cand[c];
-            D3 q = {{C[0] * p.x + C[1] * p.y + C[2], C[3] * p.x + C[4] * p.y + C[5], C[6] * p.x + C[7] * p.y + C[8]}};
-            D3 m = {{-(double)p.z, -(double)p.w, -1.0}};
-            D3 tt = {{C[9], C[10], C[11]}};
-            const double aa = dot3(q, q), ab = dot3(q, m), bb = dot3(m, m);
-            const double ra = -dot3(q, tt), rb = -dot3(m, tt);
-            const double det = aa * bb - ab * ab;
-            if (det <= 0) continue;
-            const double z1 = (ra * bb - ab * rb) / det, z2 = (aa * rb - ab * ra) / det;
-            votes[c] += (z1 > 0 && z2 > 0) ? 1 : 0;
+    for (int c = 0; c < 4; c++) {  // candidate-outer: 12 candidate floats live, not 48
+        for (unsigned mk = inl_mask; mk; mk &= mk - 1) {
+            const float4 p = P[t + __builtin_ctz(mk) * NT];
+            // depths z1, z2 of the midpoint triangulation, q z1 + t = -m z2 in the least-
+            // squares sense: z = num / det with det > 0, so only the numerators' signs count
+            const float *C = s_cand[c];
+            const F3 q = {{C[0] * p.x + C[1] * p.y + C[2], C[3] * p.x + C[4] * p.y + C[5], C[6] * p.x + C[7] * p.y + C[8]}};
+            const F3 m = {{-p.z, -p.w, -1.f}};
+            const F3 tt = {{C[9], C[10], C[11]}};
+            const float aa = dot3(q, q), ab = dot3(q, m), bb = dot3(m, m);
+            const float ra = -dot3(q, tt), rb = -dot3(m, tt);
+            const float det = aa * bb - ab * ab;
+            const float n1 = ra * bb - ab * rb, n2 = aa * rb - ab * ra;
+            votes[c] += (det > 0.f && n1 > 0.f && n2 > 0.f) ? 1 : 0;
         }
     }
     const long long tk4 = PE_TRACE ? clock64() : 0;
@@ -596,9 +693,9 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
     __shared__ float s_red[2][4][22];
     float R[9], tv[3], bs[6];  // the state: rotation, unit translation, tangent basis at t
 #pragma unroll
-    for (int i = 0; i < 9; i++) R[i] = (float)s_pose[i];
+    for (int i = 0; i < 9; i++) R[i] = s_pose[i];
 #pragma unroll
-    for (int i = 0; i < 3; i++) tv[i] = (float)s_pose[9 + i];
+    for (int i = 0; i < 3; i++) tv[i] = s_pose[9 + i];
     tangent_basis_f(tv, bs);
     const float th_max = sqrtf(a.thr2), th_min = 0.01f * th_max;
     float th = th_max;
