@@ -328,6 +328,42 @@ __device__ __forceinline__ void rodrigues_f(const float w[3], float R[3][3]) {
         }
 }
 
+// The 22 per-lane sums of one Gauss-Newton pass reduced over the wave by recursive
+// halving: at each xor level the lane keeps half of its (padded) values, the upper half
+// if its level bit is set, and adds its partner's partials of them.  Levels 32, 16, 8, 4,
+// 2 take 22 -> 11 -> 6 (of 12) -> 3 -> 2 (of 4) -> 1 values, level 1 finishes the pair.
+// Returns the full wave sum of value vi (vi = -1 for lanes left holding padding).
+template <int NV, int NK, int LVL>
+__device__ __forceinline__ void gn_halve(const float (&in)[NV], float (&out)[NK], bool hi) {
+#pragma unroll
+    for (int j = 0; j < NK; j++) {
+        const float lo_v = j < NV ? in[j] : 0.f, hi_v = NK + j < NV ? in[NK + j] : 0.f;
+        const float send = hi ? lo_v : hi_v, keep = hi ? hi_v : lo_v;
+        float recv;
+        if (LVL == 32)
+            recv = __shfl_xor(send, 32, 64);
+        else
+            recv = __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(send), (LVL << 10) | 0x1F));
+        out[j] = keep + recv;
+    }
+}
+__device__ __forceinline__ float gn_reduce_scatter22(const float (&acc)[22], int lane, int &vi) {
+    float b11[11], c6[6], d3[3], e2[2], f1[1];
+    const bool h5 = lane & 32, h4 = lane & 16, h3 = lane & 8, h2 = lane & 4, h1 = lane & 2;
+    gn_halve<22, 11, 32>(acc, b11, h5);
+    gn_halve<11, 6, 16>(b11, c6, h4);
+    gn_halve<6, 3, 8>(c6, d3, h3);
+    gn_halve<3, 2, 4>(d3, e2, h2);
+    gn_halve<2, 1, 2>(e2, f1, h1);
+    const float f = f1[0] + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(f1[0]), (1 << 10) | 0x1F));
+    // index held: within 22 by 11 h5; within 11 (as 12) by 6 h4; within 6 by 3 h3;
+    // within 3 (as 4) by 2 h2; within 2 by h1
+    const int i4 = (h2 ? 2 : 0) + (h1 ? 1 : 0);          // in the 3-group
+    const int i16 = (h4 ? 6 : 0) + (h3 ? 3 : 0) + i4;   // in the 11-group
+    vi = (i4 < 3 && i16 < 11) ? (h5 ? 11 : 0) + i16 : -1;
+    return f;
+}
+
 __device__ __forceinline__ int block_sum_i(int v, int *red) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -691,6 +727,7 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
     //         22 block sums (identical float ops in every lane): one block barrier per
     //         iteration (the partial sums are double-buffered), no broadcast of the update. ----
     __shared__ float s_red[2][4][22];
+    __shared__ float s_state[2][16];  // wave 0's update, double-buffered like s_red
     float R[9], tv[3], bs[6];  // the state: rotation, unit translation, tangent basis at t
 #pragma unroll
     for (int i = 0; i < 9; i++) R[i] = s_pose[i];
@@ -742,108 +779,115 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
             acc[20] += r * r;
             acc[21] += 1.f;
         }
-        // one block reduction of all 22 sums: wave shuffles, then 4 partials in LDS
-        // (levels outer, sums inner: 22 independent shuffles in flight per level)
-        if (!PE_NORED) {
-#pragma unroll
-            for (int k = 0; k < 22; k++) acc[k] += __shfl_xor(acc[k], 32, 64);
-#define PE_SWZ(O)                                                                            \
-    _Pragma("unroll") for (int k = 0; k < 22; k++) acc[k] += __int_as_float(                 \
-        __builtin_amdgcn_ds_swizzle(__float_as_int(acc[k]), ((O) << 10) | 0x1F))
-            PE_SWZ(16);
-            PE_SWZ(8);
-            PE_SWZ(4);
-            PE_SWZ(2);
-            PE_SWZ(1);
-#undef PE_SWZ
-        }
+        // the 22 sums reduced over the wave by recursive halving (a reduce-scatter: at
+        // level 2^L each lane keeps half of its values and receives its partner's partials
+        // of them, 94 VALU ops instead of 6 x 22 x 2), then 4 wave partials in LDS
         float(*red)[22] = s_red[it & 1];
-        if (lane < 22) {
-            float v = acc[0];
+        if (!PE_NORED) {
+            int vi;  // the sum this lane holds after the halving
+            const float f = gn_reduce_scatter22(acc, lane, vi);
+            if (vi >= 0) red[w][vi] = f;
+        } else if (lane < 22) {
+            red[w][lane] = acc[0];
+        }
+        __syncthreads();
+        // wave 0 solves (H + lambda diag H) d = -g and updates the state; the other waves
+        // take it from LDS after the second barrier (their VALU goes to the CU's other blocks)
+        float *st = s_state[it & 1];
+        if (w == 0 && !PE_NOSOLVE) {
+            float H[15], g[5];
 #pragma unroll
-            for (int k = 1; k < 22; k++) v = lane == k ? acc[k] : v;
-            red[w][lane] = v;
+            for (int k = 0; k < 15; k++) H[k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+#pragma unroll
+            for (int k = 0; k < 5; k++) g[k] = red[0][15 + k] + red[1][15 + k] + red[2][15 + k] + red[3][15 + k];
+            const float r2 = red[0][20] + red[1][20] + red[2][20] + red[3][20];
+            const float cnt = red[0][21] + red[1][21] + red[2][21] + red[3][21];
+            // float Cholesky on the native reciprocal square root (the step only has to be a
+            // descent direction); every loop fully unrolled: static register indexing
+            float A[5][5];
+#pragma unroll
+            for (int u = 0, k = 0; u < 5; u++)
+#pragma unroll
+                for (int v = u; v < 5; v++, k++) {
+                    A[u][v] = H[k];
+                    A[v][u] = H[k];
+                }
+#pragma unroll
+            for (int u = 0; u < 5; u++) A[u][u] = A[u][u] * (1.0f + 1e-6f) + 1e-30f;
+            float L[5][5] = {}, rl[5] = {};
+            bool ok = cnt >= 5.f;
+#pragma unroll
+            for (int i = 0; i < 5; i++)
+#pragma unroll
+                for (int j = 0; j <= i; j++) {
+                    float sum = A[i][j];
+#pragma unroll
+                    for (int m = 0; m < j; m++) sum -= L[i][m] * L[j][m];
+                    if (i == j) {
+                        ok = ok && sum > 0.f;
+                        rl[i] = __builtin_amdgcn_rsqf(fmaxf(sum, 1e-30f));  // 1 / L[i][i]
+                        L[i][i] = fmaxf(sum, 1e-30f) * rl[i];
+                    } else {
+                        L[i][j] = sum * rl[j];
+                    }
+                }
+            float y[5], d[5];
+#pragma unroll
+            for (int i = 0; i < 5; i++) {
+                float sum = -g[i];
+#pragma unroll
+                for (int m = 0; m < i; m++) sum -= L[i][m] * y[m];
+                y[i] = sum * rl[i];
+            }
+#pragma unroll
+            for (int i = 4; i >= 0; i--) {
+                float sum = y[i];
+#pragma unroll
+                for (int m = i + 1; m < 5; m++) sum -= L[m][i] * d[m];
+                d[i] = sum * rl[i];
+            }
+            float dR[3][3];
+            rodrigues_f(d, dR);
+            float Rn[9], tn[3];
+#pragma unroll
+            for (int i = 0; i < 3; i++)
+#pragma unroll
+                for (int j = 0; j < 3; j++)
+                    Rn[i * 3 + j] = dR[i][0] * R[0 * 3 + j] + dR[i][1] * R[1 * 3 + j] + dR[i][2] * R[2 * 3 + j];
+#pragma unroll
+            for (int i = 0; i < 3; i++) tn[i] = tv[i] + d[3] * bs[i] + d[4] * bs[3 + i];
+            const float rn = __builtin_amdgcn_rsqf(tn[0] * tn[0] + tn[1] * tn[1] + tn[2] * tn[2]);
+            const float th_new = fminf(th_max, fmaxf(3.f * sqrtf(r2 / cnt), th_min));
+            float dmax = 0.f;
+#pragma unroll
+            for (int i = 0; i < 5; i++) dmax = fmaxf(dmax, fabsf(d[i]));
+            // converged: a step below the float residual's resolution (1e-6 rad / unit-t, 100x
+            // under the 1e-4 tolerance) and an inlier band that moved < 0.1 %
+            const bool done = dmax < 1e-6f && fabsf(th_new - th) <= 1e-3f * th;
+            // lane k < 14 stores word k of the state (static register indexing):
+            // R (9), t (3), th, flags (bit 0: failed -- keep the old state; bit 1: converged)
+            if (lane < 14) {
+                float v = 0.f;
+#pragma unroll
+                for (int k = 0; k < 9; k++) v = lane == k ? Rn[k] : v;
+#pragma unroll
+                for (int k = 0; k < 3; k++) v = lane == 9 + k ? tn[k] * rn : v;
+                v = lane == 12 ? th_new : v;
+                v = lane == 13 ? __int_as_float((ok ? 0 : 1) | (done ? 2 : 0)) : v;
+                st[lane] = v;
+            }
         }
         __syncthreads();
         if (PE_NOSOLVE) continue;
-        float H[15], g[5];
+        const int flags = __float_as_int(st[13]);
+        if (flags & 1) break;  // the same decision in every thread
 #pragma unroll
-        for (int k = 0; k < 15; k++) H[k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+        for (int i = 0; i < 9; i++) R[i] = st[i];
 #pragma unroll
-        for (int k = 0; k < 5; k++) g[k] = red[0][15 + k] + red[1][15 + k] + red[2][15 + k] + red[3][15 + k];
-        const float r2 = red[0][20] + red[1][20] + red[2][20] + red[3][20];
-        const float cnt = red[0][21] + red[1][21] + red[2][21] + red[3][21];
-        // (H + lambda diag H) d = -g: float Cholesky on the native reciprocal square root (the
-        // step only has to be a descent direction); every loop fully unrolled: static register
-        // indexing, no private (scratch) arrays
-        float A[5][5];
-#pragma unroll
-        for (int u = 0, k = 0; u < 5; u++)
-#pragma unroll
-            for (int v = u; v < 5; v++, k++) {
-                A[u][v] = H[k];
-                A[v][u] = H[k];
-            }
-#pragma unroll
-        for (int u = 0; u < 5; u++) A[u][u] = A[u][u] * (1.0f + 1e-6f) + 1e-30f;
-        float L[5][5] = {}, rl[5] = {};
-        bool ok = cnt >= 5.f;
-#pragma unroll
-        for (int i = 0; i < 5; i++)
-#pragma unroll
-            for (int j = 0; j <= i; j++) {
-                float sum = A[i][j];
-#pragma unroll
-                for (int m = 0; m < j; m++) sum -= L[i][m] * L[j][m];
-                if (i == j) {
-                    ok = ok && sum > 0.f;
-                    rl[i] = __builtin_amdgcn_rsqf(fmaxf(sum, 1e-30f));  // 1 / L[i][i]
-                    L[i][i] = fmaxf(sum, 1e-30f) * rl[i];
-                } else {
-                    L[i][j] = sum * rl[j];
-                }
-            }
-        if (!ok) break;  // the same decision in every thread
-        float y[5], d[5];
-#pragma unroll
-        for (int i = 0; i < 5; i++) {
-            float sum = -g[i];
-#pragma unroll
-            for (int m = 0; m < i; m++) sum -= L[i][m] * y[m];
-            y[i] = sum * rl[i];
-        }
-#pragma unroll
-        for (int i = 4; i >= 0; i--) {
-            float sum = y[i];
-#pragma unroll
-            for (int m = i + 1; m < 5; m++) sum -= L[m][i] * d[m];
-            d[i] = sum * rl[i];
-        }
-        float dR[3][3];
-        rodrigues_f(d, dR);
-        float Rn[9], tn[3];
-#pragma unroll
-        for (int i = 0; i < 3; i++)
-#pragma unroll
-            for (int j = 0; j < 3; j++)
-                Rn[i * 3 + j] = dR[i][0] * R[0 * 3 + j] + dR[i][1] * R[1 * 3 + j] + dR[i][2] * R[2 * 3 + j];
-#pragma unroll
-        for (int i = 0; i < 3; i++) tn[i] = tv[i] + d[3] * bs[i] + d[4] * bs[3 + i];
-        const float rn = __builtin_amdgcn_rsqf(tn[0] * tn[0] + tn[1] * tn[1] + tn[2] * tn[2]);
-#pragma unroll
-        for (int i = 0; i < 9; i++) R[i] = Rn[i];
-#pragma unroll
-        for (int i = 0; i < 3; i++) tv[i] = tn[i] * rn;
+        for (int i = 0; i < 3; i++) tv[i] = st[9 + i];
         tangent_basis_f(tv, bs);
-        const float th_new = fminf(th_max, fmaxf(3.f * sqrtf(r2 / cnt), th_min));
-        float dmax = 0.f;
-#pragma unroll
-        for (int i = 0; i < 5; i++) dmax = fmaxf(dmax, fabsf(d[i]));
-        // converged: a step below the float residual's resolution (1e-6 rad / unit-t, 100x
-        // under the 1e-4 tolerance) and an inlier band that moved < 0.1 %
-        const bool done = dmax < 1e-6f && fabsf(th_new - th) <= 1e-3f * th;
-        th = th_new;
-        if (done) break;
+        th = st[12];
+        if (flags & 2) break;
     }
     {  // [R | t] row-major, thread t < 12 writes entry t (static register indexing)
         float v = 0.f;
