@@ -4,6 +4,7 @@ bytes per launch from FETCH_SIZE / WRITE_SIZE (MI355X_MICROARCH.md: FETCH_SIZE c
 the bytes of a 16-B/lane coalesced read -> x2; WRITE_SIZE exact for 16-B stores; units KB)."""
 import csv
 import glob
+import re
 import json
 import os
 import sys
@@ -27,12 +28,19 @@ def rows(pattern):
 
 
 stats = rows("trace/**/*kernel_stats.csv")
-def argval(flag, default):
+def bench_default(flag):
+    """bench.py's own argparse default for `flag` (the profile ran bench.py with these)."""
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")).read()
+    m = re.search(r'add_argument\("%s", type=int, default=(\d+)' % re.escape(flag), src)
+    return int(m.group(1))
+
+
+def argval(flag):
     toks = args.split()
-    return int(toks[toks.index(flag) + 1]) if flag in toks else default
+    return int(toks[toks.index(flag) + 1]) if flag in toks else bench_default(flag)
 
 
-summary = {"tag": tag, "bench_args": args, "batch": argval("--batch", 1024), "kp": argval("--kp", 1024),
+summary = {"tag": tag, "bench_args": args, "batch": argval("--batch"), "kp": argval("--kp"),
            "kernels": {}}
 for r in stats:
     name = r.get("Name", r.get("KernelName", "?"))
