@@ -35,6 +35,13 @@ constexpr int NMS_T = 1024;  // threads of the per-frame block
 #define KP_NCHW 0  // 1: sample the corners from NCHW directly (measured 2.09 ms vs 0.81 + 0.24 ms
                    // transposed, per 256 KITTI frames: 64 channel planes per gather)
 #endif
+#ifndef KP_EXP
+#define KP_EXP 0  // timing experiments only (wrong results): 1 no descriptor stores, 2 no plane copy, 3 no keypoint phase
+#endif
+#ifndef KP_TRANSPOSE
+#define KP_TRANSPOSE 0  // 1: always the NCHW->NHWC transpose + per-keypoint-wave sampling
+#endif
+constexpr int KP_PLANE_CELLS = 9216;  // cells whose 4 channel planes fit LDS (144 KiB): KITTI 47x155 = 7285
 constexpr int HN = 8;        // listed higher-priority neighbours per candidate
 constexpr int SORT_N = 4096; // survivors sorted in LDS (more: ranked by counting)
 __host__ __device__ inline long hn_cands(long P) { return (P + 7) / 8; }  // candidates with a list (more: rescanned)
@@ -52,12 +59,14 @@ struct KpScratch {
 };
 
 size_t a256(size_t x) { return mv::align_up(x, 256); }
+bool kp_planes_path(int Hc, int Wc) { return (long)Hc * Wc <= KP_PLANE_CELLS && !KP_TRANSPOSE && !KP_NCHW; }
 
 size_t kp_scratch_bytes(int B, int Hc, int Wc, int cap) {
     const size_t P = (size_t)Hc * Wc * 64;
     const size_t hnc = (size_t)hn_cands((long)P);
     return a256((size_t)B * P * 4) * 4 + a256((size_t)B * hnc * HN * 4) + a256((size_t)B * hnc * 4) +
-           a256((size_t)B * P) + a256((size_t)B * cap * 4) + a256((size_t)B * Hc * Wc * 256 * 4);
+           a256((size_t)B * P) + a256((size_t)B * cap * 4) +
+           (kp_planes_path(Hc, Wc) ? 0 : a256((size_t)B * Hc * Wc * 256 * 4));  // the NHWC copy
 }
 
 KpScratch kp_scratch_map(char *base, int B, int Hc, int Wc, int cap) {
@@ -396,6 +405,69 @@ __global__ __launch_bounds__(NMS_T) void k_kp_nms(int Hh, int Wh, int H, int W, 
     }
 }
 
+// grid_sample's coordinate arithmetic for a keypoint at heatmap pixel pix (row-major, Wh
+// wide): pairwise_pnp.py:245-246's normalisation to [-1, 1] (double, rounded to float),
+// torch's unnormalise (align_corners = False: one fma), floor, and the 4 corner weights
+__device__ __forceinline__ void kp_geometry(int pix, int Hc, int Wc, int H, int W, int Wh, int &x0, int &y0,
+                                            float w[4]) {
+    const double x = (double)(pix % Wh), y = (double)(pix / Wh);
+    const float gx = (float)(x / ((double)W / 2.) - 1.), gy = (float)(y / ((double)H / 2.) - 1.);
+    const float ix = fmaf(gx + 1.f, (float)Wc / 2.f, -0.5f), iy = fmaf(gy + 1.f, (float)Hc / 2.f, -0.5f);
+    const float x0f = floorf(ix), y0f = floorf(iy);
+    const float wx = ix - x0f, e = 1.f - wx, n = iy - y0f, s = 1.f - n;
+    w[0] = s * e;
+    w[1] = s * wx;
+    w[2] = n * e;
+    w[3] = n * wx;
+    x0 = (int)x0f;
+    y0 = (int)y0f;
+}
+
+// torch grid_sample's CPU arithmetic for 4 channels: a product, then an fma chain over the
+// other three corners (nw, ne, sw, se)
+__device__ __forceinline__ float4 kp_bilinear4(float4 a, float4 bq, float4 c, float4 dd, float wnw, float wne,
+                                               float wsw, float wse) {
+    float v[4];
+    const float *A = &a.x, *Bv = &bq.x, *C = &c.x, *Dv = &dd.x;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        float r = __fmul_rn(A[i], wnw);
+        r = fmaf(Bv[i], wne, r);
+        r = fmaf(C[i], wsw, r);
+        v[i] = fmaf(Dv[i], wse, r);
+    }
+    return make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// a wave's 256-channel row (lane holds channels 4 lane .. 4 lane + 3): L2 norm with the
+// reference's sequential sum of squares (numpy axis-0 reduce) in one lane, IEEE sqrt and
+// division, stored to out
+__device__ __forceinline__ void kp_normalize_store(float4 v, float *sq, float &nrm, int lane, float *out) {
+    sq[4 * lane + 0] = __fmul_rn(v.x, v.x);
+    sq[4 * lane + 1] = __fmul_rn(v.y, v.y);
+    sq[4 * lane + 2] = __fmul_rn(v.z, v.z);
+    sq[4 * lane + 3] = __fmul_rn(v.w, v.w);
+    // wave-local LDS hand-off (waves of the block retire independently: no block barrier)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane == 0) {
+        float ss = 0.f;
+        for (int ch = 0; ch < 256; ch++) ss = __fadd_rn(ss, sq[ch]);  // numpy's sequential axis-0 sum
+        nrm = sqrtf(ss);  // IEEE sqrt (-fhip-fp32-correctly-rounded-divide-sqrt; __fsqrt_rn is the native one here)
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const float m = nrm;
+    float4 o;
+    o.x = __fdiv_rn(v.x, m);
+    o.y = __fdiv_rn(v.y, m);
+    o.z = __fdiv_rn(v.z, m);
+    o.w = __fdiv_rn(v.w, m);
+    *reinterpret_cast<float4 *>(out + 4 * lane) = o;
+}
+
 // [B][256][HW] -> [B][HW][256], 64 x 64 tiles
 __global__ __launch_bounds__(256) void k_kp_nhwc(int HW, const float *__restrict__ in, float *__restrict__ out) {
     __shared__ float tile[64][65];
@@ -427,14 +499,10 @@ __global__ __launch_bounds__(256) void k_kp_sample(int B, int cap, int Hc, int W
     if (q >= (long)B * cap) return;
     const int b = (int)(q / cap), slot = (int)(q % cap);
     if (slot >= num_kp[b]) return;  // wave-uniform
-    const int pix = slot_pix[q];
-    const double x = (double)(pix % Wh), y = (double)(pix / Wh);
-    const float gx = (float)(x / ((double)W / 2.) - 1.), gy = (float)(y / ((double)H / 2.) - 1.);
-    const float ix = fmaf(gx + 1.f, (float)Wc / 2.f, -0.5f), iy = fmaf(gy + 1.f, (float)Hc / 2.f, -0.5f);
-    const float x0f = floorf(ix), y0f = floorf(iy);
-    const float wx = ix - x0f, e = 1.f - wx, n = iy - y0f, s = 1.f - n;
-    const float wnw = s * e, wne = s * wx, wsw = n * e, wse = n * wx;
-    const int x0 = (int)x0f, y0 = (int)y0f;
+    int x0, y0;
+    float w[4];
+    kp_geometry(slot_pix[q], Hc, Wc, H, W, Wh, x0, y0, w);
+    const float wnw = w[0], wne = w[1], wsw = w[2], wse = w[3];
     const float *D = nhwc + (long)b * Hc * Wc * 256 + (NCHW ? 4l * lane * Hc * Wc : 4 * lane);
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
     const long plane = (long)Hc * Wc;
@@ -447,37 +515,102 @@ __global__ __launch_bounds__(256) void k_kp_sample(int B, int cap, int Hc, int W
             return *reinterpret_cast<const float4 *>(D + ((long)yy * Wc + xx) * 256);
         }
     };
-    const float4 a = at(y0, x0), bq = at(y0, x0 + 1), c = at(y0 + 1, x0), dd = at(y0 + 1, x0 + 1);
-    float v[4];
-    const float *A = &a.x, *Bv = &bq.x, *C = &c.x, *Dv = &dd.x;
+    const float4 v = kp_bilinear4(at(y0, x0), at(y0, x0 + 1), at(y0 + 1, x0), at(y0 + 1, x0 + 1), wnw, wne, wsw, wse);
+    kp_normalize_store(v, sq[wv], nrm[wv], lane, desc + q * 256);
+}
+
+// 4 channels per workgroup, all keypoints of its frame: the channels' planes -- 4 Hc Wc
+// contiguous floats of the network's [256][Hc][Wc] output -- are copied once into LDS with
+// 16-B loads (16 in flight per thread: one workgroup per CU fills the LDS, so the bytes in
+// flight have to come from the loads themselves), and each keypoint's 4 raw bilinear values
+// are written to its descriptor row (16 B); k_kp_normalize then finishes the rows in place.
+// Replaces the NCHW->NHWC transpose (7.4 MB read + 7.4 MB written per KITTI frame) and the
+// 4 KiB corner reads per keypoint by one 7.4 MB read.  XCD-aware: the 8 channel quads that
+// share a 128-B line of every descriptor row run on one XCD (consecutively on it), so their
+// 16-B pieces merge in that XCD's L2 instead of leaving 8 partial lines.
+__global__ __launch_bounds__(256) void k_kp_sample_planes(int B, int cap, int Hc, int Wc, int H, int W, int Wh,
+                                                          const int *__restrict__ num_kp,
+                                                          const int *__restrict__ slot_pix,
+                                                          const float *__restrict__ coarse, float *__restrict__ desc) {
+    __shared__ __attribute__((aligned(16))) float plf[4 * KP_PLANE_CELLS + 4];
+    const int i = blockIdx.x, xcd = i & 7, k = i >> 3;
+    const int G = xcd + 8 * (k >> 3);  // (frame, group of 8 quads)
+    const int b = G >> 3, quad = ((G & 7) << 3) | (k & 7);
+    if (b >= B) return;
+    const int nk = min(num_kp[b], cap);
+    if (nk <= 0) return;  // block-uniform
+    const int HW = Hc * Wc, c0 = quad * 4, nf = 4 * HW;
+    // the first KPF slots of every thread: pixel loads issued and the bilinear geometry
+    // (grid_sample's unnormalise, floor, weights) computed before the plane copy, so that
+    // their latency hides under it
+    constexpr int KPF = 4;
+    int gx0[KPF], gy0[KPF];
+    float gw[KPF][4];  // nw, ne, sw, se
+    int gpix[KPF];
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        float r = __fmul_rn(A[i], wnw);
-        r = fmaf(Bv[i], wne, r);
-        r = fmaf(C[i], wsw, r);
-        r = fmaf(Dv[i], wse, r);
-        v[i] = r;
-        sq[wv][4 * lane + i] = __fmul_rn(r, r);
+    for (int u = 0; u < KPF; u++)  // branch-free (clamped) so the KPF loads are in flight together
+        gpix[u] = slot_pix[(long)b * cap + min((int)threadIdx.x + 256 * u, nk - 1)];
+#pragma unroll
+    for (int u = 0; u < KPF; u++) kp_geometry(gpix[u], Hc, Wc, H, W, Wh, gx0[u], gy0[u], gw[u]);
+    const float *I = coarse + ((long)b * 256 + c0) * HW;  // 4-B aligned
+    // I[h] is the first 16-B aligned float; I[f] goes to plf[f + o] with h + o in {0, 4}, so
+    // the aligned body lands on 16-B aligned LDS slots.  Head and tail (< 4 floats each) are
+    // copied one float at a time: nothing outside [I, I + nf) is read.
+    const int h = (int)(((16 - ((uintptr_t)I & 15)) & 15) >> 2), o = (4 - h) & 3;
+    const int n4 = (nf - h) >> 2, tail = nf - h - 4 * n4;
+    const float4 *G4 = reinterpret_cast<const float4 *>(I + h);
+    float4 *L4 = reinterpret_cast<float4 *>(plf + h + o);
+    // 16 loads in flight per thread to the end: past n4 the index is clamped, so a lane
+    // re-copies float4 n4 - 1 onto itself -- branch-free, or the compiler sinks each load
+    // into its store's branch and serialises them
+    for (int j = KP_EXP == 2 ? n4 : threadIdx.x; j < n4; j += 16 * 256) {
+        float4 t[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) t[u] = G4[min(j + u * 256, n4 - 1)];
+#pragma unroll
+        for (int u = 0; u < 16; u++) L4[min(j + u * 256, n4 - 1)] = t[u];
     }
-    // wave-local LDS hand-off (waves of the block retire independently: no block barrier)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (lane == 0) {
-        float ss = 0.f;
-        for (int ch = 0; ch < 256; ch++) ss = __fadd_rn(ss, sq[wv][ch]);  // numpy's sequential axis-0 sum
-        nrm[wv] = sqrtf(ss);  // IEEE sqrt (-fhip-fp32-correctly-rounded-divide-sqrt; __fsqrt_rn is the native one here)
+    if (threadIdx.x < h) plf[threadIdx.x + o] = I[threadIdx.x];
+    if (threadIdx.x < tail) plf[h + 4 * n4 + o + threadIdx.x] = I[h + 4 * n4 + threadIdx.x];
+    __syncthreads();
+    if (KP_EXP == 3) return;
+    const float *L = plf + o;  // plane c of the quad: L + c HW
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto at = [&](int yy, int xx) {
+        if (!(xx >= 0 && xx < Wc && yy >= 0 && yy < Hc)) return z;
+        const float *c = L + yy * Wc + xx;
+        return make_float4(c[0], c[HW], c[2 * HW], c[3 * HW]);
+    };
+    auto emit = [&](int slot, int x0, int y0, const float *w) {
+        const float4 v = kp_bilinear4(at(y0, x0), at(y0, x0 + 1), at(y0 + 1, x0), at(y0 + 1, x0 + 1), w[0], w[1],
+                                      w[2], w[3]);
+        if (KP_EXP != 1 || v.x == 1234.5f) *reinterpret_cast<float4 *>(desc + ((long)b * cap + slot) * 256 + c0) = v;
+    };
+#pragma unroll
+    for (int u = 0; u < KPF; u++) {
+        const int slot = threadIdx.x + 256 * u;
+        if (slot < nk) emit(slot, gx0[u], gy0[u], gw[u]);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const float m = nrm[wv];
-    float4 o;
-    o.x = __fdiv_rn(v[0], m);
-    o.y = __fdiv_rn(v[1], m);
-    o.z = __fdiv_rn(v[2], m);
-    o.w = __fdiv_rn(v[3], m);
-    *reinterpret_cast<float4 *>(desc + q * 256 + 4 * lane) = o;
+    for (int slot = threadIdx.x + 256 * KPF; slot < nk; slot += 256) {  // cap > 1024
+        int x0, y0;
+        float w[4];
+        kp_geometry(slot_pix[(long)b * cap + slot], Hc, Wc, H, W, Wh, x0, y0, w);
+        emit(slot, x0, y0, w);
+    }
+}
+
+// one wave per keypoint: the raw row written by k_kp_sample_planes, normalised in place
+__global__ __launch_bounds__(256) void k_kp_normalize(int B, int cap, const int *__restrict__ num_kp,
+                                                      float *__restrict__ desc) {
+    __shared__ float sq[4][256];
+    __shared__ float nrm[4];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const long q = (long)blockIdx.x * 4 + wv;
+    if (q >= (long)B * cap) return;
+    const int b = (int)(q / cap), slot = (int)(q % cap);
+    if (slot >= num_kp[b]) return;  // wave-uniform
+    const float4 v = *reinterpret_cast<const float4 *>(desc + q * 256 + 4 * lane);
+    kp_normalize_store(v, sq[wv], nrm[wv], lane, desc + q * 256);
 }
 
 }  // namespace
@@ -515,6 +648,20 @@ extern "C" int mv_keypoints_dev(mv_context *ctx, const mv_kp_params *p, int batc
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     const int HW = Hc * Wc;
+    const long waves = (long)batch * cap;
+    if (kp_planes_path(Hc, Wc)) {
+        MV_PROF_BEGIN(s, "k_kp_sample_planes");
+        hipLaunchKernelGGL(k_kp_sample_planes, dim3((unsigned)batch * 64), dim3(256), 0, s, batch, cap, Hc, Wc, H, W,
+                           Wc * 8, num_kp, m.slot_pix, coarse_desc, desc);
+        MV_PROF_END(s);
+        MV_LAUNCH_CHECK();
+        MV_PROF_BEGIN(s, "k_kp_normalize");
+        hipLaunchKernelGGL(k_kp_normalize, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, batch, cap, num_kp,
+                           desc);
+        MV_PROF_END(s);
+        MV_LAUNCH_CHECK();
+        return mv::set_status(MV_OK);
+    }
     if (!KP_NCHW) {
         MV_PROF_BEGIN(s, "k_kp_nhwc");
         hipLaunchKernelGGL(k_kp_nhwc, dim3((unsigned)((HW + 63) / 64), 4, (unsigned)batch), dim3(256), 0, s, HW,
@@ -522,7 +669,6 @@ extern "C" int mv_keypoints_dev(mv_context *ctx, const mv_kp_params *p, int batc
         MV_PROF_END(s);
         MV_LAUNCH_CHECK();
     }
-    const long waves = (long)batch * cap;
     MV_PROF_BEGIN(s, "k_kp_sample");
     hipLaunchKernelGGL(k_kp_sample<KP_NCHW != 0>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, batch, cap, Hc,
                        Wc, H, W, Wc * 8, num_kp, m.slot_pix, KP_NCHW ? coarse_desc : m.nhwc, desc);

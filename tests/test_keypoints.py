@@ -139,6 +139,19 @@ def test_gpu_keypoints_batch_cap_and_edges(ctx, orc, torch_cuda):
 
 
 @pytest.mark.gpu
+def test_gpu_keypoints_large_frame_transpose_path(ctx, orc, torch_cuda):
+    """frames above the 9216 cells whose 4-channel planes fit LDS take the NCHW->NHWC
+    transpose + per-keypoint sampling path: the same bits."""
+    frames = [synth.synth_superpoint_outputs(50 + i, 60, 160) for i in range(2)]
+    n, kp, conf, dd, st = _gpu_batch(ctx, torch_cuda, frames, 480, 1280, 1024)
+    for b, (s_, d_) in enumerate(frames):
+        pts, d, _ = orc.keypoints(s_, d_, 480, 1280)
+        k = min(1024, pts.shape[0])
+        assert n[b] == k and k > 100, b
+        assert (kp[b, :k] == pts[:k, :2]).all() and (dd[b, :k].view(np.int32) == d[:k].view(np.int32)).all(), b
+
+
+@pytest.mark.gpu
 def test_gpu_keypoints_feed_allpairs(ctx, orc, torch_cuda):
     """image pair -> keypoints -> all-pairs match on the device, end to end against the oracle."""
     torch = torch_cuda

@@ -76,9 +76,10 @@ def run(batch=256, steps=10, warmup=2, distinct=8, check=1, cpu_seconds=0.0, cap
     el = time.perf_counter() - t0
     mvtrack.profile_enable(False)
     stages = {}
-    for k in ("k_kp_heat", "k_kp_nms", "k_kp_nhwc", "k_kp_sample"):
+    for k in ("k_kp_heat", "k_kp_nms", "k_kp_sample_planes", "k_kp_normalize", "k_kp_nhwc", "k_kp_sample"):
         ms, c = mvtrack.profile_query(k)
-        stages[k] = round(ms / max(c, 1), 4)
+        if c:  # the planes path (frames up to 9216 cells) or the transpose path
+            stages[k] = round(ms / c, 4)
     checked = 0
     if check:
         import oracle
