@@ -32,7 +32,8 @@ void mv_kp_params_default(mv_kp_params *p);
  * Outputs per frame b: num_kp[b] keypoints (at most cap: the cap most confident, a prefix of
  * the reference's list; status[b] = MV_ERR_CAPACITY when more survived), kp [B][cap][2]
  * (x, y pixels), conf [B][cap], desc [B][cap][256] unit rows.  heat (may be NULL):
- * [B][Hc*8][Wc*8] heatmap.  Rows past num_kp are not written. */
+ * [B][Hc*8][Wc*8] heatmap.  Rows past num_kp are not written.  Alignment: coarse_desc 4 B,
+ * desc and heat 16 B (MV_ERR_INVALID_ARG otherwise). */
 int mv_keypoints_dev(mv_context *ctx, const mv_kp_params *p, int batch, int Hc, int Wc, int H, int W,
                      const float *semi, const float *coarse_desc, int cap, int *num_kp, float *kp, float *conf,
                      float *desc, float *heat, int *status);

@@ -38,10 +38,18 @@ constexpr int NMS_T = 1024;  // threads of the per-frame block
 #ifndef KP_EXP
 #define KP_EXP 0  // timing experiments only (wrong results): 1 no descriptor stores, 2 no plane copy, 3 no keypoint phase
 #endif
+#ifndef KP_TRACE
+#define KP_TRACE 0  // printf k_kp_nms's per-phase clock64() deltas for frame 0 (timing only)
+#endif
 #ifndef KP_TRANSPOSE
 #define KP_TRANSPOSE 0  // 1: always the NCHW->NHWC transpose + per-keypoint-wave sampling
 #endif
 constexpr int KP_PLANE_CELLS = 9216;  // cells whose 4 channel planes fit LDS (144 KiB): KITTI 47x155 = 7285
+constexpr int NC_LDS = 8192;  // candidates per frame held in LDS (more: the global per-pixel path)
+constexpr int ROW_LDS = 2048; // heat rows indexed in LDS
+#ifndef KP_NMS_GLOBAL
+#define KP_NMS_GLOBAL 0  // 1: always the global per-pixel path (the LDS path's timing baseline)
+#endif
 constexpr int HN = 8;        // listed higher-priority neighbours per candidate
 constexpr int SORT_N = 4096; // survivors sorted in LDS (more: ranked by counting)
 __host__ __device__ inline long hn_cands(long P) { return (P + 7) / 8; }  // candidates with a list (more: rescanned)
@@ -178,6 +186,59 @@ __device__ int list_higher_any(const float *__restrict__ heat, int Hh, int Wh, f
     return cnt;
 }
 
+// The same window queries against the candidate list held in LDS (row-major pixel order,
+// row r's candidates at ids [s_row[r], s_row[r + 1])): per window row a binary search for
+// the first column >= xk - d, then a scan to xk + d -- LDS reads instead of the (2d+1)^2
+// scattered heat loads per candidate (each a 64-line gather per wave instruction).
+// list: the higher-priority candidates' ids (the first HN to out), their count returned.
+__device__ int list_higher_lds(const int *s_cp, const float *s_cc, const int *s_row, int Hh, int Wh, int d, int k,
+                               int pk, float ck, int *__restrict__ out) {
+    const int yk = pk / Wh, xk = pk % Wh, xa = max(xk - d, 0), xb = min(xk + d, Wh - 1);
+    int cnt = 0;
+    for (int yy = max(yk - d, 0); yy <= min(yk + d, Hh - 1); yy++) {
+        int lo = s_row[yy], hi = s_row[yy + 1];
+        const int end = hi, pa = yy * Wh + xa, pb = yy * Wh + xb;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s_cp[mid] < pa) lo = mid + 1;
+            else hi = mid;
+        }
+        for (int j = lo; j < end; j++) {
+            const int pj = s_cp[j];
+            if (pj > pb) break;
+            if (j != k && before(s_cc[j], pj, ck, pk)) {
+                if (out && cnt < HN) out[cnt] = j;
+                cnt++;
+            }
+        }
+    }
+    return cnt;
+}
+
+// rescan (more than HN higher-priority neighbours): any of them kept / still undecided
+__device__ void rescan_higher_lds(const int *s_cp, const float *s_cc, const int *s_row, const unsigned char *s_st,
+                                  int Hh, int Wh, int d, int k, int pk, float ck, bool &supp, bool &blocked) {
+    const int yk = pk / Wh, xk = pk % Wh, xa = max(xk - d, 0), xb = min(xk + d, Wh - 1);
+    for (int yy = max(yk - d, 0); yy <= min(yk + d, Hh - 1); yy++) {
+        int lo = s_row[yy], hi = s_row[yy + 1];
+        const int end = hi, pa = yy * Wh + xa, pb = yy * Wh + xb;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s_cp[mid] < pa) lo = mid + 1;
+            else hi = mid;
+        }
+        for (int j = lo; j < end; j++) {
+            const int pj = s_cp[j];
+            if (pj > pb) break;
+            if (j != k && before(s_cc[j], pj, ck, pk)) {
+                const unsigned char sj = __atomic_load_n(&s_st[j], __ATOMIC_RELAXED);
+                supp |= sj == 1;
+                blocked |= sj == 0;
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(NMS_T) void k_kp_nms(int Hh, int Wh, int H, int W, float thresh, int nms_dist,
                                                   int border, int cap, const float *__restrict__ heat_all,
                                                   int *__restrict__ hn_all, int *__restrict__ hc_all,
@@ -189,6 +250,10 @@ __global__ __launch_bounds__(NMS_T) void k_kp_nms(int Hh, int Wh, int H, int W, 
     __shared__ int wsum[NMS_T / 64];
     __shared__ int s_base, s_flag, s_nk;
     __shared__ unsigned long long skey[SORT_N];  // bitonic keys (or the rank tiles)
+    __shared__ int s_cp[NC_LDS];                 // LDS path: candidate pixels (row-major order)
+    __shared__ float s_cc[NC_LDS];               //           their confidences
+    __shared__ int s_row[ROW_LDS + 1];           //           first candidate id of each heat row
+    __shared__ unsigned char s_st[NC_LDS];       //           state per candidate id
     const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
     const long P = (long)Hh * Wh;
     const float *heat = heat_all + b * P;
@@ -201,21 +266,48 @@ __global__ __launch_bounds__(NMS_T) void k_kp_nms(int Hh, int Wh, int H, int W, 
     int *kept = kept_all + b * P;
     int *slot_pix = slot_pix_all + (long)b * cap;
 
-    // (a) row-major compaction of the candidates: wave w owns a contiguous chunk of pixels;
-    //     count (ballots, 4 groups of 64 pixels in flight), one block scan, then write
-    constexpr int NWV = NMS_T / 64;
-    const long cw = ((P + NWV * 256 - 1) / (NWV * 256)) * 256;  // pixels per wave, multiple of 256
-    const long q0 = min(P, (long)w * cw), q1 = min(P, q0 + cw);
+    // (a) row-major compaction of the candidates in ONE pass over the heatmap: wave w owns a
+    //     contiguous chunk of pixels, reads it with 8 float4 loads per lane in flight (a
+    //     heatmap is ~1.9 MB per KITTI frame and one 1024-thread block per frame per CU has
+    //     to keep that many bytes in flight), and writes its candidates in pixel order to its
+    //     own segment of two scratch arrays free at this point (kept: pixel, hn: confidence
+    //     bits); after the block scan each wave moves its segment to its final ids
+    const long long tk0 = KP_TRACE ? clock64() : 0;
+    constexpr int NWV = NMS_T / 64, CU_ = 8;
+    const long cw = ((P + NWV * 256 * CU_ - 1) / (NWV * 256 * CU_)) * (256 * CU_);  // pixels per wave
+    const long q0 = min(P, (long)w * cw), q1 = min(P, q0 + cw);  // multiples of 4 (P = 64 Hc Wc)
+    int *spix = kept + q0;
+    float *sconf = reinterpret_cast<float *>(hn) + q0;  // hn holds >= P ints
+    const unsigned long long lt = (1ull << lane) - 1ull;
     int cntw = 0;
-    for (long p0 = q0; p0 < q1; p0 += 256) {
-        float h[4];
+    for (long p0 = q0; p0 < q1; p0 += 256 * CU_) {
+        float4 h[CU_];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const long p = p0 + 64 * u + lane;
-            h[u] = p < q1 ? heat[p] : __builtin_nanf("");
+        for (int u = 0; u < CU_; u++)  // clamped: branch-free, so all CU_ loads are in flight
+            h[u] = *reinterpret_cast<const float4 *>(heat + min(p0 + 256 * u + 4 * lane, q1 - 4));
+#pragma unroll
+        for (int u = 0; u < CU_; u++) {
+            const long p = p0 + 256 * u + 4 * lane;
+            const bool v = p < q1;
+            const float hv[4] = {h[u].x, h[u].y, h[u].z, h[u].w};
+            unsigned long long m[4];
+            int r = cntw;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                m[e] = __ballot(v && hv[e] >= thresh);
+                r += __popcll(m[e] & lt);  // candidates of lower lanes (pixels p0 + 256 u + < 4 lane)
+            }
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                if (v && hv[e] >= thresh) {
+                    spix[r] = (int)(p + e);
+                    sconf[r] = hv[e];
+                    st[p + e] = 0;
+                    r++;
+                }
+                cntw += __popcll(m[e]);
+            }
         }
-#pragma unroll
-        for (int u = 0; u < 4; u++) cntw += __popcll(__ballot(h[u] >= thresh));
     }
     if (lane == 0) wsum[w] = cntw;
     __syncthreads();
@@ -229,27 +321,32 @@ __global__ __launch_bounds__(NMS_T) void k_kp_nms(int Hh, int Wh, int H, int W, 
         s_base = acc;
     }
     __syncthreads();
+    const bool lds_path = s_base <= NC_LDS && Hh <= ROW_LDS && !KP_NMS_GLOBAL;  // block-uniform
     {
-        int off = wsum[w];
-        for (long p0 = q0; p0 < q1; p0 += 256) {
-            float h[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const long p = p0 + 64 * u + lane;
-                h[u] = p < q1 ? heat[p] : __builtin_nanf("");
+        const int off = wsum[w];
+        for (int i = lane; i < cntw; i += 64) {
+            const int pp = spix[i];
+            const float cc = sconf[i];
+            cpix[off + i] = pp;
+            cconf[off + i] = cc;
+            if (lds_path) {
+                s_cp[off + i] = pp;
+                s_cc[off + i] = cc;
+                s_st[off + i] = 0;
             }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const bool c = h[u] >= thresh;
-                const unsigned long long m = __ballot(c);
-                if (c) {
-                    const long p = p0 + 64 * u + lane;
-                    const int id = off + __popcll(m & ((1ull << lane) - 1ull));
-                    cpix[id] = (int)p;
-                    cconf[id] = h[u];
-                    st[p] = 0;
-                }
-                off += __popcll(m);
+        }
+    }
+    if (lds_path) {  // row index: s_row[y] = first id whose row is >= y (candidates are row-major)
+        __syncthreads();
+        const int ncl = s_base;
+        if (ncl == 0) {
+            for (int y = t; y <= Hh; y += NMS_T) s_row[y] = 0;
+        } else {
+            for (int k = t; k < ncl; k += NMS_T) {
+                const int r = s_cp[k] / Wh, rp = k > 0 ? s_cp[k - 1] / Wh : -1;
+                for (int y = rp + 1; y <= r; y++) s_row[y] = k;
+                if (k == ncl - 1)
+                    for (int y = r + 1; y <= Hh; y++) s_row[y] = ncl;
             }
         }
     }
@@ -262,25 +359,35 @@ __global__ __launch_bounds__(NMS_T) void k_kp_nms(int Hh, int Wh, int H, int W, 
     //     keeps those without any; later rounds only read the listed neighbours' states.
     const int d = nms_dist;
     __syncthreads();
+    const long long tk1 = KP_TRACE ? clock64() : 0;
     for (int k = t; k < nc; k += NMS_T) {
         const int pk = cpix[k];
         const float ck = cconf[k];
         int cnt = 0;
         int *out = k < HNC ? hn + (long)k * HN : nullptr;
-        if (d == 4)
+        if (lds_path)
+            cnt = list_higher_lds(s_cp, s_cc, s_row, Hh, Wh, d, k, pk, ck, out);  // ids, not pixels
+        else if (d == 4)
             cnt = list_higher<4>(heat, Hh, Wh, thresh, pk, ck, out);
         else
             cnt = list_higher_any(heat, Hh, Wh, thresh, d, pk, ck, out);
         if (k < HNC) hcnt[k] = cnt;  // > HN: the list is partial, rescanned each round
-        if (cnt == 0) st[pk] = 1;
+        if (cnt == 0) {
+            if (lds_path) s_st[k] = 1;
+            else st[pk] = 1;
+        }
     }
+    int rounds = 0;
+    __syncthreads();
+    const long long tk2 = KP_TRACE ? clock64() : 0;
     for (;;) {
+        rounds++;
         if (t == 0) s_flag = 0;
         __syncthreads();
         int undecided = 0;
         for (int k = t; k < nc; k += NMS_T) {
-            const int pk = cpix[k];
-            if (st[pk] != 0) continue;
+            const int pk = lds_path ? s_cp[k] : cpix[k];
+            if ((lds_path ? s_st[k] : st[pk]) != 0) continue;
             bool supp = false, blocked = false;
             const int c = k < HNC ? hcnt[k] : HN + 1;
             if (c <= HN) {
@@ -290,10 +397,13 @@ __global__ __launch_bounds__(NMS_T) void k_kp_nms(int Hh, int Wh, int H, int W, 
 #pragma unroll
                 for (int i = 0; i < HN; i++) {
                     if (q[i] < 0) continue;
-                    const unsigned char sj = __atomic_load_n(&st[q[i]], __ATOMIC_RELAXED);
+                    const unsigned char sj = lds_path ? __atomic_load_n(&s_st[q[i]], __ATOMIC_RELAXED)
+                                                      : __atomic_load_n(&st[q[i]], __ATOMIC_RELAXED);
                     supp |= sj == 1;
                     blocked |= sj == 0;
                 }
+            } else if (lds_path) {
+                rescan_higher_lds(s_cp, s_cc, s_row, s_st, Hh, Wh, d, k, pk, s_cc[k], supp, blocked);
             } else {  // more than HN higher neighbours: rescan the window
                 const float ck = cconf[k];
                 const int yk = pk / Wh, xk = pk % Wh;
@@ -307,12 +417,13 @@ __global__ __launch_bounds__(NMS_T) void k_kp_nms(int Hh, int Wh, int H, int W, 
                         blocked |= sj == 0;
                     }
             }
-            if (supp)
-                st[pk] = 2;
-            else if (!blocked)
-                st[pk] = 1;
-            else
+            const unsigned char ns = supp ? 2 : (!blocked ? 1 : 0);
+            if (ns == 0)
                 undecided = 1;
+            else if (lds_path)
+                s_st[k] = ns;
+            else
+                st[pk] = ns;
         }
         if (undecided) s_flag = 1;
         __syncthreads();
@@ -320,11 +431,12 @@ __global__ __launch_bounds__(NMS_T) void k_kp_nms(int Hh, int Wh, int H, int W, 
     }
 
     // (c) survivors inside the border; slot = rank (confidence desc, ties reversed row-major)
+    const long long tk3 = KP_TRACE ? clock64() : 0;
     if (t == 0) s_nk = 0;
     __syncthreads();
     for (int k = t; k < nc; k += NMS_T) {
         const int p = cpix[k], y = p / Wh, x = p % Wh;
-        if (st[p] != 1) continue;
+        if ((lds_path ? s_st[k] : st[p]) != 1) continue;
         if (x < border || x >= W - border || y < border || y >= H - border) continue;
         kept[atomicAdd(&s_nk, 1)] = k;
     }
@@ -403,6 +515,9 @@ __global__ __launch_bounds__(NMS_T) void k_kp_nms(int Hh, int Wh, int H, int W, 
         num_kp[b] = min(nk, cap);
         status[b] = nk > cap ? MV_ERR_CAPACITY : MV_OK;
     }
+    if (KP_TRACE && b == 0 && t == 0)
+        printf("nms phases (clk): compact %lld list %lld rounds %lld (%d) survivors+sort %lld  nc %d nk %d\n",
+               tk1 - tk0, tk2 - tk1, tk3 - tk2, rounds, clock64() - tk3, nc, nk);
 }
 
 // grid_sample's coordinate arithmetic for a keypoint at heatmap pixel pix (row-major, Wh
@@ -629,7 +744,7 @@ extern "C" int mv_keypoints_dev(mv_context *ctx, const mv_kp_params *p, int batc
                desc && status);
     MV_REQUIRE(Hc * 8 <= H && Wc * 8 <= W && p->nms_dist >= 0 && p->border >= 0);
     MV_REQUIRE((long)Hc * Wc * 64 < (1l << 30) && (long)batch * cap < (1l << 31));
-    MV_REQUIRE(((uintptr_t)coarse_desc & 3) == 0 && ((uintptr_t)desc & 15) == 0);
+    MV_REQUIRE(((uintptr_t)coarse_desc & 3) == 0 && ((uintptr_t)desc & 15) == 0 && ((uintptr_t)heat & 15) == 0);
     MV_HIP_TRY(hipSetDevice(ctx->device));
     char *scr = (char *)mv::scratch(ctx, kp_scratch_bytes(batch, Hc, Wc, cap));
     if (!scr) return MV_ERR_OUT_OF_MEMORY;

@@ -152,6 +152,24 @@ def test_gpu_keypoints_large_frame_transpose_path(ctx, orc, torch_cuda):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("Hc,Wc,p_corner,dustbin,nc_lo,nc_hi", [(12, 16, 0.0, -5.0, 3000, 8192),
+                                                               (47, 155, 1.0, 2.0, 8193, 10 ** 6)])
+def test_gpu_keypoints_dense_candidates(ctx, orc, torch_cuda, Hc, Wc, p_corner, dustbin, nc_lo, nc_hi):
+    """dense candidate fields: a third of the pixels above threshold (most candidates have
+    more than 8 higher-priority neighbours: the window rescans, many rounds) within the 8192
+    candidates the NMS keeps in LDS, and more than 8192 (the global per-pixel path)."""
+    s_, d_ = synth.synth_superpoint_outputs(7, Hc, Wc, p_corner=p_corner, dustbin=dustbin)
+    H, W = Hc * 8, Wc * 8
+    pts, d, heat = orc.keypoints(s_, d_, H, W)
+    assert nc_lo <= int((heat >= 0.015).sum()) <= nc_hi  # the path this case is for
+    n, kp, conf, dd, st = _gpu_batch(ctx, torch_cuda, [(s_, d_)], H, W, 8192)
+    k = pts.shape[0]
+    assert n[0] == k and st[0] == 0
+    assert (kp[0, :k] == pts[:, :2]).all() and (conf[0, :k].view(np.int32) == pts[:, 2].view(np.int32)).all()
+    assert (dd[0, :k].view(np.int32) == d.view(np.int32)).all()
+
+
+@pytest.mark.gpu
 def test_gpu_keypoints_feed_allpairs(ctx, orc, torch_cuda):
     """image pair -> keypoints -> all-pairs match on the device, end to end against the oracle."""
     torch = torch_cuda
