@@ -107,6 +107,16 @@ template <int N>
 __device__ __forceinline__ void wait_vm_q8() {
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
+typedef float f2q __attribute__((ext_vector_type(2)));
+#ifndef Q8_PKFMA
+#define Q8_PKFMA 0  // 1: dequantise two rows per v_pk_fma_f32 (measured 2.47 vs 2.42 ms: not kept)
+#endif
+// d = a * r + c on both halves (one issue): v_pk_fma_f32, inline so it is never scalarised
+__device__ __forceinline__ f2q pkfma_q8(f2q a, f2q r, f2q c) {
+    f2q d;
+    asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(r), "v"(c));
+    return d;
+}
 __device__ __forceinline__ float tag_q8(float f, unsigned keep, unsigned tag) {
     float r;
     asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(keep), "s"(tag));
@@ -489,15 +499,32 @@ __device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *
     // (the fold of one group never waits on the MFMAs in flight), with one accumulator set.
     // The B fragments are read from LDS once per group (2 ds_read_b128 per MFMA pair).
     // fold rows 2 S, 2 S + 1 of group FG (tile tags G0, G0 + 1; scales R, offsets C)
+#if Q8_PKFMA
+    // rows 2 S and 2 S + 1 of a half share the lane's column, hence its scale and offset: one
+    // v_pk_fma_f32 (splat operands) dequantises both (adjacent accumulator registers)
+#define Q8_FOLD2(FG, S, G0, R0, R1, C0, C1)                                                  \
+    do {                                                                                     \
+        const f2q a2_ = pkfma_q8(                                                            \
+            f2q{__int_as_float(acc[FG][0][2 * (S)]), __int_as_float(acc[FG][0][2 * (S) + 1])}, (R0), (C0)); \
+        const f2q b2_ = pkfma_q8(                                                            \
+            f2q{__int_as_float(acc[FG][1][2 * (S)]), __int_as_float(acc[FG][1][2 * (S) + 1])}, (R1), (C1)); \
+        _Pragma("unroll") for (int u_ = 0; u_ < 2; u_++) {                                   \
+            const int q = 2 * (S) + u_;                                                      \
+            if (Q8_EXP_NOFOLD && q != 0) continue;                                           \
+            fold3_q8(tag_q8(a2_[u_], vkeep, (G0)), tag_q8(b2_[u_], vkeep, (G0) + 1u), m1[FG][q], m2[FG][q]); \
+        }                                                                                    \
+    } while (0)
+#else
 #define Q8_FOLD2(FG, S, G0, R0, R1, C0, C1)                                                  \
     do {                                                                                     \
         _Pragma("unroll") for (int q = 2 * (S); q < 2 * (S) + 2; q++) {                      \
             if (Q8_EXP_NOFOLD && q != 0) continue;                                           \
-            const float a_ = __builtin_fmaf(__int_as_float(acc[FG][0][q]), (R0), (C0));      \
-            const float b_ = __builtin_fmaf(__int_as_float(acc[FG][1][q]), (R1), (C1));      \
+            const float a_ = __builtin_fmaf(__int_as_float(acc[FG][0][q]), (R0).x, (C0).x);  \
+            const float b_ = __builtin_fmaf(__int_as_float(acc[FG][1][q]), (R1).x, (C1).x);  \
             fold3_q8(tag_q8(a_, vkeep, (G0)), tag_q8(b_, vkeep, (G0) + 1u), m1[FG][q], m2[FG][q]); \
         }                                                                                    \
     } while (0)
+#endif
     // group G's MFMAs on slot J (fragments read PF k32 steps ahead), folding group FG meanwhile
 #define Q8_SEG(J, G, FG, G0, R0, R1, C0, C1)                                                 \
     do {                                                                                     \
@@ -541,10 +568,14 @@ __device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *
             const float *rl_ = reinterpret_cast<const float *>(lds + (J) * Q_SLOT + Q_TILE); \
             const int col_ = tc * Q_BN + fr;                                                 \
             const float s0_ = rl_[fr], s1_ = rl_[fr + 32];                                   \
-            pr0 = col_ < n1 ? 2097152.0f * s0_ : 0.f;                                        \
-            pr1 = col_ + 32 < n1 ? 2097152.0f * s1_ : 0.f;                                   \
-            pc0 = col_ < n1 ? -8388608.0f * s0_ : -3.0e38f;                                  \
-            pc1 = col_ + 32 < n1 ? -8388608.0f * s1_ : -3.0e38f;                             \
+            const float r0_ = col_ < n1 ? 2097152.0f * s0_ : 0.f;                            \
+            const float r1_ = col_ + 32 < n1 ? 2097152.0f * s1_ : 0.f;                       \
+            const float c0_ = col_ < n1 ? -8388608.0f * s0_ : -3.0e38f;                      \
+            const float c1_ = col_ + 32 < n1 ? -8388608.0f * s1_ : -3.0e38f;                 \
+            pr0 = f2q{r0_, r0_};                                                             \
+            pr1 = f2q{r1_, r1_};                                                             \
+            pc0 = f2q{c0_, c0_};                                                             \
+            pc1 = f2q{c1_, c1_};                                                             \
         }                                                                                    \
         const unsigned gc_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)tc);              \
         Q8_SEG(J, 1, 0, gc_, pr0, pr1, pc0, pc1);                                            \
@@ -564,7 +595,8 @@ __device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *
     }
     __syncthreads();
     Q8_STAMP(2);
-    float pr0 = 0.f, pr1 = 0.f, pc0 = -3.0e38f, pc1 = -3.0e38f;  // scales of the tile before
+    // scales of the tile before, as splat pairs (the packed dequantisation's operands)
+    f2q pr0 = {0.f, 0.f}, pr1 = {0.f, 0.f}, pc0 = {-3.0e38f, -3.0e38f}, pc1 = {-3.0e38f, -3.0e38f};
     for (int T = 0; T < ntc; T += 4) {
         Q8_SLOT(0);
         if (T + 1 < ntc) Q8_SLOT(1);
