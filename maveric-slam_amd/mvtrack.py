@@ -146,6 +146,18 @@ def lib():
             "mv_write_trajectory_ply": (_I, [ctypes.c_char_p, _I, _P]),
             "mv_read_transform_npy": (_I, [ctypes.c_char_p, _P]),
             "mv_compute_trajectory": (_I, [_P, _I, _I, ctypes.c_char_p, ctypes.c_char_p, _I, ctypes.POINTER(_I)]),
+            "mv_local_feature_init": (None, [_P]),
+            "mv_local_feature_init_with_id": (None, [_P, _I, _I]),
+            "mv_local_feature_update": (None, [_P, _I]),
+            "mv_local_feature_remove_old_frame": (ctypes.c_bool, [_P, _I]),
+            "mv_local_feature_pool_init": (None, [_P]),
+            "mv_local_feature_pool_insert": (_I, [_P, _I, _P, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_bool)]),
+            "mv_local_feature_pool_delete": (_I, [_P, _I]),
+            "mv_local_feature_pool_remove_old": (_I, [_P, _I]),
+            "mv_local_feature_pool_valid_keys": (None, [_P, ctypes.POINTER(_I), _P]),
+            "mv_local_feature_pool_load_factor": (_F, [_P]),
+            "mv_local_feature_pool_check_invariant": (_I, [_P, _I]),
+            "mv_local_feature_pool_track_frame": (_I, [_P, _I, _I, _P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -218,6 +230,88 @@ def chain_sharded(chain_local, rebase, gather, rank, rel_local, mode):
     if rank == 0:
         return poses
     return rebase(poses, start)
+
+
+# ---------------- local feature pool (include/feature_pool.h; include/local_feature_pool.h) ----------------
+MAX_LOCAL_FRAMES, LOCAL_FEATURE_POOL_CAPACITY = 8, 3000
+
+
+class LocalFeature(ctypes.Structure):
+    """mv_local_feature = the reference's LocalFeature (local_feature_pool.h:16-22)."""
+    _fields_ = [("word_id", _I), ("frame_ptr", _I), ("num_frames", _I), ("frames", _I * MAX_LOCAL_FRAMES),
+                ("coords_3D", _F * 3)]
+
+
+class _LfpEntry(ctypes.Structure):
+    _fields_ = [("key", _I), ("value", LocalFeature), ("is_occupied", ctypes.c_bool)]
+
+
+class _LfpPool(ctypes.Structure):
+    _fields_ = [("entries", _LfpEntry * LOCAL_FEATURE_POOL_CAPACITY), ("size", _I), ("capacity", _I)]
+
+
+class LocalFeaturePool:
+    """The local feature pool (host, C): the reference's LocalFeaturePool API with error codes
+    in place of its exit() calls.  table() -> int32 [capacity, 13] (key, occupied, word_id,
+    frame_ptr, num_frames, frames[8]), the layout the parity tests compare slot by slot."""
+
+    def __init__(self):
+        self._p = _LfpPool()
+        ctypes.memset(ctypes.byref(self._p), 0, ctypes.sizeof(self._p))
+        lib().mv_local_feature_pool_init(ctypes.byref(self._p))
+
+    @property
+    def size(self):
+        return self._p.size
+
+    @property
+    def capacity(self):
+        return self._p.capacity
+
+    def insert(self, key, frame_num):
+        """local_feature_pool_insert of a feature first seen at frame_num -> (status,
+        inserted, the entry's LocalFeature or None)"""
+        f = LocalFeature()
+        lib().mv_local_feature_init_with_id(ctypes.byref(f), key, frame_num)
+        out = _P()
+        ins = ctypes.c_bool(False)
+        st = lib().mv_local_feature_pool_insert(ctypes.byref(self._p), key, ctypes.byref(f), ctypes.byref(out),
+                                                ctypes.byref(ins))
+        feat = ctypes.cast(out, ctypes.POINTER(LocalFeature)).contents if out.value else None
+        return st, ins.value, feat
+
+    def delete(self, key):
+        return lib().mv_local_feature_pool_delete(ctypes.byref(self._p), key)
+
+    def remove_old(self, current_frame_num):
+        return lib().mv_local_feature_pool_remove_old(ctypes.byref(self._p), current_frame_num)
+
+    def valid_keys(self):
+        keys = np.zeros(LOCAL_FEATURE_POOL_CAPACITY, np.int32)
+        n = _I(0)
+        lib().mv_local_feature_pool_valid_keys(ctypes.byref(self._p), ctypes.byref(n), _np(keys))
+        return keys[:n.value].copy()
+
+    def load_factor(self):
+        return float(lib().mv_local_feature_pool_load_factor(ctypes.byref(self._p)))
+
+    def check_invariant(self, cur_frame):
+        return lib().mv_local_feature_pool_check_invariant(ctypes.byref(self._p), cur_frame)
+
+    def track_frame(self, frame_num, word_ids):
+        ids = np.ascontiguousarray(word_ids, np.int32)
+        return lib().mv_local_feature_pool_track_frame(ctypes.byref(self._p), frame_num, ids.size, _np(ids))
+
+    def table(self):
+        # an entry is 16 words: key, word_id, frame_ptr, num_frames, frames[8], coords[3],
+        # is_occupied (byte 0 of word 15)
+        assert ctypes.sizeof(_LfpEntry) == 64
+        raw = np.frombuffer(self._p, dtype=np.int32, count=LOCAL_FEATURE_POOL_CAPACITY * 16).reshape(-1, 16)
+        t = np.empty((self._p.capacity, 13), np.int32)
+        t[:, 0] = raw[:, 0]
+        t[:, 1] = raw[:, 15] & 0xFF
+        t[:, 2:13] = raw[:, 1:12]
+        return t
 
 
 def _t(x):

@@ -365,3 +365,54 @@ def ref_lba():
         R.ref_lba_schur_main.argtypes = [_I, _I, _I, _P]
         _ref_lba = R
     return _ref_lba
+
+
+# ---------------- local feature pool: the reference's own code (oracle/ref_pool_harness.c) ----------------
+REF_POOL_SO = os.path.join(HERE, "_ref", "libmv_ref_pool.so")
+_ref_pool = None
+
+
+def ref_pool_available():
+    return os.path.exists(REF_POOL_SO)
+
+
+def ref_pool():
+    """include/local_feature_pool.h + src/local_feature_matching.c's generator, compiled from
+    the reference's sources (oracle/Makefile); build-container only."""
+    global _ref_pool
+    if _ref_pool is None:
+        R = ctypes.CDLL(REF_POOL_SO)
+        R.ref_pool_run.argtypes = [_I, _I, _P, _P, _P]
+        R.ref_pool_run.restype = _I
+        R.ref_pool_replay.argtypes = [_I, _P, _P, _P, _P]
+        R.ref_pool_replay.restype = _I
+        _ref_pool = R
+    return _ref_pool
+
+
+def ref_pool_run(num_frames, nfeat=200):
+    """the reference workload (srand(0), generate_word_ids): ids [F, nfeat], the table after
+    each frame [F, capacity, 13] (key, occupied, word_id, frame_ptr, num_frames, frames[8]),
+    sizes [F]"""
+    R = ref_pool()
+    cap = R.ref_pool_capacity()
+    ids = np.zeros((num_frames, nfeat), np.int32)
+    tab = np.zeros((num_frames, cap, 13), np.int32)
+    sz = np.zeros(num_frames, np.int32)
+    done = R.ref_pool_run(num_frames, nfeat, _ptr(ids), _ptr(tab), _ptr(sz))
+    assert done == num_frames, "the reference pool gave up in frame %d" % done
+    return ids, tab, sz
+
+
+def ref_pool_replay(id_lists):
+    """the same frame loop on the given per-frame id lists -> (tables, sizes, frames completed:
+    len(id_lists), or the frame in which the reference exit()ed)"""
+    R = ref_pool()
+    cap = R.ref_pool_capacity()
+    n = np.array([len(x) for x in id_lists], np.int32)
+    flat = np.ascontiguousarray(np.concatenate([np.asarray(x, np.int32) for x in id_lists]) if len(id_lists) else
+                                np.zeros(0, np.int32))
+    tab = np.zeros((len(id_lists), cap, 13), np.int32)
+    sz = np.zeros(len(id_lists), np.int32)
+    done = R.ref_pool_replay(len(id_lists), _ptr(n), _ptr(flat), _ptr(tab), _ptr(sz))
+    return tab, sz, done
