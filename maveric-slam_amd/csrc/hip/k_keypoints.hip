@@ -36,7 +36,7 @@ constexpr int NMS_T = 1024;  // threads of the per-frame block
                    // transposed, per 256 KITTI frames: 64 channel planes per gather)
 #endif
 #ifndef KP_EXP
-#define KP_EXP 0  // timing experiments only (wrong results): 1 no descriptor stores, 2 no plane copy, 3 no keypoint phase
+#define KP_EXP 0  // timing experiments only (wrong results): 1 no descriptor stores, 2 no plane copy, 3 no keypoint phase, 4 geometry stubbed
 #endif
 #ifndef KP_TRACE
 #define KP_TRACE 0  // printf k_kp_nms's per-phase clock64() deltas for frame 0 (timing only)
@@ -44,6 +44,10 @@ constexpr int NMS_T = 1024;  // threads of the per-frame block
 #ifndef KP_TRANSPOSE
 #define KP_TRANSPOSE 0  // 1: always the NCHW->NHWC transpose + per-keypoint-wave sampling
 #endif
+#ifndef KP_CH
+#define KP_CH 4  // channels per k_kp_sample_planes workgroup (4: 144 KiB of LDS, 2: 72 KiB)
+#endif
+static_assert(KP_CH == 2 || KP_CH == 4, "KP_CH");
 constexpr int KP_PLANE_CELLS = 9216;  // cells whose 4 channel planes fit LDS (144 KiB): KITTI 47x155 = 7285
 constexpr int NC_LDS = 8192;  // candidates per frame held in LDS (more: the global per-pixel path)
 constexpr int ROW_LDS = 2048; // heat rows indexed in LDS
@@ -643,18 +647,24 @@ __global__ __launch_bounds__(256) void k_kp_sample(int B, int cap, int Hc, int W
 // 4 KiB corner reads per keypoint by one 7.4 MB read.  XCD-aware: the 8 channel quads that
 // share a 128-B line of every descriptor row run on one XCD (consecutively on it), so their
 // 16-B pieces merge in that XCD's L2 instead of leaving 8 partial lines.
+template <int CH>
+struct KpCh {
+    float v[CH];
+};
+template <int CH>
 __global__ __launch_bounds__(256) void k_kp_sample_planes(int B, int cap, int Hc, int Wc, int H, int W, int Wh,
                                                           const int *__restrict__ num_kp,
                                                           const int *__restrict__ slot_pix,
                                                           const float *__restrict__ coarse, float *__restrict__ desc) {
-    __shared__ __attribute__((aligned(16))) float plf[4 * KP_PLANE_CELLS + 4];
+    __shared__ __attribute__((aligned(16))) float plf[CH * KP_PLANE_CELLS + 4];
+    constexpr int LG = 32 / CH;  // workgroups whose pieces share a 128-B line of a row
     const int i = blockIdx.x, xcd = i & 7, k = i >> 3;
-    const int G = xcd + 8 * (k >> 3);  // (frame, group of 8 quads)
-    const int b = G >> 3, quad = ((G & 7) << 3) | (k & 7);
+    const int G = xcd + 8 * (k / LG);  // (frame, line group)
+    const int b = G >> 3, cb = (G & 7) * LG + k % LG;
     if (b >= B) return;
     const int nk = min(num_kp[b], cap);
     if (nk <= 0) return;  // block-uniform
-    const int HW = Hc * Wc, c0 = quad * 4, nf = 4 * HW;
+    const int HW = Hc * Wc, c0 = cb * CH, nf = CH * HW;
     // the first KPF slots of every thread: pixel loads issued and the bilinear geometry
     // (grid_sample's unnormalise, floor, weights) computed before the plane copy, so that
     // their latency hides under it
@@ -666,7 +676,15 @@ __global__ __launch_bounds__(256) void k_kp_sample_planes(int B, int cap, int Hc
     for (int u = 0; u < KPF; u++)  // branch-free (clamped) so the KPF loads are in flight together
         gpix[u] = slot_pix[(long)b * cap + min((int)threadIdx.x + 256 * u, nk - 1)];
 #pragma unroll
-    for (int u = 0; u < KPF; u++) kp_geometry(gpix[u], Hc, Wc, H, W, Wh, gx0[u], gy0[u], gw[u]);
+    for (int u = 0; u < KPF; u++) {
+        if (KP_EXP == 4) {  // timing only: the geometry stubbed
+            gx0[u] = (gpix[u] % Wh) >> 3;
+            gy0[u] = (gpix[u] / Wh) >> 3;
+            gw[u][0] = gw[u][1] = gw[u][2] = gw[u][3] = 0.25f;
+        } else {
+            kp_geometry(gpix[u], Hc, Wc, H, W, Wh, gx0[u], gy0[u], gw[u]);
+        }
+    }
     const float *I = coarse + ((long)b * 256 + c0) * HW;  // 4-B aligned
     // I[h] is the first 16-B aligned float; I[f] goes to plf[f + o] with h + o in {0, 4}, so
     // the aligned body lands on 16-B aligned LDS slots.  Head and tail (< 4 floats each) are
@@ -689,17 +707,31 @@ __global__ __launch_bounds__(256) void k_kp_sample_planes(int B, int cap, int Hc
     if (threadIdx.x < tail) plf[h + 4 * n4 + o + threadIdx.x] = I[h + 4 * n4 + threadIdx.x];
     __syncthreads();
     if (KP_EXP == 3) return;
-    const float *L = plf + o;  // plane c of the quad: L + c HW
-    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float *L = plf + o;  // plane c of the group: L + c HW
     auto at = [&](int yy, int xx) {
-        if (!(xx >= 0 && xx < Wc && yy >= 0 && yy < Hc)) return z;
-        const float *c = L + yy * Wc + xx;
-        return make_float4(c[0], c[HW], c[2 * HW], c[3 * HW]);
+        KpCh<CH> r;
+        const bool in = xx >= 0 && xx < Wc && yy >= 0 && yy < Hc;
+        const float *c = L + (in ? yy * Wc + xx : 0);
+#pragma unroll
+        for (int j = 0; j < CH; j++) r.v[j] = in ? c[j * HW] : 0.f;
+        return r;
     };
     auto emit = [&](int slot, int x0, int y0, const float *w) {
-        const float4 v = kp_bilinear4(at(y0, x0), at(y0, x0 + 1), at(y0 + 1, x0), at(y0 + 1, x0 + 1), w[0], w[1],
-                                      w[2], w[3]);
-        if (KP_EXP != 1 || v.x == 1234.5f) *reinterpret_cast<float4 *>(desc + ((long)b * cap + slot) * 256 + c0) = v;
+        const KpCh<CH> a = at(y0, x0), bq = at(y0, x0 + 1), c = at(y0 + 1, x0), dd = at(y0 + 1, x0 + 1);
+        KpCh<CH> v;
+#pragma unroll
+        for (int j = 0; j < CH; j++) {  // torch grid_sample's CPU arithmetic (as kp_bilinear4)
+            float r = __fmul_rn(a.v[j], w[0]);
+            r = fmaf(bq.v[j], w[1], r);
+            r = fmaf(c.v[j], w[2], r);
+            v.v[j] = fmaf(dd.v[j], w[3], r);
+        }
+        float *out = desc + ((long)b * cap + slot) * 256 + c0;
+        if (KP_EXP == 1 && v.v[0] != 1234.5f) return;
+        if constexpr (CH == 4)
+            *reinterpret_cast<float4 *>(out) = make_float4(v.v[0], v.v[1], v.v[2], v.v[3]);
+        else
+            *reinterpret_cast<float2 *>(out) = make_float2(v.v[0], v.v[1]);
     };
 #pragma unroll
     for (int u = 0; u < KPF; u++) {
@@ -766,8 +798,8 @@ extern "C" int mv_keypoints_dev(mv_context *ctx, const mv_kp_params *p, int batc
     const long waves = (long)batch * cap;
     if (kp_planes_path(Hc, Wc)) {
         MV_PROF_BEGIN(s, "k_kp_sample_planes");
-        hipLaunchKernelGGL(k_kp_sample_planes, dim3((unsigned)batch * 64), dim3(256), 0, s, batch, cap, Hc, Wc, H, W,
-                           Wc * 8, num_kp, m.slot_pix, coarse_desc, desc);
+        hipLaunchKernelGGL(k_kp_sample_planes<KP_CH>, dim3((unsigned)batch * (256 / KP_CH)), dim3(256), 0, s, batch,
+                           cap, Hc, Wc, H, W, Wc * 8, num_kp, m.slot_pix, coarse_desc, desc);
         MV_PROF_END(s);
         MV_LAUNCH_CHECK();
         MV_PROF_BEGIN(s, "k_kp_normalize");
