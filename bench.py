@@ -11,7 +11,7 @@ with the pose of the metric's "match+PnP".  Pairs are independent: with --gpus N
 (one process per GPU, torch.distributed) processes its own B pairs -- weak scaling, no
 data-path collective.  value = pairs processed by all ranks / max-over-ranks wall time.
 
-Extra fields: roofline of the dominant kernel (k_ap_match), its average launch duration
+Extra fields: roofline of the dominant kernel (k_q8_match), its average launch duration
 measured with HIP events on the launch stream over a second, profiled run of the same steps
 (the headline loop itself runs unprofiled); cpu_baseline = the gemmini matmul
 + row argmax (+ as-built stub pose) on host cores (rank 0, N = 1 only).
@@ -39,9 +39,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4096,
+    ap.add_argument("--batch", type=int, default=8192,
                     help="frame-pairs per GPU per step (one launch each; SURVEY §8d: >= 1000 pairs per launch; "
-                         "1024 / 2048 / 4096 measured 1.32 / 1.42 / 1.46 M pairs/s: launch tails amortised)")
+                         "1024 / 2048 / 4096 / 8192 measured 1.32 / 1.42 / 1.56 / 1.59 M pairs/s: launch tails "
+                         "amortised, and more of the pose overlaps the next match)")
     ap.add_argument("--kp", type=int, default=1024, help="keypoints per frame")
     ap.add_argument("--hypotheses", type=int, default=256)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
