@@ -182,6 +182,27 @@ __device__ __forceinline__ f2v msac_cost2(const float e[9], float4 A, float4 B, 
     return r;
 }
 
+// msac_cost of one correspondence under two hypotheses at once (packed FP32, the point's
+// coordinates splat): the survivors' full re-score
+__device__ __forceinline__ f2v msac_cost2h(const f2v E[9], float4 p, float thr2, int &na, int &nb) {
+    const float x1 = p.x, y1 = p.y, x2 = p.z, y2 = p.w;
+    const f2v ex0 = E[0] * x1 + (E[1] * y1 + E[2]);
+    const f2v ex1 = E[3] * x1 + (E[4] * y1 + E[5]);
+    const f2v ex2 = E[6] * x1 + (E[7] * y1 + E[8]);
+    const f2v etx0 = E[0] * x2 + (E[3] * y2 + E[6]);
+    const f2v etx1 = E[1] * x2 + (E[4] * y2 + E[7]);
+    const f2v num = x2 * ex0 + (y2 * ex1 + ex2);
+    const f2v den = ex0 * ex0 + ex1 * ex1 + etx0 * etx0 + etx1 * etx1;
+    const f2v nn = num * num, td = thr2 * den;
+    const bool ia = nn.x < td.x, ib = nn.y < td.y;
+    na += ia ? 1 : 0;
+    nb += ib ? 1 : 0;
+    f2v r;
+    r.x = ia ? nn.x * __builtin_amdgcn_rcpf(den.x) : thr2;
+    r.y = ib ? nn.y * __builtin_amdgcn_rcpf(den.y) : thr2;
+    return r;
+}
+
 // ---- small 3-vector algebra ----
 template <typename T>
 struct V3 {
@@ -508,9 +529,11 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
         int idx[8];
         const unsigned long long base = a.seed ^ ((unsigned long long)b << 40) ^ ((unsigned long long)h << 8);
         int drawn = 0;
-        for (int d = 0; d < 64 && drawn < 8; d++) {
-            const unsigned long long r = splitmix64(base + d);
-            const int c = (int)(((r >> 32) * (unsigned long long)n) >> 32);
+        unsigned long long r = 0;
+        for (int d = 0; d < 64 && drawn < 8; d++) {  // two 32-bit draws per splitmix64 output
+            if ((d & 1) == 0) r = splitmix64(base + (d >> 1));
+            const unsigned u = (d & 1) ? (unsigned)r : (unsigned)(r >> 32);
+            const int c = (int)(((unsigned long long)u * (unsigned)n) >> 32);
             bool dup = false;
 #pragma unroll
             for (int q = 0; q < 8; q++) dup |= (q < drawn) && idx[q] == c;
@@ -579,14 +602,18 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
     float cs[NS];
     int cn[NS];
 #pragma unroll
-    for (int sv = 0; sv < NS; sv++) {
-        cs[sv] = 0.f;
-        cn[sv] = 0;
-        if (s_sh[sv] < 0) continue;
-        float e[9];
+    for (int sv = 0; sv < NS; sv += 2) {  // two survivors per packed instruction
+        f2v E2[9];
 #pragma unroll
-        for (int q = 0; q < 9; q++) e[q] = s_sE[sv][q];
-        for (int i = t; i < n; i += NT) cs[sv] += msac_cost(e, P[i], a.thr2, cn[sv]);
+        for (int q = 0; q < 9; q++) E2[q] = f2v{s_sE[sv][q], s_sE[sv + 1][q]};
+        f2v acc = {0.f, 0.f};
+        int na = 0, nb = 0;
+        if (s_sh[sv] >= 0 || s_sh[sv + 1] >= 0)
+            for (int i = t; i < n; i += NT) acc += msac_cost2h(E2, P[i], a.thr2, na, nb);
+        cs[sv] = s_sh[sv] >= 0 ? acc.x : 0.f;
+        cs[sv + 1] = s_sh[sv + 1] >= 0 ? acc.y : 0.f;
+        cn[sv] = s_sh[sv] >= 0 ? na : 0;
+        cn[sv + 1] = s_sh[sv + 1] >= 0 ? nb : 0;
     }
     __shared__ float s_red2[4][2 * NS];
     {
