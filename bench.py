@@ -430,7 +430,7 @@ def main():
         import bench_i8
         import bench_keypoints
 
-        r = bench_i8.run(batch=256, kp=2048, steps=args.extra_steps, warmup=2, check=1)
+        r = bench_i8.run(batch=2048, kp=2048, steps=args.extra_steps, warmup=2, check=1)
         out["i8_allpairs"] = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "stages_ms",
                                                   "mfma_roofline", "checked_pairs")}
         r = bench_keypoints.run(batch=256, steps=args.extra_steps, warmup=2, check=1)
