@@ -433,7 +433,7 @@ def main():
         r = bench_i8.run(batch=2048, kp=2048, steps=args.extra_steps, warmup=2, check=1)
         out["i8_allpairs"] = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "stages_ms",
                                                   "mfma_roofline", "checked_pairs")}
-        r = bench_keypoints.run(batch=256, steps=args.extra_steps, warmup=2, check=1)
+        r = bench_keypoints.run(batch=1024, steps=args.extra_steps, warmup=2, check=1)
         out["keypoints"] = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "stages_ms",
                                                "hbm_roofline", "checked_frames")}
     if rank == 0:

@@ -48,7 +48,7 @@ def cpu_baseline(frames, H, W, seconds):
                       % (total, dt, threads)}
 
 
-def run(batch=256, steps=10, warmup=2, distinct=8, check=1, cpu_seconds=0.0, cap=1024):
+def run(batch=1024, steps=10, warmup=2, distinct=8, check=1, cpu_seconds=0.0, cap=1024):
     dev = torch.device("cuda", 0)
     Hc, Wc, H, W = 47, 155, 376, 1241
     frames = [synth.synth_superpoint_outputs(100 + k, Hc, Wc) for k in range(distinct)]
@@ -114,7 +114,8 @@ def run(batch=256, steps=10, warmup=2, distinct=8, check=1, cpu_seconds=0.0, cap
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--batch", type=int, default=1024,
+                    help="frames per launch (256 / 512 / 1024 measured 227 k / 241 k / 247 k frames/s)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--check", type=int, default=1)
