@@ -117,6 +117,24 @@ __device__ __forceinline__ f2q pkfma_q8(f2q a, f2q r, f2q c) {
     asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(r), "v"(c));
     return d;
 }
+#ifndef Q8_EXP_INTFOLD
+#define Q8_EXP_INTFOLD 0
+#endif
+template <int SH>  // an inline constant: a VOP3 may read one SGPR only (the tag)
+__device__ __forceinline__ int lshl_or_q8(int d, unsigned tag) {
+    int r;
+    asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(d), "n"(SH), "s"(tag));
+    return r;
+}
+// the tagged top-2 fold on integer keys held in the float registers' bits
+__device__ __forceinline__ void fold3_i8k(int a, int b, float &m1f, float &m2f) {
+    int md, m1 = __float_as_int(m1f), m2 = __float_as_int(m2f);
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(md) : "v"(m1), "v"(a), "v"(b));
+    asm("v_max3_i32 %0, %1, %2, %3" : "=v"(m1) : "v"(m1), "v"(a), "v"(b));
+    asm("v_max_i32 %0, %1, %2" : "=v"(m2) : "v"(m2), "v"(md));
+    m1f = __int_as_float(m1);
+    m2f = __int_as_float(m2);
+}
 __device__ __forceinline__ float tag_q8(float f, unsigned keep, unsigned tag) {
     float r;
     asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(keep), "s"(tag));
@@ -512,6 +530,17 @@ __device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *
             const int q = 2 * (S) + u_;                                                      \
             if (Q8_EXP_NOFOLD && q != 0) continue;                                           \
             fold3_q8(tag_q8(a2_[u_], vkeep, (G0)), tag_q8(b2_[u_], vkeep, (G0) + 1u), m1[FG][q], m2[FG][q]); \
+        }                                                                                    \
+    } while (0)
+#elif Q8_EXP_INTFOLD
+    // timing experiment only (wrong results): the integer fold of DESIGN §8 item 1 --
+    // key = (D << shift) | tag in one v_lshl_or_b32, top-2 on v_max3_i32 / v_med3_i32
+#define Q8_FOLD2(FG, S, G0, R0, R1, C0, C1)                                                  \
+    do {                                                                                     \
+        _Pragma("unroll") for (int q = 2 * (S); q < 2 * (S) + 2; q++) {                      \
+            const int ka_ = lshl_or_q8<9>(acc[FG][0][q], (G0));                             \
+            const int kb_ = lshl_or_q8<9>(acc[FG][1][q], (G0) + 1u);                        \
+            fold3_i8k(ka_, kb_, m1[FG][q], m2[FG][q]);                                       \
         }                                                                                    \
     } while (0)
 #else
