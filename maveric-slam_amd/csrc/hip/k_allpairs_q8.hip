@@ -65,7 +65,10 @@ constexpr int Q_TILE = Q_BN * KD;                  // 16 KiB: one int8 column ti
 constexpr int Q_SLOT = Q_TILE + Q_BN * 4;          // + the tile's 64 scales s_j
 constexpr int Q_OFF_MISC = Q_NBUF * Q_SLOT;        // [2][NW] f32 per-wave max |b|^2, |eps|^2
 constexpr int Q_OFF_ROW = Q_OFF_MISC + 2 * Q_NW * 4;  // [BM] float2 per row (|a|^2, s_a; s_a < 0: exact path)
-constexpr int Q_LDS = Q_OFF_ROW + 2 * 32 * Q_RG * Q_NW * 4;
+constexpr int Q_OFF_TEXP = Q_OFF_ROW + 2 * 32 * Q_RG * Q_NW * 4;  // [16] i32 tile exponents (integer fold)
+constexpr int Q_LDS = Q_OFF_TEXP + 16 * 4;
+constexpr int QI_TB = 5, QI_SHR = 4;  // integer fold: tag bits (<= 16 tiles), exponent span (2^22 << 9 < 2^31)
+constexpr int QI_NONE = -100000;      // exponent of an all-zero tile
 constexpr int MT_STRIDE = 32 * 8 + 16;             // epilogue transpose row: 32 (m1, m2) + pad
 constexpr int Q_NCAND = 16;                        // listed candidates per row (more: wide row)
 constexpr int Q_OFF_CL = Q_NW * 32 * MT_STRIDE;    // epilogue, inside the ring: [BM][NCAND]
@@ -117,15 +120,6 @@ __device__ __forceinline__ f2q pkfma_q8(f2q a, f2q r, f2q c) {
     asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(r), "v"(c));
     return d;
 }
-#ifndef Q8_EXP_INTFOLD
-#define Q8_EXP_INTFOLD 0
-#endif
-template <int SH>  // an inline constant: a VOP3 may read one SGPR only (the tag)
-__device__ __forceinline__ int lshl_or_q8(int d, unsigned tag) {
-    int r;
-    asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(d), "n"(SH), "s"(tag));
-    return r;
-}
 // the tagged top-2 fold on integer keys held in the float registers' bits
 __device__ __forceinline__ void fold3_i8k(int a, int b, float &m1f, float &m2f) {
     int md, m1 = __float_as_int(m1f), m2 = __float_as_int(m2f);
@@ -139,6 +133,18 @@ __device__ __forceinline__ float tag_q8(float f, unsigned keep, unsigned tag) {
     float r;
     asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(keep), "s"(tag));
     return r;
+}
+// an integer-fold key -> the float path's tagged screen value: tag = column tag (2 tc + half),
+// D = the integer dot, f = D 2^e_t exactly (|D| < 2^22), its low tb bits replaced by the tag
+// as tag_q8 does; keys below every real one (tile -1, INT_MIN) -> -inf
+__device__ __forceinline__ float q8_key_value(int key, const int *texp, int e_base, unsigned keep) {
+    if (key < (int)0x82000000) return -__builtin_inff();  // |real keys| <= 127^2 256 2^9 < 2^31 - 2^25
+    const unsigned tag = (unsigned)key & ((1u << QI_TB) - 1u);
+    const int e = texp[tag >> 1];
+    const int sh = e == QI_NONE ? 0 : e - e_base;
+    const int d = (key >> QI_TB) >> sh;
+    const float f = e == QI_NONE ? 0.f : ldexpf((float)d, e);
+    return __uint_as_float((__float_as_uint(f) & keep) | tag);
 }
 __device__ __forceinline__ void fold3_q8(float a, float b, float &m1, float &m2) {
     float md;
@@ -167,6 +173,20 @@ __device__ __forceinline__ i32x16 mfma_i8_from4(i32x4 a, i32x4 b) {
     i32x16 d;
     asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, 4.0" : "=&v"(d) : "v"(a), "v"(b));
     return d;
+}
+// the integer fold's chain start: C = 0 (inline constant)
+__device__ __forceinline__ i32x16 mfma_i8_from0(i32x4 a, i32x4 b) {
+    i32x16 d;
+    asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "v"(b));
+    return d;
+}
+// key = (D << sh) | tag: the integer fold's dequantisation (tile scale 2^e_t relative to the
+// pair's base exponent) and column tag in one instruction; sh in a VGPR, the tag in an SGPR
+// (a VOP3 reads one SGPR)
+__device__ __forceinline__ int lshl_or_v_q8(int d, int sh, unsigned tag) {
+    int r;
+    asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(d), "v"(sh), "s"(tag));
+    return r;
 }
 // four int8 RNE(x q) packed into a dword (byte i = element i): the magic sum's low byte is
 // the two's-complement integer
@@ -220,9 +240,13 @@ __device__ __forceinline__ bool better_q8(int dmode, float v, int j, float bv, i
 //      load instruction reads 256 contiguous bytes of 4 rows), QS_RPG rows per lane group in
 //      flight; a 256-thread block strides over the batch (rows >= n1 are never read
 //      downstream and are not written) ----
-#ifndef QS_RPG
-#define QS_RPG 2
+#ifndef Q8_INTFOLD
+#define Q8_INTFOLD 0  // 1: integer fold for pairs with whole 64-column tiles (bit-exact; measured no faster yet)
 #endif
+#ifndef QS_RPG
+#define QS_RPG (Q8_INTFOLD ? 4 : 2)  // Q8_INTFOLD: one pass = one 64-row tile
+#endif
+static_assert(!Q8_INTFOLD || QS_RPG == 4, "tile mode stages whole 64-row tiles per pass");
 #ifndef QS_GRID
 #define QS_GRID (256 * 64)
 #endif
@@ -247,6 +271,36 @@ __device__ __forceinline__ void q8_split_pass(long R0, long rows, int cap, const
             x[r][u] = __builtin_nontemporal_load(
                 reinterpret_cast<const f32x4v *>(desc1 + c[r] * KD + 4 * (sub + 16 * u)));
     }
+    // tile mode (Q8_INTFOLD): the pass's 64 rows are one 64-column tile of one pair whose n1 is a
+    // multiple of 64 -- their codes share one power-of-two scale (the integer fold's input)
+    const int pair0 = (int)(min(R0, rows - 1) / cap);
+    const bool tile_mode = Q8_INTFOLD && (cap & 63) == 0 && (min(max(n1v[pair0], 0), cap) & 63) == 0;
+    float tile_max = 0.f;
+    if (Q8_INTFOLD) {
+        __shared__ float s_tmax[16];
+        float mm = 0.f;
+#pragma unroll
+        for (int r = 0; r < QS_RPG; r++) {
+            float m = 0.f;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                m = absmax3(m, x[r][u][0], x[r][u][1]);
+                m = absmax3(m, x[r][u][2], x[r][u][3]);
+            }
+            const long R = R0 + 16 * r + rg;
+            const bool live = R < rows && (int)(c[r] - (long)(c[r] / cap) * cap) < n1v[c[r] / cap];
+            mm = fmaxf(mm, live ? m : 0.f);
+        }
+        mm = fmaxf(mm, swz_xor_q8<1>(mm));
+        mm = fmaxf(mm, swz_xor_q8<2>(mm));
+        mm = fmaxf(mm, swz_xor_q8<4>(mm));
+        mm = fmaxf(mm, swz_xor_q8<8>(mm));
+        if (sub == 0) s_tmax[rg] = mm;
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 16; i++) tile_max = fmaxf(tile_max, s_tmax[i]);
+        __syncthreads();  // s_tmax is rewritten by the next pass
+    }
 #pragma unroll
     for (int r = 0; r < QS_RPG; r++) {
         const long R = R0 + 16 * r + rg;
@@ -266,8 +320,18 @@ __device__ __forceinline__ void q8_split_pass(long R0, long rows, int cap, const
         q2 += swz_xor_q8<2>(q2);
         q2 += swz_xor_q8<4>(q2);
         q2 += swz_xor_q8<8>(q2);
-        const float q = m > 0.f ? 127.f / m : 0.f;
-        const float s = m / 127.f;
+        float q = m > 0.f ? 127.f / m : 0.f;
+        float s = m / 127.f;
+        float mr = m;  // the magnitude the range check sees
+        if (tile_mode) {  // one power-of-two scale 2^e >= M / 127 for the tile's 64 rows
+            const float M = tile_max;
+            int ex;
+            (void)frexpf(M, &ex);  // M < 2^ex
+            const int e = ldexpf(127.f, ex - 7) >= M ? ex - 7 : ex - 6;
+            s = M > 0.f ? ldexpf(1.f, e) : 0.f;
+            q = M > 0.f ? ldexpf(1.f, -e) : 0.f;
+            mr = M;
+        }
         int pk[4];
         float e2 = 0.f;
 #pragma unroll
@@ -286,7 +350,7 @@ __device__ __forceinline__ void q8_split_pass(long R0, long rows, int cap, const
         e2 += swz_xor_q8<8>(e2);
         // finite (|b|^2 propagates NaN / inf) and a representable scale (zero rows: s = 0,
         // q = 0, every screen value of the column 0 -- exact, no flag needed)
-        const bool ok = q2 <= FLT_MAX && (m == 0.f || (m >= SCALE_LO && m <= SCALE_HI));
+        const bool ok = q2 <= FLT_MAX && (mr == 0.f || (mr >= SCALE_LO && mr <= SCALE_HI));
         const int pair = (int)(c[r] / cap);
         if (R < rows && (int)(c[r] - (long)pair * cap) < n1v[pair]) {
 #pragma unroll
@@ -373,6 +437,19 @@ __device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *
         if (lane == 0) {
             misc[w] = bm;
             misc[Q_NW + w] = em;
+        }
+        // integer fold: each tile's scale exponent (tile t's rows all hold 2^e_t), published by
+        // the barrier after the A phase
+        if (Q8_INTFOLD && t < 16) {
+            int ex = QI_NONE;
+            if (t < ntc) {
+                const float st = sb[t * Q_BN];
+                if (st > 0.f) {
+                    (void)frexpf(st, &ex);
+                    ex -= 1;  // st = 2^(ex - 1)
+                }
+            }
+            reinterpret_cast<int *>(lds + Q_OFF_TEXP)[t] = ex;
         }
     }
 
@@ -492,19 +569,44 @@ __device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *
     // f = fma(t, 2^21 s_j, -2^23 s_j) = RN(D s_j) (the product is exact inside the fma).
     // Columns past n1 (last tile only) get s = 0 and the offset -3e38.  The low tb bits of f
     // are then replaced by the column tag 2 tc + half.
+    // The integer fold (Q8_INTFOLD; pairs with whole 64-column tiles, at most 16 of them, whose
+    // tile scales 2^e_t span <= 2^QI_SHR): the accumulators start at 0 and each value becomes
+    // the key (D << (e_t - e_base + QI_TB)) | tag -- one v_lshl_or_b32 in place of the
+    // dequantising FMA and the tag -- folded with v_max3_i32 / v_med3_i32 (|D| < 2^22: the key
+    // fits 31 bits).  After the sweep the keys become the float path's tagged values exactly
+    // (f = D 2^e_t is exact), so the merge and the decisions are shared.
+    const int *texp = reinterpret_cast<const int *>(lds + Q_OFF_TEXP);
+    bool int_ok = false;
+    int e_base = 0;
+    if (Q8_INTFOLD && ntc > 0 && ntc <= 16 && (n1 & (Q_BN - 1)) == 0 && (cap & (Q_BN - 1)) == 0) {
+        int emx = QI_NONE, emn = 1 << 30;
+        for (int i = 0; i < ntc; i++) {
+            const int e = texp[i];
+            if (e != QI_NONE) {
+                emx = max(emx, e);
+                emn = min(emn, e);
+            }
+        }
+        int_ok = emx == QI_NONE || emx - emn <= QI_SHR;
+        e_base = emx == QI_NONE ? 0 : emx - QI_SHR;
+    }
     i32x16 acc[Q_RG][2];
     float m1[Q_RG][16], m2[Q_RG][16];
+    {
+        const float minit = int_ok ? __int_as_float((int)0x80000000) : -__builtin_inff();
+        const int ainit = int_ok ? -(1 << 22) : 0;  // "tile -1": -3e38 (float) / INT_MIN keys
 #pragma unroll
-    for (int g = 0; g < Q_RG; g++)
+        for (int g = 0; g < Q_RG; g++)
 #pragma unroll
-        for (int q = 0; q < 16; q++) {
-            m1[g][q] = -__builtin_inff();
-            m2[g][q] = -__builtin_inff();
+            for (int q = 0; q < 16; q++) {
+                m1[g][q] = minit;
+                m2[g][q] = minit;
+            }
+#pragma unroll
+        for (int q = 0; q < 16; q++) {  // "tile -1" of group 1, folded beside tile 0: never a maximum
+            acc[1][0][q] = ainit;
+            acc[1][1][q] = ainit;
         }
-#pragma unroll
-    for (int q = 0; q < 16; q++) {  // "tile -1" of group 1, folded beside tile 0: -3e38, never a maximum
-        acc[1][0][q] = 0;
-        acc[1][1][q] = 0;
     }
     const int tb = 2 * ntc <= 256 ? 8 : 32 - __builtin_clz(2 * ntc - 1);
     const unsigned tkeep = ~((1u << tb) - 1u);
@@ -520,7 +622,7 @@ __device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *
 #if Q8_PKFMA
     // rows 2 S and 2 S + 1 of a half share the lane's column, hence its scale and offset: one
     // v_pk_fma_f32 (splat operands) dequantises both (adjacent accumulator registers)
-#define Q8_FOLD2(FG, S, G0, R0, R1, C0, C1)                                                  \
+#define Q8_FOLD2_F(FG, S, G0, R0, R1, C0, C1)                                                \
     do {                                                                                     \
         const f2q a2_ = pkfma_q8(                                                            \
             f2q{__int_as_float(acc[FG][0][2 * (S)]), __int_as_float(acc[FG][0][2 * (S) + 1])}, (R0), (C0)); \
@@ -532,19 +634,8 @@ __device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *
             fold3_q8(tag_q8(a2_[u_], vkeep, (G0)), tag_q8(b2_[u_], vkeep, (G0) + 1u), m1[FG][q], m2[FG][q]); \
         }                                                                                    \
     } while (0)
-#elif Q8_EXP_INTFOLD
-    // timing experiment only (wrong results): the integer fold of DESIGN §8 item 1 --
-    // key = (D << shift) | tag in one v_lshl_or_b32, top-2 on v_max3_i32 / v_med3_i32
-#define Q8_FOLD2(FG, S, G0, R0, R1, C0, C1)                                                  \
-    do {                                                                                     \
-        _Pragma("unroll") for (int q = 2 * (S); q < 2 * (S) + 2; q++) {                      \
-            const int ka_ = lshl_or_q8<9>(acc[FG][0][q], (G0));                             \
-            const int kb_ = lshl_or_q8<9>(acc[FG][1][q], (G0) + 1u);                        \
-            fold3_i8k(ka_, kb_, m1[FG][q], m2[FG][q]);                                       \
-        }                                                                                    \
-    } while (0)
 #else
-#define Q8_FOLD2(FG, S, G0, R0, R1, C0, C1)                                                  \
+#define Q8_FOLD2_F(FG, S, G0, R0, R1, C0, C1)                                                \
     do {                                                                                     \
         _Pragma("unroll") for (int q = 2 * (S); q < 2 * (S) + 2; q++) {                      \
             if (Q8_EXP_NOFOLD && q != 0) continue;                                           \
@@ -554,6 +645,15 @@ __device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *
         }                                                                                    \
     } while (0)
 #endif
+    // the integer fold of rows 2 S, 2 S + 1 of group FG (the tile's shift in shv)
+#define Q8_FOLD2_I(FG, S, G0, R0, R1, C0, C1)                                                \
+    do {                                                                                     \
+        _Pragma("unroll") for (int q = 2 * (S); q < 2 * (S) + 2; q++) {                      \
+            const int ka_ = lshl_or_v_q8(acc[FG][0][q], shv, (G0));                          \
+            const int kb_ = lshl_or_v_q8(acc[FG][1][q], shv, (G0) + 1u);                     \
+            fold3_i8k(ka_, kb_, m1[FG][q], m2[FG][q]);                                       \
+        }                                                                                    \
+    } while (0)
     // group G's MFMAs on slot J (fragments read PF k32 steps ahead), folding group FG meanwhile
 #define Q8_SEG(J, G, FG, G0, R0, R1, C0, C1)                                                 \
     do {                                                                                     \
@@ -571,8 +671,8 @@ __device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *
             if (s_ >= PF) {                                                                  \
                 const int m_ = s_ - PF;                                                      \
                 if (m_ == 0) {                                                               \
-                    acc[G][0] = mfma_i8_from4(aI[G][0], b0_[0]);                             \
-                    acc[G][1] = mfma_i8_from4(aI[G][0], b1_[0]);                             \
+                    acc[G][0] = Q8_MFMA0(aI[G][0], b0_[0]);                                  \
+                    acc[G][1] = Q8_MFMA0(aI[G][0], b1_[0]);                                  \
                 } else {                                                                     \
                     acc[G][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b0_[m_], acc[G][0], 0, 0, 0); \
                     acc[G][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b1_[m_], acc[G][1], 0, 0, 0); \
@@ -593,19 +693,7 @@ __device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *
         }                                                                                    \
         const unsigned gp_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)max(tc - 1, 0));  \
         Q8_SEG(J, 0, 1, gp_, pr0, pr1, pc0, pc1);                                            \
-        {                                                                                    \
-            const float *rl_ = reinterpret_cast<const float *>(lds + (J) * Q_SLOT + Q_TILE); \
-            const int col_ = tc * Q_BN + fr;                                                 \
-            const float s0_ = rl_[fr], s1_ = rl_[fr + 32];                                   \
-            const float r0_ = col_ < n1 ? 2097152.0f * s0_ : 0.f;                            \
-            const float r1_ = col_ + 32 < n1 ? 2097152.0f * s1_ : 0.f;                       \
-            const float c0_ = col_ < n1 ? -8388608.0f * s0_ : -3.0e38f;                      \
-            const float c1_ = col_ + 32 < n1 ? -8388608.0f * s1_ : -3.0e38f;                 \
-            pr0 = f2q{r0_, r0_};                                                             \
-            pr1 = f2q{r1_, r1_};                                                             \
-            pc0 = f2q{c0_, c0_};                                                             \
-            pc1 = f2q{c1_, c1_};                                                             \
-        }                                                                                    \
+        Q8_SCALES(J, tc);                                                                    \
         const unsigned gc_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)tc);              \
         Q8_SEG(J, 1, 0, gc_, pr0, pr1, pc0, pc1);                                            \
         if (ntile < ntc) {                                                                   \
@@ -624,23 +712,71 @@ __device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *
     }
     __syncthreads();
     Q8_STAMP(2);
-    // scales of the tile before, as splat pairs (the packed dequantisation's operands)
+    // scales of the tile before, as splat pairs (the packed dequantisation's operands); the
+    // integer fold's shift of the tile before (tile -1: any)
     f2q pr0 = {0.f, 0.f}, pr1 = {0.f, 0.f}, pc0 = {-3.0e38f, -3.0e38f}, pc1 = {-3.0e38f, -3.0e38f};
-    for (int T = 0; T < ntc; T += 4) {
-        Q8_SLOT(0);
-        if (T + 1 < ntc) Q8_SLOT(1);
-        if (T + 2 < ntc) Q8_SLOT(2);
-        if (T + 3 < ntc) Q8_SLOT(3);
-    }
-    if (ntc > 0) {  // group 1 of the last tile
-        const unsigned gl_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)(ntc - 1));
+    int shv = QI_SHR + QI_TB;
+#define Q8_SWEEP()                                                                           \
+    do {                                                                                     \
+        for (int T = 0; T < ntc; T += 4) {                                                   \
+            Q8_SLOT(0);                                                                      \
+            if (T + 1 < ntc) Q8_SLOT(1);                                                     \
+            if (T + 2 < ntc) Q8_SLOT(2);                                                     \
+            if (T + 3 < ntc) Q8_SLOT(3);                                                     \
+        }                                                                                    \
+        if (ntc > 0) { /* group 1 of the last tile */                                        \
+            const unsigned gl_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)(ntc - 1));   \
+            _Pragma("unroll") for (int s = 0; s < 8; s++) Q8_FOLD2(1, s, gl_, pr0, pr1, pc0, pc1); \
+        }                                                                                    \
+    } while (0)
+    if (Q8_INTFOLD && int_ok) {
+#define Q8_FOLD2 Q8_FOLD2_I
+#define Q8_MFMA0 mfma_i8_from0
+#define Q8_SCALES(J, TC)                                                                     \
+    do {                                                                                     \
+        const int e_ = texp[TC];                                                             \
+        shv = (e_ == QI_NONE ? 0 : e_ - e_base) + QI_TB;                                     \
+    } while (0)
+        Q8_SWEEP();
+#undef Q8_FOLD2
+#undef Q8_MFMA0
+#undef Q8_SCALES
+        // keys -> the float path's tagged values (exact: f = D 2^e_t), for the shared merge
 #pragma unroll
-        for (int s = 0; s < 8; s++) Q8_FOLD2(1, s, gl_, pr0, pr1, pc0, pc1);
+        for (int g = 0; g < Q_RG; g++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                m1[g][q] = q8_key_value(__float_as_int(m1[g][q]), texp, e_base, vkeep);
+                m2[g][q] = q8_key_value(__float_as_int(m2[g][q]), texp, e_base, vkeep);
+            }
+    } else {
+#define Q8_FOLD2 Q8_FOLD2_F
+#define Q8_MFMA0 mfma_i8_from4
+#define Q8_SCALES(J, TC)                                                                     \
+    do {                                                                                     \
+        const float *rl_ = reinterpret_cast<const float *>(lds + (J) * Q_SLOT + Q_TILE);     \
+        const int col_ = (TC) * Q_BN + fr;                                                   \
+        const float s0_ = rl_[fr], s1_ = rl_[fr + 32];                                       \
+        const float r0_ = col_ < n1 ? 2097152.0f * s0_ : 0.f;                                \
+        const float r1_ = col_ + 32 < n1 ? 2097152.0f * s1_ : 0.f;                           \
+        const float c0_ = col_ < n1 ? -8388608.0f * s0_ : -3.0e38f;                          \
+        const float c1_ = col_ + 32 < n1 ? -8388608.0f * s1_ : -3.0e38f;                     \
+        pr0 = f2q{r0_, r0_};                                                                 \
+        pr1 = f2q{r1_, r1_};                                                                 \
+        pc0 = f2q{c0_, c0_};                                                                 \
+        pc1 = f2q{c1_, c1_};                                                                 \
+    } while (0)
+        Q8_SWEEP();
+#undef Q8_FOLD2
+#undef Q8_MFMA0
+#undef Q8_SCALES
     }
     Q8_STAMP(3);
 #undef Q8_STAGE
 #undef Q8_OFFSETS
-#undef Q8_FOLD2
+#undef Q8_FOLD2_F
+#undef Q8_FOLD2_I
+#undef Q8_SWEEP
 #undef Q8_SEG
 #undef Q8_SLOT
 
