@@ -590,14 +590,6 @@ __device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *
         int_ok = emx == QI_NONE || emx - emn <= QI_SHR;
         e_base = emx == QI_NONE ? 0 : emx - QI_SHR;
     }
-    // the tiles' shifts (0 .. QI_SHR) packed 4 bits each: the sweep's per-tile update is then
-    // scalar arithmetic, not an LDS read whose lgkmcnt wait would also wait for the B fragments
-    unsigned long long shmask = 0;
-    if (Q8_INTFOLD && int_ok)
-        for (int i = 0; i < ntc; i++) {
-            const int e = texp[i];
-            shmask |= (unsigned long long)(e == QI_NONE ? 0 : e - e_base) << (4 * i);
-        }
     i32x16 acc[Q_RG][2];
     float m1[Q_RG][16], m2[Q_RG][16];
     {
@@ -740,7 +732,11 @@ __device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *
     if (Q8_INTFOLD && int_ok) {
 #define Q8_FOLD2 Q8_FOLD2_I
 #define Q8_MFMA0 mfma_i8_from0
-#define Q8_SCALES(J, TC) shv = (int)((shmask >> (4 * (TC))) & 15u) + QI_TB
+#define Q8_SCALES(J, TC)                                                                     \
+    do {                                                                                     \
+        const int e_ = texp[TC];                                                             \
+        shv = (e_ == QI_NONE ? 0 : e_ - e_base) + QI_TB;                                     \
+    } while (0)
         Q8_SWEEP();
 #undef Q8_FOLD2
 #undef Q8_MFMA0
