@@ -47,10 +47,12 @@ def parse():
     ap.add_argument("--hypotheses", type=int, default=256)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pipeline", type=int, default=2,
+    ap.add_argument("--pipeline", type=int, default=3,
                     help="contexts (each with its own stream) taking the batches in turn: one batch's pose "
                          "overlaps the next batch's match.  The per-kernel durations (roofline, stages) "
-                         "come from a second loop on ONE context, where kernels do not overlap")
+                         "come from a second loop on ONE context, where kernels do not overlap.  At 8192 "
+                         "pairs, 40 steps, two runs each: P = 2 / 3 / 4 / 6 measured 1.58 / 1.60 / 1.58 / "
+                         "1.57 M pairs/s (tools/sweep_batch.sh; 4 hardware queues per process)")
     ap.add_argument("--score-steps", type=int, default=10,
                     help="secondary: steps timed with the exact score materialised (0 = skip)")
     ap.add_argument("--extra-steps", type=int, default=10,
