@@ -1,0 +1,95 @@
+"""Pipelined contexts (bench.py --pipeline P): P contexts, each on its own HIP stream, take the
+batches in turn -- match with the next batch's frame 1 staged in the same launch
+(mv_match_allpairs_f32_run_prepare_dev) and the pose of the matches -- with no host
+synchronisation between batches, so one context's pose runs beside another's match.  Every
+batch's match indices, inlier counts, status and pose must be bit-identical to one context
+running the same batches one after the other (and the indices equal the oracle's)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_pipelined_contexts_equal_sequential(ctx, orc, torch_cuda, P):
+    import bench
+    import mvtrack
+    import synth
+
+    torch = torch_cuda
+    dev = torch.device("cuda:0")
+    B, n, K = 4, 512, 7
+    batches = [bench.gen_batch(torch, dev, B, n, seed=300 + k) for k in range(K)]
+    nn_ = torch.full((B,), n, dtype=torch.int32, device=dev)
+    Km = synth.KITTI_K
+    prm = mvtrack.pose_params(mvtrack.AS_INTENDED, fx=Km[0, 0], fy=Km[1, 1], cx=Km[0, 2], cy=Km[1, 2],
+                              hypotheses=256, inlier_thresh=1.0, refine_iters=10, seed=7)
+
+    def outputs():
+        return dict(idx=torch.full((B, n), -7, dtype=torch.int32, device=dev),
+                    T=torch.zeros((B, 3, 4), dtype=torch.float32, device=dev),
+                    nm=torch.zeros(B, dtype=torch.int32, device=dev),
+                    ni=torch.zeros(B, dtype=torch.int32, device=dev),
+                    st=torch.full((B,), 99, dtype=torch.int32, device=dev))
+
+    def host(o):
+        return {k: v.cpu().numpy() for k, v in o.items()}
+
+    # one context, one batch after the other
+    ref = []
+    ctx.set_stream(torch.cuda.current_stream())
+    try:
+        for d0, d1, kp0, kp1 in batches:
+            o = outputs()
+            ctx.match_allpairs_f32_prepare(d1, nn_)
+            ctx.match_allpairs_f32_run(d0, d1, nn_, nn_, o["idx"], None, 0.8)
+            ctx.pose_from_matches(prm, nn_, o["idx"], kp0, kp1, o["T"], o["nm"], o["ni"], o["st"])
+            torch.cuda.synchronize()
+            ref.append(host(o))
+    finally:
+        ctx.set_stream(None)
+
+    # P contexts on P streams, batches in turn, no host sync until the end
+    ctxs, streams = [], []
+    try:
+        for _ in range(P):
+            c = mvtrack.Context(0)
+            s = torch.cuda.Stream(device=dev)
+            c.set_stream(s)
+            c.reserve(B, n)
+            ctxs.append(c)
+            streams.append(s)
+        torch.cuda.synchronize()  # the batches were drawn on the default stream
+        for c in range(P):
+            ctxs[c].match_allpairs_f32_prepare(batches[c][1], nn_)
+        outs = []
+        for k, (d0, d1, kp0, kp1) in enumerate(batches):
+            cx = ctxs[k % P]
+            o = outputs()
+            streams[k % P].wait_stream(torch.cuda.current_stream())  # the output buffers' fills
+            if k + P < K:
+                cx.match_allpairs_f32_run_prepare(d0, d1, nn_, nn_, o["idx"], None, batches[k + P][1], nn_, 0.8)
+            else:
+                cx.match_allpairs_f32_run(d0, d1, nn_, nn_, o["idx"], None, 0.8)
+            cx.pose_from_matches(prm, nn_, o["idx"], kp0, kp1, o["T"], o["nm"], o["ni"], o["st"])
+            outs.append(o)
+        torch.cuda.synchronize()
+        got = [host(o) for o in outs]
+    finally:
+        for c in ctxs:
+            c.close()
+
+    for k in range(K):
+        for key in ("idx", "nm", "ni", "st"):
+            assert (got[k][key] == ref[k][key]).all(), (P, k, key)
+        assert (_bits(got[k]["T"]) == _bits(ref[k]["T"])).all(), (P, k)
+        assert (ref[k]["st"] == 0).all(), (k, ref[k]["st"])
+    # the sequential reference itself against the oracle (first and last batch, one pair each)
+    for k in (0, K - 1):
+        d0, d1 = batches[k][0][0].cpu().numpy(), batches[k][1][0].cpu().numpy()
+        i2, _ = orc.allpairs_f32(d0, d1, 0.8)
+        assert (ref[k]["idx"][0] == i2).all(), k
