@@ -167,6 +167,16 @@ int mv_match_allpairs_f32_run_prepare_dev(mv_context *ctx, int batch, int cap, c
                                           const float *desc0, const float *desc1, double thresh, int *match_idx,
                                           float *match_score, int next_batch, int next_cap, const int *next_n1,
                                           const float *next_desc1);
+/* Sequence mode: the all-pairs match of CONSECUTIVE frames of one track (the reference's
+ * driver, scripts/run_pairwise_pnp.sh:7-20, runs pairwise_pnp.py on frames i, i + 1).
+ * desc[frames][cap][256] fp32, n[frames]; pair b = (frame b, frame b + 1) for
+ * b < frames - 1, outputs match_idx / match_score [frames - 1][cap] exactly as
+ * mv_match_allpairs_f32_dev on (desc[b], desc[b + 1]) would give them.  Every frame is
+ * quantised once and its int8 image serves as frame 1 of one pair and frame 0 of the next.
+ * Int8 screen only (MV_ERR_INVALID_ARG under MV_SCREEN_F16); frames >= 2; invalidates a
+ * prepared batch (the scratch image is reused). */
+int mv_match_sequence_f32_dev(mv_context *ctx, int frames, int cap, const int *n, const float *desc, double thresh,
+                              int *match_idx, float *match_score);
 /* nn_match_two_way (pairwise_pnp.py:281-323): mutual nearest neighbours under the
  * float32 distance sqrt(2 - 2 clip(s, -1, 1)) of the score s above (np.argmin: the first
  * NaN, else the first minimum), kept when dist < (float)nn_thresh and the reverse nearest

@@ -1056,3 +1056,20 @@ extern "C" int mv_debug_ap_trace(void *host, long bytes) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ap_trace), (size_t)bytes) == hipSuccess ? 0 : -3;
 }
 #endif
+
+extern "C" int mv_match_sequence_f32_dev(mv_context *ctx, int frames, int cap, const int *n, const float *desc,
+                                         double thresh, int *match_idx, float *match_score) {
+    MV_REQUIRE(ctx != nullptr && frames >= 2 && cap > 0 && n && desc && match_idx);
+    if (ctx->ap_screen != MV_SCREEN_I8) {
+        mv::set_error(MV_ERR_INVALID_ARG, "mv_match_sequence_f32_dev: the int8 screen only");
+        return MV_ERR_INVALID_ARG;
+    }
+    MV_HIP_TRY(hipSetDevice(ctx->device));
+    void *scr = ap_scratch(ctx, mv::allpairs_f32_scratch_bytes(frames, cap));
+    if (!scr) return MV_ERR_OUT_OF_MEMORY;
+    ctx->prep_desc1 = nullptr;  // the prepared image is overwritten
+    if (ctx->aux_stream) MV_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_prep, 0));  // a staging in flight
+    const int st = mv::launch_allpairs_q8_sequence(ctx->stream, scr, frames, cap, n, desc, thresh, match_idx,
+                                                   match_score);
+    return st != MV_OK ? st : mv::set_status(MV_OK);
+}

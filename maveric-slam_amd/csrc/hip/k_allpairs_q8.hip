@@ -375,13 +375,21 @@ __global__ __launch_bounds__(256) void k_q8_split(int batch, int cap, const int 
 }
 
 // ---- k_q8_match ----
+// AI8 (sequence mode): frame 0 arrives already quantised by k_q8_split -- its int8 image q0,
+// scales s0v, |a|^2 na2v and pair flags bad0 (the previous pair's frame-1 image) -- so the A
+// phase copies 256 B per row instead of reading 1 KiB of fp32 and quantising it.  The window
+// is unchanged: the split's codes RNE(a RN(127/m)) with s_a = RN(m/127) satisfy the same
+// |1 - q s_a| < 2^-21 that the in-register quantisation guarantees.
+template <bool AI8>
 __device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *__restrict__ n0v,
                                                       const int *__restrict__ n1v, const float *__restrict__ desc0,
                                                       const float *__restrict__ desc1, const char *__restrict__ q1,
                                                       const float *__restrict__ s1v, const float *__restrict__ nb2v,
                                                       const float *__restrict__ eb2v, const int *__restrict__ bad,
                                                       double thresh, int dmode, int *__restrict__ match_idx,
-                                                      float *__restrict__ match_score) {
+                                                      float *__restrict__ match_score, const char *__restrict__ q0,
+                                                      const float *__restrict__ s0v, const float *__restrict__ na2v,
+                                                      const int *__restrict__ bad0) {
     __shared__ __attribute__((aligned(16))) char lds[Q_LDS];
     float *misc = reinterpret_cast<float *>(lds + Q_OFF_MISC);
 #ifdef Q8_EXP_TRACE
@@ -505,6 +513,30 @@ __device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *
         constexpr int QB = Q8_QB;  // row quads (4 QB loads per lane) in flight
 #pragma unroll
         for (int g = 0; g < Q_RG; g++) {
+            if constexpr (AI8) {
+                // the group's 32 rows of the split image: lane sub holds chunk sub (k = 16 sub ..
+                // +15) of row 4 qd + rq, stored at the swizzled chunk the readback expects
+                const char *QA = q0 + (size_t)pair * cap * KD;
+                i32x4 v[8];
+#pragma unroll
+                for (int qd = 0; qd < 8; qd++) {
+                    const int ga = min(row0 + w * 64 + g * 32 + 4 * qd + rq, n0 - 1);
+                    v[qd] = *reinterpret_cast<const i32x4 *>(QA + (size_t)ga * KD + 16 * sub);
+                }
+                if (lane < 32) {  // row lane of the group: |a|^2 and s_a (< 0: exact path)
+                    const size_t ga = (size_t)pair * cap + min(row0 + w * 64 + g * 32 + lane, n0 - 1);
+                    const float sa = s0v[ga], q2 = na2v[ga];
+                    // the in-register path's range rule on m = 127 s_a, conservatively; zero rows too
+                    const bool afull = bad0[pair] != 0 || !(q2 <= FLT_MAX) || !(sa >= SCALE_LO) ||
+                                       !(sa <= SCALE_HI * (1.f / 128.f));
+                    rowv[w * 64 + g * 32 + lane] = make_float2(q2, afull ? -1.f : sa);
+                }
+#pragma unroll
+                for (int qd = 0; qd < 8; qd++) {
+                    const int r = 4 * qd + rq;
+                    *reinterpret_cast<i32x4 *>(img + r * KD + ((sub ^ (r & 15)) << 4)) = v[qd];
+                }
+            } else {
 #pragma unroll
             for (int qd0 = 0; qd0 < 8; qd0 += QB) {
                 f32x4v x[QB][4];
@@ -546,6 +578,7 @@ __device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *
                             pack4_q8(x[qd][u][0], x[qd][u][1], x[qd][u][2], x[qd][u][3], q);
                 }
             }
+            }  // !AI8
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own image writes
 #pragma unroll
             for (int s2 = 0; s2 < KD / 32; s2++)
@@ -997,6 +1030,7 @@ __device__ __forceinline__ void q8_match_block(int tiles_r, int cap, const int *
 // given (nrows > 0) -- this block's share of the next batch's frame-1 staging (the k_q8_split
 // passes, rows blockIdx * rpb .. +rpb): the separate staging kernel, its launch and its
 // stream hand-off leave the pipelined step; its HBM reads overlap the co-resident block's sweep.
+template <bool AI8>
 __global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, const int *__restrict__ n0v,
                                                       const int *__restrict__ n1v, const float *__restrict__ desc0,
                                                       const float *__restrict__ desc1, const char *__restrict__ q1,
@@ -1007,13 +1041,15 @@ __global__ __launch_bounds__(Q_NT, 2) void k_q8_match(int tiles_r, int cap, cons
                                                       const int *__restrict__ nn1, const float *__restrict__ ndesc1,
                                                       char *__restrict__ nq1, float *__restrict__ ns1,
                                                       float *__restrict__ nnb2, float *__restrict__ neb2,
-                                                      int *__restrict__ nbad) {
+                                                      int *__restrict__ nbad, const char *__restrict__ q0,
+                                                      const float *__restrict__ s0v, const float *__restrict__ na2v,
+                                                      const int *__restrict__ bad0) {
     const long rpb = ((nrows + gridDim.x - 1) / gridDim.x + QS_ROWS - 1) / QS_ROWS * QS_ROWS;
     const long lo = (long)blockIdx.x * rpb, hi = min(lo + rpb, nrows);
     if (Q8_FUSE_HEAD)  // timing switch: the staging share before the tile instead of after it
         for (long R0 = lo; R0 < hi; R0 += QS_ROWS) q8_split_pass(R0, hi, ncap, nn1, ndesc1, nq1, ns1, nnb2, neb2, nbad);
-    q8_match_block(tiles_r, cap, n0v, n1v, desc0, desc1, q1, s1v, nb2v, eb2v, bad, thresh, dmode, match_idx,
-                   match_score);
+    q8_match_block<AI8>(tiles_r, cap, n0v, n1v, desc0, desc1, q1, s1v, nb2v, eb2v, bad, thresh, dmode, match_idx,
+                        match_score, q0, s0v, na2v, bad0);
     if (!Q8_FUSE_HEAD && nrows > 0) {
         __syncthreads();  // every wave is past its sweep (the tail needs no LDS)
         for (long R0 = lo; R0 < hi; R0 += QS_ROWS) q8_split_pass(R0, hi, ncap, nn1, ndesc1, nq1, ns1, nnb2, neb2, nbad);
@@ -1086,9 +1122,10 @@ int launch_allpairs_q8_match_prepare(hipStream_t s, void *scratch, int batch, in
         MV_HIP_TRY(hipMemsetAsync(nm.bad, 0, (size_t)next_batch * 4, s));
     }
     MV_PROF_BEGIN(s, "k_q8_match");
-    hipLaunchKernelGGL(k_q8_match, dim3((unsigned)blocks), dim3(Q_NT), 0, s, tiles_r, cap, n0, n1, desc0, desc1, m.q1,
-                       m.s1, m.nb2, m.eb2, m.bad, dmode ? -1e300 : thresh, dmode, match_idx, match_score, nrows,
-                       next_cap, next_n1, next_desc1, nm.q1, nm.s1, nm.nb2, nm.eb2, nm.bad);
+    hipLaunchKernelGGL(k_q8_match<false>, dim3((unsigned)blocks), dim3(Q_NT), 0, s, tiles_r, cap, n0, n1, desc0,
+                       desc1, m.q1, m.s1, m.nb2, m.eb2, m.bad, dmode ? -1e300 : thresh, dmode, match_idx, match_score,
+                       nrows, next_cap, next_n1, next_desc1, nm.q1, nm.s1, nm.nb2, nm.eb2, nm.bad,
+                       (const char *)nullptr, (const float *)nullptr, (const float *)nullptr, (const int *)nullptr);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     return MV_OK;
@@ -1099,6 +1136,32 @@ int launch_allpairs_q8_match(hipStream_t s, void *scratch, int batch, int cap, c
                              float *match_score, int dmode) {
     return launch_allpairs_q8_match_prepare(s, scratch, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
                                             match_score, dmode, nullptr, 0, 0, nullptr, nullptr);
+}
+
+// Sequence mode: frames 0 .. F-1 of one track, pair b = (frame b, frame b + 1).  Every frame
+// is quantised ONCE (one k_q8_split over all F frames); pair b then reads frame b's image as
+// its A operand and frame b + 1's as its B operand -- plain offsets into the one scratch.
+int launch_allpairs_q8_sequence(hipStream_t s, void *scratch, int frames, int cap, const int *n, const float *desc,
+                                double thresh, int *match_idx, float *match_score) {
+    MV_REQUIRE(frames >= 2 && cap > 0 && n && desc && match_idx && scratch);
+    MV_REQUIRE(((uintptr_t)desc & 15) == 0);
+    MV_REQUIRE((long)cap * KD < (1l << 31));
+    const int st = launch_allpairs_q8_prepare(s, scratch, frames, cap, n, desc);
+    if (st != MV_OK) return st;
+    const int batch = frames - 1, tiles_r = (cap + Q_BM - 1) / Q_BM;
+    const long blocks = (long)batch * tiles_r;
+    MV_REQUIRE(blocks < (1l << 31));
+    const Q8Scratch m = q8_map(scratch, frames, cap);
+    const size_t fr = (size_t)cap;
+    MV_PROF_BEGIN(s, "k_q8_match_seq");
+    hipLaunchKernelGGL(k_q8_match<true>, dim3((unsigned)blocks), dim3(Q_NT), 0, s, tiles_r, cap, n, n + 1, desc,
+                       desc + fr * KD, m.q1 + fr * KD, m.s1 + fr, m.nb2 + fr, m.eb2 + fr, m.bad + 1, thresh, 0,
+                       match_idx, match_score, 0l, 0, (const int *)nullptr, (const float *)nullptr, (char *)nullptr,
+                       (float *)nullptr, (float *)nullptr, (float *)nullptr, (int *)nullptr, (const char *)m.q1,
+                       (const float *)m.s1, (const float *)m.nb2, (const int *)m.bad);
+    MV_PROF_END(s);
+    MV_LAUNCH_CHECK();
+    return MV_OK;
 }
 
 }  // namespace mv

@@ -99,6 +99,9 @@ int launch_allpairs_q8_prepare(hipStream_t s, void *scratch, int batch, int cap,
 int launch_allpairs_q8_match(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
                              const float *desc0, const float *desc1, double thresh, int *match_idx,
                              float *match_score, int dmode = 0);
+// sequence mode: frames 0 .. frames-1, pair b = (b, b + 1); every frame quantised once
+int launch_allpairs_q8_sequence(hipStream_t s, void *scratch, int frames, int cap, const int *n, const float *desc,
+                                double thresh, int *match_idx, float *match_score);
 // the match plus the next batch's frame-1 staging into next_scratch, in one launch
 int launch_allpairs_q8_match_prepare(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
                                      const float *desc0, const float *desc1, double thresh, int *match_idx,

@@ -116,6 +116,7 @@ def lib():
             "mv_match_allpairs_f32_prepare_dev": (_I, [_P, _I, _I, _P, _P]),
             "mv_match_allpairs_f32_run_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _D, _P, _P]),
             "mv_match_allpairs_f32_run_prepare_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _D, _P, _P, _I, _I, _P, _P]),
+            "mv_match_sequence_f32_dev": (_I, [_P, _I, _I, _P, _P, _D, _P, _P]),
             "mv_match_allpairs_i8_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P]),
             "mv_match_two_way_f32_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _D, _P, _P]),
             "mv_run_nms_batch_dev": (_I, [_P, _I, _I, _I, _P, _P, _P, _P]),
@@ -628,6 +629,13 @@ class Context:
         B, cap = pts0.shape[0], pts0.shape[1]
         check(lib().mv_pose_batch_dev(self.h, ctypes.byref(params), B, cap, _t(n), _t(pts0), _t(pts1), _t(T),
                                       _t(num_inliers), _t(status)), "pose_batch")
+
+    def match_sequence_f32(self, desc, n, match_idx, match_score, thresh=0.8):
+        """Consecutive frames desc[F][cap][256] -> pairs (b, b + 1): match_idx[F-1][cap]
+        (mv_match_sequence_f32_dev; every frame quantised once)."""
+        F, cap = desc.shape[0], desc.shape[1]
+        check(lib().mv_match_sequence_f32_dev(self.h, F, cap, _t(n), _t(desc), float(thresh), _t(match_idx),
+                                              _t(match_score)), "match_sequence_f32")
 
     def pose_from_matches(self, params, n0, match_idx, kp0, kp1, T, num_matches, num_inliers, status):
         B, cap = kp0.shape[0], kp0.shape[1]
