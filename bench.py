@@ -435,6 +435,12 @@ def main():
         r = bench_i8.run(batch=2048, kp=2048, steps=args.extra_steps, warmup=2, check=1)
         out["i8_allpairs"] = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "stages_ms",
                                                   "mfma_roofline", "checked_pairs")}
+        import bench_sequence
+
+        # the headline's workload as a TRACK (consecutive frames, each quantised once)
+        r = bench_sequence.run(frames=B + 1, kp=n, steps=args.extra_steps, warmup=2, check=1, pipeline=P)
+        out["sequence"] = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "pairs_per_step", "stages_ms",
+                                              "staging", "hbm_roofline", "checked_pairs", "pose_ok")}
         r = bench_keypoints.run(batch=1024, steps=args.extra_steps, warmup=2, check=1)
         out["keypoints"] = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "stages_ms",
                                                "hbm_roofline", "checked_frames")}

@@ -177,6 +177,14 @@ int mv_match_allpairs_f32_run_prepare_dev(mv_context *ctx, int batch, int cap, c
  * prepared batch (the scratch image is reused). */
 int mv_match_sequence_f32_dev(mv_context *ctx, int frames, int cap, const int *n, const float *desc, double thresh,
                               int *match_idx, float *match_score);
+/* Pipelined sequence mode: a track processed in chunks of frames.  Stage the first chunk with
+ * mv_match_allpairs_f32_prepare_dev(ctx, frames, cap, n, desc) (the images of all its frames),
+ * then call this per chunk: ONE kernel matches the chunk's frames - 1 pairs from the prepared
+ * images and stages the next chunk's frames (next_*) into the context's second image, which
+ * becomes the prepared one.  (frames, cap, n, desc) must be those of the last prepare. */
+int mv_match_sequence_f32_run_prepare_dev(mv_context *ctx, int frames, int cap, const int *n, const float *desc,
+                                          double thresh, int *match_idx, float *match_score, int next_frames,
+                                          int next_cap, const int *next_n, const float *next_desc);
 /* nn_match_two_way (pairwise_pnp.py:281-323): mutual nearest neighbours under the
  * float32 distance sqrt(2 - 2 clip(s, -1, 1)) of the score s above (np.argmin: the first
  * NaN, else the first minimum), kept when dist < (float)nn_thresh and the reverse nearest

@@ -944,6 +944,38 @@ extern "C" int mv_match_allpairs_f32_run_dev(mv_context *ctx, int batch, int cap
                     match_idx, match_score);
 }
 
+namespace {
+// the context's second image, grown to `need` bytes (run_prepare's staging target)
+int ap_scratch2(mv_context *ctx, size_t need) {
+    if (ctx->ap_scratch2_bytes >= need) return MV_OK;
+    if (ctx->ap_scratch2) {
+        (void)hipDeviceSynchronize();  // growing: nothing may still use the old buffer
+        (void)hipFree(ctx->ap_scratch2);
+        ctx->ap_scratch2 = nullptr;
+        ctx->ap_scratch2_bytes = 0;
+    }
+    const size_t b = mv::align_up(need, 1 << 20);
+    if (hipMalloc(&ctx->ap_scratch2, b) != hipSuccess) {
+        mv::set_error(MV_ERR_OUT_OF_MEMORY, "all-pairs scratch allocation of %zu bytes failed", b);
+        return MV_ERR_OUT_OF_MEMORY;
+    }
+    ctx->ap_scratch2_bytes = b;
+    return MV_OK;
+}
+void ap_swap_prepared(mv_context *ctx, int batch, int cap, const int *n1, const float *desc1) {
+    void *t = ctx->ap_scratch;
+    size_t tb = ctx->ap_scratch_bytes;
+    ctx->ap_scratch = ctx->ap_scratch2;
+    ctx->ap_scratch_bytes = ctx->ap_scratch2_bytes;
+    ctx->ap_scratch2 = t;
+    ctx->ap_scratch2_bytes = tb;
+    ctx->prep_batch = batch;
+    ctx->prep_cap = cap;
+    ctx->prep_n1 = n1;
+    ctx->prep_desc1 = desc1;
+}
+}  // namespace
+
 extern "C" int mv_match_allpairs_f32_run_prepare_dev(mv_context *ctx, int batch, int cap, const int *n0,
                                                      const int *n1, const float *desc0, const float *desc1,
                                                      double thresh, int *match_idx, float *match_score,
@@ -1072,4 +1104,27 @@ extern "C" int mv_match_sequence_f32_dev(mv_context *ctx, int frames, int cap, c
     const int st = mv::launch_allpairs_q8_sequence(ctx->stream, scr, frames, cap, n, desc, thresh, match_idx,
                                                    match_score);
     return st != MV_OK ? st : mv::set_status(MV_OK);
+}
+
+extern "C" int mv_match_sequence_f32_run_prepare_dev(mv_context *ctx, int frames, int cap, const int *n,
+                                                     const float *desc, double thresh, int *match_idx,
+                                                     float *match_score, int next_frames, int next_cap,
+                                                     const int *next_n, const float *next_desc) {
+    MV_REQUIRE(ctx != nullptr && frames >= 2 && next_frames >= 2 && next_cap > 0 && next_n && next_desc);
+    if (ctx->ap_screen != MV_SCREEN_I8 || !ctx->prep_desc1 || ctx->prep_batch != frames || ctx->prep_cap != cap ||
+        ctx->prep_n1 != n || ctx->prep_desc1 != desc || ctx->prep_screen != MV_SCREEN_I8) {
+        mv::set_error(MV_ERR_INVALID_ARG,
+                      "mv_match_sequence_f32_run_prepare_dev: no matching prepare for these frames (int8 screen)");
+        return MV_ERR_INVALID_ARG;
+    }
+    MV_HIP_TRY(hipSetDevice(ctx->device));
+    const int sc = ap_scratch2(ctx, mv::allpairs_f32_scratch_bytes(next_frames, next_cap));
+    if (sc != MV_OK) return sc;
+    if (ctx->aux_stream) MV_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_prep, 0));
+    const int st = mv::launch_allpairs_q8_sequence(ctx->stream, ctx->ap_scratch, frames, cap, n, desc, thresh,
+                                                   match_idx, match_score, true, ctx->ap_scratch2, next_frames,
+                                                   next_cap, next_n, next_desc);
+    if (st != MV_OK) return st;
+    ap_swap_prepared(ctx, next_frames, next_cap, next_n, next_desc);
+    return mv::set_status(MV_OK);
 }

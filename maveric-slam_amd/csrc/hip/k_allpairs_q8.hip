@@ -1141,24 +1141,40 @@ int launch_allpairs_q8_match(hipStream_t s, void *scratch, int batch, int cap, c
 // Sequence mode: frames 0 .. F-1 of one track, pair b = (frame b, frame b + 1).  Every frame
 // is quantised ONCE (one k_q8_split over all F frames); pair b then reads frame b's image as
 // its A operand and frame b + 1's as its B operand -- plain offsets into the one scratch.
+// prepared = true: the frames' images are already in scratch (a prepare / the previous
+// run_prepare staged them).  next_scratch: the launch also stages the next chunk's frames into
+// it (k_q8_split passes after each workgroup's tile, as launch_allpairs_q8_match_prepare).
 int launch_allpairs_q8_sequence(hipStream_t s, void *scratch, int frames, int cap, const int *n, const float *desc,
-                                double thresh, int *match_idx, float *match_score) {
+                                double thresh, int *match_idx, float *match_score, bool prepared,
+                                void *next_scratch, int next_frames, int next_cap, const int *next_n,
+                                const float *next_desc) {
     MV_REQUIRE(frames >= 2 && cap > 0 && n && desc && match_idx && scratch);
     MV_REQUIRE(((uintptr_t)desc & 15) == 0);
     MV_REQUIRE((long)cap * KD < (1l << 31));
-    const int st = launch_allpairs_q8_prepare(s, scratch, frames, cap, n, desc);
-    if (st != MV_OK) return st;
+    if (!prepared) {
+        const int st = launch_allpairs_q8_prepare(s, scratch, frames, cap, n, desc);
+        if (st != MV_OK) return st;
+    }
     const int batch = frames - 1, tiles_r = (cap + Q_BM - 1) / Q_BM;
     const long blocks = (long)batch * tiles_r;
     MV_REQUIRE(blocks < (1l << 31));
     const Q8Scratch m = q8_map(scratch, frames, cap);
+    Q8Scratch nm = {};
+    long nrows = 0;
+    if (next_scratch) {
+        MV_REQUIRE(next_frames > 0 && next_cap > 0 && next_n && next_desc && next_scratch != scratch);
+        MV_REQUIRE(((uintptr_t)next_desc & 15) == 0);
+        MV_REQUIRE((long)next_cap * KD < (1l << 31));
+        nm = q8_map(next_scratch, next_frames, next_cap);
+        nrows = (long)next_frames * next_cap;
+        MV_HIP_TRY(hipMemsetAsync(nm.bad, 0, (size_t)next_frames * 4, s));
+    }
     const size_t fr = (size_t)cap;
     MV_PROF_BEGIN(s, "k_q8_match_seq");
     hipLaunchKernelGGL(k_q8_match<true>, dim3((unsigned)blocks), dim3(Q_NT), 0, s, tiles_r, cap, n, n + 1, desc,
                        desc + fr * KD, m.q1 + fr * KD, m.s1 + fr, m.nb2 + fr, m.eb2 + fr, m.bad + 1, thresh, 0,
-                       match_idx, match_score, 0l, 0, (const int *)nullptr, (const float *)nullptr, (char *)nullptr,
-                       (float *)nullptr, (float *)nullptr, (float *)nullptr, (int *)nullptr, (const char *)m.q1,
-                       (const float *)m.s1, (const float *)m.nb2, (const int *)m.bad);
+                       match_idx, match_score, nrows, next_cap, next_n, next_desc, nm.q1, nm.s1, nm.nb2, nm.eb2,
+                       nm.bad, (const char *)m.q1, (const float *)m.s1, (const float *)m.nb2, (const int *)m.bad);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     return MV_OK;

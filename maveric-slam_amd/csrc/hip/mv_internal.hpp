@@ -101,7 +101,9 @@ int launch_allpairs_q8_match(hipStream_t s, void *scratch, int batch, int cap, c
                              float *match_score, int dmode = 0);
 // sequence mode: frames 0 .. frames-1, pair b = (b, b + 1); every frame quantised once
 int launch_allpairs_q8_sequence(hipStream_t s, void *scratch, int frames, int cap, const int *n, const float *desc,
-                                double thresh, int *match_idx, float *match_score);
+                                double thresh, int *match_idx, float *match_score, bool prepared = false,
+                                void *next_scratch = nullptr, int next_frames = 0, int next_cap = 0,
+                                const int *next_n = nullptr, const float *next_desc = nullptr);
 // the match plus the next batch's frame-1 staging into next_scratch, in one launch
 int launch_allpairs_q8_match_prepare(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
                                      const float *desc0, const float *desc1, double thresh, int *match_idx,

@@ -117,6 +117,7 @@ def lib():
             "mv_match_allpairs_f32_run_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _D, _P, _P]),
             "mv_match_allpairs_f32_run_prepare_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _D, _P, _P, _I, _I, _P, _P]),
             "mv_match_sequence_f32_dev": (_I, [_P, _I, _I, _P, _P, _D, _P, _P]),
+            "mv_match_sequence_f32_run_prepare_dev": (_I, [_P, _I, _I, _P, _P, _D, _P, _P, _I, _I, _P, _P]),
             "mv_match_allpairs_i8_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _P]),
             "mv_match_two_way_f32_dev": (_I, [_P, _I, _I, _P, _P, _P, _P, _D, _P, _P]),
             "mv_run_nms_batch_dev": (_I, [_P, _I, _I, _I, _P, _P, _P, _P]),
@@ -636,6 +637,16 @@ class Context:
         F, cap = desc.shape[0], desc.shape[1]
         check(lib().mv_match_sequence_f32_dev(self.h, F, cap, _t(n), _t(desc), float(thresh), _t(match_idx),
                                               _t(match_score)), "match_sequence_f32")
+
+    def match_sequence_f32_run_prepare(self, desc, n, match_idx, match_score, next_desc, next_n, thresh=0.8):
+        """Match the prepared chunk desc[F] (pairs b, b + 1) and stage the next chunk's frames in the
+        same launch (mv_match_sequence_f32_run_prepare_dev); prepare the first chunk with
+        match_allpairs_f32_prepare(desc, n)."""
+        F, cap = desc.shape[0], desc.shape[1]
+        nF, ncap = next_desc.shape[0], next_desc.shape[1]
+        check(lib().mv_match_sequence_f32_run_prepare_dev(self.h, F, cap, _t(n), _t(desc), float(thresh),
+                                                          _t(match_idx), _t(match_score), nF, ncap, _t(next_n),
+                                                          _t(next_desc)), "match_sequence_f32_run_prepare")
 
     def pose_from_matches(self, params, n0, match_idx, kp0, kp1, T, num_matches, num_inliers, status):
         B, cap = kp0.shape[0], kp0.shape[1]

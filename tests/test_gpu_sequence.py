@@ -118,3 +118,54 @@ def test_sequence_refuses_f16_screen_and_short_tracks(ctx, torch_cuda):
         ctx.set_allpairs_screen("i8")
     with pytest.raises(RuntimeError):
         ctx.match_sequence_f32(D[:1], n[:1], idx, None)
+
+
+def test_sequence_run_prepare_chain(ctx, orc, torch_cuda):
+    """A track processed in chunks: the first chunk prepared, then each chunk matched while the next one's frames are staged in the
+    same launch; chunks of different lengths and caps, ragged counts, scores and indices-only,
+    each equal to the oracle pair by pair; a run without its prepare is refused."""
+    torch = torch_cuda
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(29)
+    chunks = []
+    for k, (F, cap) in enumerate(((4, 512), (6, 384), (3, 640), (5, 512))):
+        ns = [int(rng.integers(1, cap + 1)) for _ in range(F)]
+        if k == 1:
+            ns[2] = 0
+        D = _track(rng, F, cap, ns)
+        chunks.append((D, ns, torch.from_numpy(D).to(dev), torch.from_numpy(np.asarray(ns, np.int32)).to(dev)))
+    ctx.set_stream(torch.cuda.current_stream())
+    try:
+        D, ns, d, n = chunks[0]
+        ctx.match_allpairs_f32_prepare(d, n)
+        for k, (D, ns, d, n) in enumerate(chunks):
+            F, cap = D.shape[0], D.shape[1]
+            scores = k % 2 == 0
+            idx = torch.full((F - 1, cap), -7, dtype=torch.int32, device=dev)
+            sc = torch.zeros((F - 1, cap), dtype=torch.float32, device=dev) if scores else None
+            if k + 1 < len(chunks):
+                ctx.match_sequence_f32_run_prepare(d, n, idx, sc, chunks[k + 1][2], chunks[k + 1][3])
+            else:
+                ctx.match_sequence_f32(d, n, idx, sc)
+            torch.cuda.synchronize()
+            idx = idx.cpu().numpy()
+            sc = sc.cpu().numpy() if scores else None
+            for b in range(F - 1):
+                n0, n1 = ns[b], ns[b + 1]
+                assert (idx[b, n0:] == -1).all(), (k, b)
+                if n0 == 0:
+                    continue
+                if n1 == 0:
+                    assert (idx[b, :n0] == -1).all(), (k, b)
+                    continue
+                i2, s2 = orc.allpairs_f32(D[b, :n0], D[b + 1, :n1], 0.8)
+                assert (idx[b, :n0] == i2).all(), (k, b)
+                if scores:
+                    assert (_bits(sc[b, :n0]) == _bits(s2)).all(), (k, b)
+        # the one-shot call invalidated the prepared image: run_prepare is refused
+        D, ns, d, n = chunks[0]
+        with pytest.raises(RuntimeError):
+            ctx.match_sequence_f32_run_prepare(d, n, torch.empty((D.shape[0] - 1, D.shape[1]), dtype=torch.int32,
+                                                                 device=dev), None, d, n)
+    finally:
+        ctx.set_stream(None)
