@@ -6,7 +6,7 @@ frames) and matched as frame 1 of one pair and frame 0 of the next (k_q8_match<A
 the headline's pose per pair.  One step = one chunk of FRAMES frames = FRAMES - 1 pairs; P
 contexts on P streams take the chunks in turn.  Synthetic track: frame b + 1 re-observes 60 %
 of frame b (+ noise |0.3|); each pair's keypoints are exact projections under the 785 -> 786
-pose for its re-observed rows (as bench.gen_batch).  Prints one JSON line.  GPU only."""
+pose for its re-observed rows (as bench.gen_batch); see gen_track.  Prints one JSON line.  GPU only."""
 import argparse
 import json
 import os
@@ -26,34 +26,38 @@ HBM_PEAK_GBS = 8000.0
 
 
 def gen_track(dev, F, n, seed):
-    """F consecutive frames [F][n][256] and per-pair keypoints [F-1][n][2] x 2."""
+    """F consecutive frames [F][n][256] and per-pair keypoints [F-1][n][2] x 2, in a few
+    launches: landmarks along the track, frame b observes landmarks b s .. b s + n - 1 (s = 0.4 n,
+    so 60 % of frame b is re-observed by frame b + 1) in a random row order, each observation
+    the landmark's unit descriptor + noise |0.3| / sqrt 2 per frame (|0.3| between frames)."""
     import synth
 
     g = torch.Generator(device=dev)
     g.manual_seed(seed)
     m = int(round(0.6 * n))
-    d = torch.empty((F, n, KD), device=dev)
-    x = torch.randn((n, KD), generator=g, device=dev)
-    d[0] = x / x.norm(dim=1, keepdim=True)
-    srcs = torch.argsort(torch.rand((F - 1, n), generator=g, device=dev), dim=1)[:, :m]
-    orders = torch.argsort(torch.rand((F - 1, n), generator=g, device=dev), dim=1)
-    for b in range(F - 1):
-        y = torch.randn((n, KD), generator=g, device=dev)
-        y[:m] = d[b][srcs[b]] + torch.randn((m, KD), generator=g, device=dev) * (0.3 / 16.0)
-        y = y / y.norm(dim=1, keepdim=True)
-        d[b + 1] = y[orders[b]]
+    sh = n - m
+    base = torch.randn(((F - 1) * sh + n, KD), generator=g, device=dev)
+    base = base / base.norm(dim=1, keepdim=True)
+    perm = torch.argsort(torch.rand((F, n), generator=g, device=dev), dim=1)  # row -> local landmark
+    lid = perm + torch.arange(F, device=dev)[:, None] * sh
+    d = base[lid] + torch.randn((F, n, KD), generator=g, device=dev) * (0.3 / 16.0 / np.sqrt(2.0))
+    d = d / d.norm(dim=2, keepdim=True)
+    del base
     rng = np.random.default_rng(seed)
+    perm_h = perm.cpu().numpy()
+    inv = np.argsort(perm_h, axis=1)  # local landmark -> row
     kp0 = np.empty((F - 1, n, 2), np.float32)
     kp1 = np.empty((F - 1, n, 2), np.float32)
-    src_h, order_h = srcs.cpu().numpy(), orders.cpu().numpy()
     R, t = synth.T_785_786[:, :3], synth.T_785_786[:, 3]
     for b in range(F - 1):
         _, x0, x1 = synth.synth_scene(rng, n, R, t)
         k1 = np.stack([rng.uniform(0, synth.KITTI_W, n), rng.uniform(0, synth.KITTI_H, n)], 1)
-        k1[:m] = x1[src_h[b]]
+        loc = perm_h[b + 1]  # frame b + 1's rows: local landmark; re-observed when loc < m
+        re = loc < m
+        k1[re] = x1[inv[b][loc[re] + sh]]  # the frame-b row of the same landmark
         kp0[b] = x0
-        kp1[b] = k1[order_h[b]]
-    return d, torch.from_numpy(kp0).to(dev), torch.from_numpy(kp1).to(dev)
+        kp1[b] = k1
+    return d.contiguous(), torch.from_numpy(kp0).to(dev), torch.from_numpy(kp1).to(dev)
 
 
 def run(frames=8193, kp=1024, steps=20, warmup=3, check=1, pipeline=3, fused=True):
@@ -127,11 +131,12 @@ def run(frames=8193, kp=1024, steps=20, warmup=3, check=1, pipeline=3, fused=Tru
     assert ok == B and float(err.max()) < 1e-3, "pose failed: ok=%d max|dR|=%g" % (ok, err.max())
     for c in ctxs:
         c.close()
-    # algorithmic bytes of k_q8_match_seq per pair: per row of frame 0 its int8 row + s + |a|^2
-    # (264 B), per column of frame 1 its int8 row + s + |b|^2 + |eps|^2 (268 B), the index (4 B)
-    # fused: the launch also stages the next chunk (per frame row 1 KiB read + 268 B written)
+    # algorithmic bytes of k_q8_match_seq: every frame's image read ONCE (int8 row + s + |b|^2 +
+    # |eps|^2 = 268 B per row; pair b's frame 1 is pair b + 1's frame 0 -- the same bytes, and
+    # rocprof counts them once: profiles/r02i_seq_summary.json, 1.003x this figure), the
+    # index (4 B per row); fused: the next chunk's staging (per row 1 KiB read + 268 B written)
     split_bytes = F * n * (KD * 4 + 268)
-    seq_bytes = B * n * (264 + 268 + 4) + (split_bytes if fused else 0)
+    seq_bytes = F * n * 268 + B * n * 4 + (split_bytes if fused else 0)
     mseq = stages["k_q8_match_seq"] * 1e-3
     return {
         "metric": "tracked frame-pairs/sec, sequence mode (consecutive frames, each quantised once), "
