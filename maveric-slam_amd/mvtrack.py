@@ -205,6 +205,20 @@ def read_transform_npy(path):
     return st, T.reshape(3, 4)
 
 
+def sequence_shard(frames, world, rank):
+    """Frames [lo, hi) of a track of `frames` frames that `rank` of `world` matches in sequence
+    mode: the frames - 1 pairs (b, b + 1) are split into contiguous, near-equal ranges, and a
+    rank's frames run one past its last pair, so neighbouring ranks share one boundary frame
+    and every pair is matched by exactly one rank -- no data-path collective.  A rank with no
+    pair gets lo == hi."""
+    if frames < 2 or world < 1 or not 0 <= rank < world:
+        raise ValueError("sequence_shard: frames >= 2, 0 <= rank < world")
+    pairs = frames - 1
+    p_lo = rank * pairs // world
+    p_hi = (rank + 1) * pairs // world
+    return (p_lo, p_hi + 1) if p_hi > p_lo else (p_lo, p_lo)
+
+
 def chain_sharded(chain_local, rebase, gather, rank, rel_local, mode):
     """A sequence sharded over ranks in order (rank r holds transforms [k_r, k_{r+1})):
     each rank chains its shard from the identity (chain_local(rel) -> poses [len+1, 3, 4]),

@@ -153,3 +153,87 @@ def test_two_rank_sharded_trajectory_gloo():
         assert got.shape == full.shape
         assert np.abs(got - full).max() < 1e-12
         assert np.abs(out[1][mode][0] - out[0][mode][-1]).max() < 1e-12  # rank 1 starts where rank 0 ends
+
+
+def test_sequence_shard_covers_every_pair_once():
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "maveric-slam_amd"))
+    import mvtrack
+
+    for F in (2, 3, 5, 17, 8193):
+        for W in (1, 2, 3, 4, 8, 16):
+            seen = []
+            prev_hi = None
+            for r in range(W):
+                lo, hi = mvtrack.sequence_shard(F, W, r)
+                if hi > lo:
+                    assert hi - lo >= 2
+                    if prev_hi is not None:
+                        assert lo == prev_hi - 1  # one shared boundary frame
+                    prev_hi = hi
+                    seen += list(range(lo, hi - 1))
+            assert seen == list(range(F - 1)), (F, W)
+    with pytest.raises(ValueError):
+        mvtrack.sequence_shard(1, 2, 0)
+
+
+def _seq_worker(rank, world, port, q):
+    import sys
+
+    import torch
+    import torch.distributed as dist
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "oracle"), os.path.join(root, "maveric-slam_amd")):
+        sys.path.insert(0, p)
+    import mvtrack
+    import oracle
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    F, n = 6, 40
+    rng = np.random.default_rng(5)  # every rank sees the same track (its frames only are used)
+    D = rng.standard_normal((F, n, 256)).astype(np.float32)
+    for b in range(1, F):
+        D[b, :24] = D[b - 1, rng.permutation(n)[:24]] + 0.02 * rng.standard_normal((24, 256)).astype(np.float32)
+    D /= np.linalg.norm(D, axis=2, keepdims=True)
+    lo, hi = mvtrack.sequence_shard(F, world, rank)
+    mine = [(b, oracle.allpairs_f32(D[b], D[b + 1], 0.8)[0].tolist()) for b in range(lo, hi - 1)]
+    out = [None] * world
+    dist.all_gather_object(out, mine)  # validation only
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def test_two_rank_sequence_shards_gloo():
+    """Sequence mode over 2 ranks: each matches its contiguous pair range (one shared boundary
+    frame, no exchange); together they reproduce the single-process track pair for pair."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    import oracle
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_seq_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    F, n = 6, 40
+    rng = np.random.default_rng(5)
+    D = rng.standard_normal((F, n, 256)).astype(np.float32)
+    for b in range(1, F):
+        D[b, :24] = D[b - 1, rng.permutation(n)[:24]] + 0.02 * rng.standard_normal((24, 256)).astype(np.float32)
+    D /= np.linalg.norm(D, axis=2, keepdims=True)
+    got = sorted(x for shard in res[0] for x in shard)
+    assert [b for b, _ in got] == list(range(F - 1))
+    for b, idx in got:
+        assert idx == oracle.allpairs_f32(D[b], D[b + 1], 0.8)[0].tolist(), b
+    assert res[0] == res[1]
