@@ -988,21 +988,8 @@ extern "C" int mv_match_allpairs_f32_run_prepare_dev(mv_context *ctx, int batch,
         return MV_ERR_INVALID_ARG;
     }
     MV_HIP_TRY(hipSetDevice(ctx->device));
-    const size_t need = mv::allpairs_f32_scratch_bytes(next_batch, next_cap);
-    if (ctx->ap_scratch2_bytes < need) {
-        if (ctx->ap_scratch2) {
-            (void)hipDeviceSynchronize();  // growing: nothing may still use the old buffer
-            (void)hipFree(ctx->ap_scratch2);
-            ctx->ap_scratch2 = nullptr;
-            ctx->ap_scratch2_bytes = 0;
-        }
-        const size_t b = mv::align_up(need, 1 << 20);
-        if (hipMalloc(&ctx->ap_scratch2, b) != hipSuccess) {
-            mv::set_error(MV_ERR_OUT_OF_MEMORY, "all-pairs scratch allocation of %zu bytes failed", b);
-            return MV_ERR_OUT_OF_MEMORY;
-        }
-        ctx->ap_scratch2_bytes = b;
-    }
+    const int sc = ap_scratch2(ctx, mv::allpairs_f32_scratch_bytes(next_batch, next_cap));
+    if (sc != MV_OK) return sc;
     if (ctx->aux_stream) MV_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_prep, 0));
     int st;
     if (ctx->ap_screen == MV_SCREEN_I8) {
@@ -1016,17 +1003,7 @@ extern "C" int mv_match_allpairs_f32_run_prepare_dev(mv_context *ctx, int batch,
             st = ap_prepare(ctx->ap_screen, ctx->stream, ctx->ap_scratch2, next_batch, next_cap, next_n1, next_desc1);
     }
     if (st != MV_OK) return st;
-    // the next batch's image is now the prepared one
-    void *t = ctx->ap_scratch;
-    size_t tb = ctx->ap_scratch_bytes;
-    ctx->ap_scratch = ctx->ap_scratch2;
-    ctx->ap_scratch_bytes = ctx->ap_scratch2_bytes;
-    ctx->ap_scratch2 = t;
-    ctx->ap_scratch2_bytes = tb;
-    ctx->prep_batch = next_batch;
-    ctx->prep_cap = next_cap;
-    ctx->prep_n1 = next_n1;
-    ctx->prep_desc1 = next_desc1;
+    ap_swap_prepared(ctx, next_batch, next_cap, next_n1, next_desc1);  // the next batch is now the prepared one
     return mv::set_status(MV_OK);
 }
 
