@@ -84,6 +84,10 @@ def test_no_device_fails_loudly(capfd):
                     pr.ctypes.data_as(ctypes.c_void_p))
     assert ns.value == -1
     assert "no HIP device" in capfd.readouterr().err
+    # without a context (none can exist here) the batched entry points refuse, never compute
+    assert L.mv_match_sequence_f32_dev(None, 3, 64, None, None, 0.8, None, None) != mvtrack.MV_OK
+    assert L.mv_match_sequence_f32_run_prepare_dev(None, 3, 64, None, None, 0.8, None, None, 3, 64, None,
+                                                   None) != mvtrack.MV_OK
 
 
 def test_frame_header_compiles_as_c(tmp_path):
