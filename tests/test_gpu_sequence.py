@@ -169,3 +169,69 @@ def test_sequence_run_prepare_chain(ctx, orc, torch_cuda):
                                                                  device=dev), None, d, n)
     finally:
         ctx.set_stream(None)
+
+
+def test_sequence_track_end_to_end(ctx, orc, torch_cuda):
+    """A camera moving by the 785 -> 786 transform per frame through a 3-D scene: each frame
+    re-observes the previous frame's points still in view (60 % of its rows) and adds fresh
+    ones; per-frame keypoints are exact projections.  Sequence-mode match + pose over the
+    per-frame keypoints as two offset views (kp[:-1], kp[1:]) recovers every pair's rotation."""
+    import mvtrack
+    import synth
+
+    torch = torch_cuda
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(41)
+    F, n = 6, 512
+    m = int(0.6 * n)
+    R, t = synth.T_785_786[:, :3], synth.T_785_786[:, 3]
+    K = synth.KITTI_K
+
+    def project(P):
+        q = P @ K.T
+        return q[:, :2] / q[:, 2:3]
+
+    P, _, _ = synth.synth_scene(rng, n, R, t)  # frame 0 points, visible in frame 1
+    desc = [rng.standard_normal((n, 256))]
+    pts = [P]
+    for k in range(1, F):
+        Q = pts[-1] @ R.T + t  # the previous frame's points in frame k
+        q = project(Q)
+        vis = np.nonzero((Q[:, 2] > 0.5) & (q[:, 0] >= 0) & (q[:, 0] < synth.KITTI_W) & (q[:, 1] >= 0) &
+                         (q[:, 1] < synth.KITTI_H))[0]
+        src = rng.permutation(vis)[:m]
+        fresh, _, _ = synth.synth_scene(rng, n - len(src), R, t)
+        order = rng.permutation(n)
+        Pk = np.concatenate([Q[src], fresh])[order]
+        dk = np.concatenate([desc[-1][src] / np.linalg.norm(desc[-1][src], axis=1, keepdims=True) +
+                             rng.standard_normal((len(src), 256)) * (0.3 / 16),
+                             rng.standard_normal((n - len(src), 256))])[order]
+        pts.append(Pk)
+        desc.append(dk)
+    D = np.stack([d / np.linalg.norm(d, axis=1, keepdims=True) for d in desc]).astype(np.float32)
+    KP = np.stack([project(p) for p in pts]).astype(np.float32)
+    d = torch.from_numpy(D).to(dev)
+    kp = torch.from_numpy(KP).to(dev)
+    nf = torch.full((F,), n, dtype=torch.int32, device=dev)
+    idx = torch.empty((F - 1, n), dtype=torch.int32, device=dev)
+    T = torch.empty((F - 1, 3, 4), dtype=torch.float32, device=dev)
+    nm = torch.empty(F - 1, dtype=torch.int32, device=dev)
+    ni = torch.empty(F - 1, dtype=torch.int32, device=dev)
+    st = torch.full((F - 1,), 99, dtype=torch.int32, device=dev)
+    prm = mvtrack.pose_params(mvtrack.AS_INTENDED, fx=K[0, 0], fy=K[1, 1], cx=K[0, 2], cy=K[1, 2],
+                              hypotheses=256, inlier_thresh=1.0, refine_iters=10, seed=7)
+    ctx.set_stream(torch.cuda.current_stream())
+    try:
+        ctx.match_sequence_f32(d, nf, idx, None, 0.8)
+        ctx.pose_from_matches(prm, nf[:-1], idx, kp[:-1], kp[1:], T, nm, ni, st)
+        torch.cuda.synchronize()
+    finally:
+        ctx.set_stream(None)
+    idx = idx.cpu().numpy()
+    for b in range(F - 1):
+        i2, _ = orc.allpairs_f32(D[b], D[b + 1], 0.8)
+        assert (idx[b] == i2).all(), b
+    assert (st.cpu().numpy() == 0).all(), st
+    assert (nm.cpu().numpy() >= 0.5 * n).all(), nm
+    Rg = T[:, :, :3].double().cpu().numpy()
+    assert np.abs(Rg - R[None]).max() < 1e-3
