@@ -138,11 +138,20 @@ float mv_scale_as_built(float scale); /* low 32 bits of (double)scale, SURVEY F7
  * only where the rounding window does not already decide the row; match_idx is
  * identical either way. */
 /* How the all-pairs fp32 match screens its candidates before the exact fp32 re-score (the
- * outputs are bit-identical either way): MV_SCREEN_I8 (default) quantises both frames per row
- * to int8 and screens on the int8 matrix cores with a rigorous quantisation window;
- * MV_SCREEN_F16 screens on fp16 MFMAs (2^14-scaled operands).  The environment variable
- * MV_AP_SCREEN=f16 selects the fp16 screen for contexts created afterwards. */
-typedef enum { MV_SCREEN_I8 = 0, MV_SCREEN_F16 = 1 } mv_allpairs_screen;
+ * outputs are bit-identical either way):
+ *   MV_SCREEN_I8 (default)  ONE kernel reads both fp32 frames once, quantises them per row to
+ *                           int8 inside the workgroup and screens on the int8 matrix cores with
+ *                           a rigorous quantisation window (no staged image: prepare/run only
+ *                           record the batch, and run_prepare stages nothing);
+ *   MV_SCREEN_F16           screens on fp16 MFMAs against a staged fp16 image of frame 1
+ *                           (2^14-scaled operands);
+ *   MV_SCREEN_I8_STAGED     the int8 screen against a staged int8 image of frame 1 (the
+ *                           image sequence mode reuses; run_prepare stages the next batch's
+ *                           image inside the match launch).
+ * Sequence mode always uses staged int8 images (under MV_SCREEN_I8 or MV_SCREEN_I8_STAGED).
+ * The environment variable MV_AP_SCREEN=f16 / i8s selects the fp16 / staged-int8 screen for
+ * contexts created afterwards. */
+typedef enum { MV_SCREEN_I8 = 0, MV_SCREEN_F16 = 1, MV_SCREEN_I8_STAGED = 2 } mv_allpairs_screen;
 int mv_context_set_allpairs_screen(mv_context *ctx, int screen);
 int mv_context_allpairs_screen(mv_context *ctx);
 int mv_match_allpairs_f32_dev(mv_context *ctx, int batch, int cap, const int *n0, const int *n1,

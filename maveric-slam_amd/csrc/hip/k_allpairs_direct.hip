@@ -1,0 +1,345 @@
+// k_allpairs_direct.hip -- all-pairs fp32 descriptor match (python/pairwise_pnp.py:635-659,
+// exact score in the gemmini_functions_cpu.h:45-49 order) in ONE pass over the fp32 inputs:
+// the default screen (MV_SCREEN_I8).  SURVEY §8(d)'s algorithmic bytes per pair -- both frames
+// read once (2 x n x 1 KiB), the match written once -- are the only HBM traffic: frame 1 is
+// quantised to int8 INSIDE the workgroup, never staged through memory.
+//
+//   k_q8d_match  one 512-thread workgroup (8 waves x 64 rows, one per CU, 2 waves per SIMD)
+//                owns 512 query rows of one pair; a pair's row blocks sit on one XCD, so
+//                frame 1 comes from HBM once and from that XCD's L2 for the other block.
+//     A phase    each wave reads its 64 frame-0 rows as fp32 once and quantises them into 64
+//                VGPRs of int8 MFMA operands (per-row scale s_a; q8_common.hpp).
+//     B stream   frame 1 streams as fp32 half-tiles (32 rows = 32 KiB) through a 3-slot LDS
+//                staging ring by LDS-DMA (global_load_lds_dwordx4, one 1-KiB row per wave
+//                instruction, issued one tile ahead).  Inside the sweep of tile t every thread
+//                quantises 16 values of tile t + 1 from staging (16 lanes per frame-1 row: the
+//                row's max |b| and |b|^2 by DPP reductions, q_jk = RNE(b_jk RN(127 RN(1/m))),
+//                s_j = RN(m RN(1/127))) into the int8 tile ring (2 slots of 16 KiB + 64 scales),
+//                beside the MFMAs of tile t.
+//     sweep      v_mfma_i32_32x32x32_i8 over 64-column tiles, the exact integer dot D_ij turned
+//                into the screen RN(D_ij s_j) by one FMA, tagged with its column tile and folded
+//                into a lane-local top-2 per row (as k_q8_match).
+//     epilogue   q8_common.hpp: the window decisions, exact re-scores where it does not decide.
+// The window's B terms come from the sweep itself: every workgroup quantises the whole frame 1
+// of its pair, so Bn = max_j |b_j| (from the fp32 |b_j|^2) and Eb = 8 max_j s_j + 2^-21 Bn
+// (|eps_j| <= 8 s_j + 2^-21 |b_j|, q8_common.hpp) and the pair's range flag (a non-finite value
+// or a row scale outside [2^-40, 2^40]: every row takes the exact path) are known to it after
+// the sweep, before any decision.
+// LDS (135.8 KiB): staging 3 x 32 KiB | int8 ring 2 x 16.25 KiB | (|a|^2, s_a) per row |
+// per-wave statistics; the A images (8 x 8 KiB) use staging slot 2 + the ring before the
+// sweep, the epilogue (102 KiB) the staging + ring after it.
+// Bound: HBM -- 2 KiB read + 4 B written per query row (2,105,344 B per 1024^2
+// pair); int8 MFMA 2 n0 n1 256 ops per pair beside it.
+#include "q8_common.hpp"
+
+namespace {
+
+using namespace q8;
+
+constexpr int D_NW = 8, D_NT = 64 * D_NW, D_BM = 32 * RG * D_NW;  // 512 rows per workgroup
+constexpr int D_HROWS = 32, D_HALF = D_HROWS * KD * 4;             // one staging slot: 32 fp32 rows
+constexpr int D_OFF_RING = 3 * D_HALF;                              // 2 int8 tile slots
+constexpr int D_OFF_ROW = D_OFF_RING + 2 * SLOT;                    // [BM] float2 (|a|^2, s_a)
+constexpr int D_OFF_MISC = D_OFF_ROW + D_BM * 8;                    // [NW][4] per-wave statistics
+constexpr int D_LDS = D_OFF_MISC + D_NW * 16;
+constexpr int D_OFF_AIMG = 2 * D_HALF;  // A images: staging slot 2 + the ring (before the sweep)
+static_assert(D_OFF_AIMG + D_NW * 32 * KD <= D_OFF_ROW, "A images fit staging slot 2 + the ring");
+static_assert(epi_bytes<D_NW>() <= D_OFF_ROW, "the epilogue fits staging + ring");
+static_assert(D_LDS <= 160 * 1024, "one workgroup per CU");
+constexpr int D_PF = 2;  // k32 steps of B fragments read ahead of the MFMAs
+
+// DPP row-of-16 reductions (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror): every
+// lane of the 16 ends with the same value
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float max16(float v) {
+    v = fmaxf(v, dppf<0xB1>(v));
+    v = fmaxf(v, dppf<0x4E>(v));
+    v = fmaxf(v, dppf<0x141>(v));
+    return fmaxf(v, dppf<0x140>(v));
+}
+__device__ __forceinline__ float sum16(float v) {
+    v += dppf<0xB1>(v);
+    v += dppf<0x4E>(v);
+    v += dppf<0x141>(v);
+    return v + dppf<0x140>(v);
+}
+
+// Half h of frame 1 (rows 32 h .. +31, clamped to n1 - 1) -> staging slot at LDS byte `slot`:
+// wave w copies rows 4 w .. +3, one 1-KiB row per instruction.  Within a row, LDS position p
+// (16-B unit) holds source chunk 4 (p & 15) + (p >> 4), so that the reader below -- lane sub
+// taking positions sub + 16 i, i.e. the 16 consecutive floats 16 sub .. +15 -- is conflict-free.
+__device__ __forceinline__ void dma_half(const float *B, int h, int n1, int wu, unsigned chunk16, unsigned slot) {
+    const unsigned dst = slot + (unsigned)(wu * 4 * KD * 4);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int j = min(32 * h + 4 * wu + i, n1 - 1);
+        const unsigned voff = (unsigned)j * (KD * 4) + chunk16;
+        if (i == 0) glds16<0>(B, voff, dst);
+        if (i == 1) glds16<KD * 4>(B, voff, dst);
+        if (i == 2) glds16<2 * KD * 4>(B, voff, dst);
+        if (i == 3) glds16<3 * KD * 4>(B, voff, dst);
+    }
+}
+
+// Quantise staging slot `stg` (frame-1 rows j0 .. j0 + 31) into rows 32 hh .. +31 of the int8
+// tile slot `rq`: thread t takes floats 16 sub .. +15 of row t >> 4.  Rows j >= n1 (padding,
+// or a half past the end) are written but excluded from the statistics (their columns are
+// masked by the dequantisation operands).
+__device__ __forceinline__ void quant_half(const char *stg, char *rq, int hh, int j0, int n1, int t, float &smax,
+                                           float &b2max, bool &bad) {
+    const int r = t >> 4, sub = t & 15;
+    const char *src = stg + r * (KD * 4) + sub * 16;
+    const f32x4v x0 = *reinterpret_cast<const f32x4v *>(src);
+    const f32x4v x1 = *reinterpret_cast<const f32x4v *>(src + 256);
+    const f32x4v x2 = *reinterpret_cast<const f32x4v *>(src + 512);
+    const f32x4v x3 = *reinterpret_cast<const f32x4v *>(src + 768);
+    float m = absmax3(0.f, x0[0], x0[1]);
+    m = absmax3(m, x0[2], x0[3]);
+    m = absmax3(m, x1[0], x1[1]);
+    m = absmax3(m, x1[2], x1[3]);
+    m = absmax3(m, x2[0], x2[1]);
+    m = absmax3(m, x2[2], x2[3]);
+    m = absmax3(m, x3[0], x3[1]);
+    m = absmax3(m, x3[2], x3[3]);
+    float qa = __builtin_fmaf(x0[0], x0[0], __builtin_fmaf(x0[1], x0[1], __builtin_fmaf(x0[2], x0[2], x0[3] * x0[3])));
+    float qb = __builtin_fmaf(x1[0], x1[0], __builtin_fmaf(x1[1], x1[1], __builtin_fmaf(x1[2], x1[2], x1[3] * x1[3])));
+    qa = __builtin_fmaf(x2[0], x2[0], __builtin_fmaf(x2[1], x2[1], __builtin_fmaf(x2[2], x2[2], __builtin_fmaf(x2[3], x2[3], qa))));
+    qb = __builtin_fmaf(x3[0], x3[0], __builtin_fmaf(x3[1], x3[1], __builtin_fmaf(x3[2], x3[2], __builtin_fmaf(x3[3], x3[3], qb))));
+    m = max16(m);
+    const float q2 = sum16(qa + qb);
+    const float q = m > 0.f ? 127.f * __builtin_amdgcn_rcpf(m) : 0.f;
+    const float s = m * (1.f / 127.f);
+    i32x4 code;
+    code[0] = pack4(x0[0], x0[1], x0[2], x0[3], q);
+    code[1] = pack4(x1[0], x1[1], x1[2], x1[3], q);
+    code[2] = pack4(x2[0], x2[1], x2[2], x2[3], q);
+    code[3] = pack4(x3[0], x3[1], x3[2], x3[3], q);
+    const int row = 32 * hh + r;
+    *reinterpret_cast<i32x4 *>(rq + row * KD + ((sub ^ (row & 15)) << 4)) = code;
+    if (sub == 0) reinterpret_cast<float *>(rq + TILE)[row] = s;
+    // finite (|b|^2 propagates NaN / inf) and a representable scale (zero rows: s = 0, codes
+    // 0, every screen value of the column 0 -- exact, no flag needed)
+    const bool live = j0 + r < n1;
+    const bool ok = q2 <= FLT_MAX && (m == 0.f || (m >= SCALE_LO && m <= SCALE_HI));
+    smax = live ? fmaxf(smax, s) : smax;
+    b2max = live ? fmaxf(b2max, q2) : b2max;
+    bad = bad || (live && !ok);
+}
+
+__global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, const int *__restrict__ n0v,
+                                                       const int *__restrict__ n1v, const float *__restrict__ desc0,
+                                                       const float *__restrict__ desc1, double thresh, int dmode,
+                                                       int *__restrict__ match_idx, float *__restrict__ match_score) {
+    __shared__ __attribute__((aligned(16))) char lds[D_LDS];
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int pair = L / tiles_r, tr = L % tiles_r;
+    const int n0 = min(max(n0v[pair], 0), cap), n1 = min(max(n1v[pair], 0), cap);
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int row0 = tr * D_BM;
+    int *oidx = match_idx + (size_t)pair * cap + row0;
+    float *oscore = match_score ? match_score + (size_t)pair * cap + row0 : nullptr;  // null: indices only
+    if (row0 + t < cap && (row0 + t >= n0 || n1 <= 0)) {  // rows in [n0, cap): no match
+        oidx[t] = -1;
+        if (oscore) oscore[t] = 0.f;
+    }
+    if (row0 >= n0 || n1 <= 0) return;
+    const float *A = desc0 + (size_t)pair * cap * KD;
+    const float *B = desc1 + (size_t)pair * cap * KD;
+    const int ntc = (n1 + BN - 1) / BN, nh = 2 * ntc;  // column tiles, staging halves (>= 2)
+
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    const unsigned chunk16 = (unsigned)(4 * (lane & 15) + (lane >> 4)) * 16;
+    const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char *)lds;
+    char *ring = lds + D_OFF_RING;
+    float2 *rowv = reinterpret_cast<float2 *>(lds + D_OFF_ROW);
+    float *misc = reinterpret_cast<float *>(lds + D_OFF_MISC);
+
+    // ---- prologue: halves 0, 1 in flight beside the A phase; then tile 0 quantised ----
+    dma_half(B, 0, n1, wu, chunk16, lds_base);
+    dma_half(B, 1, n1, wu, chunk16, lds_base + D_HALF);
+    const int fr = lane & 31, fh = lane >> 5;
+    i32x4 aI[RG][KD / 32];
+    a_phase<false>(lds + D_OFF_AIMG + w * 32 * KD, rowv, w * 64, row0, n0, lane, A, nullptr, nullptr, nullptr,
+                   false, aI);
+    __syncthreads();  // the A images (staging slot 2 + the ring) are consumed
+    if (nh > 2) {
+        dma_half(B, 2, n1, wu, chunk16, lds_base + 2 * D_HALF);
+        wait_vm<4>();
+    } else {
+        wait_vm<0>();
+    }
+    __syncthreads();  // halves 0, 1 landed
+    float smax = 0.f, b2max = 0.f;
+    bool bad = false;
+    quant_half(lds, ring, 0, 0, n1, t, smax, b2max, bad);
+    quant_half(lds + D_HALF, ring, 1, 32, n1, t, smax, b2max, bad);
+    __syncthreads();  // tile 0 in ring slot 0; staging slots 0, 1 free
+    if (nh > 3) dma_half(B, 3, n1, wu, chunk16, lds_base);
+
+    // B fragment: column block c (0, 1), lane row 32 c + fr, k32 step s: chunk (2 s + fh)
+    const int rdb = fr * KD;
+    const int xsw = fh ^ (fr & 15);  // chunk (2 s + fh) ^ (fr & 15) = 2 s ^ xsw
+
+    // Accumulators start at the bits of 4.0 (q8_common.hpp: mfma_i8_from4): t = 4 + D 2^-21 as
+    // a float, f = fma(t, 2^21 s_j, -2^23 s_j) = RN(D s_j).  Columns past n1 (last tile only)
+    // get s = 0 and the offset -3e38.  The low tb bits of f are then replaced by the column tag
+    // 2 tc + half.
+    i32x16 acc[RG][2];
+    float m1[RG][16], m2[RG][16];
+#pragma unroll
+    for (int g = 0; g < RG; g++)
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            m1[g][q] = -__builtin_inff();
+            m2[g][q] = -__builtin_inff();
+        }
+#pragma unroll
+    for (int q = 0; q < 16; q++) {  // "tile -1" of group 1, folded beside tile 0: never a maximum
+        acc[1][0][q] = 0;
+        acc[1][1][q] = 0;
+    }
+    const int tb = 2 * ntc <= 256 ? 8 : 32 - __builtin_clz(2 * ntc - 1);
+    const unsigned tkeep = ~((1u << tb) - 1u);
+    unsigned vkeep = tkeep;
+    asm volatile("" : "+v"(vkeep));  // a VGPR operand: v_and_or_b32 may read one SGPR only
+    float pr0 = 0.f, pr1 = 0.f, pc0 = -3.0e38f, pc1 = -3.0e38f;  // dequantisation of the tile before
+
+#define D_FOLD2(FG, S, G0)                                                                   \
+    do {                                                                                     \
+        _Pragma("unroll") for (int q = 2 * (S); q < 2 * (S) + 2; q++) {                      \
+            const float a_ = __builtin_fmaf(__int_as_float(acc[FG][0][q]), pr0, pc0);        \
+            const float b_ = __builtin_fmaf(__int_as_float(acc[FG][1][q]), pr1, pc1);        \
+            fold3(tag(a_, vkeep, (G0)), tag(b_, vkeep, (G0) + 1u), m1[FG][q], m2[FG][q]);    \
+        }                                                                                    \
+    } while (0)
+    // group G's MFMAs on the tile at `rs` (fragments read D_PF k32 steps ahead), folding group
+    // FG meanwhile, and this thread's share of the next tile's quantisation (QUANT)
+#define D_SEG(G, FG, G0, QUANT)                                                              \
+    do {                                                                                     \
+        const char *base = rs + rdb;                                                         \
+        int xs_ = xsw;                                                                       \
+        asm volatile("" : "+v"(xs_)); /* per-use offsets: not 8 loop-invariant VGPRs */      \
+        i32x4 b0_[KD / 32], b1_[KD / 32];                                                    \
+        QUANT;                                                                               \
+        _Pragma("unroll") for (int s_ = 0; s_ < KD / 32 + D_PF; s_++) {                      \
+            if (s_ < KD / 32) {                                                              \
+                const int ch_ = ((2 * s_) ^ xs_) * 16;                                       \
+                b0_[s_] = *reinterpret_cast<const i32x4 *>(base + ch_);                      \
+                b1_[s_] = *reinterpret_cast<const i32x4 *>(base + 32 * KD + ch_);            \
+            }                                                                                \
+            if (s_ >= D_PF) {                                                                \
+                const int m_ = s_ - D_PF;                                                    \
+                if (m_ == 0) {                                                               \
+                    acc[G][0] = mfma_i8_from4(aI[G][0], b0_[0]);                             \
+                    acc[G][1] = mfma_i8_from4(aI[G][0], b1_[0]);                             \
+                } else {                                                                     \
+                    acc[G][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b0_[m_], acc[G][0], 0, 0, 0); \
+                    acc[G][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b1_[m_], acc[G][1], 0, 0, 0); \
+                }                                                                            \
+                D_FOLD2(FG, m_, G0);                                                         \
+            }                                                                                \
+        }                                                                                    \
+    } while (0)
+
+    // Tile t sweeps from ring slot t & 1 while tile t + 1 is quantised into the other slot from
+    // staging halves 2t + 2 (slot (2t + 2) % 3, during group 0) and 2t + 3 (during group 1);
+    // half 2t + 4 is issued at the top (into the slot half 2t + 1 left), 2t + 5 at the middle
+    // (into the slot half 2t + 2 left).  Every half thus has one whole tile of latency cover.
+    // In the last iteration the quantisation runs on stale staging bytes into the unused slot
+    // (no DMA is in flight then): branch-free segments, nothing read afterwards.
+    int sA = 2, sB = 0;  // staging slots of halves 2t + 2, 2t + 3
+    for (int tc = 0; tc < ntc; tc++) {
+        if (2 * tc + 3 < nh) {  // half 2t + 2 landed (2t + 3 may be in flight)
+            wait_vm<4>();
+        } else {
+            wait_vm<0>();
+        }
+        __syncthreads();  // tile t complete in its slot; staging slot of half 2t + 1 free
+        const int sN = 3 - sA - sB;  // the third staging slot
+        if (2 * tc + 4 < nh) dma_half(B, 2 * tc + 4, n1, wu, chunk16, lds_base + (unsigned)(sN * D_HALF));
+        const char *rs = ring + (tc & 1) * SLOT;
+        char *rq = ring + ((tc + 1) & 1) * SLOT;
+        const char *stA = lds + sA * D_HALF, *stB = lds + sB * D_HALF;
+        const unsigned gp_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)max(tc - 1, 0));
+        D_SEG(0, 1, gp_, quant_half(stA, rq, 0, 32 * (2 * tc + 2), n1, t, smax, b2max, bad));
+        {  // the dequantisation operands of tile tc: fma(t, 2^21 s, -2^23 s)
+            const float *rl_ = reinterpret_cast<const float *>(rs + TILE);
+            const int col_ = tc * BN + fr;
+            const float s0_ = rl_[fr], s1_ = rl_[fr + 32];
+            pr0 = col_ < n1 ? 2097152.0f * s0_ : 0.f;
+            pr1 = col_ + 32 < n1 ? 2097152.0f * s1_ : 0.f;
+            pc0 = col_ < n1 ? -8388608.0f * s0_ : -3.0e38f;
+            pc1 = col_ + 32 < n1 ? -8388608.0f * s1_ : -3.0e38f;
+        }
+        if (2 * tc + 4 < nh) {  // half 2t + 3 landed (2t + 4 may be in flight)
+            wait_vm<4>();
+        } else {
+            wait_vm<0>();
+        }
+        __syncthreads();  // staging slot of half 2t + 2 consumed
+        if (2 * tc + 5 < nh) dma_half(B, 2 * tc + 5, n1, wu, chunk16, lds_base + (unsigned)(sA * D_HALF));
+        const unsigned gc_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)tc);
+        D_SEG(1, 0, gc_, quant_half(stB, rq, 1, 32 * (2 * tc + 3), n1, t, smax, b2max, bad));
+        // halves 2t + 4, 2t + 5 sit in slots sN, sA
+        const int nA = sN, nB = sA;
+        sA = nA;
+        sB = nB;
+    }
+    {  // group 1 of the last tile
+        const unsigned gl_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)(ntc - 1));
+#pragma unroll
+        for (int s = 0; s < 8; s++) D_FOLD2(1, s, gl_);
+    }
+#undef D_FOLD2
+#undef D_SEG
+
+    // ---- the pair's frame-1 statistics (every workgroup of the pair computes the same) ----
+    smax = fmaxf(smax, swz_xor<16>(smax));
+    b2max = fmaxf(b2max, swz_xor<16>(b2max));
+    smax = fmaxf(smax, __shfl_xor(smax, 32, 64));
+    b2max = fmaxf(b2max, __shfl_xor(b2max, 32, 64));
+    const bool wbad = __ballot(bad) != 0;
+    if (lane == 0) {
+        misc[4 * w] = smax;
+        misc[4 * w + 1] = b2max;
+        misc[4 * w + 2] = wbad ? 1.f : 0.f;
+    }
+    __syncthreads();  // also: every wave is past its sweep (staging + ring free for the epilogue)
+    float S = 0.f, B2 = 0.f;
+    bool flagged = false;
+#pragma unroll
+    for (int k = 0; k < D_NW; k++) {
+        S = fmaxf(S, misc[4 * k]);
+        B2 = fmaxf(B2, misc[4 * k + 1]);
+        flagged = flagged || misc[4 * k + 2] != 0.f;
+    }
+    const double Bn = sqrt((double)B2) * 1.0001;
+    const double Eb = (8.001 * (double)S + 4.76837158203125e-07 * Bn) * 1.0001 + 1e-30;
+    epilogue<D_NW>(lds, rowv, m1, m2, Bn, Eb, flagged, tb, tkeep, w, lane, row0, n0, n1, A, B, oidx, oscore, thresh,
+                   dmode);
+}
+
+}  // namespace
+
+namespace mv {
+
+int launch_allpairs_q8d_match(hipStream_t s, int batch, int cap, const int *n0, const int *n1, const float *desc0,
+                              const float *desc1, double thresh, int *match_idx, float *match_score, int dmode) {
+    MV_REQUIRE(batch > 0 && cap > 0 && n0 && n1 && desc0 && desc1 && match_idx);
+    MV_REQUIRE(((uintptr_t)desc0 & 15) == 0 && ((uintptr_t)desc1 & 15) == 0);
+    MV_REQUIRE((long)cap * KD * 4 < (1l << 32));  // 32-bit DMA source offsets within a pair
+    const int tiles_r = (cap + D_BM - 1) / D_BM;
+    const long blocks = (long)batch * tiles_r;
+    MV_REQUIRE(blocks < (1l << 31));
+    MV_PROF_BEGIN(s, "k_q8d_match");
+    hipLaunchKernelGGL(k_q8d_match, dim3((unsigned)blocks), dim3(D_NT), 0, s, tiles_r, cap, n0, n1, desc0, desc1,
+                       dmode ? -1e300 : thresh, dmode, match_idx, match_score);
+    MV_PROF_END(s);
+    MV_LAUNCH_CHECK();
+    return MV_OK;
+}
+
+}  // namespace mv

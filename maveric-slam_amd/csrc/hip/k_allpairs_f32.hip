@@ -790,6 +790,12 @@ size_t allpairs_f32_scratch_bytes(int batch, int cap) {
     const size_t f16 = rows * ROW_BYTES + align_up(rows * 4, 256) + align_up((size_t)batch * 4, 256);
     return std::max(f16, allpairs_q8_scratch_bytes(batch, cap));
 }
+// one staged image under `screen`: fp16 (516 B per row) or int8 (268 B per row)
+size_t ap_image_bytes(int screen, int batch, int cap) {
+    if (screen != MV_SCREEN_F16) return allpairs_q8_scratch_bytes(batch, cap);
+    const size_t rows = (size_t)batch * cap;
+    return rows * ROW_BYTES + align_up(rows * 4, 256) + align_up((size_t)batch * 4, 256);
+}
 
 namespace {
 struct ApScratch {
@@ -849,7 +855,7 @@ namespace {
 void *ap_scratch(mv_context *ctx, size_t bytes) {
     if (bytes <= ctx->ap_scratch_bytes) return ctx->ap_scratch;
     if (ctx->ap_scratch) {
-        (void)hipDeviceSynchronize();  // growing: nothing may still use the old buffer
+        (void)mv::quiesce(ctx);  // growing: nothing of this context may still use the old buffer
         (void)hipFree(ctx->ap_scratch);
         ctx->ap_scratch = nullptr;
         ctx->ap_scratch_bytes = 0;
@@ -867,13 +873,19 @@ void *ap_scratch(mv_context *ctx, size_t bytes) {
 }  // namespace
 
 namespace {
+// staging of frame 1 for the screens that match against an image (fp16, staged int8; the
+// default int8 screen stages only for sequence mode, which reuses the images)
 int ap_prepare(int screen, hipStream_t s, void *scr, int batch, int cap, const int *n1, const float *desc1) {
     return screen == MV_SCREEN_F16 ? mv::launch_allpairs_f32_prepare(s, scr, batch, cap, n1, desc1)
                                    : mv::launch_allpairs_q8_prepare(s, scr, batch, cap, n1, desc1);
 }
+// the match; MV_SCREEN_I8 reads both fp32 frames directly (no image, scr unused)
 int ap_match(int screen, hipStream_t s, void *scr, int batch, int cap, const int *n0, const int *n1,
              const float *desc0, const float *desc1, double thresh, int *match_idx, float *match_score,
              int dmode = 0) {
+    if (screen == MV_SCREEN_I8)
+        return mv::launch_allpairs_q8d_match(s, batch, cap, n0, n1, desc0, desc1, thresh, match_idx, match_score,
+                                             dmode);
     return screen == MV_SCREEN_F16
                ? mv::launch_allpairs_f32_match(s, scr, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
                                                match_score, dmode)
@@ -887,9 +899,13 @@ extern "C" int mv_match_allpairs_f32_dev(mv_context *ctx, int batch, int cap, co
                                          float *match_score) {
     MV_REQUIRE(ctx != nullptr && batch > 0 && cap > 0);
     MV_HIP_TRY(hipSetDevice(ctx->device));
-    void *scr = ap_scratch(ctx, mv::allpairs_f32_scratch_bytes(batch, cap));
+    if (ctx->ap_screen == MV_SCREEN_I8)  // one pass, no image
+        return ap_match(ctx->ap_screen, ctx->stream, nullptr, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
+                        match_score);
+    void *scr = ap_scratch(ctx, mv::ap_image_bytes(ctx->ap_screen, batch, cap));
     if (!scr) return MV_ERR_OUT_OF_MEMORY;
     ctx->prep_desc1 = nullptr;  // the prepared image is overwritten
+    if (ctx->aux_stream) MV_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_prep, 0));  // a staging in flight
     const int st = ap_prepare(ctx->ap_screen, ctx->stream, scr, batch, cap, n1, desc1);
     if (st != MV_OK) return st;
     return ap_match(ctx->ap_screen, ctx->stream, scr, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
@@ -900,7 +916,7 @@ extern "C" int mv_match_allpairs_f32_prepare_dev(mv_context *ctx, int batch, int
                                                  const float *desc1) {
     MV_REQUIRE(ctx != nullptr && batch > 0 && cap > 0 && n1 && desc1);
     MV_HIP_TRY(hipSetDevice(ctx->device));
-    void *scr = ap_scratch(ctx, mv::allpairs_f32_scratch_bytes(batch, cap));
+    void *scr = ap_scratch(ctx, mv::ap_image_bytes(ctx->ap_screen, batch, cap));
     if (!scr) return MV_ERR_OUT_OF_MEMORY;
     if (!ctx->aux_stream) {
 #if AP_AUX_PRIO
@@ -922,6 +938,7 @@ extern "C" int mv_match_allpairs_f32_prepare_dev(mv_context *ctx, int batch, int
     if (st != MV_OK) return st;
     MV_HIP_TRY(hipEventRecord(ctx->ev_prep, ctx->aux_stream));
     ctx->prep_screen = ctx->ap_screen;
+    ctx->prep_staged = true;
     ctx->prep_batch = batch;
     ctx->prep_cap = cap;
     ctx->prep_n1 = n1;
@@ -949,7 +966,7 @@ namespace {
 int ap_scratch2(mv_context *ctx, size_t need) {
     if (ctx->ap_scratch2_bytes >= need) return MV_OK;
     if (ctx->ap_scratch2) {
-        (void)hipDeviceSynchronize();  // growing: nothing may still use the old buffer
+        (void)mv::quiesce(ctx);  // growing: nothing of this context may still use the old buffer
         (void)hipFree(ctx->ap_scratch2);
         ctx->ap_scratch2 = nullptr;
         ctx->ap_scratch2_bytes = 0;
@@ -973,6 +990,7 @@ void ap_swap_prepared(mv_context *ctx, int batch, int cap, const int *n1, const 
     ctx->prep_cap = cap;
     ctx->prep_n1 = n1;
     ctx->prep_desc1 = desc1;
+    ctx->prep_staged = true;
 }
 }  // namespace
 
@@ -988,11 +1006,22 @@ extern "C" int mv_match_allpairs_f32_run_prepare_dev(mv_context *ctx, int batch,
         return MV_ERR_INVALID_ARG;
     }
     MV_HIP_TRY(hipSetDevice(ctx->device));
-    const int sc = ap_scratch2(ctx, mv::allpairs_f32_scratch_bytes(next_batch, next_cap));
+    if (ctx->ap_screen == MV_SCREEN_I8) {  // one pass: nothing to stage for the next batch
+        const int st = ap_match(ctx->ap_screen, ctx->stream, nullptr, batch, cap, n0, n1, desc0, desc1, thresh,
+                                match_idx, match_score);
+        if (st != MV_OK) return st;
+        ctx->prep_batch = next_batch;
+        ctx->prep_cap = next_cap;
+        ctx->prep_n1 = next_n1;
+        ctx->prep_desc1 = next_desc1;
+        ctx->prep_staged = false;  // recorded, not staged (sequence mode needs a prepare)
+        return mv::set_status(MV_OK);
+    }
+    const int sc = ap_scratch2(ctx, mv::ap_image_bytes(ctx->ap_screen, next_batch, next_cap));
     if (sc != MV_OK) return sc;
     if (ctx->aux_stream) MV_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_prep, 0));
     int st;
-    if (ctx->ap_screen == MV_SCREEN_I8) {
+    if (ctx->ap_screen == MV_SCREEN_I8_STAGED) {
         st = mv::launch_allpairs_q8_match_prepare(ctx->stream, ctx->ap_scratch, batch, cap, n0, n1, desc0, desc1,
                                                   thresh, match_idx, match_score, 0, ctx->ap_scratch2, next_batch,
                                                   next_cap, next_n1, next_desc1);
@@ -1035,9 +1064,14 @@ extern "C" int mv_match_two_way_f32_dev(mv_context *ctx, int batch, int cap, con
         return MV_ERR_INVALID_ARG;
     }
     MV_HIP_TRY(hipSetDevice(ctx->device));
-    void *scr = ap_scratch(ctx, mv::allpairs_f32_scratch_bytes(batch, cap));
-    if (!scr) return MV_ERR_OUT_OF_MEMORY;
-    ctx->prep_desc1 = nullptr;  // the prepared image is overwritten
+    const int sc = ctx->ap_screen;
+    void *scr = nullptr;
+    if (sc != MV_SCREEN_I8) {  // the image screens stage each direction
+        scr = ap_scratch(ctx, mv::ap_image_bytes(ctx->ap_screen, batch, cap));
+        if (!scr) return MV_ERR_OUT_OF_MEMORY;
+        ctx->prep_desc1 = nullptr;  // the prepared image is overwritten
+        if (ctx->aux_stream) MV_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_prep, 0));  // a staging in flight
+    }
     const size_t nb = mv::align_up((size_t)batch * cap * 4, 256);
     char *tmp = (char *)mv::scratch(ctx, 2 * nb);
     if (!tmp) return MV_ERR_OUT_OF_MEMORY;
@@ -1045,11 +1079,10 @@ extern "C" int mv_match_two_way_f32_dev(mv_context *ctx, int batch, int cap, con
     float *fdist = match_dist ? match_dist : (float *)(tmp + nb);
     hipStream_t s = ctx->stream;
     // forward: rows of frame 0 against frame 1 (argmin distance + its exact distance)
-    const int sc = ctx->ap_screen;
-    int st = ap_prepare(sc, s, scr, batch, cap, n1, desc1);
+    int st = sc == MV_SCREEN_I8 ? MV_OK : ap_prepare(sc, s, scr, batch, cap, n1, desc1);
     if (st == MV_OK) st = ap_match(sc, s, scr, batch, cap, n0, n1, desc0, desc1, 0.0, match_idx, fdist, 1);
     // reverse: rows of frame 1 against frame 0 (indices only)
-    if (st == MV_OK) st = ap_prepare(sc, s, scr, batch, cap, n0, desc0);
+    if (st == MV_OK && sc != MV_SCREEN_I8) st = ap_prepare(sc, s, scr, batch, cap, n0, desc0);
     if (st == MV_OK) st = ap_match(sc, s, scr, batch, cap, n1, n0, desc1, desc0, 0.0, ridx, nullptr, 1);
     if (st != MV_OK) return st;
     const long total = (long)batch * cap;
@@ -1069,12 +1102,12 @@ extern "C" int mv_debug_ap_trace(void *host, long bytes) {
 extern "C" int mv_match_sequence_f32_dev(mv_context *ctx, int frames, int cap, const int *n, const float *desc,
                                          double thresh, int *match_idx, float *match_score) {
     MV_REQUIRE(ctx != nullptr && frames >= 2 && cap > 0 && n && desc && match_idx);
-    if (ctx->ap_screen != MV_SCREEN_I8) {
-        mv::set_error(MV_ERR_INVALID_ARG, "mv_match_sequence_f32_dev: the int8 screen only");
+    if (ctx->ap_screen == MV_SCREEN_F16) {
+        mv::set_error(MV_ERR_INVALID_ARG, "mv_match_sequence_f32_dev: the int8 screens only");
         return MV_ERR_INVALID_ARG;
     }
     MV_HIP_TRY(hipSetDevice(ctx->device));
-    void *scr = ap_scratch(ctx, mv::allpairs_f32_scratch_bytes(frames, cap));
+    void *scr = ap_scratch(ctx, mv::ap_image_bytes(ctx->ap_screen, frames, cap));
     if (!scr) return MV_ERR_OUT_OF_MEMORY;
     ctx->prep_desc1 = nullptr;  // the prepared image is overwritten
     if (ctx->aux_stream) MV_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_prep, 0));  // a staging in flight
@@ -1088,14 +1121,14 @@ extern "C" int mv_match_sequence_f32_run_prepare_dev(mv_context *ctx, int frames
                                                      float *match_score, int next_frames, int next_cap,
                                                      const int *next_n, const float *next_desc) {
     MV_REQUIRE(ctx != nullptr && frames >= 2 && next_frames >= 2 && next_cap > 0 && next_n && next_desc);
-    if (ctx->ap_screen != MV_SCREEN_I8 || !ctx->prep_desc1 || ctx->prep_batch != frames || ctx->prep_cap != cap ||
-        ctx->prep_n1 != n || ctx->prep_desc1 != desc || ctx->prep_screen != MV_SCREEN_I8) {
+    if (ctx->ap_screen == MV_SCREEN_F16 || !ctx->prep_desc1 || !ctx->prep_staged || ctx->prep_batch != frames ||
+        ctx->prep_cap != cap || ctx->prep_n1 != n || ctx->prep_desc1 != desc || ctx->prep_screen == MV_SCREEN_F16) {
         mv::set_error(MV_ERR_INVALID_ARG,
                       "mv_match_sequence_f32_run_prepare_dev: no matching prepare for these frames (int8 screen)");
         return MV_ERR_INVALID_ARG;
     }
     MV_HIP_TRY(hipSetDevice(ctx->device));
-    const int sc = ap_scratch2(ctx, mv::allpairs_f32_scratch_bytes(next_frames, next_cap));
+    const int sc = ap_scratch2(ctx, mv::ap_image_bytes(ctx->ap_screen, next_frames, next_cap));
     if (sc != MV_OK) return sc;
     if (ctx->aux_stream) MV_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_prep, 0));
     const int st = mv::launch_allpairs_q8_sequence(ctx->stream, ctx->ap_scratch, frames, cap, n, desc, thresh,

@@ -5,6 +5,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
+
 #include "mv_internal.hpp"
 
 namespace {
@@ -16,7 +18,7 @@ thread_local char g_last_msg[512] = "";
 // (the main thread's lives until process exit).
 pthread_once_t g_key_once = PTHREAD_ONCE_INIT;
 pthread_key_t g_ctx_key;
-bool g_no_device_reported = false;
+std::atomic<bool> g_no_device_reported{false};
 
 void destroy_thread_context(void *p) { (void)mv_context_destroy(static_cast<mv_context *>(p)); }
 void make_key() { (void)pthread_key_create(&g_ctx_key, destroy_thread_context); }
@@ -37,10 +39,19 @@ int set_status(int status) {
     return status;
 }
 
+int quiesce(mv_context *ctx) {
+    MV_HIP_TRY(hipStreamSynchronize(ctx->own_stream));
+    if (ctx->stream != ctx->own_stream) MV_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    for (int i = 0; i < ctx->n_used_streams && i < 4; i++)
+        if (ctx->used_streams[i] != ctx->stream) MV_HIP_TRY(hipStreamSynchronize(ctx->used_streams[i]));
+    if (ctx->aux_stream) MV_HIP_TRY(hipStreamSynchronize(ctx->aux_stream));
+    return MV_OK;
+}
+
 void *scratch(mv_context *ctx, size_t bytes) {
     if (bytes <= ctx->scratch_bytes) return ctx->scratch;
     if (ctx->scratch) {
-        (void)hipDeviceSynchronize();  // the old buffer may be in use on any stream the context used
+        (void)quiesce(ctx);  // the old buffer may be in use on any stream the context used
         (void)hipFree(ctx->scratch);
         ctx->scratch = nullptr;
         ctx->scratch_bytes = 0;
@@ -58,7 +69,7 @@ void *scratch(mv_context *ctx, size_t bytes) {
 void *stage(mv_context *ctx, size_t bytes) {
     if (bytes <= ctx->stage_bytes) return ctx->stage_dev;
     if (ctx->stage_dev) {
-        (void)hipDeviceSynchronize();
+        (void)quiesce(ctx);
         (void)hipFree(ctx->stage_dev);
         ctx->stage_dev = nullptr;
         ctx->stage_bytes = 0;
@@ -127,7 +138,9 @@ int mv_context_create(int device, mv_context **out) {
     }
     c->stream = c->own_stream;
     const char *scr = getenv("MV_AP_SCREEN");
-    c->ap_screen = (scr && strcmp(scr, "f16") == 0) ? MV_SCREEN_F16 : MV_SCREEN_I8;
+    c->ap_screen = (scr && strcmp(scr, "f16") == 0)   ? MV_SCREEN_F16
+                   : (scr && strcmp(scr, "i8s") == 0) ? MV_SCREEN_I8_STAGED
+                                                      : MV_SCREEN_I8;
     *out = c;
     return mv::set_status(MV_OK);
 }
@@ -154,6 +167,11 @@ int mv_context_destroy(mv_context *ctx) {
 int mv_context_set_stream(mv_context *ctx, void *s) {
     MV_REQUIRE(ctx != nullptr);
     ctx->stream = s ? (hipStream_t)s : ctx->own_stream;
+    if (ctx->stream != ctx->own_stream) {  // remembered for quiesce()
+        bool seen = false;
+        for (int i = 0; i < ctx->n_used_streams && i < 4; i++) seen = seen || ctx->used_streams[i] == ctx->stream;
+        if (!seen) ctx->used_streams[ctx->n_used_streams++ % 4] = ctx->stream;
+    }
     return MV_OK;
 }
 
@@ -166,7 +184,7 @@ int mv_context_synchronize(mv_context *ctx) {
 }
 
 int mv_context_set_allpairs_screen(mv_context *ctx, int screen) {
-    MV_REQUIRE(ctx != nullptr && (screen == MV_SCREEN_I8 || screen == MV_SCREEN_F16));
+    MV_REQUIRE(ctx != nullptr && (screen == MV_SCREEN_I8 || screen == MV_SCREEN_F16 || screen == MV_SCREEN_I8_STAGED));
     ctx->ap_screen = screen;
     return MV_OK;
 }
@@ -175,26 +193,31 @@ int mv_context_allpairs_screen(mv_context *ctx) { return ctx ? ctx->ap_screen : 
 
 int mv_context_reserve(mv_context *ctx, int batch, int cap) {
     MV_REQUIRE(ctx != nullptr && batch > 0 && cap > 0);
-    if (ctx->ap_scratch_bytes < mv::allpairs_f32_scratch_bytes(batch, cap)) {
+    // the staged images of the context's CURRENT screen (ap_image_bytes): the default one-pass
+    // int8 screen uses them only in sequence mode; run_prepare's second image as well
+    const size_t img = mv::ap_image_bytes(ctx->ap_screen, batch, cap);
+    if (ctx->ap_scratch_bytes < img) {
         if (ctx->ap_scratch) {
-            MV_HIP_TRY(hipDeviceSynchronize());
+            const int q = mv::quiesce(ctx);
+            if (q != MV_OK) return q;
             MV_HIP_TRY(hipFree(ctx->ap_scratch));
             ctx->ap_scratch = nullptr;
             ctx->ap_scratch_bytes = 0;
         }
         ctx->prep_desc1 = nullptr;  // a prepared frame 1 lived in the freed buffer
-        const size_t ab = mv::align_up(mv::allpairs_f32_scratch_bytes(batch, cap), 1 << 20);
+        const size_t ab = mv::align_up(img, 1 << 20);
         if (hipMalloc(&ctx->ap_scratch, ab) != hipSuccess) return MV_ERR_OUT_OF_MEMORY;
         ctx->ap_scratch_bytes = ab;
     }
-    if (ctx->ap_scratch2_bytes < mv::allpairs_f32_scratch_bytes(batch, cap)) {  // run_prepare's second image
+    if (ctx->ap_scratch2_bytes < img) {  // run_prepare's second image
         if (ctx->ap_scratch2) {
-            MV_HIP_TRY(hipDeviceSynchronize());
+            const int q = mv::quiesce(ctx);
+            if (q != MV_OK) return q;
             MV_HIP_TRY(hipFree(ctx->ap_scratch2));
             ctx->ap_scratch2 = nullptr;
             ctx->ap_scratch2_bytes = 0;
         }
-        const size_t ab = mv::align_up(mv::allpairs_f32_scratch_bytes(batch, cap), 1 << 20);
+        const size_t ab = mv::align_up(img, 1 << 20);
         if (hipMalloc(&ctx->ap_scratch2, ab) != hipSuccess) return MV_ERR_OUT_OF_MEMORY;
         ctx->ap_scratch2_bytes = ab;
     }
@@ -215,11 +238,10 @@ mv_context *mv_default_context(void) {
     }
     const int n = mv_device_count();
     if (n <= 0) {
-        if (!g_no_device_reported)
+        if (!g_no_device_reported.exchange(true))
             fprintf(stderr,
                     "maveric_hip: no HIP device visible -- this library has no CPU fallback "
                     "(hipGetDeviceCount = %d)\n", n);
-        g_no_device_reported = true;
         mv::set_error(MV_ERR_NO_DEVICE, "no HIP device visible");
         return nullptr;
     }

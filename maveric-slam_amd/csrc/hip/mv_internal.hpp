@@ -27,7 +27,10 @@ struct mv_context {
     const int *prep_n1;
     const float *prep_desc1;
     int prep_screen;
+    bool prep_staged;  // the prepared batch's frame 1 sits staged in ap_scratch (false: recorded only)
     int ap_screen;  // mv_allpairs_screen of the fp32 all-pairs match (0 = int8, the default)
+    hipStream_t used_streams[4];  // user streams set on this context (ring): quiesced before a buffer is freed
+    int n_used_streams;
 };
 
 namespace mv {
@@ -40,6 +43,13 @@ void *scratch(mv_context *ctx, size_t bytes);
 void *stage(mv_context *ctx, size_t bytes);
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Wait for every stream this context has issued work on (its own, the current and recent user
+// streams, the staging stream) -- before a context buffer is freed; other contexts and threads
+// are not blocked (no device-wide synchronisation, no effect on their graph captures).
+int quiesce(mv_context *ctx);
+// bytes of one staged frame-1 image (ap_scratch / ap_scratch2) under `screen`
+size_t ap_image_bytes(int screen, int batch, int cap);
 
 // Kernel profiler (mv_profile_* in maveric_hip.h): when enabled, launchers
 // bracket each kernel with hipEventRecord on the launch stream -- no sync.
@@ -109,6 +119,9 @@ int launch_allpairs_q8_match_prepare(hipStream_t s, void *scratch, int batch, in
                                      const float *desc0, const float *desc1, double thresh, int *match_idx,
                                      float *match_score, int dmode, void *next_scratch, int next_batch,
                                      int next_cap, const int *next_n1, const float *next_desc1);
+// the single-pass int8 screen (k_allpairs_direct.hip): no scratch, frame 1 quantised in-kernel
+int launch_allpairs_q8d_match(hipStream_t s, int batch, int cap, const int *n0, const int *n1, const float *desc0,
+                              const float *desc1, double thresh, int *match_idx, float *match_score, int dmode = 0);
 size_t allpairs_i8_scratch_bytes(int batch, int cap);
 int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
                        const int8_t *desc0, const int8_t *desc1, int *match_idx, int *match_dot);

@@ -34,7 +34,7 @@ _F = ctypes.c_float
 _D = ctypes.c_double
 
 
-SCREENS = {"i8": 0, "f16": 1}  # mv_allpairs_screen
+SCREENS = {"i8": 0, "f16": 1, "i8s": 2}  # mv_allpairs_screen (i8s: int8 against a staged image)
 
 
 class MVError(RuntimeError):
@@ -410,11 +410,15 @@ class Context:
         check(lib().mv_context_set_stream(self.h, ptr), "set_stream")
 
     def set_allpairs_screen(self, screen):
-        """'i8' (default) or 'f16': how the fp32 all-pairs match screens before its exact re-score."""
+        """'i8' (default: one pass, frame 1 quantised in-kernel), 'f16' or 'i8s' (int8 against a
+        staged image): how the fp32 all-pairs match screens before its exact re-score."""
         check(lib().mv_context_set_allpairs_screen(self.h, SCREENS[screen]), "set_allpairs_screen")
 
     def allpairs_screen(self):
-        return {v: k for k, v in SCREENS.items()}[lib().mv_context_allpairs_screen(self.h)]
+        r = lib().mv_context_allpairs_screen(self.h)
+        if r < 0:
+            check(r, "allpairs_screen")
+        return {v: k for k, v in SCREENS.items()}[r]
 
     def synchronize(self):
         check(lib().mv_context_synchronize(self.h), "synchronize")

@@ -45,9 +45,10 @@ def ctx():
     c.close()
 
 
-@pytest.fixture(params=["i8", "f16"])
+@pytest.fixture(params=["i8", "i8s", "f16"])
 def screen(request, ctx):
-    """both fp32 screens (int8 MFMA, the default, and fp16 MFMA) must give identical outputs"""
+    """every fp32 screen (int8 MFMA one-pass -- the default --, int8 against a staged image, fp16
+    MFMA) must give identical outputs"""
     ctx.set_allpairs_screen(request.param)
     yield request.param
     ctx.set_allpairs_screen("i8")

@@ -403,6 +403,8 @@ def test_allpairs_screen_selection(ctx):
     assert c.allpairs_screen() == "i8"  # the default
     c.set_allpairs_screen("f16")
     assert c.allpairs_screen() == "f16"
+    c.set_allpairs_screen("i8s")
+    assert c.allpairs_screen() == "i8s"
     with pytest.raises(RuntimeError):
         mvtrack.check(mvtrack.lib().mv_context_set_allpairs_screen(c.h, 7), "bad screen")
     c.close()
