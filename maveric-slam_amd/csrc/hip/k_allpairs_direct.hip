@@ -46,25 +46,55 @@ constexpr int D_OFF_AIMG = 2 * D_HALF;  // A images: staging slot 2 + the ring (
 static_assert(D_OFF_AIMG + D_NW * 32 * KD <= D_OFF_ROW, "A images fit staging slot 2 + the ring");
 static_assert(epi_bytes<D_NW>() <= D_OFF_ROW, "the epilogue fits staging + ring");
 static_assert(D_LDS <= 160 * 1024, "one workgroup per CU");
-constexpr int D_PF = 2;  // k32 steps of B fragments read ahead of the MFMAs
+#ifndef D_PF
+#define D_PF 1  // k32 steps of B fragments read ahead of the MFMAs
+#endif
+#ifndef D_EXP_NOQ
+#define D_EXP_NOQ 0  // timing experiment only (wrong results): no quantisation in the sweep
+#endif
+#ifndef D_EXP_NODMA
+#define D_EXP_NODMA 0  // timing experiment only (wrong results): no frame-1 DMA in the sweep
+#endif
+#ifndef QS_LOAD
+#define QS_LOAD 1  // the k32 step whose slot issues the quantisation's staging reads
+#endif
 
-// DPP row-of-16 reductions (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror): every
-// lane of the 16 ends with the same value
-template <int CTRL>
-__device__ __forceinline__ float dppf(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+#ifdef MV_TRACE  // phase stamps (s_memtime) per (block, wave): tools/trace_direct.py
+constexpr int D_TRACE_BLOCKS = 16384;
+__device__ unsigned long long g_d_trace[D_TRACE_BLOCKS * D_NW * 10];
+#define D_STAMP(K) do { __builtin_amdgcn_sched_barrier(0); ts_[K] = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
+#define D_SYNC() do { const unsigned long long b_ = __builtin_amdgcn_s_memtime(); __syncthreads(); ts_[9] += __builtin_amdgcn_s_memtime() - b_; } while (0)
+#define D_WAITVM(N) do { __builtin_amdgcn_sched_barrier(0); const unsigned long long b_ = __builtin_amdgcn_s_memtime(); wait_vm<N>(); ts_[8] += __builtin_amdgcn_s_memtime() - b_; __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define D_WAITVM(N) wait_vm<N>()
+#define D_STAMP(K) do { } while (0)
+#define D_SYNC() __syncthreads()
+#endif
+
+// max |b| and sum |b|^2 over a row's 16 lanes (quad_perm [1,0,3,2], [2,3,0,1],
+// row_half_mirror, row_mirror), the two reductions interleaved so that every DPP read is two
+// instructions behind the write it reads (no NaN canonicalisation in the max: NaN is caught by
+// |b|^2); every lane of the 16 ends with the same values
+__device__ __forceinline__ void row16_max_sum(float &m, float &q2) {
+    asm("s_nop 1\n\t"
+        "v_max_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_add_f32_dpp %1, %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 0\n\t"
+        "v_max_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_add_f32_dpp %1, %1, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 0\n\t"
+        "v_max_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "v_add_f32_dpp %1, %1, %1 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 0\n\t"
+        "v_max_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "v_add_f32_dpp %1, %1, %1 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1"
+        : "+v"(m), "+v"(q2));
 }
-__device__ __forceinline__ float max16(float v) {
-    v = fmaxf(v, dppf<0xB1>(v));
-    v = fmaxf(v, dppf<0x4E>(v));
-    v = fmaxf(v, dppf<0x141>(v));
-    return fmaxf(v, dppf<0x140>(v));
-}
-__device__ __forceinline__ float sum16(float v) {
-    v += dppf<0xB1>(v);
-    v += dppf<0x4E>(v);
-    v += dppf<0x141>(v);
-    return v + dppf<0x140>(v);
+__device__ __forceinline__ float vmax(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
 }
 
 // Half h of frame 1 (rows 32 h .. +31, clamped to n1 - 1) -> staging slot at LDS byte `slot`:
@@ -87,46 +117,75 @@ __device__ __forceinline__ void dma_half(const float *B, int h, int n1, int wu, 
 // Quantise staging slot `stg` (frame-1 rows j0 .. j0 + 31) into rows 32 hh .. +31 of the int8
 // tile slot `rq`: thread t takes floats 16 sub .. +15 of row t >> 4.  Rows j >= n1 (padding,
 // or a half past the end) are written but excluded from the statistics (their columns are
-// masked by the dequantisation operands).
+// masked by the dequantisation operands).  In stages, so that the sweep can spread them over
+// its MFMA steps (stage k runs beside k32 step k); branch-free, so that a segment stays one
+// basic block.
+struct QHalf {
+    f32x4v x0, x1, x2, x3;
+    float m, qa, qb, q, s;
+    i32x4 code;
+    __device__ __forceinline__ void load(const char *stg, int t) {  // 4 ds_read_b128
+        const char *src = stg + (t >> 4) * (KD * 4) + (t & 15) * 16;
+        x0 = *reinterpret_cast<const f32x4v *>(src);
+        x1 = *reinterpret_cast<const f32x4v *>(src + 256);
+        x2 = *reinterpret_cast<const f32x4v *>(src + 512);
+        x3 = *reinterpret_cast<const f32x4v *>(src + 768);
+    }
+    __device__ __forceinline__ void absmax() {
+        m = absmax3(0.f, x0[0], x0[1]);
+        m = absmax3(m, x0[2], x0[3]);
+        m = absmax3(m, x1[0], x1[1]);
+        m = absmax3(m, x1[2], x1[3]);
+        m = absmax3(m, x2[0], x2[1]);
+        m = absmax3(m, x2[2], x2[3]);
+        m = absmax3(m, x3[0], x3[1]);
+        m = absmax3(m, x3[2], x3[3]);
+    }
+    __device__ __forceinline__ void sumsq() {
+        qa = __builtin_fmaf(x0[0], x0[0], __builtin_fmaf(x0[1], x0[1], __builtin_fmaf(x0[2], x0[2], x0[3] * x0[3])));
+        qb = __builtin_fmaf(x1[0], x1[0], __builtin_fmaf(x1[1], x1[1], __builtin_fmaf(x1[2], x1[2], x1[3] * x1[3])));
+        qa = __builtin_fmaf(x2[0], x2[0], __builtin_fmaf(x2[1], x2[1], __builtin_fmaf(x2[2], x2[2], __builtin_fmaf(x2[3], x2[3], qa))));
+        qb = __builtin_fmaf(x3[0], x3[0], __builtin_fmaf(x3[1], x3[1], __builtin_fmaf(x3[2], x3[2], __builtin_fmaf(x3[3], x3[3], qb))));
+    }
+    __device__ __forceinline__ void reduce() {
+        qa = qa + qb;
+        row16_max_sum(m, qa);  // qa = |b|^2 from here on
+        q = m > 0.f ? 127.f * __builtin_amdgcn_rcpf(m) : 0.f;
+        s = m * (1.f / 127.f);
+    }
+    __device__ __forceinline__ void pack01() {
+        code[0] = pack4(x0[0], x0[1], x0[2], x0[3], q);
+        code[1] = pack4(x1[0], x1[1], x1[2], x1[3], q);
+    }
+    __device__ __forceinline__ void pack23() {
+        code[2] = pack4(x2[0], x2[1], x2[2], x2[3], q);
+        code[3] = pack4(x3[0], x3[1], x3[2], x3[3], q);
+    }
+    // the codes and the scale into the tile slot; the pair statistics: finite (|b|^2 propagates
+    // NaN / inf) and a representable scale (zero rows: s = 0, codes 0, every screen value of the
+    // column 0 -- exact, no flag needed)
+    __device__ __forceinline__ void store(char *rq, int hh, int j0, int n1, int t, float &smax, float &b2max,
+                                          bool &bad) {
+        const int r = t >> 4, sub = t & 15, row = 32 * hh + r;
+        *reinterpret_cast<i32x4 *>(rq + row * KD + ((sub ^ (row & 15)) << 4)) = code;
+        if (sub == 0) reinterpret_cast<float *>(rq + TILE)[row] = s;
+        const bool live = j0 + r < n1;
+        const bool ok = (qa <= FLT_MAX) & ((m == 0.f) | ((m >= SCALE_LO) & (m <= SCALE_HI)));
+        smax = vmax(smax, live ? s : 0.f);
+        b2max = vmax(b2max, live ? qa : 0.f);
+        bad = bad | (live & !ok);
+    }
+};
 __device__ __forceinline__ void quant_half(const char *stg, char *rq, int hh, int j0, int n1, int t, float &smax,
                                            float &b2max, bool &bad) {
-    const int r = t >> 4, sub = t & 15;
-    const char *src = stg + r * (KD * 4) + sub * 16;
-    const f32x4v x0 = *reinterpret_cast<const f32x4v *>(src);
-    const f32x4v x1 = *reinterpret_cast<const f32x4v *>(src + 256);
-    const f32x4v x2 = *reinterpret_cast<const f32x4v *>(src + 512);
-    const f32x4v x3 = *reinterpret_cast<const f32x4v *>(src + 768);
-    float m = absmax3(0.f, x0[0], x0[1]);
-    m = absmax3(m, x0[2], x0[3]);
-    m = absmax3(m, x1[0], x1[1]);
-    m = absmax3(m, x1[2], x1[3]);
-    m = absmax3(m, x2[0], x2[1]);
-    m = absmax3(m, x2[2], x2[3]);
-    m = absmax3(m, x3[0], x3[1]);
-    m = absmax3(m, x3[2], x3[3]);
-    float qa = __builtin_fmaf(x0[0], x0[0], __builtin_fmaf(x0[1], x0[1], __builtin_fmaf(x0[2], x0[2], x0[3] * x0[3])));
-    float qb = __builtin_fmaf(x1[0], x1[0], __builtin_fmaf(x1[1], x1[1], __builtin_fmaf(x1[2], x1[2], x1[3] * x1[3])));
-    qa = __builtin_fmaf(x2[0], x2[0], __builtin_fmaf(x2[1], x2[1], __builtin_fmaf(x2[2], x2[2], __builtin_fmaf(x2[3], x2[3], qa))));
-    qb = __builtin_fmaf(x3[0], x3[0], __builtin_fmaf(x3[1], x3[1], __builtin_fmaf(x3[2], x3[2], __builtin_fmaf(x3[3], x3[3], qb))));
-    m = max16(m);
-    const float q2 = sum16(qa + qb);
-    const float q = m > 0.f ? 127.f * __builtin_amdgcn_rcpf(m) : 0.f;
-    const float s = m * (1.f / 127.f);
-    i32x4 code;
-    code[0] = pack4(x0[0], x0[1], x0[2], x0[3], q);
-    code[1] = pack4(x1[0], x1[1], x1[2], x1[3], q);
-    code[2] = pack4(x2[0], x2[1], x2[2], x2[3], q);
-    code[3] = pack4(x3[0], x3[1], x3[2], x3[3], q);
-    const int row = 32 * hh + r;
-    *reinterpret_cast<i32x4 *>(rq + row * KD + ((sub ^ (row & 15)) << 4)) = code;
-    if (sub == 0) reinterpret_cast<float *>(rq + TILE)[row] = s;
-    // finite (|b|^2 propagates NaN / inf) and a representable scale (zero rows: s = 0, codes
-    // 0, every screen value of the column 0 -- exact, no flag needed)
-    const bool live = j0 + r < n1;
-    const bool ok = q2 <= FLT_MAX && (m == 0.f || (m >= SCALE_LO && m <= SCALE_HI));
-    smax = live ? fmaxf(smax, s) : smax;
-    b2max = live ? fmaxf(b2max, q2) : b2max;
-    bad = bad || (live && !ok);
+    QHalf h;
+    h.load(stg, t);
+    h.absmax();
+    h.sumsq();
+    h.reduce();
+    h.pack01();
+    h.pack23();
+    h.store(rq, hh, j0, n1, t, smax, b2max, bad);
 }
 
 __global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, const int *__restrict__ n0v,
@@ -134,6 +193,10 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, con
                                                        const float *__restrict__ desc1, double thresh, int dmode,
                                                        int *__restrict__ match_idx, float *__restrict__ match_score) {
     __shared__ __attribute__((aligned(16))) char lds[D_LDS];
+#ifdef MV_TRACE
+    unsigned long long ts_[10] = {};
+    D_STAMP(0);
+#endif
     const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int pair = L / tiles_r, tr = L % tiles_r;
     const int n0 = min(max(n0v[pair], 0), cap), n1 = min(max(n1v[pair], 0), cap);
@@ -164,6 +227,7 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, con
     i32x4 aI[RG][KD / 32];
     a_phase<false>(lds + D_OFF_AIMG + w * 32 * KD, rowv, w * 64, row0, n0, lane, A, nullptr, nullptr, nullptr,
                    false, aI);
+    D_STAMP(1);
     __syncthreads();  // the A images (staging slot 2 + the ring) are consumed
     if (nh > 2) {
         dma_half(B, 2, n1, wu, chunk16, lds_base + 2 * D_HALF);
@@ -178,6 +242,7 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, con
     quant_half(lds + D_HALF, ring, 1, 32, n1, t, smax, b2max, bad);
     __syncthreads();  // tile 0 in ring slot 0; staging slots 0, 1 free
     if (nh > 3) dma_half(B, 3, n1, wu, chunk16, lds_base);
+    D_STAMP(2);
 
     // B fragment: column block c (0, 1), lane row 32 c + fr, k32 step s: chunk (2 s + fh)
     const int rdb = fr * KD;
@@ -216,15 +281,24 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, con
         }                                                                                    \
     } while (0)
     // group G's MFMAs on the tile at `rs` (fragments read D_PF k32 steps ahead), folding group
-    // FG meanwhile, and this thread's share of the next tile's quantisation (QUANT)
-#define D_SEG(G, FG, G0, QUANT)                                                              \
+    // FG meanwhile, and this thread's share of the next tile's quantisation from staging STG
+    // into rows 32 HH .. of slot rq (frame-1 rows J0 ..), one stage per k32 step; every step
+    // is fenced (sched_barrier) so that the stages stay spread over the MFMAs
+#define D_SEG(G, FG, G0, STG, HH, J0)                                                        \
     do {                                                                                     \
         const char *base = rs + rdb;                                                         \
         int xs_ = xsw;                                                                       \
         asm volatile("" : "+v"(xs_)); /* per-use offsets: not 8 loop-invariant VGPRs */      \
         i32x4 b0_[KD / 32], b1_[KD / 32];                                                    \
-        QUANT;                                                                               \
+        QHalf qh_;                                                                           \
         _Pragma("unroll") for (int s_ = 0; s_ < KD / 32 + D_PF; s_++) {                      \
+            if (D_EXP_NOQ) {} else if (s_ == QS_LOAD) qh_.load((STG), t);                    \
+            if (!D_EXP_NOQ && s_ == QS_LOAD + 1) qh_.absmax();                                             \
+            if (!D_EXP_NOQ && s_ == QS_LOAD + 2) qh_.sumsq();                                              \
+            if (!D_EXP_NOQ && s_ == QS_LOAD + 3) qh_.reduce();                                             \
+            if (!D_EXP_NOQ && s_ == QS_LOAD + 4) qh_.pack01();                                             \
+            if (!D_EXP_NOQ && s_ == QS_LOAD + 5) qh_.pack23();                                             \
+            if (!D_EXP_NOQ && s_ == QS_LOAD + 6) qh_.store(rq, (HH), (J0), n1, t, smax, b2max, bad);       \
             if (s_ < KD / 32) {                                                              \
                 const int ch_ = ((2 * s_) ^ xs_) * 16;                                       \
                 b0_[s_] = *reinterpret_cast<const i32x4 *>(base + ch_);                      \
@@ -241,6 +315,7 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, con
                 }                                                                            \
                 D_FOLD2(FG, m_, G0);                                                         \
             }                                                                                \
+            __builtin_amdgcn_sched_barrier(0);                                               \
         }                                                                                    \
     } while (0)
 
@@ -253,18 +328,18 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, con
     int sA = 2, sB = 0;  // staging slots of halves 2t + 2, 2t + 3
     for (int tc = 0; tc < ntc; tc++) {
         if (2 * tc + 3 < nh) {  // half 2t + 2 landed (2t + 3 may be in flight)
-            wait_vm<4>();
+            D_WAITVM(4);
         } else {
-            wait_vm<0>();
+            D_WAITVM(0);
         }
-        __syncthreads();  // tile t complete in its slot; staging slot of half 2t + 1 free
+        D_SYNC();  // tile t complete in its slot; staging slot of half 2t + 1 free
         const int sN = 3 - sA - sB;  // the third staging slot
-        if (2 * tc + 4 < nh) dma_half(B, 2 * tc + 4, n1, wu, chunk16, lds_base + (unsigned)(sN * D_HALF));
+        if (!D_EXP_NODMA && 2 * tc + 4 < nh) dma_half(B, 2 * tc + 4, n1, wu, chunk16, lds_base + (unsigned)(sN * D_HALF));
         const char *rs = ring + (tc & 1) * SLOT;
         char *rq = ring + ((tc + 1) & 1) * SLOT;
         const char *stA = lds + sA * D_HALF, *stB = lds + sB * D_HALF;
         const unsigned gp_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)max(tc - 1, 0));
-        D_SEG(0, 1, gp_, quant_half(stA, rq, 0, 32 * (2 * tc + 2), n1, t, smax, b2max, bad));
+        D_SEG(0, 1, gp_, stA, 0, 32 * (2 * tc + 2));
         {  // the dequantisation operands of tile tc: fma(t, 2^21 s, -2^23 s)
             const float *rl_ = reinterpret_cast<const float *>(rs + TILE);
             const int col_ = tc * BN + fr;
@@ -275,14 +350,14 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, con
             pc1 = col_ + 32 < n1 ? -8388608.0f * s1_ : -3.0e38f;
         }
         if (2 * tc + 4 < nh) {  // half 2t + 3 landed (2t + 4 may be in flight)
-            wait_vm<4>();
+            D_WAITVM(4);
         } else {
-            wait_vm<0>();
+            D_WAITVM(0);
         }
-        __syncthreads();  // staging slot of half 2t + 2 consumed
-        if (2 * tc + 5 < nh) dma_half(B, 2 * tc + 5, n1, wu, chunk16, lds_base + (unsigned)(sA * D_HALF));
+        D_SYNC();  // staging slot of half 2t + 2 consumed
+        if (!D_EXP_NODMA && 2 * tc + 5 < nh) dma_half(B, 2 * tc + 5, n1, wu, chunk16, lds_base + (unsigned)(sA * D_HALF));
         const unsigned gc_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)tc);
-        D_SEG(1, 0, gc_, quant_half(stB, rq, 1, 32 * (2 * tc + 3), n1, t, smax, b2max, bad));
+        D_SEG(1, 0, gc_, stB, 1, 32 * (2 * tc + 3));
         // halves 2t + 4, 2t + 5 sit in slots sN, sA
         const int nA = sN, nB = sA;
         sA = nA;
@@ -296,6 +371,7 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, con
 #undef D_FOLD2
 #undef D_SEG
 
+    D_STAMP(3);
     // ---- the pair's frame-1 statistics (every workgroup of the pair computes the same) ----
     smax = fmaxf(smax, swz_xor<16>(smax));
     b2max = fmaxf(b2max, swz_xor<16>(b2max));
@@ -318,8 +394,20 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, con
     }
     const double Bn = sqrt((double)B2) * 1.0001;
     const double Eb = (8.001 * (double)S + 4.76837158203125e-07 * Bn) * 1.0001 + 1e-30;
+    D_STAMP(4);
     epilogue<D_NW>(lds, rowv, m1, m2, Bn, Eb, flagged, tb, tkeep, w, lane, row0, n0, n1, A, B, oidx, oscore, thresh,
                    dmode);
+#ifdef MV_TRACE
+    D_STAMP(5);
+    if (lane == 0 && blockIdx.x < D_TRACE_BLOCKS) {
+        unsigned long long *o = g_d_trace + ((size_t)blockIdx.x * D_NW + w) * 10;
+        for (int k = 0; k < 6; k++) o[k] = ts_[k];
+        o[6] = __smid();
+        o[7] = __builtin_amdgcn_s_memrealtime();
+        o[8] = ts_[8];
+        o[9] = ts_[9];
+    }
+#endif
 }
 
 }  // namespace
@@ -343,3 +431,9 @@ int launch_allpairs_q8d_match(hipStream_t s, int batch, int cap, const int *n0, 
 }
 
 }  // namespace mv
+
+#ifdef MV_TRACE
+extern "C" int mv_debug_direct_trace(void *host, long bytes) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_d_trace), (size_t)bytes) == hipSuccess ? 0 : -3;
+}
+#endif

@@ -171,6 +171,37 @@ typedef struct {
 
 static int32_t wrap_mul(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
 
+/* squared_dist, tracking_main.c:18-43: the full 256-D dot and both squared norms when
+ * *norm1_squared is 0 (the first valid candidate of a query), else the 64-D dot and query norm
+ * with *norm1_squared left as it was (stale).  Pinned against the reference's own function
+ * (tests/test_oracle_pinning.py::test_squared_dist_pinned). */
+ORC_EXPORT void orc_squared_dist(const int8_t *desc1, const int8_t *desc2, int32_t *sum, int32_t *norm1_squared,
+                                 int32_t *norm2_squared) {
+    int32_t s = 0, n2 = 0;
+    if (*norm1_squared == 0) {
+        int32_t n1 = 0;
+        for (int k = 0; k < 256; k++) {
+            s += desc1[k] * desc2[k];
+            n1 += desc1[k] * desc1[k];
+            n2 += desc2[k] * desc2[k];
+        }
+        *norm1_squared = n1;
+    } else {
+        for (int k = 0; k < 64; k++) {
+            s += desc1[k] * desc2[k];
+            n2 += desc2[k] * desc2[k];
+        }
+    }
+    *sum = s;
+    *norm2_squared = n2;
+}
+/* tracking_main.c:154: (int)dot*dot / (float)(int)(n1*n2), both int products wrapping */
+ORC_EXPORT float orc_window_score(int32_t dot, int32_t n1, int32_t n2) {
+    return (float)wrap_mul(dot, dot) / (float)wrap_mul(n1, n2);
+}
+/* tracking_main.c:155: the float score against MATCH_THRESHOLD^2 in double */
+ORC_EXPORT int orc_window_pass(float d) { return (double)d > 0.9 * 0.9; }
+
 /* Returns the number of matches; points are [max_matches][2] (x, y) pixels.
  * q_of_match (optional) receives the query slot i of each match. */
 ORC_EXPORT int orc_window_match(int rows, int cols, const int8_t *desc0, const int *max_idx0,
@@ -203,21 +234,9 @@ ORC_EXPORT int orc_window_match(int rows, int cols, const int8_t *desc0, const i
                     /* squared_dist(desc0, desc1, ...) :18-43 -- note the argument order:
                      * its "desc1/norm1" is the CANDIDATE, "desc2/norm2" the query. */
                     int32_t dot = 0, n2 = 0;
-                    if (n1 == 0) {
-                        for (int k = 0; k < 256; k++) {
-                            dot += c[k] * q[k];
-                            n1 += c[k] * c[k];
-                            n2 += q[k] * q[k];
-                        }
-                    } else {
-                        for (int k = 0; k < 64; k++) {
-                            dot += c[k] * q[k];
-                            n2 += q[k] * q[k];
-                        }
-                    }
-                    /* :154  (int)dot*dot / (float)(int)(n1*n2), both products wrap */
-                    float d = (float)wrap_mul(dot, dot) / (float)wrap_mul(n1, n2);
-                    if ((double)d > 0.9 * 0.9) { /* :155, MATCH_THRESHOLD^2 in double */
+                    orc_squared_dist(c, q, &dot, &n1, &n2);
+                    const float d = orc_window_score(dot, n1, n2);
+                    if (orc_window_pass(d)) {
                         if (!found || d > best) {
                             found = 1;
                             best_index = idx0;

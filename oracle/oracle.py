@@ -68,8 +68,37 @@ def lib():
         L.orc_kp_select.restype = _I
         L.orc_kp_select.argtypes = [_P, _I, _I, _I, _I, _F, _I, _I, _I, _P]
         L.orc_kp_sample.argtypes = [_P, _I, _I, _I, _I, _I, _P, _P]
+        L.orc_squared_dist.argtypes = [_P, _P, _P, _P, _P]
+        L.orc_window_score.restype = _F
+        L.orc_window_score.argtypes = [_I, _I, _I]
+        L.orc_window_pass.restype = _I
+        L.orc_window_pass.argtypes = [_F]
         _lib = L
     return _lib
+
+
+REF_WINDOW_SO = os.path.join(HERE, "_ref", "libmv_ref_window.so")
+_ref_window = None
+
+
+def ref_window_available():
+    return os.path.exists(REF_WINDOW_SO)
+
+
+def ref_window():
+    """The reference's own squared_dist (tracking_main.c:18-43) and window score line (:154,
+    MATCH_THRESHOLD :12), extracted from its text and compiled by oracle/Makefile; build-container
+    only."""
+    global _ref_window
+    if _ref_window is None:
+        R = ctypes.CDLL(REF_WINDOW_SO)
+        R.ref_squared_dist.argtypes = [_P, _P, _P, _P, _P]
+        R.ref_window_score.restype = _F
+        R.ref_window_score.argtypes = [_I, _I, _I]
+        R.ref_window_pass.restype = _I
+        R.ref_window_pass.argtypes = [_F]
+        _ref_window = R
+    return _ref_window
 
 
 def ref_available():

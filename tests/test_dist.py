@@ -179,6 +179,29 @@ def test_sequence_shard_covers_every_pair_once():
         mvtrack.sequence_shard(1, 2, 0)
 
 
+def test_bench_spawns_ranks_and_gathers_results():
+    """bench.py --gpus 2 without a launcher starts its own 2 rank processes; --harness-cpu runs
+    the same harness (barrier-bracketed timing, max over ranks, the per-step all-gather of every
+    pair's T + match count) with the CPU oracle as the step over gloo: n_gpus 2, the gathered
+    buffer holds N x B pairs from both ranks, one all-gather per step (warmup included)."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--harness-cpu", "--batch", "3",
+                        "--kp", "32", "--steps", "2", "--warmup", "1"], capture_output=True, text=True, timeout=300,
+                       env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["n_gpus"] == 2 and d["steps"] == 2
+    assert d["gathered_pairs"] == 2 * 3 and d["gathered_ranks"] == [0, 1]
+    assert d["all_gathers"] == 3
+    assert d["gathered_matches"] > 0 and d["value"] > 0
+
+
 def _seq_worker(rank, world, port, q):
     import sys
 
@@ -208,8 +231,10 @@ def _seq_worker(rank, world, port, q):
 
 
 def test_two_rank_sequence_shards_gloo():
-    """Sequence mode over 2 ranks: each matches its contiguous pair range (one shared boundary
-    frame, no exchange); together they reproduce the single-process track pair for pair."""
+    """The sequence partition over 2 ranks (mvtrack.sequence_shard, one shared boundary frame,
+    no exchange): each rank's contiguous pair range, matched by the CPU oracle and gathered,
+    covers the track pair for pair.  The GPU sequence kernel on the same shards is
+    test_two_rank_sequence_shards_gpu."""
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -236,4 +261,91 @@ def test_two_rank_sequence_shards_gloo():
     assert [b for b, _ in got] == list(range(F - 1))
     for b, idx in got:
         assert idx == oracle.allpairs_f32(D[b], D[b + 1], 0.8)[0].tolist(), b
+    assert res[0] == res[1]
+
+
+def _seq_gpu_worker(rank, world, port, q):
+    import sys
+
+    import torch
+    import torch.distributed as dist
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "oracle"), os.path.join(root, "maveric-slam_amd")):
+        sys.path.insert(0, p)
+    import mvtrack
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    D = _seq_track()
+    F, n = D.shape[0], D.shape[1]
+    lo, hi = mvtrack.sequence_shard(F, world, rank)
+    dev = torch.device("cuda:0")
+    ctx = mvtrack.Context(0)
+    ctx.set_stream(torch.cuda.current_stream())
+    d = torch.from_numpy(np.ascontiguousarray(D[lo:hi])).to(dev)
+    ns = torch.full((hi - lo,), n, dtype=torch.int32, device=dev)
+    idx = torch.empty((hi - lo - 1, n), dtype=torch.int32, device=dev)
+    ctx.match_sequence_f32(d, ns, idx, None, 0.8)
+    torch.cuda.synchronize()
+    mine = [(lo + b, idx[b].cpu().numpy().tolist()) for b in range(hi - lo - 1)]
+    ctx.close()
+    out = [None] * world
+    dist.all_gather_object(out, mine)
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def _seq_track():
+    F, n = 9, 96
+    rng = np.random.default_rng(8)
+    D = rng.standard_normal((F, n, 256)).astype(np.float32)
+    for b in range(1, F):
+        D[b, :60] = D[b - 1, rng.permutation(n)[:60]] + 0.02 * rng.standard_normal((60, 256)).astype(np.float32)
+    D /= np.linalg.norm(D, axis=2, keepdims=True)
+    return D
+
+
+@pytest.mark.gpu
+def test_two_rank_sequence_shards_gpu():
+    """Sequence mode sharded over 2 ranks (two processes on the GPU, gloo for the gather): each
+    rank runs mv_match_sequence_f32_dev on its contiguous frame range (one shared boundary
+    frame); the gathered per-pair indices equal a single-process sequence match of the whole
+    track and the oracle, pair for pair."""
+    import sys
+
+    import torch
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "oracle"), os.path.join(root, "maveric-slam_amd")):
+        sys.path.insert(0, p)
+    import mvtrack
+    import oracle
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_seq_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    D = _seq_track()
+    F, n = D.shape[0], D.shape[1]
+    got = sorted(x for shard in res[0] for x in shard)
+    assert [b for b, _ in got] == list(range(F - 1))
+    dev = torch.device("cuda:0")
+    c = mvtrack.Context(0)
+    c.set_stream(torch.cuda.current_stream())
+    d = torch.from_numpy(D).to(dev)
+    idx = torch.empty((F - 1, n), dtype=torch.int32, device=dev)
+    c.match_sequence_f32(d, torch.full((F,), n, dtype=torch.int32, device=dev), idx, None, 0.8)
+    torch.cuda.synchronize()
+    full = idx.cpu().numpy()
+    c.close()
+    for b, ix in got:
+        assert ix == full[b].tolist(), b
+        assert ix == oracle.allpairs_f32(D[b], D[b + 1], 0.8)[0].tolist(), b
     assert res[0] == res[1]

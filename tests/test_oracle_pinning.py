@@ -230,3 +230,41 @@ def test_window_as_intended_matches_bruteforce(orc):
         x0, y0, p0 = bj
         idx = r["max_idx0"][p0]
         assert r["points1"][k, 0] == x0 * 8 + idx % 8 and r["points1"][k, 1] == y0 * 8 + idx // 8
+
+
+@pytest.mark.skipif("not __import__('oracle').ref_window_available()", reason="oracle/_ref not built here")
+def test_squared_dist_pinned(orc):
+    """The oracle's squared_dist and window score (the arithmetic of tracking_main.c's windowed
+    match) bit for bit against the reference's OWN squared_dist (:18-43) and score
+    line (:154-155), extracted from its text at build time: random int8 descriptors incl. the
+    extremes, per query a sequence of candidates through the latched (stale) norm1 and the 64-D
+    branch, the int32 wrap of dot^2 and n1 n2 (most pairs overflow), and the threshold test."""
+    R, L, P = orc.ref_window(), orc.lib(), orc._ptr
+    rng = np.random.default_rng(18)
+    wraps = calls = 0
+    for q in range(300):
+        if q % 3 == 0:
+            query = rng.integers(-128, 128, 256).astype(np.int8)
+        else:
+            query = np.clip(np.round(rng.normal(0, 24 + q % 40, 256)), -128, 127).astype(np.int8)
+        n1r = np.zeros(1, np.int32)
+        n1o = np.zeros(1, np.int32)
+        for c in range(int(rng.integers(1, 12))):  # the window's candidates, first one latches norm1
+            cand = np.clip(np.round(query * rng.uniform(-1, 1.2) + rng.normal(0, 20, 256)), -128, 127).astype(np.int8)
+            if c == 5:
+                cand = np.full(256, -128, np.int8)  # extremes: 256 x 128^2 products
+            sr, n2r = np.zeros(1, np.int32), np.zeros(1, np.int32)
+            so, n2o = np.zeros(1, np.int32), np.zeros(1, np.int32)
+            R.ref_squared_dist(P(cand), P(query), P(sr), P(n1r), P(n2r))
+            L.orc_squared_dist(P(cand), P(query), P(so), P(n1o), P(n2o))
+            assert (sr[0], n1r[0], n2r[0]) == (so[0], n1o[0], n2o[0]), (q, c)
+            dr = R.ref_window_score(int(sr[0]), int(n1r[0]), int(n2r[0]))
+            do = L.orc_window_score(int(so[0]), int(n1o[0]), int(n2o[0]))
+            assert np.float32(dr).view(np.int32) == np.float32(do).view(np.int32) or (dr != dr and do != do), (q, c)
+            assert R.ref_window_pass(dr) == L.orc_window_pass(do)
+            calls += 1
+            wraps += int(int(n1r[0]) * int(n2r[0]) > 2**31 - 1)
+    assert calls > 1000 and wraps > calls // 2  # the overflowing products are exercised
+    # threshold edges of the score test
+    for d in (np.float32(0.81), np.nextafter(np.float32(0.81), np.float32(1)), np.nextafter(np.float32(0.81), np.float32(0))):
+        assert R.ref_window_pass(float(d)) == L.orc_window_pass(float(d))

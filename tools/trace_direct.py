@@ -1,0 +1,56 @@
+"""Phase timing of k_q8d_match (library built with EXTRA=-DMV_TRACE): per (block, wave)
+s_memtime stamps at entry, A phase done, tile 0 quantised, sweep done, statistics, epilogue
+done; plus the cycles each wave spent in the sweep's barriers."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "maveric-slam_amd"))
+import bench  # noqa: E402
+import mvtrack  # noqa: E402
+
+B, n = int(os.environ.get("TB", "8192")), 1024
+dev = torch.device("cuda", 0)
+d0, d1, _, _ = bench.gen_batch(torch, dev, B, n, seed=3)
+nn_ = torch.full((B,), n, dtype=torch.int32, device=dev)
+idx = torch.empty((B, n), dtype=torch.int32, device=dev)
+ctx = mvtrack.Context(0)
+ctx.set_stream(torch.cuda.current_stream())
+for _ in range(3):
+    ctx.match_allpairs_f32(d0, d1, nn_, nn_, idx, None)
+torch.cuda.synchronize()
+NW = 8
+nblk = min(B * 2, 16384)
+buf = np.zeros(nblk * NW * 10, np.uint64)
+lib = mvtrack.lib()
+lib.mv_debug_direct_trace.argtypes = [ctypes.c_void_p, ctypes.c_long]
+assert lib.mv_debug_direct_trace(buf.ctypes.data, buf.nbytes) == 0
+tr = buf.reshape(nblk, NW, 10).astype(np.int64)
+st = tr[:, :, :6]
+d = np.diff(st, axis=2)
+names = ["A-phase", "tile0-quant", "sweep", "stats", "epilogue"]
+print("per-wave phase cycles (median / p10 / p90 / max):")
+for k, nm in enumerate(names):
+    v = d[:, :, k].ravel()
+    print("  %-12s %9.0f %9.0f %9.0f %9.0f" % (nm, np.median(v), np.percentile(v, 10), np.percentile(v, 90), v.max()))
+for k, nm in ((9, "sweep-barrier"), (8, "sweep-vmwait")):
+    v = tr[:, :, k].ravel()
+    print("  %-12s %9.0f %9.0f %9.0f %9.0f" % (nm, np.median(v), np.percentile(v, 10), np.percentile(v, 90), v.max()))
+tot = st[:, :, 5] - st[:, :, 0]
+print("wave total median %.0f; sweep per tile %.0f" % (np.median(tot), np.median(d[:, :, 2]) / 16))
+sm = tr[:, 0, 6]
+start, end = st[:, :, 0].min(1), st[:, :, 5].max(1)
+cu = np.unique(sm)[0]
+sel = np.where(sm == cu)[0]
+o = sel[np.argsort(start[sel])]
+print("distinct CU ids", len(np.unique(sm)), "; CU", cu, "timeline (start, end, dur):")
+for b in o[:12]:
+    print("  blk %5d  %9d %9d %9d" % (b, start[b] - start[o[0]], end[b] - start[o[0]], end[b] - start[b]))
+rt = tr[:, 0, 7]
+a, b = o[0], o[-1]
+if rt[b] != rt[a]:
+    print("SCLK over the CU's run: %.3f GHz" % ((st[b, 0, 5] - st[a, 0, 5]) / ((rt[b] - rt[a]) / 100e6) / 1e9))
