@@ -12,19 +12,24 @@
 //     B stream   frame 1 streams as fp32 half-tiles (32 rows = 32 KiB) through a 3-slot LDS
 //                staging ring by LDS-DMA (global_load_lds_dwordx4, one 1-KiB row per wave
 //                instruction, issued one tile ahead).  Inside the sweep of tile t every thread
-//                quantises 16 values of tile t + 1 from staging (16 lanes per frame-1 row: the
-//                row's max |b| and |b|^2 by DPP reductions, q_jk = RNE(b_jk RN(127 RN(1/m))),
-//                s_j = RN(m RN(1/127))) into the int8 tile ring (2 slots of 16 KiB + 64 scales),
-//                beside the MFMAs of tile t.
-//     sweep      v_mfma_i32_32x32x32_i8 over 64-column tiles, the exact integer dot D_ij turned
-//                into the screen RN(D_ij s_j) by one FMA, tagged with its column tile and folded
-//                into a lane-local top-2 per row (as k_q8_match).
+//                quantises 16 values of tile t + 1 from staging (16 lanes per frame-1 row; the
+//                row's max |b| and |b|^2 by DPP reductions) into the int8 tile ring (2 slots of
+//                16 KiB + 64 per-column words), one stage per MFMA step.
+//     sweep      v_mfma_i32_32x32x32_i8 over 64-column tiles.  Integer keys (the fast path):
+//                column j is quantised with the power-of-two multiple q_j = 127 * 2^e_j,
+//                e_j in {0, 1, 2} (|b_jk| <= 1 required, as for unit-norm descriptors), so the
+//                exact integer dot D_ij scaled by 2^(2 - e_j) is one exact integer in the units
+//                of 1/508 for every column: the key (D_ij << (tb + 2 - e_j)) | tag -- ONE
+//                v_lshl_or_b32 per value, the column's shift riding in a VGPR -- is folded into a
+//                lane-local top-2 per row with v_max3_i32 / v_med3_i32 / v_max_i32.  A pair with
+//                a column outside that range (or a non-finite value) is swept again on the
+//                float path: per-column scale s_j = RN(m_j RN(1/127)), screen RN(D s_j) by one
+//                FMA, tagged in the low mantissa bits (as k_q8_match).
 //     epilogue   q8_common.hpp: the window decisions, exact re-scores where it does not decide.
 // The window's B terms come from the sweep itself: every workgroup quantises the whole frame 1
-// of its pair, so Bn = max_j |b_j| (from the fp32 |b_j|^2) and Eb = 8 max_j s_j + 2^-21 Bn
-// (|eps_j| <= 8 s_j + 2^-21 |b_j|, q8_common.hpp) and the pair's range flag (a non-finite value
-// or a row scale outside [2^-40, 2^40]: every row takes the exact path) are known to it after
-// the sweep, before any decision.
+// of its pair, so Bn = max_j |b_j| (from the fp32 |b_j|^2) and Eb = 8 max_j s_j (+ 2^-21 Bn on
+// the float path; the integer path's scaling is exact: |b_jk - q_jk / q_j| <= 1 / (2 q_j)) and
+// the pair's range flags are known to it after the sweep, before any decision.
 // LDS (135.8 KiB): staging 3 x 32 KiB | int8 ring 2 x 16.25 KiB | (|a|^2, s_a) per row |
 // per-wave statistics; the A images (8 x 8 KiB) use staging slot 2 + the ring before the
 // sweep, the epilogue (102 KiB) the staging + ring after it.
@@ -46,27 +51,16 @@ constexpr int D_OFF_AIMG = 2 * D_HALF;  // A images: staging slot 2 + the ring (
 static_assert(D_OFF_AIMG + D_NW * 32 * KD <= D_OFF_ROW, "A images fit staging slot 2 + the ring");
 static_assert(epi_bytes<D_NW>() <= D_OFF_ROW, "the epilogue fits staging + ring");
 static_assert(D_LDS <= 160 * 1024, "one workgroup per CU");
-#ifndef D_PF
-#define D_PF 1  // k32 steps of B fragments read ahead of the MFMAs
-#endif
-#ifndef D_EXP_NOQ
-#define D_EXP_NOQ 0  // timing experiment only (wrong results): no quantisation in the sweep
-#endif
-#ifndef D_EXP_NODMA
-#define D_EXP_NODMA 0  // timing experiment only (wrong results): no frame-1 DMA in the sweep
-#endif
-#ifndef QS_LOAD
-#define QS_LOAD 1  // the k32 step whose slot issues the quantisation's staging reads
-#endif
+constexpr int D_PF = 1;       // k32 steps of B fragments read ahead of the MFMAs
+constexpr int QS_LOAD = 1;    // the k32 step whose slot issues the quantisation's staging reads
+constexpr float IK_MMAX = 1.003f;  // integer path: max |b_jk| allowed (RNE(x 127) stays <= 127)
 
 #ifdef MV_TRACE  // phase stamps (s_memtime) per (block, wave): tools/trace_direct.py
 constexpr int D_TRACE_BLOCKS = 16384;
 __device__ unsigned long long g_d_trace[D_TRACE_BLOCKS * D_NW * 10];
 #define D_STAMP(K) do { __builtin_amdgcn_sched_barrier(0); ts_[K] = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
 #define D_SYNC() do { const unsigned long long b_ = __builtin_amdgcn_s_memtime(); __syncthreads(); ts_[9] += __builtin_amdgcn_s_memtime() - b_; } while (0)
-#define D_WAITVM(N) do { __builtin_amdgcn_sched_barrier(0); const unsigned long long b_ = __builtin_amdgcn_s_memtime(); wait_vm<N>(); ts_[8] += __builtin_amdgcn_s_memtime() - b_; __builtin_amdgcn_sched_barrier(0); } while (0)
 #else
-#define D_WAITVM(N) wait_vm<N>()
 #define D_STAMP(K) do { } while (0)
 #define D_SYNC() __syncthreads()
 #endif
@@ -90,6 +84,15 @@ __device__ __forceinline__ void row16_max_sum(float &m, float &q2) {
         "v_add_f32_dpp %1, %1, %1 row_mirror row_mask:0xf bank_mask:0xf\n\t"
         "s_nop 1"
         : "+v"(m), "+v"(q2));
+}
+// the top-2 fold on integer keys held in float registers' bits (as fold3 on floats)
+__device__ __forceinline__ void fold3i(int a, int b, float &m1f, float &m2f) {
+    int md, m1 = __float_as_int(m1f), m2 = __float_as_int(m2f);
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(md) : "v"(m1), "v"(a), "v"(b));
+    asm("v_max3_i32 %0, %1, %2, %3" : "=v"(m1) : "v"(m1), "v"(a), "v"(b));
+    asm("v_max_i32 %0, %1, %2" : "=v"(m2) : "v"(m2), "v"(md));
+    m1f = __int_as_float(m1);
+    m2f = __int_as_float(m2);
 }
 __device__ __forceinline__ float vmax(float a, float b) {
     float r;
@@ -115,14 +118,20 @@ __device__ __forceinline__ void dma_half(const float *B, int h, int n1, int wu, 
 }
 
 // Quantise staging slot `stg` (frame-1 rows j0 .. j0 + 31) into rows 32 hh .. +31 of the int8
-// tile slot `rq`: thread t takes floats 16 sub .. +15 of row t >> 4.  Rows j >= n1 (padding,
-// or a half past the end) are written but excluded from the statistics (their columns are
-// masked by the dequantisation operands).  In stages, so that the sweep can spread them over
-// its MFMA steps (stage k runs beside k32 step k); branch-free, so that a segment stays one
-// basic block.
+// tile slot `rq`: thread t takes floats 16 sub .. +15 of row t >> 4.  In stages, so that the
+// sweep spreads them over its MFMA steps; branch-free, so that a segment stays one basic block.
+//   IK: q_j = 127 * 2^e_j (e_j = 2, 1, 0 for m_j <= 1/4, <= 1/2, above), the per-column word
+//       = the key shift tb + 2 - e_j; rows j >= n1 (padding) get q = 0 (zero codes: D = 0).
+//   float: q_j = RN(127 RN(1/m_j)), the per-column word = s_j = RN(m_j RN(1/127)).
+// Statistics over the rows below n1 of real halves (`live`: a half past the end holds stale
+// bytes; clamped padding rows duplicate row n1 - 1): max s_j (the window's Eb), max |b_j|^2
+// (Bn), and `bad`: IK -- a value outside [-IK_MMAX, IK_MMAX] or non-finite (the pair takes the
+// float path); float -- non-finite or a row scale outside [2^-40, 2^40] (the exact path).
+template <bool IK>
 struct QHalf {
     f32x4v x0, x1, x2, x3;
     float m, qa, qb, q, s;
+    int sh;
     i32x4 code;
     __device__ __forceinline__ void load(const char *stg, int t) {  // 4 ds_read_b128
         const char *src = stg + (t >> 4) * (KD * 4) + (t & 15) * 16;
@@ -147,11 +156,18 @@ struct QHalf {
         qa = __builtin_fmaf(x2[0], x2[0], __builtin_fmaf(x2[1], x2[1], __builtin_fmaf(x2[2], x2[2], __builtin_fmaf(x2[3], x2[3], qa))));
         qb = __builtin_fmaf(x3[0], x3[0], __builtin_fmaf(x3[1], x3[1], __builtin_fmaf(x3[2], x3[2], __builtin_fmaf(x3[3], x3[3], qb))));
     }
-    __device__ __forceinline__ void reduce() {
+    __device__ __forceinline__ void reduce(int j, int n1, int tb) {
         qa = qa + qb;
         row16_max_sum(m, qa);  // qa = |b|^2 from here on
-        q = m > 0.f ? 127.f * __builtin_amdgcn_rcpf(m) : 0.f;
-        s = m * (1.f / 127.f);
+        if constexpr (IK) {
+            const int e = m > 0.5f ? 0 : (m > 0.25f ? 1 : 2);
+            q = j < n1 ? (e == 0 ? 127.f : (e == 1 ? 254.f : 508.f)) : 0.f;
+            s = e == 0 ? (1.f / 127.f) : (e == 1 ? (1.f / 254.f) : (1.f / 508.f));  // >= 1/q: Eb bound
+            sh = tb + 2 - e;
+        } else {
+            q = m > 0.f ? 127.f * __builtin_amdgcn_rcpf(m) : 0.f;
+            s = m * (1.f / 127.f);
+        }
     }
     __device__ __forceinline__ void pack01() {
         code[0] = pack4(x0[0], x0[1], x0[2], x0[3], q);
@@ -161,31 +177,235 @@ struct QHalf {
         code[2] = pack4(x2[0], x2[1], x2[2], x2[3], q);
         code[3] = pack4(x3[0], x3[1], x3[2], x3[3], q);
     }
-    // the codes and the scale into the tile slot; the pair statistics: finite (|b|^2 propagates
-    // NaN / inf) and a representable scale (zero rows: s = 0, codes 0, every screen value of the
-    // column 0 -- exact, no flag needed)
-    __device__ __forceinline__ void store(char *rq, int hh, int j0, int n1, int t, float &smax, float &b2max,
-                                          bool &bad) {
+    __device__ __forceinline__ void store(char *rq, int hh, int t, bool live, float &smax, float &b2max, bool &bad) {
         const int r = t >> 4, sub = t & 15, row = 32 * hh + r;
         *reinterpret_cast<i32x4 *>(rq + row * KD + ((sub ^ (row & 15)) << 4)) = code;
-        if (sub == 0) reinterpret_cast<float *>(rq + TILE)[row] = s;
-        const bool live = j0 + r < n1;
-        const bool ok = (qa <= FLT_MAX) & ((m == 0.f) | ((m >= SCALE_LO) & (m <= SCALE_HI)));
+        if constexpr (IK) {
+            if (sub == 0) reinterpret_cast<int *>(rq + TILE)[row] = sh;
+            bad = bad | (live & !((qa <= 1e30f) & (m <= IK_MMAX)));
+        } else {
+            if (sub == 0) reinterpret_cast<float *>(rq + TILE)[row] = s;
+            bad = bad | (live & !((qa <= FLT_MAX) & ((m == 0.f) | ((m >= SCALE_LO) & (m <= SCALE_HI)))));
+        }
         smax = vmax(smax, live ? s : 0.f);
         b2max = vmax(b2max, live ? qa : 0.f);
-        bad = bad | (live & !ok);
     }
 };
-__device__ __forceinline__ void quant_half(const char *stg, char *rq, int hh, int j0, int n1, int t, float &smax,
-                                           float &b2max, bool &bad) {
-    QHalf h;
-    h.load(stg, t);
-    h.absmax();
-    h.sumsq();
-    h.reduce();
-    h.pack01();
-    h.pack23();
-    h.store(rq, hh, j0, n1, t, smax, b2max, bad);
+
+// The pair's frame-1 state after a sweep (every workgroup of the pair computes the same).
+struct Sweep {
+    float smax, b2max;
+    bool bad;
+};
+
+// The sweep over all column tiles of frame 1 against the wave's A rows (aI): m1 / m2 get the
+// lane-local tagged top-2 per row (IK: integer keys in the registers' bits).  first: halves 0, 1
+// were issued before the A phase (else they are issued here).  Ends with every DMA drained and
+// every wave past its last LDS read of staging / ring (the epilogue may reuse them).
+template <bool IK>
+__device__ __forceinline__ Sweep sweep(char *lds, const float *B, int n1, int t, int lane, int wu, unsigned chunk16,
+                                       unsigned lds_base, const i32x4 (&aI)[RG][KD / 32], float (&m1)[RG][16],
+                                       float (&m2)[RG][16], int tb, unsigned tkeep, bool first) {
+    const int ntc = (n1 + BN - 1) / BN, nh = 2 * ntc;  // column tiles, staging halves (>= 2)
+    const int fr = lane & 31, fh = lane >> 5;
+    char *ring = lds + D_OFF_RING;
+    Sweep st = {0.f, 0.f, false};
+    if (!first) {
+        dma_half(B, 0, n1, wu, chunk16, lds_base);
+        dma_half(B, 1, n1, wu, chunk16, lds_base + D_HALF);
+    }
+    if (nh > 2) {
+        dma_half(B, 2, n1, wu, chunk16, lds_base + 2 * D_HALF);
+        wait_vm<4>();
+    } else {
+        wait_vm<0>();
+    }
+    __syncthreads();  // halves 0, 1 landed
+    {
+        QHalf<IK> h;
+#pragma unroll
+        for (int hh = 0; hh < 2; hh++) {
+            h.load(lds + hh * D_HALF, t);
+            h.absmax();
+            h.sumsq();
+            h.reduce(32 * hh + (t >> 4), n1, tb);
+            h.pack01();
+            h.pack23();
+            h.store(ring, hh, t, true, st.smax, st.b2max, st.bad);
+        }
+    }
+    __syncthreads();  // tile 0 in ring slot 0; staging slots 0, 1 free
+    if (nh > 3) dma_half(B, 3, n1, wu, chunk16, lds_base);
+
+    // B fragment: column block c (0, 1), lane row 32 c + fr, k32 step s: chunk (2 s + fh)
+    const int rdb = fr * KD;
+    const int xsw = fh ^ (fr & 15);  // chunk (2 s + fh) ^ (fr & 15) = 2 s ^ xsw
+
+    i32x16 acc[RG][2];
+    const float kinit = IK ? __int_as_float((int)0x80000000) : -__builtin_inff();
+#pragma unroll
+    for (int g = 0; g < RG; g++)
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            m1[g][q] = kinit;
+            m2[g][q] = kinit;
+        }
+    // "tile -1" of group 1, folded beside tile 0, never a maximum: IK -2^22 (below every real
+    // dot, |D| <= 127^2 256 < 2^22) at the widest shift; float 0 with the offset -3e38
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        acc[1][0][q] = IK ? -(1 << 22) : 0;
+        acc[1][1][q] = IK ? -(1 << 22) : 0;
+    }
+    unsigned vkeep = tkeep;
+    asm volatile("" : "+v"(vkeep));  // a VGPR operand: v_and_or_b32 may read one SGPR only
+    // the tile before: float dequantisation (fma(t, 2^21 s, -2^23 s); -3e38 past n1) / key shifts
+    float pr0 = 0.f, pr1 = 0.f, pc0 = -3.0e38f, pc1 = -3.0e38f;
+    int sh0 = tb + 2, sh1 = tb + 2;
+
+    // the fold of rows 2 S, 2 S + 1 of group FG (tile tags G0, G0 + 1)
+#define D_FOLD2(FG, S, G0)                                                                   \
+    do {                                                                                     \
+        _Pragma("unroll") for (int q = 2 * (S); q < 2 * (S) + 2; q++) {                      \
+            if constexpr (IK) {                                                              \
+                /* v_lshl_or_b32 keys; v_max3_i32 / v_med3_i32 / v_max_i32 top-2 */          \
+                const int ka_ = (int)(((unsigned)acc[FG][0][q] << sh0) | (G0));              \
+                const int kb_ = (int)(((unsigned)acc[FG][1][q] << sh1) | ((G0) + 1u));       \
+                fold3i(ka_, kb_, m1[FG][q], m2[FG][q]);                                      \
+            } else {                                                                         \
+                const float a_ = __builtin_fmaf(__int_as_float(acc[FG][0][q]), pr0, pc0);    \
+                const float b_ = __builtin_fmaf(__int_as_float(acc[FG][1][q]), pr1, pc1);    \
+                fold3(tag(a_, vkeep, (G0)), tag(b_, vkeep, (G0) + 1u), m1[FG][q], m2[FG][q]); \
+            }                                                                                \
+        }                                                                                    \
+    } while (0)
+    // group G's MFMAs on the tile at `rs` (fragments read D_PF k32 steps ahead), folding group
+    // FG meanwhile, and this thread's share of the next tile's quantisation from staging STG
+    // into rows 32 HH .. of slot rq, one stage per k32 step; every step is fenced
+    // (sched_barrier) so that the stages stay spread over the MFMAs
+#define D_SEG(G, FG, G0, STG, HH, J0, LIVE)                                                  \
+    do {                                                                                     \
+        const char *base = rs + rdb;                                                         \
+        int xs_ = xsw;                                                                       \
+        asm volatile("" : "+v"(xs_)); /* per-use offsets: not 8 loop-invariant VGPRs */      \
+        i32x4 b0_[KD / 32], b1_[KD / 32];                                                    \
+        QHalf<IK> qh_;                                                                       \
+        _Pragma("unroll") for (int s_ = 0; s_ < KD / 32 + D_PF; s_++) {                      \
+            if (s_ == QS_LOAD) qh_.load((STG), t);                                           \
+            if (s_ == QS_LOAD + 1) qh_.absmax();                                             \
+            if (s_ == QS_LOAD + 2) qh_.sumsq();                                              \
+            if (s_ == QS_LOAD + 3) qh_.reduce((J0) + (t >> 4), n1, tb);                      \
+            if (s_ == QS_LOAD + 4) qh_.pack01();                                             \
+            if (s_ == QS_LOAD + 5) qh_.pack23();                                             \
+            if (s_ == QS_LOAD + 6) qh_.store(rq, (HH), t, (LIVE), st.smax, st.b2max, st.bad); \
+            if (s_ < KD / 32) {                                                              \
+                const int ch_ = ((2 * s_) ^ xs_) * 16;                                       \
+                b0_[s_] = *reinterpret_cast<const i32x4 *>(base + ch_);                      \
+                b1_[s_] = *reinterpret_cast<const i32x4 *>(base + 32 * KD + ch_);            \
+            }                                                                                \
+            if (s_ >= D_PF) {                                                                \
+                const int m_ = s_ - D_PF;                                                    \
+                if (m_ == 0) {                                                               \
+                    if constexpr (IK) {                                                      \
+                        const i32x16 z_ = {};                                                \
+                        acc[G][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][0], b0_[0], z_, 0, 0, 0); \
+                        acc[G][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][0], b1_[0], z_, 0, 0, 0); \
+                    } else {                                                                 \
+                        acc[G][0] = mfma_i8_from4(aI[G][0], b0_[0]);                         \
+                        acc[G][1] = mfma_i8_from4(aI[G][0], b1_[0]);                         \
+                    }                                                                        \
+                } else {                                                                     \
+                    acc[G][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b0_[m_], acc[G][0], 0, 0, 0); \
+                    acc[G][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b1_[m_], acc[G][1], 0, 0, 0); \
+                }                                                                            \
+                D_FOLD2(FG, m_, G0);                                                         \
+            }                                                                                \
+            __builtin_amdgcn_sched_barrier(0);                                               \
+        }                                                                                    \
+    } while (0)
+
+    // Tile t sweeps from ring slot t & 1 while tile t + 1 is quantised into the other slot from
+    // staging halves 2t + 2 (during group 0) and 2t + 3 (during group 1); half 2t + 4 is issued
+    // at the top (into the slot half 2t + 1 left), 2t + 5 at the middle (into the slot half
+    // 2t + 2 left).  Every half thus has one whole tile of latency cover.  In the last
+    // iteration the quantisation runs on stale staging bytes into the unused slot (no DMA is in
+    // flight then, `live` false): branch-free segments, nothing read afterwards.
+    int sA = 2, sB = 0;  // staging slots of halves 2t + 2, 2t + 3
+    for (int tc = 0; tc < ntc; tc++) {
+        if (2 * tc + 3 < nh) {  // half 2t + 2 landed (2t + 3 may be in flight)
+            wait_vm<4>();
+        } else {
+            wait_vm<0>();
+        }
+        D_SYNC();  // tile t complete in its slot; staging slot of half 2t + 1 free
+        const int sN = 3 - sA - sB;  // the third staging slot
+        if (2 * tc + 4 < nh) dma_half(B, 2 * tc + 4, n1, wu, chunk16, lds_base + (unsigned)(sN * D_HALF));
+        const char *rs = ring + (tc & 1) * SLOT;
+        char *rq = ring + ((tc + 1) & 1) * SLOT;
+        const char *stA = lds + sA * D_HALF, *stB = lds + sB * D_HALF;
+        const bool live = tc + 1 < ntc;
+        const unsigned gp_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)max(tc - 1, 0));
+        D_SEG(0, 1, gp_, stA, 0, 32 * (2 * tc + 2), live);
+        if constexpr (IK) {  // the key shifts of tile tc's columns
+            const int *rl_ = reinterpret_cast<const int *>(rs + TILE);
+            sh0 = rl_[fr];
+            sh1 = rl_[fr + 32];
+        } else {  // the dequantisation operands of tile tc: fma(t, 2^21 s, -2^23 s)
+            const float *rl_ = reinterpret_cast<const float *>(rs + TILE);
+            const int col_ = tc * BN + fr;
+            const float s0_ = rl_[fr], s1_ = rl_[fr + 32];
+            pr0 = col_ < n1 ? 2097152.0f * s0_ : 0.f;
+            pr1 = col_ + 32 < n1 ? 2097152.0f * s1_ : 0.f;
+            pc0 = col_ < n1 ? -8388608.0f * s0_ : -3.0e38f;
+            pc1 = col_ + 32 < n1 ? -8388608.0f * s1_ : -3.0e38f;
+        }
+        if (2 * tc + 4 < nh) {  // half 2t + 3 landed (2t + 4 may be in flight)
+            wait_vm<4>();
+        } else {
+            wait_vm<0>();
+        }
+        D_SYNC();  // staging slot of half 2t + 2 consumed
+        if (2 * tc + 5 < nh) dma_half(B, 2 * tc + 5, n1, wu, chunk16, lds_base + (unsigned)(sA * D_HALF));
+        const unsigned gc_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)tc);
+        D_SEG(1, 0, gc_, stB, 1, 32 * (2 * tc + 3), live);
+        // halves 2t + 4, 2t + 5 sit in slots sN, sA
+        const int nA = sN, nB = sA;
+        sA = nA;
+        sB = nB;
+    }
+    {  // group 1 of the last tile
+        const unsigned gl_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)(ntc - 1));
+#pragma unroll
+        for (int s = 0; s < 8; s++) D_FOLD2(1, s, gl_);
+    }
+#undef D_FOLD2
+#undef D_SEG
+    return st;
+}
+
+// The block-wide reduction of the sweep statistics (one barrier; every wave is then past its
+// sweep, so staging + ring are free for the epilogue).
+__device__ __forceinline__ Sweep block_stats(Sweep st, float *misc, int w, int lane) {
+    float smax = fmaxf(st.smax, swz_xor<16>(st.smax));
+    float b2max = fmaxf(st.b2max, swz_xor<16>(st.b2max));
+    smax = fmaxf(smax, __shfl_xor(smax, 32, 64));
+    b2max = fmaxf(b2max, __shfl_xor(b2max, 32, 64));
+    const bool wbad = __ballot(st.bad) != 0;
+    __syncthreads();  // misc may still be read by a previous call
+    if (lane == 0) {
+        misc[4 * w] = smax;
+        misc[4 * w + 1] = b2max;
+        misc[4 * w + 2] = wbad ? 1.f : 0.f;
+    }
+    __syncthreads();
+    Sweep r = {0.f, 0.f, false};
+#pragma unroll
+    for (int k = 0; k < D_NW; k++) {
+        r.smax = fmaxf(r.smax, misc[4 * k]);
+        r.b2max = fmaxf(r.b2max, misc[4 * k + 1]);
+        r.bad = r.bad || misc[4 * k + 2] != 0.f;
+    }
+    return r;
 }
 
 __global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, const int *__restrict__ n0v,
@@ -211,203 +431,57 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, con
     if (row0 >= n0 || n1 <= 0) return;
     const float *A = desc0 + (size_t)pair * cap * KD;
     const float *B = desc1 + (size_t)pair * cap * KD;
-    const int ntc = (n1 + BN - 1) / BN, nh = 2 * ntc;  // column tiles, staging halves (>= 2)
+    const int ntc = (n1 + BN - 1) / BN;
 
     const int wu = __builtin_amdgcn_readfirstlane(w);
     const unsigned chunk16 = (unsigned)(4 * (lane & 15) + (lane >> 4)) * 16;
     const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char *)lds;
-    char *ring = lds + D_OFF_RING;
     float2 *rowv = reinterpret_cast<float2 *>(lds + D_OFF_ROW);
     float *misc = reinterpret_cast<float *>(lds + D_OFF_MISC);
 
-    // ---- prologue: halves 0, 1 in flight beside the A phase; then tile 0 quantised ----
+    // ---- prologue: halves 0, 1 in flight beside the A phase ----
     dma_half(B, 0, n1, wu, chunk16, lds_base);
     dma_half(B, 1, n1, wu, chunk16, lds_base + D_HALF);
-    const int fr = lane & 31, fh = lane >> 5;
     i32x4 aI[RG][KD / 32];
     a_phase<false>(lds + D_OFF_AIMG + w * 32 * KD, rowv, w * 64, row0, n0, lane, A, nullptr, nullptr, nullptr,
                    false, aI);
     D_STAMP(1);
     __syncthreads();  // the A images (staging slot 2 + the ring) are consumed
-    if (nh > 2) {
-        dma_half(B, 2, n1, wu, chunk16, lds_base + 2 * D_HALF);
-        wait_vm<4>();
-    } else {
-        wait_vm<0>();
-    }
-    __syncthreads();  // halves 0, 1 landed
-    float smax = 0.f, b2max = 0.f;
-    bool bad = false;
-    quant_half(lds, ring, 0, 0, n1, t, smax, b2max, bad);
-    quant_half(lds + D_HALF, ring, 1, 32, n1, t, smax, b2max, bad);
-    __syncthreads();  // tile 0 in ring slot 0; staging slots 0, 1 free
-    if (nh > 3) dma_half(B, 3, n1, wu, chunk16, lds_base);
-    D_STAMP(2);
-
-    // B fragment: column block c (0, 1), lane row 32 c + fr, k32 step s: chunk (2 s + fh)
-    const int rdb = fr * KD;
-    const int xsw = fh ^ (fr & 15);  // chunk (2 s + fh) ^ (fr & 15) = 2 s ^ xsw
-
-    // Accumulators start at the bits of 4.0 (q8_common.hpp: mfma_i8_from4): t = 4 + D 2^-21 as
-    // a float, f = fma(t, 2^21 s_j, -2^23 s_j) = RN(D s_j).  Columns past n1 (last tile only)
-    // get s = 0 and the offset -3e38.  The low tb bits of f are then replaced by the column tag
-    // 2 tc + half.
-    i32x16 acc[RG][2];
     float m1[RG][16], m2[RG][16];
-#pragma unroll
-    for (int g = 0; g < RG; g++)
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-            m1[g][q] = -__builtin_inff();
-            m2[g][q] = -__builtin_inff();
-        }
-#pragma unroll
-    for (int q = 0; q < 16; q++) {  // "tile -1" of group 1, folded beside tile 0: never a maximum
-        acc[1][0][q] = 0;
-        acc[1][1][q] = 0;
-    }
-    const int tb = 2 * ntc <= 256 ? 8 : 32 - __builtin_clz(2 * ntc - 1);
-    const unsigned tkeep = ~((1u << tb) - 1u);
-    unsigned vkeep = tkeep;
-    asm volatile("" : "+v"(vkeep));  // a VGPR operand: v_and_or_b32 may read one SGPR only
-    float pr0 = 0.f, pr1 = 0.f, pc0 = -3.0e38f, pc1 = -3.0e38f;  // dequantisation of the tile before
 
-#define D_FOLD2(FG, S, G0)                                                                   \
-    do {                                                                                     \
-        _Pragma("unroll") for (int q = 2 * (S); q < 2 * (S) + 2; q++) {                      \
-            const float a_ = __builtin_fmaf(__int_as_float(acc[FG][0][q]), pr0, pc0);        \
-            const float b_ = __builtin_fmaf(__int_as_float(acc[FG][1][q]), pr1, pc1);        \
-            fold3(tag(a_, vkeep, (G0)), tag(b_, vkeep, (G0) + 1u), m1[FG][q], m2[FG][q]);    \
-        }                                                                                    \
-    } while (0)
-    // group G's MFMAs on the tile at `rs` (fragments read D_PF k32 steps ahead), folding group
-    // FG meanwhile, and this thread's share of the next tile's quantisation from staging STG
-    // into rows 32 HH .. of slot rq (frame-1 rows J0 ..), one stage per k32 step; every step
-    // is fenced (sched_barrier) so that the stages stay spread over the MFMAs
-#define D_SEG(G, FG, G0, STG, HH, J0)                                                        \
-    do {                                                                                     \
-        const char *base = rs + rdb;                                                         \
-        int xs_ = xsw;                                                                       \
-        asm volatile("" : "+v"(xs_)); /* per-use offsets: not 8 loop-invariant VGPRs */      \
-        i32x4 b0_[KD / 32], b1_[KD / 32];                                                    \
-        QHalf qh_;                                                                           \
-        _Pragma("unroll") for (int s_ = 0; s_ < KD / 32 + D_PF; s_++) {                      \
-            if (D_EXP_NOQ) {} else if (s_ == QS_LOAD) qh_.load((STG), t);                    \
-            if (!D_EXP_NOQ && s_ == QS_LOAD + 1) qh_.absmax();                                             \
-            if (!D_EXP_NOQ && s_ == QS_LOAD + 2) qh_.sumsq();                                              \
-            if (!D_EXP_NOQ && s_ == QS_LOAD + 3) qh_.reduce();                                             \
-            if (!D_EXP_NOQ && s_ == QS_LOAD + 4) qh_.pack01();                                             \
-            if (!D_EXP_NOQ && s_ == QS_LOAD + 5) qh_.pack23();                                             \
-            if (!D_EXP_NOQ && s_ == QS_LOAD + 6) qh_.store(rq, (HH), (J0), n1, t, smax, b2max, bad);       \
-            if (s_ < KD / 32) {                                                              \
-                const int ch_ = ((2 * s_) ^ xs_) * 16;                                       \
-                b0_[s_] = *reinterpret_cast<const i32x4 *>(base + ch_);                      \
-                b1_[s_] = *reinterpret_cast<const i32x4 *>(base + 32 * KD + ch_);            \
-            }                                                                                \
-            if (s_ >= D_PF) {                                                                \
-                const int m_ = s_ - D_PF;                                                    \
-                if (m_ == 0) {                                                               \
-                    acc[G][0] = mfma_i8_from4(aI[G][0], b0_[0]);                             \
-                    acc[G][1] = mfma_i8_from4(aI[G][0], b1_[0]);                             \
-                } else {                                                                     \
-                    acc[G][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b0_[m_], acc[G][0], 0, 0, 0); \
-                    acc[G][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b1_[m_], acc[G][1], 0, 0, 0); \
-                }                                                                            \
-                D_FOLD2(FG, m_, G0);                                                         \
-            }                                                                                \
-            __builtin_amdgcn_sched_barrier(0);                                               \
-        }                                                                                    \
-    } while (0)
-
-    // Tile t sweeps from ring slot t & 1 while tile t + 1 is quantised into the other slot from
-    // staging halves 2t + 2 (slot (2t + 2) % 3, during group 0) and 2t + 3 (during group 1);
-    // half 2t + 4 is issued at the top (into the slot half 2t + 1 left), 2t + 5 at the middle
-    // (into the slot half 2t + 2 left).  Every half thus has one whole tile of latency cover.
-    // In the last iteration the quantisation runs on stale staging bytes into the unused slot
-    // (no DMA is in flight then): branch-free segments, nothing read afterwards.
-    int sA = 2, sB = 0;  // staging slots of halves 2t + 2, 2t + 3
-    for (int tc = 0; tc < ntc; tc++) {
-        if (2 * tc + 3 < nh) {  // half 2t + 2 landed (2t + 3 may be in flight)
-            D_WAITVM(4);
-        } else {
-            D_WAITVM(0);
-        }
-        D_SYNC();  // tile t complete in its slot; staging slot of half 2t + 1 free
-        const int sN = 3 - sA - sB;  // the third staging slot
-        if (!D_EXP_NODMA && 2 * tc + 4 < nh) dma_half(B, 2 * tc + 4, n1, wu, chunk16, lds_base + (unsigned)(sN * D_HALF));
-        const char *rs = ring + (tc & 1) * SLOT;
-        char *rq = ring + ((tc + 1) & 1) * SLOT;
-        const char *stA = lds + sA * D_HALF, *stB = lds + sB * D_HALF;
-        const unsigned gp_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)max(tc - 1, 0));
-        D_SEG(0, 1, gp_, stA, 0, 32 * (2 * tc + 2));
-        {  // the dequantisation operands of tile tc: fma(t, 2^21 s, -2^23 s)
-            const float *rl_ = reinterpret_cast<const float *>(rs + TILE);
-            const int col_ = tc * BN + fr;
-            const float s0_ = rl_[fr], s1_ = rl_[fr + 32];
-            pr0 = col_ < n1 ? 2097152.0f * s0_ : 0.f;
-            pr1 = col_ + 32 < n1 ? 2097152.0f * s1_ : 0.f;
-            pc0 = col_ < n1 ? -8388608.0f * s0_ : -3.0e38f;
-            pc1 = col_ + 32 < n1 ? -8388608.0f * s1_ : -3.0e38f;
-        }
-        if (2 * tc + 4 < nh) {  // half 2t + 3 landed (2t + 4 may be in flight)
-            D_WAITVM(4);
-        } else {
-            D_WAITVM(0);
-        }
-        D_SYNC();  // staging slot of half 2t + 2 consumed
-        if (!D_EXP_NODMA && 2 * tc + 5 < nh) dma_half(B, 2 * tc + 5, n1, wu, chunk16, lds_base + (unsigned)(sA * D_HALF));
-        const unsigned gc_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)tc);
-        D_SEG(1, 0, gc_, stB, 1, 32 * (2 * tc + 3));
-        // halves 2t + 4, 2t + 5 sit in slots sN, sA
-        const int nA = sN, nB = sA;
-        sA = nA;
-        sB = nB;
-    }
-    {  // group 1 of the last tile
-        const unsigned gl_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)(ntc - 1));
-#pragma unroll
-        for (int s = 0; s < 8; s++) D_FOLD2(1, s, gl_);
-    }
-#undef D_FOLD2
-#undef D_SEG
-
-    D_STAMP(3);
-    // ---- the pair's frame-1 statistics (every workgroup of the pair computes the same) ----
-    smax = fmaxf(smax, swz_xor<16>(smax));
-    b2max = fmaxf(b2max, swz_xor<16>(b2max));
-    smax = fmaxf(smax, __shfl_xor(smax, 32, 64));
-    b2max = fmaxf(b2max, __shfl_xor(b2max, 32, 64));
-    const bool wbad = __ballot(bad) != 0;
-    if (lane == 0) {
-        misc[4 * w] = smax;
-        misc[4 * w + 1] = b2max;
-        misc[4 * w + 2] = wbad ? 1.f : 0.f;
-    }
-    __syncthreads();  // also: every wave is past its sweep (staging + ring free for the epilogue)
-    float S = 0.f, B2 = 0.f;
-    bool flagged = false;
-#pragma unroll
-    for (int k = 0; k < D_NW; k++) {
-        S = fmaxf(S, misc[4 * k]);
-        B2 = fmaxf(B2, misc[4 * k + 1]);
-        flagged = flagged || misc[4 * k + 2] != 0.f;
-    }
-    const double Bn = sqrt((double)B2) * 1.0001;
-    const double Eb = (8.001 * (double)S + 4.76837158203125e-07 * Bn) * 1.0001 + 1e-30;
-    D_STAMP(4);
-    epilogue<D_NW>(lds, rowv, m1, m2, Bn, Eb, flagged, tb, tkeep, w, lane, row0, n0, n1, A, B, oidx, oscore, thresh,
-                   dmode);
+    // the integer-key sweep; tag width: keys (D << (tb + 2)) | tag must fit 31 bits
+    const int tbi = 2 * ntc <= 2 ? 1 : 32 - __builtin_clz(2 * ntc - 1);
+    if (tbi <= 7) {
+        const Sweep st = block_stats(sweep<true>(lds, B, n1, t, lane, wu, chunk16, lds_base, aI, m1, m2, tbi,
+                                                 ~((1u << tbi) - 1u), true), misc, w, lane);
+        D_STAMP(2);
+        if (!st.bad) {
+            const double Bn = sqrt((double)st.b2max) * 1.0001;
+            const double Eb = 8.0001 * (double)st.smax + 1e-30;  // exact power-of-two scaling
+            epilogue<D_NW, true>(lds, rowv, m1, m2, Bn, Eb, false, tbi, ~((1u << tbi) - 1u), w, lane, row0, n0,
+                                 n1, A, B, oidx, oscore, thresh, dmode, 1.0 / 508.0);
+            D_STAMP(3);
 #ifdef MV_TRACE
-    D_STAMP(5);
-    if (lane == 0 && blockIdx.x < D_TRACE_BLOCKS) {
-        unsigned long long *o = g_d_trace + ((size_t)blockIdx.x * D_NW + w) * 10;
-        for (int k = 0; k < 6; k++) o[k] = ts_[k];
-        o[6] = __smid();
-        o[7] = __builtin_amdgcn_s_memrealtime();
-        o[8] = ts_[8];
-        o[9] = ts_[9];
-    }
+            if (lane == 0 && blockIdx.x < D_TRACE_BLOCKS) {
+                unsigned long long *o = g_d_trace + ((size_t)blockIdx.x * D_NW + w) * 10;
+                for (int k = 0; k < 4; k++) o[k] = ts_[k];
+                o[6] = __smid();
+                o[7] = __builtin_amdgcn_s_memrealtime();
+                o[9] = ts_[9];
+            }
 #endif
+            return;
+        }
+    }
+    // the float path: a column outside the integer keys' range, a non-finite value, or too many
+    // column tiles for the key width
+    const int tb = 2 * ntc <= 256 ? 8 : 32 - __builtin_clz(2 * ntc - 1);
+    const Sweep st = block_stats(sweep<false>(lds, B, n1, t, lane, wu, chunk16, lds_base, aI, m1, m2, tb,
+                                              ~((1u << tb) - 1u), tbi > 7), misc, w, lane);
+    const double Bn = sqrt((double)st.b2max) * 1.0001;
+    const double Eb = (8.001 * (double)st.smax + 4.76837158203125e-07 * Bn) * 1.0001 + 1e-30;
+    epilogue<D_NW, false>(lds, rowv, m1, m2, Bn, Eb, st.bad, tb, ~((1u << tb) - 1u), w, lane, row0, n0, n1, A, B,
+                          oidx, oscore, thresh, dmode);
 }
 
 }  // namespace

@@ -254,17 +254,32 @@ __device__ __forceinline__ void a_phase(char *img, float2 *rowv, int rbase, int 
 //      rare wide rows are re-scored by the whole wave.  epi = the block's epilogue LDS
 //      (epi_bytes<NW>()), free of every other use.  Bn, Eb: upper bounds of max |b_j| and
 //      max |eps_j| over the pair's columns; flagged: every row of the pair takes the exact
-//      path.  tb, tkeep: the tag width and mask of the sweep. ----
-template <int NW>
+//      path.  tb, tkeep: the tag width and mask of the sweep.
+//      IK = false: m1/m2 hold tagged float screen values (the tag moves a value by < 2^(tb-23)
+//      relative: the rho term), a column's real screen = value * s_a.  IK = true: they hold the
+//      bits of exact integer keys (D_eff << tb) | tag, real screen = (key >> tb) * s_a * bscale;
+//      padding columns (index >= n1, zero codes) are excluded by index. ----
+template <int NW, bool IK = false>
 __device__ __forceinline__ void epilogue(char *epi, const float2 *rowv, float (&m1)[RG][16], float (&m2)[RG][16],
                                          double Bn, double Eb, bool flagged, int tb, unsigned tkeep, int w, int lane,
                                          int row0, int n0, int n1, const float *__restrict__ A,
                                          const float *__restrict__ B, int *__restrict__ oidx,
-                                         float *__restrict__ oscore, double thresh, int dmode) {
+                                         float *__restrict__ oscore, double thresh, int dmode, double bscale = 1.0) {
     const int fr = lane & 31, fh = lane >> 5;
     const double u24 = 5.9604644775390625e-08;
     const double gam_e = KD * u24 / (1.0 - KD * u24);
-    const double rho = ldexp(1.0, tb - 23);
+    const double rho = IK ? 0.0 : ldexp(1.0, tb - 23);
+    // key order and value: float compares of the tagged screen values, or signed-int compares of
+    // the key bits
+    auto kgt = [](float a, float b) { return IK ? __float_as_int(a) > __float_as_int(b) : a > b; };
+    auto kmax = [&](float a, float b) { return kgt(a, b) ? a : b; };
+    auto kmin = [&](float a, float b) { return kgt(a, b) ? b : a; };
+    auto kval = [&](float a) { return IK ? (double)(__float_as_int(a) >> tb) : (double)a; };
+    const float kneg = IK ? __int_as_float((int)0x80000000) : -__builtin_inff();
+    auto kcol = [&](float a, int lanecol) {  // the column of a tagged value held by lane column lanecol
+        const unsigned tg = __float_as_uint(a) & ~tkeep;
+        return (int)(tg >> 1) * BN + (int)(tg & 1) * 32 + lanecol;
+    };
     // dmode 1: distinct dots can round to one distance: columns within TIE of the maximiser's
     // exact dot are competitors (a distance tie needs |d1 - d2| of a few ulp)
     const double tie = dmode ? 1e-5 : 0.0;
@@ -291,20 +306,20 @@ __device__ __forceinline__ void epilogue(char *epi, const float2 *rowv, float (&
             e1[2 * i + 1] = v.z;
             e2[2 * i + 1] = v.w;
         }
-        float M = -__builtin_inff(), M2 = -__builtin_inff();
+        float M = kneg, M2 = kneg;
         int E = 0;
 #pragma unroll
         for (int i = 0; i < 16; i++) {  // equal maxima land in M2: ambiguous
-            M2 = fmaxf(fmaxf(M2, e2[i]), fminf(M, e1[i]));
-            E = e1[i] > M ? fh * 16 + i : E;
-            M = fmaxf(M, e1[i]);
+            M2 = kmax(kmax(M2, e2[i]), kmin(M, e1[i]));
+            E = kgt(e1[i], M) ? fh * 16 + i : E;
+            M = kmax(M, e1[i]);
         }
         {
             const float oM = __shfl_xor(M, 32, 64), oM2 = __shfl_xor(M2, 32, 64);
             const int oE = __shfl_xor(E, 32, 64);
-            M2 = fmaxf(fmaxf(M2, oM2), fminf(M, oM));
-            E = (oM > M || (oM == M && oE < E)) ? oE : E;
-            M = fmaxf(M, oM);
+            M2 = kmax(kmax(M2, oM2), kmin(M, oM));
+            E = (kgt(oM, M) || (!kgt(M, oM) && oE < E)) ? oE : E;
+            M = kmax(M, oM);
         }
         // the mt region is rewritten by the next group: its reads must have completed
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
@@ -324,8 +339,9 @@ __device__ __forceinline__ void epilogue(char *epi, const float2 *rowv, float (&
             const double ea = 8.001 * s_a + 4.76837158203125e-07 * an;  // |1 - q s_a| < 2^-21
             const double dq = (an * Eb + ea * Bn + ea * Eb) * 1.0001;
             const double delta = dq + u24 * (an * Bn + dq) * 1.01 + gam_e * an * Bn + 1e-30;
-            const double Ms = (double)M * s_a;
-            const double M2s = M2 > -__builtin_inff() ? (double)M2 * s_a : -__builtin_inf();
+            const double sa_k = s_a * bscale;  // screen units -> units of a.b
+            const double Ms = kval(M) * sa_k;
+            const double M2s = kgt(M2, kneg) ? kval(M2) * sa_k : -__builtin_inf();
             const double dp = delta + 2.2 * rho * (fabs(Ms) + 2.0 * delta);
             // competitors: columns whose exact score can reach the maximiser's; for the distance
             // (dmode 1) also every column that can clip to 1 with it (distance-0 ties), and a
@@ -336,9 +352,8 @@ __device__ __forceinline__ void epilogue(char *epi, const float2 *rowv, float (&
                 if (fh == 0) lmask[rl] = 0xffffffffu;
             } else if (Ms + dp > thresh) {
                 if (M2s < lo) {
-                    const unsigned tg = __float_as_uint(M) & ~tkeep;
-                    const int I = (int)(tg >> 1) * BN + (int)(tg & 1) * 32 + E;
-                    if (I >= n1) {  // cannot happen for a tagged in-range maximum; never read past n1
+                    const int I = kcol(M, E);
+                    if (I >= n1) {  // a padding column on top (IK: all real dots below 0); never read past n1
                         wide = true;
                         if (fh == 0) lmask[rl] = 0xffffffffu;
                     } else if (fh == 0) {
@@ -354,13 +369,15 @@ __device__ __forceinline__ void epilogue(char *epi, const float2 *rowv, float (&
                         bj = I;
                     }
                 } else {  // both lanes of the row take this branch
-                    const double lim = lo / s_a;  // in screen units
-                    const float pad_hi = -1.0e38f;  // padding columns (past n1) are never candidates
+                    const double lim = lo / sa_k;  // in screen units
+                    const float pad_hi = -1.0e38f;  // float: padding columns (past n1) sit at -3e38
                     unsigned in1 = 0, in2 = 0;
 #pragma unroll
-                    for (int i = 0; i < 16; i++) {
-                        in1 |= ((double)e1[i] >= lim && e1[i] > pad_hi ? 1u : 0u) << i;
-                        in2 |= ((double)e2[i] >= lim && e2[i] > pad_hi ? 1u : 0u) << i;
+                    for (int i = 0; i < 16; i++) {  // padding columns (past n1) are never candidates
+                        in1 |= (kval(e1[i]) >= lim && (IK || e1[i] > pad_hi) && kcol(e1[i], fh * 16 + i) < n1 ? 1u : 0u)
+                               << i;
+                        in2 |= (kval(e2[i]) >= lim && (IK || e2[i] > pad_hi) && kcol(e2[i], fh * 16 + i) < n1 ? 1u : 0u)
+                               << i;
                     }
                     const unsigned o1 = __shfl_xor(in1, 32, 64), o2 = __shfl_xor(in2, 32, 64);
                     const unsigned inside = fh ? (o1 | (in1 << 16)) : (in1 | (o1 << 16));
@@ -371,10 +388,7 @@ __device__ __forceinline__ void epilogue(char *epi, const float2 *rowv, float (&
                         int k = fh ? __popc(o1) : 0;
 #pragma unroll
                         for (int i = 0; i < 16; i++)
-                            if ((in1 >> i) & 1u) {
-                                const unsigned tg = __float_as_uint(e1[i]) & ~tkeep;
-                                clist[rl * NCAND + k++] = (int)(tg >> 1) * BN + (int)(tg & 1) * 32 + fh * 16 + i;
-                            }
+                            if ((in1 >> i) & 1u) clist[rl * NCAND + k++] = kcol(e1[i], fh * 16 + i);
                         const int nc = __popc(inside);
                         for (int c = fh; c < nc; c += 2) {  // the row's two lanes split the list
                             const int j = clist[rl * NCAND + c];
