@@ -64,7 +64,10 @@ int mv_device_count(void);              /* 0 when no HIP device is visible */
 
 int mv_context_create(int device, mv_context **out);
 int mv_context_destroy(mv_context *ctx);
-int mv_context_set_stream(mv_context *ctx, void *hip_stream); /* NULL: the context's own stream */
+/* Every later call runs on `hip_stream`; NULL is HIP's null (legacy default) stream, which is
+ * what torch.cuda.current_stream() is until another stream is made current. */
+int mv_context_set_stream(mv_context *ctx, void *hip_stream);
+int mv_context_use_own_stream(mv_context *ctx); /* back to the context's own non-blocking stream */
 void *mv_context_stream(mv_context *ctx);
 int mv_context_synchronize(mv_context *ctx);
 /* Pre-size scratch for up to `batch` pairs of `cap` keypoints / cells. */

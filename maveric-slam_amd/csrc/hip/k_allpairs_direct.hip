@@ -53,6 +53,9 @@ static_assert(epi_bytes<D_NW>() <= D_OFF_ROW, "the epilogue fits staging + ring"
 static_assert(D_LDS <= 160 * 1024, "one workgroup per CU");
 constexpr int D_PF = 1;       // k32 steps of B fragments read ahead of the MFMAs
 constexpr int QS_LOAD = 1;    // the k32 step whose slot issues the quantisation's staging reads
+#ifndef D_QB
+#define D_QB 4  // A phase: frame-0 row quads in flight per wave (4 x 16-B loads per lane each)
+#endif
 constexpr float IK_MMAX = 1.003f;  // integer path: max |b_jk| allowed (RNE(x 127) stays <= 127)
 
 #ifdef MV_TRACE  // phase stamps (s_memtime) per (block, wave): tools/trace_direct.py
@@ -85,12 +88,20 @@ __device__ __forceinline__ void row16_max_sum(float &m, float &q2) {
         "s_nop 1"
         : "+v"(m), "+v"(q2));
 }
-// the top-2 fold on integer keys held in float registers' bits (as fold3 on floats)
-__device__ __forceinline__ void fold3i(int a, int b, float &m1f, float &m2f) {
-    int md, m1 = __float_as_int(m1f), m2 = __float_as_int(m2f);
-    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(md) : "v"(m1), "v"(a), "v"(b));
-    asm("v_max3_i32 %0, %1, %2, %3" : "=v"(m1) : "v"(m1), "v"(a), "v"(b));
-    asm("v_max_i32 %0, %1, %2" : "=v"(m2) : "v"(m2), "v"(md));
+// two values of one row folded into its lane-local top-2 on integer keys (held in float
+// registers' bits): the keys (d << sh) | tag by v_lshl_or_b32 (shift per lane in a VGPR, tag in
+// an SGPR), m1' = max3(m1, ka, kb), m2' = max(m2, med3(m1, ka, kb)) -- one asm block, so that
+// no hazard padding is placed between its dependent instructions
+__device__ __forceinline__ void fold_keys(int a, int b, int sha, int shb, unsigned ta, unsigned tb, float &m1f,
+                                          float &m2f) {
+    int ka, kb, md, m1 = __float_as_int(m1f), m2 = __float_as_int(m2f);
+    asm("v_lshl_or_b32 %0, %5, %7, %9\n\t"
+        "v_lshl_or_b32 %1, %6, %8, %10\n\t"
+        "v_med3_i32 %2, %3, %0, %1\n\t"
+        "v_max3_i32 %3, %3, %0, %1\n\t"
+        "v_max_i32 %4, %4, %2"
+        : "=&v"(ka), "=&v"(kb), "=&v"(md), "+v"(m1), "+v"(m2)
+        : "v"(a), "v"(b), "v"(sha), "v"(shb), "s"(ta), "s"(tb));
     m1f = __int_as_float(m1);
     m2f = __int_as_float(m2);
 }
@@ -269,9 +280,7 @@ __device__ __forceinline__ Sweep sweep(char *lds, const float *B, int n1, int t,
         _Pragma("unroll") for (int q = 2 * (S); q < 2 * (S) + 2; q++) {                      \
             if constexpr (IK) {                                                              \
                 /* v_lshl_or_b32 keys; v_max3_i32 / v_med3_i32 / v_max_i32 top-2 */          \
-                const int ka_ = (int)(((unsigned)acc[FG][0][q] << sh0) | (G0));              \
-                const int kb_ = (int)(((unsigned)acc[FG][1][q] << sh1) | ((G0) + 1u));       \
-                fold3i(ka_, kb_, m1[FG][q], m2[FG][q]);                                      \
+                fold_keys(acc[FG][0][q], acc[FG][1][q], sh0, sh1, (G0), (G0) + 1u, m1[FG][q], m2[FG][q]); \
             } else {                                                                         \
                 const float a_ = __builtin_fmaf(__int_as_float(acc[FG][0][q]), pr0, pc0);    \
                 const float b_ = __builtin_fmaf(__int_as_float(acc[FG][1][q]), pr1, pc1);    \
@@ -443,8 +452,8 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, con
     dma_half(B, 0, n1, wu, chunk16, lds_base);
     dma_half(B, 1, n1, wu, chunk16, lds_base + D_HALF);
     i32x4 aI[RG][KD / 32];
-    a_phase<false>(lds + D_OFF_AIMG + w * 32 * KD, rowv, w * 64, row0, n0, lane, A, nullptr, nullptr, nullptr,
-                   false, aI);
+    a_phase<false, D_QB>(lds + D_OFF_AIMG + w * 32 * KD, rowv, w * 64, row0, n0, lane, A, nullptr, nullptr, nullptr,
+                         false, aI);
     D_STAMP(1);
     __syncthreads();  // the A images (staging slot 2 + the ring) are consumed
     float m1[RG][16], m2[RG][16];

@@ -166,12 +166,18 @@ int mv_context_destroy(mv_context *ctx) {
 
 int mv_context_set_stream(mv_context *ctx, void *s) {
     MV_REQUIRE(ctx != nullptr);
-    ctx->stream = s ? (hipStream_t)s : ctx->own_stream;
+    ctx->stream = (hipStream_t)s;  // NULL is HIP's null stream (torch's default stream), not "unset"
     if (ctx->stream != ctx->own_stream) {  // remembered for quiesce()
         bool seen = false;
         for (int i = 0; i < ctx->n_used_streams && i < 4; i++) seen = seen || ctx->used_streams[i] == ctx->stream;
         if (!seen) ctx->used_streams[ctx->n_used_streams++ % 4] = ctx->stream;
     }
+    return MV_OK;
+}
+
+int mv_context_use_own_stream(mv_context *ctx) {
+    MV_REQUIRE(ctx != nullptr);
+    ctx->stream = ctx->own_stream;
     return MV_OK;
 }
 

@@ -167,12 +167,11 @@ __device__ __forceinline__ bool better(int dmode, float v, int j, float bv, int 
 //      rowv[r] = (|a|^2, s_a); s_a < 0 marks a row for the exact path (non-finite, zero or out
 //      of range).  AI8 (sequence mode): the rows arrive already quantised by k_q8_split (q0,
 //      s0, |a|^2, pair flag bad0) and are copied (256 B per row). ----
-template <bool AI8>
+template <bool AI8, int QB = 4>  // QB: row quads (4 loads per lane each) in flight
 __device__ __forceinline__ void a_phase(char *img, float2 *rowv, int rbase, int row0, int n0, int lane,
                                         const float *__restrict__ A, const char *__restrict__ QA,
                                         const float *__restrict__ s0p, const float *__restrict__ na2p, bool bad0,
                                         i32x4 (&aI)[RG][KD / 32]) {
-    constexpr int QB = 4;  // row quads (4 loads per lane each) in flight
     const int fr = lane & 31, fh = lane >> 5;
     const int sub = lane & 15, rq = lane >> 4;
 #pragma unroll

@@ -93,6 +93,7 @@ def lib():
             "mv_context_create": (_I, [_I, ctypes.POINTER(_P)]),
             "mv_context_destroy": (_I, [_P]),
             "mv_context_set_stream": (_I, [_P, _P]),
+            "mv_context_use_own_stream": (_I, [_P]),
             "mv_context_set_allpairs_screen": (_I, [_P, _I]),
             "mv_context_allpairs_screen": (_I, [_P]),
             "mv_context_stream": (_P, [_P]),
@@ -406,8 +407,12 @@ class Context:
             pass
 
     def set_stream(self, stream):
-        ptr = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
-        check(lib().mv_context_set_stream(self.h, ptr), "set_stream")
+        """Run later calls on `stream` (a torch.cuda.Stream -- torch's default stream is HIP's null
+        stream, handle 0, and is used as such); None: back to the context's own stream."""
+        if stream is None:
+            check(lib().mv_context_use_own_stream(self.h), "use_own_stream")
+        else:
+            check(lib().mv_context_set_stream(self.h, ctypes.c_void_p(stream.cuda_stream)), "set_stream")
 
     def set_allpairs_screen(self, screen):
         """'i8' (default: one pass, frame 1 quantised in-kernel), 'f16' or 'i8s' (int8 against a
