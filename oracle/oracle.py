@@ -73,6 +73,12 @@ def lib():
         L.orc_window_score.argtypes = [_I, _I, _I]
         L.orc_window_pass.restype = _I
         L.orc_window_pass.argtypes = [_F]
+        L.orc_sp_resize.argtypes = [_P, _I, _I, _I, _I, _P]
+        L.orc_sp_quantize.argtypes = [_P, ctypes.c_long, _D, _P]
+        L.orc_sp_conv.argtypes = [_P, _I, _I, _P, _D, _I, _I, _P]
+        L.orc_sp_min_gap.restype = _F
+        L.orc_sp_min_gap.argtypes = [_P, _I, _I, _I, _D, _P]
+        L.orc_sp_forward.argtypes = [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]
         _lib = L
     return _lib
 
@@ -445,3 +451,78 @@ def ref_pool_replay(id_lists):
     sz = np.zeros(len(id_lists), np.int32)
     done = R.ref_pool_replay(len(id_lists), _ptr(n), _ptr(flat), _ptr(tab), _ptr(sz))
     return tab, sz, done
+
+
+# ---------------- quantized SuperPoint front-end (sp_oracle.c) ----------------
+SP_LAYERS = ("conv1a", "conv1b", "conv2a", "conv2b", "conv3a", "conv3b", "conv4a", "conv4b",
+             "convPa", "convPb", "convDa", "convDb")
+
+
+class SpLayer(ctypes.Structure):
+    _fields_ = [("w", _P), ("bias", _P), ("cin", _I), ("cout", _I), ("k", _I), ("w_scale", _D), ("out_scale", _D)]
+
+
+class SpNet(ctypes.Structure):
+    _fields_ = [("in_scale", _D), ("layer", SpLayer * 12)]
+
+
+def sp_net(weights):
+    """ctypes net from a weights dict (tests/golden/superpoint_qnonorm.npz layout: <layer>_w,
+    <layer>_bias, <layer>_meta = [w_scale, w_zp, out_scale, out_zp], input_scale); the arrays
+    are kept alive on the returned object"""
+    net = SpNet()
+    net.in_scale = float(weights["input_scale"])
+    keep = []
+    for i, n in enumerate(SP_LAYERS):
+        w = np.ascontiguousarray(weights[n + "_w"], np.int8)
+        b = np.ascontiguousarray(weights[n + "_bias"], np.float32)
+        meta = weights[n + "_meta"]
+        if meta[1] != 0 or meta[3] != 0:
+            raise ValueError("zero points other than 0 are not restated")
+        keep += [w, b]
+        L = net.layer[i]
+        L.w, L.bias = w.ctypes.data, b.ctypes.data
+        L.cout, L.cin, L.k = w.shape[0], w.shape[1], w.shape[2]
+        L.w_scale, L.out_scale = float(meta[0]), float(meta[2])
+    net._keep = keep
+    return net
+
+
+def sp_resize(img, oh=192, ow=640):
+    img = np.ascontiguousarray(img, np.uint8)
+    out = np.zeros((oh, ow), np.float32)
+    lib().orc_sp_resize(_ptr(img), img.shape[0], img.shape[1], oh, ow, _ptr(out))
+    return out
+
+
+def sp_quantize(x, scale):
+    x = np.ascontiguousarray(x, np.float32)
+    q = np.zeros(x.shape, np.int8)
+    lib().orc_sp_quantize(_ptr(x), x.size, float(scale), _ptr(q))
+    return q
+
+
+def sp_conv(x, net, i, in_scale, relu, pool):
+    """layer i of the net on CHW int8 x"""
+    x = np.ascontiguousarray(x, np.int8)
+    c, h, w = x.shape
+    L = net.layer[i]
+    out = np.zeros((L.cout, h // 2, w // 2) if pool else (L.cout, h, w), np.int8)
+    lib().orc_sp_conv(_ptr(x), h, w, ctypes.byref(L), float(in_scale), int(relu), int(pool), _ptr(out))
+    return out
+
+
+def sp_forward(img, net, oh=192, ow=640):
+    """(semi [cells][65], desc [cells][256], semi_scale, desc_scale, semi_raw, desc_raw)"""
+    img = np.ascontiguousarray(img, np.uint8)
+    cells = (oh // 8) * (ow // 8)
+    semi = np.zeros((cells, 65), np.int8)
+    desc = np.zeros((cells, 256), np.int8)
+    sr = np.zeros((65, oh // 8, ow // 8), np.int8)
+    dr = np.zeros((256, oh // 8, ow // 8), np.int8)
+    ss, ds = ctypes.c_float(), ctypes.c_float()
+    r = lib().orc_sp_forward(_ptr(img), img.shape[0], img.shape[1], oh, ow, ctypes.byref(net), _ptr(semi), _ptr(desc),
+                             ctypes.byref(ss), ctypes.byref(ds), _ptr(sr), _ptr(dr))
+    if r != 0:
+        raise ValueError("orc_sp_forward: %d" % r)
+    return semi, desc, np.float32(ss.value), np.float32(ds.value), sr, dr
