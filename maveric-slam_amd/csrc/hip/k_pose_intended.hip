@@ -11,20 +11,20 @@
 //      hypotheses are MSAC-scored (sum of min(Sampson^2, (thr_px / f)^2)) on an evenly
 //      strided subset of 128 correspondences (LDS broadcast reads);
 //   3. preemption: the 2 best of each wave survive and are MSAC-scored on ALL
-//      correspondences by the whole block; lowest (cost, hypothesis id) -> E;
-//   4. E = U diag(s1,s2,s3) V^T (closed-form eigenvectors of E^T E), the four (R, t)
-//      candidates R = U W V^T / U W^T V^T, t = +-u3, cheirality vote by
-//      triangulated depth over the inliers (block reduction);
-//   5. Gauss-Newton: residual r_i = (x2^T [t]x R x1) / s_i (Sampson), inliers
-//      re-selected each iteration at min(thr, 3 rms) so outliers that fell inside
-//      the RANSAC band drop out (exact data converges to machine precision),
-//      per-correspondence Jacobian d r / d(omega, tangent(t)) (5 dof),
-//      J^T J and J^T r assembled with wave64 shuffle reductions + LDS
-//      (the [J|r]^T[J|r] pattern of src/local_bundle_adjustment.c:161-176),
-//      5x5 LM-damped Cholesky solve in one lane, R <- exp(omega) R,
-//      t <- normalise(t + B d).  The Gauss-Newton state, the per-correspondence terms, the
-//      22 sums and the solve are float (the output is float).  Stops early once the step is below 1e-7 and the
-//      inlier band is unchanged (refine_iters is the maximum).
+//      correspondences by the whole block; the two lowest (cost, hypothesis id) are the
+//      two starts, one per half of the block (waves 0-1 and 2-3);
+//   4. per start: E = U diag(s1,s2,s3) V^T (closed-form eigenvectors of E^T E), the four
+//      (R, t) candidates R = U W V^T / U W^T V^T, t = +-u3, cheirality vote by triangulated
+//      depth over the inliers;
+//   5. per start: robust Gauss-Newton (IRLS) on the Sampson residuals r_i =
+//      (x2^T [t]x R x1) / s_i with Cauchy weights whose scale shrinks from thr towards
+//      2 rms (exact data converges to machine precision, noisy data keeps ~2 sigma),
+//      per-correspondence Jacobian d r / d(omega, tangent(t)) (5 dof), J^T W J and
+//      J^T W r assembled with wave64 reductions + LDS (the [J|r]^T[J|r] pattern of
+//      src/local_bundle_adjustment.c:161-176), 5x5 Cholesky solve, R <- exp(omega) R,
+//      t <- normalise(t + B d); float throughout (the output is float); stops once the
+//      step is below 1e-6 and the scale settles (refine_iters is the maximum);
+//   6. the refined pose with the lower robust cost (Cauchy at thr, capped at 3 thr) wins.
 // Output T = [R | t] with x1 ~ R x0 + t, |t| = 1 (the OpenCV recoverPose convention).
 #include <math.h>
 
@@ -40,12 +40,6 @@ namespace {
 
 constexpr int NT = 256;
 // timing experiments only (wrong results): skip the GN per-point pass / reduction / solve
-#ifndef PE_NOPOINTS
-#define PE_NOPOINTS 0
-#endif
-#ifndef PE_NORED
-#define PE_NORED 0
-#endif
 #ifndef PE_TRACE
 #define PE_TRACE 0  // printf per-phase clock64() deltas of block 0 (timing experiments only)
 #endif
@@ -60,9 +54,6 @@ constexpr int NT = 256;
 #endif
 #ifndef PE_WAVES
 #define PE_WAVES 4  // waves per SIMD (4: 128 VGPRs, 13 spilled, 3% faster than 3 at 142)
-#endif
-#ifndef PE_NOSOLVE
-#define PE_NOSOLVE 0
 #endif
 constexpr int MAXP = 4096;  // correspondences per pair held in LDS (float4 each)
 
@@ -385,15 +376,6 @@ __device__ __forceinline__ float gn_reduce_scatter22(const float (&acc)[22], int
     return f;
 }
 
-__device__ __forceinline__ int block_sum_i(int v, int *red) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    return red[0] + red[1] + red[2] + red[3];
-}
-
 struct PoseArgs {
     int cap;
     float fx, fy, cx, cy;
@@ -412,9 +394,6 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
                                                     int *__restrict__ status) {
     extern __shared__ __attribute__((aligned(16))) float4 P[];  // [min(cap, MAXP)]
     __shared__ int wsum[4];
-    __shared__ int s_best[2];
-    __shared__ float s_E[9];
-    __shared__ float s_pose[12];  // R (9) + t (3)
     const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int n_in = min(max(nv[b], 0), a.cap);
     const long long tk0 = PE_TRACE ? clock64() : 0;
@@ -634,24 +613,40 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
         }
     }
     __syncthreads();
+    // ---- 3b. the two lowest (full cost, hypothesis id) survivors are both refined, one per
+    //         half of the block (waves 0-1, 2-3), and the refined pose with the lower robust
+    //         cost wins.  Under pixel noise one start is not enough: the robust cost has local
+    //         minima along the rotation / translation-direction ambiguity of forward motion and
+    //         the best 8-point sample's pose can sit in one (the same algorithm on the CPU,
+    //         0.5-1 px noise, 30 % outliers: single starts end 2-7 deg off in translation
+    //         direction where the fit from the true pose is within 0.5; two starts: <= 1.6). ----
+    __shared__ float s_E[2][9];
+    __shared__ int s_nh;  // starts found (0, 1, 2)
     if (t == 0) {
-        int bs = -1;
-        float bc = 0.f;
+        int b0 = -1, b1 = -1;
+        float c0 = 0.f, c1 = 0.f;
         for (int sv = 0; sv < NS; sv++) {
             if (s_sh[sv] < 0) continue;
             const float c = s_red2[0][sv] + s_red2[1][sv] + s_red2[2][sv] + s_red2[3][sv];
-            if (bs < 0 || c < bc || (c == bc && s_sh[sv] < s_sh[bs])) {
-                bs = sv;
-                bc = c;
+            if (b0 < 0 || c < c0 || (c == c0 && s_sh[sv] < s_sh[b0])) {
+                b1 = b0;
+                c1 = c0;
+                b0 = sv;
+                c0 = c;
+            } else if (b1 < 0 || c < c1 || (c == c1 && s_sh[sv] < s_sh[b1])) {
+                b1 = sv;
+                c1 = c;
             }
         }
-        s_best[0] = bs < 0 ? -1
-                           : (int)(s_red2[0][NS + bs] + s_red2[1][NS + bs] + s_red2[2][NS + bs] + s_red2[3][NS + bs]);
-        if (bs >= 0)
-            for (int r = 0; r < 9; r++) s_E[r] = s_sE[bs][r];
+        s_nh = b0 < 0 ? 0 : (b1 < 0 ? 1 : 2);
+        if (b0 >= 0)
+            for (int r = 0; r < 9; r++) {
+                s_E[0][r] = s_sE[b0][r];
+                s_E[1][r] = s_sE[b1 >= 0 ? b1 : b0][r];
+            }
     }
     __syncthreads();
-    if (s_best[0] < 0) {
+    if (s_nh == 0) {
         if (t < 12) To[t] = (t % 4 == t / 4) ? 1.f : 0.f;
         if (t == 0) {
             num_inliers[b] = 0;
@@ -660,15 +655,17 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
         }
         return;
     }
+    constexpr int HT = NT / 2;  // threads per half
+    static_assert(MAXP <= 32 * HT, "the inlier mask holds 32 correspondences per thread");
+    const int hh = w >> 1, ht = t & (HT - 1);
     float E[9];
-    for (int r = 0; r < 9; r++) E[r] = s_E[r];
-    const int ninl = s_best[0];
+    for (int r = 0; r < 9; r++) E[r] = s_E[hh][r];
 
     const long long tk3 = PE_TRACE ? clock64() : 0;
-    // ---- 4. decomposition + cheirality ----
-    __shared__ float s_cand[4][12];
-    __shared__ float s_uv[2][3][3];
-    if (t == 0) {
+    // ---- 4. decomposition + cheirality, per half ----
+    __shared__ float s_cand[2][4][12];
+    __shared__ float s_uv[2][2][3][3];
+    if (ht == 0) {
         float U[3][3], V[3][3];
         if (PE_NODECOMP) {
             for (int i = 0; i < 3; i++)
@@ -678,49 +675,47 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
         }
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) {
-                s_uv[0][i][j] = U[i][j];
-                s_uv[1][i][j] = V[i][j];
+                s_uv[hh][0][i][j] = U[i][j];
+                s_uv[hh][1][i][j] = V[i][j];
             }
     }
     __syncthreads();
-    if (t < 4) {  // candidate c = t, one lane each
+    if (ht < 4) {  // candidate c = ht, one lane each
         const float W[3][3] = {{0, -1, 0}, {1, 0, 0}, {0, 0, 1}};
         float U[3][3], V[3][3];
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) {
-                U[i][j] = s_uv[0][i][j];
-                V[i][j] = s_uv[1][i][j];
+                U[i][j] = s_uv[hh][0][i][j];
+                V[i][j] = s_uv[hh][1][i][j];
             }
-        {
-            const int c = t;
-            float R[3][3];
-            for (int i = 0; i < 3; i++)
-                for (int j = 0; j < 3; j++) {
-                    float s = 0;
-                    for (int k = 0; k < 3; k++) {
-                        float uw = 0;
-                        for (int l = 0; l < 3; l++) uw += U[i][l] * (c < 2 ? W[l][k] : W[k][l]);
-                        s += uw * V[j][k];
-                    }
-                    R[i][j] = s;
+        const int c = ht;
+        float R[3][3];
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) {
+                float s = 0;
+                for (int k = 0; k < 3; k++) {
+                    float uw = 0;
+                    for (int l = 0; l < 3; l++) uw += U[i][l] * (c < 2 ? W[l][k] : W[k][l]);
+                    s += uw * V[j][k];
                 }
-            const float sg = (c & 1) ? -1.f : 1.f;
-            for (int i = 0; i < 9; i++) s_cand[c][i] = R[i / 3][i % 3];
-            for (int i = 0; i < 3; i++) s_cand[c][9 + i] = sg * U[i][2];
-        }
+                R[i][j] = s;
+            }
+        const float sg = (c & 1) ? -1.f : 1.f;
+        for (int i = 0; i < 9; i++) s_cand[hh][c][i] = R[i / 3][i % 3];
+        for (int i = 0; i < 3; i++) s_cand[hh][c][9 + i] = sg * U[i][2];
     }
     __syncthreads();
     int votes[4] = {0, 0, 0, 0};
-    unsigned inl_mask = 0;  // bit k: correspondence t + k NT is a Sampson inlier of E (n <= 32 NT)
-    for (int i = t, k = 0; i < n; i += NT, k++)
+    unsigned inl_mask = 0;  // bit k: correspondence ht + k HT is a Sampson inlier of E
+    for (int i = ht, k = 0; i < n; i += HT, k++)
         inl_mask |= sampson_inlier(E, P[i], a.thr2) ? 1u << k : 0u;
 #pragma unroll
     for (int c = 0; c < 4; c++) {  // candidate-outer: 12 candidate floats live, not 48
         for (unsigned mk = inl_mask; mk; mk &= mk - 1) {
-            const float4 p = P[t + __builtin_ctz(mk) * NT];
+            const float4 p = P[ht + __builtin_ctz(mk) * HT];
             // depths z1, z2 of the midpoint triangulation, q z1 + t = -m z2 in the least-
             // squares sense: z = num / det with det > 0, so only the numerators' signs count
-            const float *C = s_cand[c];
+            const float *C = s_cand[hh][c];
             const F3 q = {{C[0] * p.x + C[1] * p.y + C[2], C[3] * p.x + C[4] * p.y + C[5], C[6] * p.x + C[7] * p.y + C[8]}};
             const F3 m = {{-p.z, -p.w, -1.f}};
             const F3 tt = {{C[9], C[10], C[11]}};
@@ -732,44 +727,51 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
         }
     }
     const long long tk4 = PE_TRACE ? clock64() : 0;
-    __shared__ int s_votes[4];
+    __shared__ int s_votes[4][4];  // [wave][candidate]
+#pragma unroll
     for (int c = 0; c < 4; c++) {
-        int v = block_sum_i(votes[c], wsum);
-        if (t == 0) s_votes[c] = v;
-        __syncthreads();
-    }
-    if (t == 0) {
-        int bc = 0;
-        for (int c = 1; c < 4; c++)
-            if (s_votes[c] > s_votes[bc]) bc = c;
-        for (int i = 0; i < 12; i++) s_pose[i] = s_cand[bc][i];
+        int v = votes[c];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (lane == 0) s_votes[w][c] = v;
     }
     __syncthreads();
+    int bc = 0, bv = s_votes[2 * hh][0] + s_votes[2 * hh + 1][0];
+    for (int c = 1; c < 4; c++) {
+        const int v = s_votes[2 * hh][c] + s_votes[2 * hh + 1][c];
+        if (v > bv) {
+            bv = v;
+            bc = c;
+        }
+    }
 
     const long long tk5 = PE_TRACE ? clock64() : 0;
-    // ---- 5. Gauss-Newton, inliers re-selected every iteration with the current
-    //         model: |r_i| < th_k, th_0 = thr, th_{k+1} = min(thr, max(3 rms_k, 0.01 px))
-    //         (removes outliers that fell inside the RANSAC band; noisy data keeps thr).
-    //         Every thread holds the pose and solves the 5x5 normal equations itself from the
-    //         22 block sums (identical float ops in every lane): one block barrier per
-    //         iteration (the partial sums are double-buffered), no broadcast of the update. ----
+    // ---- 5. robust Gauss-Newton per half: iteratively reweighted, Cauchy weights
+    //         1 / (1 + (r / c)^2) on the Sampson residuals below 3 thr (none above), the scale
+    //         c_0 = thr, c_{k+1} = min(thr, max(2 rms_w, 0.01 thr)) (rms_w: the weighted rms of
+    //         iteration k), so on exact data c shrinks until the outliers that fell inside the
+    //         band no longer pull (converges to machine precision) and on noisy data it settles
+    //         near 2 sigma.  Weights and Sampson denominators are frozen within an iteration.
+    //         The solving wave of each half (waves 0 and 2) solves its 5x5 normal equations
+    //         from the half's 22 sums; one block barrier per iteration (partial sums and states
+    //         double-buffered), the loop runs until both halves stop. ----
     __shared__ float s_red[2][4][22];
-    __shared__ float s_state[2][16];  // wave 0's update, double-buffered like s_red
-    float R[9], tv[3], bs[6];  // the state: rotation, unit translation, tangent basis at t
+    __shared__ float s_state[2][2][16];  // [iteration parity][half]
+    float R[9], tv[3], bs[6];            // the state: rotation, unit translation, tangent basis at t
 #pragma unroll
-    for (int i = 0; i < 9; i++) R[i] = s_pose[i];
+    for (int i = 0; i < 9; i++) R[i] = s_cand[hh][bc][i];
 #pragma unroll
-    for (int i = 0; i < 3; i++) tv[i] = s_pose[9 + i];
+    for (int i = 0; i < 3; i++) tv[i] = s_cand[hh][bc][9 + i];
     tangent_basis_f(tv, bs);
-    const float th_max = sqrtf(a.thr2), th_min = 0.01f * th_max;
-    float th = th_max;
+    const float th_max = sqrtf(a.thr2), th_min = 0.01f * th_max, r_cap = 3.f * th_max;
+    float csc = th_max;  // the Cauchy scale
+    bool act = true;    // this half is still iterating
     for (int it = 0; it < a.refine_iters; it++) {
-        // the per-correspondence Jacobian and the 22 sums are float (the fixed point is set
-        // by the float residual, ~1e-7 of a unit vector)
-        float acc[22];  // J^T J (15, upper), J^T r (5), sum r^2, count
+        float acc[22];  // sum w J^T J (15, upper), sum w J^T r (5), sum w r^2, sum w
 #pragma unroll
         for (int k = 0; k < 22; k++) acc[k] = 0.f;
-        for (int i = t; i < (PE_NOPOINTS ? 0 : n); i += NT) {
+        const float rcs = __builtin_amdgcn_rcpf(csc);
+        for (int i = ht; i < (act ? n : 0); i += HT) {
             const float4 p = P[i];
             const float x1[3] = {p.x, p.y, 1.f}, x2[3] = {p.z, p.w, 1.f};
             const float q[3] = {R[0] * x1[0] + R[1] * x1[1] + R[2], R[3] * x1[0] + R[4] * x1[1] + R[5],
@@ -785,8 +787,10 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
             const float s2 = Ex1[0] * Ex1[0] + Ex1[1] * Ex1[1] + Etx2[0] * Etx2[0] + Etx2[1] * Etx2[1];
             if (!(s2 > 0.f)) continue;
             const float inv = __builtin_amdgcn_rsqf(s2);  // native: a GN weight, not an output
-            const float r = e * inv;  // Sampson distance (weight frozen at the current model)
-            if (!(fabsf(r) < th)) continue;
+            const float r = e * inv;                      // Sampson distance
+            if (!(fabsf(r) < r_cap)) continue;
+            const float u = r * rcs;
+            const float wt = __builtin_amdgcn_rcpf(1.f + u * u);
             // d e / d omega = q x (x2 x t)  (R <- exp(omega) R);  d e / d t = q x x2
             const float dw[3] = {q[1] * x2t[2] - q[2] * x2t[1], q[2] * x2t[0] - q[0] * x2t[2],
                                  q[0] * x2t[1] - q[1] * x2t[0]};
@@ -795,142 +799,181 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
             const float J[5] = {dw[0] * inv, dw[1] * inv, dw[2] * inv,
                                 (dt[0] * bs[0] + dt[1] * bs[1] + dt[2] * bs[2]) * inv,
                                 (dt[0] * bs[3] + dt[1] * bs[4] + dt[2] * bs[5]) * inv};
+            float Jw[5];
+#pragma unroll
+            for (int v = 0; v < 5; v++) Jw[v] = J[v] * wt;
             int k = 0;
 #pragma unroll
-            for (int u = 0; u < 5; u++) {
+            for (int v = 0; v < 5; v++) {
 #pragma unroll
-                for (int v = u; v < 5; v++) acc[k++] += J[u] * J[v];
+                for (int x = v; x < 5; x++) acc[k++] += Jw[v] * J[x];
             }
 #pragma unroll
-            for (int u = 0; u < 5; u++) acc[15 + u] += J[u] * r;
-            acc[20] += r * r;
-            acc[21] += 1.f;
+            for (int v = 0; v < 5; v++) acc[15 + v] += Jw[v] * r;
+            acc[20] += wt * r * r;
+            acc[21] += wt;
         }
         // the 22 sums reduced over the wave by recursive halving (a reduce-scatter: at
         // level 2^L each lane keeps half of its values and receives its partner's partials
-        // of them, 94 VALU ops instead of 6 x 22 x 2), then 4 wave partials in LDS
+        // of them, 94 VALU ops instead of 6 x 22 x 2), then the 4 wave partials in LDS
         float(*red)[22] = s_red[it & 1];
-        if (!PE_NORED) {
+        {
             int vi;  // the sum this lane holds after the halving
             const float f = gn_reduce_scatter22(acc, lane, vi);
             if (vi >= 0) red[w][vi] = f;
-        } else if (lane < 22) {
-            red[w][lane] = acc[0];
         }
         __syncthreads();
-        // wave 0 solves (H + lambda diag H) d = -g and updates the state; the other waves
-        // take it from LDS after the second barrier (their VALU goes to the CU's other blocks)
-        float *st = s_state[it & 1];
-        if (w == 0 && !PE_NOSOLVE) {
-            float H[15], g[5];
+        float *st = s_state[it & 1][hh];
+        if ((w & 1) == 0) {
+            if (act) {
+                float H[15], g[5];
 #pragma unroll
-            for (int k = 0; k < 15; k++) H[k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+                for (int k = 0; k < 15; k++) H[k] = red[w][k] + red[w + 1][k];
 #pragma unroll
-            for (int k = 0; k < 5; k++) g[k] = red[0][15 + k] + red[1][15 + k] + red[2][15 + k] + red[3][15 + k];
-            const float r2 = red[0][20] + red[1][20] + red[2][20] + red[3][20];
-            const float cnt = red[0][21] + red[1][21] + red[2][21] + red[3][21];
-            // float Cholesky on the native reciprocal square root (the step only has to be a
-            // descent direction); every loop fully unrolled: static register indexing
-            float A[5][5];
+                for (int k = 0; k < 5; k++) g[k] = red[w][15 + k] + red[w + 1][15 + k];
+                const float r2 = red[w][20] + red[w + 1][20];
+                const float cnt = red[w][21] + red[w + 1][21];
+                // float Cholesky on the native reciprocal square root (the step only has to be
+                // a descent direction); every loop fully unrolled: static register indexing
+                float A[5][5];
 #pragma unroll
-            for (int u = 0, k = 0; u < 5; u++)
+                for (int v = 0, k = 0; v < 5; v++)
 #pragma unroll
-                for (int v = u; v < 5; v++, k++) {
-                    A[u][v] = H[k];
-                    A[v][u] = H[k];
-                }
-#pragma unroll
-            for (int u = 0; u < 5; u++) A[u][u] = A[u][u] * (1.0f + 1e-6f) + 1e-30f;
-            float L[5][5] = {}, rl[5] = {};
-            bool ok = cnt >= 5.f;
-#pragma unroll
-            for (int i = 0; i < 5; i++)
-#pragma unroll
-                for (int j = 0; j <= i; j++) {
-                    float sum = A[i][j];
-#pragma unroll
-                    for (int m = 0; m < j; m++) sum -= L[i][m] * L[j][m];
-                    if (i == j) {
-                        ok = ok && sum > 0.f;
-                        rl[i] = __builtin_amdgcn_rsqf(fmaxf(sum, 1e-30f));  // 1 / L[i][i]
-                        L[i][i] = fmaxf(sum, 1e-30f) * rl[i];
-                    } else {
-                        L[i][j] = sum * rl[j];
+                    for (int x = v; x < 5; x++, k++) {
+                        A[v][x] = H[k];
+                        A[x][v] = H[k];
                     }
+#pragma unroll
+                for (int v = 0; v < 5; v++) A[v][v] = A[v][v] * (1.0f + 1e-6f) + 1e-30f;
+                float L[5][5] = {}, rl[5] = {};
+                bool ok = cnt >= 5.f;
+#pragma unroll
+                for (int i = 0; i < 5; i++)
+#pragma unroll
+                    for (int j = 0; j <= i; j++) {
+                        float sum = A[i][j];
+#pragma unroll
+                        for (int m = 0; m < j; m++) sum -= L[i][m] * L[j][m];
+                        if (i == j) {
+                            ok = ok && sum > 0.f;
+                            rl[i] = __builtin_amdgcn_rsqf(fmaxf(sum, 1e-30f));  // 1 / L[i][i]
+                            L[i][i] = fmaxf(sum, 1e-30f) * rl[i];
+                        } else {
+                            L[i][j] = sum * rl[j];
+                        }
+                    }
+                float y[5], d[5];
+#pragma unroll
+                for (int i = 0; i < 5; i++) {
+                    float sum = -g[i];
+#pragma unroll
+                    for (int m = 0; m < i; m++) sum -= L[i][m] * y[m];
+                    y[i] = sum * rl[i];
                 }
-            float y[5], d[5];
 #pragma unroll
-            for (int i = 0; i < 5; i++) {
-                float sum = -g[i];
+                for (int i = 4; i >= 0; i--) {
+                    float sum = y[i];
 #pragma unroll
-                for (int m = 0; m < i; m++) sum -= L[i][m] * y[m];
-                y[i] = sum * rl[i];
-            }
+                    for (int m = i + 1; m < 5; m++) sum -= L[m][i] * d[m];
+                    d[i] = sum * rl[i];
+                }
+                float dR[3][3];
+                rodrigues_f(d, dR);
+                float Rn[9], tn[3];
 #pragma unroll
-            for (int i = 4; i >= 0; i--) {
-                float sum = y[i];
+                for (int i = 0; i < 3; i++)
 #pragma unroll
-                for (int m = i + 1; m < 5; m++) sum -= L[m][i] * d[m];
-                d[i] = sum * rl[i];
-            }
-            float dR[3][3];
-            rodrigues_f(d, dR);
-            float Rn[9], tn[3];
+                    for (int j = 0; j < 3; j++)
+                        Rn[i * 3 + j] = dR[i][0] * R[0 * 3 + j] + dR[i][1] * R[1 * 3 + j] + dR[i][2] * R[2 * 3 + j];
 #pragma unroll
-            for (int i = 0; i < 3; i++)
+                for (int i = 0; i < 3; i++) tn[i] = tv[i] + d[3] * bs[i] + d[4] * bs[3 + i];
+                const float rn = __builtin_amdgcn_rsqf(tn[0] * tn[0] + tn[1] * tn[1] + tn[2] * tn[2]);
+                const float cs_new = fminf(th_max, fmaxf(2.f * sqrtf(r2 / cnt), th_min));
+                float dmax = 0.f;
 #pragma unroll
-                for (int j = 0; j < 3; j++)
-                    Rn[i * 3 + j] = dR[i][0] * R[0 * 3 + j] + dR[i][1] * R[1 * 3 + j] + dR[i][2] * R[2 * 3 + j];
+                for (int i = 0; i < 5; i++) dmax = fmaxf(dmax, fabsf(d[i]));
+                // converged: a step below the float residual's resolution (1e-6 rad / unit-t,
+                // 100x under the 1e-4 tolerance) and a scale that moved < 0.1 %
+                const bool done = dmax < 1e-6f && fabsf(cs_new - csc) <= 1e-3f * csc;
+                // lane k < 14 stores word k of the state (static register indexing):
+                // R (9), t (3), scale, flags (bit 0: failed -- keep the old state; bit 1: converged)
+                if (lane < 14) {
+                    float v = 0.f;
 #pragma unroll
-            for (int i = 0; i < 3; i++) tn[i] = tv[i] + d[3] * bs[i] + d[4] * bs[3 + i];
-            const float rn = __builtin_amdgcn_rsqf(tn[0] * tn[0] + tn[1] * tn[1] + tn[2] * tn[2]);
-            const float th_new = fminf(th_max, fmaxf(3.f * sqrtf(r2 / cnt), th_min));
-            float dmax = 0.f;
+                    for (int k = 0; k < 9; k++) v = lane == k ? Rn[k] : v;
 #pragma unroll
-            for (int i = 0; i < 5; i++) dmax = fmaxf(dmax, fabsf(d[i]));
-            // converged: a step below the float residual's resolution (1e-6 rad / unit-t, 100x
-            // under the 1e-4 tolerance) and an inlier band that moved < 0.1 %
-            const bool done = dmax < 1e-6f && fabsf(th_new - th) <= 1e-3f * th;
-            // lane k < 14 stores word k of the state (static register indexing):
-            // R (9), t (3), th, flags (bit 0: failed -- keep the old state; bit 1: converged)
-            if (lane < 14) {
-                float v = 0.f;
-#pragma unroll
-                for (int k = 0; k < 9; k++) v = lane == k ? Rn[k] : v;
-#pragma unroll
-                for (int k = 0; k < 3; k++) v = lane == 9 + k ? tn[k] * rn : v;
-                v = lane == 12 ? th_new : v;
-                v = lane == 13 ? __int_as_float((ok ? 0 : 1) | (done ? 2 : 0)) : v;
-                st[lane] = v;
+                    for (int k = 0; k < 3; k++) v = lane == 9 + k ? tn[k] * rn : v;
+                    v = lane == 12 ? cs_new : v;
+                    v = lane == 13 ? __int_as_float((ok ? 0 : 1) | (done ? 2 : 0)) : v;
+                    st[lane] = v;
+                }
+            } else if (lane == 13) {
+                st[13] = __int_as_float(2);  // a stopped half stays stopped
             }
         }
         __syncthreads();
-        if (PE_NOSOLVE) continue;
-        const int flags = __float_as_int(st[13]);
-        if (flags & 1) break;  // the same decision in every thread
+        const int f0 = __float_as_int(s_state[it & 1][0][13]), f1 = __float_as_int(s_state[it & 1][1][13]);
+        const int fl = hh ? f1 : f0;
+        if (act && !(fl & 1)) {
 #pragma unroll
-        for (int i = 0; i < 9; i++) R[i] = st[i];
+            for (int i = 0; i < 9; i++) R[i] = st[i];
 #pragma unroll
-        for (int i = 0; i < 3; i++) tv[i] = st[9 + i];
-        tangent_basis_f(tv, bs);
-        th = st[12];
-        if (flags & 2) break;
+            for (int i = 0; i < 3; i++) tv[i] = st[9 + i];
+            tangent_basis_f(tv, bs);
+            csc = st[12];
+        }
+        act = act && !(fl & 3);
+        if ((f0 & 3) && (f1 & 3)) break;  // the same decision in every thread
     }
-    {  // [R | t] row-major, thread t < 12 writes entry t (static register indexing)
+
+    // ---- 6. each half's robust cost at its refined pose (Cauchy at the scale thr, capped at
+    //         3 thr), the lower wins (a tie: the better RANSAC start); its inliers (Sampson
+    //         distance < thr) are the reported count ----
+    float rcost = 0.f;
+    int ninl = 0;
+    for (int i = ht; i < n; i += HT) {
+        const float4 p = P[i];
+        const float q[3] = {R[0] * p.x + R[1] * p.y + R[2], R[3] * p.x + R[4] * p.y + R[5], R[6] * p.x + R[7] * p.y + R[8]};
+        const float x2t[3] = {p.w * tv[2] - tv[1], tv[0] - p.z * tv[2], p.z * tv[1] - p.w * tv[0]};
+        const float e = x2t[0] * q[0] + x2t[1] * q[1] + x2t[2] * q[2];
+        const float Ex1[2] = {tv[1] * q[2] - tv[2] * q[1], tv[2] * q[0] - tv[0] * q[2]};
+        float Etx2[2];
+#pragma unroll
+        for (int c = 0; c < 2; c++) Etx2[c] = R[c] * x2t[0] + R[3 + c] * x2t[1] + R[6 + c] * x2t[2];
+        const float s2 = Ex1[0] * Ex1[0] + Ex1[1] * Ex1[1] + Etx2[0] * Etx2[0] + Etx2[1] * Etx2[1];
+        const float ar = s2 > 0.f ? fabsf(e) * __builtin_amdgcn_rsqf(s2) : r_cap;
+        const float u = fminf(ar, r_cap) / th_max;
+        rcost += __logf(1.f + u * u);
+        ninl += ar < th_max ? 1 : 0;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        rcost += __shfl_xor(rcost, o, 64);
+        ninl += __shfl_xor(ninl, o, 64);
+    }
+    __shared__ float s_fin[4];
+    __shared__ int s_fin_n[4];
+    if (lane == 0) {
+        s_fin[w] = rcost;
+        s_fin_n[w] = ninl;
+    }
+    __syncthreads();
+    const int win = (s_nh > 1 && s_fin[2] + s_fin[3] < s_fin[0] + s_fin[1]) ? 1 : 0;
+    if (hh == win) {  // [R | t] row-major, thread ht < 12 writes entry ht (static register indexing)
         float v = 0.f;
 #pragma unroll
-        for (int k = 0; k < 12; k++) v = t == k ? (k % 4 < 3 ? R[(k / 4) * 3 + k % 4] : tv[k / 4]) : v;
-        if (t < 12) To[t] = v;
+        for (int k = 0; k < 12; k++) v = ht == k ? (k % 4 < 3 ? R[(k / 4) * 3 + k % 4] : tv[k / 4]) : v;
+        if (ht < 12) To[ht] = v;
+        if (ht == 0) {
+            num_inliers[b] = s_fin_n[2 * win] + s_fin_n[2 * win + 1];
+            if (num_matches) num_matches[b] = n_all;
+            status[b] = MV_OK;
+        }
     }
     if (PE_TRACE && b == 0 && t == 0) {
         const long long tk6 = clock64();
         printf("pose phases (clk): compact %lld hyp+score %lld argmin %lld decomp %lld cheir %lld gn %lld\n",
                tk1 - tk0, tk2 - tk1, tk3 - tk2, tk4 - tk3, tk5 - tk4, tk6 - tk5);
-    }
-    if (t == 0) {
-        num_inliers[b] = ninl;
-        if (num_matches) num_matches[b] = n_all;
-        status[b] = MV_OK;
     }
 }
 

@@ -1,0 +1,522 @@
+// k_superpoint.hip -- the quantized SuperPoint front-end (include/superpoint.h)
+// on gfx950: grayscale frames -> int8 semi / desc + scales, bit-identical to the CPU oracle
+// (oracle/sp_oracle.c, itself bit-identical to PyTorch's quantized kernels).
+//
+//   k_sp_conv1a   image -> (/ 255, bilinear resize, quantize) in LDS with a 1-pixel halo ->
+//                 conv1a (Cin = 1: 9 taps as three v_dot4_i32_i8 per output channel) -> relu ->
+//                 NHWC int8 [oh][ow][64].
+//   k_sp_conv     every other layer as an implicit GEMM on v_mfma_i32_32x32x32_i8: A = the
+//                 layer's weights as MFMA fragments (64 couts per workgroup, prefetched from
+//                 L2 four k32 steps ahead), B = 32 pixels x 32 channels of one tap read from the
+//                 workgroup's NHWC input tile in LDS (16 x 32 output pixels + halo, 16-B chunks
+//                 XOR-swizzled by pixel: conflict-free ds_read_b128).  Wave w owns tile rows
+//                 4w .. 4w + 3, i.e. 8 MFMAs (4 pixel rows x 2 cout blocks) per k32 step.
+//                 Epilogue: int32 + quantised bias -> fp32 x rs -> round to nearest even ->
+//                 clamp (relu) -> the 2 x 2 max pool on the int32 accumulators (requantisation is
+//                 monotonic: the max commutes with it) -> NHWC int8, or for the two heads the
+//                 Frame layout [cells][C] (cell = gx * rows + gy).
+//   k_sp_min_gap  run()'s output quantisation (superpoint_inference.py:199-206): the 256-code
+//                 presence mask of one head of one frame, the smallest float gap between its
+//                 present dequantised values, then every value rounded to that step, in place.
+// Bounds: MFMA i8 (2 x 10.4 GMAC per 192 x 640 frame) with HBM beside it (~16 MB of int8
+// activations written and read per frame).
+#include <math.h>
+
+#include "mv_internal.hpp"
+#include "superpoint.h"
+
+struct mv_superpoint {
+    int device;
+    void *wdev;           // fragments + packed conv1a weights + quantised biases
+    size_t wbytes;
+    size_t frag_off[12];  // byte offsets into wdev (layer 0: packed dot4 weights [64][3])
+    size_t bq_off[12];    // int32 quantised biases [cout_pad]
+    float rs[12];         // requantisation scales
+    int cout_pad[12], ns[12];
+    float in_inv;         // 1 / (float) in_scale
+    float dq_semi, dq_desc;  // the heads' dequantisation scales (float) out_scale
+    void *act;            // activation ping-pong buffers
+    size_t act_bytes;
+};
+
+namespace {
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int SP_NT = 256;          // 4 waves
+constexpr int TY = 16, TX = 32;     // conv output tile (before pooling)
+constexpr int C1_TY = 16, C1_TX = 64;  // conv1a output tile
+
+__device__ __forceinline__ float requant_f(int acc, float rs, float lo) {
+    float v = __builtin_rintf((float)acc * rs);
+    return fminf(fmaxf(v, lo), 127.f);
+}
+__device__ __forceinline__ int pack4i(float a, float b, float c, float d) {
+    return ((int)a & 0xff) | (((int)b & 0xff) << 8) | (((int)c & 0xff) << 16) | ((int)d << 24);
+}
+
+// torch's bilinear source index (align_corners=False): lambda1, i0, i1
+__device__ __forceinline__ float sp_src(float scale, int d, int n_in, int &i0, int &i1) {
+    float src = __builtin_fmaf(scale, (float)d + 0.5f, -0.5f);
+    src = src < 0.f ? 0.f : src;
+    int i = (int)floorf(src);
+    i = i > n_in - 1 ? n_in - 1 : i;
+    float lam = src - (float)i;
+    lam = lam < 0.f ? 0.f : (lam > 1.f ? 1.f : lam);
+    i0 = i;
+    i1 = i + (i < n_in - 1 ? 1 : 0);
+    return lam;
+}
+
+__global__ __launch_bounds__(SP_NT) void k_sp_conv1a(const uint8_t *__restrict__ img, int H, int W, int oh, int ow,
+                                                     int tiles_x, float in_inv, const int *__restrict__ wpk,
+                                                     const int *__restrict__ bq, float rs, int8_t *__restrict__ out) {
+    __shared__ int8_t q[C1_TY + 2][C1_TX + 4];
+    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x, b = blockIdx.y;
+    const int y0 = ty * C1_TY, x0 = tx * C1_TX, t = threadIdx.x;
+    const uint8_t *im = img + (size_t)b * H * W;
+    const float sy = (float)H / (float)oh, sx = (float)W / (float)ow;
+    for (int i = t; i < (C1_TY + 2) * (C1_TX + 2); i += SP_NT) {
+        const int r = i / (C1_TX + 2), c = i % (C1_TX + 2);
+        const int gy = y0 + r - 1, gx = x0 + c - 1;
+        int v = 0;
+        if (gy >= 0 && gy < oh && gx >= 0 && gx < ow) {
+            int ya, yb, xa, xb;
+            const float h1 = sp_src(sy, gy, H, ya, yb), w1 = sp_src(sx, gx, W, xa, xb);
+            const float h0 = 1.f - h1, w0 = 1.f - w1;
+            const float a00 = (float)im[(size_t)ya * W + xa] / 255.0f, a01 = (float)im[(size_t)ya * W + xb] / 255.0f;
+            const float a10 = (float)im[(size_t)yb * W + xa] / 255.0f, a11 = (float)im[(size_t)yb * W + xb] / 255.0f;
+            const float t0 = __builtin_fmaf(a00, w0, a01 * w1);
+            const float t1 = __builtin_fmaf(a10, w0, a11 * w1);
+            const float x = __builtin_fmaf(t0, h0, t1 * h1);
+            float qv = __builtin_rintf(x * in_inv);
+            qv = fminf(fmaxf(qv, -128.f), 127.f);
+            v = (int)qv;
+        }
+        q[r][c] = (int8_t)v;
+    }
+    __syncthreads();
+    for (int k = 0; k < C1_TY * C1_TX / SP_NT; k++) {
+        const int p = t + SP_NT * k, r = p / C1_TX, c = p % C1_TX;
+        const int gy = y0 + r, gx = x0 + c;
+        if (gy >= oh || gx >= ow) continue;
+        const int p0 = (q[r][c] & 0xff) | ((q[r][c + 1] & 0xff) << 8) | ((q[r][c + 2] & 0xff) << 16) | ((int)q[r + 1][c] << 24);
+        const int p1 = (q[r + 1][c + 1] & 0xff) | ((q[r + 1][c + 2] & 0xff) << 8) | ((q[r + 2][c] & 0xff) << 16) |
+                       ((int)q[r + 2][c + 1] << 24);
+        const int p2 = q[r + 2][c + 2] & 0xff;
+        i32x4 *dst = reinterpret_cast<i32x4 *>(out + (((size_t)b * oh + gy) * ow + gx) * 64);
+#pragma unroll
+        for (int g = 0; g < 4; g++) {  // 16 channels per 16-B store
+            i32x4 o;
+#pragma unroll
+            for (int d = 0; d < 4; d++) {
+                float v[4];
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int co = 16 * g + 4 * d + e;
+                    int acc = __builtin_amdgcn_sdot4(p0, wpk[3 * co], 0, false);
+                    acc = __builtin_amdgcn_sdot4(p1, wpk[3 * co + 1], acc, false);
+                    acc = __builtin_amdgcn_sdot4(p2, wpk[3 * co + 2], acc, false);
+                    v[e] = requant_f(acc + bq[co], rs, 0.f);
+                }
+                o[d] = pack4i(v[0], v[1], v[2], v[3]);
+            }
+            dst[g] = o;
+        }
+    }
+}
+
+// OMODE 0: NHWC [B][Ho][Wo][cstride]; OMODE 1: the Frame layout [B][Ho * Wo][cstride] with
+// cell = x * Ho + y, channels >= cstride not stored (cstride = 65 for semi)
+template <int CIN, int KS, bool POOL, bool RELU, int OMODE>
+__global__ __launch_bounds__(SP_NT, 2) void k_sp_conv(const int8_t *__restrict__ in, int H, int W,
+                                                      const i32x4 *__restrict__ wf, const int *__restrict__ bq,
+                                                      float rs, int ngroups, int tiles_x, int tiles_y,
+                                                      int8_t *__restrict__ out, int cstride) {
+    constexpr int P = KS / 2, IY = TY + 2 * P, IX = TX + 2 * P, NCH = CIN / 16, NS = KS * KS * CIN / 32;
+    constexpr int SWS = NCH >= 16 ? 1 : 16 / NCH;  // pixels per 256-B LDS bank row
+    constexpr int PF = 4;                          // weight fragments in flight (k32 steps)
+    static_assert(CIN % 32 == 0 && NCH <= 16, "channels in 32-k steps, at most 256");
+    __shared__ i32x4 tile[IY * IX * NCH];
+    int bid = blockIdx.x;
+    const int tx = bid % tiles_x;
+    bid /= tiles_x;
+    const int ty = bid % tiles_y;
+    bid /= tiles_y;
+    const int g = bid % ngroups, b = bid / ngroups;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, fr = lane & 31, fh = lane >> 5;
+    const int y0 = ty * TY, x0 = tx * TX;
+
+    // ---- the input tile (zero outside the image), 8 16-B loads in flight per thread ----
+    const int8_t *src = in + (size_t)b * H * W * CIN;
+    constexpr int NCHUNK = IY * IX * NCH;
+    for (int i0 = 0; i0 < NCHUNK; i0 += 8 * SP_NT) {
+        i32x4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int i = i0 + u * SP_NT + t;
+            const int c = i % NCH, px = i / NCH, x = px % IX, r = px / IX;
+            const int gy = y0 + r - P, gx = x0 + x - P;
+            v[u] = i32x4{0, 0, 0, 0};
+            if (i < NCHUNK && gy >= 0 && gy < H && gx >= 0 && gx < W)
+                v[u] = *reinterpret_cast<const i32x4 *>(src + ((size_t)gy * W + gx) * CIN + c * 16);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int i = i0 + u * SP_NT + t;
+            if (i >= NCHUNK) continue;
+            const int c = i % NCH, px = i / NCH, x = px % IX;
+            tile[px * NCH + (c ^ ((x / SWS) & (NCH - 1)))] = v[u];
+        }
+    }
+    __syncthreads();
+
+    // ---- K loop: 9 taps (or 1) x CIN / 32 steps ----
+    const i32x4 *wa = wf + (size_t)(2 * g) * NS * 64 + lane, *wb = wa + NS * 64;
+    i32x4 ra[PF], rb[PF];
+#pragma unroll
+    for (int u = 0; u < PF; u++) {
+        ra[u] = u < NS ? wa[u * 64] : i32x4{0, 0, 0, 0};
+        rb[u] = u < NS ? wb[u * 64] : i32x4{0, 0, 0, 0};
+    }
+    i32x16 acc[4][2];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        acc[j][0] = i32x16{};
+        acc[j][1] = i32x16{};
+    }
+#pragma unroll 1
+    for (int s0 = 0; s0 < NS; s0 += PF) {
+#pragma unroll
+        for (int u = 0; u < PF; u++) {
+            const int s = s0 + u;
+            if (s < NS) {
+                const i32x4 a0 = ra[u], a1 = rb[u];
+                if (s + PF < NS) {
+                    ra[u] = wa[(s + PF) * 64];
+                    rb[u] = wb[(s + PF) * 64];
+                }
+                const int tap = s * 32 / CIN, ky = tap / KS, kx = tap % KS;
+                const int c = (s * 32 % CIN) / 16 + fh;
+                const int x = fr + kx;
+                const int sw = c ^ ((x / SWS) & (NCH - 1));
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const i32x4 bv = tile[((4 * w + j + ky) * IX + x) * NCH + sw];
+                    acc[j][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bv, acc[j][0], 0, 0, 0);
+                    acc[j][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bv, acc[j][1], 0, 0, 0);
+                }
+            }
+        }
+    }
+
+    // ---- epilogue: lane = pixel fr of each row; 16 couts (4 groups of 4) per 32-cout block ----
+    const float lo = RELU ? 0.f : -128.f;
+    if constexpr (POOL) {
+        const int Ho = H / 2, Wo = W / 2;
+#pragma unroll
+        for (int jp = 0; jp < 2; jp++) {
+            const int gy = y0 + 4 * w + 2 * jp, gx = x0 + fr;
+#pragma unroll
+            for (int cb = 0; cb < 2; cb++) {
+                int m[16];
+#pragma unroll
+                for (int q = 0; q < 16; q++) {
+                    const int v = max(acc[2 * jp][cb][q], acc[2 * jp + 1][cb][q]);
+                    m[q] = max(v, __shfl_xor(v, 1, 64));
+                }
+                if ((fr & 1) == 0 && gy < H && gx < W) {
+                    int8_t *dst = out + (((size_t)b * Ho + gy / 2) * Wo + gx / 2) * cstride;
+#pragma unroll
+                    for (int qq = 0; qq < 4; qq++) {
+                        const int co = 64 * g + 32 * cb + 8 * qq + 4 * fh;
+                        float v[4];
+#pragma unroll
+                        for (int e = 0; e < 4; e++) v[e] = requant_f(m[4 * qq + e] + bq[co + e], rs, lo);
+                        *reinterpret_cast<int *>(dst + co) = pack4i(v[0], v[1], v[2], v[3]);
+                    }
+                }
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int gy = y0 + 4 * w + j, gx = x0 + fr;
+            if (gy >= H || gx >= W) continue;
+            int8_t *dst = OMODE == 0 ? out + (((size_t)b * H + gy) * W + gx) * cstride
+                                     : out + ((size_t)b * H * W + (size_t)gx * H + gy) * cstride;
+#pragma unroll
+            for (int cb = 0; cb < 2; cb++) {
+#pragma unroll
+                for (int qq = 0; qq < 4; qq++) {
+                    const int co = 64 * g + 32 * cb + 8 * qq + 4 * fh;
+                    float v[4];
+#pragma unroll
+                    for (int e = 0; e < 4; e++) v[e] = requant_f(acc[j][cb][4 * qq + e] + bq[co + e], rs, lo);
+                    if (OMODE == 0 || (cstride % 4 == 0 && co + 4 <= cstride)) {
+                        *reinterpret_cast<int *>(dst + co) = pack4i(v[0], v[1], v[2], v[3]);
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; e++)
+                            if (co + e < cstride) dst[co + e] = (int8_t)(int)v[e];
+                    }
+                }
+            }
+        }
+    }
+}
+
+// run()'s output quantisation of head h (0: semi, C = 65; 1: desc, C = 256) of frame b, in place
+__global__ __launch_bounds__(SP_NT) void k_sp_min_gap(int8_t *__restrict__ semi, int8_t *__restrict__ desc, long cells,
+                                                      float s_semi, float s_desc, float *__restrict__ semi_scale,
+                                                      float *__restrict__ desc_scale) {
+    __shared__ unsigned pres[8];
+    __shared__ float gmin[SP_NT / 64];
+    const int b = blockIdx.x, h = blockIdx.y, t = threadIdx.x, lane = t & 63;
+    const int C = h ? 256 : 65;
+    const float s = h ? s_desc : s_semi;
+    int8_t *base = (h ? desc : semi) + (size_t)b * cells * C;
+    const long n = cells * C;
+    if (t < 8) pres[t] = 0u;
+    __syncthreads();
+    unsigned m[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    for (long i = t; i < n; i += SP_NT) {
+        const int v = base[i] + 128;
+        const unsigned bit = 1u << (v & 31);
+#pragma unroll
+        for (int k = 0; k < 8; k++) m[k] |= (v >> 5) == k ? bit : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        unsigned x = m[k];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) x |= __shfl_xor(x, o, 64);
+        if (lane == 0 && x) atomicOr(&pres[k], x);
+    }
+    __syncthreads();
+    // thread v: the gap from code v (present) to the next present code, in dequantised floats
+    float gap = INFINITY;
+    int cnt = 0;
+    {
+        const int v = t;
+        const bool here = (pres[v >> 5] >> (v & 31)) & 1u;
+        int nx = -1;
+        for (int u = v + 1; u < 256 && nx < 0; u++)
+            if ((pres[u >> 5] >> (u & 31)) & 1u) nx = u;
+        if (here && nx >= 0) {
+            const float d = (float)(nx - 128) * s - (float)(v - 128) * s;
+            gap = d > 0.f ? d : INFINITY;
+        }
+        cnt = here ? 1 : 0;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        gap = fminf(gap, __shfl_xor(gap, o, 64));
+        cnt += __shfl_xor(cnt, o, 64);
+    }
+    __shared__ int cnts[SP_NT / 64];
+    if (lane == 0) {
+        gmin[t >> 6] = gap;
+        cnts[t >> 6] = cnt;
+    }
+    __syncthreads();
+    float g = gmin[0];
+    int distinct = cnts[0];
+#pragma unroll
+    for (int k = 1; k < SP_NT / 64; k++) {
+        g = fminf(g, gmin[k]);
+        distinct += cnts[k];
+    }
+    if (distinct < 2) g = 0.f;
+    if (t == 0) (h ? desc_scale : semi_scale)[b] = g;
+    if (g == 0.f) return;  // fewer than two distinct values: the raw codes stay
+    for (long i = t; i < n; i += SP_NT) {
+        const float f = (float)base[i] * s;
+        float r = __builtin_rintf(f / g);
+        r = fminf(fmaxf(r, -128.f), 127.f);
+        base[i] = (int8_t)(int)r;
+    }
+}
+
+template <int CIN, int KS, bool POOL, bool RELU, int OMODE>
+int launch_conv(hipStream_t st, const mv_superpoint *net, int li, int B, int H, int W, const int8_t *in,
+                int8_t *out, int cstride) {
+    const int tiles_x = (W + TX - 1) / TX, tiles_y = (H + TY - 1) / TY, ngroups = net->cout_pad[li] / 64;
+    const long blocks = (long)B * ngroups * tiles_y * tiles_x;
+    MV_REQUIRE(blocks < (1l << 31));
+    const char *wd = static_cast<const char *>(net->wdev);
+    hipLaunchKernelGGL((k_sp_conv<CIN, KS, POOL, RELU, OMODE>), dim3((unsigned)blocks), dim3(SP_NT), 0, st, in, H, W,
+                       reinterpret_cast<const i32x4 *>(wd + net->frag_off[li]),
+                       reinterpret_cast<const int *>(wd + net->bq_off[li]), net->rs[li], ngroups, tiles_x, tiles_y,
+                       out, cstride);
+    MV_LAUNCH_CHECK();
+    return MV_OK;
+}
+
+constexpr int SP_CIN[12] = {1, 64, 64, 64, 64, 128, 128, 128, 128, 256, 128, 256};
+constexpr int SP_COUT[12] = {64, 64, 64, 64, 128, 128, 128, 128, 256, 65, 256, 256};
+constexpr int SP_K[12] = {3, 3, 3, 3, 3, 3, 3, 3, 3, 1, 3, 1};
+
+}  // namespace
+
+extern "C" int mv_superpoint_create(mv_context *ctx, const mv_sp_weights *wt, mv_superpoint **out) {
+    MV_REQUIRE(ctx && wt && out && wt->in_scale > 0.0);
+    *out = nullptr;
+    for (int l = 0; l < 12; l++) {
+        const mv_sp_layer &L = wt->layer[l];
+        MV_REQUIRE(L.w && L.bias && L.cin == SP_CIN[l] && L.cout == SP_COUT[l] && L.k == SP_K[l]);
+        MV_REQUIRE(L.w_scale > 0.0 && L.out_scale > 0.0);
+    }
+    MV_HIP_TRY(hipSetDevice(ctx->device));
+    mv_superpoint *net = new mv_superpoint();
+    net->device = ctx->device;
+    net->in_inv = 1.0f / (float)wt->in_scale;
+    net->dq_semi = (float)wt->layer[9].out_scale;
+    net->dq_desc = (float)wt->layer[11].out_scale;
+    // host image of the device weights
+    size_t off = 0;
+    for (int l = 0; l < 12; l++) {
+        const mv_sp_layer &L = wt->layer[l];
+        net->cout_pad[l] = (L.cout + 63) / 64 * 64;
+        net->ns[l] = L.k * L.k * L.cin / 32;
+        net->frag_off[l] = off;
+        off += l == 0 ? 64 * 3 * 4 : (size_t)net->cout_pad[l] / 32 * net->ns[l] * 64 * 16;
+        off = mv::align_up(off, 256);
+        net->bq_off[l] = off;
+        off += (size_t)net->cout_pad[l] * 4;
+        off = mv::align_up(off, 256);
+    }
+    char *hbuf = static_cast<char *>(calloc(off, 1));
+    if (!hbuf) {
+        delete net;
+        return MV_ERR_OUT_OF_MEMORY;
+    }
+    double in_scale = wt->in_scale;
+    for (int l = 0; l < 12; l++) {
+        const mv_sp_layer &L = wt->layer[l];
+        const int K = L.k, CIN = L.cin, COUT = L.cout;
+        if (l == 10) in_scale = wt->layer[7].out_scale;  // convDa reads conv4b, like convPa
+        // PyTorch's QuantizeBias (qint32 at w_scale * in_scale, float reciprocal) and XNNPACK's
+        // fp32 requantisation scale
+        const float binv = 1.0f / (float)(L.w_scale * in_scale);
+        net->rs[l] = (float)in_scale * (float)L.w_scale / (float)L.out_scale;
+        int *bq = reinterpret_cast<int *>(hbuf + net->bq_off[l]);
+        for (int co = 0; co < COUT; co++) {
+            float v = nearbyintf(L.bias[co] * binv);
+            v = v < -2147483648.f ? -2147483648.f : (v > 2147483520.f ? 2147483520.f : v);
+            bq[co] = (int)v;
+        }
+        if (l == 0) {
+            int *pk = reinterpret_cast<int *>(hbuf + net->frag_off[0]);
+            for (int co = 0; co < 64; co++) {
+                unsigned wv[12] = {0};
+                for (int tp = 0; tp < 9; tp++) wv[tp] = (uint8_t)L.w[co * 9 + tp];
+                for (int d = 0; d < 3; d++)
+                    pk[3 * co + d] = (int)(wv[4 * d] | (wv[4 * d + 1] << 8) | (wv[4 * d + 2] << 16) | (wv[4 * d + 3] << 24));
+            }
+        } else {
+            // fragment (cb, s): lane -> cout cb * 32 + lane % 32, k = 32 s + 16 (lane / 32) + i,
+            // k = tap * CIN + cin, tap = ky * K + kx
+            int8_t *fr = reinterpret_cast<int8_t *>(hbuf + net->frag_off[l]);
+            const int NS = net->ns[l];
+            for (int cb = 0; cb < net->cout_pad[l] / 32; cb++)
+                for (int s = 0; s < NS; s++)
+                    for (int ln = 0; ln < 64; ln++)
+                        for (int i = 0; i < 16; i++) {
+                            const int co = cb * 32 + ln % 32, k = 32 * s + 16 * (ln / 32) + i;
+                            const int tap = k / CIN, ci = k % CIN, ky = tap / K, kx = tap % K;
+                            fr[(((size_t)cb * NS + s) * 64 + ln) * 16 + i] =
+                                co < COUT ? L.w[(((size_t)co * CIN + ci) * K + ky) * K + kx] : 0;
+                        }
+        }
+        in_scale = L.out_scale;
+    }
+    if (hipMalloc(&net->wdev, off) != hipSuccess) {
+        free(hbuf);
+        delete net;
+        return MV_ERR_OUT_OF_MEMORY;
+    }
+    net->wbytes = off;
+    const hipError_t e = hipMemcpy(net->wdev, hbuf, off, hipMemcpyHostToDevice);
+    free(hbuf);
+    if (e != hipSuccess) {
+        (void)hipFree(net->wdev);
+        delete net;
+        mv::set_error(MV_ERR_HIP, "hipMemcpy of the SuperPoint weights: %s", hipGetErrorString(e));
+        return MV_ERR_HIP;
+    }
+    *out = net;
+    return MV_OK;
+}
+
+extern "C" int mv_superpoint_destroy(mv_superpoint *net) {
+    if (!net) return MV_OK;
+    (void)hipSetDevice(net->device);
+    (void)hipDeviceSynchronize();  // the net's buffers may be in use on any stream it was run on
+    if (net->act) (void)hipFree(net->act);
+    if (net->wdev) (void)hipFree(net->wdev);
+    delete net;
+    return MV_OK;
+}
+
+extern "C" int mv_superpoint_forward_dev(mv_context *ctx, mv_superpoint *net, int batch, int H, int W, int oh,
+                                         int ow, const uint8_t *images, int8_t *semi, int8_t *desc,
+                                         float *semi_scale, float *desc_scale) {
+    MV_REQUIRE(ctx && net && batch > 0 && H > 0 && W > 0 && oh >= 8 && ow >= 8 && oh % 8 == 0 && ow % 8 == 0);
+    MV_REQUIRE(images && semi && desc && semi_scale && desc_scale && net->device == ctx->device);
+    MV_REQUIRE((long)oh * ow * 64 < (1l << 31) && (long)batch * H * W < (1l << 40));
+    MV_HIP_TRY(hipSetDevice(ctx->device));
+    // activation buffers: A holds conv1a's output (the largest), B conv1b's pooled output
+    const size_t a_bytes = mv::align_up((size_t)batch * oh * ow * 64, 256);
+    const size_t need = a_bytes + (size_t)batch * (oh / 2) * (ow / 2) * 64;
+    if (net->act_bytes < need) {
+        if (net->act) {
+            const int q = mv::quiesce(ctx);
+            if (q != MV_OK) return q;
+            MV_HIP_TRY(hipFree(net->act));
+            net->act = nullptr;
+            net->act_bytes = 0;
+        }
+        if (hipMalloc(&net->act, need) != hipSuccess) return MV_ERR_OUT_OF_MEMORY;
+        net->act_bytes = need;
+    }
+    int8_t *A = static_cast<int8_t *>(net->act), *Bf = A + a_bytes;
+    hipStream_t st = ctx->stream;
+    const char *wd = static_cast<const char *>(net->wdev);
+    int r;
+    MV_PROF_BEGIN(st, "k_sp_conv1a");
+    {
+        const int tiles_x = (ow + C1_TX - 1) / C1_TX, tiles_y = (oh + C1_TY - 1) / C1_TY;
+        hipLaunchKernelGGL(k_sp_conv1a, dim3((unsigned)(tiles_x * tiles_y), (unsigned)batch), dim3(SP_NT), 0, st,
+                           images, H, W, oh, ow, tiles_x, net->in_inv,
+                           reinterpret_cast<const int *>(wd + net->frag_off[0]),
+                           reinterpret_cast<const int *>(wd + net->bq_off[0]), net->rs[0], A);
+        MV_LAUNCH_CHECK();
+    }
+    MV_PROF_END(st);
+    int h = oh, w = ow;
+    MV_PROF_BEGIN(st, "k_sp_conv");
+    if ((r = launch_conv<64, 3, true, true, 0>(st, net, 1, batch, h, w, A, Bf, 64)) != MV_OK) return r;
+    h /= 2, w /= 2;
+    if ((r = launch_conv<64, 3, false, true, 0>(st, net, 2, batch, h, w, Bf, A, 64)) != MV_OK) return r;
+    if ((r = launch_conv<64, 3, true, true, 0>(st, net, 3, batch, h, w, A, Bf, 64)) != MV_OK) return r;
+    h /= 2, w /= 2;
+    if ((r = launch_conv<64, 3, false, true, 0>(st, net, 4, batch, h, w, Bf, A, 128)) != MV_OK) return r;
+    if ((r = launch_conv<128, 3, true, true, 0>(st, net, 5, batch, h, w, A, Bf, 128)) != MV_OK) return r;
+    h /= 2, w /= 2;
+    if ((r = launch_conv<128, 3, false, true, 0>(st, net, 6, batch, h, w, Bf, A, 128)) != MV_OK) return r;
+    if ((r = launch_conv<128, 3, false, true, 0>(st, net, 7, batch, h, w, A, Bf, 128)) != MV_OK) return r;
+    // heads: Bf holds the shared encoder output
+    if ((r = launch_conv<128, 3, false, true, 0>(st, net, 8, batch, h, w, Bf, A, 256)) != MV_OK) return r;
+    if ((r = launch_conv<256, 1, false, false, 1>(st, net, 9, batch, h, w, A, semi, 65)) != MV_OK) return r;
+    if ((r = launch_conv<128, 3, false, true, 0>(st, net, 10, batch, h, w, Bf, A, 256)) != MV_OK) return r;
+    if ((r = launch_conv<256, 1, false, false, 1>(st, net, 11, batch, h, w, A, desc, 256)) != MV_OK) return r;
+    MV_PROF_END(st);
+    MV_PROF_BEGIN(st, "k_sp_min_gap");
+    hipLaunchKernelGGL(k_sp_min_gap, dim3((unsigned)batch, 2), dim3(SP_NT), 0, st, semi, desc, (long)h * w,
+                       net->dq_semi, net->dq_desc, semi_scale, desc_scale);
+    MV_LAUNCH_CHECK();
+    MV_PROF_END(st);
+    return MV_OK;
+}

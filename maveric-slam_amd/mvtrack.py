@@ -55,6 +55,14 @@ class KpParams(ctypes.Structure):
     _fields_ = [("conf_thresh", _F), ("nms_dist", _I), ("border", _I)]
 
 
+class SpLayer(ctypes.Structure):
+    _fields_ = [("w", _P), ("bias", _P), ("cin", _I), ("cout", _I), ("k", _I), ("w_scale", _D), ("out_scale", _D)]
+
+
+class SpWeights(ctypes.Structure):
+    _fields_ = [("in_scale", _D), ("layer", SpLayer * 12)]
+
+
 class TrackParams(ctypes.Structure):
     _fields_ = [("window", WindowParams), ("pose", PoseParams), ("top_n", _I), ("valid_cap", _I)]
 
@@ -126,6 +134,9 @@ def lib():
             "mv_pose_normal_equations_dev": (_I, [_P, _I, _P, _P, _P, _P, _P]),
             "mv_lba_schur_dev": (_I, [_P, _I, _I, _I, _I, _I, _P, _P]),
             "mv_pose_batch_dev": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P]),
+            "mv_superpoint_create": (_I, [_P, _P, ctypes.POINTER(_P)]),
+            "mv_superpoint_destroy": (_I, [_P]),
+            "mv_superpoint_forward_dev": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
             "mv_pose_from_matches_dev": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
             "mv_ransac_stub_host": (_I, [_P, _I, _P, _P, _F, _P, _P, _P]),
             "mv_recover_pose_host": (_I, [_P, _P, _P, _P, _P]),
@@ -676,3 +687,111 @@ class Context:
         check(lib().mv_pose_from_matches_dev(self.h, ctypes.byref(params), B, cap, _t(n0), _t(match_idx), _t(kp0),
                                              _t(kp1), _t(T), _t(num_matches), _t(num_inliers), _t(status)),
               "pose_from_matches")
+
+
+# ---------------- quantized SuperPoint front-end (include/superpoint.h) ----------------
+SP_LAYERS = ("conv1a", "conv1b", "conv2a", "conv2b", "conv3a", "conv3b", "conv4a", "conv4b",
+             "convPa", "convPb", "convDa", "convDb")
+
+
+def superpoint_weights(src):
+    """Weights dict (<layer>_w, <layer>_bias, <layer>_meta = [w_scale, w_zp, out_scale, out_zp],
+    input_scale) from the reference's TorchScript archive (read without unpickling or running it:
+    sp_weights.load_superpoint), from an .npz of that layout, or from such a dict."""
+    if isinstance(src, dict):
+        return src
+    if str(src).endswith(".npz"):
+        return dict(np.load(src, allow_pickle=False))
+    import sp_weights
+
+    L = sp_weights.load_superpoint(src)
+    out = {"input_scale": np.float64(L["input"]["scale"])}
+    for n in SP_LAYERS:
+        d = L[n]
+        if d["w_zp"] != 0 or d["out_zp"] != 0:
+            raise MVError("%s: non-zero zero points are not supported" % n)
+        out[n + "_w"], out[n + "_bias"] = d["w"], d["bias"]
+        out[n + "_meta"] = np.array([d["w_scale"], d["w_zp"], d["out_scale"], d["out_zp"]], np.float64)
+    return out
+
+
+class SuperPoint:
+    """The quantized SuperPoint network on the GPU (mv_superpoint_*): uint8 frames [B][H][W] ->
+    Frame-layout int8 semi [B][cells][65], desc [B][cells][256] and their run() scales."""
+
+    def __init__(self, ctx, weights):
+        W = superpoint_weights(weights)
+        sw = SpWeights()
+        sw.in_scale = float(W["input_scale"])
+        keep = []
+        for i, n in enumerate(SP_LAYERS):
+            w = np.ascontiguousarray(W[n + "_w"], np.int8)
+            b = np.ascontiguousarray(W[n + "_bias"], np.float32)
+            meta = W[n + "_meta"]
+            keep += [w, b]
+            L = sw.layer[i]
+            L.w, L.bias = w.ctypes.data, b.ctypes.data
+            L.cout, L.cin, L.k = w.shape[0], w.shape[1], w.shape[2]
+            L.w_scale, L.out_scale = float(meta[0]), float(meta[2])
+        h = _P()
+        check(lib().mv_superpoint_create(ctx.h, ctypes.byref(sw), ctypes.byref(h)), "superpoint_create")
+        self.h, self.ctx = h, ctx
+
+    def close(self):
+        if self.h:
+            lib().mv_superpoint_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def forward(self, images, oh=192, ow=640, out=None):
+        """images: torch uint8 [B][H][W] on the context's device; returns (semi, desc,
+        semi_scale, desc_scale) torch tensors (or fills `out`, the same four)"""
+        import torch
+
+        B, H, W = images.shape
+        cells = (oh // 8) * (ow // 8)
+        if out is None:
+            dev = images.device
+            out = (torch.empty((B, cells, 65), dtype=torch.int8, device=dev),
+                   torch.empty((B, cells, 256), dtype=torch.int8, device=dev),
+                   torch.empty(B, dtype=torch.float32, device=dev), torch.empty(B, dtype=torch.float32, device=dev))
+        semi, desc, ss, ds = out
+        check(lib().mv_superpoint_forward_dev(self.ctx.h, self.h, B, H, W, oh, ow, _t(images), _t(semi), _t(desc),
+                                              _t(ss), _t(ds)), "superpoint_forward")
+        return semi, desc, ss, ds
+
+
+class SuperPointFrontend:
+    """Mirror of SuperPointFrontend (python/superpoint_inference.py:86-208) on the GPU: the
+    network from the same archive (read without unpickling), run() on one frame.  run() takes the
+    8-bit grayscale frame as decoded (the driver's / 255 and resize to 192 x 640,
+    superpoint_inference.py:613-628, happen on the GPU) and returns run()'s
+    (scale0, q_outs0 [1, 65, Hc, Wc], scale1, q_outs1 [1, 256, Hc, Wc], None): the int8 codes as
+    torch int32 tensors like the reference's .int(); the float network outputs are not kept."""
+
+    def __init__(self, weights_path, nms_dist=4, conf_thresh=0.015, nn_thresh=0.7, cuda=True, ctx=None, size=(192, 640)):
+        self.name = "SuperPoint"
+        self.nms_dist, self.conf_thresh, self.nn_thresh = nms_dist, conf_thresh, nn_thresh
+        self.cell, self.border_remove = 8, 4
+        self.ctx = ctx or Context(0)
+        self.net = SuperPoint(self.ctx, weights_path)
+        self.size = size
+
+    def run(self, img):
+        import torch
+
+        img = torch.as_tensor(np.ascontiguousarray(img, np.uint8)).cuda()
+        oh, ow = self.size
+        stream = torch.cuda.current_stream()
+        self.ctx.set_stream(stream)
+        semi, desc, ss, ds = self.net.forward(img[None], oh, ow)
+        torch.cuda.synchronize()
+        hc, wc = oh // 8, ow // 8
+        q0 = semi[0].view(wc, hc, 65).permute(2, 1, 0)[None].int()
+        q1 = desc[0].view(wc, hc, 256).permute(2, 1, 0)[None].int()
+        return float(ss[0].item()), q0, float(ds[0].item()), q1, None

@@ -151,8 +151,8 @@ static int cmp_float(const void *a, const void *b) {
 
 /* run()'s per-output quantisation (superpoint_inference.py:199-206) of the int8 network output
  * q [C][hc][wc] (its dequantised values (float) q * (float) scale) into out [cells][C]
- * (cell p = gx * hc + gy); returns scale0 (0 if fewer than two distinct values: torch.min of
- * an empty tensor raises there) */
+ * (cell p = gx * hc + gy); returns scale0 (0 if fewer than two distinct values -- torch.min of
+ * an empty tensor raises there -- and then the raw codes are written) */
 ORC_EXPORT float orc_sp_min_gap(const int8_t *q, int C, int hc, int wc, double scale, int8_t *out) {
     const float s = (float)scale;
     int present[256] = {0};
@@ -168,11 +168,16 @@ ORC_EXPORT float orc_sp_min_gap(const int8_t *q, int C, int hc, int wc, double s
         const float d = vals[i] - vals[i - 1];
         if (d > 0.f && d < g) g = d;
     }
-    if (nv < 2) return 0.f;
+    if (nv < 2) g = 0.f; /* the raw codes are written */
     for (int c = 0; c < C; c++)
         for (int gy = 0; gy < hc; gy++)
             for (int gx = 0; gx < wc; gx++) {
-                const float f = (float)q[((size_t)c * hc + gy) * wc + gx] * s;
+                const int8_t qv = q[((size_t)c * hc + gy) * wc + gx];
+                if (g == 0.f) {
+                    out[((size_t)gx * hc + gy) * C + c] = qv;
+                    continue;
+                }
+                const float f = (float)qv * s;
                 float r = nearbyintf(f / g);
                 r = r < -128.f ? -128.f : (r > 127.f ? 127.f : r);
                 out[((size_t)gx * hc + gy) * C + c] = (int8_t)r;

@@ -171,6 +171,7 @@ def test_min_gap_edge_cases(orc):
     lib = orc.lib()
     # one distinct value: torch.min of an empty tensor raises in the reference; the oracle says 0
     assert lib.orc_sp_min_gap(q.ctypes.data_as(ctypes.c_void_p), 3, 2, 2, 0.5, out.ctypes.data_as(ctypes.c_void_p)) == 0
+    assert (out == 0).all()
     q[0, 0, 0], q[1, 1, 1] = 5, -7  # gaps of 5 and 7 codes: scale0 = 5 s, values rounded to 1 / -1.4 -> -1
     g = lib.orc_sp_min_gap(q.ctypes.data_as(ctypes.c_void_p), 3, 2, 2, 0.5, out.ctypes.data_as(ctypes.c_void_p))
     assert g == np.float32(2.5)
