@@ -53,6 +53,9 @@ static_assert(epi_bytes<D_NW>() <= D_OFF_ROW, "the epilogue fits staging + ring"
 static_assert(D_LDS <= 160 * 1024, "one workgroup per CU");
 constexpr int D_PF = 1;       // k32 steps of B fragments read ahead of the MFMAs
 constexpr int QS_LOAD = 1;    // the k32 step whose slot issues the quantisation's staging reads
+#ifndef D_EXPE
+#define D_EXPE 1  // per-column scale exponent from m's exponent bits (else by comparisons)
+#endif
 #ifndef D_QB
 #define D_QB 4  // A phase: frame-0 row quads in flight per wave (4 x 16-B loads per lane each)
 #endif
@@ -131,7 +134,7 @@ __device__ __forceinline__ void dma_half(const float *B, int h, int n1, int wu, 
 // Quantise staging slot `stg` (frame-1 rows j0 .. j0 + 31) into rows 32 hh .. +31 of the int8
 // tile slot `rq`: thread t takes floats 16 sub .. +15 of row t >> 4.  In stages, so that the
 // sweep spreads them over its MFMA steps; branch-free, so that a segment stays one basic block.
-//   IK: q_j = 127 * 2^e_j (e_j = 2, 1, 0 for m_j <= 1/4, <= 1/2, above), the per-column word
+//   IK: q_j = 127 * 2^e_j (e_j = 2, 1, 0 for m_j < 1/4, < 1/2, above), the per-column word
 //       = the key shift tb + 2 - e_j; rows j >= n1 (padding) get q = 0 (zero codes: D = 0).
 //   float: q_j = RN(127 RN(1/m_j)), the per-column word = s_j = RN(m_j RN(1/127)).
 // Statistics over the rows below n1 of real halves (`live`: a half past the end holds stale
@@ -171,9 +174,16 @@ struct QHalf {
         qa = qa + qb;
         row16_max_sum(m, qa);  // qa = |b|^2 from here on
         if constexpr (IK) {
+#if D_EXPE
+            // e from m's biased exponent: [1/2, 2) -> 0, [1/4, 1/2) -> 1, below -> 2 (m q_e < 128)
+            const int e = min(max(126 - (int)((__float_as_uint(m) >> 23) & 0xffu), 0), 2);
+            q = j < n1 ? __builtin_ldexpf(127.f, e) : 0.f;
+            s = __builtin_ldexpf(1.f / 127.f, -e);  // = 1 / q rounded: the Eb bound
+#else
             const int e = m > 0.5f ? 0 : (m > 0.25f ? 1 : 2);
             q = j < n1 ? (e == 0 ? 127.f : (e == 1 ? 254.f : 508.f)) : 0.f;
             s = e == 0 ? (1.f / 127.f) : (e == 1 ? (1.f / 254.f) : (1.f / 508.f));  // >= 1/q: Eb bound
+#endif
             sh = tb + 2 - e;
         } else {
             q = m > 0.f ? 127.f * __builtin_amdgcn_rcpf(m) : 0.f;

@@ -15,9 +15,10 @@
 //                 clamp (relu) -> the 2 x 2 max pool on the int32 accumulators (requantisation is
 //                 monotonic: the max commutes with it) -> NHWC int8, or for the two heads the
 //                 Frame layout [cells][C] (cell = gx * rows + gy).
-//   k_sp_min_gap  run()'s output quantisation (superpoint_inference.py:199-206): the 256-code
-//                 presence mask of one head of one frame, the smallest float gap between its
-//                 present dequantised values, then every value rounded to that step, in place.
+//   k_sp_presence / k_sp_min_gap  run()'s output quantisation (superpoint_inference.py:199-206):
+//                 the 256-code presence mask of each head of each frame (32 workgroups per head),
+//                 the smallest float gap between its present dequantised values, then every value
+//                 rounded to that step, in place.
 // Bounds: MFMA i8 (2 x 10.4 GMAC per 192 x 640 frame) with HBM beside it (~16 MB of int8
 // activations written and read per frame).
 #include <math.h>
@@ -48,12 +49,22 @@ constexpr int SP_NT = 256;          // 4 waves
 constexpr int TY = 16, TX = 32;     // conv output tile (before pooling)
 constexpr int C1_TY = 16, C1_TX = 64;  // conv1a output tile
 
-__device__ __forceinline__ float requant_f(int acc, float rs, float lo) {
-    float v = __builtin_rintf((float)acc * rs);
-    return fminf(fmaxf(v, lo), 127.f);
+// Requantisation, bit-identical to clamp(rint((float) a * rs), lo, 127): the product rounded to
+// float, + 1.5 * 2^23 rounds it to an integer (round to nearest even) held in the low mantissa
+// bits, v_med3_i32 clamps on those bits (monotonic: out-of-range sums clamp to the right end),
+// and the code is the low byte (the magic's low byte is 0).  lo_bits: MAGIC_BITS + lo.
+constexpr float SP_MAGIC = 12582912.0f;
+constexpr int SP_MAGIC_BITS = 0x4B400000;
+__device__ __forceinline__ int requant_bits(int a, float rs, int lo_bits) {
+    const float f = (float)a * rs;
+    const int bits = __float_as_int(f + SP_MAGIC);
+    return max(min(bits, SP_MAGIC_BITS + 127), lo_bits);
 }
-__device__ __forceinline__ int pack4i(float a, float b, float c, float d) {
-    return ((int)a & 0xff) | (((int)b & 0xff) << 8) | (((int)c & 0xff) << 16) | ((int)d << 24);
+// low bytes of four requantised words -> one dword
+__device__ __forceinline__ int pack4b(int a, int b, int c, int d) {
+    const unsigned ab = __builtin_amdgcn_perm((unsigned)b, (unsigned)a, 0x0c0c0400u);
+    const unsigned cd = __builtin_amdgcn_perm((unsigned)d, (unsigned)c, 0x0c0c0400u);
+    return (int)__builtin_amdgcn_perm(cd, ab, 0x05040100u);
 }
 
 // torch's bilinear source index (align_corners=False): lambda1, i0, i1
@@ -111,16 +122,16 @@ __global__ __launch_bounds__(SP_NT) void k_sp_conv1a(const uint8_t *__restrict__
             i32x4 o;
 #pragma unroll
             for (int d = 0; d < 4; d++) {
-                float v[4];
+                int v[4];
 #pragma unroll
                 for (int e = 0; e < 4; e++) {
                     const int co = 16 * g + 4 * d + e;
-                    int acc = __builtin_amdgcn_sdot4(p0, wpk[3 * co], 0, false);
+                    int acc = __builtin_amdgcn_sdot4(p0, wpk[3 * co], bq[co], false);
                     acc = __builtin_amdgcn_sdot4(p1, wpk[3 * co + 1], acc, false);
                     acc = __builtin_amdgcn_sdot4(p2, wpk[3 * co + 2], acc, false);
-                    v[e] = requant_f(acc + bq[co], rs, 0.f);
+                    v[e] = requant_bits(acc, rs, SP_MAGIC_BITS);
                 }
-                o[d] = pack4i(v[0], v[1], v[2], v[3]);
+                o[d] = pack4b(v[0], v[1], v[2], v[3]);
             }
             dst[g] = o;
         }
@@ -212,7 +223,7 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv(const int8_t *__restrict__
     }
 
     // ---- epilogue: lane = pixel fr of each row; 16 couts (4 groups of 4) per 32-cout block ----
-    const float lo = RELU ? 0.f : -128.f;
+    const int lo = SP_MAGIC_BITS + (RELU ? 0 : -128);
     if constexpr (POOL) {
         const int Ho = H / 2, Wo = W / 2;
 #pragma unroll
@@ -231,10 +242,10 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv(const int8_t *__restrict__
 #pragma unroll
                     for (int qq = 0; qq < 4; qq++) {
                         const int co = 64 * g + 32 * cb + 8 * qq + 4 * fh;
-                        float v[4];
+                        int v[4];
 #pragma unroll
-                        for (int e = 0; e < 4; e++) v[e] = requant_f(m[4 * qq + e] + bq[co + e], rs, lo);
-                        *reinterpret_cast<int *>(dst + co) = pack4i(v[0], v[1], v[2], v[3]);
+                        for (int e = 0; e < 4; e++) v[e] = requant_bits(m[4 * qq + e] + bq[co + e], rs, lo);
+                        *reinterpret_cast<int *>(dst + co) = pack4b(v[0], v[1], v[2], v[3]);
                     }
                 }
             }
@@ -251,15 +262,15 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv(const int8_t *__restrict__
 #pragma unroll
                 for (int qq = 0; qq < 4; qq++) {
                     const int co = 64 * g + 32 * cb + 8 * qq + 4 * fh;
-                    float v[4];
+                    int v[4];
 #pragma unroll
-                    for (int e = 0; e < 4; e++) v[e] = requant_f(acc[j][cb][4 * qq + e] + bq[co + e], rs, lo);
+                    for (int e = 0; e < 4; e++) v[e] = requant_bits(acc[j][cb][4 * qq + e] + bq[co + e], rs, lo);
                     if (OMODE == 0 || (cstride % 4 == 0 && co + 4 <= cstride)) {
-                        *reinterpret_cast<int *>(dst + co) = pack4i(v[0], v[1], v[2], v[3]);
+                        *reinterpret_cast<int *>(dst + co) = pack4b(v[0], v[1], v[2], v[3]);
                     } else {
 #pragma unroll
                         for (int e = 0; e < 4; e++)
-                            if (co + e < cstride) dst[co + e] = (int8_t)(int)v[e];
+                            if (co + e < cstride) dst[co + e] = (int8_t)v[e];
                     }
                 }
             }
@@ -267,43 +278,162 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv(const int8_t *__restrict__
     }
 }
 
-// run()'s output quantisation of head h (0: semi, C = 65; 1: desc, C = 256) of frame b, in place
-__global__ __launch_bounds__(SP_NT) void k_sp_min_gap(int8_t *__restrict__ semi, int8_t *__restrict__ desc, long cells,
-                                                      float s_semi, float s_desc, float *__restrict__ semi_scale,
-                                                      float *__restrict__ desc_scale) {
-    __shared__ unsigned pres[8];
-    __shared__ float gmin[SP_NT / 64];
-    const int b = blockIdx.x, h = blockIdx.y, t = threadIdx.x, lane = t & 63;
-    const int C = h ? 256 : 65;
-    const float s = h ? s_desc : s_semi;
-    int8_t *base = (h ? desc : semi) + (size_t)b * cells * C;
-    const long n = cells * C;
-    if (t < 8) pres[t] = 0u;
-    __syncthreads();
-    unsigned m[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    for (long i = t; i < n; i += SP_NT) {
-        const int v = base[i] + 128;
-        const unsigned bit = 1u << (v & 31);
+// The 1 x 1 heads (convPb, convDb: 256 input channels, no halo): the same wave tiling and
+// epilogue as k_sp_conv, with the pixels' channel chunks read straight from HBM / L2 (a 256-B
+// row per pixel, every byte used once: no LDS tile to stage), 2 k32 steps ahead.
+template <int OMODE>
+__global__ __launch_bounds__(SP_NT, 2) void k_sp_conv1x1(const int8_t *__restrict__ in, int H, int W,
+                                                         const i32x4 *__restrict__ wf, const int *__restrict__ bq,
+                                                         float rs, int ngroups, int tiles_x, int tiles_y,
+                                                         int8_t *__restrict__ out, int cstride) {
+    constexpr int NS = 8;  // 256 channels
+    int bid = blockIdx.x;
+    const int tx = bid % tiles_x;
+    bid /= tiles_x;
+    const int ty = bid % tiles_y;
+    bid /= tiles_y;
+    const int g = bid % ngroups, b = bid / ngroups;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, fr = lane & 31, fh = lane >> 5;
+    const int y0 = ty * TY, x0 = tx * TX, gx = x0 + fr, gxc = min(gx, W - 1);
+    const i32x4 *px[4];
 #pragma unroll
-        for (int k = 0; k < 8; k++) m[k] |= (v >> 5) == k ? bit : 0u;
+    for (int j = 0; j < 4; j++) {
+        const int gyc = min(y0 + 4 * w + j, H - 1);
+        px[j] = reinterpret_cast<const i32x4 *>(in + (((size_t)b * H + gyc) * W + gxc) * 256) + fh;
+    }
+    const i32x4 *wa = wf + (size_t)(2 * g) * NS * 64 + lane, *wb = wa + NS * 64;
+    i32x4 bq_[3][4], aq[3][2];
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) bq_[s][j] = px[j][2 * s];
+        aq[s][0] = wa[s * 64];
+        aq[s][1] = wb[s * 64];
+    }
+    i32x16 acc[4][2];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        acc[j][0] = i32x16{};
+        acc[j][1] = i32x16{};
     }
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-        unsigned x = m[k];
+    for (int s = 0; s < NS; s++) {
+        if (s + 2 < NS) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) bq_[(s + 2) % 3][j] = px[j][2 * (s + 2)];
+            aq[(s + 2) % 3][0] = wa[(s + 2) * 64];
+            aq[(s + 2) % 3][1] = wb[(s + 2) * 64];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            acc[j][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aq[s % 3][0], bq_[s % 3][j], acc[j][0], 0, 0, 0);
+            acc[j][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aq[s % 3][1], bq_[s % 3][j], acc[j][1], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    const int lo = SP_MAGIC_BITS - 128;  // the heads have no relu
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int gy = y0 + 4 * w + j;
+        if (gy >= H || gx >= W) continue;
+        int8_t *dst = OMODE == 0 ? out + (((size_t)b * H + gy) * W + gx) * cstride
+                                 : out + ((size_t)b * H * W + (size_t)gx * H + gy) * cstride;
+#pragma unroll
+        for (int cb = 0; cb < 2; cb++) {
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) {
+                const int co = 64 * g + 32 * cb + 8 * qq + 4 * fh;
+                int v[4];
+#pragma unroll
+                for (int e = 0; e < 4; e++) v[e] = requant_bits(acc[j][cb][4 * qq + e] + bq[co + e], rs, lo);
+                if (OMODE == 0 || (cstride % 4 == 0 && co + 4 <= cstride)) {
+                    *reinterpret_cast<int *>(dst + co) = pack4b(v[0], v[1], v[2], v[3]);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; e++)
+                        if (co + e < cstride) dst[co + e] = (int8_t)v[e];
+                }
+            }
+        }
+    }
+}
+
+// run()'s output quantisation (superpoint_inference.py:199-206), head h (0: semi, C = 65;
+// 1: desc, C = 256) of frame b, split over SP_MG_CHUNKS workgroups per head: k_sp_presence ORs
+// the 256-code presence mask of a chunk into pres[b][h][8]; k_sp_min_gap derives the smallest
+// gap between present dequantised codes (every workgroup, from the same mask) and rounds its
+// chunk to that step in place.
+constexpr int SP_MG_CHUNKS = 32;
+
+__device__ __forceinline__ void sp_head(int8_t *semi, int8_t *desc, long cells, int b, int h, int8_t *&base, long &lo,
+                                        long &hi) {
+    const int C = h ? 256 : 65;
+    base = (h ? desc : semi) + (size_t)b * cells * C;
+    const long n = cells * C, per = ((n + SP_MG_CHUNKS - 1) / SP_MG_CHUNKS + 15) / 16 * 16;
+    lo = min(n, per * blockIdx.z);
+    hi = min(n, lo + per);
+}
+
+__global__ __launch_bounds__(SP_NT) void k_sp_presence(const int8_t *__restrict__ semi, const int8_t *__restrict__ desc,
+                                                       long cells, unsigned *__restrict__ pres) {
+    const int b = blockIdx.x, h = blockIdx.y, t = threadIdx.x, lane = t & 63;
+    int8_t *base;
+    long lo, hi;
+    sp_head(const_cast<int8_t *>(semi), const_cast<int8_t *>(desc), cells, b, h, base, lo, hi);
+    unsigned m[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    const bool al = ((uintptr_t)(base + lo) & 15) == 0;
+    for (long i = lo + 16 * t; i < hi; i += 16 * SP_NT) {
+        int v4[4];
+        if (al && i + 16 <= hi) {
+            const i32x4 v = *reinterpret_cast<const i32x4 *>(base + i);
+            v4[0] = v[0], v4[1] = v[1], v4[2] = v[2], v4[3] = v[3];
+        } else {
+            for (int k = 0; k < 4; k++) {
+                int x = 0;
+                for (int e = 0; e < 4; e++) {
+                    const long j = i + 4 * k + e;
+                    // past the chunk: repeat its first code (already present)
+                    x |= ((j < hi ? base[j] : base[lo]) & 0xff) << (8 * e);
+                }
+                v4[k] = x;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int v = ((v4[k] << (24 - 8 * e)) >> 24) + 128;
+                const unsigned bit = 1u << (v & 31);
+#pragma unroll
+                for (int q = 0; q < 8; q++) m[q] |= (v >> 5) == q ? bit : 0u;
+            }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        unsigned x = m[q];
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) x |= __shfl_xor(x, o, 64);
-        if (lane == 0 && x) atomicOr(&pres[k], x);
+        if (lane == 0 && x) atomicOr(&pres[(b * 2 + h) * 8 + q], x);
     }
-    __syncthreads();
+}
+
+__global__ __launch_bounds__(SP_NT) void k_sp_min_gap(int8_t *__restrict__ semi, int8_t *__restrict__ desc, long cells,
+                                                      float s_semi, float s_desc, const unsigned *__restrict__ pres,
+                                                      float *__restrict__ semi_scale, float *__restrict__ desc_scale) {
+    __shared__ float gmin[SP_NT / 64];
+    __shared__ int cnts[SP_NT / 64];
+    const int b = blockIdx.x, h = blockIdx.y, t = threadIdx.x, lane = t & 63;
+    const float s = h ? s_desc : s_semi;
+    const unsigned *pm = pres + (b * 2 + h) * 8;
     // thread v: the gap from code v (present) to the next present code, in dequantised floats
     float gap = INFINITY;
-    int cnt = 0;
+    int cnt;
     {
         const int v = t;
-        const bool here = (pres[v >> 5] >> (v & 31)) & 1u;
+        const bool here = (pm[v >> 5] >> (v & 31)) & 1u;
         int nx = -1;
         for (int u = v + 1; u < 256 && nx < 0; u++)
-            if ((pres[u >> 5] >> (u & 31)) & 1u) nx = u;
+            if ((pm[u >> 5] >> (u & 31)) & 1u) nx = u;
         if (here && nx >= 0) {
             const float d = (float)(nx - 128) * s - (float)(v - 128) * s;
             gap = d > 0.f ? d : INFINITY;
@@ -315,7 +445,6 @@ __global__ __launch_bounds__(SP_NT) void k_sp_min_gap(int8_t *__restrict__ semi,
         gap = fminf(gap, __shfl_xor(gap, o, 64));
         cnt += __shfl_xor(cnt, o, 64);
     }
-    __shared__ int cnts[SP_NT / 64];
     if (lane == 0) {
         gmin[t >> 6] = gap;
         cnts[t >> 6] = cnt;
@@ -329,9 +458,12 @@ __global__ __launch_bounds__(SP_NT) void k_sp_min_gap(int8_t *__restrict__ semi,
         distinct += cnts[k];
     }
     if (distinct < 2) g = 0.f;
-    if (t == 0) (h ? desc_scale : semi_scale)[b] = g;
+    if (t == 0 && blockIdx.z == 0) (h ? desc_scale : semi_scale)[b] = g;
     if (g == 0.f) return;  // fewer than two distinct values: the raw codes stay
-    for (long i = t; i < n; i += SP_NT) {
+    int8_t *base;
+    long lo, hi;
+    sp_head(semi, desc, cells, b, h, base, lo, hi);
+    for (long i = lo + t; i < hi; i += SP_NT) {
         const float f = (float)base[i] * s;
         float r = __builtin_rintf(f / g);
         r = fminf(fmaxf(r, -128.f), 127.f);
@@ -347,6 +479,21 @@ int launch_conv(hipStream_t st, const mv_superpoint *net, int li, int B, int H, 
     MV_REQUIRE(blocks < (1l << 31));
     const char *wd = static_cast<const char *>(net->wdev);
     hipLaunchKernelGGL((k_sp_conv<CIN, KS, POOL, RELU, OMODE>), dim3((unsigned)blocks), dim3(SP_NT), 0, st, in, H, W,
+                       reinterpret_cast<const i32x4 *>(wd + net->frag_off[li]),
+                       reinterpret_cast<const int *>(wd + net->bq_off[li]), net->rs[li], ngroups, tiles_x, tiles_y,
+                       out, cstride);
+    MV_LAUNCH_CHECK();
+    return MV_OK;
+}
+
+template <int OMODE>
+int launch_conv1x1(hipStream_t st, const mv_superpoint *net, int li, int B, int H, int W, const int8_t *in,
+                   int8_t *out, int cstride) {
+    const int tiles_x = (W + TX - 1) / TX, tiles_y = (H + TY - 1) / TY, ngroups = net->cout_pad[li] / 64;
+    const long blocks = (long)B * ngroups * tiles_y * tiles_x;
+    MV_REQUIRE(blocks < (1l << 31));
+    const char *wd = static_cast<const char *>(net->wdev);
+    hipLaunchKernelGGL((k_sp_conv1x1<OMODE>), dim3((unsigned)blocks), dim3(SP_NT), 0, st, in, H, W,
                        reinterpret_cast<const i32x4 *>(wd + net->frag_off[li]),
                        reinterpret_cast<const int *>(wd + net->bq_off[li]), net->rs[li], ngroups, tiles_x, tiles_y,
                        out, cstride);
@@ -469,7 +616,8 @@ extern "C" int mv_superpoint_forward_dev(mv_context *ctx, mv_superpoint *net, in
     MV_HIP_TRY(hipSetDevice(ctx->device));
     // activation buffers: A holds conv1a's output (the largest), B conv1b's pooled output
     const size_t a_bytes = mv::align_up((size_t)batch * oh * ow * 64, 256);
-    const size_t need = a_bytes + (size_t)batch * (oh / 2) * (ow / 2) * 64;
+    const size_t b_bytes = mv::align_up((size_t)batch * (oh / 2) * (ow / 2) * 64, 256);
+    const size_t need = a_bytes + b_bytes + (size_t)batch * 2 * 8 * sizeof(unsigned);  // + presence masks
     if (net->act_bytes < need) {
         if (net->act) {
             const int q = mv::quiesce(ctx);
@@ -509,13 +657,18 @@ extern "C" int mv_superpoint_forward_dev(mv_context *ctx, mv_superpoint *net, in
     if ((r = launch_conv<128, 3, false, true, 0>(st, net, 7, batch, h, w, A, Bf, 128)) != MV_OK) return r;
     // heads: Bf holds the shared encoder output
     if ((r = launch_conv<128, 3, false, true, 0>(st, net, 8, batch, h, w, Bf, A, 256)) != MV_OK) return r;
-    if ((r = launch_conv<256, 1, false, false, 1>(st, net, 9, batch, h, w, A, semi, 65)) != MV_OK) return r;
+    if ((r = launch_conv1x1<1>(st, net, 9, batch, h, w, A, semi, 65)) != MV_OK) return r;
     if ((r = launch_conv<128, 3, false, true, 0>(st, net, 10, batch, h, w, Bf, A, 256)) != MV_OK) return r;
-    if ((r = launch_conv<256, 1, false, false, 1>(st, net, 11, batch, h, w, A, desc, 256)) != MV_OK) return r;
+    if ((r = launch_conv1x1<1>(st, net, 11, batch, h, w, A, desc, 256)) != MV_OK) return r;
     MV_PROF_END(st);
     MV_PROF_BEGIN(st, "k_sp_min_gap");
-    hipLaunchKernelGGL(k_sp_min_gap, dim3((unsigned)batch, 2), dim3(SP_NT), 0, st, semi, desc, (long)h * w,
-                       net->dq_semi, net->dq_desc, semi_scale, desc_scale);
+    unsigned *pres = reinterpret_cast<unsigned *>(Bf + b_bytes);
+    MV_HIP_TRY(hipMemsetAsync(pres, 0, (size_t)batch * 2 * 8 * sizeof(unsigned), st));
+    hipLaunchKernelGGL(k_sp_presence, dim3((unsigned)batch, 2, SP_MG_CHUNKS), dim3(SP_NT), 0, st, semi, desc,
+                       (long)h * w, pres);
+    MV_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_sp_min_gap, dim3((unsigned)batch, 2, SP_MG_CHUNKS), dim3(SP_NT), 0, st, semi, desc,
+                       (long)h * w, net->dq_semi, net->dq_desc, pres, semi_scale, desc_scale);
     MV_LAUNCH_CHECK();
     MV_PROF_END(st);
     return MV_OK;

@@ -60,7 +60,7 @@ void mv_pose_params_default(mv_pose_params *p, int semantics) {
     } else {
         p->hypotheses = 256;
         p->inlier_thresh = 1.0f;  // px, cv2.findEssentialMat default
-        p->refine_iters = 10;
+        p->refine_iters = 20;
     }
     p->seed = 0;
 }

@@ -90,12 +90,20 @@ def test_superpoint_frontend_mirror(ctx, torch_cuda, weights):
 
 
 def test_superpoint_into_window_track(ctx, orc, torch_cuda, sp, weights):
-    """frames -> network -> the as-built windowed track (tracking_main.c's path) end to end: the
-    GPU front-end's int8 frames give the oracle's match list of the oracle's frames"""
+    """image -> network -> the windowed int8 track (tracking_main.c's path, both semantics): the
+    GPU front-end's frames give the same matched points as the oracle's front-end + track"""
+    import mvtrack
+
     ims = load_golden("kitti00_images.npz")
     imgs = [ims["img_000000"], ims["img_000001"]]
     semi, desc, ss, ds = _run(ctx, torch_cuda, sp, imgs, 192, 640)
     net = orc.sp_net(weights)
-    o0 = orc.sp_forward(imgs[0], net)
-    o1 = orc.sp_forward(imgs[1], net)
-    assert (semi[0] == o0[0]).all() and (desc[1] == o1[1]).all()
+    ref = [orc.sp_forward(im, net) for im in imgs]
+    frames = [dict(rows=24, cols=80, semi=semi[b], desc=desc[b], semi_scale=np.float32(ss[b])) for b in range(2)]
+    oframes = [dict(rows=24, cols=80, semi=r[0], desc=r[1], semi_scale=np.float32(r[2])) for r in ref]
+    for sem, as_built in ((mvtrack.AS_BUILT, True), (mvtrack.AS_INTENDED, False)):
+        prm = mvtrack.track_params(sem)
+        st, T, p1, p2 = ctx.track_pair_host(prm, 24, 80, frames[0], frames[1])
+        r = orc.track_window(oframes[0], oframes[1], as_built=as_built)
+        assert (p1 == r["points1"]).all() and (p2 == r["points2"]).all()
+        assert len(p1) > 0
