@@ -2,9 +2,10 @@
 // on gfx950: grayscale frames -> int8 semi / desc + scales, bit-identical to the CPU oracle
 // (oracle/sp_oracle.c, itself bit-identical to PyTorch's quantized kernels).
 //
-//   k_sp_conv1a   image -> (/ 255, bilinear resize, quantize) in LDS with a 1-pixel halo ->
-//                 conv1a (Cin = 1: 9 taps as three v_dot4_i32_i8 per output channel) -> relu ->
-//                 NHWC int8 [oh][ow][64].
+//   conv1a        fused into conv1b's workgroups: image -> (/ 255, bilinear resize, quantize) in
+//                 LDS over the tile + 2 pixels -> conv1a (Cin = 1: 9 taps as three v_dot4_i32_i8
+//                 per output channel) + relu over the tile + 1 pixel, written as conv1b's input
+//                 tile -- conv1a's 64-channel full-resolution output never reaches HBM.
 //   k_sp_conv     every other layer as an implicit GEMM on v_mfma_i32_32x32x32_i8: A = the
 //                 layer's weights as MFMA fragments (64 couts per workgroup, prefetched from
 //                 L2 four k32 steps ahead), B = 32 pixels x 32 channels of one tap read from the
@@ -47,7 +48,6 @@ typedef int i32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int SP_NT = 256;          // 4 waves
 constexpr int TY = 16, TX = 32;     // conv output tile (before pooling)
-constexpr int C1_TY = 16, C1_TX = 64;  // conv1a output tile
 
 // Requantisation, bit-identical to clamp(rint((float) a * rs), lo, 127): the product rounded to
 // float, + 1.5 * 2^23 rounds it to an integer (round to nearest even) held in the low mantissa
@@ -80,76 +80,38 @@ __device__ __forceinline__ float sp_src(float scale, int d, int n_in, int &i0, i
     return lam;
 }
 
-__global__ __launch_bounds__(SP_NT) void k_sp_conv1a(const uint8_t *__restrict__ img, int H, int W, int oh, int ow,
-                                                     int tiles_x, float in_inv, const int *__restrict__ wpk,
-                                                     const int *__restrict__ bq, float rs, int8_t *__restrict__ out) {
-    __shared__ int8_t q[C1_TY + 2][C1_TX + 4];
-    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x, b = blockIdx.y;
-    const int y0 = ty * C1_TY, x0 = tx * C1_TX, t = threadIdx.x;
-    const uint8_t *im = img + (size_t)b * H * W;
-    const float sy = (float)H / (float)oh, sx = (float)W / (float)ow;
-    for (int i = t; i < (C1_TY + 2) * (C1_TX + 2); i += SP_NT) {
-        const int r = i / (C1_TX + 2), c = i % (C1_TX + 2);
-        const int gy = y0 + r - 1, gx = x0 + c - 1;
-        int v = 0;
-        if (gy >= 0 && gy < oh && gx >= 0 && gx < ow) {
-            int ya, yb, xa, xb;
-            const float h1 = sp_src(sy, gy, H, ya, yb), w1 = sp_src(sx, gx, W, xa, xb);
-            const float h0 = 1.f - h1, w0 = 1.f - w1;
-            const float a00 = (float)im[(size_t)ya * W + xa] / 255.0f, a01 = (float)im[(size_t)ya * W + xb] / 255.0f;
-            const float a10 = (float)im[(size_t)yb * W + xa] / 255.0f, a11 = (float)im[(size_t)yb * W + xb] / 255.0f;
-            const float t0 = __builtin_fmaf(a00, w0, a01 * w1);
-            const float t1 = __builtin_fmaf(a10, w0, a11 * w1);
-            const float x = __builtin_fmaf(t0, h0, t1 * h1);
-            float qv = __builtin_rintf(x * in_inv);
-            qv = fminf(fmaxf(qv, -128.f), 127.f);
-            v = (int)qv;
-        }
-        q[r][c] = (int8_t)v;
-    }
-    __syncthreads();
-    for (int k = 0; k < C1_TY * C1_TX / SP_NT; k++) {
-        const int p = t + SP_NT * k, r = p / C1_TX, c = p % C1_TX;
-        const int gy = y0 + r, gx = x0 + c;
-        if (gy >= oh || gx >= ow) continue;
-        const int p0 = (q[r][c] & 0xff) | ((q[r][c + 1] & 0xff) << 8) | ((q[r][c + 2] & 0xff) << 16) | ((int)q[r + 1][c] << 24);
-        const int p1 = (q[r + 1][c + 1] & 0xff) | ((q[r + 1][c + 2] & 0xff) << 8) | ((q[r + 2][c] & 0xff) << 16) |
-                       ((int)q[r + 2][c + 1] << 24);
-        const int p2 = q[r + 2][c + 2] & 0xff;
-        i32x4 *dst = reinterpret_cast<i32x4 *>(out + (((size_t)b * oh + gy) * ow + gx) * 64);
-#pragma unroll
-        for (int g = 0; g < 4; g++) {  // 16 channels per 16-B store
-            i32x4 o;
-#pragma unroll
-            for (int d = 0; d < 4; d++) {
-                int v[4];
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    const int co = 16 * g + 4 * d + e;
-                    int acc = __builtin_amdgcn_sdot4(p0, wpk[3 * co], bq[co], false);
-                    acc = __builtin_amdgcn_sdot4(p1, wpk[3 * co + 1], acc, false);
-                    acc = __builtin_amdgcn_sdot4(p2, wpk[3 * co + 2], acc, false);
-                    v[e] = requant_bits(acc, rs, SP_MAGIC_BITS);
-                }
-                o[d] = pack4b(v[0], v[1], v[2], v[3]);
-            }
-            dst[g] = o;
-        }
-    }
-}
-
 // OMODE 0: NHWC [B][Ho][Wo][cstride]; OMODE 1: the Frame layout [B][Ho * Wo][cstride] with
 // cell = x * Ho + y, channels >= cstride not stored (cstride = 65 for semi)
-template <int CIN, int KS, bool POOL, bool RELU, int OMODE>
-__global__ __launch_bounds__(SP_NT, 2) void k_sp_conv(const int8_t *__restrict__ in, int H, int W,
+// conv1a fused in front of conv1b (FUSE1A): the workgroup computes its own input tile -- the
+// image resized and quantised over the tile + 2 pixels into LDS, conv1a + relu over the tile +
+// 1 pixel (zero outside the image: conv1b's padding) -- instead of loading conv1a's output.
+struct Conv1aArgs {
+    const uint8_t *img;
+    int H, W;  // source frame
+    float in_inv, rs;
+    const int *wpk, *bq;
+};
+
+#ifndef SP_OCC64
+#define SP_OCC64 3  // workgroups per CU for the 64-channel layers (LDS 50 KB; VGPRs <= 168)
+#endif
+template <int CIN, int KS, bool POOL, bool RELU, int OMODE, bool FUSE1A = false>
+__global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(const int8_t *__restrict__ in, int H, int W,
                                                       const i32x4 *__restrict__ wf, const int *__restrict__ bq,
                                                       float rs, int ngroups, int tiles_x, int tiles_y,
-                                                      int8_t *__restrict__ out, int cstride) {
+                                                      int8_t *__restrict__ out, int cstride, Conv1aArgs c1) {
     constexpr int P = KS / 2, IY = TY + 2 * P, IX = TX + 2 * P, NCH = CIN / 16, NS = KS * KS * CIN / 32;
-    constexpr int SWS = NCH >= 16 ? 1 : 16 / NCH;  // pixels per 256-B LDS bank row
-    constexpr int PF = 4;                          // weight fragments in flight (k32 steps)
+    constexpr int PF = (CIN == 64 && SP_OCC64 > 2) ? 2 : 4;  // weight fragments in flight (k32 steps)
     static_assert(CIN % 32 == 0 && NCH <= 16, "channels in 32-k steps, at most 256");
-    __shared__ i32x4 tile[IY * IX * NCH];
+    // LDS tile layout.  64 channels: each pixel's 4 chunks padded to 5 (an odd stride: 16 lanes
+    // reading one chunk of 16 consecutive pixels hit 16 distinct bank groups), so a B fragment's
+    // address is a per-lane base + a compile-time offset (ds_read_b128 immediate, no VALU).
+    // 128 channels (the padding would cost the second workgroup per CU): chunk c of pixel x
+    // stored at c ^ ((x / 2) & 7), the lane's XOR term precomputed per tap column.
+    constexpr bool PADL = NCH <= 4;
+    constexpr int PS = PADL ? NCH + 1 : NCH;  // chunks per pixel
+    constexpr int SWS = NCH >= 16 ? 1 : 16 / NCH;
+    __shared__ i32x4 tile[IY * IX * PS];
     int bid = blockIdx.x;
     const int tx = bid % tiles_x;
     bid /= tiles_x;
@@ -158,11 +120,94 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv(const int8_t *__restrict__
     const int g = bid % ngroups, b = bid / ngroups;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, fr = lane & 31, fh = lane >> 5;
     const int y0 = ty * TY, x0 = tx * TX;
+    auto chunk_at = [&](int px, int x, int c) { return px * PS + (PADL ? c : (c ^ ((x / SWS) & (NCH - 1)))); };
 
+    constexpr int NCHUNK = IY * IX * NCH;
+    if constexpr (FUSE1A) {
+        static_assert(CIN == 64 && KS == 3 && PADL, "conv1a feeds conv1b");
+        constexpr int QY = IY + 2, QX = IX + 2, QXS = QX + 2;
+        __shared__ int8_t qim[QY * QXS];
+        __shared__ float lut[256];  // k / 255 (IEEE division), the driver's astype(float32) / 255.
+        lut[t] = (float)t / 255.0f;
+        __syncthreads();
+        const uint8_t *im = c1.img + (size_t)b * c1.H * c1.W;
+        const float sy = (float)c1.H / (float)H, sx = (float)c1.W / (float)W;
+        for (int i = t; i < QY * QX; i += SP_NT) {
+            const int r = i / QX, c = i % QX;
+            const int gy = y0 + r - 2, gx = x0 + c - 2;
+            int v = 0;
+            if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+                int ya, yb, xa, xb;
+                const float h1 = sp_src(sy, gy, c1.H, ya, yb), w1 = sp_src(sx, gx, c1.W, xa, xb);
+                const float h0 = 1.f - h1, w0 = 1.f - w1;
+                const float a00 = lut[im[(size_t)ya * c1.W + xa]], a01 = lut[im[(size_t)ya * c1.W + xb]];
+                const float a10 = lut[im[(size_t)yb * c1.W + xa]], a11 = lut[im[(size_t)yb * c1.W + xb]];
+                const float t0 = __builtin_fmaf(a00, w0, a01 * w1);
+                const float t1 = __builtin_fmaf(a10, w0, a11 * w1);
+                const float x = __builtin_fmaf(t0, h0, t1 * h1);
+                float qv = __builtin_rintf(x * c1.in_inv);
+                qv = fminf(fmaxf(qv, -128.f), 127.f);
+                v = (int)qv;
+            }
+            qim[r * QXS + c] = (int8_t)v;
+        }
+        __syncthreads();
+        // conv1a + relu over the tile + halo on v_mfma_i32_32x32x16_i8: K = the 9 taps (+ 7 zero),
+        // A = the weights (lanes < 32: taps 0-7, lanes >= 32: tap 8), B = 32 tile pixels' taps;
+        // pixels outside the image are conv1b's zero padding, not conv1a evaluated there
+        long a1[2];
+#pragma unroll
+        for (int cb = 0; cb < 2; cb++) {
+            const int co = 32 * cb + fr;
+            const unsigned lo = (unsigned)(fh ? c1.wpk[3 * co + 2] : c1.wpk[3 * co]);
+            const unsigned hi = fh ? 0u : (unsigned)c1.wpk[3 * co + 1];
+            a1[cb] = (long)(((unsigned long long)hi << 32) | lo);
+        }
+        int bias[2][16];
+#pragma unroll
+        for (int cb = 0; cb < 2; cb++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) bias[cb][q] = c1.bq[32 * cb + (q & 3) + 8 * (q >> 2) + 4 * fh];
+        constexpr int NPX = IY * IX, NBLK = (NPX + 31) / 32;
+#pragma unroll 1
+        for (int blk = w; blk < NBLK; blk += SP_NT / 64) {
+            const int px = blk * 32 + fr, pxc = min(px, NPX - 1);
+            const int r = pxc / IX, x = pxc % IX;
+            const int8_t *q0 = qim + r * QXS + x;
+            auto u8 = [](int8_t v) { return (unsigned)(uint8_t)v; };
+            unsigned lo, hi;
+            if (fh == 0) {
+                lo = u8(q0[0]) | (u8(q0[1]) << 8) | (u8(q0[2]) << 16) | (u8(q0[QXS]) << 24);
+                hi = u8(q0[QXS + 1]) | (u8(q0[QXS + 2]) << 8) | (u8(q0[2 * QXS]) << 16) | (u8(q0[2 * QXS + 1]) << 24);
+            } else {
+                lo = u8(q0[2 * QXS + 2]);
+                hi = 0u;
+            }
+            const long bv = (long)(((unsigned long long)hi << 32) | lo);
+            const int gy = y0 + r - 1, gx = x0 + x - 1;
+            const bool in_img = px < NPX && gy >= 0 && gy < H && gx >= 0 && gx < W;
+#pragma unroll
+            for (int cb = 0; cb < 2; cb++) {
+                i32x16 c0;
+#pragma unroll
+                for (int q = 0; q < 16; q++) c0[q] = bias[cb][q];
+                const i32x16 d = __builtin_amdgcn_mfma_i32_32x32x16_i8(a1[cb], bv, c0, 0, 0, 0);
+#pragma unroll
+                for (int qq = 0; qq < 4; qq++) {
+                    int v[4];
+#pragma unroll
+                    for (int e = 0; e < 4; e++) v[e] = requant_bits(d[4 * qq + e], c1.rs, SP_MAGIC_BITS);
+                    const int ch = 32 * cb + 8 * qq + 4 * fh;
+                    if (px < NPX)
+                        reinterpret_cast<int *>(tile + chunk_at(px, x, ch >> 4))[(ch & 15) >> 2] =
+                            in_img ? pack4b(v[0], v[1], v[2], v[3]) : 0;
+                }
+            }
+        }
+    }
     // ---- the input tile (zero outside the image), 8 16-B loads in flight per thread ----
     const int8_t *src = in + (size_t)b * H * W * CIN;
-    constexpr int NCHUNK = IY * IX * NCH;
-    for (int i0 = 0; i0 < NCHUNK; i0 += 8 * SP_NT) {
+    for (int i0 = 0; i0 < (FUSE1A ? 0 : NCHUNK); i0 += 8 * SP_NT) {
         i32x4 v[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
@@ -178,12 +223,12 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv(const int8_t *__restrict__
             const int i = i0 + u * SP_NT + t;
             if (i >= NCHUNK) continue;
             const int c = i % NCH, px = i / NCH, x = px % IX;
-            tile[px * NCH + (c ^ ((x / SWS) & (NCH - 1)))] = v[u];
+            tile[chunk_at(px, x, c)] = v[u];
         }
     }
     __syncthreads();
 
-    // ---- K loop: 9 taps (or 1) x CIN / 32 steps ----
+    // ---- K loop: 9 taps (or 1) x CIN / 32 steps, fully unrolled: every LDS offset a constant ----
     const i32x4 *wa = wf + (size_t)(2 * g) * NS * 64 + lane, *wb = wa + NS * 64;
     i32x4 ra[PF], rb[PF];
 #pragma unroll
@@ -197,29 +242,27 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv(const int8_t *__restrict__
         acc[j][0] = i32x16{};
         acc[j][1] = i32x16{};
     }
-#pragma unroll 1
-    for (int s0 = 0; s0 < NS; s0 += PF) {
+    // per-lane bases: row 4w + j, column fr, chunk half fh (padded layout); XOR terms per kx
+    const i32x4 *lb = tile + ((4 * w) * IX + fr) * PS + (PADL ? fh : 0);
+    int xs[KS];
 #pragma unroll
-        for (int u = 0; u < PF; u++) {
-            const int s = s0 + u;
-            if (s < NS) {
-                const i32x4 a0 = ra[u], a1 = rb[u];
-                if (s + PF < NS) {
-                    ra[u] = wa[(s + PF) * 64];
-                    rb[u] = wb[(s + PF) * 64];
-                }
-                const int tap = s * 32 / CIN, ky = tap / KS, kx = tap % KS;
-                const int c = (s * 32 % CIN) / 16 + fh;
-                const int x = fr + kx;
-                const int sw = c ^ ((x / SWS) & (NCH - 1));
+    for (int kx = 0; kx < KS; kx++) xs[kx] = fh ^ (((fr + kx) / SWS) & (NCH - 1));
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const i32x4 bv = tile[((4 * w + j + ky) * IX + x) * NCH + sw];
-                    acc[j][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bv, acc[j][0], 0, 0, 0);
-                    acc[j][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bv, acc[j][1], 0, 0, 0);
-                }
-            }
+    for (int s = 0; s < NS; s++) {
+        const i32x4 a0 = ra[s % PF], a1 = rb[s % PF];
+        if (s + PF < NS) {
+            ra[s % PF] = wa[(s + PF) * 64];
+            rb[s % PF] = wb[(s + PF) * 64];
         }
+        const int tap = s * 32 / CIN, ky = tap / KS, kx = tap % KS, c0 = (s * 32 % CIN) / 16;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int off = ((j + ky) * IX + kx) * PS;
+            const i32x4 bv = PADL ? lb[off + c0] : lb[off + (c0 ^ xs[kx])];
+            acc[j][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bv, acc[j][0], 0, 0, 0);
+            acc[j][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bv, acc[j][1], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
     }
 
     // ---- epilogue: lane = pixel fr of each row; 16 couts (4 groups of 4) per 32-cout block ----
@@ -471,17 +514,17 @@ __global__ __launch_bounds__(SP_NT) void k_sp_min_gap(int8_t *__restrict__ semi,
     }
 }
 
-template <int CIN, int KS, bool POOL, bool RELU, int OMODE>
+template <int CIN, int KS, bool POOL, bool RELU, int OMODE, bool FUSE1A = false>
 int launch_conv(hipStream_t st, const mv_superpoint *net, int li, int B, int H, int W, const int8_t *in,
-                int8_t *out, int cstride) {
+                int8_t *out, int cstride, Conv1aArgs c1 = Conv1aArgs{}) {
     const int tiles_x = (W + TX - 1) / TX, tiles_y = (H + TY - 1) / TY, ngroups = net->cout_pad[li] / 64;
     const long blocks = (long)B * ngroups * tiles_y * tiles_x;
     MV_REQUIRE(blocks < (1l << 31));
     const char *wd = static_cast<const char *>(net->wdev);
-    hipLaunchKernelGGL((k_sp_conv<CIN, KS, POOL, RELU, OMODE>), dim3((unsigned)blocks), dim3(SP_NT), 0, st, in, H, W,
-                       reinterpret_cast<const i32x4 *>(wd + net->frag_off[li]),
+    hipLaunchKernelGGL((k_sp_conv<CIN, KS, POOL, RELU, OMODE, FUSE1A>), dim3((unsigned)blocks), dim3(SP_NT), 0, st, in,
+                       H, W, reinterpret_cast<const i32x4 *>(wd + net->frag_off[li]),
                        reinterpret_cast<const int *>(wd + net->bq_off[li]), net->rs[li], ngroups, tiles_x, tiles_y,
-                       out, cstride);
+                       out, cstride, c1);
     MV_LAUNCH_CHECK();
     return MV_OK;
 }
@@ -614,9 +657,10 @@ extern "C" int mv_superpoint_forward_dev(mv_context *ctx, mv_superpoint *net, in
     MV_REQUIRE(images && semi && desc && semi_scale && desc_scale && net->device == ctx->device);
     MV_REQUIRE((long)oh * ow * 64 < (1l << 31) && (long)batch * H * W < (1l << 40));
     MV_HIP_TRY(hipSetDevice(ctx->device));
-    // activation buffers: A holds conv1a's output (the largest), B conv1b's pooled output
-    const size_t a_bytes = mv::align_up((size_t)batch * oh * ow * 64, 256);
-    const size_t b_bytes = mv::align_up((size_t)batch * (oh / 2) * (ow / 2) * 64, 256);
+    // activation ping-pong buffers, oh * ow * 16 bytes per frame each (conv1b's pooled output, the
+    // largest after the fused conv1a)
+    const size_t a_bytes = mv::align_up((size_t)batch * oh * ow * 16, 256);
+    const size_t b_bytes = a_bytes;
     const size_t need = a_bytes + b_bytes + (size_t)batch * 2 * 8 * sizeof(unsigned);  // + presence masks
     if (net->act_bytes < need) {
         if (net->act) {
@@ -633,19 +677,14 @@ extern "C" int mv_superpoint_forward_dev(mv_context *ctx, mv_superpoint *net, in
     hipStream_t st = ctx->stream;
     const char *wd = static_cast<const char *>(net->wdev);
     int r;
-    MV_PROF_BEGIN(st, "k_sp_conv1a");
-    {
-        const int tiles_x = (ow + C1_TX - 1) / C1_TX, tiles_y = (oh + C1_TY - 1) / C1_TY;
-        hipLaunchKernelGGL(k_sp_conv1a, dim3((unsigned)(tiles_x * tiles_y), (unsigned)batch), dim3(SP_NT), 0, st,
-                           images, H, W, oh, ow, tiles_x, net->in_inv,
-                           reinterpret_cast<const int *>(wd + net->frag_off[0]),
-                           reinterpret_cast<const int *>(wd + net->bq_off[0]), net->rs[0], A);
-        MV_LAUNCH_CHECK();
-    }
-    MV_PROF_END(st);
     int h = oh, w = ow;
     MV_PROF_BEGIN(st, "k_sp_conv");
-    if ((r = launch_conv<64, 3, true, true, 0>(st, net, 1, batch, h, w, A, Bf, 64)) != MV_OK) return r;
+    {
+        const Conv1aArgs c1{images, H, W, net->in_inv, net->rs[0], reinterpret_cast<const int *>(wd + net->frag_off[0]),
+                            reinterpret_cast<const int *>(wd + net->bq_off[0])};
+        if ((r = launch_conv<64, 3, true, true, 0, true>(st, net, 1, batch, h, w, nullptr, Bf, 64, c1)) != MV_OK)
+            return r;
+    }
     h /= 2, w /= 2;
     if ((r = launch_conv<64, 3, false, true, 0>(st, net, 2, batch, h, w, Bf, A, 64)) != MV_OK) return r;
     if ((r = launch_conv<64, 3, true, true, 0>(st, net, 3, batch, h, w, A, Bf, 64)) != MV_OK) return r;

@@ -81,7 +81,7 @@ def run(batch=64, steps=10, warmup=2, check=1, cpu_seconds=0.0, oh=192, ow=640):
     el = time.perf_counter() - t0
     mvtrack.profile_enable(False)
     stages = {}
-    for k in ("k_sp_conv1a", "k_sp_conv", "k_sp_min_gap"):
+    for k in ("k_sp_conv", "k_sp_min_gap"):
         ms, c = mvtrack.profile_query(k)
         if c:
             stages[k] = round(ms / c, 4)
