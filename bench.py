@@ -696,6 +696,12 @@ def main():
         r = bench_keypoints.run(batch=1024, steps=args.extra_steps, warmup=2, check=1)
         out["keypoints"] = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "stages_ms",
                                                "hbm_roofline", "checked_frames")}
+        # the quantized SuperPoint network (KITTI frames -> int8 semi / desc)
+        import bench_superpoint
+
+        r = bench_superpoint.run(batch=64, steps=args.extra_steps, warmup=2, check=1)
+        out["superpoint"] = {k: r[k] for k in ("metric", "value", "unit", "batch", "ms_per_step", "stages_ms",
+                                                "mfma_roofline", "oracle_exact")}
     if rank == 0:
         print(json.dumps(out), flush=True)
     for cx in ctxs:

@@ -47,6 +47,14 @@ for r in stats:
     short = short_name(name)
     summary["kernels"][short] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                                  "total_ns": float(r["TotalDurationNs"]), "pct": float(r.get("Percentage", 0))}
+# median launch duration from the trace (the mean carries the first, cold launch)
+durs = {}
+for r in rows("trace/**/*kernel_trace.csv"):
+    durs.setdefault(short_name(r.get("Kernel_Name", "?")), []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+for k, v in durs.items():
+    if k in summary["kernels"]:
+        v = sorted(v)
+        summary["kernels"][k]["median_ns"] = float(v[len(v) // 2] if len(v) % 2 else (v[len(v) // 2 - 1] + v[len(v) // 2]) / 2)
 per = {}
 for r in rows("pmc_*/**/*counter_collection.csv"):
     name = short_name(r.get("Kernel_Name", r.get("KernelName", "?")))
