@@ -12,10 +12,10 @@
 //      strided subset of 128 correspondences (LDS broadcast reads);
 //   3. preemption: the 2 best of each wave survive and are MSAC-scored on ALL
 //      correspondences by the whole block; the two lowest (cost, hypothesis id) are the
-//      two starts, one per half of the block (waves 0-1 and 2-3);
+//      starts of the refinement;
 //   4. per start: E = U diag(s1,s2,s3) V^T (closed-form eigenvectors of E^T E), the four
 //      (R, t) candidates R = U W V^T / U W^T V^T, t = +-u3, cheirality vote by triangulated
-//      depth over the inliers;
+//      depth over the inliers (block reduction);
 //   5. per start: robust Gauss-Newton (IRLS) on the Sampson residuals r_i =
 //      (x2^T [t]x R x1) / s_i with Cauchy weights whose scale shrinks from thr towards
 //      2 rms (exact data converges to machine precision, noisy data keeps ~2 sigma),
@@ -24,7 +24,8 @@
 //      src/local_bundle_adjustment.c:161-176), 5x5 Cholesky solve, R <- exp(omega) R,
 //      t <- normalise(t + B d); float throughout (the output is float); stops once the
 //      step is below 1e-6 and the scale settles (refine_iters is the maximum);
-//   6. the refined pose with the lower robust cost (Cauchy at thr, capped at 3 thr) wins.
+//   6. the refined pose with the lower robust cost (Cauchy at thr, capped at 3 thr) wins;
+//      the second start is refined only when the first did not reach an exact fit.
 // Output T = [R | t] with x1 ~ R x0 + t, |t| = 1 (the OpenCV recoverPose convention).
 #include <math.h>
 
@@ -613,9 +614,8 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
         }
     }
     __syncthreads();
-    // ---- 3b. the two lowest (full cost, hypothesis id) survivors are both refined, one per
-    //         half of the block (waves 0-1, 2-3), and the refined pose with the lower robust
-    //         cost wins.  Under pixel noise one start is not enough: the robust cost has local
+    // ---- 3b. the two lowest (full cost, hypothesis id) survivors are the starts of the
+    //         refinement (below), and the refined pose with the lower robust cost wins.  Under pixel noise one start is not enough: the robust cost has local
     //         minima along the rotation / translation-direction ambiguity of forward motion and
     //         the best 8-point sample's pose can sit in one (the same algorithm on the CPU,
     //         0.5-1 px noise, 30 % outliers: single starts end 2-7 deg off in translation
@@ -655,184 +655,186 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
         }
         return;
     }
-    constexpr int HT = NT / 2;  // threads per half
-    static_assert(MAXP <= 32 * HT, "the inlier mask holds 32 correspondences per thread");
-    const int hh = w >> 1, ht = t & (HT - 1);
-    float E[9];
-    for (int r = 0; r < 9; r++) E[r] = s_E[hh][r];
-
-    const long long tk3 = PE_TRACE ? clock64() : 0;
-    // ---- 4. decomposition + cheirality, per half ----
-    __shared__ float s_cand[2][4][12];
-    __shared__ float s_uv[2][2][3][3];
-    if (ht == 0) {
-        float U[3][3], V[3][3];
-        if (PE_NODECOMP) {
-            for (int i = 0; i < 3; i++)
-                for (int j = 0; j < 3; j++) U[i][j] = V[i][j] = i == j;
-        } else {
-            essential_uv(E, U, V);
-        }
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) {
-                s_uv[hh][0][i][j] = U[i][j];
-                s_uv[hh][1][i][j] = V[i][j];
-            }
-    }
-    __syncthreads();
-    if (ht < 4) {  // candidate c = ht, one lane each
-        const float W[3][3] = {{0, -1, 0}, {1, 0, 0}, {0, 0, 1}};
-        float U[3][3], V[3][3];
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) {
-                U[i][j] = s_uv[hh][0][i][j];
-                V[i][j] = s_uv[hh][1][i][j];
-            }
-        const int c = ht;
-        float R[3][3];
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) {
-                float s = 0;
-                for (int k = 0; k < 3; k++) {
-                    float uw = 0;
-                    for (int l = 0; l < 3; l++) uw += U[i][l] * (c < 2 ? W[l][k] : W[k][l]);
-                    s += uw * V[j][k];
-                }
-                R[i][j] = s;
-            }
-        const float sg = (c & 1) ? -1.f : 1.f;
-        for (int i = 0; i < 9; i++) s_cand[hh][c][i] = R[i / 3][i % 3];
-        for (int i = 0; i < 3; i++) s_cand[hh][c][9 + i] = sg * U[i][2];
-    }
-    __syncthreads();
-    int votes[4] = {0, 0, 0, 0};
-    unsigned inl_mask = 0;  // bit k: correspondence ht + k HT is a Sampson inlier of E
-    for (int i = ht, k = 0; i < n; i += HT, k++)
-        inl_mask |= sampson_inlier(E, P[i], a.thr2) ? 1u << k : 0u;
-#pragma unroll
-    for (int c = 0; c < 4; c++) {  // candidate-outer: 12 candidate floats live, not 48
-        for (unsigned mk = inl_mask; mk; mk &= mk - 1) {
-            const float4 p = P[ht + __builtin_ctz(mk) * HT];
-            // depths z1, z2 of the midpoint triangulation, q z1 + t = -m z2 in the least-
-            // squares sense: z = num / det with det > 0, so only the numerators' signs count
-            const float *C = s_cand[hh][c];
-            const F3 q = {{C[0] * p.x + C[1] * p.y + C[2], C[3] * p.x + C[4] * p.y + C[5], C[6] * p.x + C[7] * p.y + C[8]}};
-            const F3 m = {{-p.z, -p.w, -1.f}};
-            const F3 tt = {{C[9], C[10], C[11]}};
-            const float aa = dot3(q, q), ab = dot3(q, m), bb = dot3(m, m);
-            const float ra = -dot3(q, tt), rb = -dot3(m, tt);
-            const float det = aa * bb - ab * ab;
-            const float n1 = ra * bb - ab * rb, n2 = aa * rb - ab * ra;
-            votes[c] += (det > 0.f && n1 > 0.f && n2 > 0.f) ? 1 : 0;
-        }
-    }
-    const long long tk4 = PE_TRACE ? clock64() : 0;
+    // ---- 4-6, per start (a block-uniform loop): decomposition + cheirality, robust
+    //      Gauss-Newton, the robust cost of the refined pose.  The second start is refined only
+    //      when the first did not reach an exact fit (its Cauchy scale still above the floor:
+    //      noisy data) -- exact data costs one refinement, as a single start did. ----
+    __shared__ float s_cand[4][12];
+    __shared__ float s_uv[2][3][3];
     __shared__ int s_votes[4][4];  // [wave][candidate]
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-        int v = votes[c];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        if (lane == 0) s_votes[w][c] = v;
-    }
-    __syncthreads();
-    int bc = 0, bv = s_votes[2 * hh][0] + s_votes[2 * hh + 1][0];
-    for (int c = 1; c < 4; c++) {
-        const int v = s_votes[2 * hh][c] + s_votes[2 * hh + 1][c];
-        if (v > bv) {
-            bv = v;
-            bc = c;
-        }
-    }
-
-    const long long tk5 = PE_TRACE ? clock64() : 0;
-    // ---- 5. robust Gauss-Newton per half: iteratively reweighted, Cauchy weights
-    //         1 / (1 + (r / c)^2) on the Sampson residuals below 3 thr (none above), the scale
-    //         c_0 = thr, c_{k+1} = min(thr, max(2 rms_w, 0.01 thr)) (rms_w: the weighted rms of
-    //         iteration k), so on exact data c shrinks until the outliers that fell inside the
-    //         band no longer pull (converges to machine precision) and on noisy data it settles
-    //         near 2 sigma.  Weights and Sampson denominators are frozen within an iteration.
-    //         The solving wave of each half (waves 0 and 2) solves its 5x5 normal equations
-    //         from the half's 22 sums; one block barrier per iteration (partial sums and states
-    //         double-buffered), the loop runs until both halves stop. ----
     __shared__ float s_red[2][4][22];
-    __shared__ float s_state[2][2][16];  // [iteration parity][half]
-    float R[9], tv[3], bs[6];            // the state: rotation, unit translation, tangent basis at t
-#pragma unroll
-    for (int i = 0; i < 9; i++) R[i] = s_cand[hh][bc][i];
-#pragma unroll
-    for (int i = 0; i < 3; i++) tv[i] = s_cand[hh][bc][9 + i];
-    tangent_basis_f(tv, bs);
+    __shared__ float s_state[2][16];
+    __shared__ float s_fin[4];
+    __shared__ int s_fin_n[4];
+    static_assert(MAXP <= 32 * NT, "the inlier mask holds 32 correspondences per thread");
     const float th_max = sqrtf(a.thr2), th_min = 0.01f * th_max, r_cap = 3.f * th_max;
-    float csc = th_max;  // the Cauchy scale
-    bool act = true;    // this half is still iterating
-    for (int it = 0; it < a.refine_iters; it++) {
-        float acc[22];  // sum w J^T J (15, upper), sum w J^T r (5), sum w r^2, sum w
-#pragma unroll
-        for (int k = 0; k < 22; k++) acc[k] = 0.f;
-        const float rcs = __builtin_amdgcn_rcpf(csc);
-        for (int i = ht; i < (act ? n : 0); i += HT) {
-            const float4 p = P[i];
-            const float x1[3] = {p.x, p.y, 1.f}, x2[3] = {p.z, p.w, 1.f};
-            const float q[3] = {R[0] * x1[0] + R[1] * x1[1] + R[2], R[3] * x1[0] + R[4] * x1[1] + R[5],
-                                R[6] * x1[0] + R[7] * x1[1] + R[8]};
-            // e = x2^T [t]x R x1 = (x2 x t) . (R x1)
-            const float x2t[3] = {x2[1] * tv[2] - x2[2] * tv[1], x2[2] * tv[0] - x2[0] * tv[2],
-                                  x2[0] * tv[1] - x2[1] * tv[0]};
-            const float e = x2t[0] * q[0] + x2t[1] * q[1] + x2t[2] * q[2];
-            const float Ex1[2] = {tv[1] * q[2] - tv[2] * q[1], tv[2] * q[0] - tv[0] * q[2]};  // (E x1)_{0,1}
-            float Etx2[2];  // (E^T x2)_{0,1} = (R^T (x2 x t))_{0,1}
-#pragma unroll
-            for (int c = 0; c < 2; c++) Etx2[c] = R[c] * x2t[0] + R[3 + c] * x2t[1] + R[6 + c] * x2t[2];
-            const float s2 = Ex1[0] * Ex1[0] + Ex1[1] * Ex1[1] + Etx2[0] * Etx2[0] + Etx2[1] * Etx2[1];
-            if (!(s2 > 0.f)) continue;
-            const float inv = __builtin_amdgcn_rsqf(s2);  // native: a GN weight, not an output
-            const float r = e * inv;                      // Sampson distance
-            if (!(fabsf(r) < r_cap)) continue;
-            const float u = r * rcs;
-            const float wt = __builtin_amdgcn_rcpf(1.f + u * u);
-            // d e / d omega = q x (x2 x t)  (R <- exp(omega) R);  d e / d t = q x x2
-            const float dw[3] = {q[1] * x2t[2] - q[2] * x2t[1], q[2] * x2t[0] - q[0] * x2t[2],
-                                 q[0] * x2t[1] - q[1] * x2t[0]};
-            const float dt[3] = {q[1] * x2[2] - q[2] * x2[1], q[2] * x2[0] - q[0] * x2[2],
-                                 q[0] * x2[1] - q[1] * x2[0]};
-            const float J[5] = {dw[0] * inv, dw[1] * inv, dw[2] * inv,
-                                (dt[0] * bs[0] + dt[1] * bs[1] + dt[2] * bs[2]) * inv,
-                                (dt[0] * bs[3] + dt[1] * bs[4] + dt[2] * bs[5]) * inv};
-            float Jw[5];
-#pragma unroll
-            for (int v = 0; v < 5; v++) Jw[v] = J[v] * wt;
-            int k = 0;
-#pragma unroll
-            for (int v = 0; v < 5; v++) {
-#pragma unroll
-                for (int x = v; x < 5; x++) acc[k++] += Jw[v] * J[x];
+    float bR[9], bT[3], bcost = __builtin_inff();
+    int bn = 0;
+    const long long tk3 = PE_TRACE ? clock64() : 0;
+    long long tk4 = 0, tk5 = 0;
+    for (int sti = 0; sti < s_nh; sti++) {
+        float E[9];
+        for (int r = 0; r < 9; r++) E[r] = s_E[sti][r];
+        if (t == 0) {
+            float U[3][3], V[3][3];
+            if (PE_NODECOMP) {
+                for (int i = 0; i < 3; i++)
+                    for (int j = 0; j < 3; j++) U[i][j] = V[i][j] = i == j;
+            } else {
+                essential_uv(E, U, V);
             }
-#pragma unroll
-            for (int v = 0; v < 5; v++) acc[15 + v] += Jw[v] * r;
-            acc[20] += wt * r * r;
-            acc[21] += wt;
-        }
-        // the 22 sums reduced over the wave by recursive halving (a reduce-scatter: at
-        // level 2^L each lane keeps half of its values and receives its partner's partials
-        // of them, 94 VALU ops instead of 6 x 22 x 2), then the 4 wave partials in LDS
-        float(*red)[22] = s_red[it & 1];
-        {
-            int vi;  // the sum this lane holds after the halving
-            const float f = gn_reduce_scatter22(acc, lane, vi);
-            if (vi >= 0) red[w][vi] = f;
+            for (int i = 0; i < 3; i++)
+                for (int j = 0; j < 3; j++) {
+                    s_uv[0][i][j] = U[i][j];
+                    s_uv[1][i][j] = V[i][j];
+                }
         }
         __syncthreads();
-        float *st = s_state[it & 1][hh];
-        if ((w & 1) == 0) {
-            if (act) {
+        if (t < 4) {  // candidate c = t, one lane each
+            const float W[3][3] = {{0, -1, 0}, {1, 0, 0}, {0, 0, 1}};
+            float U[3][3], V[3][3];
+            for (int i = 0; i < 3; i++)
+                for (int j = 0; j < 3; j++) {
+                    U[i][j] = s_uv[0][i][j];
+                    V[i][j] = s_uv[1][i][j];
+                }
+            const int c = t;
+            float R[3][3];
+            for (int i = 0; i < 3; i++)
+                for (int j = 0; j < 3; j++) {
+                    float s = 0;
+                    for (int k = 0; k < 3; k++) {
+                        float uw = 0;
+                        for (int l = 0; l < 3; l++) uw += U[i][l] * (c < 2 ? W[l][k] : W[k][l]);
+                        s += uw * V[j][k];
+                    }
+                    R[i][j] = s;
+                }
+            const float sg = (c & 1) ? -1.f : 1.f;
+            for (int i = 0; i < 9; i++) s_cand[c][i] = R[i / 3][i % 3];
+            for (int i = 0; i < 3; i++) s_cand[c][9 + i] = sg * U[i][2];
+        }
+        __syncthreads();
+        int votes[4] = {0, 0, 0, 0};
+        unsigned inl_mask = 0;  // bit k: correspondence t + k NT is a Sampson inlier of E
+        for (int i = t, k = 0; i < n; i += NT, k++)
+            inl_mask |= sampson_inlier(E, P[i], a.thr2) ? 1u << k : 0u;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {  // candidate-outer: 12 candidate floats live, not 48
+            for (unsigned mk = inl_mask; mk; mk &= mk - 1) {
+                const float4 p = P[t + __builtin_ctz(mk) * NT];
+                // depths z1, z2 of the midpoint triangulation, q z1 + t = -m z2 in the least-
+                // squares sense: z = num / det with det > 0, so only the numerators' signs count
+                const float *C = s_cand[c];
+                const F3 q = {{C[0] * p.x + C[1] * p.y + C[2], C[3] * p.x + C[4] * p.y + C[5], C[6] * p.x + C[7] * p.y + C[8]}};
+                const F3 m = {{-p.z, -p.w, -1.f}};
+                const F3 tt = {{C[9], C[10], C[11]}};
+                const float aa = dot3(q, q), ab = dot3(q, m), bb = dot3(m, m);
+                const float ra = -dot3(q, tt), rb = -dot3(m, tt);
+                const float det = aa * bb - ab * ab;
+                const float n1 = ra * bb - ab * rb, n2 = aa * rb - ab * ra;
+                votes[c] += (det > 0.f && n1 > 0.f && n2 > 0.f) ? 1 : 0;
+            }
+        }
+        if (PE_TRACE && sti == 0) tk4 = clock64();
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            int v = votes[c];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            if (lane == 0) s_votes[w][c] = v;
+        }
+        __syncthreads();
+        int bc = 0, bv = s_votes[0][0] + s_votes[1][0] + s_votes[2][0] + s_votes[3][0];
+        for (int c = 1; c < 4; c++) {
+            const int v = s_votes[0][c] + s_votes[1][c] + s_votes[2][c] + s_votes[3][c];
+            if (v > bv) {
+                bv = v;
+                bc = c;
+            }
+        }
+        if (PE_TRACE && sti == 0) tk5 = clock64();
+
+        // ---- robust Gauss-Newton: iteratively reweighted, Cauchy weights 1 / (1 + (r / c)^2)
+        //      on the Sampson residuals below 3 thr (none above), the scale c_0 = thr,
+        //      c_{k+1} = min(thr, max(2 rms_w, 0.01 thr)) (rms_w: the weighted rms of iteration
+        //      k): on exact data c shrinks until the outliers that fell inside the band no
+        //      longer pull (converges to machine precision), on noisy data it settles near
+        //      2 sigma.  Weights and Sampson denominators are frozen within an iteration.  Wave
+        //      0 solves the 5x5 normal equations from the 22 block sums; one block barrier per
+        //      iteration (sums and state double-buffered). ----
+        float R[9], tv[3], bs[6];
+#pragma unroll
+        for (int i = 0; i < 9; i++) R[i] = s_cand[bc][i];
+#pragma unroll
+        for (int i = 0; i < 3; i++) tv[i] = s_cand[bc][9 + i];
+        tangent_basis_f(tv, bs);
+        float csc = th_max;  // the Cauchy scale
+        for (int it = 0; it < a.refine_iters; it++) {
+            float acc[22];  // sum w J^T J (15, upper), sum w J^T r (5), sum w r^2, sum w
+#pragma unroll
+            for (int k = 0; k < 22; k++) acc[k] = 0.f;
+            const float rcs = __builtin_amdgcn_rcpf(csc);
+            for (int i = t; i < n; i += NT) {
+                const float4 p = P[i];
+                const float x1[3] = {p.x, p.y, 1.f}, x2[3] = {p.z, p.w, 1.f};
+                const float q[3] = {R[0] * x1[0] + R[1] * x1[1] + R[2], R[3] * x1[0] + R[4] * x1[1] + R[5],
+                                    R[6] * x1[0] + R[7] * x1[1] + R[8]};
+                // e = x2^T [t]x R x1 = (x2 x t) . (R x1)
+                const float x2t[3] = {x2[1] * tv[2] - x2[2] * tv[1], x2[2] * tv[0] - x2[0] * tv[2],
+                                      x2[0] * tv[1] - x2[1] * tv[0]};
+                const float e = x2t[0] * q[0] + x2t[1] * q[1] + x2t[2] * q[2];
+                const float Ex1[2] = {tv[1] * q[2] - tv[2] * q[1], tv[2] * q[0] - tv[0] * q[2]};  // (E x1)_{0,1}
+                float Etx2[2];  // (E^T x2)_{0,1} = (R^T (x2 x t))_{0,1}
+#pragma unroll
+                for (int c = 0; c < 2; c++) Etx2[c] = R[c] * x2t[0] + R[3 + c] * x2t[1] + R[6 + c] * x2t[2];
+                const float s2 = Ex1[0] * Ex1[0] + Ex1[1] * Ex1[1] + Etx2[0] * Etx2[0] + Etx2[1] * Etx2[1];
+                if (!(s2 > 0.f)) continue;
+                const float inv = __builtin_amdgcn_rsqf(s2);  // native: a GN weight, not an output
+                const float r = e * inv;                      // Sampson distance
+                if (!(fabsf(r) < r_cap)) continue;
+                const float u = r * rcs;
+                const float wt = __builtin_amdgcn_rcpf(1.f + u * u);
+                // d e / d omega = q x (x2 x t)  (R <- exp(omega) R);  d e / d t = q x x2
+                const float dw[3] = {q[1] * x2t[2] - q[2] * x2t[1], q[2] * x2t[0] - q[0] * x2t[2],
+                                     q[0] * x2t[1] - q[1] * x2t[0]};
+                const float dt[3] = {q[1] * x2[2] - q[2] * x2[1], q[2] * x2[0] - q[0] * x2[2],
+                                     q[0] * x2[1] - q[1] * x2[0]};
+                const float J[5] = {dw[0] * inv, dw[1] * inv, dw[2] * inv,
+                                    (dt[0] * bs[0] + dt[1] * bs[1] + dt[2] * bs[2]) * inv,
+                                    (dt[0] * bs[3] + dt[1] * bs[4] + dt[2] * bs[5]) * inv};
+                float Jw[5];
+#pragma unroll
+                for (int v = 0; v < 5; v++) Jw[v] = J[v] * wt;
+                int k = 0;
+#pragma unroll
+                for (int v = 0; v < 5; v++) {
+#pragma unroll
+                    for (int x = v; x < 5; x++) acc[k++] += Jw[v] * J[x];
+                }
+#pragma unroll
+                for (int v = 0; v < 5; v++) acc[15 + v] += Jw[v] * r;
+                acc[20] += wt * r * r;
+                acc[21] += wt;
+            }
+            // the 22 sums reduced over the wave by recursive halving (a reduce-scatter), then
+            // the 4 wave partials in LDS
+            float(*red)[22] = s_red[it & 1];
+            {
+                int vi;  // the sum this lane holds after the halving
+                const float f = gn_reduce_scatter22(acc, lane, vi);
+                if (vi >= 0) red[w][vi] = f;
+            }
+            __syncthreads();
+            float *st = s_state[it & 1];
+            if (w == 0) {
                 float H[15], g[5];
 #pragma unroll
-                for (int k = 0; k < 15; k++) H[k] = red[w][k] + red[w + 1][k];
+                for (int k = 0; k < 15; k++) H[k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
 #pragma unroll
-                for (int k = 0; k < 5; k++) g[k] = red[w][15 + k] + red[w + 1][15 + k];
-                const float r2 = red[w][20] + red[w + 1][20];
-                const float cnt = red[w][21] + red[w + 1][21];
+                for (int k = 0; k < 5; k++) g[k] = red[0][15 + k] + red[1][15 + k] + red[2][15 + k] + red[3][15 + k];
+                const float r2 = red[0][20] + red[1][20] + red[2][20] + red[3][20];
+                const float cnt = red[0][21] + red[1][21] + red[2][21] + red[3][21];
                 // float Cholesky on the native reciprocal square root (the step only has to be
                 // a descent direction); every loop fully unrolled: static register indexing
                 float A[5][5];
@@ -907,68 +909,71 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
                     v = lane == 13 ? __int_as_float((ok ? 0 : 1) | (done ? 2 : 0)) : v;
                     st[lane] = v;
                 }
-            } else if (lane == 13) {
-                st[13] = __int_as_float(2);  // a stopped half stays stopped
             }
-        }
-        __syncthreads();
-        const int f0 = __float_as_int(s_state[it & 1][0][13]), f1 = __float_as_int(s_state[it & 1][1][13]);
-        const int fl = hh ? f1 : f0;
-        if (act && !(fl & 1)) {
+            __syncthreads();
+            const int flags = __float_as_int(st[13]);
+            if (flags & 1) break;  // the same decision in every thread
 #pragma unroll
             for (int i = 0; i < 9; i++) R[i] = st[i];
 #pragma unroll
             for (int i = 0; i < 3; i++) tv[i] = st[9 + i];
             tangent_basis_f(tv, bs);
             csc = st[12];
+            if (flags & 2) break;
         }
-        act = act && !(fl & 3);
-        if ((f0 & 3) && (f1 & 3)) break;  // the same decision in every thread
-    }
 
-    // ---- 6. each half's robust cost at its refined pose (Cauchy at the scale thr, capped at
-    //         3 thr), the lower wins (a tie: the better RANSAC start); its inliers (Sampson
-    //         distance < thr) are the reported count ----
-    float rcost = 0.f;
-    int ninl = 0;
-    for (int i = ht; i < n; i += HT) {
-        const float4 p = P[i];
-        const float q[3] = {R[0] * p.x + R[1] * p.y + R[2], R[3] * p.x + R[4] * p.y + R[5], R[6] * p.x + R[7] * p.y + R[8]};
-        const float x2t[3] = {p.w * tv[2] - tv[1], tv[0] - p.z * tv[2], p.z * tv[1] - p.w * tv[0]};
-        const float e = x2t[0] * q[0] + x2t[1] * q[1] + x2t[2] * q[2];
-        const float Ex1[2] = {tv[1] * q[2] - tv[2] * q[1], tv[2] * q[0] - tv[0] * q[2]};
-        float Etx2[2];
+        // ---- the robust cost of the refined pose (Cauchy at the scale thr, capped at 3 thr) and
+        //      its inliers (Sampson distance < thr): the lower cost over the starts wins ----
+        float rcost = 0.f;
+        int ninl = 0;
+        for (int i = t; i < n; i += NT) {
+            const float4 p = P[i];
+            const float q[3] = {R[0] * p.x + R[1] * p.y + R[2], R[3] * p.x + R[4] * p.y + R[5],
+                                R[6] * p.x + R[7] * p.y + R[8]};
+            const float x2t[3] = {p.w * tv[2] - tv[1], tv[0] - p.z * tv[2], p.z * tv[1] - p.w * tv[0]};
+            const float e = x2t[0] * q[0] + x2t[1] * q[1] + x2t[2] * q[2];
+            const float Ex1[2] = {tv[1] * q[2] - tv[2] * q[1], tv[2] * q[0] - tv[0] * q[2]};
+            float Etx2[2];
 #pragma unroll
-        for (int c = 0; c < 2; c++) Etx2[c] = R[c] * x2t[0] + R[3 + c] * x2t[1] + R[6 + c] * x2t[2];
-        const float s2 = Ex1[0] * Ex1[0] + Ex1[1] * Ex1[1] + Etx2[0] * Etx2[0] + Etx2[1] * Etx2[1];
-        const float ar = s2 > 0.f ? fabsf(e) * __builtin_amdgcn_rsqf(s2) : r_cap;
-        const float u = fminf(ar, r_cap) / th_max;
-        rcost += __logf(1.f + u * u);
-        ninl += ar < th_max ? 1 : 0;
-    }
+            for (int c = 0; c < 2; c++) Etx2[c] = R[c] * x2t[0] + R[3 + c] * x2t[1] + R[6 + c] * x2t[2];
+            const float s2 = Ex1[0] * Ex1[0] + Ex1[1] * Ex1[1] + Etx2[0] * Etx2[0] + Etx2[1] * Etx2[1];
+            const float ar = s2 > 0.f ? fabsf(e) * __builtin_amdgcn_rsqf(s2) : r_cap;
+            const float u = fminf(ar, r_cap) / th_max;
+            rcost += __logf(1.f + u * u);
+            ninl += ar < th_max ? 1 : 0;
+        }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        rcost += __shfl_xor(rcost, o, 64);
-        ninl += __shfl_xor(ninl, o, 64);
+        for (int o = 32; o > 0; o >>= 1) {
+            rcost += __shfl_xor(rcost, o, 64);
+            ninl += __shfl_xor(ninl, o, 64);
+        }
+        if (lane == 0) {
+            s_fin[w] = rcost;
+            s_fin_n[w] = ninl;
+        }
+        __syncthreads();
+        const float cost = s_fin[0] + s_fin[1] + s_fin[2] + s_fin[3];
+        if (cost < bcost) {  // the same decision in every thread (a tie keeps the earlier start)
+            bcost = cost;
+            bn = s_fin_n[0] + s_fin_n[1] + s_fin_n[2] + s_fin_n[3];
+#pragma unroll
+            for (int i = 0; i < 9; i++) bR[i] = R[i];
+#pragma unroll
+            for (int i = 0; i < 3; i++) bT[i] = tv[i];
+        }
+        __syncthreads();  // s_uv, s_cand, s_votes, s_fin are the next start's
+        if (csc <= th_min * 1.0001f) break;  // an exact fit: no second start needed
     }
-    __shared__ float s_fin[4];
-    __shared__ int s_fin_n[4];
-    if (lane == 0) {
-        s_fin[w] = rcost;
-        s_fin_n[w] = ninl;
-    }
-    __syncthreads();
-    const int win = (s_nh > 1 && s_fin[2] + s_fin[3] < s_fin[0] + s_fin[1]) ? 1 : 0;
-    if (hh == win) {  // [R | t] row-major, thread ht < 12 writes entry ht (static register indexing)
+    {  // [R | t] row-major, thread t < 12 writes entry t (static register indexing)
         float v = 0.f;
 #pragma unroll
-        for (int k = 0; k < 12; k++) v = ht == k ? (k % 4 < 3 ? R[(k / 4) * 3 + k % 4] : tv[k / 4]) : v;
-        if (ht < 12) To[ht] = v;
-        if (ht == 0) {
-            num_inliers[b] = s_fin_n[2 * win] + s_fin_n[2 * win + 1];
-            if (num_matches) num_matches[b] = n_all;
-            status[b] = MV_OK;
-        }
+        for (int k = 0; k < 12; k++) v = t == k ? (k % 4 < 3 ? bR[(k / 4) * 3 + k % 4] : bT[k / 4]) : v;
+        if (t < 12) To[t] = v;
+    }
+    if (t == 0) {
+        num_inliers[b] = bn;
+        if (num_matches) num_matches[b] = n_all;
+        status[b] = MV_OK;
     }
     if (PE_TRACE && b == 0 && t == 0) {
         const long long tk6 = clock64();

@@ -408,3 +408,38 @@ def test_allpairs_screen_selection(ctx):
     with pytest.raises(RuntimeError):
         mvtrack.check(mvtrack.lib().mv_context_set_allpairs_screen(c.h, 7), "bad screen")
     c.close()
+
+
+def test_prepare_then_one_shot_calls(ctx, screen, orc, torch_cuda):
+    """a prepare of batch A still staging on the auxiliary stream must not race the
+    one-shot match / two-way of batch B that follow on the context stream (they wait for it)."""
+    torch = torch_cuda
+    dev = torch.device("cuda:0")
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)  # noqa: E731
+    B, n = 64, 512
+    pa = [synth.synth_pair_f32(900 + k, n=n) for k in range(B)]
+    pb = [synth.synth_pair_f32(950 + k, n=n) for k in range(2)]
+    A1 = t(np.stack([p["desc1"] for p in pa]))
+    NA = t(np.full(B, n, np.int32))
+    D0 = t(np.stack([p["desc0"] for p in pb]))
+    D1 = t(np.stack([p["desc1"] for p in pb]))
+    N2 = t(np.full(2, n, np.int32))
+    idx = torch.full((2, n), -7, dtype=torch.int32, device=dev)
+    dist = torch.zeros((2, n), dtype=torch.float32, device=dev)
+    ctx.set_stream(torch.cuda.current_stream())
+    try:
+        for _ in range(3):
+            ctx.match_allpairs_f32_prepare(A1, NA)  # a large staging in flight ...
+            ctx.match_allpairs_f32(D0, D1, N2, N2, idx, None, 0.8)  # ... then a one-shot batch
+            torch.cuda.synchronize()
+            for k, p in enumerate(pb):
+                i2, _ = orc.allpairs_f32(p["desc0"], p["desc1"], 0.8)
+                assert (idx[k].cpu().numpy() == i2).all(), k
+            ctx.match_allpairs_f32_prepare(A1, NA)
+            ctx.match_two_way_f32(D0, D1, N2, N2, idx, dist, 0.7)
+            torch.cuda.synchronize()
+            for k, p in enumerate(pb):
+                i2, _ = orc.two_way_f32(p["desc0"], p["desc1"], 0.7)
+                assert (idx[k].cpu().numpy() == i2).all(), k
+    finally:
+        ctx.set_stream(None)
