@@ -321,15 +321,19 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
     }
 }
 
-// The 1 x 1 heads (convPb, convDb: 256 input channels, no halo): the same wave tiling and
-// epilogue as k_sp_conv, with the pixels' channel chunks read straight from HBM / L2 (a 256-B
-// row per pixel, every byte used once: no LDS tile to stage), 2 k32 steps ahead.
+// The 1 x 1 heads (convPb, convDb: 256 input channels, no halo): a workgroup takes 8 x 32
+// pixels x 128 output channels; its 64 KiB input tile is staged into LDS with all 16 loads of a
+// thread in flight at once (each pixel's 16 chunks padded to 17: conflict-free fragment reads
+// at compile-time offsets), wave w owns tile rows 2w, 2w + 1 against 4 channel blocks (8 MFMAs
+// per k32 step); weights from L2 two steps ahead; the heads' outputs in the Frame layout.
+constexpr int H1_TY = 8, H1_PS = 17, H1_CB = 4;
 template <int OMODE>
 __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv1x1(const int8_t *__restrict__ in, int H, int W,
                                                          const i32x4 *__restrict__ wf, const int *__restrict__ bq,
                                                          float rs, int ngroups, int tiles_x, int tiles_y,
                                                          int8_t *__restrict__ out, int cstride) {
-    constexpr int NS = 8;  // 256 channels
+    constexpr int NS = 8, NCH = 16, NCHUNK = H1_TY * TX * NCH;  // 256 channels
+    __shared__ i32x4 tile[H1_TY * TX * H1_PS];
     int bid = blockIdx.x;
     const int tx = bid % tiles_x;
     bid /= tiles_x;
@@ -337,55 +341,62 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv1x1(const int8_t *__restric
     bid /= tiles_y;
     const int g = bid % ngroups, b = bid / ngroups;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, fr = lane & 31, fh = lane >> 5;
-    const int y0 = ty * TY, x0 = tx * TX, gx = x0 + fr, gxc = min(gx, W - 1);
-    const i32x4 *px[4];
+    const int y0 = ty * H1_TY, x0 = tx * TX;
+    {  // the tile: 16 chunks per thread, every load issued before the first store
+        i32x4 v[NCHUNK / SP_NT];
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int gyc = min(y0 + 4 * w + j, H - 1);
-        px[j] = reinterpret_cast<const i32x4 *>(in + (((size_t)b * H + gyc) * W + gxc) * 256) + fh;
+        for (int u = 0; u < NCHUNK / SP_NT; u++) {
+            const int i = u * SP_NT + t, c = i % NCH, px = i / NCH, x = px % TX, r = px / TX;
+            const int gy = min(y0 + r, H - 1), gx = min(x0 + x, W - 1);  // clamped: never stored
+            v[u] = *reinterpret_cast<const i32x4 *>(in + (((size_t)b * H + gy) * W + gx) * 256 + c * 16);
+        }
+#pragma unroll
+        for (int u = 0; u < NCHUNK / SP_NT; u++) {
+            const int i = u * SP_NT + t, c = i % NCH, px = i / NCH;
+            tile[px * H1_PS + c] = v[u];
+        }
     }
-    const i32x4 *wa = wf + (size_t)(2 * g) * NS * 64 + lane, *wb = wa + NS * 64;
-    i32x4 bq_[3][4], aq[3][2];
+    __syncthreads();
+    const i32x4 *wa = wf + (size_t)(H1_CB * g) * NS * 64 + lane;
+    i32x4 aq[3][H1_CB];
 #pragma unroll
-    for (int s = 0; s < 2; s++) {
+    for (int s = 0; s < 2; s++)
 #pragma unroll
-        for (int j = 0; j < 4; j++) bq_[s][j] = px[j][2 * s];
-        aq[s][0] = wa[s * 64];
-        aq[s][1] = wb[s * 64];
-    }
-    i32x16 acc[4][2];
+        for (int cb = 0; cb < H1_CB; cb++) aq[s][cb] = wa[(cb * NS + s) * 64];
+    i32x16 acc[2][H1_CB];
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        acc[j][0] = i32x16{};
-        acc[j][1] = i32x16{};
-    }
+    for (int j = 0; j < 2; j++)
+#pragma unroll
+        for (int cb = 0; cb < H1_CB; cb++) acc[j][cb] = i32x16{};
+    const i32x4 *lb = tile + ((2 * w) * TX + fr) * H1_PS + fh;
 #pragma unroll
     for (int s = 0; s < NS; s++) {
         if (s + 2 < NS) {
 #pragma unroll
-            for (int j = 0; j < 4; j++) bq_[(s + 2) % 3][j] = px[j][2 * (s + 2)];
-            aq[(s + 2) % 3][0] = wa[(s + 2) * 64];
-            aq[(s + 2) % 3][1] = wb[(s + 2) * 64];
+            for (int cb = 0; cb < H1_CB; cb++) aq[(s + 2) % 3][cb] = wa[(cb * NS + s + 2) * 64];
         }
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            acc[j][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aq[s % 3][0], bq_[s % 3][j], acc[j][0], 0, 0, 0);
-            acc[j][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aq[s % 3][1], bq_[s % 3][j], acc[j][1], 0, 0, 0);
+        for (int j = 0; j < 2; j++) {
+            const i32x4 bv = lb[j * TX * H1_PS + 2 * s];
+#pragma unroll
+            for (int cb = 0; cb < H1_CB; cb++)
+                acc[j][cb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aq[s % 3][cb], bv, acc[j][cb], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
     }
     const int lo = SP_MAGIC_BITS - 128;  // the heads have no relu
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int gy = y0 + 4 * w + j;
+    for (int j = 0; j < 2; j++) {
+        const int gy = y0 + 2 * w + j, gx = x0 + fr;
         if (gy >= H || gx >= W) continue;
         int8_t *dst = OMODE == 0 ? out + (((size_t)b * H + gy) * W + gx) * cstride
                                  : out + ((size_t)b * H * W + (size_t)gx * H + gy) * cstride;
 #pragma unroll
-        for (int cb = 0; cb < 2; cb++) {
+        for (int cb = 0; cb < H1_CB; cb++) {
 #pragma unroll
             for (int qq = 0; qq < 4; qq++) {
-                const int co = 64 * g + 32 * cb + 8 * qq + 4 * fh;
+                const int co = 32 * (H1_CB * g + cb) + 8 * qq + 4 * fh;
+                if (co >= cstride) continue;
                 int v[4];
 #pragma unroll
                 for (int e = 0; e < 4; e++) v[e] = requant_bits(acc[j][cb][4 * qq + e] + bq[co + e], rs, lo);
@@ -474,9 +485,12 @@ __global__ __launch_bounds__(SP_NT) void k_sp_min_gap(int8_t *__restrict__ semi,
     {
         const int v = t;
         const bool here = (pm[v >> 5] >> (v & 31)) & 1u;
+        // the next present code above v: the rest of v's word, then the following words
         int nx = -1;
-        for (int u = v + 1; u < 256 && nx < 0; u++)
-            if ((pm[u >> 5] >> (u & 31)) & 1u) nx = u;
+        const unsigned rest = (v & 31) == 31 ? 0u : pm[v >> 5] & ~((2u << (v & 31)) - 1u);
+        if (rest) nx = (v & ~31) + __builtin_ctz(rest);
+        for (int k = (v >> 5) + 1; k < 8 && nx < 0; k++)
+            if (pm[k]) nx = 32 * k + __builtin_ctz(pm[k]);
         if (here && nx >= 0) {
             const float d = (float)(nx - 128) * s - (float)(v - 128) * s;
             gap = d > 0.f ? d : INFINITY;
@@ -506,11 +520,28 @@ __global__ __launch_bounds__(SP_NT) void k_sp_min_gap(int8_t *__restrict__ semi,
     int8_t *base;
     long lo, hi;
     sp_head(semi, desc, cells, b, h, base, lo, hi);
-    for (long i = lo + t; i < hi; i += SP_NT) {
-        const float f = (float)base[i] * s;
+    auto requant = [&](int q) {  // round(outs / scale0) of one code, clamped to int8
+        const float f = (float)q * s;
         float r = __builtin_rintf(f / g);
-        r = fminf(fmaxf(r, -128.f), 127.f);
-        base[i] = (int8_t)(int)r;
+        return (int)fminf(fmaxf(r, -128.f), 127.f);
+    };
+    const bool al = ((uintptr_t)(base + lo) & 15) == 0;
+    long i = lo + 16 * t;
+    for (; al && i + 16 <= hi; i += 16 * SP_NT) {  // 16 codes per thread per step
+        i32x4 v = *reinterpret_cast<const i32x4 *>(base + i);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            int o[4];
+#pragma unroll
+            for (int e = 0; e < 4; e++) o[e] = requant((v[k] << (24 - 8 * e)) >> 24);
+            v[k] = (o[0] & 0xff) | ((o[1] & 0xff) << 8) | ((o[2] & 0xff) << 16) | (o[3] << 24);
+        }
+        *reinterpret_cast<i32x4 *>(base + i) = v;
+    }
+    if (al) {  // the one partial chunk at the end (its thread only)
+        for (long j = i; j < hi && j < i + 16; j++) base[j] = (int8_t)requant(base[j]);
+    } else {
+        for (long j = lo + t; j < hi; j += SP_NT) base[j] = (int8_t)requant(base[j]);
     }
 }
 
@@ -532,7 +563,9 @@ int launch_conv(hipStream_t st, const mv_superpoint *net, int li, int B, int H, 
 template <int OMODE>
 int launch_conv1x1(hipStream_t st, const mv_superpoint *net, int li, int B, int H, int W, const int8_t *in,
                    int8_t *out, int cstride) {
-    const int tiles_x = (W + TX - 1) / TX, tiles_y = (H + TY - 1) / TY, ngroups = net->cout_pad[li] / 64;
+    const int tiles_x = (W + TX - 1) / TX, tiles_y = (H + H1_TY - 1) / H1_TY;
+    const int ngroups = (net->cout_pad[li] + 32 * H1_CB - 1) / (32 * H1_CB);
+    MV_REQUIRE(net->cout_pad[li] % (32 * H1_CB) == 0);  // whole 128-channel groups (65 -> 128, 256)
     const long blocks = (long)B * ngroups * tiles_y * tiles_x;
     MV_REQUIRE(blocks < (1l << 31));
     const char *wd = static_cast<const char *>(net->wdev);
