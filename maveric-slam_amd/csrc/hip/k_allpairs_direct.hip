@@ -56,6 +56,9 @@ constexpr int QS_LOAD = 1;    // the k32 step whose slot issues the quantisation
 #ifndef D_EXPE
 #define D_EXPE 1  // per-column scale exponent from m's exponent bits (else by comparisons)
 #endif
+#ifndef D_MIDSYNC
+#define D_MIDSYNC 0  // 1: the block barrier before half 2t + 5's DMA (not needed, see the sweep)
+#endif
 #ifndef D_QB
 #define D_QB 4  // A phase: frame-0 row quads in flight per wave (4 x 16-B loads per lane each)
 #endif
@@ -383,7 +386,12 @@ __device__ __forceinline__ Sweep sweep(char *lds, const float *B, int n1, int t,
         } else {
             wait_vm<0>();
         }
-        D_SYNC();  // staging slot of half 2t + 2 consumed
+#if D_MIDSYNC
+        D_SYNC();
+#endif
+        // the staging slot of half 2t + 2 is free for half 2t + 5: a wave quantises exactly the
+        // staging rows it copies itself (rows 4 w .. +3 of every half), so its own reads of them
+        // (done in group 0) and its own vmcnt are the whole condition -- no block barrier
         if (2 * tc + 5 < nh) dma_half(B, 2 * tc + 5, n1, wu, chunk16, lds_base + (unsigned)(sA * D_HALF));
         const unsigned gc_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)tc);
         D_SEG(1, 0, gc_, stB, 1, 32 * (2 * tc + 3), live);
