@@ -68,7 +68,7 @@ constexpr float IK_MMAX = 1.003f;  // integer path: max |b_jk| allowed (RNE(x 12
 constexpr int D_TRACE_BLOCKS = 16384;
 __device__ unsigned long long g_d_trace[D_TRACE_BLOCKS * D_NW * 10];
 #define D_STAMP(K) do { __builtin_amdgcn_sched_barrier(0); ts_[K] = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
-#define D_SYNC() do { const unsigned long long b_ = __builtin_amdgcn_s_memtime(); __syncthreads(); ts_[9] += __builtin_amdgcn_s_memtime() - b_; } while (0)
+#define D_SYNC() __syncthreads()
 #else
 #define D_STAMP(K) do { } while (0)
 #define D_SYNC() __syncthreads()

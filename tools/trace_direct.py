@@ -1,6 +1,5 @@
 """Phase timing of k_q8d_match (library built with EXTRA=-DMV_TRACE): per (block, wave)
-s_memtime stamps at entry, A phase done, tile 0 quantised, sweep done, statistics, epilogue
-done; plus the cycles each wave spent in the sweep's barriers."""
+s_memtime stamps at entry, A phase done, sweep + statistics done, epilogue done."""
 import ctypes
 import os
 import sys
@@ -30,20 +29,17 @@ lib = mvtrack.lib()
 lib.mv_debug_direct_trace.argtypes = [ctypes.c_void_p, ctypes.c_long]
 assert lib.mv_debug_direct_trace(buf.ctypes.data, buf.nbytes) == 0
 tr = buf.reshape(nblk, NW, 10).astype(np.int64)
-st = tr[:, :, :6]
+st = tr[:, :, :4]
 d = np.diff(st, axis=2)
-names = ["A-phase", "tile0-quant", "sweep", "stats", "epilogue"]
+names = ["A-phase", "sweep+stats", "epilogue"]
 print("per-wave phase cycles (median / p10 / p90 / max):")
 for k, nm in enumerate(names):
     v = d[:, :, k].ravel()
     print("  %-12s %9.0f %9.0f %9.0f %9.0f" % (nm, np.median(v), np.percentile(v, 10), np.percentile(v, 90), v.max()))
-for k, nm in ((9, "sweep-barrier"), (8, "sweep-vmwait")):
-    v = tr[:, :, k].ravel()
-    print("  %-12s %9.0f %9.0f %9.0f %9.0f" % (nm, np.median(v), np.percentile(v, 10), np.percentile(v, 90), v.max()))
-tot = st[:, :, 5] - st[:, :, 0]
-print("wave total median %.0f; sweep per tile %.0f" % (np.median(tot), np.median(d[:, :, 2]) / 16))
+tot = st[:, :, 3] - st[:, :, 0]
+print("wave total median %.0f; sweep per tile %.0f" % (np.median(tot), np.median(d[:, :, 1]) / 16))
 sm = tr[:, 0, 6]
-start, end = st[:, :, 0].min(1), st[:, :, 5].max(1)
+start, end = st[:, :, 0].min(1), st[:, :, 3].max(1)
 cu = np.unique(sm)[0]
 sel = np.where(sm == cu)[0]
 o = sel[np.argsort(start[sel])]
@@ -53,4 +49,4 @@ for b in o[:12]:
 rt = tr[:, 0, 7]
 a, b = o[0], o[-1]
 if rt[b] != rt[a]:
-    print("SCLK over the CU's run: %.3f GHz" % ((st[b, 0, 5] - st[a, 0, 5]) / ((rt[b] - rt[a]) / 100e6) / 1e9))
+    print("SCLK over the CU's run: %.3f GHz" % ((st[b, 0, 3] - st[a, 0, 3]) / ((rt[b] - rt[a]) / 100e6) / 1e9))
