@@ -68,35 +68,28 @@ __device__ __forceinline__ bool better(long long d, long long nb, int j, long lo
 // below M (1 - 1e-5) the screen maximiser is the exact one and one integer dot +
 // the u128 threshold decide; otherwise one wave re-scores the row exactly.
 // ---------------------------------------------------------------------------
-// timing experiments only (wrong results): I8_EXP_NOEXACT skips the per-row exact decision,
-// I8_EXP_NODMA / NOBAR drop the tile DMA / the per-tile barrier
-#ifdef I8_EXP_NODMA
-#define I8_NODMA 1
-#else
-#define I8_NODMA 0
-#endif
-#ifdef I8_EXP_NOBAR
-#define I8_NOBAR 1
-#else
-#define I8_NOBAR 0
-#endif
+// the fold of rows 2 s, 2 s + 1 runs one k32 step after the MFMAs of step s: the folded group's
+// accumulators come from the chain's LAST MFMA, issued at the end of the previous segment
+constexpr int I8_LAG = 1;
 #ifndef I8_PF
 #define I8_PF 2  // k32 steps of B fragments read ahead of the MFMAs
 #endif
-#ifdef I8_EXP_TRACE
-constexpr int I8_TRACE_BLOCKS = 8192;
-__device__ unsigned long long g_i8_trace[I8_TRACE_BLOCKS * 4 * 10];
-#endif
+// 4 waves (64 query rows each) per workgroup share one frame-1 tile ring, two workgroups per CU
+// (8 waves sharing one ring, one workgroup per CU -- half the DMA pieces per wave: 1.5 % slower)
 constexpr int M_NW = 4, M_NT = 64 * M_NW, M_RG = 2, M_BM = 32 * M_RG * M_NW, M_BN = 64, M_NBUF = 4;
+constexpr int M_RPW = M_BN / M_NW;                // tile rows each wave copies
+constexpr int M_DPW = M_RPW / 4;                  // its 1-KiB DMA pieces per tile (+ one of column words)
+static_assert(M_DPW == 2 || M_DPW == 4, "8 or 4 waves");
 constexpr int M_TILE = M_BN * KD;                 // 16 KiB: one column tile, whole K
 constexpr int M_SLOT = M_TILE + M_BN * 4;         // + the tile's 64 rsqrt|b|^2
-constexpr int M_OFF_NA = M_NBUF * M_SLOT;         // [BM] i32 |a|^2
-constexpr int M_LDS = M_OFF_NA + M_BM * 4;
 constexpr int MT_STRIDE = 32 * 8 + 16;            // epilogue transpose row: 32 (m1, m2) + pad
 constexpr int M_NCAND = 16;                       // listed candidates per row (more: deep row)
-constexpr int M_OFF_CL = M_NW * 32 * MT_STRIDE;   // epilogue, inside the ring: [BM][NCAND] candidates
+constexpr int M_OFF_CL = M_NW * 32 * MT_STRIDE;   // epilogue, over the ring: [BM][NCAND] candidates
 constexpr int M_OFF_LM = M_OFF_CL + M_BM * M_NCAND * 4;  // [BM] deep rows' inside entries
-static_assert(M_OFF_LM + M_BM * 4 <= M_NBUF * M_SLOT, "epilogue fits the ring");
+constexpr int M_EPI = M_OFF_LM + M_BM * 4, M_RING = M_NBUF * M_SLOT;
+constexpr int M_OFF_NA = M_EPI > M_RING ? M_EPI : M_RING;  // [BM] i32 |a|^2
+constexpr int M_LDS = M_OFF_NA + M_BM * 4;
+static_assert(M_LDS <= 160 * 1024, "LDS");
 
 #pragma clang diagnostic ignored "-Winline-asm"
 template <int KOFF, int DOFF>
@@ -152,13 +145,6 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
                                                       int *__restrict__ match_dot) {
     __shared__ __attribute__((aligned(16))) char lds[M_LDS];
     int *na_s = reinterpret_cast<int *>(lds + M_OFF_NA);
-#ifdef I8_EXP_TRACE
-#define I8_STAMP(K) do { __builtin_amdgcn_sched_barrier(0); ts_[K] = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
-    unsigned long long ts_[8];
-    I8_STAMP(0);
-#else
-#define I8_STAMP(K) do { } while (0)
-#endif
     const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int pair = L / tiles_r, tr = L % tiles_r;
     const int n0 = min(max(n0v[pair], 0), cap), n1 = min(max(n1v[pair], 0), cap);
@@ -200,31 +186,32 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
         if (fh == 0) na_s[w * 64 + g * 32 + fr] = q;
         na_r[g] = q;
     }
-    I8_STAMP(1);
 
-    // ---- B DMA: wave w fills rows w*16 .. +15 of a tile, 4 rows (1 KiB) per instruction;
+    // ---- B DMA: wave w fills rows w*RPW .. +RPW-1 of a tile, 4 rows (1 KiB) per instruction;
     //      lane l -> row (l >> 4), chunk position l & 15, source chunk (l & 15) ^ (row & 15) ----
     const int wu = __builtin_amdgcn_readfirstlane(w);
-    const int dr = wu * 16 + (lane >> 4);
+    const int dr = wu * M_RPW + (lane >> 4);
     const unsigned dcb = (unsigned)((lane & 15) ^ (dr & 15)) * 16;
-    unsigned oB[4], oR;
+    unsigned oB[M_DPW], oR;
     const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char *)lds;
-    const unsigned dst_w = lds_base + (unsigned)(wu * 16 * KD);
+    const unsigned dst_w = lds_base + (unsigned)(wu * M_RPW * KD);
     // + every wave copies the tile's 64 rsqrt|b|^2 (identical bytes) so that all waves
-    //   count the same 5 loads per tile; compiler-visible loads here would make the
+    //   count the same DPW + 1 loads per tile; compiler-visible loads here would make the
     //   compiler's vmcnt waits drain the whole DMA ring
 #define I8_STAGE(SLOT)                                                                       \
     do {                                                                                     \
         glds16_i8<0, (SLOT) * M_SLOT>(B, oB[0], dst_w);                                      \
         glds16_i8<0, (SLOT) * M_SLOT + 4 * KD>(B, oB[1], dst_w);                             \
-        glds16_i8<0, (SLOT) * M_SLOT + 8 * KD>(B, oB[2], dst_w);                             \
-        glds16_i8<0, (SLOT) * M_SLOT + 12 * KD>(B, oB[3], dst_w);                            \
+        if constexpr (M_DPW == 4) {                                                          \
+            glds16_i8<0, (SLOT) * M_SLOT + 8 * KD>(B, oB[M_DPW - 2], dst_w);                 \
+            glds16_i8<0, (SLOT) * M_SLOT + 12 * KD>(B, oB[M_DPW - 1], dst_w);                \
+        }                                                                                    \
         glds4_i8<(SLOT) * M_SLOT + M_TILE>(rnb, oR, lds_base);                               \
     } while (0)
 #define I8_OFFSETS(TC)                                                                       \
     do {                                                                                     \
         const int nb_ = (TC) * M_BN + dr;                                                    \
-        _Pragma("unroll") for (int g_ = 0; g_ < 4; g_++)                                     \
+        _Pragma("unroll") for (int g_ = 0; g_ < M_DPW; g_++)                                 \
             oB[g_] = (unsigned)min(nb_ + 4 * g_, n1 - 1) * KD + (dcb ^ (64u * g_));          \
         oR = (unsigned)min((TC) * M_BN + lane, n1 - 1) * 4;                                  \
     } while (0)
@@ -291,9 +278,11 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
                     acc[G][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b0_[m_], acc[G][0], 0, 0, 0); \
                     acc[G][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b1_[m_], acc[G][1], 0, 0, 0); \
                 }                                                                            \
-                I8_FOLD2(FG, m_, G0, R0, R1, C0, C1);                                        \
+                if (m_ >= I8_LAG) I8_FOLD2(FG, m_ - I8_LAG, G0, R0, R1, C0, C1);             \
             }                                                                                \
         }                                                                                    \
+        _Pragma("unroll") for (int m_ = KD / 32 - I8_LAG; m_ < KD / 32; m_++)                \
+            I8_FOLD2(FG, m_, G0, R0, R1, C0, C1);                                            \
     } while (0)
     // ring: tile g lives in slot g % 4; at tile g issue tile g + 3 into the slot read at g - 1
     // (whose norms the previous tile left in pr*/pc*)
@@ -304,7 +293,7 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
         const int ntile = tc + M_NBUF - 1;                                                   \
         if (ntile < ntc) {                                                                   \
             I8_OFFSETS(ntile);                                                               \
-            if (!I8_NODMA) I8_STAGE((J + M_NBUF - 1) % M_NBUF);                              \
+            I8_STAGE((J + M_NBUF - 1) % M_NBUF);                              \
         }                                                                                    \
         const unsigned gp_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)max(tc - 1, 0));  \
         I8_SEG(J, 0, 1, gp_, pr0, pr1, pc0, pc1);                                            \
@@ -320,11 +309,11 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
         const unsigned gc_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)tc);              \
         I8_SEG(J, 1, 0, gc_, pr0, pr1, pc0, pc1);                                            \
         if (ntile < ntc) {                                                                   \
-            wait_vm_i8<5 * (M_NBUF - 2)>();                                                  \
+            wait_vm_i8<(M_DPW + 1) * (M_NBUF - 2)>();                                                  \
         } else {                                                                             \
             wait_vm_i8<0>();                                                                 \
         }                                                                                    \
-        if (!I8_NOBAR) __syncthreads();                                                      \
+        __syncthreads();                                                      \
     } while (0)
 
     // prologue: tiles 0, 1, 2
@@ -336,14 +325,12 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
     }
     wait_vm_i8<0>();
     __syncthreads();
-    I8_STAMP(2);
     for (int T = 0; T < ntc; T += 4) {
         I8_SLOT(0);
         if (T + 1 < ntc) I8_SLOT(1);
         if (T + 2 < ntc) I8_SLOT(2);
         if (T + 3 < ntc) I8_SLOT(3);
     }
-    I8_STAMP(3);
     {  // group 1 of the last tile
         const unsigned gl_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)(ntc - 1));
 #pragma unroll
@@ -402,7 +389,6 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
             E = (oM > M || (oM == M && oE < E)) ? oE : E;
             M = fmaxf(M, oM);
         }
-        if (g == 0) I8_STAMP(4);
 
         // ---- decide the row in its own two lanes: exact integer dots with the screen
         //      maximiser, or -- runner-up inside the window -- with the maximum of every entry
@@ -411,11 +397,7 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
         //      ("deep" row, below) ----
         const int rl = w * 64 + g * 32 + fr;
         const bool live = row0 + rl < n0;
-#ifdef I8_EXP_NOEXACT
-        const bool cand = false;
-#else
         const bool cand = live && na_r[g] > 0 && M > 1e-30f;  // else every dot <= 0 (tagged zeros are subnormal)
-#endif
         const float lim = M * keep_frac;
         const bool ambig = cand && M2 >= lim;
         int nc = cand ? 1 : 0;
@@ -441,9 +423,6 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
                         clist[rl * M_NCAND + k++] = (int)(tag >> 1) * M_BN + (int)(tag & 1) * 32 + fh * 16 + i;
                     }
             }
-#ifdef I8_EXP_PRINT
-            if (fh == 0) printf("I8AMB pair %d row %d M %.9g M2 %.9g nc %d\n", pair, row0 + rl, M, M2, nc);
-#endif
         }
         const unsigned tagM = __float_as_uint(M) & ~tkeep;
         const int I = (int)(tagM >> 1) * M_BN + (int)(tagM & 1) * 32 + E;
@@ -477,18 +456,13 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
         }
         deep_rows[g] = (unsigned)__ballot(fh == 0 && live && nc < 0);
     }
-    I8_STAMP(5);
 
     // ---- deep rows (rare): the wave scores every column of every inside entry exactly,
     //      one column per lane (lane l: column f + 32 (l + 64 i) of inside entry f) ----
-    I8_STAMP(6);
 #pragma unroll
     for (int g = 0; g < M_RG; g++)
         for (unsigned dm = deep_rows[g]; dm; dm &= dm - 1) {
             const int rl = w * 64 + g * 32 + __builtin_ctz(dm);
-#ifdef I8_EXP_PRINT
-            if (lane == 0) printf("I8DEEP pair %d row %d lanes %x\n", pair, row0 + rl, lmask[rl]);
-#endif
             const i32x4 *arow = reinterpret_cast<const i32x4 *>(A + (size_t)(row0 + rl) * KD);
             i32x4 av[KD / 16];
 #pragma unroll
@@ -533,15 +507,6 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
                 odot[rl] = keep ? (int)bd : 0;
             }
         }
-#ifdef I8_EXP_TRACE
-    I8_STAMP(7);
-    if (lane == 0 && blockIdx.x < I8_TRACE_BLOCKS) {
-        unsigned long long *o = g_i8_trace + ((size_t)blockIdx.x * M_NW + w) * 10;
-        for (int k = 0; k < 8; k++) o[k] = ts_[k];
-        o[8] = __smid();
-        o[9] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
 }
 
 }  // namespace
@@ -587,10 +552,3 @@ extern "C" int mv_match_allpairs_i8_dev(mv_context *ctx, int batch, int cap, con
     if (!scr) return MV_ERR_OUT_OF_MEMORY;
     return mv::launch_allpairs_i8(ctx->stream, scr, batch, cap, n0, n1, desc0, desc1, match_idx, match_dot);
 }
-
-#ifdef I8_EXP_TRACE
-// timing experiment only: copy the per-(block, wave) phase stamps of the last launch
-extern "C" int mv_debug_i8_trace(void *host, long bytes) {
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_i8_trace), (size_t)bytes) == hipSuccess ? 0 : -3;
-}
-#endif
