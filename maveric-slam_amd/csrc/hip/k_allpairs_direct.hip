@@ -59,9 +59,6 @@ constexpr int QS_LOAD = 1;    // the k32 step whose slot issues the quantisation
 #ifndef D_MIDSYNC
 #define D_MIDSYNC 0  // 1: the block barrier before half 2t + 5's DMA (not needed, see the sweep)
 #endif
-#ifndef D_LAG
-#define D_LAG 0  // k32 steps the fold of rows 2 s, 2 s + 1 runs behind the MFMAs of step s
-#endif
 #ifndef D_QB
 #define D_QB 4  // A phase: frame-0 row quads in flight per wave (4 x 16-B loads per lane each)
 #endif
@@ -343,11 +340,10 @@ __device__ __forceinline__ Sweep sweep(char *lds, const float *B, int n1, int t,
                     acc[G][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b0_[m_], acc[G][0], 0, 0, 0); \
                     acc[G][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b1_[m_], acc[G][1], 0, 0, 0); \
                 }                                                                            \
-                if (m_ >= D_LAG) D_FOLD2(FG, m_ - D_LAG, G0);                                \
+                D_FOLD2(FG, m_, G0);                                                         \
             }                                                                                \
             __builtin_amdgcn_sched_barrier(0);                                               \
         }                                                                                    \
-        _Pragma("unroll") for (int m_ = KD / 32 - D_LAG; m_ < KD / 32; m_++) D_FOLD2(FG, m_, G0); \
     } while (0)
 
     // Tile t sweeps from ring slot t & 1 while tile t + 1 is quantised into the other slot from
