@@ -53,12 +53,6 @@ static_assert(epi_bytes<D_NW>() <= D_OFF_ROW, "the epilogue fits staging + ring"
 static_assert(D_LDS <= 160 * 1024, "one workgroup per CU");
 constexpr int D_PF = 1;       // k32 steps of B fragments read ahead of the MFMAs
 constexpr int QS_LOAD = 1;    // the k32 step whose slot issues the quantisation's staging reads
-#ifndef D_EXPE
-#define D_EXPE 1  // per-column scale exponent from m's exponent bits (else by comparisons)
-#endif
-#ifndef D_MIDSYNC
-#define D_MIDSYNC 0  // 1: the block barrier before half 2t + 5's DMA (not needed, see the sweep)
-#endif
 #ifndef D_QB
 #define D_QB 4  // A phase: frame-0 row quads in flight per wave (4 x 16-B loads per lane each)
 #endif
@@ -177,16 +171,10 @@ struct QHalf {
         qa = qa + qb;
         row16_max_sum(m, qa);  // qa = |b|^2 from here on
         if constexpr (IK) {
-#if D_EXPE
             // e from m's biased exponent: [1/2, 2) -> 0, [1/4, 1/2) -> 1, below -> 2 (m q_e < 128)
             const int e = min(max(126 - (int)((__float_as_uint(m) >> 23) & 0xffu), 0), 2);
             q = j < n1 ? __builtin_ldexpf(127.f, e) : 0.f;
             s = __builtin_ldexpf(1.f / 127.f, -e);  // = 1 / q rounded: the Eb bound
-#else
-            const int e = m > 0.5f ? 0 : (m > 0.25f ? 1 : 2);
-            q = j < n1 ? (e == 0 ? 127.f : (e == 1 ? 254.f : 508.f)) : 0.f;
-            s = e == 0 ? (1.f / 127.f) : (e == 1 ? (1.f / 254.f) : (1.f / 508.f));  // >= 1/q: Eb bound
-#endif
             sh = tb + 2 - e;
         } else {
             q = m > 0.f ? 127.f * __builtin_amdgcn_rcpf(m) : 0.f;
@@ -386,9 +374,6 @@ __device__ __forceinline__ Sweep sweep(char *lds, const float *B, int n1, int t,
         } else {
             wait_vm<0>();
         }
-#if D_MIDSYNC
-        D_SYNC();
-#endif
         // the staging slot of half 2t + 2 is free for half 2t + 5: a wave quantises exactly the
         // staging rows it copies itself (rows 4 w .. +3 of every half), so its own reads of them
         // (done in group 0) and its own vmcnt are the whole condition -- no block barrier
