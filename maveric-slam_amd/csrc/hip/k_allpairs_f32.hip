@@ -52,50 +52,6 @@ namespace {
 #endif
 constexpr int NW = AP_NW, NT = 64 * NW, BM = 32 * NW, BN = 64, BK = 128, KD = 256, KS = KD / BK, RW = BM / NW;
 constexpr int NBUF = 4;  // ring slots: two column tiles of KS = 2 slices
-// timing experiments only (wrong results): drop the DMA waits / barriers / MFMAs / DMAs
-#ifndef AP_EXP_NOWAIT
-#define AP_EXP_NOWAIT 0
-#endif
-#ifndef AP_EXP_NOBAR
-#define AP_EXP_NOBAR 0
-#endif
-#ifndef AP_EXP_NOMFMA
-#define AP_EXP_NOMFMA 0
-#endif
-#ifndef AP_EXP_NOEXACT
-#define AP_EXP_NOEXACT 0
-#endif
-#ifndef AP_EXP_NOALOAD
-#define AP_EXP_NOALOAD 0
-#endif
-#ifndef AP_EXP_NOFOLD
-#define AP_EXP_NOFOLD 0
-#endif
-#ifndef AP_AUX_PRIO
-#define AP_AUX_PRIO 0
-#endif
-#ifndef AP_STAGGER
-#define AP_STAGGER 0  // > 0: first-generation second-slot blocks start this many 100-MHz ticks late
-#endif
-#ifndef AP_SETPRIO
-#define AP_SETPRIO 0  // 1: raised wave priority while a slot's MFMAs and fold issue
-#endif
-#ifndef AP_DMA_SPREAD
-#define AP_DMA_SPREAD 0  // 1: the slot's DMA pieces issued between its k16 steps, not before them
-#endif
-#ifndef AP_EXP_MX
-#define AP_EXP_MX 0  // timing only: the sweep on MX-fp8 MFMAs (2x the FP16 rate), wrong results
-#endif
-#ifndef AP_EXP_ACOAL
-#define AP_EXP_ACOAL 0
-#endif
-#ifndef AP_EXP_NODMA
-#define AP_EXP_NODMA 0
-#endif
-#ifdef AP_EXP_TRACE
-constexpr int AP_TRACE_BLOCKS = 16384;
-__device__ unsigned long long g_ap_trace[AP_TRACE_BLOCKS * 4 * 10];
-#endif
 constexpr int ROW_BYTES = KD * 2;                // fp16 row: 512 B
 constexpr int SL_ROW = BK * 2;                   // one row of one slice: 128 fp16 = 256 B = 16 chunks
 constexpr int SL_BYTES = BN * SL_ROW;            // one B slice: 16 KiB
@@ -120,7 +76,6 @@ static_assert(LDS_BYTES * (8 / NW) <= 160 * 1024, "LDS per CU");
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-typedef int v8i_t __attribute__((ext_vector_type(8)));
 
 // 16-B-per-lane HBM/L2 -> LDS DMA (global_load_lds_dwordx4, SADDR form): source = SGPR
 // base + 32-bit VGPR byte offset; LDS destination = M0 (wave-uniform byte address) + lane *
@@ -298,22 +253,6 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
     float *anrm = reinterpret_cast<float *>(lds + OFF_ANRM);
     float *misc = reinterpret_cast<float *>(lds + OFF_MISC);
 
-#ifdef AP_EXP_TRACE
-#define AP_STAMP(K) do { __builtin_amdgcn_sched_barrier(0); ts_[K] = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
-    unsigned long long ts_[8];
-    AP_STAMP(0);
-#else
-#define AP_STAMP(K) do { } while (0)
-#endif
-#if AP_STAGGER > 0
-    // blocks 256..511 (the second slot of every CU in the first dispatch generation) start
-    // AP_STAGGER ticks (100 MHz) late, so that co-resident blocks' A-load bursts alternate
-    // with each other's MFMA sweeps instead of coinciding generation after generation
-    if (blockIdx.x >= 256 && blockIdx.x < 512) {
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)AP_STAGGER) __builtin_amdgcn_s_sleep(8);
-    }
-#endif
     const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int pair = L / tiles_r, tr = L % tiles_r;
     const int n0 = min(max(n0v[pair], 0), cap), n1 = min(max(n1v[pair], 0), cap);
@@ -368,8 +307,6 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
             glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES + 12 * SL_ROW>(SB, oB[RPW / 4 - 1], dst_w); \
         }                                                                                    \
     } while (0)
-#define AP_STAGE_PIECE(SLOT, KSI, G)                                                         \
-    glds16<(KSI) * SL_ROW, (SLOT) * SL_BYTES + (G) * 4 * SL_ROW>(SB, oB[G], dst_w)
 #define AP_TILE_OFFSETS(TC)                                                                  \
     do {                                                                                     \
         const int nb_ = (TC) * BN + dr;                                                      \
@@ -397,17 +334,8 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
         float4 xs[KD / 8];  // all 32 loads in flight at once, then convert
 #pragma unroll
         for (int s = 0; s < KD / 16; s++) {
-            if (AP_EXP_NOALOAD) {
-                xs[2 * s] = make_float4(0.01f * s, 0.f, 0.f, 0.f);
-                xs[2 * s + 1] = xs[2 * s];
-            } else if (AP_EXP_ACOAL) {  // timing only: row-contiguous 1-KiB loads (wrong layout)
-                const float *rb = A + (size_t)min(row0 + w * RW + 2 * s, n0 - 1) * KD + 4 * lane;
-                xs[2 * s] = *reinterpret_cast<const float4 *>(rb);
-                xs[2 * s + 1] = *reinterpret_cast<const float4 *>(rb + (2 * s + 1 < RW ? KD : 0));
-            } else {
-                xs[2 * s] = *reinterpret_cast<const float4 *>(arow + s * 16);
-                xs[2 * s + 1] = *reinterpret_cast<const float4 *>(arow + s * 16 + 4);
-            }
+            xs[2 * s] = *reinterpret_cast<const float4 *>(arow + s * 16);
+            xs[2 * s + 1] = *reinterpret_cast<const float4 *>(arow + s * 16 + 4);
         }
         float q = 0.f;
         int out = 0;  // any |a_k| >= 2 or NaN (comparisons with NaN are false)
@@ -427,7 +355,6 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
         if (fh == 0) anrm[w * RW + fr] = out ? -1.f : q;
     }
 
-    AP_STAMP(1);
 
     // ---- B fragment map: column block c (0, 1) of a tile, lane l reads row 32 c + (l & 31)
     //      at chunk (2 s + (l >> 5)) ^ (row & 15) for k16 step s of the slice ----
@@ -462,41 +389,20 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
 #define AP_FOLD_ROWS(X0, X1, TC, Q0, Q1)                                                      \
     do {                                                                                      \
         const unsigned g0_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)(TC)), g1_ = g0_ + 1u; \
-        if (!AP_EXP_NOFOLD)                                                                   \
-            _Pragma("unroll") for (int q = (Q0); q < (Q1); q++)                               \
-                fold3(tagf(X0[q], vkeep, g0_), tagf(X1[q], vkeep, g1_), m1[q], m2[q]);        \
-        else if ((Q0) == 0) /* timing experiment: keep the MFMAs live at 1/16 of the work */   \
-            fold3(X0[0] + X0[5] + X0[10] + X0[15], X1[0] + X1[5] + X1[10] + X1[15], m1[0], m2[0]); \
+        _Pragma("unroll") for (int q = (Q0); q < (Q1); q++)                                   \
+            fold3(tagf(X0[q], vkeep, g0_), tagf(X1[q], vkeep, g1_), m1[q], m2[q]);            \
     } while (0)
 #define AP_FOLD(X0, X1, TC) AP_FOLD_ROWS(X0, X1, TC, 0, 16)
 #define AP_SLOT(J, C0, C1, F0, F1, FOLD)                                                      \
     do {                                                                                      \
         constexpr int nx = (J) + NBUF - 1;                                                    \
         const int ntile = T + nx / KS; /* tile of the slice issued now */                     \
-        const bool dma_ = !AP_EXP_NODMA && ntile < ntc;                                       \
-        if (dma_) {                                                                           \
+        if (ntile < ntc) {                                                                    \
             if constexpr (nx % KS == 0) AP_TILE_OFFSETS(ntile);                               \
-            if constexpr (!AP_DMA_SPREAD) AP_STAGE(nx % NBUF, nx % KS);                       \
+            AP_STAGE(nx % NBUF, nx % KS);                                                     \
         }                                                                                     \
         const char *base = lds + OFF_STAGE + (J) * SL_BYTES + rdb;                            \
-        if constexpr (AP_SETPRIO) __builtin_amdgcn_s_setprio(1);                              \
-        if (AP_EXP_MX) {                                                                      \
-            /* timing only: MX-fp8 MFMAs (K = 64, 32 B per lane) on the first slice of a tile */ \
-            if ((J) % KS == 0) {                                                              \
-                v8i_t b0m_[4], b1m_[4];                                                       \
-                _Pragma("unroll") for (int m_ = 0; m_ < 4; m_++) {                            \
-                    const int ch_ = ((4 * m_) ^ xsw) * 16;                                    \
-                    b0m_[m_] = *reinterpret_cast<const v8i_t *>(base + ch_);                  \
-                    b1m_[m_] = *reinterpret_cast<const v8i_t *>(base + 32 * SL_ROW + ch_);    \
-                }                                                                             \
-                _Pragma("unroll") for (int m_ = 0; m_ < 4; m_++) {                            \
-                    v8i_t a_;                                                                 \
-                    __builtin_memcpy(&a_, &aF[2 * m_], 32);                                   \
-                    C0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a_, b0m_[m_], m_ == 0 ? zero16 : C0, 0, 0, 0, 127, 0, 127); \
-                    C1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a_, b1m_[m_], m_ == 0 ? zero16 : C1, 0, 0, 0, 127, 0, 127); \
-                }                                                                             \
-            }                                                                                 \
-        } else if (!AP_EXP_NOMFMA) {                                                          \
+        {                                                                                     \
             /* fragment reads run PF k16 steps ahead of the MFMAs (counted lgkm waits) */      \
             constexpr int PF = 4;                                                             \
             f16x8 b0_[BK / 16], b1_[BK / 16];                                                 \
@@ -505,13 +411,6 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
                     const int ch_ = ((2 * s_) ^ xsw) * 16;                                    \
                     b0_[s_] = *reinterpret_cast<const f16x8 *>(base + ch_);                   \
                     b1_[s_] = *reinterpret_cast<const f16x8 *>(base + 32 * SL_ROW + ch_);     \
-                }                                                                             \
-                /* spread: one DMA piece after every other k16 step's fragment reads */         \
-                if constexpr (AP_DMA_SPREAD) if (dma_) {                                      \
-                    if (s_ == 1) AP_STAGE_PIECE(nx % NBUF, nx % KS, 0);                       \
-                    if (s_ == 3) AP_STAGE_PIECE(nx % NBUF, nx % KS, 1);                       \
-                    if (RPW == 16 && s_ == 5) AP_STAGE_PIECE(nx % NBUF, nx % KS, RPW / 4 - 2); \
-                    if (RPW == 16 && s_ == 7) AP_STAGE_PIECE(nx % NBUF, nx % KS, RPW / 4 - 1); \
                 }                                                                             \
                 if (s_ >= PF) {                                                               \
                     const int m_ = s_ - PF;                                                   \
@@ -524,19 +423,16 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
         }                                                                                     \
         /* the previous tile's fold, half of its rows beside each k-slice's MFMAs */          \
         if (FOLD) AP_FOLD_ROWS(F0, F1, T + (J) / KS - 1, 8 * ((J) % KS), 8 * ((J) % KS) + 8);  \
-        if constexpr (AP_SETPRIO) __builtin_amdgcn_s_setprio(0);                              \
-        if (AP_EXP_NOWAIT) {                                                                  \
-        } else if (ntile < ntc) {                                                             \
+        if (ntile < ntc) {                                                                    \
             wait_vm<DMA_PER_SLICE * (NBUF - 2)>();                                            \
         } else {                                                                              \
             wait_vm<0>(); /* tail of the sweep: drain */                                      \
         }                                                                                     \
-        if (!AP_EXP_NOBAR) __syncthreads();                                                   \
+        __syncthreads();                                                                      \
     } while (0)
 
     wait_vm<0>();
     __syncthreads();
-    AP_STAMP(2);
     float bmax2 = misc[0];
 #pragma unroll
     for (int k = 1; k < NW; k++) bmax2 = fmaxf(bmax2, misc[k]);
@@ -548,7 +444,6 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
             AP_SLOT(3, accB0, accB1, accA0, accA1, true);
         }
     }
-    AP_STAMP(3);
     if (ntc > 0) {  // the last tile: columns past n1 pushed to a finite -3e38 (a tag keeps it finite)
         const int tl = ntc - 1;
         f32x16 x0 = (tl & 1) ? accB0 : accA0, x1 = (tl & 1) ? accB1 : accA1;
@@ -608,7 +503,6 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
         M = fmaxf(M, oM);
     }
 
-    AP_STAMP(4);
     // ---- decide row w*32 + fr in its two lanes.  Window (unscaled): delta bounds screen vs
     //      exact score per column; a tag moves a value by < rho |value|, rho = 2^(tb-23), so
     //      dp = delta + 2.2 rho (|M| + 2 delta) bounds |tagged screen - exact| for every column
@@ -640,7 +534,7 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
     // exact dot are treated as competitors (a distance tie needs |d1 - d2| of a few ulp)
     const double tie = dmode ? 1e-5 : 0.0;
     if (wide && fh == 0) lmask[rl] = 0xffffffffu;
-    if (live && !full && !AP_EXP_NOFOLD) {  // (the NOFOLD experiment leaves untagged values)
+    if (live && !full) {
         const double an = sqrt(fmax((double)an2, 0.0));
         const double delta =
             (rel * an * Bn + 1.001 * 5.9604644775390625e-08 * (an + Bn) + 3.552713678800501e-15) * 1.01 + 1e-30;
@@ -666,7 +560,7 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
                     // clears both tests, the maximiser's exact dot decides nothing -- skip it
                     const bool sure = !oscore && (dmode || Ms - dp > fmax(thresh, 0.0));
                     // (Ms = M 2^-28 is exact in float, and Ms > thresh, Ms > 0: the keep test passes)
-                    bs = sure ? (float)Ms : AP_EXP_NOEXACT ? M : exact_dot(arow, B + (size_t)I * KD);
+                    bs = sure ? (float)Ms : exact_dot(arow, B + (size_t)I * KD);
                     if (dmode) bs = sure ? 0.f : dist_of(bs);
                     bj = I;
                 }
@@ -724,7 +618,6 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
         if (oscore) oscore[rl] = keep ? bs : 0.f;
     }
 
-    AP_STAMP(5);
     // ---- wide rows (rare): the wave scores every column of every listed lane exactly, one
     //      column per lane at a time (lane l: columns f + 32 (l + 64 i) of inside lane f) ----
     for (unsigned dm = (unsigned)__ballot(fh == 0 && wide); dm; dm &= dm - 1) {
@@ -767,16 +660,6 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
             if (oscore) oscore[r] = keep ? ws : 0.f;
         }
     }
-#ifdef AP_EXP_TRACE
-    AP_STAMP(6);
-    AP_STAMP(7);
-    if (lane == 0 && blockIdx.x < AP_TRACE_BLOCKS) {
-        unsigned long long *o = g_ap_trace + ((size_t)blockIdx.x * NW + w) * 10;
-        for (int k = 0; k < 8; k++) o[k] = ts_[k];
-        o[8] = __smid();
-        o[9] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
 }
 
 }  // namespace
@@ -919,15 +802,7 @@ extern "C" int mv_match_allpairs_f32_prepare_dev(mv_context *ctx, int batch, int
     void *scr = ap_scratch(ctx, mv::ap_image_bytes(ctx->ap_screen, batch, cap));
     if (!scr) return MV_ERR_OUT_OF_MEMORY;
     if (!ctx->aux_stream) {
-#if AP_AUX_PRIO
-        // the staging stream at the highest priority: its HBM-bound split then runs ahead of
-        // the latency-bound pose kernels it overlaps (timing switch, AP_AUX_PRIO=1)
-        int prio_lo = 0, prio_hi = 0;
-        MV_HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-        MV_HIP_TRY(hipStreamCreateWithPriority(&ctx->aux_stream, hipStreamNonBlocking, prio_hi));
-#else
         MV_HIP_TRY(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
-#endif
         MV_HIP_TRY(hipEventCreateWithFlags(&ctx->ev_in, hipEventDisableTiming));
         MV_HIP_TRY(hipEventCreateWithFlags(&ctx->ev_prep, hipEventDisableTiming));
     }
@@ -1092,12 +967,6 @@ extern "C" int mv_match_two_way_f32_dev(mv_context *ctx, int batch, int cap, con
     return mv::set_status(MV_OK);
 }
 
-#ifdef AP_EXP_TRACE
-// timing experiment only: per-(block, wave) phase stamps of the last k_ap_match launch
-extern "C" int mv_debug_ap_trace(void *host, long bytes) {
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ap_trace), (size_t)bytes) == hipSuccess ? 0 : -3;
-}
-#endif
 
 extern "C" int mv_match_sequence_f32_dev(mv_context *ctx, int frames, int cap, const int *n, const float *desc,
                                          double thresh, int *match_idx, float *match_score) {

@@ -44,15 +44,6 @@ constexpr int NT = 256;
 #ifndef PE_TRACE
 #define PE_TRACE 0  // printf per-phase clock64() deltas of block 0 (timing experiments only)
 #endif
-#ifndef PE_NODECOMP
-#define PE_NODECOMP 0
-#endif
-#ifndef PE_NOSCORE
-#define PE_NOSCORE 0
-#endif
-#ifndef PE_NOHYP
-#define PE_NOHYP 0
-#endif
 #ifndef PE_WAVES
 #define PE_WAVES 4  // waves per SIMD (4: 128 VGPRs, 13 spilled, 3% faster than 3 at 142)
 #endif
@@ -526,13 +517,9 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
         }
         if (drawn < 8) continue;
         float e[9];
-        if (PE_NOHYP) {
-            for (int r = 0; r < 9; r++) e[r] = P[idx[r & 7]].x + r;
-        } else if (!eight_point(P, idx, e)) {
-            continue;
-        }
+        if (!eight_point(P, idx, e)) continue;
         f2v acc = {0.f, 0.f};
-        const int m2 = PE_NOSCORE ? 0 : m / 2;
+        const int m2 = m / 2;
         int k = 0;
         for (; k + 2 <= m2; k += 2) {  // 4 LDS broadcast reads in flight per step
             const float4 A0 = s_sub[k][0], B0 = s_sub[k][1], A1 = s_sub[k + 1][0], B1 = s_sub[k + 1][1];
@@ -541,7 +528,7 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
         }
         if (k < m2) acc += msac_cost2(e, s_sub[k][0], s_sub[k][1], a.thr2);
         float cost = acc.x + acc.y;
-        if (!PE_NOSCORE && (m & 1)) {
+        if (m & 1) {
             int c = 0;
             cost += msac_cost(e, P[((m - 1) * step16) >> 16], a.thr2, c);
         }
@@ -677,12 +664,7 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
         for (int r = 0; r < 9; r++) E[r] = s_E[sti][r];
         if (t == 0) {
             float U[3][3], V[3][3];
-            if (PE_NODECOMP) {
-                for (int i = 0; i < 3; i++)
-                    for (int j = 0; j < 3; j++) U[i][j] = V[i][j] = i == j;
-            } else {
-                essential_uv(E, U, V);
-            }
+            essential_uv(E, U, V);
             for (int i = 0; i < 3; i++)
                 for (int j = 0; j < 3; j++) {
                     s_uv[0][i][j] = U[i][j];
