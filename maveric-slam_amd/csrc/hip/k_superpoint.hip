@@ -61,6 +61,15 @@ __device__ __forceinline__ int requant_bits(int a, float rs, int lo_bits) {
     return max(min(bits, SP_MAGIC_BITS + 127), lo_bits);
 }
 // low bytes of four requantised words -> one dword
+// The 4 packed dwords a lane holds of one 32-channel block (channels 8 qq + 4 fh .. +3, qq = 0..3:
+// the MFMA's row layout) regrouped across the lane pair (l, l ^ 32) into 16 CONTIGUOUS channels
+// 16 fh .. +15 by two v_permlane32_swap (lanes 32-63 of the first operand <-> lanes 0-31 of the
+// second): one 16-B store per lane instead of four scattered 4-B ones.
+__device__ __forceinline__ i32x4 regroup16(const int (&d)[4]) {
+    const auto p02 = __builtin_amdgcn_permlane32_swap(d[0], d[2], false, false);
+    const auto p13 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);
+    return i32x4{(int)p02[0], (int)p02[1], (int)p13[0], (int)p13[1]};
+}
 __device__ __forceinline__ int pack4b(int a, int b, int c, int d) {
     const unsigned ab = __builtin_amdgcn_perm((unsigned)b, (unsigned)a, 0x0c0c0400u);
     const unsigned cd = __builtin_amdgcn_perm((unsigned)d, (unsigned)c, 0x0c0c0400u);
@@ -236,11 +245,27 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
         ra[u] = u < NS ? wa[u * 64] : i32x4{0, 0, 0, 0};
         rb[u] = u < NS ? wb[u * 64] : i32x4{0, 0, 0, 0};
     }
+    // the accumulators start at the layer's quantised bias (row q of channel block cb = channel
+    // 64 g + 32 cb + 8 (q >> 2) + 4 fh + (q & 3)): no add in the epilogue, and the 2 x 2 max pool
+    // commutes with it
     i32x16 acc[4][2];
+    {
+        i32x16 b0, b1;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        acc[j][0] = i32x16{};
-        acc[j][1] = i32x16{};
+        for (int qq = 0; qq < 4; qq++) {
+            const i32x4 x0 = *reinterpret_cast<const i32x4 *>(bq + 64 * g + 8 * qq + 4 * fh);
+            const i32x4 x1 = *reinterpret_cast<const i32x4 *>(bq + 64 * g + 32 + 8 * qq + 4 * fh);
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                b0[4 * qq + e] = x0[e];
+                b1[4 * qq + e] = x1[e];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            acc[j][0] = b0;
+            acc[j][1] = b1;
+        }
     }
     // per-lane bases: row 4w + j, column fr, chunk half fh (padded layout); XOR terms per kx
     const i32x4 *lb = tile + ((4 * w) * IX + fr) * PS + (PADL ? fh : 0);
@@ -267,6 +292,76 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
 
     // ---- epilogue: lane = pixel fr of each row; 16 couts (4 groups of 4) per 32-cout block ----
     const int lo = SP_MAGIC_BITS + (RELU ? 0 : -128);
+    if constexpr (CIN == 64) {
+        // 64-channel layers (168 VGPRs: the lane-pair regroup below spilled the K loop): each wave writes its
+        // requantised outputs into its own LDS rows (64 B + 16 B of pad per pixel), then reads them
+        // back 16 B per lane and stores whole pixel runs -- 2 KiB contiguous per output row
+        constexpr int PB = 80;
+        static_assert(4 * 4 * 32 * PB <= IY * IX * PS * 16, "staging fits the input tile");
+        __syncthreads();  // every wave past its last read of the input tile
+        char *stg = reinterpret_cast<char *>(tile) + w * (4 * 32 * PB);
+        if constexpr (POOL) {
+            const int Ho = H / 2, Wo = W / 2;
+#pragma unroll
+            for (int jp = 0; jp < 2; jp++) {
+#pragma unroll
+                for (int cb = 0; cb < 2; cb++) {
+                    int m[16];
+#pragma unroll
+                    for (int q = 0; q < 16; q++) {
+                        const int v = max(acc[2 * jp][cb][q], acc[2 * jp + 1][cb][q]);
+                        m[q] = max(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));  // lane ^ 1 (quad_perm [1,0,3,2])
+                    }
+                    if ((fr & 1) == 0) {
+#pragma unroll
+                        for (int qq = 0; qq < 4; qq++) {
+                            int v[4];
+#pragma unroll
+                            for (int e = 0; e < 4; e++) v[e] = requant_bits(m[4 * qq + e], rs, lo);
+                            *reinterpret_cast<int *>(stg + (jp * 16 + fr / 2) * PB + 32 * cb + 8 * qq + 4 * fh) =
+                                pack4b(v[0], v[1], v[2], v[3]);
+                        }
+                    }
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes done
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int jp = 0; jp < 2; jp++) {
+                const int p = lane >> 2, k = lane & 3;  // 16 pooled pixels x 4 chunks
+                const int gy = y0 + 4 * w + 2 * jp, gx = x0 + 2 * p;
+                const i32x4 v = *reinterpret_cast<const i32x4 *>(stg + (jp * 16 + p) * PB + 16 * k);
+                if (gy < H && gx < W)
+                    *reinterpret_cast<i32x4 *>(out + (((size_t)b * Ho + gy / 2) * Wo + gx / 2) * cstride + 64 * g + 16 * k) = v;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+#pragma unroll
+                for (int cb = 0; cb < 2; cb++)
+#pragma unroll
+                    for (int qq = 0; qq < 4; qq++) {
+                        int v[4];
+#pragma unroll
+                        for (int e = 0; e < 4; e++) v[e] = requant_bits(acc[j][cb][4 * qq + e], rs, lo);
+                        *reinterpret_cast<int *>(stg + (j * 32 + fr) * PB + 32 * cb + 8 * qq + 4 * fh) =
+                            pack4b(v[0], v[1], v[2], v[3]);
+                    }
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+                    const int c = lane + 64 * i, p = c >> 2, k = c & 3;  // 32 pixels x 4 chunks
+                    const int gy = y0 + 4 * w + j, gx = x0 + p;
+                    const i32x4 v = *reinterpret_cast<const i32x4 *>(stg + (j * 32 + p) * PB + 16 * k);
+                    if (gy < H && gx < W)
+                        *reinterpret_cast<i32x4 *>(out + (((size_t)b * H + gy) * W + gx) * cstride + 64 * g + 16 * k) = v;
+                }
+        }
+        return;
+    }
     if constexpr (POOL) {
         const int Ho = H / 2, Wo = W / 2;
 #pragma unroll
@@ -278,36 +373,53 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
 #pragma unroll
                 for (int q = 0; q < 16; q++) {
                     const int v = max(acc[2 * jp][cb][q], acc[2 * jp + 1][cb][q]);
-                    m[q] = max(v, __shfl_xor(v, 1, 64));
+                    m[q] = max(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));  // lane ^ 1 (quad_perm [1,0,3,2])
                 }
-                if ((fr & 1) == 0 && gy < H && gx < W) {
+                if ((fr & 1) == 0 && gy < H && gx < W) {  // both lanes of a pair (same fr) or neither
                     int8_t *dst = out + (((size_t)b * Ho + gy / 2) * Wo + gx / 2) * cstride;
+                    int d[4];
 #pragma unroll
                     for (int qq = 0; qq < 4; qq++) {
                         const int co = 64 * g + 32 * cb + 8 * qq + 4 * fh;
                         int v[4];
 #pragma unroll
-                        for (int e = 0; e < 4; e++) v[e] = requant_bits(m[4 * qq + e] + bq[co + e], rs, lo);
-                        *reinterpret_cast<int *>(dst + co) = pack4b(v[0], v[1], v[2], v[3]);
+                        for (int e = 0; e < 4; e++) v[e] = requant_bits(m[4 * qq + e], rs, lo);
+                        d[qq] = pack4b(v[0], v[1], v[2], v[3]);
                     }
+                    *reinterpret_cast<i32x4 *>(dst + 64 * g + 32 * cb + 16 * fh) = regroup16(d);
                 }
+                __builtin_amdgcn_sched_barrier(0);  // one block at a time: the register budget
             }
         }
     } else {
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int gy = y0 + 4 * w + j, gx = x0 + fr;
-            if (gy >= H || gx >= W) continue;
+            if (gy >= H || gx >= W) continue;  // both lanes of a pair (same fr) or neither
             int8_t *dst = OMODE == 0 ? out + (((size_t)b * H + gy) * W + gx) * cstride
                                      : out + ((size_t)b * H * W + (size_t)gx * H + gy) * cstride;
 #pragma unroll
             for (int cb = 0; cb < 2; cb++) {
+                if constexpr (OMODE == 0) {  // NHWC activations: 64 / 128 / 256 channels (host-checked)
+                    int d[4];
+#pragma unroll
+                    for (int qq = 0; qq < 4; qq++) {
+                        const int co = 64 * g + 32 * cb + 8 * qq + 4 * fh;
+                        int v[4];
+#pragma unroll
+                        for (int e = 0; e < 4; e++) v[e] = requant_bits(acc[j][cb][4 * qq + e], rs, lo);
+                        d[qq] = pack4b(v[0], v[1], v[2], v[3]);
+                    }
+                    *reinterpret_cast<i32x4 *>(dst + 64 * g + 32 * cb + 16 * fh) = regroup16(d);
+                    __builtin_amdgcn_sched_barrier(0);  // one block at a time: the register budget
+                    continue;
+                }
 #pragma unroll
                 for (int qq = 0; qq < 4; qq++) {
                     const int co = 64 * g + 32 * cb + 8 * qq + 4 * fh;
                     int v[4];
 #pragma unroll
-                    for (int e = 0; e < 4; e++) v[e] = requant_bits(acc[j][cb][4 * qq + e] + bq[co + e], rs, lo);
+                    for (int e = 0; e < 4; e++) v[e] = requant_bits(acc[j][cb][4 * qq + e], rs, lo);
                     if (OMODE == 0 || (cstride % 4 == 0 && co + 4 <= cstride)) {
                         *reinterpret_cast<int *>(dst + co) = pack4b(v[0], v[1], v[2], v[3]);
                     } else {
@@ -363,11 +475,19 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv1x1(const int8_t *__restric
     for (int s = 0; s < 2; s++)
 #pragma unroll
         for (int cb = 0; cb < H1_CB; cb++) aq[s][cb] = wa[(cb * NS + s) * 64];
-    i32x16 acc[2][H1_CB];
+    i32x16 acc[2][H1_CB];  // from the quantised bias, as in k_sp_conv
 #pragma unroll
-    for (int j = 0; j < 2; j++)
+    for (int cb = 0; cb < H1_CB; cb++) {
+        i32x16 bv;
 #pragma unroll
-        for (int cb = 0; cb < H1_CB; cb++) acc[j][cb] = i32x16{};
+        for (int qq = 0; qq < 4; qq++) {
+            const i32x4 x = *reinterpret_cast<const i32x4 *>(bq + 32 * (H1_CB * g + cb) + 8 * qq + 4 * fh);
+#pragma unroll
+            for (int e = 0; e < 4; e++) bv[4 * qq + e] = x[e];
+        }
+        acc[0][cb] = bv;
+        acc[1][cb] = bv;
+    }
     const i32x4 *lb = tile + ((2 * w) * TX + fr) * H1_PS + fh;
 #pragma unroll
     for (int s = 0; s < NS; s++) {
@@ -393,13 +513,26 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv1x1(const int8_t *__restric
                                  : out + ((size_t)b * H * W + (size_t)gx * H + gy) * cstride;
 #pragma unroll
         for (int cb = 0; cb < H1_CB; cb++) {
+            if (cstride % 16 == 0 && 32 * (H1_CB * g + cb) < cstride) {  // convDb (256 channels)
+                int d[4];
+#pragma unroll
+                for (int qq = 0; qq < 4; qq++) {
+                    const int co = 32 * (H1_CB * g + cb) + 8 * qq + 4 * fh;
+                    int v[4];
+#pragma unroll
+                    for (int e = 0; e < 4; e++) v[e] = requant_bits(acc[j][cb][4 * qq + e], rs, lo);
+                    d[qq] = pack4b(v[0], v[1], v[2], v[3]);
+                }
+                *reinterpret_cast<i32x4 *>(dst + 32 * (H1_CB * g + cb) + 16 * fh) = regroup16(d);
+                continue;
+            }
 #pragma unroll
             for (int qq = 0; qq < 4; qq++) {
                 const int co = 32 * (H1_CB * g + cb) + 8 * qq + 4 * fh;
                 if (co >= cstride) continue;
                 int v[4];
 #pragma unroll
-                for (int e = 0; e < 4; e++) v[e] = requant_bits(acc[j][cb][4 * qq + e] + bq[co + e], rs, lo);
+                for (int e = 0; e < 4; e++) v[e] = requant_bits(acc[j][cb][4 * qq + e], rs, lo);
                 if (OMODE == 0 || (cstride % 4 == 0 && co + 4 <= cstride)) {
                     *reinterpret_cast<int *>(dst + co) = pack4b(v[0], v[1], v[2], v[3]);
                 } else {
@@ -551,6 +684,8 @@ int launch_conv(hipStream_t st, const mv_superpoint *net, int li, int B, int H, 
     const int tiles_x = (W + TX - 1) / TX, tiles_y = (H + TY - 1) / TY, ngroups = net->cout_pad[li] / 64;
     const long blocks = (long)B * ngroups * tiles_y * tiles_x;
     MV_REQUIRE(blocks < (1l << 31));
+    // the epilogue stores 16 B per lane: NHWC outputs with 16-B aligned pixels
+    MV_REQUIRE((OMODE != 0 && !POOL) || (cstride % 16 == 0 && cstride >= 64 * ngroups && ((uintptr_t)out & 15) == 0));
     const char *wd = static_cast<const char *>(net->wdev);
     hipLaunchKernelGGL((k_sp_conv<CIN, KS, POOL, RELU, OMODE, FUSE1A>), dim3((unsigned)blocks), dim3(SP_NT), 0, st, in,
                        H, W, reinterpret_cast<const i32x4 *>(wd + net->frag_off[li]),
