@@ -380,7 +380,6 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
                     int d[4];
 #pragma unroll
                     for (int qq = 0; qq < 4; qq++) {
-                        const int co = 64 * g + 32 * cb + 8 * qq + 4 * fh;
                         int v[4];
 #pragma unroll
                         for (int e = 0; e < 4; e++) v[e] = requant_bits(m[4 * qq + e], rs, lo);
@@ -404,7 +403,6 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
                     int d[4];
 #pragma unroll
                     for (int qq = 0; qq < 4; qq++) {
-                        const int co = 64 * g + 32 * cb + 8 * qq + 4 * fh;
                         int v[4];
 #pragma unroll
                         for (int e = 0; e < 4; e++) v[e] = requant_bits(acc[j][cb][4 * qq + e], rs, lo);
@@ -517,7 +515,6 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv1x1(const int8_t *__restric
                 int d[4];
 #pragma unroll
                 for (int qq = 0; qq < 4; qq++) {
-                    const int co = 32 * (H1_CB * g + cb) + 8 * qq + 4 * fh;
                     int v[4];
 #pragma unroll
                     for (int e = 0; e < 4; e++) v[e] = requant_bits(acc[j][cb][4 * qq + e], rs, lo);
@@ -563,44 +560,63 @@ __device__ __forceinline__ void sp_head(int8_t *semi, int8_t *desc, long cells, 
 
 __global__ __launch_bounds__(SP_NT) void k_sp_presence(const int8_t *__restrict__ semi, const int8_t *__restrict__ desc,
                                                        long cells, unsigned *__restrict__ pres) {
-    const int b = blockIdx.x, h = blockIdx.y, t = threadIdx.x, lane = t & 63;
+    // per wave 8 replicas of a 256-byte "seen" array in LDS (lane l stores into replica l & 7,
+    // replicas 65 dwords apart: neighbouring lanes' equal codes land in different banks): one
+    // byte store per code (lanes storing the same code store the same 1: no atomics), then the
+    // replicas are ORed and 4 ballots turn them into the 256-bit mask
+    constexpr int RS = 65 * 4;  // replica stride, bytes
+    __shared__ unsigned seen_w[SP_NT / 64][8 * RS / 4];
+    const int b = blockIdx.x, h = blockIdx.y, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    unsigned char *seen_all = reinterpret_cast<unsigned char *>(seen_w[w]);
+    unsigned char *seen = seen_all + (lane & 7) * RS;
+    for (int i = lane; i < 8 * RS / 4; i += 64) seen_w[w][i] = 0u;
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
     int8_t *base;
     long lo, hi;
     sp_head(const_cast<int8_t *>(semi), const_cast<int8_t *>(desc), cells, b, h, base, lo, hi);
-    unsigned m[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     const bool al = ((uintptr_t)(base + lo) & 15) == 0;
-    for (long i = lo + 16 * t; i < hi; i += 16 * SP_NT) {
-        int v4[4];
-        if (al && i + 16 <= hi) {
-            const i32x4 v = *reinterpret_cast<const i32x4 *>(base + i);
-            v4[0] = v[0], v4[1] = v[1], v4[2] = v[2], v4[3] = v[3];
-        } else {
-            for (int k = 0; k < 4; k++) {
-                int x = 0;
-                for (int e = 0; e < 4; e++) {
-                    const long j = i + 4 * k + e;
-                    // past the chunk: repeat its first code (already present)
-                    x |= ((j < hi ? base[j] : base[lo]) & 0xff) << (8 * e);
-                }
-                v4[k] = x;
-            }
+    constexpr int U = 4;  // 16-B loads in flight per thread
+    for (long i0 = lo + 16 * t; i0 < hi; i0 += 16 * SP_NT * U) {
+        i32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const long i = i0 + 16 * SP_NT * u;
+            if (al && i + 16 <= hi) v[u] = *reinterpret_cast<const i32x4 *>(base + i);
         }
 #pragma unroll
-        for (int k = 0; k < 4; k++)
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                const int v = ((v4[k] << (24 - 8 * e)) >> 24) + 128;
-                const unsigned bit = 1u << (v & 31);
-#pragma unroll
-                for (int q = 0; q < 8; q++) m[q] |= (v >> 5) == q ? bit : 0u;
+        for (int u = 0; u < U; u++) {
+            const long i = i0 + 16 * SP_NT * u;
+            if (i >= hi) break;
+            if (!(al && i + 16 <= hi)) {
+                for (int k = 0; k < 4; k++) {
+                    int x = 0;
+                    for (int e = 0; e < 4; e++) {
+                        const long j = i + 4 * k + e;
+                        // past the chunk: repeat its first code (already present)
+                        x |= ((j < hi ? base[j] : base[lo]) & 0xff) << (8 * e);
+                    }
+                    v[u][k] = x;
+                }
             }
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+#pragma unroll
+                for (int e = 0; e < 4; e++) seen[((v[u][k] << (24 - 8 * e)) >> 24) + 128] = 1;
+        }
     }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int q = 0; q < 8; q++) {
-        unsigned x = m[q];
+    for (int k = 0; k < 4; k++) {  // codes 64 k .. 64 k + 63: words 2 k, 2 k + 1
+        unsigned any = 0;
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) x |= __shfl_xor(x, o, 64);
-        if (lane == 0 && x) atomicOr(&pres[(b * 2 + h) * 8 + q], x);
+        for (int r = 0; r < 8; r++) any |= seen_all[r * RS + 64 * k + lane];
+        const unsigned long long bm = __ballot(any != 0);
+        if (lane == 0) {
+            if ((unsigned)bm) atomicOr(&pres[(b * 2 + h) * 8 + 2 * k], (unsigned)bm);
+            if ((unsigned)(bm >> 32)) atomicOr(&pres[(b * 2 + h) * 8 + 2 * k + 1], (unsigned)(bm >> 32));
+        }
     }
 }
 
@@ -609,6 +625,7 @@ __global__ __launch_bounds__(SP_NT) void k_sp_min_gap(int8_t *__restrict__ semi,
                                                       float *__restrict__ semi_scale, float *__restrict__ desc_scale) {
     __shared__ float gmin[SP_NT / 64];
     __shared__ int cnts[SP_NT / 64];
+    __shared__ unsigned char lut[256];  // code + 128 -> its rounded value (one division per code)
     const int b = blockIdx.x, h = blockIdx.y, t = threadIdx.x, lane = t & 63;
     const float s = h ? s_desc : s_semi;
     const unsigned *pm = pres + (b * 2 + h) * 8;
@@ -658,23 +675,43 @@ __global__ __launch_bounds__(SP_NT) void k_sp_min_gap(int8_t *__restrict__ semi,
         float r = __builtin_rintf(f / g);
         return (int)fminf(fmaxf(r, -128.f), 127.f);
     };
+    lut[t] = (unsigned char)requant(t - 128);  // SP_NT = 256 threads: one code each
+    __syncthreads();
     const bool al = ((uintptr_t)(base + lo) & 15) == 0;
-    long i = lo + 16 * t;
-    for (; al && i + 16 <= hi; i += 16 * SP_NT) {  // 16 codes per thread per step
-        i32x4 v = *reinterpret_cast<const i32x4 *>(base + i);
+    if (al) {
+        constexpr int U = 4;  // 16 codes per load, 4 loads in flight per thread
+        long i0 = lo + 16 * t;
+        for (; i0 + 16 * SP_NT * (U - 1) + 16 <= hi; i0 += 16 * SP_NT * U) {
+            i32x4 v[U];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            int o[4];
+            for (int u = 0; u < U; u++) v[u] = *reinterpret_cast<const i32x4 *>(base + i0 + 16 * SP_NT * u);
 #pragma unroll
-            for (int e = 0; e < 4; e++) o[e] = requant((v[k] << (24 - 8 * e)) >> 24);
-            v[k] = (o[0] & 0xff) | ((o[1] & 0xff) << 8) | ((o[2] & 0xff) << 16) | (o[3] << 24);
+            for (int u = 0; u < U; u++) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const unsigned x = (unsigned)v[u][k] ^ 0x80808080u;  // bytes = code + 128
+                    v[u][k] = (int)(lut[x & 0xff] | (lut[(x >> 8) & 0xff] << 8) | (lut[(x >> 16) & 0xff] << 16) |
+                                    ((unsigned)lut[x >> 24] << 24));
+                }
+                *reinterpret_cast<i32x4 *>(base + i0 + 16 * SP_NT * u) = v[u];
+            }
         }
-        *reinterpret_cast<i32x4 *>(base + i) = v;
-    }
-    if (al) {  // the one partial chunk at the end (its thread only)
-        for (long j = i; j < hi && j < i + 16; j++) base[j] = (int8_t)requant(base[j]);
+        for (; i0 < hi; i0 += 16 * SP_NT) {  // the rest: whole 16-B pieces, then the partial one
+            if (i0 + 16 <= hi) {
+                i32x4 v = *reinterpret_cast<const i32x4 *>(base + i0);
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const unsigned x = (unsigned)v[k] ^ 0x80808080u;
+                    v[k] = (int)(lut[x & 0xff] | (lut[(x >> 8) & 0xff] << 8) | (lut[(x >> 16) & 0xff] << 16) |
+                                 ((unsigned)lut[x >> 24] << 24));
+                }
+                *reinterpret_cast<i32x4 *>(base + i0) = v;
+            } else {
+                for (long j = i0; j < hi; j++) base[j] = (int8_t)lut[(int)base[j] + 128];
+            }
+        }
     } else {
-        for (long j = lo + t; j < hi; j += SP_NT) base[j] = (int8_t)requant(base[j]);
+        for (long j = lo + t; j < hi; j += SP_NT) base[j] = (int8_t)lut[(int)base[j] + 128];
     }
 }
 
