@@ -544,7 +544,9 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv1x1(const int8_t *__restric
 
 // run()'s output quantisation (superpoint_inference.py:199-206), head h (0: semi, C = 65;
 // 1: desc, C = 256) of frame b, split over SP_MG_CHUNKS workgroups per head: k_sp_presence ORs
-// the 256-code presence mask of a chunk into pres[b][h][8]; k_sp_min_gap derives the smallest
+// the 256-code presence mask of a chunk into pres[b][h][chunk][8] (its own slot: no atomics, no
+// clearing -- 128 waves ORing into one (frame, head)'s 32 B serialised at the L2); k_sp_min_gap
+// ORs a head's chunk masks, derives the smallest
 // gap between present dequantised codes (every workgroup, from the same mask) and rounds its
 // chunk to that step in place.
 constexpr int SP_MG_CHUNKS = 32;
@@ -607,6 +609,7 @@ __global__ __launch_bounds__(SP_NT) void k_sp_presence(const int8_t *__restrict_
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
+    __shared__ unsigned wm[SP_NT / 64][8];
 #pragma unroll
     for (int k = 0; k < 4; k++) {  // codes 64 k .. 64 k + 63: words 2 k, 2 k + 1
         unsigned any = 0;
@@ -614,9 +617,16 @@ __global__ __launch_bounds__(SP_NT) void k_sp_presence(const int8_t *__restrict_
         for (int r = 0; r < 8; r++) any |= seen_all[r * RS + 64 * k + lane];
         const unsigned long long bm = __ballot(any != 0);
         if (lane == 0) {
-            if ((unsigned)bm) atomicOr(&pres[(b * 2 + h) * 8 + 2 * k], (unsigned)bm);
-            if ((unsigned)(bm >> 32)) atomicOr(&pres[(b * 2 + h) * 8 + 2 * k + 1], (unsigned)(bm >> 32));
+            wm[w][2 * k] = (unsigned)bm;
+            wm[w][2 * k + 1] = (unsigned)(bm >> 32);
         }
+    }
+    __syncthreads();
+    if (t < 8) {
+        unsigned x = 0;
+#pragma unroll
+        for (int k = 0; k < SP_NT / 64; k++) x |= wm[k][t];
+        pres[((size_t)(b * 2 + h) * SP_MG_CHUNKS + blockIdx.z) * 8 + t] = x;
     }
 }
 
@@ -628,7 +638,15 @@ __global__ __launch_bounds__(SP_NT) void k_sp_min_gap(int8_t *__restrict__ semi,
     __shared__ unsigned char lut[256];  // code + 128 -> its rounded value (one division per code)
     const int b = blockIdx.x, h = blockIdx.y, t = threadIdx.x, lane = t & 63;
     const float s = h ? s_desc : s_semi;
-    const unsigned *pm = pres + (b * 2 + h) * 8;
+    __shared__ unsigned pm[8];  // the head's mask: its chunks' masks ORed
+    if (t < 8) {
+        const unsigned *pc = pres + (size_t)(b * 2 + h) * SP_MG_CHUNKS * 8 + t;
+        unsigned x = 0;
+#pragma unroll
+        for (int c = 0; c < SP_MG_CHUNKS; c++) x |= pc[8 * c];
+        pm[t] = x;
+    }
+    __syncthreads();
     // thread v: the gap from code v (present) to the next present code, in dequantised floats
     float gap = INFINITY;
     int cnt;
@@ -866,7 +884,7 @@ extern "C" int mv_superpoint_forward_dev(mv_context *ctx, mv_superpoint *net, in
     // largest after the fused conv1a)
     const size_t a_bytes = mv::align_up((size_t)batch * oh * ow * 16, 256);
     const size_t b_bytes = a_bytes;
-    const size_t need = a_bytes + b_bytes + (size_t)batch * 2 * 8 * sizeof(unsigned);  // + presence masks
+    const size_t need = a_bytes + b_bytes + (size_t)batch * 2 * SP_MG_CHUNKS * 8 * sizeof(unsigned);  // + presence masks
     if (net->act_bytes < need) {
         if (net->act) {
             const int q = mv::quiesce(ctx);
@@ -907,7 +925,6 @@ extern "C" int mv_superpoint_forward_dev(mv_context *ctx, mv_superpoint *net, in
     MV_PROF_END(st);
     MV_PROF_BEGIN(st, "k_sp_min_gap");
     unsigned *pres = reinterpret_cast<unsigned *>(Bf + b_bytes);
-    MV_HIP_TRY(hipMemsetAsync(pres, 0, (size_t)batch * 2 * 8 * sizeof(unsigned), st));
     hipLaunchKernelGGL(k_sp_presence, dim3((unsigned)batch, 2, SP_MG_CHUNKS), dim3(SP_NT), 0, st, semi, desc,
                        (long)h * w, pres);
     MV_LAUNCH_CHECK();
