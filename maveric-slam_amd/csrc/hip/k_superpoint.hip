@@ -137,20 +137,33 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
         constexpr int QY = IY + 2, QX = IX + 2, QXS = QX + 2;
         __shared__ int8_t qim[QY * QXS];
         __shared__ float lut[256];  // k / 255 (IEEE division), the driver's astype(float32) / 255.
+        // the bilinear source rows / columns of the tile's QY rows and QX columns, once per
+        // workgroup: (weight of the far sample, its complement, near / far offsets)
+        __shared__ float4 rowc[QY], colc[QX];
         lut[t] = (float)t / 255.0f;
+        const float sy = (float)c1.H / (float)H, sx = (float)c1.W / (float)W;
+        if (t < QY) {
+            int ya, yb;
+            const float h1 = sp_src(sy, min(max(y0 + t - 2, 0), H - 1), c1.H, ya, yb);
+            rowc[t] = make_float4(h1, 1.f - h1, __int_as_float(ya * c1.W), __int_as_float(yb * c1.W));
+        } else if (t >= 64 && t < 64 + QX) {
+            int xa, xb;
+            const float w1 = sp_src(sx, min(max(x0 + (t - 64) - 2, 0), W - 1), c1.W, xa, xb);
+            colc[t - 64] = make_float4(w1, 1.f - w1, __int_as_float(xa), __int_as_float(xb));
+        }
         __syncthreads();
         const uint8_t *im = c1.img + (size_t)b * c1.H * c1.W;
-        const float sy = (float)c1.H / (float)H, sx = (float)c1.W / (float)W;
         for (int i = t; i < QY * QX; i += SP_NT) {
             const int r = i / QX, c = i % QX;
             const int gy = y0 + r - 2, gx = x0 + c - 2;
             int v = 0;
             if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
-                int ya, yb, xa, xb;
-                const float h1 = sp_src(sy, gy, c1.H, ya, yb), w1 = sp_src(sx, gx, c1.W, xa, xb);
-                const float h0 = 1.f - h1, w0 = 1.f - w1;
-                const float a00 = lut[im[(size_t)ya * c1.W + xa]], a01 = lut[im[(size_t)ya * c1.W + xb]];
-                const float a10 = lut[im[(size_t)yb * c1.W + xa]], a11 = lut[im[(size_t)yb * c1.W + xb]];
+                const float4 rc = rowc[r], cc = colc[c];
+                const float h1 = rc.x, h0 = rc.y, w1 = cc.x, w0 = cc.y;
+                const int ra = __float_as_int(rc.z), rb = __float_as_int(rc.w);
+                const int xa = __float_as_int(cc.z), xb = __float_as_int(cc.w);
+                const float a00 = lut[im[ra + xa]], a01 = lut[im[ra + xb]];
+                const float a10 = lut[im[rb + xa]], a11 = lut[im[rb + xb]];
                 const float t0 = __builtin_fmaf(a00, w0, a01 * w1);
                 const float t1 = __builtin_fmaf(a10, w0, a11 * w1);
                 const float x = __builtin_fmaf(t0, h0, t1 * h1);
@@ -304,24 +317,25 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
             const int Ho = H / 2, Wo = W / 2;
 #pragma unroll
             for (int jp = 0; jp < 2; jp++) {
+                // both lanes of a column pair hold the pair's 2 x 2 maxima of both channel blocks:
+                // the even lane requantises block 0, the odd lane block 1
+                const int cbx = fr & 1;
+                int m[16];
 #pragma unroll
-                for (int cb = 0; cb < 2; cb++) {
-                    int m[16];
+                for (int q = 0; q < 16; q++) {
+                    int v0 = max(acc[2 * jp][0][q], acc[2 * jp + 1][0][q]);
+                    int v1 = max(acc[2 * jp][1][q], acc[2 * jp + 1][1][q]);
+                    v0 = max(v0, __builtin_amdgcn_update_dpp(0, v0, 0xB1, 0xF, 0xF, false));  // lane ^ 1
+                    v1 = max(v1, __builtin_amdgcn_update_dpp(0, v1, 0xB1, 0xF, 0xF, false));
+                    m[q] = cbx ? v1 : v0;
+                }
 #pragma unroll
-                    for (int q = 0; q < 16; q++) {
-                        const int v = max(acc[2 * jp][cb][q], acc[2 * jp + 1][cb][q]);
-                        m[q] = max(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));  // lane ^ 1 (quad_perm [1,0,3,2])
-                    }
-                    if ((fr & 1) == 0) {
+                for (int qq = 0; qq < 4; qq++) {
+                    int v[4];
 #pragma unroll
-                        for (int qq = 0; qq < 4; qq++) {
-                            int v[4];
-#pragma unroll
-                            for (int e = 0; e < 4; e++) v[e] = requant_bits(m[4 * qq + e], rs, lo);
-                            *reinterpret_cast<int *>(stg + (jp * 16 + fr / 2) * PB + 32 * cb + 8 * qq + 4 * fh) =
-                                pack4b(v[0], v[1], v[2], v[3]);
-                        }
-                    }
+                    for (int e = 0; e < 4; e++) v[e] = requant_bits(m[4 * qq + e], rs, lo);
+                    *reinterpret_cast<int *>(stg + (jp * 16 + fr / 2) * PB + 32 * cbx + 8 * qq + 4 * fh) =
+                        pack4b(v[0], v[1], v[2], v[3]);
                 }
             }
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes done
@@ -366,28 +380,28 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
         const int Ho = H / 2, Wo = W / 2;
 #pragma unroll
         for (int jp = 0; jp < 2; jp++) {
-            const int gy = y0 + 4 * w + 2 * jp, gx = x0 + fr;
+            // the even lane of a column pair requantises channel block 0, the odd lane block 1
+            const int cbx = fr & 1, gy = y0 + 4 * w + 2 * jp, gx = x0 + fr - cbx;
+            int m[16];
 #pragma unroll
-            for (int cb = 0; cb < 2; cb++) {
-                int m[16];
+            for (int q = 0; q < 16; q++) {
+                int v0 = max(acc[2 * jp][0][q], acc[2 * jp + 1][0][q]);
+                int v1 = max(acc[2 * jp][1][q], acc[2 * jp + 1][1][q]);
+                v0 = max(v0, __builtin_amdgcn_update_dpp(0, v0, 0xB1, 0xF, 0xF, false));  // lane ^ 1
+                v1 = max(v1, __builtin_amdgcn_update_dpp(0, v1, 0xB1, 0xF, 0xF, false));
+                m[q] = cbx ? v1 : v0;
+            }
+            if (gy < H && gx < W) {  // both lanes of a regroup pair (same fr) or neither
+                int8_t *dst = out + (((size_t)b * Ho + gy / 2) * Wo + gx / 2) * cstride;
+                int d[4];
 #pragma unroll
-                for (int q = 0; q < 16; q++) {
-                    const int v = max(acc[2 * jp][cb][q], acc[2 * jp + 1][cb][q]);
-                    m[q] = max(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));  // lane ^ 1 (quad_perm [1,0,3,2])
+                for (int qq = 0; qq < 4; qq++) {
+                    int v[4];
+#pragma unroll
+                    for (int e = 0; e < 4; e++) v[e] = requant_bits(m[4 * qq + e], rs, lo);
+                    d[qq] = pack4b(v[0], v[1], v[2], v[3]);
                 }
-                if ((fr & 1) == 0 && gy < H && gx < W) {  // both lanes of a pair (same fr) or neither
-                    int8_t *dst = out + (((size_t)b * Ho + gy / 2) * Wo + gx / 2) * cstride;
-                    int d[4];
-#pragma unroll
-                    for (int qq = 0; qq < 4; qq++) {
-                        int v[4];
-#pragma unroll
-                        for (int e = 0; e < 4; e++) v[e] = requant_bits(m[4 * qq + e], rs, lo);
-                        d[qq] = pack4b(v[0], v[1], v[2], v[3]);
-                    }
-                    *reinterpret_cast<i32x4 *>(dst + 64 * g + 32 * cb + 16 * fh) = regroup16(d);
-                }
-                __builtin_amdgcn_sched_barrier(0);  // one block at a time: the register budget
+                *reinterpret_cast<i32x4 *>(dst + 64 * g + 32 * cbx + 16 * fh) = regroup16(d);
             }
         }
     } else {
