@@ -60,6 +60,12 @@ __device__ __forceinline__ int requant_bits(int a, float rs, int lo_bits) {
     const int bits = __float_as_int(f + SP_MAGIC);
     return max(min(bits, SP_MAGIC_BITS + 127), lo_bits);
 }
+// the same from the exact integer already held as a float (conv1a on the f16 matrix cores)
+__device__ __forceinline__ int requant_bitsf(float a, float rs, int lo_bits) {
+    const float f = a * rs;
+    const int bits = __float_as_int(f + SP_MAGIC);
+    return max(min(bits, SP_MAGIC_BITS + 127), lo_bits);
+}
 // four at once (the packed v_pk_mul_f32 / v_pk_add_f32 form measured 1-3 % slower)
 __device__ __forceinline__ void requant4(int (&v)[4], int a0, int a1, int a2, int a3, float rs, int lo_bits) {
     v[0] = requant_bits(a0, rs, lo_bits);
@@ -184,47 +190,56 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
         // conv1a + relu over the tile + halo on v_mfma_i32_32x32x16_i8: K = the 9 taps (+ 7 zero),
         // A = the weights (lanes < 32: taps 0-7, lanes >= 32: tap 8), B = 32 tile pixels' taps;
         // pixels outside the image are conv1b's zero padding, not conv1a evaluated there
-        long a1[2];
+        // on the f16 matrix cores: int8 taps and weights are exact in f16, every partial sum an
+        // integer below 2^24 (exact in f32), the bias the C input -- the accumulator IS the
+        // integer sum as a float, so the requantisation skips its int -> float conversion
+        typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+        typedef float f32x16 __attribute__((ext_vector_type(16)));
+        h8 a1[2];
+        f32x16 bias[2];
 #pragma unroll
         for (int cb = 0; cb < 2; cb++) {
             const int co = 32 * cb + fr;
             const unsigned lo = (unsigned)(fh ? c1.wpk[3 * co + 2] : c1.wpk[3 * co]);
             const unsigned hi = fh ? 0u : (unsigned)c1.wpk[3 * co + 1];
-            a1[cb] = (long)(((unsigned long long)hi << 32) | lo);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                a1[cb][k] = (_Float16)(float)(((int)(lo << (24 - 8 * k))) >> 24);
+                a1[cb][4 + k] = (_Float16)(float)(((int)(hi << (24 - 8 * k))) >> 24);
+            }
+#pragma unroll
+            for (int q = 0; q < 16; q++) bias[cb][q] = (float)c1.bq[32 * cb + (q & 3) + 8 * (q >> 2) + 4 * fh];
         }
-        int bias[2][16];
-#pragma unroll
-        for (int cb = 0; cb < 2; cb++)
-#pragma unroll
-            for (int q = 0; q < 16; q++) bias[cb][q] = c1.bq[32 * cb + (q & 3) + 8 * (q >> 2) + 4 * fh];
         constexpr int NPX = IY * IX, NBLK = (NPX + 31) / 32;
 #pragma unroll 1
         for (int blk = w; blk < NBLK; blk += SP_NT / 64) {
             const int px = blk * 32 + fr, pxc = min(px, NPX - 1);
             const int r = pxc / IX, x = pxc % IX;
             const int8_t *q0 = qim + r * QXS + x;
-            auto u8 = [](int8_t v) { return (unsigned)(uint8_t)v; };
-            unsigned lo, hi;
-            if (fh == 0) {
-                lo = u8(q0[0]) | (u8(q0[1]) << 8) | (u8(q0[2]) << 16) | (u8(q0[QXS]) << 24);
-                hi = u8(q0[QXS + 1]) | (u8(q0[QXS + 2]) << 8) | (u8(q0[2 * QXS]) << 16) | (u8(q0[2 * QXS + 1]) << 24);
-            } else {
-                lo = u8(q0[2 * QXS + 2]);
-                hi = 0u;
-            }
-            const long bv = (long)(((unsigned long long)hi << 32) | lo);
             const int gy = y0 + r - 1, gx = x0 + x - 1;
             const bool in_img = px < NPX && gy >= 0 && gy < H && gx >= 0 && gx < W;
+            h8 bv;
+            if (fh == 0) {
+                bv[0] = (_Float16)(float)q0[0];
+                bv[1] = (_Float16)(float)q0[1];
+                bv[2] = (_Float16)(float)q0[2];
+                bv[3] = (_Float16)(float)q0[QXS];
+                bv[4] = (_Float16)(float)q0[QXS + 1];
+                bv[5] = (_Float16)(float)q0[QXS + 2];
+                bv[6] = (_Float16)(float)q0[2 * QXS];
+                bv[7] = (_Float16)(float)q0[2 * QXS + 1];
+            } else {
+                bv = h8{};
+                bv[0] = (_Float16)(float)q0[2 * QXS + 2];
+            }
 #pragma unroll
             for (int cb = 0; cb < 2; cb++) {
-                i32x16 c0;
-#pragma unroll
-                for (int q = 0; q < 16; q++) c0[q] = bias[cb][q];
-                const i32x16 d = __builtin_amdgcn_mfma_i32_32x32x16_i8(a1[cb], bv, c0, 0, 0, 0);
+                const f32x16 d = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[cb], bv, bias[cb], 0, 0, 0);
 #pragma unroll
                 for (int qq = 0; qq < 4; qq++) {
                     int v[4];
-                    requant4(v, d[4 * qq], d[4 * qq + 1], d[4 * qq + 2], d[4 * qq + 3], c1.rs, SP_MAGIC_BITS);
+#pragma unroll
+                    for (int e = 0; e < 4; e++) v[e] = requant_bitsf(d[4 * qq + e], c1.rs, SP_MAGIC_BITS);
                     const int ch = 32 * cb + 8 * qq + 4 * fh;
                     if (px < NPX)
                         reinterpret_cast<int *>(tile + chunk_at(px, x, ch >> 4))[(ch & 15) >> 2] =
@@ -265,25 +280,17 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
         rb[u] = u < NS ? wb[u * 64] : i32x4{0, 0, 0, 0};
     }
     // the accumulators start at the layer's quantised bias (row q of channel block cb = channel
-    // 64 g + 32 cb + 8 (q >> 2) + 4 fh + (q & 3)): no add in the epilogue, and the 2 x 2 max pool
-    // commutes with it
-    i32x16 acc[4][2];
-    {
-        i32x16 b0, b1;
+    // 64 g + 32 cb + 8 (q >> 2) + 4 fh + (q & 3)), the C operand of each chain's first MFMA: no
+    // add in the epilogue, and the 2 x 2 max pool commutes with it
+    i32x16 acc[4][2], b0, b1;
 #pragma unroll
-        for (int qq = 0; qq < 4; qq++) {
-            const i32x4 x0 = *reinterpret_cast<const i32x4 *>(bq + 64 * g + 8 * qq + 4 * fh);
-            const i32x4 x1 = *reinterpret_cast<const i32x4 *>(bq + 64 * g + 32 + 8 * qq + 4 * fh);
+    for (int qq = 0; qq < 4; qq++) {
+        const i32x4 x0 = *reinterpret_cast<const i32x4 *>(bq + 64 * g + 8 * qq + 4 * fh);
+        const i32x4 x1 = *reinterpret_cast<const i32x4 *>(bq + 64 * g + 32 + 8 * qq + 4 * fh);
 #pragma unroll
-            for (int e = 0; e < 4; e++) {
-                b0[4 * qq + e] = x0[e];
-                b1[4 * qq + e] = x1[e];
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            acc[j][0] = b0;
-            acc[j][1] = b1;
+        for (int e = 0; e < 4; e++) {
+            b0[4 * qq + e] = x0[e];
+            b1[4 * qq + e] = x1[e];
         }
     }
     // per-lane bases: row 4w + j, column fr, chunk half fh (padded layout); XOR terms per kx
@@ -303,8 +310,8 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
         for (int j = 0; j < 4; j++) {
             const int off = ((j + ky) * IX + kx) * PS;
             const i32x4 bv = PADL ? lb[off + c0] : lb[off + (c0 ^ xs[kx])];
-            acc[j][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bv, acc[j][0], 0, 0, 0);
-            acc[j][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bv, acc[j][1], 0, 0, 0);
+            acc[j][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bv, s == 0 ? b0 : acc[j][0], 0, 0, 0);
+            acc[j][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bv, s == 0 ? b1 : acc[j][1], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
     }
