@@ -187,7 +187,7 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
             qim[r * QXS + c] = (int8_t)v;
         }
         __syncthreads();
-        // conv1a + relu over the tile + halo on v_mfma_i32_32x32x16_i8: K = the 9 taps (+ 7 zero),
+        // conv1a + relu over the tile + halo on v_mfma_f32_32x32x16_f16: K = the 9 taps (+ 7 zero),
         // A = the weights (lanes < 32: taps 0-7, lanes >= 32: tap 8), B = 32 tile pixels' taps;
         // pixels outside the image are conv1b's zero padding, not conv1a evaluated there
         // on the f16 matrix cores: int8 taps and weights are exact in f16, every partial sum an
