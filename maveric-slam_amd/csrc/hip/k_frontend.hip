@@ -964,30 +964,12 @@ __global__ __launch_bounds__(256) void k_window_query(WinArgs a, int blocks_per_
 }
 
 // ---------------------------------------------------------------------------
-// Window match, tiled (as-intended; SURVEY 8(a) a7 with the exact cosine): one block per
-// (pair, band of kBandW frame-1 grid columns).  The band's queries are a contiguous run of
-// the top-N list (patch order), and every window of the band lies in the frame-0 columns
-// [X + sx - r, X + kBandW - 1 + sx + r]: their candidate cells (column masks) are staged into
-// LDS once, kChunk rows per pass (16-B chunks XOR-swizzled by row, |c|^2 and (x, y) beside
-// them).  Each wave owns 16 queries (A = 16 rows x 256 int8, 16 VGPRs, straight from HBM)
-// and sweeps every staged candidate with v_mfma_i32_16x16x64_i8 -- exact int32 dots, four
-// MFMAs per 16x16 tile; a tile element counts only when the candidate lies in the query's
-// window.  The pass test (100 dot^2 > 81 |c|^2 |q|^2) and the best (dot^2/|c|^2 compared
-// exactly, ties -> lower patch = earlier in the window scan) are integer; passing elements
-// are rare, so the exact update sits behind a branch the wave almost always skips.
-// A and B fragments use the same lane -> k map (lane l: bytes 64 s + 16 (l >> 4) .. +15 of
-// k-step s), so the dot is exact whatever k order the instruction uses; C/D: lane l holds
-// column l & 15, rows 4 (l >> 4) + j (cdna_hip_programming.md, gfx950 C/D map).
+// Window-match constants and the per-tile fold shared by the as-intended kernel below.  The
+// (pair, band of kBandW grid columns) eligibility test is kept from the band-tiled kernel this
+// replaced (measured slower and removed; in history).
 // ---------------------------------------------------------------------------
-#ifndef WIN_BAND_W
-#define WIN_BAND_W 5
-#endif
-#ifndef WIN_CHUNK
-#define WIN_CHUNK 144
-#endif
-constexpr int kBandW = WIN_BAND_W;
-constexpr int kChunk = WIN_CHUNK;  // candidate rows staged per pass (multiple of 16)
-constexpr int kBandList = 960;     // band candidate-list capacity (host checks (kBandW + 2r) * rows)
+constexpr int kBandW = 5;
+constexpr int kBandList = 960;  // candidate-list capacity the eligibility test checks ((kBandW + 2r) * rows)
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
@@ -1017,202 +999,13 @@ __device__ __forceinline__ void window_fold(const i32x4_t &acc, bool cv, int cx,
     }
 }
 
-constexpr int kBandQ = 1024;  // top-N patches cached in LDS per block (more: read from global)
-
-__global__ __launch_bounds__(256) void k_window_tile(WinArgs a, int bands, int nblocks,
-                                                     const unsigned long long *__restrict__ masks,
-                                                     const int8_t *__restrict__ desc0,
-                                                     const int8_t *__restrict__ desc1,
-                                                     const int *__restrict__ num_sel,
-                                                     const int *__restrict__ patches1,
-                                                     QueryResult *__restrict__ out) {
-    __shared__ __attribute__((aligned(16))) int8_t cand_s[kChunk * kDescD];
-    __shared__ unsigned short list_s[kBandList];  // candidates, scan order, packed x * 64 + y
-    __shared__ unsigned short pp_s[kBandQ];  // the pair's top-N patches (host: cells <= 65536)
-    __shared__ int misc_s[4];
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    // XCD-aware remap (gridDim.x is a multiple of 8): each XCD runs whole pairs
-    const int b = blockIdx.x, per_xcd = gridDim.x >> 3;
-    const int logical = (b & 7) * per_xcd + (b >> 3);
-    if (logical >= nblocks) return;  // block-uniform
-    const int pair = logical / bands, band = logical % bands;
-    const int R = a.rows, X = band * kBandW;
-    const long cells = (long)R * a.cols;
-    const int nsel = num_sel[pair];
-    const int *pp = patches1 + (long)pair * a.N;
-
-    // 1. (together) the window columns' masks and the top-N patches: the band's query run
-    //    [qa, qb) (patches ascend) and its scan-ordered candidate list
-    const int cx0 = max(X + a.shift_x - a.radius, 0);
-    const int cx1 = min(X + kBandW - 1 + a.shift_x + a.radius, a.cols - 1);
-    unsigned long long bits = 0;
-    if (w == 0 && lane <= cx1 - cx0) bits = masks[(long)pair * a.cols + cx0 + lane];
-    const int key0 = X * R, key1 = min(X + kBandW, a.cols) * R;
-    int c0 = 0, c1 = 0;
-    for (int q0 = 0; q0 < nsel; q0 += 1024) {  // four independent loads per thread per pass
-        int pv[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int q = q0 + 256 * u + t;
-            pv[u] = q < nsel ? pp[q] : 0x7fffffff;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int q = q0 + 256 * u + t;
-            if (q < kBandQ && q < nsel) pp_s[q] = pv[u];
-            c0 += pv[u] < key0;
-            c1 += pv[u] < key1;
-        }
-    }
-    c0 = wave_sum(c0);
-    c1 = wave_sum(c1);
-    if (t == 0) misc_s[0] = misc_s[1] = 0;
-    if (w == 0) {
-        const int cnt = __popcll(bits);
-        int incl = cnt;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += y;
-        }
-        if (lane == 63) misc_s[2] = incl;
-        int pos = incl - cnt;
-        const int xy = (cx0 + lane) << 6;
-        while (bits) {
-            const int yb = __ffsll((long long)bits) - 1;
-            bits &= bits - 1;
-            list_s[pos++] = xy | yb;
-        }
-    }
-    __syncthreads();
-    if (lane == 0) {
-        atomicAdd(&misc_s[0], c0);
-        atomicAdd(&misc_s[1], c1);
-    }
-    __syncthreads();
-    const int qa = misc_s[0], nq = misc_s[1] - misc_s[0], ncand = misc_s[2];
-    if (nq <= 0) return;  // block-uniform; no barrier follows for anyone
-
-    const int8_t *d0 = desc0 + pair * cells * kDescD;
-    const int8_t *d1 = desc1 + pair * cells * kDescD;
-    const int n_mt = (nq + 15) >> 4, rounds = (n_mt + 3) >> 2;
-    const int n_chunks = (ncand + kChunk - 1) / kChunk;
-    const int h = lane >> 4, col = lane & 15;
-    const int r = a.radius;
-    const int wu = __builtin_amdgcn_readfirstlane(w);
-    for (int rd = 0; rd < rounds; rd++) {
-        const int mt = rd * 4 + w;
-        const bool active = mt < n_mt;
-        int bd[4], bn[4], bk[4], rn2[4], rcx[4], rcy[4];
-        i32x4_t A[4];
-        for (int ch = 0; ch < n_chunks; ch++) {
-            const int cbase = ch * kChunk, crows = min(kChunk, ncand - cbase);
-            if (rd == 0 || n_chunks > 1) {  // (one chunk: staged once for every round)
-                if (rd > 0 || ch > 0) __syncthreads();  // the previous chunk is consumed
-                // LDS DMA: wave w fills rows 4 i + (lane >> 4), i = w, w + 4, ...; lane l
-                // fetches 16-B chunk (l & 15) ^ (row & 15) into position l & 15 (swizzle)
-                for (int i = wu; i < (crows + 3) / 4; i += 4) {
-                    const int row = 4 * i + h;
-                    const int xy = list_s[cbase + min(row, crows - 1)];
-                    const int8_t *src =
-                        d0 + ((long)(xy >> 6) * R + (xy & 63)) * kDescD + ((col ^ (row & 15)) << 4);
-                    __builtin_amdgcn_global_load_lds(src, cand_s + i * 4 * kDescD, 16, 0, 0);
-                }
-            }
-            if (ch == 0) {  // this round's queries (A: row mt*16 + col, bytes 64 s + 16 h .. +15)
-                const int rowq = mt * 16 + col;
-                const bool rv = active && rowq < nq;
-                const int qp = rv ? (qa + rowq < kBandQ ? pp_s[qa + rowq] : pp[qa + rowq]) : 0;
-                const i32x4_t *qrow = reinterpret_cast<const i32x4_t *>(d1 + (long)qp * kDescD + 16 * h);
-#pragma unroll
-                for (int s2 = 0; s2 < 4; s2++) A[s2] = rv ? qrow[4 * s2] : i32x4_t{0, 0, 0, 0};
-                int n2 = 0;
-#pragma unroll
-                for (int s2 = 0; s2 < 4; s2++)
-#pragma unroll
-                    for (int u = 0; u < 4; u++) n2 = __builtin_amdgcn_sdot4(A[s2][u], A[s2][u], n2, false);
-                n2 += __shfl_xor(n2, 16, 64);
-                n2 += __shfl_xor(n2, 32, 64);
-                // window centre of row `col`; rows past nq get a centre no candidate is near
-                const int qcx = rv ? qp / R + a.shift_x : -(1 << 20), qcy = rv ? qp % R + a.shift_y : -(1 << 20);
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    rn2[j] = __shfl(n2, 4 * h + j, 64);
-                    rcx[j] = __shfl(qcx, 4 * h + j, 64);
-                    rcy[j] = __shfl(qcy, 4 * h + j, 64);
-                    bd[j] = 0;
-                    bn[j] = 1;
-                    bk[j] = -1;
-                }
-            }
-            if (rd == 0 || n_chunks > 1) {
-                __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed
-                __syncthreads();                // ... and every other wave's
-            }
-            if (!active) continue;
-            const int ntiles = (crows + 15) >> 4;
-            for (int nt = 0; nt < ntiles; nt++) {
-                const int cr = nt * 16 + col;  // this lane's candidate (C/D column)
-                const int8_t *brow = cand_s + cr * kDescD;
-                i32x4_t acc = {0, 0, 0, 0};
-                int cna = 0;
-#pragma unroll
-                for (int s2 = 0; s2 < 4; s2++) {
-                    const i32x4_t bf = *reinterpret_cast<const i32x4_t *>(brow + (((4 * s2 + h) ^ (cr & 15)) << 4));
-                    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[s2], bf, acc, 0, 0, 0);
-#pragma unroll
-                    for (int u = 0; u < 4; u++) cna = __builtin_amdgcn_sdot4(bf[u], bf[u], cna, false);
-                }
-                cna += __shfl_xor(cna, 16, 64);
-                cna += __shfl_xor(cna, 32, 64);
-                const bool cv = cr < crows;
-                const int cxy = cv ? list_s[cbase + cr] : (1 << 24);
-                const int cx = cxy >> 6, cy = cxy & 63;
-                const int cp = cx * R + cy;
-                window_fold(acc, cv, cx, cy, cp, cna, r, rcx, rcy, rn2, bd, bn, bk);
-            }
-        }
-        if (!active) continue;
-        // best of each row over its 16 columns (lanes 16 h .. 16 h + 15)
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) {
-                const int od = __shfl_xor(bd[j], o, 64), on = __shfl_xor(bn[j], o, 64), ok = __shfl_xor(bk[j], o, 64);
-                if (better_i32(od, on, ok, bd[j], bn[j], bk[j])) {
-                    bd[j] = od;
-                    bn[j] = on;
-                    bk[j] = ok;
-                }
-            }
-        }
-        if (col == 0) {
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int qi = mt * 16 + 4 * h + j;
-                if (qi >= nq) continue;
-                QueryResult res = {0, 0, 0, -1, 0.0f};
-                if (bk[j] >= 0) {
-                    res.found = 1;
-                    res.best_patch = bk[j];
-                    res.bx = bk[j] / R;
-                    res.by = bk[j] % R;
-                    res.score = (float)((double)bd[j] * (double)bd[j] / ((double)bn[j] * (double)rn2[j]));
-                }
-                out[(long)pair * a.N + qa + qi] = res;
-            }
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------
 // Window match, per-wave MFMA (as-intended; the default): one wave owns 16 consecutive
 // top-N queries of a pair -- patch order, so they span a few grid columns -- and sweeps the
 // candidates of the union of their windows' columns (column masks -> scan-ordered list in the
 // wave's LDS slice) with v_mfma_i32_16x16x64_i8, B fragments gathered straight from L2/HBM one
 // 16-candidate tile ahead.  No block barrier and no shared staging: latency is hidden by
-// occupancy (waves are independent), the band-tiled kernel above being the shared-staging
-// alternative (WIN_TILED=1).  Epilogue as in k_window_tile.
+// occupancy (waves are independent).
 // ---------------------------------------------------------------------------
 constexpr int kWQ = 16;            // queries per wave
 
@@ -1482,26 +1275,13 @@ extern "C" int mv_window_match_batch_dev(mv_context *ctx, const mv_window_params
         MV_LAUNCH_CHECK();
         const bool tiled = !a.as_built && kBandW + 2 * p->radius <= 64 && cells <= 65536 && cols <= 1024 &&
                            (long)(kBandW + 2 * p->radius) * rows <= kBandList;
-#ifndef WIN_TILED
-#define WIN_TILED 0
-#endif
-        if (tiled && !WIN_TILED) {
+        if (tiled) {
             const int bpp = (N + 4 * kWQ - 1) / (4 * kWQ);
             const long nblk = (long)bpp * batch;
             MV_REQUIRE(nblk < (1l << 30));
             const unsigned g = (unsigned)((nblk + 7) / 8 * 8);
             MV_PROF_BEGIN(ctx->stream, "k_window_eval");
             hipLaunchKernelGGL(k_window_wave, dim3(g), dim3(256), 0, ctx->stream, a, bpp, (int)nblk, masks, desc0,
-                               desc1, num_selected, patches1, qr);
-            MV_PROF_END(ctx->stream);
-            MV_LAUNCH_CHECK();
-        } else if (tiled) {
-            const int bands = (cols + kBandW - 1) / kBandW;
-            const long nblk = (long)bands * batch;
-            MV_REQUIRE(nblk < (1l << 30));
-            const unsigned g = (unsigned)((nblk + 7) / 8 * 8);
-            MV_PROF_BEGIN(ctx->stream, "k_window_eval");
-            hipLaunchKernelGGL(k_window_tile, dim3(g), dim3(256), 0, ctx->stream, a, bands, (int)nblk, masks, desc0,
                                desc1, num_selected, patches1, qr);
             MV_PROF_END(ctx->stream);
             MV_LAUNCH_CHECK();
