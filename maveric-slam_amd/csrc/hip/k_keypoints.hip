@@ -31,13 +31,6 @@
 namespace {
 
 constexpr int NMS_T = 1024;  // threads of the per-frame block
-#ifndef KP_NCHW
-#define KP_NCHW 0  // 1: sample the corners from NCHW directly (measured 2.09 ms vs 0.81 + 0.24 ms
-                   // transposed, per 256 KITTI frames: 64 channel planes per gather)
-#endif
-#ifndef KP_EXP
-#define KP_EXP 0  // timing experiments only (wrong results): 1 no descriptor stores, 2 no plane copy, 3 no keypoint phase, 4 geometry stubbed
-#endif
 #ifndef KP_TRACE
 #define KP_TRACE 0  // printf k_kp_nms's per-phase clock64() deltas for frame 0 (timing only)
 #endif
@@ -71,7 +64,7 @@ struct KpScratch {
 };
 
 size_t a256(size_t x) { return mv::align_up(x, 256); }
-bool kp_planes_path(int Hc, int Wc) { return (long)Hc * Wc <= KP_PLANE_CELLS && !KP_TRANSPOSE && !KP_NCHW; }
+bool kp_planes_path(int Hc, int Wc) { return (long)Hc * Wc <= KP_PLANE_CELLS && !KP_TRANSPOSE; }
 
 size_t kp_scratch_bytes(int B, int Hc, int Wc, int cap) {
     const size_t P = (size_t)Hc * Wc * 64;
@@ -605,9 +598,9 @@ __global__ __launch_bounds__(256) void k_kp_nhwc(int HW, const float *__restrict
     }
 }
 
-// NCHW = true: the corners are gathered straight from the network's [256][Hc][Wc] layout (4
-// scattered floats per channel, L2-served) instead of the transposed rows
-template <bool NCHW>
+// one wave per keypoint on the transposed (NHWC) rows: 4 corners x 256 channels, 16 B per lane
+// (gathering the corners straight from the NCHW planes measured 2.09 ms against 0.81 + 0.24 ms
+// transposed per 256 KITTI frames: 64 channel planes per gather)
 __global__ __launch_bounds__(256) void k_kp_sample(int B, int cap, int Hc, int Wc, int H, int W, int Wh,
                                                    const int *__restrict__ num_kp, const int *__restrict__ slot_pix,
                                                    const float *__restrict__ nhwc, float *__restrict__ desc) {
@@ -622,17 +615,11 @@ __global__ __launch_bounds__(256) void k_kp_sample(int B, int cap, int Hc, int W
     float w[4];
     kp_geometry(slot_pix[q], Hc, Wc, H, W, Wh, x0, y0, w);
     const float wnw = w[0], wne = w[1], wsw = w[2], wse = w[3];
-    const float *D = nhwc + (long)b * Hc * Wc * 256 + (NCHW ? 4l * lane * Hc * Wc : 4 * lane);
+    const float *D = nhwc + (long)b * Hc * Wc * 256 + 4 * lane;
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    const long plane = (long)Hc * Wc;
     auto at = [&](int yy, int xx) {
         if (!(xx >= 0 && xx < Wc && yy >= 0 && yy < Hc)) return z;
-        if constexpr (NCHW) {
-            const float *q = D + (long)yy * Wc + xx;
-            return make_float4(q[0], q[plane], q[2 * plane], q[3 * plane]);
-        } else {
-            return *reinterpret_cast<const float4 *>(D + ((long)yy * Wc + xx) * 256);
-        }
+        return *reinterpret_cast<const float4 *>(D + ((long)yy * Wc + xx) * 256);
     };
     const float4 v = kp_bilinear4(at(y0, x0), at(y0, x0 + 1), at(y0 + 1, x0), at(y0 + 1, x0 + 1), wnw, wne, wsw, wse);
     kp_normalize_store(v, sq[wv], nrm[wv], lane, desc + q * 256);
@@ -677,13 +664,7 @@ __global__ __launch_bounds__(256) void k_kp_sample_planes(int B, int cap, int Hc
         gpix[u] = slot_pix[(long)b * cap + min((int)threadIdx.x + 256 * u, nk - 1)];
 #pragma unroll
     for (int u = 0; u < KPF; u++) {
-        if (KP_EXP == 4) {  // timing only: the geometry stubbed
-            gx0[u] = (gpix[u] % Wh) >> 3;
-            gy0[u] = (gpix[u] / Wh) >> 3;
-            gw[u][0] = gw[u][1] = gw[u][2] = gw[u][3] = 0.25f;
-        } else {
-            kp_geometry(gpix[u], Hc, Wc, H, W, Wh, gx0[u], gy0[u], gw[u]);
-        }
+        kp_geometry(gpix[u], Hc, Wc, H, W, Wh, gx0[u], gy0[u], gw[u]);
     }
     const float *I = coarse + ((long)b * 256 + c0) * HW;  // 4-B aligned
     // I[h] is the first 16-B aligned float; I[f] goes to plf[f + o] with h + o in {0, 4}, so
@@ -696,7 +677,7 @@ __global__ __launch_bounds__(256) void k_kp_sample_planes(int B, int cap, int Hc
     // 16 loads in flight per thread to the end: past n4 the index is clamped, so a lane
     // re-copies float4 n4 - 1 onto itself -- branch-free, or the compiler sinks each load
     // into its store's branch and serialises them
-    for (int j = KP_EXP == 2 ? n4 : threadIdx.x; j < n4; j += 16 * 256) {
+    for (int j = threadIdx.x; j < n4; j += 16 * 256) {
         float4 t[16];
 #pragma unroll
         for (int u = 0; u < 16; u++) t[u] = G4[min(j + u * 256, n4 - 1)];
@@ -706,7 +687,6 @@ __global__ __launch_bounds__(256) void k_kp_sample_planes(int B, int cap, int Hc
     if (threadIdx.x < h) plf[threadIdx.x + o] = I[threadIdx.x];
     if (threadIdx.x < tail) plf[h + 4 * n4 + o + threadIdx.x] = I[h + 4 * n4 + threadIdx.x];
     __syncthreads();
-    if (KP_EXP == 3) return;
     const float *L = plf + o;  // plane c of the group: L + c HW
     auto at = [&](int yy, int xx) {
         KpCh<CH> r;
@@ -727,7 +707,6 @@ __global__ __launch_bounds__(256) void k_kp_sample_planes(int B, int cap, int Hc
             v.v[j] = fmaf(dd.v[j], w[3], r);
         }
         float *out = desc + ((long)b * cap + slot) * 256 + c0;
-        if (KP_EXP == 1 && v.v[0] != 1234.5f) return;
         if constexpr (CH == 4)
             *reinterpret_cast<float4 *>(out) = make_float4(v.v[0], v.v[1], v.v[2], v.v[3]);
         else
@@ -809,16 +788,14 @@ extern "C" int mv_keypoints_dev(mv_context *ctx, const mv_kp_params *p, int batc
         MV_LAUNCH_CHECK();
         return mv::set_status(MV_OK);
     }
-    if (!KP_NCHW) {
-        MV_PROF_BEGIN(s, "k_kp_nhwc");
-        hipLaunchKernelGGL(k_kp_nhwc, dim3((unsigned)((HW + 63) / 64), 4, (unsigned)batch), dim3(256), 0, s, HW,
-                           coarse_desc, m.nhwc);
-        MV_PROF_END(s);
-        MV_LAUNCH_CHECK();
-    }
+    MV_PROF_BEGIN(s, "k_kp_nhwc");
+    hipLaunchKernelGGL(k_kp_nhwc, dim3((unsigned)((HW + 63) / 64), 4, (unsigned)batch), dim3(256), 0, s, HW,
+                       coarse_desc, m.nhwc);
+    MV_PROF_END(s);
+    MV_LAUNCH_CHECK();
     MV_PROF_BEGIN(s, "k_kp_sample");
-    hipLaunchKernelGGL(k_kp_sample<KP_NCHW != 0>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, batch, cap, Hc,
-                       Wc, H, W, Wc * 8, num_kp, m.slot_pix, KP_NCHW ? coarse_desc : m.nhwc, desc);
+    hipLaunchKernelGGL(k_kp_sample, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, batch, cap, Hc,
+                       Wc, H, W, Wc * 8, num_kp, m.slot_pix, m.nhwc, desc);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     return mv::set_status(MV_OK);
