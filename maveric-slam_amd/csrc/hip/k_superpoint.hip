@@ -271,6 +271,11 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
     }
     __syncthreads();
 
+    // a wave whose 4 rows all lie below the frame (the 24-row layers' second tile row: a quarter
+    // of their waves) has nothing to compute; the 128-channel epilogue has no block barrier
+    if constexpr (CIN != 64) {
+        if (y0 + 4 * w >= H) return;
+    }
     // ---- K loop: 9 taps (or 1) x CIN / 32 steps, fully unrolled: every LDS offset a constant ----
     const i32x4 *wa = wf + (size_t)(2 * g) * NS * 64 + lane, *wb = wa + NS * 64;
     i32x4 ra[PF], rb[PF];
