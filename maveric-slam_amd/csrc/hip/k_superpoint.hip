@@ -166,17 +166,33 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
         }
         __syncthreads();
         const uint8_t *im = c1.img + (size_t)b * c1.H * c1.W;
-        for (int i = t; i < QY * QX; i += SP_NT) {
+        // every pixel's four source bytes loaded before any is used (all gathers of the thread in
+        // flight at once; out-of-frame pixels read a clamped in-frame byte and store 0)
+        constexpr int NQ = (QY * QX + SP_NT - 1) / SP_NT;
+        uint8_t src4[NQ][4];
+#pragma unroll
+        for (int u = 0; u < NQ; u++) {
+            const int i = min(t + u * SP_NT, QY * QX - 1), r = i / QX, c = i % QX;
+            const float4 rc = rowc[r], cc = colc[c];
+            const int ra = __float_as_int(rc.z), rb = __float_as_int(rc.w);
+            const int xa = __float_as_int(cc.z), xb = __float_as_int(cc.w);
+            src4[u][0] = im[ra + xa];
+            src4[u][1] = im[ra + xb];
+            src4[u][2] = im[rb + xa];
+            src4[u][3] = im[rb + xb];
+        }
+#pragma unroll
+        for (int u = 0; u < NQ; u++) {
+            const int i = t + u * SP_NT;
+            if (i >= QY * QX) break;
             const int r = i / QX, c = i % QX;
             const int gy = y0 + r - 2, gx = x0 + c - 2;
             int v = 0;
             if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
                 const float4 rc = rowc[r], cc = colc[c];
                 const float h1 = rc.x, h0 = rc.y, w1 = cc.x, w0 = cc.y;
-                const int ra = __float_as_int(rc.z), rb = __float_as_int(rc.w);
-                const int xa = __float_as_int(cc.z), xb = __float_as_int(cc.w);
-                const float a00 = lut[im[ra + xa]], a01 = lut[im[ra + xb]];
-                const float a10 = lut[im[rb + xa]], a11 = lut[im[rb + xb]];
+                const float a00 = lut[src4[u][0]], a01 = lut[src4[u][1]];
+                const float a10 = lut[src4[u][2]], a11 = lut[src4[u][3]];
                 const float t0 = __builtin_fmaf(a00, w0, a01 * w1);
                 const float t1 = __builtin_fmaf(a10, w0, a11 * w1);
                 const float x = __builtin_fmaf(t0, h0, t1 * h1);
