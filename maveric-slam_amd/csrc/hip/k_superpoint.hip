@@ -142,6 +142,28 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
     const int g = bid % ngroups, b = bid / ngroups;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, fr = lane & 31, fh = lane >> 5;
     const int y0 = ty * TY, x0 = tx * TX;
+    // the first weight fragments and the bias, issued before the input tile is built so that
+    // their latency hides under it.  The accumulators start at the layer's quantised bias (row q
+    // of channel block cb = channel 64 g + 32 cb + 8 (q >> 2) + 4 fh + (q & 3)), the C operand of
+    // each chain's first MFMA: no add in the epilogue, and the 2 x 2 max pool commutes with it
+    const i32x4 *wa = wf + (size_t)(2 * g) * NS * 64 + lane, *wb = wa + NS * 64;
+    i32x4 ra[PF], rb[PF];
+#pragma unroll
+    for (int u = 0; u < PF; u++) {
+        ra[u] = u < NS ? wa[u * 64] : i32x4{0, 0, 0, 0};
+        rb[u] = u < NS ? wb[u * 64] : i32x4{0, 0, 0, 0};
+    }
+    i32x16 b0, b1;
+#pragma unroll
+    for (int qq = 0; qq < 4; qq++) {
+        const i32x4 u0 = *reinterpret_cast<const i32x4 *>(bq + 64 * g + 8 * qq + 4 * fh);
+        const i32x4 u1 = *reinterpret_cast<const i32x4 *>(bq + 64 * g + 32 + 8 * qq + 4 * fh);
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            b0[4 * qq + e] = u0[e];
+            b1[4 * qq + e] = u1[e];
+        }
+    }
     auto chunk_at = [&](int px, int x, int c) { return px * PS + (PADL ? c : (c ^ ((x / SWS) & (NCH - 1)))); };
 
     constexpr int NCHUNK = IY * IX * NCH;
@@ -293,27 +315,7 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
         if (y0 + 4 * w >= H) return;
     }
     // ---- K loop: 9 taps (or 1) x CIN / 32 steps, fully unrolled: every LDS offset a constant ----
-    const i32x4 *wa = wf + (size_t)(2 * g) * NS * 64 + lane, *wb = wa + NS * 64;
-    i32x4 ra[PF], rb[PF];
-#pragma unroll
-    for (int u = 0; u < PF; u++) {
-        ra[u] = u < NS ? wa[u * 64] : i32x4{0, 0, 0, 0};
-        rb[u] = u < NS ? wb[u * 64] : i32x4{0, 0, 0, 0};
-    }
-    // the accumulators start at the layer's quantised bias (row q of channel block cb = channel
-    // 64 g + 32 cb + 8 (q >> 2) + 4 fh + (q & 3)), the C operand of each chain's first MFMA: no
-    // add in the epilogue, and the 2 x 2 max pool commutes with it
-    i32x16 acc[4][2], b0, b1;
-#pragma unroll
-    for (int qq = 0; qq < 4; qq++) {
-        const i32x4 x0 = *reinterpret_cast<const i32x4 *>(bq + 64 * g + 8 * qq + 4 * fh);
-        const i32x4 x1 = *reinterpret_cast<const i32x4 *>(bq + 64 * g + 32 + 8 * qq + 4 * fh);
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-            b0[4 * qq + e] = x0[e];
-            b1[4 * qq + e] = x1[e];
-        }
-    }
+    i32x16 acc[4][2];
     // per-lane bases: row 4w + j, column fr, chunk half fh (padded layout); XOR terms per kx
     const i32x4 *lb = tile + ((4 * w) * IX + fr) * PS + (PADL ? fh : 0);
     int xs[KS];
