@@ -288,10 +288,11 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
     }
     // ---- the input tile (zero outside the image), 8 16-B loads in flight per thread ----
     const int8_t *src = in + (size_t)b * H * W * CIN;
-    for (int i0 = 0; i0 < (FUSE1A ? 0 : NCHUNK); i0 += 8 * SP_NT) {
-        i32x4 v[8];
+    constexpr int LIF = 8;  // 16-B loads in flight per thread (12 / 16 measured the same)
+    for (int i0 = 0; i0 < (FUSE1A ? 0 : NCHUNK); i0 += LIF * SP_NT) {
+        i32x4 v[LIF];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
+        for (int u = 0; u < LIF; u++) {
             const int i = i0 + u * SP_NT + t;
             const int c = i % NCH, px = i / NCH, x = px % IX, r = px / IX;
             const int gy = y0 + r - P, gx = x0 + x - P;
@@ -300,7 +301,7 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
                 v[u] = *reinterpret_cast<const i32x4 *>(src + ((size_t)gy * W + gx) * CIN + c * 16);
         }
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
+        for (int u = 0; u < LIF; u++) {
             const int i = i0 + u * SP_NT + t;
             if (i >= NCHUNK) continue;
             const int c = i % NCH, px = i / NCH, x = px % IX;
