@@ -498,6 +498,22 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv1x1(const int8_t *__restric
     const int g = bid % ngroups, b = bid / ngroups;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, fr = lane & 31, fh = lane >> 5;
     const int y0 = ty * H1_TY, x0 = tx * TX;
+    // the first weight fragments and the bias (each chain's first C operand) before the tile
+    const i32x4 *wa = wf + (size_t)(H1_CB * g) * NS * 64 + lane;
+    i32x4 aq[3][H1_CB];
+#pragma unroll
+    for (int s = 0; s < 2; s++)
+#pragma unroll
+        for (int cb = 0; cb < H1_CB; cb++) aq[s][cb] = wa[(cb * NS + s) * 64];
+    i32x16 bvs[H1_CB];
+#pragma unroll
+    for (int cb = 0; cb < H1_CB; cb++)
+#pragma unroll
+        for (int qq = 0; qq < 4; qq++) {
+            const i32x4 x = *reinterpret_cast<const i32x4 *>(bq + 32 * (H1_CB * g + cb) + 8 * qq + 4 * fh);
+#pragma unroll
+            for (int e = 0; e < 4; e++) bvs[cb][4 * qq + e] = x[e];
+        }
     {  // the tile: 16 chunks per thread, every load issued before the first store
         i32x4 v[NCHUNK / SP_NT];
 #pragma unroll
@@ -513,25 +529,7 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv1x1(const int8_t *__restric
         }
     }
     __syncthreads();
-    const i32x4 *wa = wf + (size_t)(H1_CB * g) * NS * 64 + lane;
-    i32x4 aq[3][H1_CB];
-#pragma unroll
-    for (int s = 0; s < 2; s++)
-#pragma unroll
-        for (int cb = 0; cb < H1_CB; cb++) aq[s][cb] = wa[(cb * NS + s) * 64];
     i32x16 acc[2][H1_CB];  // from the quantised bias, as in k_sp_conv
-#pragma unroll
-    for (int cb = 0; cb < H1_CB; cb++) {
-        i32x16 bv;
-#pragma unroll
-        for (int qq = 0; qq < 4; qq++) {
-            const i32x4 x = *reinterpret_cast<const i32x4 *>(bq + 32 * (H1_CB * g + cb) + 8 * qq + 4 * fh);
-#pragma unroll
-            for (int e = 0; e < 4; e++) bv[4 * qq + e] = x[e];
-        }
-        acc[0][cb] = bv;
-        acc[1][cb] = bv;
-    }
     const i32x4 *lb = tile + ((2 * w) * TX + fr) * H1_PS + fh;
 #pragma unroll
     for (int s = 0; s < NS; s++) {
@@ -544,11 +542,45 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv1x1(const int8_t *__restric
             const i32x4 bv = lb[j * TX * H1_PS + 2 * s];
 #pragma unroll
             for (int cb = 0; cb < H1_CB; cb++)
-                acc[j][cb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aq[s % 3][cb], bv, acc[j][cb], 0, 0, 0);
+                acc[j][cb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aq[s % 3][cb], bv, s == 0 ? bvs[cb] : acc[j][cb], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
     }
     const int lo = SP_MAGIC_BITS - 128;  // the heads have no relu
+    if (OMODE == 1 && cstride % 16 != 0) {
+        // the semi head (65 channels, Frame layout: a cell's 65 B, a tile column's 8 cells
+        // consecutive): the outputs go through LDS in that order, then leave as whole column runs
+        // of 8 x 65 B with consecutive lanes on consecutive bytes (the direct form stored single
+        // bytes 65 B apart: one partial line per lane per store)
+        __syncthreads();  // every wave past its last read of the input tile
+        int8_t *stg = reinterpret_cast<int8_t *>(tile);
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            int8_t *cell = stg + (fr * H1_TY + 2 * w + j) * cstride;
+#pragma unroll
+            for (int cb = 0; cb < H1_CB; cb++)
+#pragma unroll
+                for (int qq = 0; qq < 4; qq++) {
+                    const int co = 32 * (H1_CB * g + cb) + 8 * qq + 4 * fh;
+                    if (co >= cstride) continue;
+                    int v[4];
+                    requant4(v, acc[j][cb][4 * qq], acc[j][cb][4 * qq + 1], acc[j][cb][4 * qq + 2], acc[j][cb][4 * qq + 3], rs, lo);
+#pragma unroll
+                    for (int e = 0; e < 4; e++)
+                        if (co + e < cstride) cell[co + e] = (int8_t)v[e];
+                }
+        }
+        __syncthreads();
+        const int run = H1_TY * cstride, nb = min(H1_TY, H - y0) * cstride;  // a column's bytes, inside
+        for (int col = w; col < TX; col += SP_NT / 64) {  // a wave per column, lanes on bytes
+            const int gx = x0 + col;
+            if (gx >= W) break;
+            int8_t *gd = out + ((size_t)b * H * W + (size_t)gx * H + y0) * cstride;
+            const int8_t *ls = stg + col * run;
+            for (int o = lane; o < nb; o += 64) gd[o] = ls[o];
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < 2; j++) {
         const int gy = y0 + 2 * w + j, gx = x0 + fr;
@@ -800,6 +832,7 @@ int launch_conv1x1(hipStream_t st, const mv_superpoint *net, int li, int B, int 
     const int tiles_x = (W + TX - 1) / TX, tiles_y = (H + H1_TY - 1) / H1_TY;
     const int ngroups = (net->cout_pad[li] + 32 * H1_CB - 1) / (32 * H1_CB);
     MV_REQUIRE(net->cout_pad[li] % (32 * H1_CB) == 0);  // whole 128-channel groups (65 -> 128, 256)
+    MV_REQUIRE(!(OMODE == 1 && cstride % 16 != 0) || (long)TX * H1_TY * cstride <= (long)H1_TY * TX * H1_PS * 16);
     const long blocks = (long)B * ngroups * tiles_y * tiles_x;
     MV_REQUIRE(blocks < (1l << 31));
     const char *wd = static_cast<const char *>(net->wdev);
