@@ -163,30 +163,6 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
     const int *nb = nb_v + (size_t)pair * cap;
     const int ntc = (n1 + M_BN - 1) / M_BN;
 
-    // ---- A: the wave's 2 x 32 rows (w*64 + 32 g + fr) x 256 int8 in 64 VGPRs (i8 MFMA A
-    //      operand: lane l holds row l & 31, k = 32 s + 16 (l >> 5) .. +15 at k32 step s);
-    //      |a|^2 along the way ----
-    const int fr = lane & 31, fh = lane >> 5;
-    i32x4 aI[M_RG][KD / 32];
-    int na_r[M_RG];  // |a|^2 of row w*64 + 32 g + fr
-#pragma unroll
-    for (int g = 0; g < M_RG; g++) {
-        const int8_t *arow = A + (size_t)min(row0 + w * 64 + g * 32 + fr, n0 - 1) * KD + fh * 16;
-#pragma unroll
-        for (int s2 = 0; s2 < KD / 32; s2++) aI[g][s2] = *reinterpret_cast<const i32x4 *>(arow + s2 * 32);
-    }
-#pragma unroll
-    for (int g = 0; g < M_RG; g++) {
-        int q = 0;
-#pragma unroll
-        for (int s2 = 0; s2 < KD / 32; s2++)
-#pragma unroll
-            for (int u = 0; u < 4; u++) q = __builtin_amdgcn_sdot4(aI[g][s2][u], aI[g][s2][u], q, false);
-        q += __shfl_xor(q, 32, 64);
-        if (fh == 0) na_s[w * 64 + g * 32 + fr] = q;
-        na_r[g] = q;
-    }
-
     // ---- B DMA: wave w fills rows w*RPW .. +RPW-1 of a tile, 4 rows (1 KiB) per instruction;
     //      lane l -> row (l >> 4), chunk position l & 15, source chunk (l & 15) ^ (row & 15) ----
     const int wu = __builtin_amdgcn_readfirstlane(w);
@@ -215,6 +191,38 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
             oB[g_] = (unsigned)min(nb_ + 4 * g_, n1 - 1) * KD + (dcb ^ (64u * g_));          \
         oR = (unsigned)min((TC) * M_BN + lane, n1 - 1) * 4;                                  \
     } while (0)
+    // prologue: tiles 0, 1, 2 issued before the A rows are read, so that both latencies overlap
+    for (int g = 0; g < M_NBUF - 1 && g < ntc; g++) {
+        I8_OFFSETS(g);
+        if (g == 0) I8_STAGE(0);
+        if (g == 1) I8_STAGE(1);
+        if (g == 2) I8_STAGE(2);
+    }
+
+    // ---- A: the wave's 2 x 32 rows (w*64 + 32 g + fr) x 256 int8 in 64 VGPRs (i8 MFMA A
+    //      operand: lane l holds row l & 31, k = 32 s + 16 (l >> 5) .. +15 at k32 step s);
+    //      |a|^2 along the way ----
+    const int fr = lane & 31, fh = lane >> 5;
+    i32x4 aI[M_RG][KD / 32];
+    int na_r[M_RG];  // |a|^2 of row w*64 + 32 g + fr
+#pragma unroll
+    for (int g = 0; g < M_RG; g++) {
+        const int8_t *arow = A + (size_t)min(row0 + w * 64 + g * 32 + fr, n0 - 1) * KD + fh * 16;
+#pragma unroll
+        for (int s2 = 0; s2 < KD / 32; s2++) aI[g][s2] = *reinterpret_cast<const i32x4 *>(arow + s2 * 32);
+    }
+#pragma unroll
+    for (int g = 0; g < M_RG; g++) {
+        int q = 0;
+#pragma unroll
+        for (int s2 = 0; s2 < KD / 32; s2++)
+#pragma unroll
+            for (int u = 0; u < 4; u++) q = __builtin_amdgcn_sdot4(aI[g][s2][u], aI[g][s2][u], q, false);
+        q += __shfl_xor(q, 32, 64);
+        if (fh == 0) na_s[w * 64 + g * 32 + fr] = q;
+        na_r[g] = q;
+    }
+
     // B fragment: column block c (0, 1), lane row 32 c + fr, k32 step s: chunk (2 s + fh)
     const int rdb = fr * KD;
     const int xsw = fh ^ (fr & 15);  // chunk (2 s + fh) ^ (fr & 15) = 2 s ^ xsw
@@ -316,14 +324,7 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
         __syncthreads();                                                      \
     } while (0)
 
-    // prologue: tiles 0, 1, 2
-    for (int g = 0; g < M_NBUF - 1 && g < ntc; g++) {
-        I8_OFFSETS(g);
-        if (g == 0) I8_STAGE(0);
-        if (g == 1) I8_STAGE(1);
-        if (g == 2) I8_STAGE(2);
-    }
-    wait_vm_i8<0>();
+    wait_vm_i8<0>();  // the prologue's tiles (issued before the A rows) and the A rows
     __syncthreads();
     for (int T = 0; T < ntc; T += 4) {
         I8_SLOT(0);
