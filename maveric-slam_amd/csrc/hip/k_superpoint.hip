@@ -273,16 +273,18 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
 #pragma unroll
             for (int cb = 0; cb < 2; cb++) {
                 const f32x16 d = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[cb], bv, bias[cb], 0, 0, 0);
+                int dw[4];
 #pragma unroll
                 for (int qq = 0; qq < 4; qq++) {
                     int v[4];
 #pragma unroll
                     for (int e = 0; e < 4; e++) v[e] = requant_bitsf(d[4 * qq + e], c1.rs, SP_MAGIC_BITS);
-                    const int ch = 32 * cb + 8 * qq + 4 * fh;
-                    if (px < NPX)
-                        reinterpret_cast<int *>(tile + chunk_at(px, x, ch >> 4))[(ch & 15) >> 2] =
-                            in_img ? pack4b(v[0], v[1], v[2], v[3]) : 0;
+                    dw[qq] = pack4b(v[0], v[1], v[2], v[3]);
                 }
+                // the lane pair's 32 channels regrouped: this lane's chunk 2 cb + fh, one 16-B store
+                // (4-B stores at the 80-B pixel stride hit 4-way bank conflicts)
+                const i32x4 chunk = regroup16(dw);
+                if (px < NPX) tile[chunk_at(px, x, 2 * cb + fh)] = in_img ? chunk : i32x4{0, 0, 0, 0};
             }
         }
     }
@@ -366,13 +368,15 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
                     v1 = max(v1, __builtin_amdgcn_update_dpp(0, v1, 0xB1, 0xF, 0xF, false));
                     m[q] = cbx ? v1 : v0;
                 }
+                int dw[4];
 #pragma unroll
                 for (int qq = 0; qq < 4; qq++) {
                     int v[4];
                     requant4(v, m[4 * qq], m[4 * qq + 1], m[4 * qq + 2], m[4 * qq + 3], rs, lo);
-                    *reinterpret_cast<int *>(stg + (jp * 16 + fr / 2) * PB + 32 * cbx + 8 * qq + 4 * fh) =
-                        pack4b(v[0], v[1], v[2], v[3]);
+                    dw[qq] = pack4b(v[0], v[1], v[2], v[3]);
                 }
+                // 16-B stores (4-B ones at the 80-B pixel stride: 4-way bank conflicts)
+                *reinterpret_cast<i32x4 *>(stg + (jp * 16 + fr / 2) * PB + 32 * cbx + 16 * fh) = regroup16(dw);
             }
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes done
             __builtin_amdgcn_wave_barrier();
@@ -388,14 +392,16 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
 #pragma unroll
             for (int j = 0; j < 4; j++)
 #pragma unroll
-                for (int cb = 0; cb < 2; cb++)
+                for (int cb = 0; cb < 2; cb++) {
+                    int dw[4];
 #pragma unroll
                     for (int qq = 0; qq < 4; qq++) {
                         int v[4];
                         requant4(v, acc[j][cb][4 * qq], acc[j][cb][4 * qq + 1], acc[j][cb][4 * qq + 2], acc[j][cb][4 * qq + 3], rs, lo);
-                        *reinterpret_cast<int *>(stg + (j * 32 + fr) * PB + 32 * cb + 8 * qq + 4 * fh) =
-                            pack4b(v[0], v[1], v[2], v[3]);
+                        dw[qq] = pack4b(v[0], v[1], v[2], v[3]);
                     }
+                    *reinterpret_cast<i32x4 *>(stg + (j * 32 + fr) * PB + 32 * cb + 16 * fh) = regroup16(dw);
+                }
             __builtin_amdgcn_s_waitcnt(0xc07f);
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
