@@ -107,6 +107,43 @@ def ref_window():
     return _ref_window
 
 
+REF_NMS_SO = os.path.join(HERE, "_ref", "libmv_ref_nms.so")
+_ref_nms = None
+
+
+def ref_nms_available():
+    return os.path.exists(REF_NMS_SO)
+
+
+def ref_run_nms(semi, semi_scale, rows=192, cols=640, feature_rows=24, feature_cols=80):
+    """The reference's own cell-level NMS: the body of src/run_nms.c's main (:44-174) with its
+    grid helpers (:29-41), extracted from its text and compiled by oracle/Makefile with
+    src/top_N.c (compute_softmax reached without a prototype, as in the reference binary: F7).
+    Its grid is fixed at 24 x 80 cells (:62-63, 1920-entry arrays).  Returns (suppressions
+    [(x, y, x', y')], survivors [(x, y)]) parsed from main's printf lines.  Build container only."""
+    global _ref_nms
+    if _ref_nms is None:
+        R = ctypes.CDLL(REF_NMS_SO)
+        R.ref_run_nms.restype = _I
+        R.ref_run_nms.argtypes = [_I, _I, _I, _I, _F, _P, _F, _P, ctypes.c_char_p, _I]
+        _ref_nms = R
+    semi = np.ascontiguousarray(semi, dtype=np.int8)
+    assert semi.shape == (1920, 65)
+    desc = np.zeros((1920, 256), np.int8)  # main never reads the descriptors
+    buf = ctypes.create_string_buffer(1 << 20)
+    n = _ref_nms.ref_run_nms(rows, cols, feature_rows, feature_cols, float(semi_scale), _ptr(semi), 1.0, _ptr(desc),
+                             buf, len(buf))
+    assert n >= 0, "output buffer too small"
+    sup, kp = [], []
+    for line in buf.value.decode().splitlines():
+        if "suppressing" in line:
+            a, b = line.split(" suppressing ")
+            sup.append(tuple(int(v) for v in a.strip("()").split()) + tuple(int(v) for v in b.strip("()").split()))
+        else:
+            kp.append(tuple(int(v) for v in line.split()))
+    return sup, kp
+
+
 def ref_available():
     return os.path.exists(REF_SO)
 

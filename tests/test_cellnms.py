@@ -1,8 +1,9 @@
 """The int8 path's cell-level NMS (src/run_nms.c:65-155).
 
 run_nms.c is a standalone main that includes quantized_pair0.h, which the reference does not
-ship: it cannot be built here, so the oracle is a literal restatement (parity
-unpinned beyond its own hand-checked cases below).  GPU (marked): the wavefront kernel equals
+ship: it cannot be built whole, so the oracle is a restatement, pinned to the body of
+that main cut out of the reference text and compiled by oracle/Makefile
+(tests/test_oracle_pinning.py::test_run_nms_pinned), plus the hand-checked cases below.  GPU (marked): the wavefront kernel equals
 the sequential oracle bit for bit on the committed quantized frame (both softmax scales),
 random frames, and the full-resolution 47 x 155 grid."""
 import numpy as np

@@ -268,3 +268,35 @@ def test_squared_dist_pinned(orc):
     # threshold edges of the score test
     for d in (np.float32(0.81), np.nextafter(np.float32(0.81), np.float32(1)), np.nextafter(np.float32(0.81), np.float32(0))):
         assert R.ref_window_pass(float(d)) == L.orc_window_pass(float(d))
+
+
+@pytest.mark.skipif("not __import__('oracle').ref_nms_available()", reason="oracle/_ref not built here")
+def test_run_nms_pinned(orc):
+    """The oracle's cell-level NMS (orc_run_nms) against the reference's OWN run_nms.c main
+    (:44-174, extracted from its text at build time with its grid helpers, compute_softmax from
+    top_N.c reached without a prototype as in the reference binary, F7): the same survivors in
+    the same order, and as many suppressions as the oracle removes cells.  Frames: the committed
+    quantized_image0 and random 24 x 80 ones; semi scales chosen so that the as-built effective
+    scale (the low 32 bits of the promoted double) is 0, 2^-63, 2, 2^65 and -2."""
+    import synth
+
+    g = load_golden("quantized_image0.npz")
+    rng = np.random.default_rng(29)
+    frames = [g["semi"]] + [synth.synth_semi(rng, 1920, p_key=p) for p in (0.3, 0.5, 0.7, 0.9)]
+    scales = [float(g["semi_scale"])]
+    for low in (1, 2, 3, 6):  # float mantissa low bits -> effective 2^-63, 2, 2^65, -2
+        scales.append(float((np.array([0.35], np.float32).view(np.uint32) & ~np.uint32(7) | np.uint32(low))
+                            .view(np.float32)[0]))
+    checked = nonempty = 0
+    for semi in frames:
+        for s in scales:
+            sup, kp_ref = orc.ref_run_nms(semi, s)
+            eff = orc.scale_as_built(s)
+            _, mi, pr = orc.compute_softmax(eff, semi)
+            before = int((mi != 64).sum())
+            m2, _, kp = orc.run_nms(24, 80, mi, pr)
+            assert [tuple(int(v) for v in p) for p in kp] == kp_ref, (s, eff)
+            assert len(sup) == before - kp.shape[0], (s, eff)
+            checked += 1
+            nonempty += int(len(sup) > 0)
+    assert checked == len(frames) * len(scales) and nonempty >= len(frames)  # suppressions exercised
