@@ -39,6 +39,8 @@ struct mv_superpoint {
     float dq_semi, dq_desc;  // the heads' dequantisation scales (float) out_scale
     void *act;            // activation ping-pong buffers
     size_t act_bytes;
+    hipEvent_t done;      // recorded after each forward on its stream: the buffers' last use
+    bool used;
 };
 
 namespace {
@@ -942,6 +944,12 @@ extern "C" int mv_superpoint_create(mv_context *ctx, const mv_sp_weights *wt, mv
         mv::set_error(MV_ERR_HIP, "hipMemcpy of the SuperPoint weights: %s", hipGetErrorString(e));
         return MV_ERR_HIP;
     }
+    if (hipEventCreateWithFlags(&net->done, hipEventDisableTiming) != hipSuccess) {
+        (void)hipFree(net->wdev);
+        delete net;
+        mv::set_error(MV_ERR_HIP, "hipEventCreate for the SuperPoint net");
+        return MV_ERR_HIP;
+    }
     *out = net;
     return MV_OK;
 }
@@ -949,7 +957,8 @@ extern "C" int mv_superpoint_create(mv_context *ctx, const mv_sp_weights *wt, mv
 extern "C" int mv_superpoint_destroy(mv_superpoint *net) {
     if (!net) return MV_OK;
     (void)hipSetDevice(net->device);
-    (void)hipDeviceSynchronize();  // the net's buffers may be in use on any stream it was run on
+    if (net->used) (void)hipEventSynchronize(net->done);  // the last forward, on whatever stream it ran
+    if (net->done) (void)hipEventDestroy(net->done);
     if (net->act) (void)hipFree(net->act);
     if (net->wdev) (void)hipFree(net->wdev);
     delete net;
@@ -969,9 +978,8 @@ extern "C" int mv_superpoint_forward_dev(mv_context *ctx, mv_superpoint *net, in
     const size_t b_bytes = a_bytes;
     const size_t need = a_bytes + b_bytes + (size_t)batch * 2 * SP_MG_CHUNKS * 8 * sizeof(unsigned);  // + presence masks
     if (net->act_bytes < need) {
-        if (net->act) {
-            const int q = mv::quiesce(ctx);
-            if (q != MV_OK) return q;
+        if (net->act) {  // the previous forward (any context, any stream) may still read them
+            if (net->used) MV_HIP_TRY(hipEventSynchronize(net->done));
             MV_HIP_TRY(hipFree(net->act));
             net->act = nullptr;
             net->act_bytes = 0;
@@ -1015,5 +1023,7 @@ extern "C" int mv_superpoint_forward_dev(mv_context *ctx, mv_superpoint *net, in
                        (long)h * w, net->dq_semi, net->dq_desc, pres, semi_scale, desc_scale);
     MV_LAUNCH_CHECK();
     MV_PROF_END(st);
+    MV_HIP_TRY(hipEventRecord(net->done, st));
+    net->used = true;
     return MV_OK;
 }

@@ -285,7 +285,11 @@ __device__ __forceinline__ void epilogue(char *epi, const float2 *rowv, float (&
     char *mt = epi + w * 32 * MT_STRIDE;
     int *clist = reinterpret_cast<int *>(epi + NW * 32 * MT_STRIDE);
     unsigned *lmask = reinterpret_cast<unsigned *>(epi + NW * 32 * MT_STRIDE + NW * 64 * NCAND * 4);
+    static_assert(RG == 2, "the deferred re-scores put group g on lane half g");
     unsigned wide_rows[RG];
+    float bs_g[RG];
+    int bj_g[RG], need_g[RG];  // need_g: the maximiser's column when its exact score is deferred, else -1
+    bool out_g[RG];            // this lane writes the row (fh == 0, live, not wide)
 #pragma unroll
     for (int g = 0; g < RG; g++) {
 #pragma unroll
@@ -329,7 +333,7 @@ __device__ __forceinline__ void epilogue(char *epi, const float2 *rowv, float (&
         const bool full = flagged || rv.y < 0.f;
         const float *arow = A + (size_t)(row0 + rl) * KD;
         float bs = dmode ? __builtin_inff() : -__builtin_inff();
-        int bj = 0x7fffffff;
+        int bj = 0x7fffffff, need = -1;
         bool wide = live && full;
         if (wide && fh == 0) lmask[rl] = 0xffffffffu;
         if (live && !full) {
@@ -355,17 +359,16 @@ __device__ __forceinline__ void epilogue(char *epi, const float2 *rowv, float (&
                     if (I >= n1) {  // a padding column on top (IK: all real dots below 0); never read past n1
                         wide = true;
                         if (fh == 0) lmask[rl] = 0xffffffffu;
-                    } else if (fh == 0) {
+                    } else {
                         // decision-only (no score output): every exact score inside the window
                         // clears both tests -- the maximiser's exact dot decides nothing
                         const bool sure = !oscore && (dmode || Ms - dp > fmax(thresh, 0.0));
-                        if (sure) {
+                        if (!sure) {
+                            need = I;  // scored below, after both groups, by lane half g
+                        } else if (fh == 0) {
                             bs = dmode ? 0.f : FLT_MAX;
-                        } else {
-                            const float e = exact_dot(arow, B + (size_t)I * KD);
-                            bs = dmode ? dist(e) : e;
+                            bj = I;
                         }
-                        bj = I;
                     }
                 } else {  // both lanes of the row take this branch
                     const double lim = lo / sa_k;  // in screen units
@@ -412,13 +415,43 @@ __device__ __forceinline__ void epilogue(char *epi, const float2 *rowv, float (&
                 bj = oj;
             }
         }
-        if (fh == 0 && live && !wide) {
+        bs_g[g] = bs;
+        bj_g[g] = bj;
+        need_g[g] = need;
+        out_g[g] = fh == 0 && live && !wide;
+        wide_rows[g] = (unsigned)__ballot(fh == 0 && wide);
+    }
+
+    // ---- the maximisers' exact scores: lane (fr, fh) takes row fr of group fh, so the two
+    //      groups' sequential 256-term dots (and their row loads) run side by side instead of one
+    //      after the other on half the lanes ----
+    {
+        const int Ih = fh ? need_g[1] : need_g[0];
+        float e = 0.f;
+        if (Ih >= 0) {
+            const float *ap = A + (size_t)(row0 + w * 64 + fh * 32 + fr) * KD;
+            e = exact_dot(ap, B + (size_t)Ih * KD);
+        }
+        const float eo = __shfl_xor(e, 32, 64);
+        const float e0 = fh ? eo : e, e1 = fh ? e : eo;
+#pragma unroll
+        for (int g = 0; g < RG; g++)
+            if (need_g[g] >= 0) {
+                const float eg = g ? e1 : e0;
+                bs_g[g] = dmode ? dist(eg) : eg;
+                bj_g[g] = need_g[g];
+            }
+    }
+#pragma unroll
+    for (int g = 0; g < RG; g++)
+        if (out_g[g]) {
+            const int rl = w * 64 + g * 32 + fr;
+            const float bs = bs_g[g];
+            const int bj = bj_g[g];
             const bool keep = bj != 0x7fffffff && (dmode || ((double)bs > thresh && bs > 0.f));
             oidx[rl] = keep ? bj : -1;
             if (oscore) oscore[rl] = keep ? bs : 0.f;
         }
-        wide_rows[g] = (unsigned)__ballot(fh == 0 && wide);
-    }
 
     // ---- wide rows (rare): the wave scores every column of every listed lane exactly, one
     //      column per lane at a time (lane l: columns f + 32 (l + 64 i) of inside lane f) ----
