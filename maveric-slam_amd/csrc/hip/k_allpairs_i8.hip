@@ -29,22 +29,43 @@ __device__ __forceinline__ int xcd_remap(int b, int total) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
+// |b|^2 of 4 rows per 16-lane row group: each load instruction reads 4 whole 256-B rows (1 KiB
+// contiguous per wave), 4 rows in flight per thread, the 16 partial sums reduced by ds_swizzle
+constexpr int NRM_U = 4;  // rows per thread
+__device__ __forceinline__ int swz_xor_i8(int v, int m) {
+    switch (m) {
+        case 1: return __builtin_amdgcn_ds_swizzle(v, (1 << 10) | 0x1F);
+        case 2: return __builtin_amdgcn_ds_swizzle(v, (2 << 10) | 0x1F);
+        case 4: return __builtin_amdgcn_ds_swizzle(v, (4 << 10) | 0x1F);
+        default: return __builtin_amdgcn_ds_swizzle(v, (8 << 10) | 0x1F);
+    }
+}
 __global__ __launch_bounds__(256) void k_i8_norms(long rows, const int8_t *__restrict__ d, int *__restrict__ nrm,
                                                   float *__restrict__ rnrm) {
-    const long r = (long)blockIdx.x * 256 + threadIdx.x;
-    if (r >= rows) return;
-    const int4 *p = reinterpret_cast<const int4 *>(d + r * KD);
-    int s = 0;
+    const int t = threadIdx.x, sub = t & 15;
+    const long base = (long)blockIdx.x * (16 * NRM_U) + (t >> 4);
+    int4 x[NRM_U];
 #pragma unroll
-    for (int v = 0; v < 16; v++) {
-        int4 x = p[v];
-        s = __builtin_amdgcn_sdot4(x.x, x.x, s, false);
-        s = __builtin_amdgcn_sdot4(x.y, x.y, s, false);
-        s = __builtin_amdgcn_sdot4(x.z, x.z, s, false);
-        s = __builtin_amdgcn_sdot4(x.w, x.w, s, false);
+    for (int u = 0; u < NRM_U; u++) {
+        const long r = min(base + 16 * u, rows - 1);
+        x[u] = reinterpret_cast<const int4 *>(d + r * KD)[sub];
     }
-    nrm[r] = s;
-    if (rnrm) rnrm[r] = s > 0 ? 1.0f / sqrtf((float)s) : 0.f;
+#pragma unroll
+    for (int u = 0; u < NRM_U; u++) {
+        int s = __builtin_amdgcn_sdot4(x[u].x, x[u].x, 0, false);
+        s = __builtin_amdgcn_sdot4(x[u].y, x[u].y, s, false);
+        s = __builtin_amdgcn_sdot4(x[u].z, x[u].z, s, false);
+        s = __builtin_amdgcn_sdot4(x[u].w, x[u].w, s, false);
+        s += swz_xor_i8(s, 1);
+        s += swz_xor_i8(s, 2);
+        s += swz_xor_i8(s, 4);
+        s += swz_xor_i8(s, 8);
+        const long r = base + 16 * u;
+        if (sub == 0 && r < rows) {
+            nrm[r] = s;
+            if (rnrm) rnrm[r] = s > 0 ? 1.0f / sqrtf((float)s) : 0.f;
+        }
+    }
 }
 
 // candidate (dot, nb, j) strictly better than current best?  max dot^2/nb, ties -> lower j
@@ -526,7 +547,8 @@ int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const i
     const size_t rows = (size_t)batch * cap;
     int *nb = (int *)scratch;
     float *rnb = (float *)((char *)scratch + align_up(4 * rows, 256));
-    const int nblk = (int)((rows + 255) / 256);
+    MV_REQUIRE((rows + 16 * NRM_U - 1) / (16 * NRM_U) < (1l << 31));
+    const int nblk = (int)((rows + 16 * NRM_U - 1) / (16 * NRM_U));
     MV_PROF_BEGIN(s, "k_i8_norms");
     hipLaunchKernelGGL(k_i8_norms, dim3(nblk), dim3(256), 0, s, (long)rows, desc1, nb, rnb);
     MV_PROF_END(s);
