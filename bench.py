@@ -213,6 +213,60 @@ def gen_batch(torch, dev, B, n, seed, noise=0.3 / 16.0):
     return d0.contiguous(), d1, torch.from_numpy(kp0).to(dev), torch.from_numpy(kp1).to(dev)
 
 
+def pose_angles(T, Tg):
+    """per pair: the rotation angle of R Rg^T and the angle between the translation directions
+    (degrees; atan2 of sine and cosine, as tests/test_gpu_kitti_e2e.py)"""
+    R, t = T[:, :, :3].astype(np.float64), T[:, :, 3].astype(np.float64)
+    Rg, tg = Tg[:, :3], Tg[:, 3]
+    M = R @ Rg.T
+    s = np.linalg.norm(np.stack([M[:, 2, 1] - M[:, 1, 2], M[:, 0, 2] - M[:, 2, 0], M[:, 1, 0] - M[:, 0, 1]], 1), axis=1)
+    rot = np.degrees(np.arctan2(s / 2, (np.trace(M, axis1=1, axis2=2) - 1) / 2))
+    tra = np.degrees(np.arctan2(np.linalg.norm(np.cross(t, tg), axis=1), t @ tg))
+    return rot, tra
+
+
+def noisy_pose_line(torch, dev, cx, stream, pose_p, d0, d1, kp0, kp1, nn_, idx, T, nm, ni, st, fused, kmatch,
+                    steps, sync, barrier):
+    """The headline step with the pose on realistic keypoints: frame 1's keypoints moved by 0.5 px
+    Gaussian noise and 20 % of them replaced by uniform pixels (outlier correspondences), so the
+    RANSAC sees contamination and the Gauss-Newton iterates (the headline's exact projections let
+    it exit early).  Reports the rate, the pose kernel's time and the pose accuracy vs the truth."""
+    import mvtrack
+    import synth
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234)
+    B, n = kp1.shape[0], kp1.shape[1]
+    k1 = kp1 + 0.5 * torch.randn(kp1.shape, generator=g, device=dev)
+    out_m = torch.rand((B, n), generator=g, device=dev) < 0.2
+    rnd = torch.rand((B, n, 2), generator=g, device=dev) * torch.tensor([synth.KITTI_W, synth.KITTI_H], device=dev)
+    k1 = torch.where(out_m[:, :, None], rnd, k1).contiguous()
+    cx.set_stream(torch.cuda.current_stream())
+
+    def np_step():
+        if fused:
+            cx.match_allpairs_f32_run_prepare(d0, d1, nn_, nn_, idx, None, d1, nn_, 0.8)
+        else:
+            cx.match_allpairs_f32(d0, d1, nn_, nn_, idx, None, 0.8)
+        cx.pose_from_matches(pose_p, nn_, idx, kp0, k1, T, nm, ni, st)
+
+    cx.match_allpairs_f32_prepare(d1, nn_)
+    el = timed_loop(np_step, steps, 2, sync, barrier)
+    mvtrack.profile_enable(True)
+    timed_loop(np_step, steps, 0, sync, barrier)
+    mvtrack.profile_enable(False)
+    k_ms, k_n = mvtrack.profile_query(kmatch)
+    p_ms, p_n = mvtrack.profile_query("k_pose_ransac")
+    rot, tra = pose_angles(T.double().cpu().numpy(), synth.T_785_786)
+    cx.set_stream(stream)
+    return {"value": round(B * steps / el, 2), "unit": "pairs/s", "ms_per_step": round(el / steps * 1e3, 4),
+            "keypoints": "frame 1: +0.5 px Gaussian noise, 20% replaced by uniform pixels (outliers)",
+            "stages_ms": {kmatch: round(k_ms / max(k_n, 1), 4), "k_pose_ransac": round(p_ms / max(p_n, 1), 4)},
+            "pose_ok": int((st == 0).sum().item()), "inliers_per_pair": round(float(ni.sum().item()) / B, 1),
+            "rot_err_deg": {"median": round(float(np.median(rot)), 4), "p99": round(float(np.percentile(rot, 99)), 4)},
+            "tdir_err_deg": {"median": round(float(np.median(tra)), 4), "p99": round(float(np.percentile(tra, 99)), 4)}}
+
+
 def algorithmic_bytes_per_pair(n):
     """both fp32 frames read once (2 x n x 256 x 4 B) + idx and score per query
     row (n x 8 B) = 2,105,344 B for a 1024^2 pair -- the figure every roofline here divides by."""
@@ -667,6 +721,10 @@ def main():
             "hbm_frac_8d": round(algorithmic_bytes_per_pair(n) * B / kn_s / 1e9 / HBM_PEAK_GBS, 4),
             "matches_per_pair": round(float(nmatches[0].sum().item()) / B, 1), "checked_pairs": 1}
         cx.set_stream(streams[0])
+    if rank == 0 and world == 1 and args.extra_steps > 0:
+        out["noisy_pose"] = noisy_pose_line(torch, dev, ctxs[0], streams[0], pose_p, d0, d1, kp0, kp1, nn_,
+                                            idxs[0], Ts[0], nmatches[0], ninls[0], statuses[0], fused, kmatch,
+                                            args.extra_steps, sync, barrier)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, n)
         out["cpu_c0"] = cpu_c0(min(args.cpu_seconds, 8.0))

@@ -23,6 +23,13 @@ def main():
     K = synth.KITTI_K
     for B in [int(x) for x in os.environ.get("POSE_BATCHES", "256").split(",")]:
         d0, d1, kp0, kp1 = bench.gen_batch(torch, dev, B, n, seed=1)
+        if os.environ.get("POSE_NOISE"):  # bench.py's noisy_pose keypoints: 0.5 px noise, 20 % outliers
+            g = torch.Generator(device=dev)
+            g.manual_seed(1234)
+            k1 = kp1 + 0.5 * torch.randn(kp1.shape, generator=g, device=dev)
+            om = torch.rand((B, n), generator=g, device=dev) < 0.2
+            rnd = torch.rand((B, n, 2), generator=g, device=dev) * torch.tensor([synth.KITTI_W, synth.KITTI_H], device=dev)
+            kp1 = torch.where(om[:, :, None], rnd, k1).contiguous()
         nn_ = torch.full((B,), n, dtype=torch.int32, device=dev)
         idx = torch.empty((B, n), dtype=torch.int32, device=dev)
         score = torch.empty((B, n), dtype=torch.float32, device=dev)
@@ -30,8 +37,8 @@ def main():
         nm, ni, st = (torch.empty(B, dtype=torch.int32, device=dev) for _ in range(3))
         ctx.reserve(B, n)
         ctx.match_allpairs_f32(d0, d1, nn_, nn_, idx, score, 0.8)
-        for hyp in (64, 128, 256, 512):
-            for it in (0, 3, 10):
+        for hyp in [int(x) for x in os.environ.get("POSE_HYPS", "64,128,256,512").split(",")]:
+            for it in [int(x) for x in os.environ.get("POSE_ITERS", "0,3,10").split(",")]:
                 p = mvtrack.pose_params(mvtrack.AS_INTENDED, fx=K[0, 0], fy=K[1, 1], cx=K[0, 2], cy=K[1, 2],
                                         hypotheses=hyp, inlier_thresh=1.0, refine_iters=it, seed=7)
                 for _ in range(2):
