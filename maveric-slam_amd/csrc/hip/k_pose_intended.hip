@@ -876,9 +876,11 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
                 float dmax = 0.f;
 #pragma unroll
                 for (int i = 0; i < 5; i++) dmax = fmaxf(dmax, fabsf(d[i]));
-                // converged: a step below the float residual's resolution (1e-6 rad / unit-t,
-                // 100x under the 1e-4 tolerance) and a scale that moved < 0.1 %
-                const bool done = dmax < 1e-6f && fabsf(cs_new - csc) <= 1e-3f * csc;
+                // converged: a step below 1e-4 rad / unit-t (Gauss-Newton converges quadratically
+                // on exact data: the error left after such a step is ~1e-8) and a scale that moved
+                // < 2 % (noisy data: the pose then moves far below its noise floor); 1e-6 / 0.1 %
+                // measured the same on exact data and 9 % slower under 0.5 px noise
+                const bool done = dmax < 1e-4f && fabsf(cs_new - csc) <= 2e-2f * csc;
                 // lane k < 14 stores word k of the state (static register indexing):
                 // R (9), t (3), scale, flags (bit 0: failed -- keep the old state; bit 1: converged)
                 if (lane < 14) {
