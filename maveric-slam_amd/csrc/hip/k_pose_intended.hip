@@ -29,6 +29,8 @@
 // Output T = [R | t] with x1 ~ R x0 + t, |t| = 1 (the OpenCV recoverPose convention).
 #include <math.h>
 
+#include <type_traits>
+
 #include "mv_internal.hpp"
 
 // This kernel is the as-INTENDED pose, checked against ground truth within a tolerance,
@@ -609,6 +611,7 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
     //         direction where the fit from the true pose is within 0.5; two starts: <= 1.6). ----
     __shared__ float s_E[2][9];
     __shared__ int s_nh;  // starts found (0, 1, 2)
+    __shared__ bool s_exact;
     if (t == 0) {
         int b0 = -1, b1 = -1;
         float c0 = 0.f, c1 = 0.f;
@@ -626,6 +629,13 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
             }
         }
         s_nh = b0 < 0 ? 0 : (b1 < 0 ? 1 : 2);
+        // the best survivor's inliers fit (almost) exactly: sum of inlier r^2 = its MSAC cost
+        // minus thr^2 per outlier, below 1e-3 thr^2 per inlier (exact projections: ~1e-12;
+        // 0.5 px noise: ~0.2) -- the first start will likely be an exact fit
+        if (b0 >= 0) {
+            const float na0 = s_red2[0][NS + b0] + s_red2[1][NS + b0] + s_red2[2][NS + b0] + s_red2[3][NS + b0];
+            s_exact = c0 - ((float)n - na0) * a.thr2 <= 1e-3f * na0 * a.thr2;
+        }
         if (b0 >= 0)
             for (int r = 0; r < 9; r++) {
                 s_E[0][r] = s_sE[b0][r];
@@ -642,45 +652,60 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
         }
         return;
     }
-    // ---- 4-6, per start (a block-uniform loop): decomposition + cheirality, robust
-    //      Gauss-Newton, the robust cost of the refined pose.  The second start is refined only
-    //      when the first did not reach an exact fit (its Cauchy scale still above the floor:
-    //      noisy data) -- exact data costs one refinement, as a single start did. ----
-    __shared__ float s_cand[4][12];
-    __shared__ float s_uv[2][3][3];
+    // ---- 4-6, per start: decomposition + cheirality, robust Gauss-Newton, the robust cost of
+    //      the refined pose.  Two schedules over groups of waves, block-uniform:
+    //      - sequential (one group = the block): the starts one after the other, the second only
+    //        when the first did not reach an exact fit -- exact data costs one refinement;
+    //      - concurrent (two groups = the block's halves, waves 0-1 and 2-3): when two starts
+    //        exist and the best survivor's inliers are not an exact fit (noisy data, where both
+    //        starts are refined anyway), each half refines one start, so the two Gauss-Newton
+    //        chains share their barriers instead of running back to back.
+    //      Every barrier is block-wide: a group that has converged keeps arriving at them. ----
+    __shared__ float s_cand[2][4][12];
+    __shared__ float s_uv[2][2][3][3];
     __shared__ int s_votes[4][4];  // [wave][candidate]
     __shared__ float s_red[2][4][22];
-    __shared__ float s_state[2][16];
+    __shared__ float s_state[2][2][16];  // [iteration parity][group]
     __shared__ float s_fin[4];
     __shared__ int s_fin_n[4];
-    static_assert(MAXP <= 32 * NT, "the inlier mask holds 32 correspondences per thread");
+    static_assert(MAXP <= 32 * (NT / 2), "the inlier mask holds 32 correspondences per thread of a half");
     const float th_max = sqrtf(a.thr2), th_min = 0.01f * th_max, r_cap = 3.f * th_max;
     float bR[9], bT[3], bcost = __builtin_inff();
     int bn = 0;
     const long long tk3 = PE_TRACE ? clock64() : 0;
     long long tk4 = 0, tk5 = 0;
-    for (int sti = 0; sti < s_nh; sti++) {
+    // the schedule as a compile-time parameter: each gets its own code (constant strides)
+    auto refine = [&](auto par_c) {
+    constexpr bool par = decltype(par_c)::value;
+    constexpr int G = par ? NT / 2 : NT;       // threads per group
+    const int gid = par ? (w >> 1) : 0;        // this thread's group
+    const int gt = par ? (t & (NT / 2 - 1)) : t;
+    const int gw0 = par ? 2 * gid : 0;         // the group's first wave
+    constexpr int gnw = par ? 2 : 4;           // its waves
+    const int rounds = par ? 1 : s_nh;
+    for (int rd = 0; rd < rounds; rd++) {
+        const int sti = par ? gid : rd;
         float E[9];
         for (int r = 0; r < 9; r++) E[r] = s_E[sti][r];
-        if (t == 0) {
+        if (gt == 0) {
             float U[3][3], V[3][3];
             essential_uv(E, U, V);
             for (int i = 0; i < 3; i++)
                 for (int j = 0; j < 3; j++) {
-                    s_uv[0][i][j] = U[i][j];
-                    s_uv[1][i][j] = V[i][j];
+                    s_uv[gid][0][i][j] = U[i][j];
+                    s_uv[gid][1][i][j] = V[i][j];
                 }
         }
         __syncthreads();
-        if (t < 4) {  // candidate c = t, one lane each
+        if (gt < 4) {  // candidate c = gt, one lane each
             const float W[3][3] = {{0, -1, 0}, {1, 0, 0}, {0, 0, 1}};
             float U[3][3], V[3][3];
             for (int i = 0; i < 3; i++)
                 for (int j = 0; j < 3; j++) {
-                    U[i][j] = s_uv[0][i][j];
-                    V[i][j] = s_uv[1][i][j];
+                    U[i][j] = s_uv[gid][0][i][j];
+                    V[i][j] = s_uv[gid][1][i][j];
                 }
-            const int c = t;
+            const int c = gt;
             float R[3][3];
             for (int i = 0; i < 3; i++)
                 for (int j = 0; j < 3; j++) {
@@ -693,21 +718,21 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
                     R[i][j] = s;
                 }
             const float sg = (c & 1) ? -1.f : 1.f;
-            for (int i = 0; i < 9; i++) s_cand[c][i] = R[i / 3][i % 3];
-            for (int i = 0; i < 3; i++) s_cand[c][9 + i] = sg * U[i][2];
+            for (int i = 0; i < 9; i++) s_cand[gid][c][i] = R[i / 3][i % 3];
+            for (int i = 0; i < 3; i++) s_cand[gid][c][9 + i] = sg * U[i][2];
         }
         __syncthreads();
         int votes[4] = {0, 0, 0, 0};
-        unsigned inl_mask = 0;  // bit k: correspondence t + k NT is a Sampson inlier of E
-        for (int i = t, k = 0; i < n; i += NT, k++)
+        unsigned inl_mask = 0;  // bit k: correspondence gt + k G is a Sampson inlier of E
+        for (int i = gt, k = 0; i < n; i += G, k++)
             inl_mask |= sampson_inlier(E, P[i], a.thr2) ? 1u << k : 0u;
 #pragma unroll
         for (int c = 0; c < 4; c++) {  // candidate-outer: 12 candidate floats live, not 48
             for (unsigned mk = inl_mask; mk; mk &= mk - 1) {
-                const float4 p = P[t + __builtin_ctz(mk) * NT];
+                const float4 p = P[gt + __builtin_ctz(mk) * G];
                 // depths z1, z2 of the midpoint triangulation, q z1 + t = -m z2 in the least-
                 // squares sense: z = num / det with det > 0, so only the numerators' signs count
-                const float *C = s_cand[c];
+                const float *C = s_cand[gid][c];
                 const F3 q = {{C[0] * p.x + C[1] * p.y + C[2], C[3] * p.x + C[4] * p.y + C[5], C[6] * p.x + C[7] * p.y + C[8]}};
                 const F3 m = {{-p.z, -p.w, -1.f}};
                 const F3 tt = {{C[9], C[10], C[11]}};
@@ -718,7 +743,7 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
                 votes[c] += (det > 0.f && n1 > 0.f && n2 > 0.f) ? 1 : 0;
             }
         }
-        if (PE_TRACE && sti == 0) tk4 = clock64();
+        if (PE_TRACE && rd == 0) tk4 = clock64();
 #pragma unroll
         for (int c = 0; c < 4; c++) {
             int v = votes[c];
@@ -727,37 +752,44 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
             if (lane == 0) s_votes[w][c] = v;
         }
         __syncthreads();
-        int bc = 0, bv = s_votes[0][0] + s_votes[1][0] + s_votes[2][0] + s_votes[3][0];
+        auto gsum_votes = [&](int c) {
+            int v = 0;
+            for (int k = 0; k < gnw; k++) v += s_votes[gw0 + k][c];
+            return v;
+        };
+        int bc = 0, bv = gsum_votes(0);
         for (int c = 1; c < 4; c++) {
-            const int v = s_votes[0][c] + s_votes[1][c] + s_votes[2][c] + s_votes[3][c];
+            const int v = gsum_votes(c);
             if (v > bv) {
                 bv = v;
                 bc = c;
             }
         }
-        if (PE_TRACE && sti == 0) tk5 = clock64();
+        if (PE_TRACE && rd == 0) tk5 = clock64();
 
         // ---- robust Gauss-Newton: iteratively reweighted, Cauchy weights 1 / (1 + (r / c)^2)
         //      on the Sampson residuals below 3 thr (none above), the scale c_0 = thr,
         //      c_{k+1} = min(thr, max(2 rms_w, 0.01 thr)) (rms_w: the weighted rms of iteration
         //      k): on exact data c shrinks until the outliers that fell inside the band no
         //      longer pull (converges to machine precision), on noisy data it settles near
-        //      2 sigma.  Weights and Sampson denominators are frozen within an iteration.  Wave
-        //      0 solves the 5x5 normal equations from the 22 block sums; one block barrier per
-        //      iteration (sums and state double-buffered). ----
+        //      2 sigma.  Weights and Sampson denominators are frozen within an iteration.  The
+        //      group's first wave solves the 5x5 normal equations from the group's 22 sums; one
+        //      block barrier per iteration after the sums, one after the state (both
+        //      double-buffered). ----
         float R[9], tv[3], bs[6];
 #pragma unroll
-        for (int i = 0; i < 9; i++) R[i] = s_cand[bc][i];
+        for (int i = 0; i < 9; i++) R[i] = s_cand[gid][bc][i];
 #pragma unroll
-        for (int i = 0; i < 3; i++) tv[i] = s_cand[bc][9 + i];
+        for (int i = 0; i < 3; i++) tv[i] = s_cand[gid][bc][9 + i];
         tangent_basis_f(tv, bs);
         float csc = th_max;  // the Cauchy scale
+        bool act = true;     // this group still iterates (group-uniform)
         for (int it = 0; it < a.refine_iters; it++) {
             float acc[22];  // sum w J^T J (15, upper), sum w J^T r (5), sum w r^2, sum w
 #pragma unroll
             for (int k = 0; k < 22; k++) acc[k] = 0.f;
             const float rcs = __builtin_amdgcn_rcpf(csc);
-            for (int i = t; i < n; i += NT) {
+            for (int i = act ? gt : n; i < n; i += G) {
                 const float4 p = P[i];
                 const float x1[3] = {p.x, p.y, 1.f}, x2[3] = {p.z, p.w, 1.f};
                 const float q[3] = {R[0] * x1[0] + R[1] * x1[1] + R[2], R[3] * x1[0] + R[4] * x1[1] + R[5],
@@ -800,7 +832,7 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
                 acc[21] += wt;
             }
             // the 22 sums reduced over the wave by recursive halving (a reduce-scatter), then
-            // the 4 wave partials in LDS
+            // the group's wave partials in LDS
             float(*red)[22] = s_red[it & 1];
             {
                 int vi;  // the sum this lane holds after the halving
@@ -808,15 +840,21 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
                 if (vi >= 0) red[w][vi] = f;
             }
             __syncthreads();
-            float *st = s_state[it & 1];
-            if (w == 0) {
-                float H[15], g[5];
+            float *st = s_state[it & 1][gid];
+            if (w == gw0) {
+                float H[15], g[5], r2 = 0.f, cnt = 0.f;
 #pragma unroll
-                for (int k = 0; k < 15; k++) H[k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+                for (int k = 0; k < 15; k++) H[k] = 0.f;
 #pragma unroll
-                for (int k = 0; k < 5; k++) g[k] = red[0][15 + k] + red[1][15 + k] + red[2][15 + k] + red[3][15 + k];
-                const float r2 = red[0][20] + red[1][20] + red[2][20] + red[3][20];
-                const float cnt = red[0][21] + red[1][21] + red[2][21] + red[3][21];
+                for (int k = 0; k < 5; k++) g[k] = 0.f;
+                for (int q = 0; q < gnw; q++) {
+#pragma unroll
+                    for (int k = 0; k < 15; k++) H[k] += red[gw0 + q][k];
+#pragma unroll
+                    for (int k = 0; k < 5; k++) g[k] += red[gw0 + q][15 + k];
+                    r2 += red[gw0 + q][20];
+                    cnt += red[gw0 + q][21];
+                }
                 // float Cholesky on the native reciprocal square root (the step only has to be
                 // a descent direction); every loop fully unrolled: static register indexing
                 float A[5][5];
@@ -830,7 +868,7 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
 #pragma unroll
                 for (int v = 0; v < 5; v++) A[v][v] = A[v][v] * (1.0f + 1e-6f) + 1e-30f;
                 float L[5][5] = {}, rl[5] = {};
-                bool ok = cnt >= 5.f;
+                bool ok = act && cnt >= 5.f;
 #pragma unroll
                 for (int i = 0; i < 5; i++)
 #pragma unroll
@@ -882,7 +920,8 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
                 // measured the same on exact data and 9 % slower under 0.5 px noise
                 const bool done = dmax < 1e-4f && fabsf(cs_new - csc) <= 2e-2f * csc;
                 // lane k < 14 stores word k of the state (static register indexing):
-                // R (9), t (3), scale, flags (bit 0: failed -- keep the old state; bit 1: converged)
+                // R (9), t (3), scale, flags (bit 0: failed or stopped -- keep the old state;
+                // bit 1: converged)
                 if (lane < 14) {
                     float v = 0.f;
 #pragma unroll
@@ -896,21 +935,25 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
             }
             __syncthreads();
             const int flags = __float_as_int(st[13]);
-            if (flags & 1) break;  // the same decision in every thread
+            if (act && !(flags & 1)) {
 #pragma unroll
-            for (int i = 0; i < 9; i++) R[i] = st[i];
+                for (int i = 0; i < 9; i++) R[i] = st[i];
 #pragma unroll
-            for (int i = 0; i < 3; i++) tv[i] = st[9 + i];
-            tangent_basis_f(tv, bs);
-            csc = st[12];
-            if (flags & 2) break;
+                for (int i = 0; i < 3; i++) tv[i] = st[9 + i];
+                tangent_basis_f(tv, bs);
+                csc = st[12];
+            }
+            act = act && !(flags & 3);
+            // block-uniform exit: every group has stopped
+            const bool other = par ? !(__float_as_int(s_state[it & 1][gid ^ 1][13]) & 3) : false;
+            if (!act && !other) break;
         }
 
         // ---- the robust cost of the refined pose (Cauchy at the scale thr, capped at 3 thr) and
         //      its inliers (Sampson distance < thr): the lower cost over the starts wins ----
         float rcost = 0.f;
         int ninl = 0;
-        for (int i = t; i < n; i += NT) {
+        for (int i = gt; i < n; i += G) {
             const float4 p = P[i];
             const float q[3] = {R[0] * p.x + R[1] * p.y + R[2], R[3] * p.x + R[4] * p.y + R[5],
                                 R[6] * p.x + R[7] * p.y + R[8]};
@@ -935,19 +978,41 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
             s_fin[w] = rcost;
             s_fin_n[w] = ninl;
         }
+        if (par && gt == 0) {  // each half's refined pose, for the threads that write the output
+#pragma unroll
+            for (int i = 0; i < 9; i++) s_cand[gid][0][i] = R[i];
+#pragma unroll
+            for (int i = 0; i < 3; i++) s_cand[gid][0][9 + i] = tv[i];
+        }
         __syncthreads();
-        const float cost = s_fin[0] + s_fin[1] + s_fin[2] + s_fin[3];
-        if (cost < bcost) {  // the same decision in every thread (a tie keeps the earlier start)
-            bcost = cost;
-            bn = s_fin_n[0] + s_fin_n[1] + s_fin_n[2] + s_fin_n[3];
+        // the group costs; concurrent: start 0's group first, so a tie keeps start 0 as in the
+        // sequential schedule
+        for (int gg = 0; gg < (par ? 2 : 1); gg++) {
+            const int w0 = par ? 2 * gg : 0, nw = par ? 2 : 4;
+            float cost = 0.f;
+            int cn_ = 0;
+            for (int k = 0; k < nw; k++) {
+                cost += s_fin[w0 + k];
+                cn_ += s_fin_n[w0 + k];
+            }
+            if (cost < bcost) {  // the same decision in every thread (a tie keeps the earlier start)
+                bcost = cost;
+                bn = cn_;
 #pragma unroll
-            for (int i = 0; i < 9; i++) bR[i] = R[i];
+                for (int i = 0; i < 9; i++) bR[i] = par ? s_cand[gg][0][i] : R[i];
 #pragma unroll
-            for (int i = 0; i < 3; i++) bT[i] = tv[i];
+                for (int i = 0; i < 3; i++) bT[i] = par ? s_cand[gg][0][9 + i] : tv[i];
+            }
         }
         __syncthreads();  // s_uv, s_cand, s_votes, s_fin are the next start's
-        if (csc <= th_min * 1.0001f) break;  // an exact fit: no second start needed
+        if constexpr (!par)
+            if (csc <= th_min * 1.0001f) break;  // an exact fit: no second start needed
     }
+    };
+    if (s_nh == 2 && !s_exact)
+        refine(std::true_type{});
+    else
+        refine(std::false_type{});
     {  // [R | t] row-major, thread t < 12 writes entry t (static register indexing)
         float v = 0.f;
 #pragma unroll
