@@ -789,7 +789,7 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
 #pragma unroll
             for (int k = 0; k < 22; k++) acc[k] = 0.f;
             const float rcs = __builtin_amdgcn_rcpf(csc);
-            for (int i = act ? gt : n; i < n; i += G) {
+            for (int i = (!par || act) ? gt : n; i < n; i += G) {
                 const float4 p = P[i];
                 const float x1[3] = {p.x, p.y, 1.f}, x2[3] = {p.z, p.w, 1.f};
                 const float q[3] = {R[0] * x1[0] + R[1] * x1[1] + R[2], R[3] * x1[0] + R[4] * x1[1] + R[5],
@@ -868,7 +868,7 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
 #pragma unroll
                 for (int v = 0; v < 5; v++) A[v][v] = A[v][v] * (1.0f + 1e-6f) + 1e-30f;
                 float L[5][5] = {}, rl[5] = {};
-                bool ok = act && cnt >= 5.f;
+                bool ok = (!par || act) && cnt >= 5.f;
 #pragma unroll
                 for (int i = 0; i < 5; i++)
 #pragma unroll
@@ -935,7 +935,7 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
             }
             __syncthreads();
             const int flags = __float_as_int(st[13]);
-            if (act && !(flags & 1)) {
+            if ((!par || act) && !(flags & 1)) {
 #pragma unroll
                 for (int i = 0; i < 9; i++) R[i] = st[i];
 #pragma unroll
@@ -943,10 +943,14 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
                 tangent_basis_f(tv, bs);
                 csc = st[12];
             }
-            act = act && !(flags & 3);
-            // block-uniform exit: every group has stopped
-            const bool other = par ? !(__float_as_int(s_state[it & 1][gid ^ 1][13]) & 3) : false;
-            if (!act && !other) break;
+            if constexpr (par) {
+                act = act && !(flags & 3);
+                // block-uniform exit: every group has stopped
+                const bool other = !(__float_as_int(s_state[it & 1][gid ^ 1][13]) & 3);
+                if (!act && !other) break;
+            } else {
+                if (flags & 3) break;  // the same decision in every thread
+            }
         }
 
         // ---- the robust cost of the refined pose (Cauchy at the scale thr, capped at 3 thr) and
