@@ -78,6 +78,10 @@ def parse(argv=None):
     ap.add_argument("--window-steps", type=int, default=10,
                     help="secondary line (N = 1 only): the windowed int8 front-end of tracking_main.c "
                          "(tools/bench_window.py, 7285-cell KITTI grid, 1024 pairs); 0 = skip")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                    help="N > 1: the collective backend (nccl = RCCL over xGMI, the product path; gloo stages the "
+                         "per-step result gather through host memory -- how the N-rank GPU path is exercised on a "
+                         "one-GPU box, where RCCL refuses two ranks on one device)")
     ap.add_argument("--harness-cpu", action="store_true",
                     help="test only: the multi-rank harness with the CPU oracle as the step (gloo)")
     return ap.parse_args(argv)
@@ -160,10 +164,11 @@ class ResultGather:
     keeps it for the report / trajectory chain).  Issued on the stream that produced the
     results, so it is ordered after that batch's pose; a no-op at world size 1."""
 
-    def __init__(self, torch, dist, world, B, device, slots):
+    def __init__(self, torch, dist, world, B, device, slots, coll_device=None):
         self.torch, self.dist, self.world = torch, dist, world
+        self.coll_device = device if coll_device is None else coll_device  # gloo + GPU results: via the host
         self.res = [torch.empty((B, 13), dtype=torch.float32, device=device) for _ in range(slots)]
-        self.out = [torch.empty((world * B, 13), dtype=torch.float32, device=device) for _ in range(slots)]
+        self.out = [torch.empty((world * B, 13), dtype=torch.float32, device=self.coll_device) for _ in range(slots)]
         self.count = 0
 
     def __call__(self, slot, T, nmatch, stream=None):
@@ -174,6 +179,8 @@ class ResultGather:
             r = self.res[slot]
             r[:, :12].copy_(T.reshape(T.shape[0], 12))
             r[:, 12].copy_(nmatch.view(torch.float32))
+            if str(r.device) != str(self.coll_device):
+                r = r.to(self.coll_device)  # ordered on `stream` (a blocking copy for the host)
             self.dist.all_gather_into_tensor(self.out[slot], r)
         self.count += 1
 
@@ -378,59 +385,40 @@ def cpu_baseline(seconds, n):
     mm(n, n, KD, P(A), P(Bm), P(C))
     one = time.perf_counter() - t1
     return dict(ci, value=total / dt, unit="pairs/s", cores=threads, kind=kind,
+                all_cores_extrapolated={"value": round(total / dt / threads * ci["nproc"], 1), "cores": ci["nproc"],
+                                        "note": "per-thread rate x nproc (not run: the box grants %d of its %d "
+                                                "cores to one GPU)" % (threads, ci["nproc"])},
                 sample="%d pairs of %dx%dx%d fp32 matmul + row argmax over %.1f s on %d host threads "
                        "(gemmini_functions_cpu.h:14-56 order, gcc -O2); 1 core: %.1f ms/pair"
                        % (total, n, n, KD, dt, threads, one * 1e3))
 
 
 def cpu_c0(seconds):
-    """the as-built tracking_main path (softmax + top-N + windowed match +
-    stub RANSAC + pose, src/tracking_main.c:84-228) on a 24 x 80-cell int8 pair, CPU only: the
-    oracle's restatement ('port': tracking_main.c itself does not build), 1 core and
-    all the host threads (one pair per thread at a time)."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import concurrent.futures as cf
-
-    import oracle
-    import synth
-
-    f0, f1 = synth.synth_window_pair(1)
-    K = np.array([[517.306408, 0.0, 318.643040], [0.0, 516.469215, 255.313989], [0.0, 0.0, 1.0]], np.float32)
-
-    def one_pair():
-        r = oracle.track_window(f0, f1, as_built=True)
-        n = r["points1"].shape[0]
-        if n > 0:
-            _, E, _, _ = oracle.ransac_essential_matrix(r["points1"], r["points2"], K, 10, 1.1)
-            oracle.recover_pose(E)
-        return n
-
-    nm = one_pair()
-    t0 = time.perf_counter()
-    k = 0
-    while time.perf_counter() - t0 < min(2.0, seconds / 4):
-        one_pair()
-        k += 1
-    us1 = (time.perf_counter() - t0) / k * 1e6
+    """the as-built tracking_main path (softmax + top-N + windowed match + stub
+    RANSAC + pose, src/tracking_main.c:68-228) on the real KITTI pair (quantized_image0 -> frame
+    000001, 24 x 80 cells), CPU only: the reference's OWN main body extracted from its text and built
+    at -O2 with top_N.c / pnp_solver.c ('reference', oracle/_ref), or the oracle's restatement
+    ('port') where oracle/_ref is absent.  tools/cpu_c0.py runs as a child process (main's rand()
+    is process-global: one pair per worker PROCESS), per pair on one core and on the box's share of
+    worker processes; the all-core figure for the whole host is the per-process rate x nproc
+    (extrapolated: the box grants one GPU's share of its cores)."""
     ci = cpu_info()
-    deadline = time.perf_counter() + seconds
-
-    def worker(_):
-        c = 0
-        while time.perf_counter() < deadline:
-            one_pair()
-            c += 1
-        return c
-
-    t1 = time.perf_counter()
-    with cf.ThreadPoolExecutor(ci["threads"]) as ex:
-        tot = sum(ex.map(worker, range(ci["threads"])))
-    dt = time.perf_counter() - t1
-    return dict(ci, metric="C0 as-built tracking_main pairs/s (24x80-cell int8 pair, CPU)", kind="port",
-                us_per_pair_1core=round(us1, 1), value=round(tot / dt, 1), unit="pairs/s",
-                cores=ci["threads"], matches=nm,
-                sample="%d pairs over %.1f s on %d host threads (oracle restatement via ctypes; python "
-                       "call overhead included)" % (tot, dt, ci["threads"]))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "cpu_c0.py"), "--seconds", str(seconds),
+                        "--procs", str(ci["threads"])], capture_output=True, text=True, timeout=seconds + 120)
+    if r.returncode != 0:
+        return dict(ci, error="tools/cpu_c0.py failed: %s" % r.stderr[-400:])
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    per_proc = d["value"] / max(d["procs"], 1)
+    return dict(ci, metric="C0 as-built tracking_main pairs/s (KITTI 00 000000 -> 000001, 24x80-cell int8, CPU)",
+                kind=d["kind"], us_per_pair_1core=d["us_per_pair_1core"], value=d["value"], unit="pairs/s",
+                cores=d["procs"], matches=d["matches"],
+                all_cores_extrapolated={"value": round(per_proc * ci["nproc"], 1), "cores": ci["nproc"],
+                                        "note": "per-process rate x nproc (not run: the box grants %d of its %d "
+                                                "cores to one GPU)" % (d["procs"], ci["nproc"])},
+                sample="%d pairs over %.1f s on %d worker processes (%s; ctypes call included)" % (
+                    d["pairs"], d["seconds"], d["procs"],
+                    "src/tracking_main.c main body + top_N.c + pnp_solver.c, gcc -O2" if d["kind"] == "reference"
+                    else "oracle restatement"))
 
 
 def roofline(kernel, screen, B, n, avg_s, fused):
@@ -523,10 +511,17 @@ def main():
     import mvtrack
     import synth
 
+    # LOCAL_RANK -> device modulo the visible devices: N ranks may share a box with fewer GPUs
+    # (a rehearsal of the N-rank path; with nccl, RCCL needs one device per rank)
+    local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend="gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     B, n = args.batch, args.kp
 
     d0, d1, kp0, kp1 = gen_batch(torch, dev, B, n, seed=pair_seed(rank, 0), noise=args.noise)
@@ -553,7 +548,7 @@ def main():
     K = synth.KITTI_K
     pose_p = mvtrack.pose_params(mvtrack.AS_INTENDED, fx=K[0, 0], fy=K[1, 1], cx=K[0, 2], cy=K[1, 2],
                                  hypotheses=args.hypotheses, inlier_thresh=1.0, refine_iters=10, seed=7)
-    gather = ResultGather(torch, dist, world, B, dev, P)
+    gather = ResultGather(torch, dist, world, B, dev, P, coll_dev)
 
     # the reference keeps only the matched pairs (pairwise_pnp.py:649-657): no score output, so
     # the exact re-score runs only where the rounding window does not decide the row (indices
@@ -583,7 +578,7 @@ def main():
 
     # the headline: an unprofiled loop (no per-kernel events inside the measured wall time)
     elapsed = timed_loop(step, args.steps, args.warmup, sync, barrier)
-    elapsed = max_over_ranks(torch, dist, elapsed, dev)
+    elapsed = max_over_ranks(torch, dist, elapsed, coll_dev)
     gathers_timed = gather.count
 
     # per-kernel durations for the roofline and the stage split: a second, profiled loop of the
@@ -609,7 +604,7 @@ def main():
         for _ in range(2):
             step()
         sync()
-        el_s = max_over_ranks(torch, dist, timed_loop(step, args.score_steps, 0, sync, barrier), dev)
+        el_s = max_over_ranks(torch, dist, timed_loop(step, args.score_steps, 0, sync, barrier), coll_dev)
         mvtrack.profile_enable(True)
         timed_loop(prof_step, args.score_steps, 0, sync, barrier)
         mvtrack.profile_enable(False)
@@ -646,10 +641,11 @@ def main():
     if world > 1:  # the per-step all-gather's buffer: every rank's results, this rank's own equal to T
         sync()
         g = gather.out[0].view(world, B, 13)
-        assert torch.equal(g[rank, :, :12], Ts[0].reshape(B, 12)), "gathered results differ from this rank's"
+        assert torch.equal(g[rank, :, :12].to(dev), Ts[0].reshape(B, 12)), "gathered results differ from this rank's"
         gathered = {"pairs_per_gather": int(g.shape[0] * g.shape[1]), "gathers_in_timed_steps": gathers_timed,
-                    "bytes_per_gather": int(g.numel() * 4)}
-    sums = gather_checksums(torch, dist, [float(nmatch.sum().item()), float(ok)], dev)
+                    "bytes_per_gather": int(g.numel() * 4), "backend": args.dist_backend,
+                    "ranks_per_device": "%d ranks on %d device(s)" % (world, torch.cuda.device_count())}
+    sums = gather_checksums(torch, dist, [float(nmatch.sum().item()), float(ok)], coll_dev)
     pairs_total = B * args.steps * world
     value = pairs_total / elapsed
     k_avg_s = (k_ms / max(k_n, 1)) * 1e-3

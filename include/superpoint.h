@@ -51,7 +51,10 @@ int mv_superpoint_destroy(mv_superpoint *net);
  * superpoint_inference.py:649-655), semi_scale[B], desc_scale[B] (device).  oh, ow: the
  * network's input size (192 x 640 in the reference), multiples of 8.  A frame whose output
  * has fewer than two distinct values (torch.min of an empty tensor raises in the reference)
- * gets scale 0 and its raw int8 network output. */
+ * gets scale 0 and its raw int8 network output.  Runs on the context's stream; the net's
+ * activation buffers are shared by every context that uses the net, so a forward is ordered
+ * after the net's previous forward whatever stream that ran on (the library makes the stream
+ * wait on it).  The host calls on one net must not run concurrently from several threads. */
 int mv_superpoint_forward_dev(mv_context *ctx, mv_superpoint *net, int batch, int H, int W, int oh, int ow,
                               const uint8_t *images, int8_t *semi, int8_t *desc, float *semi_scale,
                               float *desc_scale);

@@ -799,6 +799,15 @@ extern "C" int mv_match_allpairs_f32_prepare_dev(mv_context *ctx, int batch, int
                                                  const float *desc1) {
     MV_REQUIRE(ctx != nullptr && batch > 0 && cap > 0 && n1 && desc1);
     MV_HIP_TRY(hipSetDevice(ctx->device));
+    if (ctx->ap_screen == MV_SCREEN_I8) {  // the one-pass match reads frame 1 itself: record only
+        ctx->prep_screen = ctx->ap_screen;
+        ctx->prep_staged = false;  // sequence mode stages these frames on first use
+        ctx->prep_batch = batch;
+        ctx->prep_cap = cap;
+        ctx->prep_n1 = n1;
+        ctx->prep_desc1 = desc1;
+        return mv::set_status(MV_OK);
+    }
     void *scr = ap_scratch(ctx, mv::ap_image_bytes(ctx->ap_screen, batch, cap));
     if (!scr) return MV_ERR_OUT_OF_MEMORY;
     if (!ctx->aux_stream) {
@@ -831,7 +840,7 @@ extern "C" int mv_match_allpairs_f32_run_dev(mv_context *ctx, int batch, int cap
         return MV_ERR_INVALID_ARG;
     }
     MV_HIP_TRY(hipSetDevice(ctx->device));
-    MV_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_prep, 0));
+    if (ctx->prep_staged && ctx->aux_stream) MV_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_prep, 0));
     return ap_match(ctx->ap_screen, ctx->stream, ctx->ap_scratch, batch, cap, n0, n1, desc0, desc1, thresh,
                     match_idx, match_score);
 }
@@ -990,13 +999,21 @@ extern "C" int mv_match_sequence_f32_run_prepare_dev(mv_context *ctx, int frames
                                                      float *match_score, int next_frames, int next_cap,
                                                      const int *next_n, const float *next_desc) {
     MV_REQUIRE(ctx != nullptr && frames >= 2 && next_frames >= 2 && next_cap > 0 && next_n && next_desc);
-    if (ctx->ap_screen == MV_SCREEN_F16 || !ctx->prep_desc1 || !ctx->prep_staged || ctx->prep_batch != frames ||
+    if (ctx->ap_screen == MV_SCREEN_F16 || !ctx->prep_desc1 || ctx->prep_batch != frames ||
         ctx->prep_cap != cap || ctx->prep_n1 != n || ctx->prep_desc1 != desc || ctx->prep_screen == MV_SCREEN_F16) {
         mv::set_error(MV_ERR_INVALID_ARG,
                       "mv_match_sequence_f32_run_prepare_dev: no matching prepare for these frames (int8 screen)");
         return MV_ERR_INVALID_ARG;
     }
     MV_HIP_TRY(hipSetDevice(ctx->device));
+    if (!ctx->prep_staged) {  // recorded by the one-pass screen's prepare: stage the images now
+        void *scr = ap_scratch(ctx, mv::ap_image_bytes(ctx->ap_screen, frames, cap));
+        if (!scr) return MV_ERR_OUT_OF_MEMORY;
+        if (ctx->aux_stream) MV_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_prep, 0));
+        const int ps = ap_prepare(ctx->ap_screen, ctx->stream, scr, frames, cap, n, desc);
+        if (ps != MV_OK) return ps;
+        ctx->prep_staged = true;
+    }
     const int sc = ap_scratch2(ctx, mv::ap_image_bytes(ctx->ap_screen, next_frames, next_cap));
     if (sc != MV_OK) return sc;
     if (ctx->aux_stream) MV_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_prep, 0));

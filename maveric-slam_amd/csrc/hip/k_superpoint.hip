@@ -989,6 +989,9 @@ extern "C" int mv_superpoint_forward_dev(mv_context *ctx, mv_superpoint *net, in
     }
     int8_t *A = static_cast<int8_t *>(net->act), *Bf = A + a_bytes;
     hipStream_t st = ctx->stream;
+    // the activations belong to the net, not the context: order this forward after the previous
+    // one on whatever stream (context) it ran (free on the same stream)
+    if (net->used) MV_HIP_TRY(hipStreamWaitEvent(st, net->done, 0));
     const char *wd = static_cast<const char *>(net->wdev);
     int r;
     int h = oh, w = ow;

@@ -40,11 +40,32 @@ int set_status(int status) {
 }
 
 int quiesce(mv_context *ctx) {
-    MV_HIP_TRY(hipStreamSynchronize(ctx->own_stream));
-    if (ctx->stream != ctx->own_stream) MV_HIP_TRY(hipStreamSynchronize(ctx->stream));
-    for (int i = 0; i < ctx->n_used_streams && i < 4; i++)
-        if (ctx->used_streams[i] != ctx->stream) MV_HIP_TRY(hipStreamSynchronize(ctx->used_streams[i]));
-    if (ctx->aux_stream) MV_HIP_TRY(hipStreamSynchronize(ctx->aux_stream));
+    // own_stream waits on every stream the context left (ev_retire), so these three cover all
+    // of the context's work; every stream is synchronised even after a failure, and a failure
+    // falls back to the whole device before the caller frees a buffer
+    hipError_t e = hipStreamSynchronize(ctx->own_stream);
+    if (ctx->stream != ctx->own_stream) {
+        const hipError_t e2 = hipStreamSynchronize(ctx->stream);
+        if (e == hipSuccess) e = e2;
+    }
+    if (ctx->aux_stream) {
+        const hipError_t e3 = hipStreamSynchronize(ctx->aux_stream);
+        if (e == hipSuccess) e = e3;
+    }
+    if (e != hipSuccess) {
+        (void)hipDeviceSynchronize();
+        set_error(MV_ERR_HIP, "quiesce: %s", hipGetErrorString(e));
+        return MV_ERR_HIP;
+    }
+    return MV_OK;
+}
+
+// the context moves off `old`: own_stream waits for everything issued on it so far
+static int retire_stream(mv_context *ctx, hipStream_t old) {
+    if (old == ctx->own_stream) return MV_OK;
+    if (!ctx->ev_retire) MV_HIP_TRY(hipEventCreateWithFlags(&ctx->ev_retire, hipEventDisableTiming));
+    MV_HIP_TRY(hipEventRecord(ctx->ev_retire, old));
+    MV_HIP_TRY(hipStreamWaitEvent(ctx->own_stream, ctx->ev_retire, 0));
     return MV_OK;
 }
 
@@ -155,6 +176,8 @@ int mv_context_destroy(mv_context *ctx) {
         (void)hipEventDestroy(ctx->ev_prep);
         (void)hipStreamDestroy(ctx->aux_stream);
     }
+    (void)hipStreamSynchronize(ctx->own_stream);  // the streams the context left (ev_retire)
+    if (ctx->ev_retire) (void)hipEventDestroy(ctx->ev_retire);
     if (ctx->scratch) (void)hipFree(ctx->scratch);
     if (ctx->ap_scratch) (void)hipFree(ctx->ap_scratch);
     if (ctx->ap_scratch2) (void)hipFree(ctx->ap_scratch2);
@@ -166,17 +189,22 @@ int mv_context_destroy(mv_context *ctx) {
 
 int mv_context_set_stream(mv_context *ctx, void *s) {
     MV_REQUIRE(ctx != nullptr);
-    ctx->stream = (hipStream_t)s;  // NULL is HIP's null stream (torch's default stream), not "unset"
-    if (ctx->stream != ctx->own_stream) {  // remembered for quiesce()
-        bool seen = false;
-        for (int i = 0; i < ctx->n_used_streams && i < 4; i++) seen = seen || ctx->used_streams[i] == ctx->stream;
-        if (!seen) ctx->used_streams[ctx->n_used_streams++ % 4] = ctx->stream;
+    if ((hipStream_t)s != ctx->stream) {
+        MV_HIP_TRY(hipSetDevice(ctx->device));
+        const int r = mv::retire_stream(ctx, ctx->stream);
+        if (r != MV_OK) return r;
     }
+    ctx->stream = (hipStream_t)s;  // NULL is HIP's null stream (torch's default stream), not "unset"
     return MV_OK;
 }
 
 int mv_context_use_own_stream(mv_context *ctx) {
     MV_REQUIRE(ctx != nullptr);
+    if (ctx->stream != ctx->own_stream) {
+        MV_HIP_TRY(hipSetDevice(ctx->device));
+        const int r = mv::retire_stream(ctx, ctx->stream);
+        if (r != MV_OK) return r;
+    }
     ctx->stream = ctx->own_stream;
     return MV_OK;
 }
@@ -199,10 +227,11 @@ int mv_context_allpairs_screen(mv_context *ctx) { return ctx ? ctx->ap_screen : 
 
 int mv_context_reserve(mv_context *ctx, int batch, int cap) {
     MV_REQUIRE(ctx != nullptr && batch > 0 && cap > 0);
-    // the staged images of the context's CURRENT screen (ap_image_bytes): the default one-pass
-    // int8 screen uses them only in sequence mode; run_prepare's second image as well
-    const size_t img = mv::ap_image_bytes(ctx->ap_screen, batch, cap);
-    if (ctx->ap_scratch_bytes < img) {
+    // the staged images of the context's CURRENT screen (ap_image_bytes) and run_prepare's second
+    // image; the default one-pass int8 screen stages nothing (sequence mode allocates its images
+    // on first use)
+    const size_t img = ctx->ap_screen == MV_SCREEN_I8 ? 0 : mv::ap_image_bytes(ctx->ap_screen, batch, cap);
+    if (img && ctx->ap_scratch_bytes < img) {
         if (ctx->ap_scratch) {
             const int q = mv::quiesce(ctx);
             if (q != MV_OK) return q;
@@ -215,7 +244,7 @@ int mv_context_reserve(mv_context *ctx, int batch, int cap) {
         if (hipMalloc(&ctx->ap_scratch, ab) != hipSuccess) return MV_ERR_OUT_OF_MEMORY;
         ctx->ap_scratch_bytes = ab;
     }
-    if (ctx->ap_scratch2_bytes < img) {  // run_prepare's second image
+    if (img && ctx->ap_scratch2_bytes < img) {  // run_prepare's second image
         if (ctx->ap_scratch2) {
             const int q = mv::quiesce(ctx);
             if (q != MV_OK) return q;

@@ -29,8 +29,10 @@ struct mv_context {
     int prep_screen;
     bool prep_staged;  // the prepared batch's frame 1 sits staged in ap_scratch (false: recorded only)
     int ap_screen;  // mv_allpairs_screen of the fp32 all-pairs match (0 = int8, the default)
-    hipStream_t used_streams[4];  // user streams set on this context (ring): quiesced before a buffer is freed
-    int n_used_streams;
+    // set_stream / use_own_stream away from a stream record this event on it and make own_stream
+    // wait on it: own_stream then orders after all work issued on every stream the context left
+    // (no stream handle is kept, so a caller may destroy a stream once the context moved off it)
+    hipEvent_t ev_retire;
 };
 
 namespace mv {
@@ -44,9 +46,10 @@ void *stage(mv_context *ctx, size_t bytes);
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// Wait for every stream this context has issued work on (its own, the current and recent user
-// streams, the staging stream) -- before a context buffer is freed; other contexts and threads
-// are not blocked (no device-wide synchronisation, no effect on their graph captures).
+// Wait for every stream this context has issued work on (its own stream -- which waits on every
+// stream the context left, via ev_retire --, the current stream and the staging stream) -- before
+// a context buffer is freed; other contexts and threads are not blocked (no device-wide
+// synchronisation unless a synchronisation itself fails).
 int quiesce(mv_context *ctx);
 // bytes of one staged frame-1 image (ap_scratch / ap_scratch2) under `screen`
 size_t ap_image_bytes(int screen, int batch, int cap);

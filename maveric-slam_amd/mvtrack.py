@@ -748,9 +748,10 @@ class SuperPoint:
         except Exception:
             pass
 
-    def forward(self, images, oh=192, ow=640, out=None):
+    def forward(self, images, oh=192, ow=640, out=None, ctx=None):
         """images: torch uint8 [B][H][W] on the context's device; returns (semi, desc,
-        semi_scale, desc_scale) torch tensors (or fills `out`, the same four)"""
+        semi_scale, desc_scale) torch tensors (or fills `out`, the same four).  ctx: run on another
+        context's stream (default: the one the net was created with)"""
         import torch
 
         B, H, W = images.shape
@@ -761,7 +762,7 @@ class SuperPoint:
                    torch.empty((B, cells, 256), dtype=torch.int8, device=dev),
                    torch.empty(B, dtype=torch.float32, device=dev), torch.empty(B, dtype=torch.float32, device=dev))
         semi, desc, ss, ds = out
-        check(lib().mv_superpoint_forward_dev(self.ctx.h, self.h, B, H, W, oh, ow, _t(images), _t(semi), _t(desc),
+        check(lib().mv_superpoint_forward_dev((ctx or self.ctx).h, self.h, B, H, W, oh, ow, _t(images), _t(semi), _t(desc),
                                               _t(ss), _t(ds)), "superpoint_forward")
         return semi, desc, ss, ds
 

@@ -144,6 +144,66 @@ def ref_run_nms(semi, semi_scale, rows=192, cols=640, feature_rows=24, feature_c
     return sup, kp
 
 
+REF_TRACK_SO = os.path.join(HERE, "_ref", "libmv_ref_track.so")
+REF_TRACK_TS_SO = os.path.join(HERE, "_ref", "libmv_ref_track_ts.so")
+REF_TRACK_O2_SO = os.path.join(HERE, "_ref", "libmv_ref_track_o2.so")
+_ref_track = {}
+
+
+def ref_track_available():
+    return os.path.exists(REF_TRACK_SO) and os.path.exists(REF_TRACK_TS_SO)
+
+
+def _ref_track_lib(true_scale, o2=False):
+    key = (true_scale, o2)
+    if key not in _ref_track:
+        R = ctypes.CDLL(REF_TRACK_O2_SO if o2 else REF_TRACK_TS_SO if true_scale else REF_TRACK_SO)
+        R.ref_tracking_main.restype = _I
+        R.ref_tracking_main.argtypes = [_I, _I, _I, _I, _F, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]
+        _ref_track[key] = R
+    return _ref_track[key]
+
+
+def ref_tracking_main(frame0, frame1, true_scale=False, o2=False):
+    """The reference's OWN tracking driver: the body of src/tracking_main.c's main (:69-230 --
+    softmax, top-N, the windowed match :103-194, RANSAC, pose) cut out of its text by
+    oracle/Makefile, with src/top_N.c and src/pnp_solver.c compiled from source
+    (oracle/ref_track_harness.c).  The frames take the place of quantized_pair0.h's image0_* /
+    image1_* (24 x 80 cells: main's arrays hold 1920).  true_scale=False: compute_softmax /
+    compute_top_N reached without a prototype as in the reference binary (SURVEY F7);
+    true_scale=True: top_N.h in scope, the float scale arrives.  Returns dict(status (0, 1: top_N.c
+    exit(1), 2: no matches), points1 (frame-0 pixels), points2 (frame-1 pixels), E, inliers, R1,
+    R2, t, num_inliers).  num_inliers = -1 and E = NaN when no RANSAC hypothesis had an inlier (the
+    reference then leaves both unwritten: main reads uninitialised stack).  o2: the as-built driver
+    compiled at -O2 (the C0 timing build) instead of -O0 (the reference's CMake default).  Not
+    thread-safe (main's rand() and the capture are process-global)."""
+    if o2 and true_scale:
+        raise ValueError("the -O2 build is the as-built driver only")
+    R = _ref_track_lib(bool(true_scale), bool(o2))
+    rows, cols = int(frame0["rows"]), int(frame0["cols"])
+    assert rows * cols == 1920 and int(frame1["rows"]) == rows and int(frame1["cols"]) == cols
+    s0 = np.ascontiguousarray(frame0["semi"], np.int8)
+    d0 = np.ascontiguousarray(frame0["desc"], np.int8)
+    s1 = np.ascontiguousarray(frame1["semi"], np.int8)
+    d1 = np.ascontiguousarray(frame1["desc"], np.int8)
+    n = ctypes.c_int(0)
+    p1 = np.zeros((1000, 2), np.float32)
+    p2 = np.zeros((1000, 2), np.float32)
+    E = np.zeros(9, np.float32)
+    inl = np.zeros(1000, np.int32)
+    ni = ctypes.c_int(0)
+    R1 = np.zeros(9, np.float32)
+    R2 = np.zeros(9, np.float32)
+    t = np.zeros(3, np.float32)
+    st = R.ref_tracking_main(rows * 8, cols * 8, rows, cols, float(frame0["semi_scale"]), _ptr(s0), _ptr(d0),
+                             float(frame1["semi_scale"]), _ptr(s1), _ptr(d1), ctypes.byref(n), _ptr(p1), _ptr(p2),
+                             _ptr(E), _ptr(inl), ctypes.byref(ni), _ptr(R1), _ptr(R2), _ptr(t))
+    k = n.value
+    return dict(status=st, points1=p1[:k].copy(), points2=p2[:k].copy(), E=E.reshape(3, 3),
+                inliers=inl[:max(ni.value, 0)].copy(), R1=R1.reshape(3, 3), R2=R2.reshape(3, 3), t=t,
+                num_inliers=ni.value)
+
+
 def ref_available():
     return os.path.exists(REF_SO)
 

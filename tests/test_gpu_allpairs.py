@@ -443,3 +443,44 @@ def test_prepare_then_one_shot_calls(ctx, screen, orc, torch_cuda):
                 assert (idx[k].cpu().numpy() == i2).all(), k
     finally:
         ctx.set_stream(None)
+
+
+@pytest.mark.parametrize("n1", [4096, 4097, 8192, 8193])
+def test_allpairs_f32_long_frame1(ctx, screen, orc, torch_cuda, n1):
+    """frame 1 beyond 4096 keypoints: the one-pass kernel leaves the integer keys (7-bit tags hold
+    64 column tiles, n1 <= 4096) for the float sweep with 8-bit tags, and above 8192 (128 tiles)
+    widens the tags to 9 bits (k_allpairs_direct.hip:464-495); the staged screens' tag widths
+    change at the same tile counts.  Indices and exact scores against the oracle, with a
+    re-observed subset spread over the whole of frame 1 (so late tiles hold maximisers) plus
+    duplicated columns in the first and last tiles (ties across tag groups)."""
+    rng = np.random.default_rng(n1)
+    n0 = 320
+    p = synth.synth_pair_f32(n1, n=n0, n1=n1, noise=0.3)
+    a, b = p["desc0"], p["desc1"].copy()
+    b[n1 - 5:n1] = b[0:5]  # exact duplicates: the first maximum (lowest index) must win
+    b[n1 - 70] = a[3]  # an exact match deep in the last tiles
+    for scores in (True, False):
+        idx, sc = run_f32(ctx, torch_cuda, [(a, b)], cap=n1, scores=scores)
+        i2, s2 = orc.allpairs_f32(a, b, 0.8)
+        assert (idx[0, :n0] == i2).all()
+        if scores:
+            assert (bits(sc[0, :n0]) == bits(s2)).all()
+    assert (i2 >= 0).sum() > 150 and i2[3] == n1 - 70 and (i2 > 4096).any()
+
+
+@pytest.mark.parametrize("scores", [True, False])
+def test_allpairs_f32_full_size_survey_c1_noise(ctx, screen, orc, torch_cuda, scores):
+    """SURVEY 8(d) C1 at full size: 1024 x 1024, the re-observed 60 % with sigma = 0.05 PER
+    COMPONENT (noise norm ~0.8, renormalised): re-observed cosines ~0.78 straddle the 0.8
+    threshold, so most rows take the exact re-score path -- indices (and scores) vs the oracle."""
+    pairs = []
+    for s in range(2):
+        p = synth.synth_pair_f32(900 + s, noise=0.05 * 16.0)
+        pairs.append((p["desc0"], p["desc1"]))
+    idx, sc = run_f32(ctx, torch_cuda, pairs, scores=scores)
+    for b, (a, c) in enumerate(pairs):
+        i2, s2 = orc.allpairs_f32(a, c, 0.8)
+        assert (idx[b] == i2).all()
+        if scores:
+            assert (bits(sc[b]) == bits(s2)).all()
+        assert 30 < (i2 >= 0).sum() < 500  # near the threshold: a minority of the re-observed rows pass

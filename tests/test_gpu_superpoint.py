@@ -107,3 +107,36 @@ def test_superpoint_into_window_track(ctx, orc, torch_cuda, sp, weights):
         r = orc.track_window(oframes[0], oframes[1], as_built=as_built)
         assert (p1 == r["points1"]).all() and (p2 == r["points2"]).all()
         assert len(p1) > 0
+
+
+def test_superpoint_one_net_two_streams(ctx, orc, torch_cuda, sp, weights):
+    """the net's activation buffers are shared by every context; two forwards issued on
+    two contexts with their own streams and no host synchronisation between them must both equal
+    the oracle (the second forward waits on the first one's completion event)."""
+    import mvtrack
+
+    torch = torch_cuda
+    dev = torch.device("cuda:0")
+    ims = load_golden("kitti00_images.npz")
+    rng = np.random.default_rng(5)
+    sets = [[ims["img_000000"], ims["img_000001"]] * 4, [rng.integers(0, 256, (376, 1241), dtype=np.uint8)
+                                                          for _ in range(8)]]
+    ctx2 = mvtrack.Context(0)
+    s1, s2 = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    try:
+        xs = [torch.from_numpy(np.ascontiguousarray(np.stack(s), np.uint8)).to(dev) for s in sets]
+        torch.cuda.synchronize()
+        ctx.set_stream(s1)
+        ctx2.set_stream(s2)
+        outs = []
+        for rep in range(3):
+            outs.append(sp.forward(xs[0], 192, 640, ctx=ctx))
+            outs.append(sp.forward(xs[1], 192, 640, ctx=ctx2))
+        torch.cuda.synchronize()
+    finally:
+        ctx.set_stream(None)
+        ctx2.close()
+    for k, o in enumerate(outs):
+        imgs = sets[k % 2][:2]
+        got = tuple(t.cpu().numpy()[:2] for t in o)
+        _check(orc, weights, imgs, got, 192, 640)
