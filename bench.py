@@ -756,6 +756,13 @@ def main():
         r = bench_superpoint.run(batch=64, steps=args.extra_steps, warmup=2, check=1)
         out["superpoint"] = {k: r[k] for k in ("metric", "value", "unit", "batch", "ms_per_step", "stages_ms",
                                                 "mfma_roofline", "oracle_exact")}
+        # the fp32 path of pairwise_pnp.py:577-694 from 8-bit frames to poses (SURVEY 8(f)1 + 2)
+        import bench_image_pose
+
+        r = bench_image_pose.run(frames=257, steps=args.extra_steps, warmup=2, check=1)
+        out["image_to_pose"] = {k: r[k] for k in ("metric", "value", "unit", "frames_per_step", "ms_per_step",
+                                                   "stages_ms_per_step", "keypoints_per_frame", "matches_per_pair",
+                                                   "pose_ok", "checked_pairs")}
     if rank == 0:
         print(json.dumps(out), flush=True)
     for cx in ctxs:

@@ -965,33 +965,44 @@ extern "C" int mv_superpoint_destroy(mv_superpoint *net) {
     return MV_OK;
 }
 
-extern "C" int mv_superpoint_forward_dev(mv_context *ctx, mv_superpoint *net, int batch, int H, int W, int oh,
-                                         int ow, const uint8_t *images, int8_t *semi, int8_t *desc,
-                                         float *semi_scale, float *desc_scale) {
-    MV_REQUIRE(ctx && net && batch > 0 && H > 0 && W > 0 && oh >= 8 && ow >= 8 && oh % 8 == 0 && ow % 8 == 0);
-    MV_REQUIRE(images && semi && desc && semi_scale && desc_scale && net->device == ctx->device);
-    MV_REQUIRE((long)oh * ow * 64 < (1l << 31) && (long)batch * H * W < (1l << 40));
-    MV_HIP_TRY(hipSetDevice(ctx->device));
-    // activation ping-pong buffers, oh * ow * 16 bytes per frame each (conv1b's pooled output, the
-    // largest after the fused conv1a)
-    const size_t a_bytes = mv::align_up((size_t)batch * oh * ow * 16, 256);
-    const size_t b_bytes = a_bytes;
-    const size_t need = a_bytes + b_bytes + (size_t)batch * 2 * SP_MG_CHUNKS * 8 * sizeof(unsigned);  // + presence masks
-    if (net->act_bytes < need) {
-        if (net->act) {  // the previous forward (any context, any stream) may still read them
-            if (net->used) MV_HIP_TRY(hipEventSynchronize(net->done));
-            MV_HIP_TRY(hipFree(net->act));
-            net->act = nullptr;
-            net->act_bytes = 0;
-        }
-        if (hipMalloc(&net->act, need) != hipSuccess) return MV_ERR_OUT_OF_MEMORY;
-        net->act_bytes = need;
+namespace {
+// run()'s network outputs as pairwise_pnp.py receives them (outs = net.forward(inp), :197-199: the
+// quantized model's DeQuantStub): the heads' int8 codes [B][cells][C] (cell = gx * Hc + gy, the
+// Frame layout) -> code * (float) out_scale as NCHW float32 [B][C][Hc][Wc] (PyTorch's dequantise:
+// one float product, fma(scale, code, 0)).  Thread = 4 consecutive gx of one (b, c, gy): one 16-B
+// store; the int8 reads are gathers from L2 (the codes were just written).
+__global__ __launch_bounds__(256) void k_sp_dequant_nchw(const int8_t *__restrict__ codes, int C, int Hc, int Wc,
+                                                         long total4, float scale, float *__restrict__ out) {
+    const long q = (long)blockIdx.x * 256 + threadIdx.x;
+    if (q >= total4) return;
+    const int W4 = (Wc + 3) / 4;
+    const int x4 = (int)(q % W4);
+    long r = q / W4;
+    const int gy = (int)(r % Hc);
+    r /= Hc;
+    const int c = (int)(r % C);
+    const long b = r / C;
+    const long cells = (long)Hc * Wc;
+    const int8_t *src = codes + b * cells * C + c;
+    float *dst = out + ((b * C + c) * Hc + gy) * (long)Wc;
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int gx = 4 * x4 + i;
+        v[i] = gx < Wc ? scale * (float)src[((long)gx * Hc + gy) * C] : 0.f;
     }
-    int8_t *A = static_cast<int8_t *>(net->act), *Bf = A + a_bytes;
-    hipStream_t st = ctx->stream;
-    // the activations belong to the net, not the context: order this forward after the previous
-    // one on whatever stream (context) it ran (free on the same stream)
-    if (net->used) MV_HIP_TRY(hipStreamWaitEvent(st, net->done, 0));
+    if ((Wc & 3) == 0) {
+        *reinterpret_cast<float4 *>(dst + 4 * x4) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+        for (int i = 0; i < 4; i++)
+            if (4 * x4 + i < Wc) dst[4 * x4 + i] = v[i];
+    }
+}
+
+// the network on `batch` frames into the heads' int8 codes semi [B][cells][65], desc [B][cells][256]
+// (Frame layout, before run()'s min-gap step); act: the two activation buffers of a_bytes each
+int sp_network(hipStream_t st, mv_superpoint *net, int batch, int H, int W, int oh, int ow, const uint8_t *images,
+               int8_t *A, int8_t *Bf, int8_t *semi, int8_t *desc) {
     const char *wd = static_cast<const char *>(net->wdev);
     int r;
     int h = oh, w = ow;
@@ -1017,14 +1028,86 @@ extern "C" int mv_superpoint_forward_dev(mv_context *ctx, mv_superpoint *net, in
     if ((r = launch_conv<128, 3, false, true, 0>(st, net, 10, batch, h, w, Bf, A, 256)) != MV_OK) return r;
     if ((r = launch_conv1x1<1>(st, net, 11, batch, h, w, A, desc, 256)) != MV_OK) return r;
     MV_PROF_END(st);
+    return MV_OK;
+}
+
+// the net's activation buffers (grown to `need` bytes; the previous forward on any stream may
+// still read the old ones)
+int sp_act(mv_superpoint *net, size_t need) {
+    if (net->act_bytes >= need) return MV_OK;
+    if (net->act) {
+        if (net->used) MV_HIP_TRY(hipEventSynchronize(net->done));
+        MV_HIP_TRY(hipFree(net->act));
+        net->act = nullptr;
+        net->act_bytes = 0;
+    }
+    if (hipMalloc(&net->act, need) != hipSuccess) return MV_ERR_OUT_OF_MEMORY;
+    net->act_bytes = need;
+    return MV_OK;
+}
+}  // namespace
+
+extern "C" int mv_superpoint_forward_dev(mv_context *ctx, mv_superpoint *net, int batch, int H, int W, int oh,
+                                         int ow, const uint8_t *images, int8_t *semi, int8_t *desc,
+                                         float *semi_scale, float *desc_scale) {
+    MV_REQUIRE(ctx && net && batch > 0 && H > 0 && W > 0 && oh >= 8 && ow >= 8 && oh % 8 == 0 && ow % 8 == 0);
+    MV_REQUIRE(images && semi && desc && semi_scale && desc_scale && net->device == ctx->device);
+    MV_REQUIRE((long)oh * ow * 64 < (1l << 31) && (long)batch * H * W < (1l << 40));
+    MV_HIP_TRY(hipSetDevice(ctx->device));
+    // activation ping-pong buffers, oh * ow * 16 bytes per frame each (conv1b's pooled output, the
+    // largest after the fused conv1a) + the presence masks
+    const size_t a_bytes = mv::align_up((size_t)batch * oh * ow * 16, 256);
+    const size_t need = 2 * a_bytes + (size_t)batch * 2 * SP_MG_CHUNKS * 8 * sizeof(unsigned);
+    int r = sp_act(net, need);
+    if (r != MV_OK) return r;
+    int8_t *A = static_cast<int8_t *>(net->act), *Bf = A + a_bytes;
+    hipStream_t st = ctx->stream;
+    // the activations belong to the net, not the context: order this forward after the previous
+    // one on whatever stream (context) it ran (free on the same stream)
+    if (net->used) MV_HIP_TRY(hipStreamWaitEvent(st, net->done, 0));
+    if ((r = sp_network(st, net, batch, H, W, oh, ow, images, A, Bf, semi, desc)) != MV_OK) return r;
+    const int h = oh / 8, w = ow / 8;
     MV_PROF_BEGIN(st, "k_sp_min_gap");
-    unsigned *pres = reinterpret_cast<unsigned *>(Bf + b_bytes);
+    unsigned *pres = reinterpret_cast<unsigned *>(Bf + a_bytes);
     hipLaunchKernelGGL(k_sp_presence, dim3((unsigned)batch, 2, SP_MG_CHUNKS), dim3(SP_NT), 0, st, semi, desc,
                        (long)h * w, pres);
     MV_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_sp_min_gap, dim3((unsigned)batch, 2, SP_MG_CHUNKS), dim3(SP_NT), 0, st, semi, desc,
                        (long)h * w, net->dq_semi, net->dq_desc, pres, semi_scale, desc_scale);
     MV_LAUNCH_CHECK();
+    MV_PROF_END(st);
+    MV_HIP_TRY(hipEventRecord(net->done, st));
+    net->used = true;
+    return MV_OK;
+}
+
+extern "C" int mv_superpoint_forward_raw_dev(mv_context *ctx, mv_superpoint *net, int batch, int H, int W, int oh,
+                                             int ow, const uint8_t *images, float *semi, float *coarse_desc) {
+    MV_REQUIRE(ctx && net && batch > 0 && H > 0 && W > 0 && oh >= 8 && ow >= 8 && oh % 8 == 0 && ow % 8 == 0);
+    MV_REQUIRE(images && semi && coarse_desc && net->device == ctx->device);
+    MV_REQUIRE((long)oh * ow * 64 < (1l << 31) && (long)batch * H * W < (1l << 40));
+    MV_REQUIRE(((uintptr_t)semi & 15) == 0 && ((uintptr_t)coarse_desc & 15) == 0);
+    MV_HIP_TRY(hipSetDevice(ctx->device));
+    const int h = oh / 8, w = ow / 8;
+    const size_t cells = (size_t)h * w;
+    const size_t a_bytes = mv::align_up((size_t)batch * oh * ow * 16, 256);
+    const size_t c_bytes = mv::align_up((size_t)batch * cells * (65 + 256), 256);  // the heads' codes
+    int r = sp_act(net, 2 * a_bytes + c_bytes);
+    if (r != MV_OK) return r;
+    int8_t *A = static_cast<int8_t *>(net->act), *Bf = A + a_bytes;
+    int8_t *cs = Bf + a_bytes, *cd = cs + (size_t)batch * cells * 65;
+    hipStream_t st = ctx->stream;
+    if (net->used) MV_HIP_TRY(hipStreamWaitEvent(st, net->done, 0));
+    if ((r = sp_network(st, net, batch, H, W, oh, ow, images, A, Bf, cs, cd)) != MV_OK) return r;
+    MV_PROF_BEGIN(st, "k_sp_dequant_nchw");
+    const int w4 = (w + 3) / 4;
+    for (int head = 0; head < 2; head++) {
+        const int C = head ? 256 : 65;
+        const long total4 = (long)batch * C * h * w4;
+        hipLaunchKernelGGL(k_sp_dequant_nchw, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, st, head ? cd : cs,
+                           C, h, w, total4, head ? net->dq_desc : net->dq_semi, head ? coarse_desc : semi);
+        MV_LAUNCH_CHECK();
+    }
     MV_PROF_END(st);
     MV_HIP_TRY(hipEventRecord(net->done, st));
     net->used = true;

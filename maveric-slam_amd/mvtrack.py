@@ -12,7 +12,9 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmaveric_hip.so")
+# MV_LIB: an alternate in-tree build of the same library (a tracing or A/B variant built on the
+# CPU by tools/build_variant.sh); the default is the shipping build
+LIB_PATH = os.environ.get("MV_LIB") or os.path.join(HERE, "libmaveric_hip.so")
 CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 
@@ -137,6 +139,7 @@ def lib():
             "mv_superpoint_create": (_I, [_P, _P, ctypes.POINTER(_P)]),
             "mv_superpoint_destroy": (_I, [_P]),
             "mv_superpoint_forward_dev": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
+            "mv_superpoint_forward_raw_dev": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
             "mv_pose_from_matches_dev": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
             "mv_ransac_stub_host": (_I, [_P, _I, _P, _P, _F, _P, _P, _P]),
             "mv_recover_pose_host": (_I, [_P, _P, _P, _P, _P]),
@@ -765,6 +768,23 @@ class SuperPoint:
         check(lib().mv_superpoint_forward_dev((ctx or self.ctx).h, self.h, B, H, W, oh, ow, _t(images), _t(semi), _t(desc),
                                               _t(ss), _t(ds)), "superpoint_forward")
         return semi, desc, ss, ds
+
+    def forward_raw(self, images, oh=192, ow=640, out=None, ctx=None):
+        """images: torch uint8 [B][H][W] -> the network's float outputs as pairwise_pnp.py's
+        run() receives them (semi [B, 65, oh/8, ow/8], coarse_desc [B, 256, oh/8, ow/8] float32
+        NCHW: code x the head's output scale), the input of Context.keypoints"""
+        import torch
+
+        B, H, W = images.shape
+        hc, wc = oh // 8, ow // 8
+        if out is None:
+            dev = images.device
+            out = (torch.empty((B, 65, hc, wc), dtype=torch.float32, device=dev),
+                   torch.empty((B, 256, hc, wc), dtype=torch.float32, device=dev))
+        semi, cdesc = out
+        check(lib().mv_superpoint_forward_raw_dev((ctx or self.ctx).h, self.h, B, H, W, oh, ow, _t(images),
+                                                  _t(semi), _t(cdesc)), "superpoint_forward_raw")
+        return semi, cdesc
 
 
 class SuperPointFrontend:

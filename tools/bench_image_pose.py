@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""The fp32 path of python/pairwise_pnp.py:577-694 end to end on the GPU: a track of F KITTI-shape
+8-bit frames (376 x 1241, the two committed KITTI 00 frames shifted / brightness-jittered) ->
+the quantized SuperPoint network's float outputs (mv_superpoint_forward_raw_dev) -> keypoints +
+descriptors (mv_keypoints_dev, cap 1024) -> the all-pairs match of consecutive frames
+(mv_match_allpairs_f32_dev on the views desc[0:F-1], desc[1:F]) -> the pose per pair
+(mv_pose_from_matches_dev).  One step = one track of F frames; prints one JSON line: frame-pairs/s
+(image -> pose), per-stage times (HIP events) and the checked stages.  GPU only."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "maveric-slam_amd"), os.path.join(ROOT, "oracle")):
+    sys.path.insert(0, p)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import mvtrack  # noqa: E402
+import synth  # noqa: E402
+
+CAP = 1024
+
+
+def frames_kitti(F, seed=0):
+    ims = np.load(os.path.join(ROOT, "tests", "golden", "kitti00_images.npz"))
+    base = [ims["img_000000"], ims["img_000001"]]
+    rng = np.random.default_rng(seed)
+    out = []
+    for b in range(F):
+        im = np.roll(base[b % 2], shift=(b // 2) % 17, axis=1).astype(np.int16) + rng.integers(-3, 4)
+        out.append(np.clip(im, 0, 255).astype(np.uint8))
+    return out
+
+
+def run(frames=257, steps=10, warmup=2, check=1):
+    dev = torch.device("cuda", 0)
+    W = dict(np.load(os.path.join(ROOT, "tests", "golden", "superpoint_qnonorm.npz")))
+    imgs = frames_kitti(frames)
+    x = torch.from_numpy(np.stack(imgs)).to(dev)
+    F, P = frames, frames - 1
+    ctx = mvtrack.Context(0)
+    ctx.set_stream(torch.cuda.current_stream())
+    sp = mvtrack.SuperPoint(ctx, W)
+    semi = torch.empty((F, 65, 24, 80), dtype=torch.float32, device=dev)
+    cdesc = torch.empty((F, 256, 24, 80), dtype=torch.float32, device=dev)
+    nkp = torch.empty(F, dtype=torch.int32, device=dev)
+    kp = torch.zeros((F, CAP, 2), dtype=torch.float32, device=dev)
+    conf = torch.zeros((F, CAP), dtype=torch.float32, device=dev)
+    desc = torch.zeros((F, CAP, 256), dtype=torch.float32, device=dev)
+    kst = torch.empty(F, dtype=torch.int32, device=dev)
+    idx = torch.empty((P, CAP), dtype=torch.int32, device=dev)
+    K = synth.KITTI_K  # pairwise_pnp.py:667-669
+    prm = mvtrack.pose_params(mvtrack.AS_INTENDED, fx=K[0, 0], fy=K[1, 1], cx=K[0, 2], cy=K[1, 2], hypotheses=256,
+                              inlier_thresh=1.0, refine_iters=10, seed=7)
+    T = torch.empty((P, 3, 4), dtype=torch.float32, device=dev)
+    nm = torch.empty(P, dtype=torch.int32, device=dev)
+    ni = torch.empty(P, dtype=torch.int32, device=dev)
+    st = torch.empty(P, dtype=torch.int32, device=dev)
+
+    def step():
+        sp.forward_raw(x, 192, 640, out=(semi, cdesc))
+        ctx.keypoints(semi, cdesc, 192, 640, nkp, kp, conf, desc, kst)
+        ctx.match_allpairs_f32(desc[:P], desc[1:], nkp[:P], nkp[1:], idx, None, 0.8)
+        ctx.pose_from_matches(prm, nkp[:P], idx, kp[:P], kp[1:], T, nm, ni, st)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    mvtrack.profile_enable(True)
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    mvtrack.profile_enable(False)
+    stages = {}
+    for k in ("k_sp_conv", "k_sp_dequant_nchw", "k_kp_heat", "k_kp_nms", "k_kp_sample_planes", "k_kp_normalize",
+              "k_q8d_match", "k_pose_ransac"):
+        ms, c = mvtrack.profile_query(k)
+        if c:
+            stages[k] = round(ms / steps, 4)
+    res = {"metric": "image -> pose frame-pairs/sec (quantized SuperPoint + keypoints + fp32 all-pairs + pose), "
+                     "KITTI 376x1241 frames, consecutive pairs",
+           "value": round(P * steps / el, 1), "unit": "pairs/s", "frames_per_step": F, "steps": steps,
+           "ms_per_step": round(el / steps * 1e3, 4), "stages_ms_per_step": stages,
+           "keypoints_per_frame": round(float(nkp.float().mean()), 1),
+           "matches_per_pair": round(float(nm.float().mean()), 1), "pose_ok": int((st == 0).sum())}
+    if check:
+        import oracle
+
+        net = oracle.sp_net(W)
+        s_sc, d_sc = np.float32(W["convPb_meta"][2]), np.float32(W["convDb_meta"][2])
+        chain = []
+        for b in (0, 1):
+            _, _, _, _, sr, dr = oracle.sp_forward(imgs[b], net)
+            pts, dsc, _ = oracle.keypoints(s_sc * sr.astype(np.float32), d_sc * dr.astype(np.float32), 192, 640)
+            n = int(nkp[b])
+            assert n == pts.shape[0] and (kp[b, :n].cpu().numpy() == pts[:, :2]).all(), "keypoints differ"
+            chain.append(dsc)
+        i2, _ = oracle.allpairs_f32(chain[0], chain[1], 0.8)
+        assert (idx[0, :i2.shape[0]].cpu().numpy() == i2).all(), "match differs from the oracle chain"
+        res["checked_pairs"] = 1
+    sp.close()
+    ctx.close()
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=257)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--check", type=int, default=1)
+    a = ap.parse_args()
+    print(json.dumps(run(a.frames, a.steps, a.warmup, a.check)))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,5 +1,8 @@
-"""Phase timing of k_q8d_match (library built with EXTRA=-DMV_TRACE): per (block, wave)
-s_memtime stamps at entry, A phase done, sweep + statistics done, epilogue done."""
+"""Phase timing of k_q8d_match (library built with EXTRA=-DMV_TRACE, e.g. MV_LIB=
+build_variants/libmaveric_trace.so from tools/build_variant.sh trace -DMV_TRACE): per (block, wave)
+s_memtime stamps at entry, A phase done, sweep + statistics done, epilogue done.
+Env: TB pairs (8192), TN per-component noise of the re-observed rows (bench default 0.3/16;
+SURVEY C1: 0.05), TS=1 materialise the exact scores."""
 import ctypes
 import os
 import sys
@@ -14,13 +17,14 @@ import mvtrack  # noqa: E402
 
 B, n = int(os.environ.get("TB", "8192")), 1024
 dev = torch.device("cuda", 0)
-d0, d1, _, _ = bench.gen_batch(torch, dev, B, n, seed=3)
+d0, d1, _, _ = bench.gen_batch(torch, dev, B, n, seed=3, noise=float(os.environ.get("TN", 0.3 / 16)))
+sc = torch.empty((B, n), dtype=torch.float32, device=dev) if os.environ.get("TS") == "1" else None
 nn_ = torch.full((B,), n, dtype=torch.int32, device=dev)
 idx = torch.empty((B, n), dtype=torch.int32, device=dev)
 ctx = mvtrack.Context(0)
 ctx.set_stream(torch.cuda.current_stream())
 for _ in range(3):
-    ctx.match_allpairs_f32(d0, d1, nn_, nn_, idx, None)
+    ctx.match_allpairs_f32(d0, d1, nn_, nn_, idx, sc)
 torch.cuda.synchronize()
 NW = 8
 nblk = min(B * 2, 16384)
