@@ -292,10 +292,11 @@ def design_bytes_per_pair(screen, n, fused):
     return n * (KD * 4 + KD * 2 + 4 + 4)
 
 
-def pmc_traffic(kernel, B, n, screen, fused):
+def pmc_traffic(kernel, B, n, screen, fused, noise=None):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of THIS
     command: profiles/*_summary.json written by tools/profile.sh over bench.py itself (bench_args
-    without a tool script), the same batch / kp / screen / staging mode.  None when absent."""
+    without a tool script), the same batch / kp / screen / staging mode and descriptor noise
+    (None: the default noise, i.e. no --noise in the profiled arguments).  None when absent."""
     import glob
 
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")), reverse=True):
@@ -308,7 +309,8 @@ def pmc_traffic(kernel, B, n, screen, fused):
             continue
         toks = a.split()
         sc = toks[toks.index("--screen") + 1] if "--screen" in toks else "i8"
-        if sc != screen or ("--unfused" in toks) == fused or "--noise" in toks:
+        nz = float(toks[toks.index("--noise") + 1]) if "--noise" in toks else None
+        if sc != screen or ("--unfused" in toks) == fused or nz != noise:
             continue
         k = d.get("kernels", {}).get(kernel, {})
         if d.get("batch") == B and d.get("kp") == n and "hbm_bytes_per_launch" in k:
@@ -710,11 +712,14 @@ def main():
         i2, _ = oracle.allpairs_f32(e0[0].cpu().numpy(), e1[0].cpu().numpy(), 0.8)
         assert (idxs[0][0].cpu().numpy() == i2).all(), "near-threshold match differs from the oracle"
         kn_s = kn_ms / max(kn_n, 1) * 1e-3
+        tr_nt, tr_src = pmc_traffic(kmatch, B, n, screen, fused, noise=0.05)
         out["near_threshold"] = {
             "value": round(B * args.extra_steps / el, 2), "unit": "pairs/s",
             "ms_per_step": round(el / args.extra_steps * 1e3, 4), "noise": 0.05,
             kmatch + "_ms": round(kn_s * 1e3, 4),
             "hbm_frac_8d": round(algorithmic_bytes_per_pair(n) * B / kn_s / 1e9 / HBM_PEAK_GBS, 4),
+            "traffic": tr_nt, "traffic_source": tr_src,
+            "traffic_ratio": round(tr_nt / (algorithmic_bytes_per_pair(n) * B), 4) if tr_nt else None,
             "matches_per_pair": round(float(nmatches[0].sum().item()) / B, 1), "checked_pairs": 1}
         cx.set_stream(streams[0])
     if rank == 0 and world == 1 and args.extra_steps > 0:

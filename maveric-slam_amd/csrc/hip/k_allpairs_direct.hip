@@ -43,8 +43,16 @@ using namespace q8;
 
 constexpr int D_NW = 8, D_NT = 64 * D_NW, D_BM = 32 * RG * D_NW;  // 512 rows per workgroup
 constexpr int D_HROWS = 32, D_HALF = D_HROWS * KD * 4;             // one staging slot: 32 fp32 rows
+#ifndef D_PAD
+#define D_PAD 1  // int8 ring rows padded to 272 B (conflict-free, immediate-offset fragment reads)
+#endif
+// the int8 tile ring: 64 rows (columns of frame 1) of 256 codes, row stride D_RS; D_PAD: 272 B
+// (17 chunks: the 16-lane phases of a ds_read_b128 hit distinct banks, and every B-fragment address
+// is a per-lane base + a compile-time offset); else 256 B with the 16-B chunks XOR-swizzled by row
+constexpr int D_RS = D_PAD ? KD + 16 : KD;
+constexpr int D_TILE = BN * D_RS, D_SLOT = D_TILE + BN * 4;        // + the tile's 64 per-column words
 constexpr int D_OFF_RING = 3 * D_HALF;                              // 2 int8 tile slots
-constexpr int D_OFF_ROW = D_OFF_RING + 2 * SLOT;                    // [BM] float2 (|a|^2, s_a)
+constexpr int D_OFF_ROW = D_OFF_RING + 2 * D_SLOT;                  // [BM] float2 (|a|^2, s_a)
 constexpr int D_OFF_MISC = D_OFF_ROW + D_BM * 8;                    // [NW][4] per-wave statistics
 constexpr int D_LDS = D_OFF_MISC + D_NW * 16;
 constexpr int D_OFF_AIMG = 2 * D_HALF;  // A images: staging slot 2 + the ring (before the sweep)
@@ -57,6 +65,9 @@ constexpr int QS_LOAD = 1;    // the k32 step whose slot issues the quantisation
 #define D_QB 4  // A phase: frame-0 row quads in flight per wave (4 x 16-B loads per lane each)
 #endif
 constexpr float IK_MMAX = 1.003f;  // integer path: max |b_jk| allowed (RNE(x 127) stays <= 127)
+#ifndef D_CC
+#define D_CC 0  // integer path: |b_j| bounded from the codes (v_dot4) instead of summing the fp32 squares
+#endif
 
 #ifdef MV_TRACE  // phase stamps (s_memtime) per (block, wave): tools/trace_direct.py
 constexpr int D_TRACE_BLOCKS = 16384;
@@ -105,6 +116,38 @@ __device__ __forceinline__ void fold_keys(int a, int b, int sha, int shb, unsign
     m1f = __int_as_float(m1);
     m2f = __int_as_float(m2);
 }
+// sum of an int over a row's 16 lanes (every lane of the 16 ends with it)
+__device__ __forceinline__ void row16_sum_i(int &c) {
+    asm("s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_add_u32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1"
+        : "+v"(c));
+}
+// max over a row's 16 lanes (NaN-propagating when the inputs came from v_maximum3)
+__device__ __forceinline__ void row16_max(float &m) {
+    asm("s_nop 1\n\t"
+        "v_max_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1"
+        : "+v"(m));
+}
+// max(m, |a|, |b|) propagating NaN (IEEE maximum): the codes' norm bound needs no fp32 sum to see it
+__device__ __forceinline__ float absmaximum3(float m, float a, float b) {
+    float r;
+    asm("v_maximum3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+}
 __device__ __forceinline__ float vmax(float a, float b) {
     float r;
     asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
@@ -151,7 +194,19 @@ struct QHalf {
         x2 = *reinterpret_cast<const f32x4v *>(src + 512);
         x3 = *reinterpret_cast<const f32x4v *>(src + 768);
     }
+    static constexpr bool CC = IK && D_CC;  // |b_j| from the codes
     __device__ __forceinline__ void absmax() {
+        if constexpr (CC) {
+            m = absmaximum3(0.f, x0[0], x0[1]);
+            m = absmaximum3(m, x0[2], x0[3]);
+            m = absmaximum3(m, x1[0], x1[1]);
+            m = absmaximum3(m, x1[2], x1[3]);
+            m = absmaximum3(m, x2[0], x2[1]);
+            m = absmaximum3(m, x2[2], x2[3]);
+            m = absmaximum3(m, x3[0], x3[1]);
+            m = absmaximum3(m, x3[2], x3[3]);
+            return;
+        }
         m = absmax3(0.f, x0[0], x0[1]);
         m = absmax3(m, x0[2], x0[3]);
         m = absmax3(m, x1[0], x1[1]);
@@ -162,14 +217,19 @@ struct QHalf {
         m = absmax3(m, x3[2], x3[3]);
     }
     __device__ __forceinline__ void sumsq() {
+        if constexpr (CC) return;
         qa = __builtin_fmaf(x0[0], x0[0], __builtin_fmaf(x0[1], x0[1], __builtin_fmaf(x0[2], x0[2], x0[3] * x0[3])));
         qb = __builtin_fmaf(x1[0], x1[0], __builtin_fmaf(x1[1], x1[1], __builtin_fmaf(x1[2], x1[2], x1[3] * x1[3])));
         qa = __builtin_fmaf(x2[0], x2[0], __builtin_fmaf(x2[1], x2[1], __builtin_fmaf(x2[2], x2[2], __builtin_fmaf(x2[3], x2[3], qa))));
         qb = __builtin_fmaf(x3[0], x3[0], __builtin_fmaf(x3[1], x3[1], __builtin_fmaf(x3[2], x3[2], __builtin_fmaf(x3[3], x3[3], qb))));
     }
     __device__ __forceinline__ void reduce(int j, int n1, int tb) {
-        qa = qa + qb;
-        row16_max_sum(m, qa);  // qa = |b|^2 from here on
+        if constexpr (CC) {
+            row16_max(m);
+        } else {
+            qa = qa + qb;
+            row16_max_sum(m, qa);  // qa = |b|^2 from here on
+        }
         if constexpr (IK) {
             // e from m's biased exponent: [1/2, 2) -> 0, [1/4, 1/2) -> 1, below -> 2 (m q_e < 128)
             const int e = min(max(126 - (int)((__float_as_uint(m) >> 23) & 0xffu), 0), 2);
@@ -188,15 +248,24 @@ struct QHalf {
     __device__ __forceinline__ void pack23() {
         code[2] = pack4(x2[0], x2[1], x2[2], x2[3], q);
         code[3] = pack4(x3[0], x3[1], x3[2], x3[3], q);
+        if constexpr (CC) {  // |c_j|^2 of the codes; |b_j| <= s_j (|c_j| + 8) (|b_jk - c_jk s_j| <= s_j / 2)
+            int c2 = __builtin_amdgcn_sdot4(code[0], code[0], 0, false);
+            c2 = __builtin_amdgcn_sdot4(code[1], code[1], c2, false);
+            c2 = __builtin_amdgcn_sdot4(code[2], code[2], c2, false);
+            c2 = __builtin_amdgcn_sdot4(code[3], code[3], c2, false);
+            row16_sum_i(c2);
+            const float bn = s * (__builtin_amdgcn_sqrtf((float)c2) + 8.0f) * 1.0001f;  // v_sqrt: 1 ulp
+            qa = bn * bn;  // an upper bound of |b_j|^2 (the window's Bn)
+        }
     }
     __device__ __forceinline__ void store(char *rq, int hh, int t, bool live, float &smax, float &b2max, bool &bad) {
         const int r = t >> 4, sub = t & 15, row = 32 * hh + r;
-        *reinterpret_cast<i32x4 *>(rq + row * KD + ((sub ^ (row & 15)) << 4)) = code;
+        *reinterpret_cast<i32x4 *>(rq + row * D_RS + (D_PAD ? sub << 4 : (sub ^ (row & 15)) << 4)) = code;
         if constexpr (IK) {
-            if (sub == 0) reinterpret_cast<int *>(rq + TILE)[row] = sh;
-            bad = bad | (live & !((qa <= 1e30f) & (m <= IK_MMAX)));
+            if (sub == 0) reinterpret_cast<int *>(rq + D_TILE)[row] = sh;
+            bad = bad | (live & !((qa <= 1e30f) & (m <= IK_MMAX)));  // CC: m carries any NaN
         } else {
-            if (sub == 0) reinterpret_cast<float *>(rq + TILE)[row] = s;
+            if (sub == 0) reinterpret_cast<float *>(rq + D_TILE)[row] = s;
             bad = bad | (live & !((qa <= FLT_MAX) & ((m == 0.f) | ((m >= SCALE_LO) & (m <= SCALE_HI)))));
         }
         smax = vmax(smax, live ? s : 0.f);
@@ -250,8 +319,8 @@ __device__ __forceinline__ Sweep sweep(char *lds, const float *B, int n1, int t,
     if (nh > 3) dma_half(B, 3, n1, wu, chunk16, lds_base);
 
     // B fragment: column block c (0, 1), lane row 32 c + fr, k32 step s: chunk (2 s + fh)
-    const int rdb = fr * KD;
-    const int xsw = fh ^ (fr & 15);  // chunk (2 s + fh) ^ (fr & 15) = 2 s ^ xsw
+    const int rdb = fr * D_RS + (D_PAD ? fh * 16 : 0);
+    const int xsw = fh ^ (fr & 15);  // !D_PAD: chunk (2 s + fh) ^ (fr & 15) = 2 s ^ xsw
 
     i32x16 acc[RG][2];
     const float kinit = IK ? __int_as_float((int)0x80000000) : -__builtin_inff();
@@ -297,7 +366,7 @@ __device__ __forceinline__ Sweep sweep(char *lds, const float *B, int n1, int t,
     do {                                                                                     \
         const char *base = rs + rdb;                                                         \
         int xs_ = xsw;                                                                       \
-        asm volatile("" : "+v"(xs_)); /* per-use offsets: not 8 loop-invariant VGPRs */      \
+        if (!D_PAD) asm volatile("" : "+v"(xs_)); /* per-use offsets: not 8 loop-invariant VGPRs */ \
         i32x4 b0_[KD / 32], b1_[KD / 32];                                                    \
         QHalf<IK> qh_;                                                                       \
         _Pragma("unroll") for (int s_ = 0; s_ < KD / 32 + D_PF; s_++) {                      \
@@ -309,9 +378,9 @@ __device__ __forceinline__ Sweep sweep(char *lds, const float *B, int n1, int t,
             if (s_ == QS_LOAD + 5) qh_.pack23();                                             \
             if (s_ == QS_LOAD + 6) qh_.store(rq, (HH), t, (LIVE), st.smax, st.b2max, st.bad); \
             if (s_ < KD / 32) {                                                              \
-                const int ch_ = ((2 * s_) ^ xs_) * 16;                                       \
+                const int ch_ = D_PAD ? 32 * s_ : ((2 * s_) ^ xs_) * 16;                     \
                 b0_[s_] = *reinterpret_cast<const i32x4 *>(base + ch_);                      \
-                b1_[s_] = *reinterpret_cast<const i32x4 *>(base + 32 * KD + ch_);            \
+                b1_[s_] = *reinterpret_cast<const i32x4 *>(base + 32 * D_RS + ch_);          \
             }                                                                                \
             if (s_ >= D_PF) {                                                                \
                 const int m_ = s_ - D_PF;                                                    \
@@ -350,18 +419,18 @@ __device__ __forceinline__ Sweep sweep(char *lds, const float *B, int n1, int t,
         D_SYNC();  // tile t complete in its slot; staging slot of half 2t + 1 free
         const int sN = 3 - sA - sB;  // the third staging slot
         if (2 * tc + 4 < nh) dma_half(B, 2 * tc + 4, n1, wu, chunk16, lds_base + (unsigned)(sN * D_HALF));
-        const char *rs = ring + (tc & 1) * SLOT;
-        char *rq = ring + ((tc + 1) & 1) * SLOT;
+        const char *rs = ring + (tc & 1) * D_SLOT;
+        char *rq = ring + ((tc + 1) & 1) * D_SLOT;
         const char *stA = lds + sA * D_HALF, *stB = lds + sB * D_HALF;
         const bool live = tc + 1 < ntc;
         const unsigned gp_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)max(tc - 1, 0));
         D_SEG(0, 1, gp_, stA, 0, 32 * (2 * tc + 2), live);
         if constexpr (IK) {  // the key shifts of tile tc's columns
-            const int *rl_ = reinterpret_cast<const int *>(rs + TILE);
+            const int *rl_ = reinterpret_cast<const int *>(rs + D_TILE);
             sh0 = rl_[fr];
             sh1 = rl_[fr + 32];
         } else {  // the dequantisation operands of tile tc: fma(t, 2^21 s, -2^23 s)
-            const float *rl_ = reinterpret_cast<const float *>(rs + TILE);
+            const float *rl_ = reinterpret_cast<const float *>(rs + D_TILE);
             const int col_ = tc * BN + fr;
             const float s0_ = rl_[fr], s1_ = rl_[fr + 32];
             pr0 = col_ < n1 ? 2097152.0f * s0_ : 0.f;

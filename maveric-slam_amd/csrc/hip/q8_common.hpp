@@ -144,6 +144,80 @@ __device__ __forceinline__ float exact_dot(const float *__restrict__ a, const fl
     }
     return s;
 }
+#ifndef Q8_COOP
+#define Q8_COOP 1  // the deferred maximiser re-scores load their rows cooperatively (coop_exact_dots)
+#endif
+// The reference's sequential fp32 dot for the wave's 64 (row, column) pairs at once -- lane L's
+// pair: A row `arow`, B row `bcol` (< 0: none) -- with the rows' bytes loaded COOPERATIVELY: per
+// 16-float chunk, each load instruction takes 16 pairs' 64-B segments (4 lanes per segment, 16
+// segments per instruction instead of exact_dot's one 16-B piece of 64 different rows), staged
+// through the wave's own 8 KiB of LDS (`buf`: [pair][A | B][4 x 16 B], the 16-B quarters
+// XOR-swizzled by pair: at most 2-way bank conflicts), from where each lane reads its own pair's
+// chunk and adds its 16 products in order.  The next chunk's loads are in flight meanwhile.
+__device__ __forceinline__ float coop_exact_dots(const float *__restrict__ A, const float *__restrict__ B, int arow,
+                                                 int bcol, int lane, char *buf) {
+    const int q = lane & 3;
+    const float *pa[4];
+    const float *pb[4];
+    int soff[4];
+    unsigned amask = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int p = 16 * i + (lane >> 2);
+        const int r = __shfl(arow, p, 64), c = __shfl(bcol, p, 64);
+        amask |= c >= 0 ? 1u << i : 0u;
+        pa[i] = A + (size_t)(c >= 0 ? r : 0) * KD + 4 * q;
+        pb[i] = B + (size_t)(c >= 0 ? c : 0) * KD + 4 * q;
+        soff[i] = p * 128 + ((q ^ ((p >> 2) & 3)) << 4);
+    }
+    const int roff = lane * 128;
+    const int rsw = (lane >> 2) & 3;
+    float4 na[4], nb[4];  // the next chunk, in flight while this one is staged and summed
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const bool on = (amask >> i) & 1u;
+        na[i] = on ? *reinterpret_cast<const float4 *>(pa[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
+        nb[i] = on ? *reinterpret_cast<const float4 *>(pb[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float s = 0.f;
+    for (int c = 0; c < KD / 16; c++) {
+        float4 ca[4], cb[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            ca[i] = na[i];
+            cb[i] = nb[i];
+        }
+        if (c + 1 < KD / 16) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const bool on = (amask >> i) & 1u;
+                na[i] = on ? *reinterpret_cast<const float4 *>(pa[i] + 16 * (c + 1)) : make_float4(0.f, 0.f, 0.f, 0.f);
+                nb[i] = on ? *reinterpret_cast<const float4 *>(pb[i] + 16 * (c + 1)) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            *reinterpret_cast<float4 *>(buf + soff[i]) = ca[i];
+            *reinterpret_cast<float4 *>(buf + soff[i] + 64) = cb[i];
+        }
+        // a wave's LDS operations complete in order: its reads below see every lane's writes
+        float4 a4[4], b4[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            a4[j] = *reinterpret_cast<const float4 *>(buf + roff + ((j ^ rsw) << 4));
+            b4[j] = *reinterpret_cast<const float4 *>(buf + roff + 64 + ((j ^ rsw) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            s = __fadd_rn(s, __fmul_rn(a4[j].x, b4[j].x));
+            s = __fadd_rn(s, __fmul_rn(a4[j].y, b4[j].y));
+            s = __fadd_rn(s, __fmul_rn(a4[j].z, b4[j].z));
+            s = __fadd_rn(s, __fmul_rn(a4[j].w, b4[j].w));
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this chunk's reads done before the next writes
+    }
+    return bcol >= 0 ? s : 0.f;
+}
 // nn_match_two_way's distance (pairwise_pnp.py:303): sqrt(2 - 2 clip(dot, -1, 1)) in float32
 __device__ __forceinline__ float dist(float e) {
     const float c = e != e ? e : fminf(fmaxf(e, -1.f), 1.f);
@@ -428,10 +502,15 @@ __device__ __forceinline__ void epilogue(char *epi, const float2 *rowv, float (&
     {
         const int Ih = fh ? need_g[1] : need_g[0];
         float e = 0.f;
+#if Q8_COOP
+        if (__ballot(Ih >= 0))  // wave-uniform; the wave's own transpose slice is free by now
+            e = coop_exact_dots(A, B, row0 + w * 64 + fh * 32 + fr, Ih, lane, mt);
+#else
         if (Ih >= 0) {
             const float *ap = A + (size_t)(row0 + w * 64 + fh * 32 + fr) * KD;
             e = exact_dot(ap, B + (size_t)Ih * KD);
         }
+#endif
         const float eo = __shfl_xor(e, 32, 64);
         const float e0 = fh ? eo : e, e1 = fh ? e : eo;
 #pragma unroll
