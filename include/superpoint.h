@@ -63,7 +63,7 @@ int mv_superpoint_forward_dev(mv_context *ctx, mv_superpoint *net, int batch, in
  * superpoint_inference.py's min-gap quantisation): semi [B][65][oh/8][ow/8] and coarse_desc
  * [B][256][oh/8][ow/8], NCHW float32, each value the head's int8 code times its output scale
  * (PyTorch's dequantise: one float product).  The input of mv_keypoints_dev (keypoints.h) -- the
- * fp32 path image -> keypoints -> all-pairs match -> pose.  semi / coarse_desc 16-B aligned.
+ * fp32 path image -> keypoints -> all-pairs match -> pose.  semi / coarse_desc 16-B aligned; oh <= 512.
  * Ordered after the net's previous forward like mv_superpoint_forward_dev. */
 int mv_superpoint_forward_raw_dev(mv_context *ctx, mv_superpoint *net, int batch, int H, int W, int oh, int ow,
                                   const uint8_t *images, float *semi, float *coarse_desc);

@@ -66,7 +66,10 @@ constexpr int QS_LOAD = 1;    // the k32 step whose slot issues the quantisation
 #endif
 constexpr float IK_MMAX = 1.003f;  // integer path: max |b_jk| allowed (RNE(x 127) stays <= 127)
 #ifndef D_CC
-#define D_CC 0  // integer path: |b_j| bounded from the codes (v_dot4) instead of summing the fp32 squares
+// 1: integer path, |b_j| bounded from the codes (v_dot4) and NaN caught by v_maximum3 instead of
+// summing the fp32 squares (12 VALU per tile and wave fewer) -- fails the out-of-range parity test
+// (tests/test_gpu_allpairs.py::test_allpairs_f32_out_of_screen_range): experimental, off
+#define D_CC 0
 #endif
 
 #ifdef MV_TRACE  // phase stamps (s_memtime) per (block, wave): tools/trace_direct.py
@@ -158,7 +161,19 @@ __device__ __forceinline__ float vmax(float a, float b) {
 // wave w copies rows 4 w .. +3, one 1-KiB row per instruction.  Within a row, LDS position p
 // (16-B unit) holds source chunk 4 (p & 15) + (p >> 4), so that the reader below -- lane sub
 // taking positions sub + 16 i, i.e. the 16 consecutive floats 16 sub .. +15 -- is conflict-free.
+// Timing experiments (wrong results; tools/gpu_ab.sh with --check 0): D_EXP_NODMA skips the
+// sweep's LDS-DMA issue, D_EXP_NOQUANT the next tile's quantisation, D_EXP_NOFOLD the top-2 fold.
+#ifndef D_EXP_NODMA
+#define D_EXP_NODMA 0
+#endif
+#ifndef D_EXP_NOQUANT
+#define D_EXP_NOQUANT 0
+#endif
+#ifndef D_EXP_NOFOLD
+#define D_EXP_NOFOLD 0
+#endif
 __device__ __forceinline__ void dma_half(const float *B, int h, int n1, int wu, unsigned chunk16, unsigned slot) {
+    if (D_EXP_NODMA && h >= 2) return;
     const unsigned dst = slot + (unsigned)(wu * 4 * KD * 4);
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -370,13 +385,14 @@ __device__ __forceinline__ Sweep sweep(char *lds, const float *B, int n1, int t,
         i32x4 b0_[KD / 32], b1_[KD / 32];                                                    \
         QHalf<IK> qh_;                                                                       \
         _Pragma("unroll") for (int s_ = 0; s_ < KD / 32 + D_PF; s_++) {                      \
-            if (s_ == QS_LOAD) qh_.load((STG), t);                                           \
-            if (s_ == QS_LOAD + 1) qh_.absmax();                                             \
-            if (s_ == QS_LOAD + 2) qh_.sumsq();                                              \
-            if (s_ == QS_LOAD + 3) qh_.reduce((J0) + (t >> 4), n1, tb);                      \
-            if (s_ == QS_LOAD + 4) qh_.pack01();                                             \
-            if (s_ == QS_LOAD + 5) qh_.pack23();                                             \
-            if (s_ == QS_LOAD + 6) qh_.store(rq, (HH), t, (LIVE), st.smax, st.b2max, st.bad); \
+            if (D_EXP_NOQUANT) {                                                             \
+            } else if (s_ == QS_LOAD) qh_.load((STG), t);                                    \
+            else if (s_ == QS_LOAD + 1) qh_.absmax();                                        \
+            else if (s_ == QS_LOAD + 2) qh_.sumsq();                                         \
+            else if (s_ == QS_LOAD + 3) qh_.reduce((J0) + (t >> 4), n1, tb);                 \
+            else if (s_ == QS_LOAD + 4) qh_.pack01();                                        \
+            else if (s_ == QS_LOAD + 5) qh_.pack23();                                        \
+            else if (s_ == QS_LOAD + 6) qh_.store(rq, (HH), t, (LIVE), st.smax, st.b2max, st.bad); \
             if (s_ < KD / 32) {                                                              \
                 const int ch_ = D_PAD ? 32 * s_ : ((2 * s_) ^ xs_) * 16;                     \
                 b0_[s_] = *reinterpret_cast<const i32x4 *>(base + ch_);                      \
@@ -397,7 +413,10 @@ __device__ __forceinline__ Sweep sweep(char *lds, const float *B, int n1, int t,
                     acc[G][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b0_[m_], acc[G][0], 0, 0, 0); \
                     acc[G][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b1_[m_], acc[G][1], 0, 0, 0); \
                 }                                                                            \
-                D_FOLD2(FG, m_, G0);                                                         \
+                if (D_EXP_NOFOLD)                                                            \
+                    asm volatile("" : : "v"(acc[FG][0][2 * m_]), "v"(acc[FG][1][2 * m_]));  \
+                else                                                                         \
+                    D_FOLD2(FG, m_, G0);                                                     \
             }                                                                                \
             __builtin_amdgcn_sched_barrier(0);                                               \
         }                                                                                    \

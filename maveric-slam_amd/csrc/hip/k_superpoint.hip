@@ -969,33 +969,41 @@ namespace {
 // run()'s network outputs as pairwise_pnp.py receives them (outs = net.forward(inp), :197-199: the
 // quantized model's DeQuantStub): the heads' int8 codes [B][cells][C] (cell = gx * Hc + gy, the
 // Frame layout) -> code * (float) out_scale as NCHW float32 [B][C][Hc][Wc] (PyTorch's dequantise:
-// one float product, fma(scale, code, 0)).  Thread = 4 consecutive gx of one (b, c, gy): one 16-B
-// store; the int8 reads are gathers from L2 (the codes were just written).
+// one float product, fma(scale, code, 0)).  Workgroup = (frame, 4 grid columns): the columns'
+// 4 * Hc cells are CONTIGUOUS in the Frame layout (4 Hc C bytes), read with 16-B loads into LDS;
+// then thread -> (c, gy) writes the 4 columns' values as one 16-B store.
+constexpr int SP_DQ_COLS = 4;
 __global__ __launch_bounds__(256) void k_sp_dequant_nchw(const int8_t *__restrict__ codes, int C, int Hc, int Wc,
-                                                         long total4, float scale, float *__restrict__ out) {
-    const long q = (long)blockIdx.x * 256 + threadIdx.x;
-    if (q >= total4) return;
-    const int W4 = (Wc + 3) / 4;
-    const int x4 = (int)(q % W4);
-    long r = q / W4;
-    const int gy = (int)(r % Hc);
-    r /= Hc;
-    const int c = (int)(r % C);
-    const long b = r / C;
+                                                         float scale, float *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) int8_t dq_lds[];
+    const int ncb = (Wc + SP_DQ_COLS - 1) / SP_DQ_COLS;
+    const long b = blockIdx.x / ncb;
+    const int x0 = (blockIdx.x % ncb) * SP_DQ_COLS;
+    const int nx = min(SP_DQ_COLS, Wc - x0);
     const long cells = (long)Hc * Wc;
-    const int8_t *src = codes + b * cells * C + c;
-    float *dst = out + ((b * C + c) * Hc + gy) * (long)Wc;
-    float v[4];
+    const int8_t *src = codes + (b * cells + (long)x0 * Hc) * C;
+    const int nbytes = nx * Hc * C;  // contiguous
+    const int t = threadIdx.x;
+    // 16-B pieces while aligned, the tail byte by byte (C = 65 rows are not 16-B multiples)
+    const int head = (int)((16 - ((uintptr_t)src & 15)) & 15);
+    for (int i = t; i < min(head, nbytes); i += 256) dq_lds[i] = src[i];
+    const int body = max(nbytes - head, 0) / 16;
+    for (int i = t; i < body; i += 256)
+        *reinterpret_cast<int4 *>(dq_lds + head + 16 * i) = *reinterpret_cast<const int4 *>(src + head + 16 * i);
+    for (int i = head + 16 * body + t; i < nbytes; i += 256) dq_lds[i] = src[i];
+    __syncthreads();
+    float *dst = out + b * C * cells;
+    for (int q = t; q < C * Hc; q += 256) {
+        const int c = q / Hc, gy = q % Hc;
+        float v[SP_DQ_COLS];
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const int gx = 4 * x4 + i;
-        v[i] = gx < Wc ? scale * (float)src[((long)gx * Hc + gy) * C] : 0.f;
-    }
-    if ((Wc & 3) == 0) {
-        *reinterpret_cast<float4 *>(dst + 4 * x4) = make_float4(v[0], v[1], v[2], v[3]);
-    } else {
-        for (int i = 0; i < 4; i++)
-            if (4 * x4 + i < Wc) dst[4 * x4 + i] = v[i];
+        for (int i = 0; i < SP_DQ_COLS; i++) v[i] = i < nx ? scale * (float)dq_lds[(i * Hc + gy) * C + c] : 0.f;
+        float *o = dst + ((long)c * Hc + gy) * Wc + x0;
+        if (nx == SP_DQ_COLS && (((uintptr_t)o & 15) == 0)) {
+            *reinterpret_cast<float4 *>(o) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+            for (int i = 0; i < nx; i++) o[i] = v[i];
+        }
     }
 }
 
@@ -1100,12 +1108,12 @@ extern "C" int mv_superpoint_forward_raw_dev(mv_context *ctx, mv_superpoint *net
     if (net->used) MV_HIP_TRY(hipStreamWaitEvent(st, net->done, 0));
     if ((r = sp_network(st, net, batch, H, W, oh, ow, images, A, Bf, cs, cd)) != MV_OK) return r;
     MV_PROF_BEGIN(st, "k_sp_dequant_nchw");
-    const int w4 = (w + 3) / 4;
+    const long nblk = (long)batch * ((w + SP_DQ_COLS - 1) / SP_DQ_COLS);
+    MV_REQUIRE(nblk < (1l << 31) && (size_t)SP_DQ_COLS * h * 256 <= 64 * 1024);
     for (int head = 0; head < 2; head++) {
         const int C = head ? 256 : 65;
-        const long total4 = (long)batch * C * h * w4;
-        hipLaunchKernelGGL(k_sp_dequant_nchw, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, st, head ? cd : cs,
-                           C, h, w, total4, head ? net->dq_desc : net->dq_semi, head ? coarse_desc : semi);
+        hipLaunchKernelGGL(k_sp_dequant_nchw, dim3((unsigned)nblk), dim3(256), (size_t)SP_DQ_COLS * h * C, st,
+                           head ? cd : cs, C, h, w, head ? net->dq_desc : net->dq_semi, head ? coarse_desc : semi);
         MV_LAUNCH_CHECK();
     }
     MV_PROF_END(st);

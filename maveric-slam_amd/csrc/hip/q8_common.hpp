@@ -145,7 +145,11 @@ __device__ __forceinline__ float exact_dot(const float *__restrict__ a, const fl
     return s;
 }
 #ifndef Q8_COOP
-#define Q8_COOP 1  // the deferred maximiser re-scores load their rows cooperatively (coop_exact_dots)
+// 1: the deferred maximiser re-scores load their rows cooperatively (coop_exact_dots).  Measured
+// (tools/gpu_trace_exp.sh, SURVEY C1 noise): epilogue 47.5 k cycles per wave against 43.0 k for the
+// per-lane exact_dot -- the re-scores are bound by bytes in flight (one 8-KiB chunk per wave here,
+// 32 KiB in exact_dot's batches), not by the L1's line rate; kept as a switch, off
+#define Q8_COOP 0
 #endif
 // The reference's sequential fp32 dot for the wave's 64 (row, column) pairs at once -- lane L's
 // pair: A row `arow`, B row `bcol` (< 0: none) -- with the rows' bytes loaded COOPERATIVELY: per
