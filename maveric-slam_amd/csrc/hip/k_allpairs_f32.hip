@@ -734,6 +734,33 @@ int launch_allpairs_f32_match(hipStream_t s, void *scratch, int batch, int cap, 
 
 }  // namespace mv
 
+namespace mv {
+void *q8d_exchange(mv_context *ctx, int batch, int cap, size_t *bytes) {
+    const size_t need = allpairs_q8d_xch_bytes(batch, cap);
+    *bytes = need;
+    if (!need) return nullptr;
+    if (need <= ctx->xch_bytes) {
+        *bytes = ctx->xch_bytes;
+        return ctx->xch;
+    }
+    if (ctx->xch) {
+        (void)quiesce(ctx);  // growing: nothing of this context may still use the old buffer
+        (void)hipFree(ctx->xch);
+        ctx->xch = nullptr;
+        ctx->xch_bytes = 0;
+    }
+    const size_t b = align_up(need, 1 << 20);
+    if (hipMalloc(&ctx->xch, b) != hipSuccess) {
+        set_error(MV_ERR_OUT_OF_MEMORY, "all-pairs exchange allocation of %zu bytes failed", b);
+        ctx->xch = nullptr;
+        return nullptr;
+    }
+    ctx->xch_bytes = b;
+    *bytes = b;
+    return ctx->xch;
+}
+}  // namespace mv
+
 namespace {
 void *ap_scratch(mv_context *ctx, size_t bytes) {
     if (bytes <= ctx->ap_scratch_bytes) return ctx->ap_scratch;
@@ -762,13 +789,18 @@ int ap_prepare(int screen, hipStream_t s, void *scr, int batch, int cap, const i
     return screen == MV_SCREEN_F16 ? mv::launch_allpairs_f32_prepare(s, scr, batch, cap, n1, desc1)
                                    : mv::launch_allpairs_q8_prepare(s, scr, batch, cap, n1, desc1);
 }
-// the match; MV_SCREEN_I8 reads both fp32 frames directly (no image, scr unused)
-int ap_match(int screen, hipStream_t s, void *scr, int batch, int cap, const int *n0, const int *n1,
+// the match; MV_SCREEN_I8 reads both fp32 frames directly (no image, scr unused; the context's
+// pair-exchange buffer)
+int ap_match(mv_context *ctx, int screen, hipStream_t s, void *scr, int batch, int cap, const int *n0, const int *n1,
              const float *desc0, const float *desc1, double thresh, int *match_idx, float *match_score,
              int dmode = 0) {
-    if (screen == MV_SCREEN_I8)
+    if (screen == MV_SCREEN_I8) {
+        size_t xb = 0;
+        void *x = mv::q8d_exchange(ctx, batch, cap, &xb);
+        if (!x && xb) return MV_ERR_OUT_OF_MEMORY;
         return mv::launch_allpairs_q8d_match(s, batch, cap, n0, n1, desc0, desc1, thresh, match_idx, match_score,
-                                             dmode);
+                                             dmode, x, xb);
+    }
     return screen == MV_SCREEN_F16
                ? mv::launch_allpairs_f32_match(s, scr, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
                                                match_score, dmode)
@@ -783,7 +815,7 @@ extern "C" int mv_match_allpairs_f32_dev(mv_context *ctx, int batch, int cap, co
     MV_REQUIRE(ctx != nullptr && batch > 0 && cap > 0);
     MV_HIP_TRY(hipSetDevice(ctx->device));
     if (ctx->ap_screen == MV_SCREEN_I8)  // one pass, no image
-        return ap_match(ctx->ap_screen, ctx->stream, nullptr, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
+        return ap_match(ctx, ctx->ap_screen, ctx->stream, nullptr, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
                         match_score);
     void *scr = ap_scratch(ctx, mv::ap_image_bytes(ctx->ap_screen, batch, cap));
     if (!scr) return MV_ERR_OUT_OF_MEMORY;
@@ -791,7 +823,7 @@ extern "C" int mv_match_allpairs_f32_dev(mv_context *ctx, int batch, int cap, co
     if (ctx->aux_stream) MV_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_prep, 0));  // a staging in flight
     const int st = ap_prepare(ctx->ap_screen, ctx->stream, scr, batch, cap, n1, desc1);
     if (st != MV_OK) return st;
-    return ap_match(ctx->ap_screen, ctx->stream, scr, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
+    return ap_match(ctx, ctx->ap_screen, ctx->stream, scr, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
                     match_score);
 }
 
@@ -841,7 +873,7 @@ extern "C" int mv_match_allpairs_f32_run_dev(mv_context *ctx, int batch, int cap
     }
     MV_HIP_TRY(hipSetDevice(ctx->device));
     if (ctx->prep_staged && ctx->aux_stream) MV_HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_prep, 0));
-    return ap_match(ctx->ap_screen, ctx->stream, ctx->ap_scratch, batch, cap, n0, n1, desc0, desc1, thresh,
+    return ap_match(ctx, ctx->ap_screen, ctx->stream, ctx->ap_scratch, batch, cap, n0, n1, desc0, desc1, thresh,
                     match_idx, match_score);
 }
 
@@ -891,7 +923,7 @@ extern "C" int mv_match_allpairs_f32_run_prepare_dev(mv_context *ctx, int batch,
     }
     MV_HIP_TRY(hipSetDevice(ctx->device));
     if (ctx->ap_screen == MV_SCREEN_I8) {  // one pass: nothing to stage for the next batch
-        const int st = ap_match(ctx->ap_screen, ctx->stream, nullptr, batch, cap, n0, n1, desc0, desc1, thresh,
+        const int st = ap_match(ctx, ctx->ap_screen, ctx->stream, nullptr, batch, cap, n0, n1, desc0, desc1, thresh,
                                 match_idx, match_score);
         if (st != MV_OK) return st;
         ctx->prep_batch = next_batch;
@@ -910,7 +942,7 @@ extern "C" int mv_match_allpairs_f32_run_prepare_dev(mv_context *ctx, int batch,
                                                   thresh, match_idx, match_score, 0, ctx->ap_scratch2, next_batch,
                                                   next_cap, next_n1, next_desc1);
     } else {  // the fp16 screen: the two kernels in stream order
-        st = ap_match(ctx->ap_screen, ctx->stream, ctx->ap_scratch, batch, cap, n0, n1, desc0, desc1, thresh,
+        st = ap_match(ctx, ctx->ap_screen, ctx->stream, ctx->ap_scratch, batch, cap, n0, n1, desc0, desc1, thresh,
                       match_idx, match_score);
         if (st == MV_OK)
             st = ap_prepare(ctx->ap_screen, ctx->stream, ctx->ap_scratch2, next_batch, next_cap, next_n1, next_desc1);
@@ -964,10 +996,10 @@ extern "C" int mv_match_two_way_f32_dev(mv_context *ctx, int batch, int cap, con
     hipStream_t s = ctx->stream;
     // forward: rows of frame 0 against frame 1 (argmin distance + its exact distance)
     int st = sc == MV_SCREEN_I8 ? MV_OK : ap_prepare(sc, s, scr, batch, cap, n1, desc1);
-    if (st == MV_OK) st = ap_match(sc, s, scr, batch, cap, n0, n1, desc0, desc1, 0.0, match_idx, fdist, 1);
+    if (st == MV_OK) st = ap_match(ctx, sc, s, scr, batch, cap, n0, n1, desc0, desc1, 0.0, match_idx, fdist, 1);
     // reverse: rows of frame 1 against frame 0 (indices only)
     if (st == MV_OK && sc != MV_SCREEN_I8) st = ap_prepare(sc, s, scr, batch, cap, n0, desc0);
-    if (st == MV_OK) st = ap_match(sc, s, scr, batch, cap, n1, n0, desc1, desc0, 0.0, ridx, nullptr, 1);
+    if (st == MV_OK) st = ap_match(ctx, sc, s, scr, batch, cap, n1, n0, desc1, desc0, 0.0, ridx, nullptr, 1);
     if (st != MV_OK) return st;
     const long total = (long)batch * cap;
     hipLaunchKernelGGL(k_two_way_keep, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, total, cap, n0, n1,

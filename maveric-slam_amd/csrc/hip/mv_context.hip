@@ -181,6 +181,7 @@ int mv_context_destroy(mv_context *ctx) {
     if (ctx->scratch) (void)hipFree(ctx->scratch);
     if (ctx->ap_scratch) (void)hipFree(ctx->ap_scratch);
     if (ctx->ap_scratch2) (void)hipFree(ctx->ap_scratch2);
+    if (ctx->xch) (void)hipFree(ctx->xch);
     if (ctx->stage_dev) (void)hipFree(ctx->stage_dev);
     (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
@@ -193,6 +194,11 @@ int mv_context_set_stream(mv_context *ctx, void *s) {
         MV_HIP_TRY(hipSetDevice(ctx->device));
         const int r = mv::retire_stream(ctx, ctx->stream);
         if (r != MV_OK) return r;
+        // the new stream also orders after the old one: the context's buffers (scratch, the
+        // pair exchange) are reused by its next launch
+        if (!ctx->ev_retire) MV_HIP_TRY(hipEventCreateWithFlags(&ctx->ev_retire, hipEventDisableTiming));
+        MV_HIP_TRY(hipEventRecord(ctx->ev_retire, ctx->stream));
+        MV_HIP_TRY(hipStreamWaitEvent((hipStream_t)s, ctx->ev_retire, 0));
     }
     ctx->stream = (hipStream_t)s;  // NULL is HIP's null stream (torch's default stream), not "unset"
     return MV_OK;
@@ -255,6 +261,10 @@ int mv_context_reserve(mv_context *ctx, int batch, int cap) {
         const size_t ab = mv::align_up(img, 1 << 20);
         if (hipMalloc(&ctx->ap_scratch2, ab) != hipSuccess) return MV_ERR_OUT_OF_MEMORY;
         ctx->ap_scratch2_bytes = ab;
+    }
+    if (ctx->ap_screen == MV_SCREEN_I8) {  // the one-pass screen's pair exchange
+        size_t xb = 0;
+        if (!mv::q8d_exchange(ctx, batch, cap, &xb) && xb) return MV_ERR_OUT_OF_MEMORY;
     }
     size_t need = mv::allpairs_i8_scratch_bytes(batch, cap);
     size_t b;

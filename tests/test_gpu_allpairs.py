@@ -484,3 +484,33 @@ def test_allpairs_f32_full_size_survey_c1_noise(ctx, screen, orc, torch_cuda, sc
         if scores:
             assert (bits(sc[b]) == bits(s2)).all()
         assert 30 < (i2 >= 0).sum() < 500  # near the threshold: a minority of the re-observed rows pass
+
+
+def test_allpairs_f32_pair_exchange(ctx, screen, orc, torch_cuda):
+    """The one-pass kernel's pair exchange (k_allpairs_direct.hip sweep_x: a pair's two 512-row
+    blocks each quantise half of every frame-1 tile and hand the codes to each other) runs when
+    both blocks of a pair are live: cap in (512, 1024], n0 > 512, n1 > 128.  Mixed in one batch:
+    the smallest exchanging frame 1 (3 tiles), partial last tiles, n0 just past one block, pairs
+    that do not exchange (n0 <= 512, n1 <= 128), a pair whose frame 1 leaves the integer keys'
+    range (both blocks must take the float sweep together: the range flag of the partner's half
+    arrives with its final statistics) and one with a NaN in the partner's half of a late tile.
+    Indices and exact scores against the oracle, with and without scores."""
+    rng = np.random.default_rng(77)
+    shapes = [(513, 129), (1024, 1024), (700, 191), (600, 1000), (1000, 193), (512, 1024), (900, 128),
+              (1024, 257), (777, 1024), (1024, 1023)]
+    pairs = []
+    for k, (x, y) in enumerate(shapes):
+        p = synth.synth_pair_f32(300 + k, n=x, n1=y, noise=0.2)
+        pairs.append((p["desc0"], p["desc1"].copy()))
+    pairs[7][1][200, 17] = np.float32(1.5)  # outside +-1.003: the whole pair on the float sweep
+    pairs[8][1][64 * 9 + 40, 5] = np.nan  # rows 32 .. 63 of tile 9: the second block's half
+    for scores in (True, False):
+        idx, sc = run_f32(ctx, torch_cuda, pairs, cap=1024, scores=scores)
+        for k, (a, c) in enumerate(pairs):
+            i2, s2 = orc.allpairs_f32(a, c, 0.8)
+            n0 = a.shape[0]
+            assert (idx[k, :n0] == i2).all(), (k, scores)
+            assert (idx[k, n0:] == -1).all(), k
+            if scores:
+                assert (bits(sc[k, :n0]) == bits(s2)).all(), k
+            assert (i2 >= 0).sum() > min(n0, c.shape[0]) // 4, k
