@@ -66,6 +66,9 @@ constexpr int QS_LOAD = 1;    // the k32 step whose slot issues the quantisation
 #define D_QB 4  // A phase: frame-0 row quads in flight per wave (4 x 16-B loads per lane each)
 #endif
 constexpr float IK_MMAX = 1.003f;  // integer path: max |b_jk| allowed (RNE(x 127) stays <= 127)
+#ifndef D_PKQ
+#define D_PKQ 0  // frame-1 quantisation's FMAs (|b|^2, the RNE scalings) two at a time (v_pk_fma_f32)
+#endif
 #ifndef D_CC
 // 1: integer path, |b_j| bounded from the codes (v_dot4) and NaN caught by v_maximum3 instead of
 // summing the fp32 squares (12 VALU per tile and wave fewer) -- fails the out-of-range parity test
@@ -73,10 +76,13 @@ constexpr float IK_MMAX = 1.003f;  // integer path: max |b_jk| allowed (RNE(x 12
 #define D_CC 0
 #endif
 
+#ifndef D_SKEW
+#define D_SKEW 0
+#endif
 #ifdef MV_TRACE  // phase stamps (s_memtime) per (block, wave): tools/trace_direct.py
 constexpr int D_TRACE_BLOCKS = 16384;
 __device__ unsigned long long g_d_trace[D_TRACE_BLOCKS * D_NW * 10];
-#define D_STAMP(K) do { __builtin_amdgcn_sched_barrier(0); ts_[K] = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
+#define D_STAMP(K) do { __builtin_amdgcn_sched_barrier(0); ts_[K] = __builtin_amdgcn_s_memtime(); if ((K) < 2) ts_[4 + (K)] = __builtin_amdgcn_s_memrealtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
 #define D_SYNC() __syncthreads()
 #else
 #define D_STAMP(K) do { } while (0)
@@ -243,6 +249,19 @@ struct QHalf {
     }
     __device__ __forceinline__ void sumsq() {
         if constexpr (CC) return;
+        if constexpr (D_PKQ) {  // |b|^2 in two lanes of v_pk_fma_f32 (any order: the window's Bn carries 1e-4)
+            f32x2v s2 = pk_fma_sq(f32x2v{x0[0], x0[1]}, f32x2v{0.f, 0.f});
+            s2 = pk_fma_sq(f32x2v{x0[2], x0[3]}, s2);
+            s2 = pk_fma_sq(f32x2v{x1[0], x1[1]}, s2);
+            s2 = pk_fma_sq(f32x2v{x1[2], x1[3]}, s2);
+            s2 = pk_fma_sq(f32x2v{x2[0], x2[1]}, s2);
+            s2 = pk_fma_sq(f32x2v{x2[2], x2[3]}, s2);
+            s2 = pk_fma_sq(f32x2v{x3[0], x3[1]}, s2);
+            s2 = pk_fma_sq(f32x2v{x3[2], x3[3]}, s2);
+            qa = s2[0];
+            qb = s2[1];
+            return;
+        }
         qa = __builtin_fmaf(x0[0], x0[0], __builtin_fmaf(x0[1], x0[1], __builtin_fmaf(x0[2], x0[2], x0[3] * x0[3])));
         qb = __builtin_fmaf(x1[0], x1[0], __builtin_fmaf(x1[1], x1[1], __builtin_fmaf(x1[2], x1[2], x1[3] * x1[3])));
         qa = __builtin_fmaf(x2[0], x2[0], __builtin_fmaf(x2[1], x2[1], __builtin_fmaf(x2[2], x2[2], __builtin_fmaf(x2[3], x2[3], qa))));
@@ -267,12 +286,22 @@ struct QHalf {
         }
     }
     __device__ __forceinline__ void pack01() {
+        if constexpr (D_PKQ) {
+            code[0] = pack4_pk(x0, f32x2v{q, MAGIC_RNE});
+            code[1] = pack4_pk(x1, f32x2v{q, MAGIC_RNE});
+            return;
+        }
         code[0] = pack4(x0[0], x0[1], x0[2], x0[3], q);
         code[1] = pack4(x1[0], x1[1], x1[2], x1[3], q);
     }
     __device__ __forceinline__ void pack23() {
-        code[2] = pack4(x2[0], x2[1], x2[2], x2[3], q);
-        code[3] = pack4(x3[0], x3[1], x3[2], x3[3], q);
+        if constexpr (D_PKQ) {
+            code[2] = pack4_pk(x2, f32x2v{q, MAGIC_RNE});
+            code[3] = pack4_pk(x3, f32x2v{q, MAGIC_RNE});
+        } else {
+            code[2] = pack4(x2[0], x2[1], x2[2], x2[3], q);
+            code[3] = pack4(x3[0], x3[1], x3[2], x3[3], q);
+        }
         if constexpr (CC) {  // |c_j|^2 of the codes; |b_j| <= s_j (|c_j| + 8) (|b_jk - c_jk s_j| <= s_j / 2)
             int c2 = __builtin_amdgcn_sdot4(code[0], code[0], 0, false);
             c2 = __builtin_amdgcn_sdot4(code[1], code[1], c2, false);
@@ -903,6 +932,12 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, con
     const int n0 = min(max(n0v[pair], 0), cap), n1 = min(max(n1v[pair], 0), cap);
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int row0 = tr * D_BM;
+    if (D_SKEW > 0 && blockIdx.x < 256 && ((blockIdx.x >> 4) & 1)) {
+        // timing experiment: the first dispatch wave's odd pairs (both blocks) start D_SKEW x 10 ns
+        // late, so that half of the CUs run their A phase while the other half sweeps
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)D_SKEW) __builtin_amdgcn_s_sleep(16);
+    }
     int *oidx = match_idx + (size_t)pair * cap + row0;
     float *oscore = match_score ? match_score + (size_t)pair * cap + row0 : nullptr;  // null: indices only
     if (row0 + t < cap && (row0 + t >= n0 || n1 <= 0)) {  // rows in [n0, cap): no match
@@ -965,7 +1000,7 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, con
 #ifdef MV_TRACE
             if (lane == 0 && blockIdx.x < D_TRACE_BLOCKS) {
                 unsigned long long *o = g_d_trace + ((size_t)blockIdx.x * D_NW + w) * 10;
-                for (int k = 0; k < 4; k++) o[k] = ts_[k];
+                for (int k = 0; k < 6; k++) o[k] = ts_[k];  // memtime x 4, memrealtime at entry / after A
                 o[6] = __smid();
                 o[7] = __builtin_amdgcn_s_memrealtime();
                 o[9] = ts_[9];

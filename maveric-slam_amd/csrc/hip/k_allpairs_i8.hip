@@ -152,7 +152,7 @@ __device__ __forceinline__ void fold3_i8(float a, float b, float &m1, float &m2)
 }
 
 #ifndef I8_PK
-#define I8_PK 1  // the fold's dequantising FMAs two at a time (v_pk_fma_f32)
+#define I8_PK 0  // 1: the fold's dequantising FMAs two at a time (v_pk_fma_f32)
 #endif
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 // (x, y) * r + c for two accumulator values of one column (both products exact inside the fma);

@@ -121,6 +121,28 @@ __device__ __forceinline__ int pack4(float x0, float x1, float x2, float x3, flo
     return (int)__builtin_amdgcn_perm(p23, p01, 0x05040100u);
 }
 
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+// two lanes of x * qm.x + qm.y (one v_pk_fma_f32: src1 / src2 broadcast from the pair's halves)
+__device__ __forceinline__ f32x2v pk_fma_bcast(f32x2v x, f32x2v qm) {
+    f32x2v d;
+    asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(d) : "v"(x), "v"(qm));
+    return d;
+}
+// two lanes of x * x + acc
+__device__ __forceinline__ f32x2v pk_fma_sq(f32x2v x, f32x2v acc) {
+    f32x2v d;
+    asm("v_pk_fma_f32 %0, %1, %1, %2" : "=v"(d) : "v"(x), "v"(acc));
+    return d;
+}
+// pack4 with the four RNE scalings as two v_pk_fma_f32 (the same fma per value: same codes)
+__device__ __forceinline__ int pack4_pk(f32x4v x, f32x2v qm) {
+    const f32x2v f01 = pk_fma_bcast(f32x2v{x[0], x[1]}, qm);
+    const f32x2v f23 = pk_fma_bcast(f32x2v{x[2], x[3]}, qm);
+    const unsigned p01 = __builtin_amdgcn_perm(__float_as_uint(f01[1]), __float_as_uint(f01[0]), 0x0c0c0400u);
+    const unsigned p23 = __builtin_amdgcn_perm(__float_as_uint(f23[1]), __float_as_uint(f23[0]), 0x0c0c0400u);
+    return (int)__builtin_amdgcn_perm(p23, p01, 0x05040100u);
+}
+
 // The reference's sequential fp32 dot (mul then add, k = 0..255), 4 load batches per operand.
 __device__ __forceinline__ float exact_dot(const float *__restrict__ a, const float *__restrict__ b) {
     constexpr int U = 16;

@@ -54,3 +54,25 @@ rt = tr[:, 0, 7]
 a, b = o[0], o[-1]
 if rt[b] != rt[a]:
     print("SCLK over the CU's run: %.3f GHz" % ((st[b, 0, 3] - st[a, 0, 3]) / ((rt[b] - rt[a]) / 100e6) / 1e9))
+# chip-wide phase concurrency over real time (s_memrealtime, 100 MHz, one clock for the chip):
+# per 1-us bin, how many blocks are in their A phase and how many in sweep + epilogue -- a
+# convoy (every CU loading frame 0 at once, HBM-bound, then every CU sweeping) shows as A-phase
+# counts near the CU count alternating with near zero
+r0, rA, rE = tr[:, 0, 4], tr[:, 0, 5], tr[:, 0, 7]
+if (r0 > 0).all():
+    t0 = r0.min()
+    nb = int((rE.max() - t0) // 100) + 1
+    a_cnt = np.zeros(nb)
+    s_cnt = np.zeros(nb)
+    for b in range(nblk):
+        i0, i1, i2 = (r0[b] - t0) // 100, (rA[b] - t0) // 100, (rE[b] - t0) // 100
+        a_cnt[i0:i1 + 1] += 1
+        s_cnt[i1 + 1:i2 + 1] += 1
+    mid = slice(nb // 5, 4 * nb // 5)
+    av = a_cnt[mid]
+    print("A-phase blocks in flight per us (middle 60%% of the launch): mean %.1f, p10 %.0f, p50 %.0f, p90 %.0f, "
+          "max %.0f; sweep+epilogue mean %.1f" % (av.mean(), np.percentile(av, 10), np.percentile(av, 50),
+                                                  np.percentile(av, 90), av.max(), s_cnt[mid].mean()))
+    print("A-phase real time per block: median %.2f us, sweep+epilogue %.2f us; launch %.1f us" % (
+        np.median(rA - r0) / 100, np.median(rE - rA) / 100, (rE.max() - t0) / 100))
+    print("A-phase counts, first 120 us:", " ".join("%d" % x for x in a_cnt[:120]))
