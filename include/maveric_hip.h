@@ -65,7 +65,9 @@ int mv_device_count(void);              /* 0 when no HIP device is visible */
 int mv_context_create(int device, mv_context **out);
 int mv_context_destroy(mv_context *ctx);
 /* Every later call runs on `hip_stream`; NULL is HIP's null (legacy default) stream, which is
- * what torch.cuda.current_stream() is until another stream is made current. */
+ * what torch.cuda.current_stream() is until another stream is made current.  The new stream is
+ * made to wait for the work already issued on the old one (the context's buffers -- scratch, the
+ * all-pairs pair-exchange buffer -- are reused by the next launch). */
 int mv_context_set_stream(mv_context *ctx, void *hip_stream);
 int mv_context_use_own_stream(mv_context *ctx); /* back to the context's own non-blocking stream */
 void *mv_context_stream(mv_context *ctx);

@@ -62,6 +62,9 @@ static_assert(epi_bytes<D_NW>() <= D_OFF_ROW, "the epilogue fits staging + ring"
 static_assert(D_LDS <= 160 * 1024, "one workgroup per CU");
 constexpr int D_PF = 1;       // k32 steps of B fragments read ahead of the MFMAs
 constexpr int QS_LOAD = 1;    // the k32 step whose slot issues the quantisation's staging reads
+#ifndef D_APIPE
+#define D_APIPE 0  // 1: the A phase software-pipelined (a_phase_pipe: the next 4 row quads' loads in flight)
+#endif
 #ifndef D_QB
 #define D_QB 4  // A phase: frame-0 row quads in flight per wave (4 x 16-B loads per lane each)
 #endif
@@ -972,8 +975,11 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, con
     dma_half(B, xmode ? tr : 0, n1, wu, chunk16, lds_base);
     dma_half(B, xmode ? 2 + tr : 1, n1, wu, chunk16, lds_base + D_HALF);
     i32x4 aI[RG][KD / 32];
-    a_phase<false, D_QB>(lds + D_OFF_AIMG + w * 32 * KD, rowv, w * 64, row0, n0, lane, A, nullptr, nullptr, nullptr,
-                         false, aI);
+    if (D_APIPE)
+        a_phase_pipe(lds + D_OFF_AIMG + w * 32 * KD, rowv, w * 64, row0, n0, lane, A, aI);
+    else
+        a_phase<false, D_QB>(lds + D_OFF_AIMG + w * 32 * KD, rowv, w * 64, row0, n0, lane, A, nullptr, nullptr,
+                             nullptr, false, aI);
     D_STAMP(1);
     __syncthreads();  // the A images (staging slot 2 + the ring) are consumed
     float m1[RG][16], m2[RG][16];
