@@ -596,7 +596,7 @@ __device__ __forceinline__ Sweep block_stats(Sweep st, float *misc, int w, int l
 // statistics the block recomputes them from frame 1.  Slower, never wrong, never waiting on a
 // block that may not be resident.
 #ifndef D_XCH
-#define D_XCH 1  // 0: the launcher never passes an exchange buffer (every pair as before)
+#define D_XCH 0  // 1: the pair exchange (allpairs_q8d_xch_bytes > 0); 0: every block quantises all of frame 1
 #endif
 constexpr int XR = 3;                       // exchange slots per block
 constexpr int X_SLOT = 32 * D_RS;           // 32 ring rows
