@@ -52,7 +52,10 @@ constexpr int D_HROWS = 32, D_HALF = D_HROWS * KD * 4;             // one stagin
 constexpr int D_RS = D_PAD ? KD + 16 : KD;
 constexpr int D_TILE = BN * D_RS, D_SLOT = D_TILE + BN * 4;        // + the tile's 64 per-column words
 constexpr int D_OFF_RING = 3 * D_HALF;                              // 2 int8 tile slots
-constexpr int D_OFF_ROW = D_OFF_RING + 2 * D_SLOT;                  // [BM] float2 (|a|^2, s_a)
+// [BM] float2 (|a|^2, s_a), past the int8 ring of either sweep (the pair exchange's: 4 slots of
+// 64 padded rows after 2 staging slots)
+constexpr int D_OFF_ROW = D_OFF_RING + 2 * D_SLOT > 2 * D_HALF + 4 * BN * D_RS ? D_OFF_RING + 2 * D_SLOT
+                                                                                : 2 * D_HALF + 4 * BN * D_RS;
 constexpr int D_OFF_MISC = D_OFF_ROW + D_BM * 8;                    // [NW][4] per-wave statistics
 constexpr int D_OFF_X = D_OFF_MISC + D_NW * 16;                     // pair exchange: flags, SOLO, statistics
 constexpr int D_LDS = D_OFF_X + 64;
@@ -62,16 +65,10 @@ static_assert(epi_bytes<D_NW>() <= D_OFF_ROW, "the epilogue fits staging + ring"
 static_assert(D_LDS <= 160 * 1024, "one workgroup per CU");
 constexpr int D_PF = 1;       // k32 steps of B fragments read ahead of the MFMAs
 constexpr int QS_LOAD = 1;    // the k32 step whose slot issues the quantisation's staging reads
-#ifndef D_APIPE
-#define D_APIPE 0  // 1: the A phase software-pipelined (a_phase_pipe: the next 4 row quads' loads in flight)
-#endif
 #ifndef D_QB
 #define D_QB 4  // A phase: frame-0 row quads in flight per wave (4 x 16-B loads per lane each)
 #endif
 constexpr float IK_MMAX = 1.003f;  // integer path: max |b_jk| allowed (RNE(x 127) stays <= 127)
-#ifndef D_PKQ
-#define D_PKQ 0  // frame-1 quantisation's FMAs (|b|^2, the RNE scalings) two at a time (v_pk_fma_f32)
-#endif
 #ifndef D_CC
 // 1: integer path, |b_j| bounded from the codes (v_dot4) and NaN caught by v_maximum3 instead of
 // summing the fp32 squares (12 VALU per tile and wave fewer) -- fails the out-of-range parity test
@@ -79,17 +76,25 @@ constexpr float IK_MMAX = 1.003f;  // integer path: max |b_jk| allowed (RNE(x 12
 #define D_CC 0
 #endif
 
-#ifndef D_SKEW
-#define D_SKEW 0
-#endif
 #ifdef MV_TRACE  // phase stamps (s_memtime) per (block, wave): tools/trace_direct.py
 constexpr int D_TRACE_BLOCKS = 16384;
 __device__ unsigned long long g_d_trace[D_TRACE_BLOCKS * D_NW * 10];
+// pair-exchange event counts (per wave): flag waits entered, polls, foreign-XCD flags, spin
+// timeouts, waves gone SOLO, final statistics taken / recomputed, imports
+__device__ unsigned g_x_cnt[8];
+#ifdef X_COUNT  // (global atomics: they slow the kernel down several-fold -- counts only)
+#define X_CNT(K) do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_x_cnt[K], 1u); } while (0)
+#else
+#define X_CNT(K) do { } while (0)
+#endif
 #define D_STAMP(K) do { __builtin_amdgcn_sched_barrier(0); ts_[K] = __builtin_amdgcn_s_memtime(); if ((K) < 2) ts_[4 + (K)] = __builtin_amdgcn_s_memrealtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
 #define D_SYNC() __syncthreads()
 #else
 #define D_STAMP(K) do { } while (0)
 #define D_SYNC() __syncthreads()
+#endif
+#ifndef MV_TRACE
+#define X_CNT(K) do { } while (0)
 #endif
 
 // max |b| and sum |b|^2 over a row's 16 lanes (quad_perm [1,0,3,2], [2,3,0,1],
@@ -182,6 +187,15 @@ __device__ __forceinline__ float vmax(float a, float b) {
 #ifndef D_EXP_NOFOLD
 #define D_EXP_NOFOLD 0
 #endif
+#ifndef X_EXP_NOSTORE
+#define X_EXP_NOSTORE 0  // timing experiments only (wrong results): no exchange-slot stores
+#endif
+#ifndef X_EXP_OWNIMPORT
+#define X_EXP_OWNIMPORT 0  // timing experiments only (wrong results): import this block's own slot
+#endif
+#ifndef X_EXP_NOIMPORT
+#define X_EXP_NOIMPORT 0  // timing experiments only (wrong results): imports re-read one 16-B chunk
+#endif
 __device__ __forceinline__ void dma_half(const float *B, int h, int n1, int wu, unsigned chunk16, unsigned slot) {
     if (D_EXP_NODMA && h >= 2) return;
     const unsigned dst = slot + (unsigned)(wu * 4 * KD * 4);
@@ -252,19 +266,6 @@ struct QHalf {
     }
     __device__ __forceinline__ void sumsq() {
         if constexpr (CC) return;
-        if constexpr (D_PKQ) {  // |b|^2 in two lanes of v_pk_fma_f32 (any order: the window's Bn carries 1e-4)
-            f32x2v s2 = pk_fma_sq(f32x2v{x0[0], x0[1]}, f32x2v{0.f, 0.f});
-            s2 = pk_fma_sq(f32x2v{x0[2], x0[3]}, s2);
-            s2 = pk_fma_sq(f32x2v{x1[0], x1[1]}, s2);
-            s2 = pk_fma_sq(f32x2v{x1[2], x1[3]}, s2);
-            s2 = pk_fma_sq(f32x2v{x2[0], x2[1]}, s2);
-            s2 = pk_fma_sq(f32x2v{x2[2], x2[3]}, s2);
-            s2 = pk_fma_sq(f32x2v{x3[0], x3[1]}, s2);
-            s2 = pk_fma_sq(f32x2v{x3[2], x3[3]}, s2);
-            qa = s2[0];
-            qb = s2[1];
-            return;
-        }
         qa = __builtin_fmaf(x0[0], x0[0], __builtin_fmaf(x0[1], x0[1], __builtin_fmaf(x0[2], x0[2], x0[3] * x0[3])));
         qb = __builtin_fmaf(x1[0], x1[0], __builtin_fmaf(x1[1], x1[1], __builtin_fmaf(x1[2], x1[2], x1[3] * x1[3])));
         qa = __builtin_fmaf(x2[0], x2[0], __builtin_fmaf(x2[1], x2[1], __builtin_fmaf(x2[2], x2[2], __builtin_fmaf(x2[3], x2[3], qa))));
@@ -289,22 +290,12 @@ struct QHalf {
         }
     }
     __device__ __forceinline__ void pack01() {
-        if constexpr (D_PKQ) {
-            code[0] = pack4_pk(x0, f32x2v{q, MAGIC_RNE});
-            code[1] = pack4_pk(x1, f32x2v{q, MAGIC_RNE});
-            return;
-        }
         code[0] = pack4(x0[0], x0[1], x0[2], x0[3], q);
         code[1] = pack4(x1[0], x1[1], x1[2], x1[3], q);
     }
     __device__ __forceinline__ void pack23() {
-        if constexpr (D_PKQ) {
-            code[2] = pack4_pk(x2, f32x2v{q, MAGIC_RNE});
-            code[3] = pack4_pk(x3, f32x2v{q, MAGIC_RNE});
-        } else {
-            code[2] = pack4(x2[0], x2[1], x2[2], x2[3], q);
-            code[3] = pack4(x3[0], x3[1], x3[2], x3[3], q);
-        }
+        code[2] = pack4(x2[0], x2[1], x2[2], x2[3], q);
+        code[3] = pack4(x3[0], x3[1], x3[2], x3[3], q);
         if constexpr (CC) {  // |c_j|^2 of the codes; |b_j| <= s_j (|c_j| + 8) (|b_jk - c_jk s_j| <= s_j / 2)
             int c2 = __builtin_amdgcn_sdot4(code[0], code[0], 0, false);
             c2 = __builtin_amdgcn_sdot4(code[1], code[1], c2, false);
@@ -336,7 +327,7 @@ struct QHalf {
         const int r = t >> 4, sub = t & 15, row = 32 * hh + r;
         *reinterpret_cast<i32x4 *>(rq + row * D_RS + (sub << 4)) = code;
         if (sub == 0) *reinterpret_cast<int *>(rq + row * D_RS + KD) = sh;
-        if (xon) {
+        if (xon && !X_EXP_NOSTORE) {
             *reinterpret_cast<i32x4 *>(xs + r * D_RS + (sub << 4)) = code;
             if (sub == 0) *reinterpret_cast<int *>(xs + r * D_RS + KD) = sh;
         }
@@ -598,12 +589,19 @@ __device__ __forceinline__ Sweep block_stats(Sweep st, float *misc, int w, int l
 #ifndef D_XCH
 #define D_XCH 0  // 1: the pair exchange (allpairs_q8d_xch_bytes > 0); 0: every block quantises all of frame 1
 #endif
-constexpr int XR = 3;                       // exchange slots per block
+#ifndef X_UNIQUE
+// 1: one exchange slot per tile (never reused within a launch: the imports are plain LDS-DMA
+// loads -- no line of a slot can be in this CU's L1 before the slot was written); 0: 4 slots
+// reused in turn, imported with sc1 (L1-bypassing) LDS-DMA loads
+#define X_UNIQUE 1
+#endif
+constexpr int XR = X_UNIQUE ? 16 : 4;       // exchange slots per block (16 = the tiles of cap 1024)
 constexpr int X_SLOT = 32 * D_RS;           // 32 ring rows
 constexpr int X_BLOCK = XR * X_SLOT + 256;  // + the block's final statistics
-constexpr int X_OFF_RING = 2 * D_HALF;      // exchange mode: 2 staging slots (own halves), 3 ring slots
+constexpr int X_OFF_RING = 2 * D_HALF;      // exchange mode: 2 staging slots (own halves), 4 ring slots
+constexpr int X_RSLOT = BN * D_RS;          // an exchange-mode ring slot: 64 padded rows
 constexpr unsigned X_FINAL = 0xffffu;
-static_assert(X_OFF_RING + 3 * D_SLOT <= D_OFF_ROW, "the exchange ring fits below the row data");
+static_assert(X_OFF_RING + 4 * X_RSLOT <= D_OFF_ROW, "the exchange ring fits below the row data");
 static_assert(D_PAD, "the exchange keeps the key shifts in the ring rows' padding");
 #ifndef X_SPIN
 #define X_SPIN 512  // flag polls (~0.4 us each) before SOLO
@@ -665,22 +663,36 @@ __device__ __forceinline__ int x_check(unsigned v, unsigned need, unsigned tag) 
 // poll the partner's flag (this wave, flag word xw[wu]) until >= need: true, or SOLO: false
 __device__ __forceinline__ bool x_wait(const XPair &xp, const unsigned *xw, unsigned fw_l, int wu, int lane,
                                        unsigned need) {
+    X_CNT(0);
     for (int i = 0; i < X_SPIN; i++) {
         if (lane == 0) glds4_sc1(xp.fpar, fw_l);
         wait_vm_mem<0>();
+        X_CNT(1);
         const int c = x_check(__builtin_amdgcn_readfirstlane(xw[wu]), need, xp.tag);
+        if (c < 0) X_CNT(2);
         if (c != 0) return c > 0;
         __builtin_amdgcn_s_sleep(8);
     }
+    X_CNT(3);
     return false;
 }
 // this wave's 4 rows of the partner's half, exchange slot `src` -> LDS ring rows at `dst`
 // (2 DMA instructions: 1 KiB + 64 B)
 __device__ __forceinline__ void x_import(const char *src, unsigned dst, int wu, int lane) {
+    if (X_EXP_NOIMPORT) {  // keep the instruction count: 2 dword loads of the flag line instead
+        glds16_sc1<0>(src, 0u, dst + (unsigned)(wu * 4 * D_RS));
+        if (lane < 4) glds16_sc1<1024>(src, 0u, dst + (unsigned)(wu * 4 * D_RS));
+        return;
+    }
     const unsigned v = (unsigned)(wu * 4 * D_RS + 16 * lane);
     const unsigned d = dst + (unsigned)(wu * 4 * D_RS);
-    glds16_sc1<0>(src, v, d);
-    if (lane < 4) glds16_sc1<1024>(src, v + 1024u, d);
+    if (X_UNIQUE) {
+        glds16<0>(src, v, d);
+        if (lane < 4) glds16<1024>(src, v + 1024u, d);
+    } else {
+        glds16_sc1<0>(src, v, d);
+        if (lane < 4) glds16_sc1<1024>(src, v + 1024u, d);
+    }
 }
 // SOLO: this thread's 16 values of the partner half of `tile` quantised here (frame 1 in memory)
 __device__ __forceinline__ void x_solo(char *rq, const float *B, int tile, int pw, int n1, int t, int tb) {
@@ -717,6 +729,19 @@ __device__ __forceinline__ Sweep x_stats(const float *B, int pw, int n1, int t, 
 // The integer-key sweep with the pair exchange: the same m1 / m2 and (after x_final) the same
 // statistics as sweep<true>.  Own halves of tiles 0, 1 were issued before the A phase into
 // staging slots 0, 1.  Returns this block's statistics of its own halves.
+// Schedule (tile T: own half staged at the top of T - 4 into staging slot T & 1, quantised
+// during T - 3 into ring slot T % 4 and exchange slot T % XR, stored by the top of T - 2, where
+// the flag then says "T + 1 tiles stored"; the partner half imported at the END of tile T - 2,
+// landed by the top of T):
+//   top of t    vmcnt(2) (everything but the newest import) + barrier; publish t + 3; stage t + 4
+//   seg 0       MFMAs of tile t (group 0); own tile t + 3: load .. reduce
+//   middle      LDS-DMA of the partner's flag
+//   seg 1       MFMAs (group 1); own tile t + 3: pack, store
+//   end of t    the flag >= t + 3 (the partner is past its top of t, a whole tile ago in step):
+//               import the partner half of tile t + 2
+// Exchange slot t + 3 (written in seg 1 of t) held tile t - 1, which the partner imported at the
+// end of its tile t - 3 and had landed at its top of t - 1 -- before it published t + 2, which
+// this wave saw at the end of tile t - 1.
 __device__ __forceinline__ Sweep sweep_x(char *lds, const float *B, int n1, int t, int lane, int wu, unsigned chunk16,
                                          unsigned lds_base, const i32x4 (&aI)[RG][KD / 32], float (&m1)[RG][16],
                                          float (&m2)[RG][16], int tb, const XPair &xp) {
@@ -729,7 +754,12 @@ __device__ __forceinline__ Sweep sweep_x(char *lds, const float *B, int n1, int 
     Sweep st = {0.f, 0.f, false};
     bool wsolo = false;
     if (t == 0) xw[D_NW] = 0u;
-    // ---- own halves of tiles 0, 1 -> ring slots 0, 1 and exchange slots 0, 1 ----
+    auto go_solo = [&]() {
+        X_CNT(4);
+        wsolo = true;
+        if (lane == 0) xw[D_NW] = 1u;
+    };
+    // ---- prologue: own halves of tiles 0, 1, 2 -> ring slots and exchange slots 0, 1, 2 ----
     wait_vm_mem<0>();
     __syncthreads();  // staging slots 0, 1 landed
     {
@@ -743,20 +773,45 @@ __device__ __forceinline__ Sweep sweep_x(char *lds, const float *B, int n1, int 
             h.reduce(j, n1, tb);
             h.pack01();
             h.pack23();
-            h.store_x(ring + k * D_SLOT, w, t, true, st.smax, st.b2max, st.bad, xp.own + k * X_SLOT, true);
+            h.store_x(ring + k * X_RSLOT, w, t, true, st.smax, st.b2max, st.bad, xp.own + k * X_SLOT, true);
         }
     }
     wait_vm_mem<0>();
     __syncthreads();  // every wave's stores done; staging slots 0, 1 free
     if (t == 0) x_publish(xp, 2u);
-    if (x_wait(xp, xw, fw_l, wu, lane, 1u) && !(X_FORCE_SOLO && xp.solo_at == 0)) {
-        x_import(xp.par, ring_l, wu, lane);
-    } else {
-        wsolo = true;
-        if (lane == 0) xw[D_NW] = 1u;
-        x_solo(ring, B, 0, pw, n1, t, tb);
-    }
     dma_half(B, 2 * 2 + w, n1, wu, chunk16, lds_base);  // own half of tile 2 -> staging slot 0
+    if (ntc > 3) {
+        dma_half(B, 2 * 3 + w, n1, wu, chunk16, lds_base + D_HALF);  // tile 3 -> staging slot 1
+        wait_vm_mem<4>();
+    } else {
+        wait_vm_mem<0>();
+    }
+    __syncthreads();  // tile 2 staged
+    {
+        QHalf<true> h;
+        const int j = 2 * BN + 32 * w + (t >> 4);
+        h.load(lds, t);
+        h.absmax();
+        h.sumsq();
+        h.reduce(j, n1, tb);
+        h.pack01();
+        h.pack23();
+        h.store_x(ring + 2 * X_RSLOT, w, t, true, st.smax, st.b2max, st.bad, xp.own + 2 * X_SLOT, true);
+    }
+    wait_vm_mem<0>();
+    __syncthreads();
+    // (tile 2 is published at the top of tile 0, after the imports below have landed: a flag of 3
+    // must also mean "past the import of tile 0", which exchange slot 0's reuse relies on)
+    // the partner halves of tiles 0, 1
+    if (x_wait(xp, xw, fw_l, wu, lane, 2u) && !(X_FORCE_SOLO && xp.solo_at == 0)) {
+        x_import(xp.par, ring_l, wu, lane);
+        x_import(xp.par + X_SLOT, ring_l + (unsigned)X_RSLOT, wu, lane);
+    } else {
+        go_solo();
+        x_solo(ring, B, 0, pw, n1, t, tb);
+        x_solo(ring + X_RSLOT, B, 1, pw, n1, t, tb);
+    }
+    bool pend = !wsolo;  // the newest VMEM instructions are an import (2 per wave)
 
     const int rdb = fr * D_RS + fh * 16;
     i32x16 acc[RG][2];
@@ -780,7 +835,7 @@ __device__ __forceinline__ Sweep sweep_x(char *lds, const float *B, int n1, int 
             fold_keys(acc[FG][0][q], acc[FG][1][q], sh0, sh1, (G0), (G0) + 1u, m1[FG][q], m2[FG][q]); \
     } while (0)
     // group G's MFMAs on the tile at `rs`, folding group FG meanwhile; QS: the quantisation
-    // stages of own half of tile t + 2 in this segment (0: load .. reduce; 1: pack, store)
+    // stages of own half of tile t + 3 in this segment (0: load .. reduce; 1: pack, store)
 #define X_SEG(G, FG, G0, QS)                                                                 \
     do {                                                                                     \
         const char *base = rs + rdb;                                                         \
@@ -794,7 +849,7 @@ __device__ __forceinline__ Sweep sweep_x(char *lds, const float *B, int n1, int 
             } else {                                                                         \
                 if (s_ == 1) qh.pack01();                                                    \
                 else if (s_ == 2) qh.pack23();                                               \
-                else if (s_ == 3) qh.store_x(rq, w, t, live, st.smax, st.b2max, st.bad, xq, live && !wsolo); \
+                else if (s_ == 3) qh.store_x(rq, w, t, live, st.smax, st.b2max, st.bad, xq, xon); \
             }                                                                                \
             if (s_ < KD / 32) {                                                              \
                 b0_[s_] = *reinterpret_cast<const i32x4 *>(base + 32 * s_);                  \
@@ -817,48 +872,54 @@ __device__ __forceinline__ Sweep sweep_x(char *lds, const float *B, int n1, int 
     } while (0)
 
     for (int tc = 0; tc < ntc; tc++) {
-        wait_vm_mem<0>();  // own half of tile tc + 2 staged; own stores of tile tc + 1; the import of tc
-        __syncthreads();   // tile tc complete in its ring slot; every wave's stores done
+        if (pend)
+            wait_vm_mem<2>();  // staging of tile tc + 3, own stores of tile tc + 2, the import of tile tc
+        else
+            wait_vm_mem<0>();
+        __syncthreads();  // tile tc complete in its ring slot; every wave's stores done
         const bool bsolo = xw[D_NW] != 0u;
         wsolo = wsolo | bsolo;
-        if (t == 0 && !bsolo) x_publish(xp, (unsigned)min(tc + 2, ntc));
-        const bool imp = tc + 1 < ntc, dma = tc + 3 < ntc;
-        if (imp && !wsolo && lane == 0) glds4_sc1(xp.fpar, fw_l);
-        if (dma) dma_half(B, 2 * (tc + 3) + w, n1, wu, chunk16, lds_base + (unsigned)(((tc + 1) & 1) * D_HALF));
-        const char *rs = ring + (tc % 3) * D_SLOT;
-        char *rq = ring + ((tc + 2) % 3) * D_SLOT;
-        char *xq = xp.own + ((tc + 2) % XR) * X_SLOT;
-        const char *stg = lds + (tc & 1) * D_HALF;
-        const bool live = tc + 2 < ntc;
-        const int jq = (tc + 2) * BN + 32 * w + (t >> 4);
+        if (t == 0 && !bsolo) x_publish(xp, (unsigned)min(tc + 3, ntc));
+        if (tc + 4 < ntc) dma_half(B, 2 * (tc + 4) + w, n1, wu, chunk16, lds_base + (unsigned)((tc & 1) * D_HALF));
+        const char *rs = ring + (tc & 3) * X_RSLOT;
+        char *rq = ring + ((tc + 3) & 3) * X_RSLOT;
+        char *xq = xp.own + ((tc + 3) % XR) * X_SLOT;
+        const char *stg = lds + ((tc + 1) & 1) * D_HALF;
+        const bool live = tc + 3 < ntc;
+        const bool imp = tc + 2 < ntc;
+        const bool xon = live && !wsolo;
+        const int jq = (tc + 3) * BN + 32 * w + (t >> 4);
         QHalf<true> qh;
         const unsigned gp_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)max(tc - 1, 0));
         X_SEG(0, 1, gp_, 0);
         sh0 = *reinterpret_cast<const int *>(rs + fr * D_RS + KD);  // the key shifts of tile tc's columns
         sh1 = *reinterpret_cast<const int *>(rs + (fr + 32) * D_RS + KD);
-        if (imp) {  // the partner half of tile tc + 1
-            const unsigned need = (unsigned)(tc + 2);
-            if (!wsolo) {
-                if (dma)
-                    wait_vm_mem<4>();  // the flag (the 4 DMA instructions after it may fly)
-                else
-                    wait_vm_mem<0>();
-                int c = x_check(__builtin_amdgcn_readfirstlane(xw[wu]), need, xp.tag);
-                if (c == 0) c = x_wait(xp, xw, fw_l, wu, lane, need) ? 1 : -1;
-                if (X_FORCE_SOLO && xp.solo_at >= 0 && tc + 1 >= xp.solo_at) c = -1;
-                if (c < 0) {
-                    wsolo = true;
-                    if (lane == 0) xw[D_NW] = 1u;
-                }
-            }
-            if (!wsolo)
-                x_import(xp.par + ((tc + 1) % XR) * X_SLOT,
-                         ring_l + (unsigned)(((tc + 1) % 3) * D_SLOT), wu, lane);
-            else
-                x_solo(ring + ((tc + 1) % 3) * D_SLOT, B, tc + 1, pw, n1, t, tb);
-        }
+        const bool poll = imp && !wsolo;
+        if (poll && lane == 0) glds4_sc1(xp.fpar, fw_l);
         const unsigned gc_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)tc);
         X_SEG(1, 0, gc_, 1);
+        pend = false;
+        if (imp) {  // the partner half of tile tc + 2
+            if (poll) {
+                if (xon)
+                    wait_vm_mem<2>();  // the flag (this wave's 2 exchange stores after it may fly)
+                else
+                    wait_vm_mem<0>();
+                int c = x_check(__builtin_amdgcn_readfirstlane(xw[wu]), (unsigned)(tc + 3), xp.tag);
+                if (c < 0) X_CNT(2);
+                if (c == 0) c = x_wait(xp, xw, fw_l, wu, lane, (unsigned)(tc + 3)) ? 1 : -1;
+                if (X_FORCE_SOLO && xp.solo_at >= 0 && tc + 2 >= xp.solo_at) c = -1;
+                if (c < 0) go_solo();
+            }
+            if (!wsolo) {
+                x_import((X_EXP_OWNIMPORT ? (const char *)xp.own : xp.par) + ((tc + 2) % XR) * X_SLOT,
+                         ring_l + (unsigned)(((tc + 2) & 3) * X_RSLOT), wu, lane);
+                X_CNT(7);
+                pend = true;
+            } else {
+                x_solo(ring + ((tc + 2) & 3) * X_RSLOT, B, tc + 2, pw, n1, t, tb);
+            }
+        }
     }
     {  // group 1 of the last tile
         const unsigned gl_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)(ntc - 1));
@@ -907,6 +968,7 @@ __device__ __forceinline__ Sweep x_final(Sweep st, const XPair &xp, char *lds, c
     }
     __syncthreads();
     Sweep p;
+    if (w == 0) X_CNT(pst[3] != 0.f ? 5 : 6);
     if (pst[3] != 0.f) {
         p.smax = pst[0];
         p.b2max = pst[1];
@@ -935,12 +997,6 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, con
     const int n0 = min(max(n0v[pair], 0), cap), n1 = min(max(n1v[pair], 0), cap);
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int row0 = tr * D_BM;
-    if (D_SKEW > 0 && blockIdx.x < 256 && ((blockIdx.x >> 4) & 1)) {
-        // timing experiment: the first dispatch wave's odd pairs (both blocks) start D_SKEW x 10 ns
-        // late, so that half of the CUs run their A phase while the other half sweeps
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)D_SKEW) __builtin_amdgcn_s_sleep(16);
-    }
     int *oidx = match_idx + (size_t)pair * cap + row0;
     float *oscore = match_score ? match_score + (size_t)pair * cap + row0 : nullptr;  // null: indices only
     if (row0 + t < cap && (row0 + t >= n0 || n1 <= 0)) {  // rows in [n0, cap): no match
@@ -975,11 +1031,8 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, con
     dma_half(B, xmode ? tr : 0, n1, wu, chunk16, lds_base);
     dma_half(B, xmode ? 2 + tr : 1, n1, wu, chunk16, lds_base + D_HALF);
     i32x4 aI[RG][KD / 32];
-    if (D_APIPE)
-        a_phase_pipe(lds + D_OFF_AIMG + w * 32 * KD, rowv, w * 64, row0, n0, lane, A, aI);
-    else
-        a_phase<false, D_QB>(lds + D_OFF_AIMG + w * 32 * KD, rowv, w * 64, row0, n0, lane, A, nullptr, nullptr,
-                             nullptr, false, aI);
+    a_phase<false, D_QB>(lds + D_OFF_AIMG + w * 32 * KD, rowv, w * 64, row0, n0, lane, A, nullptr, nullptr, nullptr,
+                         false, aI);
     D_STAMP(1);
     __syncthreads();  // the A images (staging slot 2 + the ring) are consumed
     float m1[RG][16], m2[RG][16];
@@ -1062,5 +1115,13 @@ int launch_allpairs_q8d_match(hipStream_t s, int batch, int cap, const int *n0, 
 #ifdef MV_TRACE
 extern "C" int mv_debug_direct_trace(void *host, long bytes) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_d_trace), (size_t)bytes) == hipSuccess ? 0 : -3;
+}
+extern "C" int mv_debug_exchange_counts(unsigned *host8, int reset) {
+    if (hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_x_cnt), 8 * sizeof(unsigned)) != hipSuccess) return -3;
+    if (reset) {
+        const unsigned z[8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_x_cnt), z, sizeof z) != hipSuccess) return -3;
+    }
+    return 0;
 }
 #endif

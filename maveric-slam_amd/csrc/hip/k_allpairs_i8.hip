@@ -151,19 +151,6 @@ __device__ __forceinline__ void fold3_i8(float a, float b, float &m1, float &m2)
     asm("v_max_f32 %0, %1, %2" : "=v"(m2) : "v"(m2), "v"(md));
 }
 
-#ifndef I8_PK
-#define I8_PK 0  // 1: the fold's dequantising FMAs two at a time (v_pk_fma_f32)
-#endif
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-// (x, y) * r + c for two accumulator values of one column (both products exact inside the fma);
-// rc = (r, c) in one register pair: src1 takes its low half, src2 its high half, for both lanes
-__device__ __forceinline__ f32x2 pk_fma_i8(int x, int y, f32x2 rc) {
-    f32x2 v, d;
-    v[0] = __int_as_float(x);
-    v[1] = __int_as_float(y);
-    asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(d) : "v"(v), "v"(rc));
-    return d;
-}
 // D = 0x40800000 (the bits of 4.0) + A.B: the first k32 step of a chain, C as the inline
 // constant 4.0 (a builtin with a constant C gets it hoisted into 16 VGPRs); the chain's next
 // MFMA reads D as SrcC with exact overlap (hardware forwarding, no wait states)
@@ -290,17 +277,6 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
     // the fold of group 1 of tile tc - 1, then tile tc's MFMAs for group 1 beside the fold of
     // group 0 of tile tc (fold rows 2 s, 2 s + 1 after k32 step s): one accumulator set, and
     // the fold never waits on the MFMAs in flight.  B fragments are read per group.
-#if I8_PK
-    // rows 2 S, 2 S + 1 of a column block share the lane's column: one v_pk_fma_f32 dequantises both
-#define I8_FOLD2(FG, S, G0, R0, R1, C0, C1)                                                  \
-    do {                                                                                     \
-        const f32x2 a2_ = pk_fma_i8(acc[FG][0][2 * (S)], acc[FG][0][2 * (S) + 1], f32x2{(R0), (C0)}); \
-        const f32x2 b2_ = pk_fma_i8(acc[FG][1][2 * (S)], acc[FG][1][2 * (S) + 1], f32x2{(R1), (C1)}); \
-        _Pragma("unroll") for (int e_ = 0; e_ < 2; e_++)                                     \
-            fold3_i8(tag_i8(a2_[e_], vkeep, (G0)), tag_i8(b2_[e_], vkeep, (G0) + 1u), m1[FG][2 * (S) + e_], \
-                     m2[FG][2 * (S) + e_]);                                                  \
-    } while (0)
-#else
 #define I8_FOLD2(FG, S, G0, R0, R1, C0, C1)                                                  \
     do {                                                                                     \
         _Pragma("unroll") for (int q = 2 * (S); q < 2 * (S) + 2; q++) {                      \
@@ -309,7 +285,6 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
             fold3_i8(tag_i8(a_, vkeep, (G0)), tag_i8(b_, vkeep, (G0) + 1u), m1[FG][q], m2[FG][q]); \
         }                                                                                    \
     } while (0)
-#endif
 #define I8_SEG(J, G, FG, G0, R0, R1, C0, C1)                                                 \
     do {                                                                                     \
         constexpr int PF = I8_PF;                                                            \

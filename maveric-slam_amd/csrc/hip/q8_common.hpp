@@ -121,28 +121,6 @@ __device__ __forceinline__ int pack4(float x0, float x1, float x2, float x3, flo
     return (int)__builtin_amdgcn_perm(p23, p01, 0x05040100u);
 }
 
-typedef float f32x2v __attribute__((ext_vector_type(2)));
-// two lanes of x * qm.x + qm.y (one v_pk_fma_f32: src1 / src2 broadcast from the pair's halves)
-__device__ __forceinline__ f32x2v pk_fma_bcast(f32x2v x, f32x2v qm) {
-    f32x2v d;
-    asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(d) : "v"(x), "v"(qm));
-    return d;
-}
-// two lanes of x * x + acc
-__device__ __forceinline__ f32x2v pk_fma_sq(f32x2v x, f32x2v acc) {
-    f32x2v d;
-    asm("v_pk_fma_f32 %0, %1, %1, %2" : "=v"(d) : "v"(x), "v"(acc));
-    return d;
-}
-// pack4 with the four RNE scalings as two v_pk_fma_f32 (the same fma per value: same codes)
-__device__ __forceinline__ int pack4_pk(f32x4v x, f32x2v qm) {
-    const f32x2v f01 = pk_fma_bcast(f32x2v{x[0], x[1]}, qm);
-    const f32x2v f23 = pk_fma_bcast(f32x2v{x[2], x[3]}, qm);
-    const unsigned p01 = __builtin_amdgcn_perm(__float_as_uint(f01[1]), __float_as_uint(f01[0]), 0x0c0c0400u);
-    const unsigned p23 = __builtin_amdgcn_perm(__float_as_uint(f23[1]), __float_as_uint(f23[0]), 0x0c0c0400u);
-    return (int)__builtin_amdgcn_perm(p23, p01, 0x05040100u);
-}
-
 // The reference's sequential fp32 dot (mul then add, k = 0..255), 4 load batches per operand.
 __device__ __forceinline__ float exact_dot(const float *__restrict__ a, const float *__restrict__ b) {
     constexpr int U = 16;
@@ -255,80 +233,6 @@ __device__ __forceinline__ bool better(int dmode, float v, int j, float bv, int 
     const bool nv = v != v, nb = bv != bv;
     if (nv || nb) return nv && (!nb || j < bj);
     return v < bv || (v == bv && j < bj);
-}
-
-// The A phase's per-quad step (a_phase below, fp32 input): this lane's 16 floats of row r of
-// the group -> |a|^2, m, the row's scale / range flag (rowv) and its codes into the image
-__device__ __forceinline__ void a_quad(const f32x4v (&x)[4], char *img, float2 *rowv, int rrow, int r, int sub) {
-    float m = 0.f, qa = 0.f, qb = 0.f;
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-        m = absmax3(m, x[u][0], x[u][1]);
-        m = absmax3(m, x[u][2], x[u][3]);
-        qa = __builtin_fmaf(x[u][0], x[u][0], qa);
-        qb = __builtin_fmaf(x[u][1], x[u][1], qb);
-        qa = __builtin_fmaf(x[u][2], x[u][2], qa);
-        qb = __builtin_fmaf(x[u][3], x[u][3], qb);
-    }
-    float q2 = qa + qb;
-    m = fmaxf(m, swz_xor<1>(m));
-    q2 += swz_xor<1>(q2);
-    m = fmaxf(m, swz_xor<2>(m));
-    q2 += swz_xor<2>(q2);
-    m = fmaxf(m, swz_xor<4>(m));
-    q2 += swz_xor<4>(q2);
-    m = fmaxf(m, swz_xor<8>(m));
-    q2 += swz_xor<8>(q2);
-    const float q = m > 0.f ? 127.f * __builtin_amdgcn_rcpf(m) : 0.f;
-    const bool afull = !(q2 <= FLT_MAX) || m < SCALE_LO || m > SCALE_HI;  // zero rows too
-    if (sub == 0) rowv[rrow] = make_float2(q2, afull ? -1.f : m * (1.f / 127.f));
-    char *rowp = img + r * KD + 4 * (sub & 3);
-#pragma unroll
-    for (int u = 0; u < 4; u++)  // k = 4 sub + 64 u: chunk (sub >> 2) + 4 u
-        *reinterpret_cast<int *>(rowp + ((((sub >> 2) + 4 * u) ^ (r & 15)) << 4)) =
-            pack4(x[u][0], x[u][1], x[u][2], x[u][3], q);
-}
-// four row quads (rows 4 qd + rq of the group, qd = q0 .. q0 + 3) of frame 0, 16 loads per lane
-__device__ __forceinline__ void a_load4(f32x4v (&x)[4][4], const float *__restrict__ A, int rowg, int q0, int n0,
-                                        int rq, int sub) {
-#pragma unroll
-    for (int qd = 0; qd < 4; qd++) {
-        const float *ar = A + (size_t)min(rowg + 4 * (q0 + qd) + rq, n0 - 1) * KD;
-#pragma unroll
-        for (int u = 0; u < 4; u++) x[qd][u] = *reinterpret_cast<const f32x4v *>(ar + 4 * (sub + 16 * u));
-    }
-}
-// The fp32 A phase software-pipelined: the next 4 row quads' loads are in flight while this
-// batch is quantised (two batches = 128 VGPRs of loads; the sweep's registers are not live yet),
-// so the wave waits for the memory once instead of once per batch.  Same outputs as a_phase.
-__device__ __forceinline__ void a_phase_pipe(char *img, float2 *rowv, int rbase, int row0, int n0, int lane,
-                                             const float *__restrict__ A, i32x4 (&aI)[RG][KD / 32]) {
-    static_assert(RG == 2, "two 32-row groups per wave");
-    const int fr = lane & 31, fh = lane >> 5, sub = lane & 15, rq = lane >> 4;
-    const int rg0 = row0 + rbase, rg1 = row0 + rbase + 32;
-    f32x4v xa[4][4], xb[4][4];
-    a_load4(xa, A, rg0, 0, n0, rq, sub);
-    a_load4(xb, A, rg0, 4, n0, rq, sub);
-#pragma unroll
-    for (int qd = 0; qd < 4; qd++) a_quad(xa[qd], img, rowv, rbase + 4 * qd + rq, 4 * qd + rq, sub);
-    a_load4(xa, A, rg1, 0, n0, rq, sub);
-#pragma unroll
-    for (int qd = 0; qd < 4; qd++) a_quad(xb[qd], img, rowv, rbase + 4 * (4 + qd) + rq, 4 * (4 + qd) + rq, sub);
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own image writes
-#pragma unroll
-    for (int s2 = 0; s2 < KD / 32; s2++)
-        aI[0][s2] = *reinterpret_cast<const i32x4 *>(img + fr * KD + (((2 * s2 + fh) ^ (fr & 15)) << 4));
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // the reads complete before group 1's writes
-    a_load4(xb, A, rg1, 4, n0, rq, sub);
-#pragma unroll
-    for (int qd = 0; qd < 4; qd++) a_quad(xa[qd], img, rowv, rbase + 32 + 4 * qd + rq, 4 * qd + rq, sub);
-#pragma unroll
-    for (int qd = 0; qd < 4; qd++) a_quad(xb[qd], img, rowv, rbase + 32 + 4 * (4 + qd) + rq, 4 * (4 + qd) + rq, sub);
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-#pragma unroll
-    for (int s2 = 0; s2 < KD / 32; s2++)
-        aI[1][s2] = *reinterpret_cast<const i32x4 *>(img + fr * KD + (((2 * s2 + fh) ^ (fr & 15)) << 4));
-    __builtin_amdgcn_s_waitcnt(0xc07f);
 }
 
 // ---- the A phase: the wave's 2 x 32 frame-0 rows (rbase + 32 g + i of the block), fp32 ->

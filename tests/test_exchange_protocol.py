@@ -11,7 +11,7 @@ import random
 
 import pytest
 
-XR = 3
+XR = 4  # X_UNIQUE=0; X_UNIQUE=1 gives every tile its own slot (xr = ntc)
 
 
 class Slot:
@@ -24,18 +24,19 @@ class Slot:
 class Block:
     """slots[s][w]: the rows of exchange slot s that wave w stores (4 w .. 4 w + 3) -- and that the
     partner's wave w imports"""
-    def __init__(self, w, W):
+    def __init__(self, w, W, xr):
         self.w = w
         self.flag = 0
         self.solo = False
-        self.slots = [[Slot() for _ in range(W)] for _ in range(XR)]
+        self.slots = [[Slot() for _ in range(W)] for _ in range(xr)]
         self.arrived = {}
 
 
-def run(ntc, W, seed, spin, force=None, max_steps=200000):
-    """force: (block, tile) -- that block's wave 0 goes SOLO at that tile (X_FORCE_SOLO)"""
+def run(ntc, W, seed, spin, force=None, xr=XR, max_steps=400000):
+    """force: (block, tile) -- that block's wave 0 goes SOLO from that tile's import on
+    (X_FORCE_SOLO); xr: exchange slots per block (ntc: one per tile, never reused)"""
     rng = random.Random(seed)
-    blocks = [Block(0, W), Block(1, W)]
+    blocks = [Block(0, W, xr), Block(1, W, xr)]
     stats = {"imports": 0, "solo_waves": 0}
 
     def barrier(b, key):
@@ -62,58 +63,62 @@ def run(ntc, W, seed, spin, force=None, max_steps=200000):
     def wave(b, w):
         p = blocks[1 - b.w]
         wsolo = False
-        pending = None  # (slot, tile, version at the read's start)
+        pending = []  # imports in flight: (slot, tile, version at the read's start)
 
-        def end_read():
-            if pending is not None:
-                s = p.slots[pending[0]][w]
-                assert s.tile == pending[1] and not s.writing and s.version == pending[2], \
-                    "slot %d overwritten during the import of tile %d" % (pending[0], pending[1])
+        def land(keep):  # the imports older than the newest `keep` have landed (vmcnt)
+            while len(pending) > keep:
+                slot, tile, ver = pending.pop(0)
+                s = p.slots[slot][w]
+                assert s.tile == tile and not s.writing and s.version == ver, \
+                    "slot %d overwritten during the import of tile %d" % (slot, tile)
 
-        def start_read(slot, tile):
+        def start_read(tile):
+            slot = tile % xr
             s = p.slots[slot][w]
             assert s.tile == tile and not s.writing, "import of tile %d found %s" % (tile, s.tile)
             stats["imports"] += 1
-            return (slot, tile, s.version)
+            pending.append((slot, tile, s.version))
 
+        def forced(tile):
+            return force is not None and force[0] == b.w and w == 0 and tile >= force[1]
+
+        # prologue: own halves of tiles 0, 1 (publish 2), tile 2, import tiles 0, 1
         for k in range(2):
-            yield from write(b, w, k, k)
-        yield from barrier(b, "pro")
+            yield from write(b, w, k % xr, k)
+        yield from barrier(b, "p0")
         if w == 0:
             b.flag = max(b.flag, 2)
-        ok = yield from wait_flag(p, 1)
-        if force == (b.w, 0) and w == 0:
-            ok = False
-        if ok:
-            pending = start_read(0, 0)
+        yield from write(b, w, 2 % xr, 2)
+        yield from barrier(b, "p1")  # tile 2 is published at the top of tile 0 (after the imports below land)
+        ok = yield from wait_flag(p, 2)
+        if ok and not forced(0):
+            start_read(0)
+            start_read(1)
         else:
             wsolo = True
             b.solo = True
         for tc in range(ntc):
             yield
-            end_read()
-            pending = None
+            land(1)  # top: everything but the newest import
             yield from barrier(b, tc)
             bsolo = b.solo
             wsolo = wsolo or bsolo
             if w == 0 and not bsolo:
-                b.flag = max(b.flag, min(tc + 2, ntc))
+                b.flag = max(b.flag, min(tc + 3, ntc))
             yield
-            if tc + 1 < ntc:
+            if tc + 3 < ntc and not wsolo:  # seg 1: own half of tile tc + 3
+                yield from write(b, w, (tc + 3) % xr, tc + 3)
+            yield
+            if tc + 2 < ntc:  # end of the tile: the partner half of tile tc + 2
                 if not wsolo:
-                    ok = yield from wait_flag(p, tc + 2)
-                    if force is not None and force[0] == b.w and w == 0 and tc + 1 >= force[1]:
-                        ok = False
-                    if not ok:
+                    ok = yield from wait_flag(p, tc + 3)
+                    if not ok or forced(tc + 2):
                         wsolo = True
                         b.solo = True
                 if not wsolo:
-                    pending = start_read((tc + 1) % XR, tc + 1)
-            yield
-            if tc + 2 < ntc and not wsolo:
-                yield from write(b, w, (tc + 2) % XR, tc + 2)
+                    start_read(tc + 2)
         yield
-        end_read()
+        land(0)
         stats["solo_waves"] += wsolo
 
     live = [wave(b, w) for b in blocks for w in range(W)]
@@ -130,10 +135,11 @@ def run(ntc, W, seed, spin, force=None, max_steps=200000):
 
 
 @pytest.mark.parametrize("ntc", [3, 4, 7, 16])
-def test_exchange_protocol_random_interleavings(ntc):
+@pytest.mark.parametrize("unique", [False, True])
+def test_exchange_protocol_random_interleavings(ntc, unique):
     """generous spin budget: no SOLO, every partner half imported, every import intact"""
     for seed in range(40):
-        st = run(ntc, W=3, seed=seed, spin=10 ** 6)
+        st = run(ntc, W=3, seed=seed, spin=10 ** 6, xr=ntc if unique else XR)
         assert st["solo_waves"] == 0
         assert st["imports"] == 2 * 3 * ntc  # both blocks, every wave, tiles 0 .. ntc - 1
 

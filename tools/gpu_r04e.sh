@@ -6,9 +6,9 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-TESTS_FOR="${TESTS_FOR:-xapipe}" VARIANTS="${VARIANTS:-xch xskew xapipe}" AB_STEPS=20 AB_SCORE=0 \
+TESTS_FOR="${TESTS_FOR:-apipe}" VARIANTS="${VARIANTS:-ship apipe}" AB_STEPS=20 AB_SCORE=0 \
     AB_NOISE=0.01875 bash tools/gpu_ab.sh || exit $?
-TRACES="${TRACES:-xapipe_trace:0.01875}" bash tools/gpu_trace_exp.sh || exit $?
+TRACES="${TRACES:-apipe_trace:0.01875}" bash tools/gpu_trace_exp.sh || exit $?
 lib() { [ "$1" = ship ] && echo maveric-slam_amd/libmaveric_hip.so || echo build_variants/libmaveric_$1.so; }
 for rep in 1 2; do
   for v in ${I8_VARIANTS:-ship i8pk}; do
