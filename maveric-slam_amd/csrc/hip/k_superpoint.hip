@@ -291,6 +291,9 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
         }
     }
     // ---- the input tile (zero outside the image), 8 16-B loads in flight per thread ----
+    // (4 consecutive lanes read one pixel's 64 contiguous bytes: giving an 8-lane group one chunk
+    // of 8 pixels instead -- conflict-free LDS stores -- made the 64-channel layers 3-4x slower:
+    // the loads must stay lane-contiguous)
     const int8_t *src = in + (size_t)b * H * W * CIN;
     constexpr int LIF = 8;  // 16-B loads in flight per thread (12 / 16 measured the same)
     for (int i0 = 0; i0 < (FUSE1A ? 0 : NCHUNK); i0 += LIF * SP_NT) {
@@ -348,9 +351,16 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
     const int lo = SP_MAGIC_BITS + (RELU ? 0 : -128);
     if constexpr (CIN == 64) {
         // 64-channel layers (168 VGPRs: the lane-pair regroup below spilled the K loop): each wave writes its
-        // requantised outputs into its own LDS rows (64 B + 16 B of pad per pixel), then reads them
-        // back 16 B per lane and stores whole pixel runs -- 2 KiB contiguous per output row
-        constexpr int PB = 80;
+        // requantised outputs into its own LDS rows (64 B per pixel), then reads them back 16 B per
+        // lane and stores whole pixel runs -- 2 KiB contiguous per output row.  Chunk c of staged
+        // pixel P sits at 16-B position (c + (P >> 1)) & 3: conflict-free for both the 8-lane
+        // ds_write_b128 groups (pixels fr .. fr + 7, one chunk: 32-bank rows) and the 16-lane
+        // ds_read_b128 groups (4 pixels x 4 chunks: 64-bank rows); the 80-B padded stride this
+        // replaces left the reads 3-way conflicted (42 % of the non-pooled layers' LDS cycles)
+        constexpr int PB = 64;
+        // per-lane bases, computed where used (the row / pair offsets are compile-time
+        // immediates; hoisted address registers spilled these 168-VGPR kernels): reads take chunk
+        // k = lane & 3 of pixel lane >> 2 (+ 16 per read), whose 16-B position is (k + (lane >> 3)) & 3
         static_assert(4 * 4 * 32 * PB <= IY * IX * PS * 16, "staging fits the input tile");
         __syncthreads();  // every wave past its last read of the input tile
         char *stg = reinterpret_cast<char *>(tile) + w * (4 * 32 * PB);
@@ -377,20 +387,25 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
                     requant4(v, m[4 * qq], m[4 * qq + 1], m[4 * qq + 2], m[4 * qq + 3], rs, lo);
                     dw[qq] = pack4b(v[0], v[1], v[2], v[3]);
                 }
-                // 16-B stores (4-B ones at the 80-B pixel stride: 4-way bank conflicts)
-                *reinterpret_cast<i32x4 *>(stg + (jp * 16 + fr / 2) * PB + 32 * cbx + 16 * fh) = regroup16(dw);
+                // 16-B stores (4-B ones would be 4-way bank conflicted)
+                // pixel jp * 16 + fr / 2, chunk 2 cbx + fh, position (chunk + (fr >> 2)) & 3 (the
+                // non-fused pooled layer keeps the plain order: the swizzled one spilled it)
+                const int pa = (fr >> 1) * PB + ((FUSE1A ? ((2 * cbx + fh + (fr >> 2)) & 3) : 2 * cbx + fh) << 4);
+                *reinterpret_cast<i32x4 *>(stg + jp * 16 * PB + pa) = regroup16(dw);
             }
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes done
             __builtin_amdgcn_wave_barrier();
+            const int ra = (lane >> 2) * PB + ((FUSE1A ? (((lane & 3) + (lane >> 3)) & 3) : lane & 3) << 4);
 #pragma unroll
             for (int jp = 0; jp < 2; jp++) {
                 const int p = lane >> 2, k = lane & 3;  // 16 pooled pixels x 4 chunks
                 const int gy = y0 + 4 * w + 2 * jp, gx = x0 + 2 * p;
-                const i32x4 v = *reinterpret_cast<const i32x4 *>(stg + (jp * 16 + p) * PB + 16 * k);
+                const i32x4 v = *reinterpret_cast<const i32x4 *>(stg + jp * 16 * PB + ra);
                 if (gy < H && gx < W)
                     *reinterpret_cast<i32x4 *>(out + (((size_t)b * Ho + gy / 2) * Wo + gx / 2) * cstride + 64 * g + 16 * k) = v;
             }
         } else {
+            const int wa = fr * PB + (((fh + (fr >> 1)) & 3) << 4);
 #pragma unroll
             for (int j = 0; j < 4; j++)
 #pragma unroll
@@ -402,17 +417,19 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
                         requant4(v, acc[j][cb][4 * qq], acc[j][cb][4 * qq + 1], acc[j][cb][4 * qq + 2], acc[j][cb][4 * qq + 3], rs, lo);
                         dw[qq] = pack4b(v[0], v[1], v[2], v[3]);
                     }
-                    *reinterpret_cast<i32x4 *>(stg + (j * 32 + fr) * PB + 32 * cb + 16 * fh) = regroup16(dw);
+                    // pixel j * 32 + fr, chunk 2 cb + fh, position (chunk + (fr >> 1)) & 3 = wa ^ 32 cb
+                    *reinterpret_cast<i32x4 *>(stg + j * 32 * PB + (wa ^ (cb << 5))) = regroup16(dw);
                 }
             __builtin_amdgcn_s_waitcnt(0xc07f);
             __builtin_amdgcn_wave_barrier();
+            const int ra = (lane >> 2) * PB + ((((lane & 3) + (lane >> 3)) & 3) << 4);
 #pragma unroll
             for (int j = 0; j < 4; j++)
 #pragma unroll
                 for (int i = 0; i < 2; i++) {
                     const int c = lane + 64 * i, p = c >> 2, k = c & 3;  // 32 pixels x 4 chunks
                     const int gy = y0 + 4 * w + j, gx = x0 + p;
-                    const i32x4 v = *reinterpret_cast<const i32x4 *>(stg + (j * 32 + p) * PB + 16 * k);
+                    const i32x4 v = *reinterpret_cast<const i32x4 *>(stg + j * 32 * PB + i * 16 * PB + ra);
                     if (gy < H && gx < W)
                         *reinterpret_cast<i32x4 *>(out + (((size_t)b * H + gy) * W + gx) * cstride + 64 * g + 16 * k) = v;
                 }
