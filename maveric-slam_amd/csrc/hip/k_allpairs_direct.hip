@@ -54,8 +54,8 @@ constexpr int D_TILE = BN * D_RS, D_SLOT = D_TILE + BN * 4;        // + the tile
 constexpr int D_OFF_RING = 3 * D_HALF;                              // 2 int8 tile slots
 // [BM] float2 (|a|^2, s_a), past the int8 ring of either sweep (the pair exchange's: 4 slots of
 // 64 padded rows after 2 staging slots)
-constexpr int D_OFF_ROW = D_OFF_RING + 2 * D_SLOT > 2 * D_HALF + 4 * BN * D_RS ? D_OFF_RING + 2 * D_SLOT
-                                                                                : 2 * D_HALF + 4 * BN * D_RS;
+constexpr int D_OFF_ROW = D_OFF_RING + 2 * D_SLOT > 2 * D_HALF + 4 * D_SLOT ? D_OFF_RING + 2 * D_SLOT
+                                                                           : 2 * D_HALF + 4 * D_SLOT;
 constexpr int D_OFF_MISC = D_OFF_ROW + D_BM * 8;                    // [NW][4] per-wave statistics
 constexpr int D_OFF_X = D_OFF_MISC + D_NW * 16;                     // pair exchange: flags, SOLO, statistics
 constexpr int D_LDS = D_OFF_X + 64;
@@ -326,10 +326,13 @@ struct QHalf {
                                             char *xs, bool xon) {
         const int r = t >> 4, sub = t & 15, row = 32 * hh + r;
         *reinterpret_cast<i32x4 *>(rq + row * D_RS + (sub << 4)) = code;
-        if (sub == 0) *reinterpret_cast<int *>(rq + row * D_RS + KD) = sh;
+        if (sub == 0) reinterpret_cast<int *>(rq + D_TILE)[row] = sh;
         if (xon && !X_EXP_NOSTORE) {
-            *reinterpret_cast<i32x4 *>(xs + r * D_RS + (sub << 4)) = code;
-            if (sub == 0) *reinterpret_cast<int *>(xs + r * D_RS + KD) = sh;
+            *reinterpret_cast<i32x4 *>(xs + r * KD + (sub << 4)) = code;
+            // this wave's 4 rows' shifts (lanes 0, 16, 32, 48), one whole 128-B line per wave
+            const i32x4 s4 = {__builtin_amdgcn_readlane(sh, 0), __builtin_amdgcn_readlane(sh, 16),
+                              __builtin_amdgcn_readlane(sh, 32), __builtin_amdgcn_readlane(sh, 48)};
+            if ((t & 63) < 8) *reinterpret_cast<i32x4 *>(xs + 32 * KD + (t >> 6) * 128 + (t & 7) * 16) = s4;
         }
         bad = bad | (live & !((qa <= 1e30f) & (m <= IK_MMAX)));
         smax = vmax(smax, live ? s : 0.f);
@@ -596,10 +599,12 @@ __device__ __forceinline__ Sweep block_stats(Sweep st, float *misc, int w, int l
 #define X_UNIQUE 1
 #endif
 constexpr int XR = X_UNIQUE ? 16 : 4;       // exchange slots per block (16 = the tiles of cap 1024)
-constexpr int X_SLOT = 32 * D_RS;           // 32 ring rows
+// an exchange slot: 32 rows of 256 codes (256-B aligned: every line written whole), then per wave
+// one 128-B line holding its 4 rows' key shifts (replicated: the line is written whole)
+constexpr int X_SLOT = 32 * KD + 8 * 128;
 constexpr int X_BLOCK = XR * X_SLOT + 256;  // + the block's final statistics
 constexpr int X_OFF_RING = 2 * D_HALF;      // exchange mode: 2 staging slots (own halves), 4 ring slots
-constexpr int X_RSLOT = BN * D_RS;          // an exchange-mode ring slot: 64 padded rows
+constexpr int X_RSLOT = D_SLOT;             // an exchange-mode ring slot: 64 padded rows + 64 key shifts
 constexpr unsigned X_FINAL = 0xffffu;
 static_assert(X_OFF_RING + 4 * X_RSLOT <= D_OFF_ROW, "the exchange ring fits below the row data");
 static_assert(D_PAD, "the exchange keeps the key shifts in the ring rows' padding");
@@ -629,6 +634,22 @@ __device__ __forceinline__ void glds4_sc1(const void *sbase, unsigned lds_byte) 
         "global_load_lds_dword %0, %2 sc1"
         :
         : "v"(0u), "s"(lds_byte), "s"(sbase)
+        : "memory", "m0");
+}
+__device__ __forceinline__ void glds4_x(const void *sbase, unsigned voff, unsigned lds_byte) {
+    asm volatile(
+        "s_mov_b32 m0, %1\n\t"
+        "global_load_lds_dword %0, %2"
+        :
+        : "v"(voff), "s"(lds_byte), "s"(sbase)
+        : "memory", "m0");
+}
+__device__ __forceinline__ void glds4_x_sc1(const void *sbase, unsigned voff, unsigned lds_byte) {
+    asm volatile(
+        "s_mov_b32 m0, %1\n\t"
+        "global_load_lds_dword %0, %2 sc1"
+        :
+        : "v"(voff), "s"(lds_byte), "s"(sbase)
         : "memory", "m0");
 }
 // vmcnt wait that is also a compiler memory barrier (LDS written by DMA is read after it; stores
@@ -676,22 +697,32 @@ __device__ __forceinline__ bool x_wait(const XPair &xp, const unsigned *xw, unsi
     X_CNT(3);
     return false;
 }
-// this wave's 4 rows of the partner's half, exchange slot `src` -> LDS ring rows at `dst`
-// (2 DMA instructions: 1 KiB + 64 B)
-__device__ __forceinline__ void x_import(const char *src, unsigned dst, int wu, int lane) {
-    if (X_EXP_NOIMPORT) {  // keep the instruction count: 2 dword loads of the flag line instead
-        glds16_sc1<0>(src, 0u, dst + (unsigned)(wu * 4 * D_RS));
-        if (lane < 4) glds16_sc1<1024>(src, 0u, dst + (unsigned)(wu * 4 * D_RS));
+// this wave's 4 rows of the partner's half (rows 4 wu .. + 3 of half pw), exchange slot `src` ->
+// the ring slot at LDS byte `slot`: one LDS-DMA per 256-B row (16 lanes) + the rows' 4 key
+// shifts (4 lanes) -- 5 instructions per wave
+__device__ __forceinline__ void x_import(const char *src, unsigned slot, int pw, int wu, int lane) {
+    if (X_EXP_NOIMPORT) {  // keep the instruction count: re-read one chunk
+#pragma unroll
+        for (int k = 0; k < 5; k++)
+            if (lane < 4) glds16<0>(src, 0u, slot + (unsigned)((32 * pw + 4 * wu + k) * D_RS));
         return;
     }
-    const unsigned v = (unsigned)(wu * 4 * D_RS + 16 * lane);
-    const unsigned d = dst + (unsigned)(wu * 4 * D_RS);
-    if (X_UNIQUE) {
-        glds16<0>(src, v, d);
-        if (lane < 4) glds16<1024>(src, v + 1024u, d);
-    } else {
-        glds16_sc1<0>(src, v, d);
-        if (lane < 4) glds16_sc1<1024>(src, v + 1024u, d);
+    if (lane < 16) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int row = 4 * wu + k;
+            if (X_UNIQUE)
+                glds16<0>(src, (unsigned)(row * KD + 16 * lane), slot + (unsigned)((32 * pw + row) * D_RS));
+            else
+                glds16_sc1<0>(src, (unsigned)(row * KD + 16 * lane), slot + (unsigned)((32 * pw + row) * D_RS));
+        }
+    }
+    if (lane < 4) {
+        const unsigned so = (unsigned)(32 * KD + wu * 128 + 4 * lane), sd = slot + (unsigned)(D_TILE + (32 * pw + 4 * wu) * 4);
+        if (X_UNIQUE)
+            glds4_x(src, so, sd);
+        else
+            glds4_x_sc1(src, so, sd);
     }
 }
 // SOLO: this thread's 16 values of the partner half of `tile` quantised here (frame 1 in memory)
@@ -705,7 +736,7 @@ __device__ __forceinline__ void x_solo(char *rq, const float *B, int tile, int p
     h.pack01();
     h.pack23();
     *reinterpret_cast<i32x4 *>(rq + row * D_RS + (sub << 4)) = h.code;
-    if (sub == 0) *reinterpret_cast<int *>(rq + row * D_RS + KD) = h.sh;
+    if (sub == 0) reinterpret_cast<int *>(rq + D_TILE)[row] = h.sh;
 }
 // the statistics of half pw of every tile, from frame 1 in memory (the partner's are missing)
 __device__ __forceinline__ Sweep x_stats(const float *B, int pw, int n1, int t, int tb) {
@@ -748,7 +779,7 @@ __device__ __forceinline__ Sweep sweep_x(char *lds, const float *B, int n1, int 
     const int ntc = (n1 + BN - 1) / BN;  // >= 3 (the kernel's condition)
     const int fr = lane & 31, fh = lane >> 5, w = xp.w, pw = 1 - w;
     char *ring = lds + X_OFF_RING;
-    const unsigned ring_l = lds_base + X_OFF_RING + (unsigned)(32 * pw * D_RS);  // partner rows of slot 0
+    const unsigned ring_l = lds_base + X_OFF_RING;  // ring slot 0
     unsigned *xw = reinterpret_cast<unsigned *>(lds + D_OFF_X);  // [NW] flags, [NW] solo
     const unsigned fw_l = lds_base + D_OFF_X + 4u * (unsigned)wu;
     Sweep st = {0.f, 0.f, false};
@@ -804,14 +835,14 @@ __device__ __forceinline__ Sweep sweep_x(char *lds, const float *B, int n1, int 
     // must also mean "past the import of tile 0", which exchange slot 0's reuse relies on)
     // the partner halves of tiles 0, 1
     if (x_wait(xp, xw, fw_l, wu, lane, 2u) && !(X_FORCE_SOLO && xp.solo_at == 0)) {
-        x_import(xp.par, ring_l, wu, lane);
-        x_import(xp.par + X_SLOT, ring_l + (unsigned)X_RSLOT, wu, lane);
+        x_import(xp.par, ring_l, pw, wu, lane);
+        x_import(xp.par + X_SLOT, ring_l + (unsigned)X_RSLOT, pw, wu, lane);
     } else {
         go_solo();
         x_solo(ring, B, 0, pw, n1, t, tb);
         x_solo(ring + X_RSLOT, B, 1, pw, n1, t, tb);
     }
-    bool pend = !wsolo;  // the newest VMEM instructions are an import (2 per wave)
+    bool pend = !wsolo;  // the newest VMEM instructions are an import (5 per wave)
 
     const int rdb = fr * D_RS + fh * 16;
     i32x16 acc[RG][2];
@@ -873,7 +904,7 @@ __device__ __forceinline__ Sweep sweep_x(char *lds, const float *B, int n1, int 
 
     for (int tc = 0; tc < ntc; tc++) {
         if (pend)
-            wait_vm_mem<2>();  // staging of tile tc + 3, own stores of tile tc + 2, the import of tile tc
+            wait_vm_mem<5>();  // staging of tile tc + 3, own stores of tile tc + 2, the import of tile tc
         else
             wait_vm_mem<0>();
         __syncthreads();  // tile tc complete in its ring slot; every wave's stores done
@@ -892,8 +923,8 @@ __device__ __forceinline__ Sweep sweep_x(char *lds, const float *B, int n1, int 
         QHalf<true> qh;
         const unsigned gp_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)max(tc - 1, 0));
         X_SEG(0, 1, gp_, 0);
-        sh0 = *reinterpret_cast<const int *>(rs + fr * D_RS + KD);  // the key shifts of tile tc's columns
-        sh1 = *reinterpret_cast<const int *>(rs + (fr + 32) * D_RS + KD);
+        sh0 = reinterpret_cast<const int *>(rs + D_TILE)[fr];  // the key shifts of tile tc's columns
+        sh1 = reinterpret_cast<const int *>(rs + D_TILE)[fr + 32];
         const bool poll = imp && !wsolo;
         if (poll && lane == 0) glds4_sc1(xp.fpar, fw_l);
         const unsigned gc_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)tc);
@@ -913,7 +944,7 @@ __device__ __forceinline__ Sweep sweep_x(char *lds, const float *B, int n1, int 
             }
             if (!wsolo) {
                 x_import((X_EXP_OWNIMPORT ? (const char *)xp.own : xp.par) + ((tc + 2) % XR) * X_SLOT,
-                         ring_l + (unsigned)(((tc + 2) & 3) * X_RSLOT), wu, lane);
+                         ring_l + (unsigned)(((tc + 2) & 3) * X_RSLOT), pw, wu, lane);
                 X_CNT(7);
                 pend = true;
             } else {

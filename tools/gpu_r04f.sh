@@ -8,4 +8,4 @@ mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 TESTS_FOR="${TESTS_FOR:-xch xsolo}" VARIANTS="${VARIANTS:-ship xch}" AB_STEPS=20 AB_SCORE=5 \
     bash tools/gpu_ab.sh || exit $?
-TRACES="${TRACES:-xch_trace:0.01875 xch_trace:0.05}" bash tools/gpu_trace_exp.sh || exit $?
+TRACES="${TRACES:-xch_trace:0.01875}" bash tools/gpu_trace_exp.sh || exit $?
