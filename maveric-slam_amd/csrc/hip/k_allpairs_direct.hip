@@ -58,7 +58,16 @@ constexpr int D_OFF_ROW = D_OFF_RING + 2 * D_SLOT > 2 * D_HALF + 4 * D_SLOT ? D_
                                                                            : 2 * D_HALF + 4 * D_SLOT;
 constexpr int D_OFF_MISC = D_OFF_ROW + D_BM * 8;                    // [NW][4] per-wave statistics
 constexpr int D_OFF_X = D_OFF_MISC + D_NW * 16;                     // pair exchange: flags, SOLO, statistics
-constexpr int D_LDS = D_OFF_X + 64;
+#ifndef D_COLWIN
+#define D_COLWIN 1  // the epilogue's window per maximiser column (0: the pair's widest, for A/B)
+#endif
+constexpr int D_OFF_COL = D_OFF_X + 64;  // integer path: each frame-1 column's key shift (1 B)
+constexpr int D_NCOL = 64 * BN;           // the integer path's column limit (2 ntc <= 128)
+#ifndef D_EXACT_EA
+#define D_EXACT_EA 0  // the A phase measures each row's quantisation residual (rowe) for the window
+#endif
+constexpr int D_OFF_ROWE = D_OFF_COL + D_NCOL;  // [BM] float |rho|^2 per row (D_EXACT_EA)
+constexpr int D_LDS = D_OFF_ROWE + (D_EXACT_EA ? D_BM * 4 : 0);
 constexpr int D_OFF_AIMG = 2 * D_HALF;  // A images: staging slot 2 + the ring (before the sweep)
 static_assert(D_OFF_AIMG + D_NW * 32 * KD <= D_OFF_ROW, "A images fit staging slot 2 + the ring");
 static_assert(epi_bytes<D_NW>() <= D_OFF_ROW, "the epilogue fits staging + ring");
@@ -306,11 +315,16 @@ struct QHalf {
             qa = bn * bn;  // an upper bound of |b_j|^2 (the window's Bn)
         }
     }
-    __device__ __forceinline__ void store(char *rq, int hh, int t, bool live, float &smax, float &b2max, bool &bad) {
+    // cs: the tile's entries of the per-column key shifts kept for the epilogue (IK; live halves)
+    __device__ __forceinline__ void store(char *rq, int hh, int t, bool live, float &smax, float &b2max, bool &bad,
+                                          unsigned char *cs) {
         const int r = t >> 4, sub = t & 15, row = 32 * hh + r;
         *reinterpret_cast<i32x4 *>(rq + row * D_RS + (D_PAD ? sub << 4 : (sub ^ (row & 15)) << 4)) = code;
         if constexpr (IK) {
-            if (sub == 0) reinterpret_cast<int *>(rq + D_TILE)[row] = sh;
+            if (sub == 0) {
+                reinterpret_cast<int *>(rq + D_TILE)[row] = sh;
+                if (live) cs[row] = (unsigned char)sh;
+            }
             bad = bad | (live & !((qa <= 1e30f) & (m <= IK_MMAX)));  // CC: m carries any NaN
         } else {
             if (sub == 0) reinterpret_cast<float *>(rq + D_TILE)[row] = s;
@@ -357,6 +371,7 @@ __device__ __forceinline__ Sweep sweep(char *lds, const float *B, int n1, int t,
     const int ntc = (n1 + BN - 1) / BN, nh = 2 * ntc;  // column tiles, staging halves (>= 2)
     const int fr = lane & 31, fh = lane >> 5;
     char *ring = lds + D_OFF_RING;
+    unsigned char *colsh = reinterpret_cast<unsigned char *>(lds + D_OFF_COL);
     Sweep st = {0.f, 0.f, false};
     if (!first) {
         dma_half(B, 0, n1, wu, chunk16, lds_base);
@@ -379,7 +394,7 @@ __device__ __forceinline__ Sweep sweep(char *lds, const float *B, int n1, int t,
             h.reduce(32 * hh + (t >> 4), n1, tb);
             h.pack01();
             h.pack23();
-            h.store(ring, hh, t, true, st.smax, st.b2max, st.bad);
+            h.store(ring, hh, t, true, st.smax, st.b2max, st.bad, colsh);
         }
     }
     __syncthreads();  // tile 0 in ring slot 0; staging slots 0, 1 free
@@ -444,7 +459,7 @@ __device__ __forceinline__ Sweep sweep(char *lds, const float *B, int n1, int t,
             else if (s_ == QS_LOAD + 3) qh_.reduce((J0) + (t >> 4), n1, tb);                 \
             else if (s_ == QS_LOAD + 4) qh_.pack01();                                        \
             else if (s_ == QS_LOAD + 5) qh_.pack23();                                        \
-            else if (s_ == QS_LOAD + 6) qh_.store(rq, (HH), t, (LIVE), st.smax, st.b2max, st.bad); \
+            else if (s_ == QS_LOAD + 6) qh_.store(rq, (HH), t, (LIVE), st.smax, st.b2max, st.bad, colsh + (tc + 1) * BN); \
             if (s_ < KD / 32) {                                                              \
                 const int ch_ = D_PAD ? 32 * s_ : ((2 * s_) ^ xs_) * 16;                     \
                 b0_[s_] = *reinterpret_cast<const i32x4 *>(base + ch_);                      \
@@ -1062,8 +1077,9 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, con
     dma_half(B, xmode ? tr : 0, n1, wu, chunk16, lds_base);
     dma_half(B, xmode ? 2 + tr : 1, n1, wu, chunk16, lds_base + D_HALF);
     i32x4 aI[RG][KD / 32];
-    a_phase<false, D_QB>(lds + D_OFF_AIMG + w * 32 * KD, rowv, w * 64, row0, n0, lane, A, nullptr, nullptr, nullptr,
-                         false, aI);
+    float *rowe = D_EXACT_EA ? reinterpret_cast<float *>(lds + D_OFF_ROWE) : nullptr;
+    a_phase<false, D_QB, D_EXACT_EA>(lds + D_OFF_AIMG + w * 32 * KD, rowv, w * 64, row0, n0, lane, A, nullptr,
+                                     nullptr, nullptr, false, aI, rowe);
     D_STAMP(1);
     __syncthreads();  // the A images (staging slot 2 + the ring) are consumed
     float m1[RG][16], m2[RG][16];
@@ -1084,8 +1100,11 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, con
         if (!st.bad) {
             const double Bn = sqrt((double)st.b2max) * 1.0001;
             const double Eb = 8.0001 * (double)st.smax + 1e-30;  // exact power-of-two scaling
+            // the window per maximiser column (its own 1 / q_j) unless the exchange ran
             epilogue<D_NW, true>(lds, rowv, m1, m2, Bn, Eb, false, tbi, ~((1u << tbi) - 1u), w, lane, row0, n0,
-                                 n1, A, B, oidx, oscore, thresh, dmode, 1.0 / 508.0);
+                                 n1, A, B, oidx, oscore, thresh, dmode, 1.0 / 508.0,
+                                 xmode || !D_COLWIN ? nullptr : reinterpret_cast<const unsigned char *>(lds + D_OFF_COL),
+                                 rowe);
             D_STAMP(3);
 #ifdef MV_TRACE
             if (lane == 0 && blockIdx.x < D_TRACE_BLOCKS) {

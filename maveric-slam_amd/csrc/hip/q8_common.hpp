@@ -245,11 +245,14 @@ __device__ __forceinline__ bool better(int dmode, float v, int j, float bv, int 
 //      rowv[r] = (|a|^2, s_a); s_a < 0 marks a row for the exact path (non-finite, zero or out
 //      of range).  AI8 (sequence mode): the rows arrive already quantised by k_q8_split (q0,
 //      s0, |a|^2, pair flag bad0) and are copied (256 B per row). ----
-template <bool AI8, int QB = 4>  // QB: row quads (4 loads per lane each) in flight
+//      EA: also rowe[r] = |rho|^2, the row's quantisation residual in code units (rho_k = a_k q -
+//      c_k, from the same magic sum), so that the epilogue's A term is s_a |rho| + |1 - q s_a| |a|
+//      instead of the worst case 8 s_a (every component off by half a step).
+template <bool AI8, int QB = 4, bool EA = false>  // QB: row quads (4 loads per lane each) in flight
 __device__ __forceinline__ void a_phase(char *img, float2 *rowv, int rbase, int row0, int n0, int lane,
                                         const float *__restrict__ A, const char *__restrict__ QA,
                                         const float *__restrict__ s0p, const float *__restrict__ na2p, bool bad0,
-                                        i32x4 (&aI)[RG][KD / 32]) {
+                                        i32x4 (&aI)[RG][KD / 32], float *rowe = nullptr) {
     const int fr = lane & 31, fh = lane >> 5;
     const int sub = lane & 15, rq = lane >> 4;
 #pragma unroll
@@ -310,6 +313,22 @@ __device__ __forceinline__ void a_phase(char *img, float2 *rowv, int rbase, int 
                     const float q = m > 0.f ? 127.f * __builtin_amdgcn_rcpf(m) : 0.f;
                     const bool afull = !(q2 <= FLT_MAX) || m < SCALE_LO || m > SCALE_HI;  // zero rows too
                     if (sub == 0) rowv[rbase + g * 32 + r] = make_float2(q2, afull ? -1.f : m * (1.f / 127.f));
+                    if constexpr (EA) {
+                        float r2 = 0.f;
+#pragma unroll
+                        for (int u = 0; u < 4; u++)
+#pragma unroll
+                            for (int i = 0; i < 4; i++) {
+                                const float f = __builtin_fmaf(x[qd][u][i], q, MAGIC_RNE);  // pack4's sum
+                                const float rho = __builtin_fmaf(x[qd][u][i], q, MAGIC_RNE - f);
+                                r2 = __builtin_fmaf(rho, rho, r2);
+                            }
+                        r2 += swz_xor<1>(r2);
+                        r2 += swz_xor<2>(r2);
+                        r2 += swz_xor<4>(r2);
+                        r2 += swz_xor<8>(r2);
+                        if (sub == 0) rowe[rbase + g * 32 + r] = r2;
+                    }
                     char *rowp = img + r * KD + 4 * (sub & 3);
 #pragma unroll
                     for (int u = 0; u < 4; u++)  // k = 4 sub + 64 u: chunk (sub >> 2) + 4 u
@@ -341,7 +360,8 @@ __device__ __forceinline__ void epilogue(char *epi, const float2 *rowv, float (&
                                          double Bn, double Eb, bool flagged, int tb, unsigned tkeep, int w, int lane,
                                          int row0, int n0, int n1, const float *__restrict__ A,
                                          const float *__restrict__ B, int *__restrict__ oidx,
-                                         float *__restrict__ oscore, double thresh, int dmode, double bscale = 1.0) {
+                                         float *__restrict__ oscore, double thresh, int dmode, double bscale = 1.0,
+                                         const unsigned char *colsh = nullptr, const float *rowe = nullptr) {
     const int fr = lane & 31, fh = lane >> 5;
     const double u24 = 5.9604644775390625e-08;
     const double gam_e = KD * u24 / (1.0 - KD * u24);
@@ -417,21 +437,38 @@ __device__ __forceinline__ void epilogue(char *epi, const float2 *rowv, float (&
         if (live && !full) {
             const double s_a = (double)rv.y;
             const double an = sqrt(fmax((double)rv.x, 0.0)) * 1.0001;
-            const double ea = 8.001 * s_a + 4.76837158203125e-07 * an;  // |1 - q s_a| < 2^-21
+            // |eps_a| <= s_a |rho| + |1 - q s_a| |a| (|1 - q s_a| < 2^-21); |rho| <= 8 without rowe
+            // (rowe: the fp32 sum of the squared residuals, relative error < 2^-18)
+            const double ea = (rowe ? s_a * (sqrt((double)rowe[rl] * 1.0001) + 1e-15) : 8.001 * s_a) +
+                              4.76837158203125e-07 * an;
             const double dq = (an * Eb + ea * Bn + ea * Eb) * 1.0001;
             const double delta = dq + u24 * (an * Bn + dq) * 1.01 + gam_e * an * Bn + 1e-30;
             const double sa_k = s_a * bscale;  // screen units -> units of a.b
             const double Ms = kval(M) * sa_k;
             const double M2s = kgt(M2, kneg) ? kval(M2) * sa_k : -__builtin_inf();
             const double dp = delta + 2.2 * rho * (fabs(Ms) + 2.0 * delta);
+            // colsh (IK): the window of the maximiser's own column I -- its 1 / q_I instead of the
+            // pair's max (Eb = 8 max_j 1 / q_j): |e_I - screen_I| <= dpI, every other column keeps
+            // dp.  So: no match when M + dpI <= thresh and M2 + dp <= thresh (no other column can
+            // clear it); competitors reach M - dpI - dp; sure when M - dpI > thresh
+            double dpI = dp;
+            if (IK && colsh && !dmode) {
+                const int I0 = kcol(M, E);
+                if (I0 < n1) {
+                    const int eI = tb + 2 - (int)colsh[I0];
+                    const double EbI = 8.0001 * (double)__builtin_ldexpf(1.f / 127.f, -eI) + 1e-30;
+                    const double dqI = (an * EbI + ea * Bn + ea * EbI) * 1.0001;
+                    dpI = fmin(dp, dqI + u24 * (an * Bn + dqI) * 1.01 + gam_e * an * Bn + 1e-30);
+                }
+            }
             // competitors: columns whose exact score can reach the maximiser's; for the distance
             // (dmode 1) also every column that can clip to 1 with it (distance-0 ties), and a
             // maximiser that can clip to -1 ties every column (all distances 2)
-            const double lo = dmode ? fmin(Ms - 2.0 * dp, 1.0 - dp) - tie : Ms - 2.0 * dp;
+            const double lo = dmode ? fmin(Ms - 2.0 * dp, 1.0 - dp) - tie : Ms - dpI - dp;
             if (dmode && Ms - dp <= -1.0 + tie) {
                 wide = true;
                 if (fh == 0) lmask[rl] = 0xffffffffu;
-            } else if (Ms + dp > thresh) {
+            } else if (Ms + dpI > thresh || M2s + dp > thresh) {
                 if (M2s < lo) {
                     const int I = kcol(M, E);
                     if (I >= n1) {  // a padding column on top (IK: all real dots below 0); never read past n1
@@ -440,7 +477,7 @@ __device__ __forceinline__ void epilogue(char *epi, const float2 *rowv, float (&
                     } else {
                         // decision-only (no score output): every exact score inside the window
                         // clears both tests -- the maximiser's exact dot decides nothing
-                        const bool sure = !oscore && (dmode || Ms - dp > fmax(thresh, 0.0));
+                        const bool sure = !oscore && (dmode || Ms - dpI > fmax(thresh, 0.0));
                         if (!sure) {
                             need = I;  // scored below, after both groups, by lane half g
                         } else if (fh == 0) {

@@ -320,6 +320,42 @@ def test_allpairs_f32_quantisation_stress(ctx, screen, orc, torch_cuda):
                     assert (bits(sc[k, :x.shape[0]]) == bits(s2)).all(), (thr, k)
 
 
+def test_allpairs_f32_column_windows(ctx, screen, orc, torch_cuda):
+    """The one-pass screen decides each row on the window of its maximiser's own column (1 / q_j
+    of that column, k_allpairs_direct.hip D_COLWIN) instead of the pair's widest: frame-1 columns
+    of all three integer-key exponents (plain unit rows: e = 2; one component at 0.35 / 0.7 of
+    the norm: e = 1 / 0), queries re-observing them with cosines that straddle the threshold, so
+    that both sides of every window and the competitor bound (M - dp_I - dp) are exercised."""
+    rng = np.random.default_rng(47)
+
+    def frame1(n1):
+        b = rng.standard_normal((n1, 256)).astype(np.float32)
+        for j, v in zip(rng.choice(n1, 2 * n1 // 5, replace=False), [0.35, 0.7] * n1):
+            c = rng.integers(256)
+            b[j, c] = 0.0
+            b[j] *= np.float32(np.sqrt(1.0 - v * v)) / np.linalg.norm(b[j])
+            b[j, c] = np.float32(v) * rng.choice([-1.0, 1.0])
+        b[:, :] /= np.linalg.norm(b, axis=1, keepdims=True)
+        return b.astype(np.float32)
+
+    pairs = []
+    for n0, n1 in ((700, 600), (300, 1000)):
+        b = frame1(n1)
+        src = rng.integers(0, n1, n0)
+        sig = rng.uniform(0.03, 0.065, n0).astype(np.float32)[:, None]
+        a = b[src] + sig * rng.standard_normal((n0, 256)).astype(np.float32)
+        a /= np.linalg.norm(a, axis=1, keepdims=True)
+        pairs.append((a.astype(np.float32), b))
+    for thr in (0.8, 0.76, 0.83):
+        for scores in (False, True):
+            idx, sc = run_f32(ctx, torch_cuda, pairs, thresh=thr, scores=scores)
+            for k, (x, y) in enumerate(pairs):
+                i2, s2 = orc.allpairs_f32(x, y, thr)
+                assert (idx[k, :x.shape[0]] == i2).all(), (thr, k, int((idx[k, :x.shape[0]] != i2).sum()))
+                if scores:
+                    assert (bits(sc[k, :x.shape[0]]) == bits(s2)).all(), (thr, k)
+
+
 def _batch_f32(torch, pairs, cap):
     B = len(pairs)
     D0 = np.zeros((B, cap, 256), np.float32)
