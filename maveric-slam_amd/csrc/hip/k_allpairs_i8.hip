@@ -68,6 +68,73 @@ __global__ __launch_bounds__(256) void k_i8_norms(long rows, const int8_t *__res
     }
 }
 
+// Integer keys (I8_KEYS, the default while 2 ntc <= 256): frame 1 is re-quantised per column to
+// unit-norm codes c_jk = RNE(b_jk s_j), s_j = RN(127 / |b_j|) (|c_jk| <= 127 since |b_jk| <= |b_j|),
+// so that the exact integer D~_ij = a_i . c_j is 127 X_ij (X = dot / |b_j|, the cosine times |a|)
+// within delta_i = (8 + 1.3e-4) |a_i| for EVERY column (|a . rho_j| <= |a| |rho_j| <= 8 |a|, the
+// s_j |b_j| = 127 (1 + eta), |eta| < 1e-6 term) -- one scale for the whole row, so the fold needs no
+// per-column multiply: key = (D~ << tb) | tag (one v_lshl_or_b32), v_max3_i32 / v_med3_i32 /
+// v_max_i32 top-2 (2.5 VALU per value against the float screen's 3.5).  The decisions stay the
+// exact integer dots with the ORIGINAL codes.  Rows [n1, cap64) of a pair are zero codes (the
+// match's tiles need no clamp; padding columns are excluded by index).  Measured (one box,
+// profiles/r04m_i8_keys_ab.log): k_i8_match 2.25 vs 2.33 ms, but k_i8_prep's extra 512 KiB per pair
+// written and read costs 0.35 vs k_i8_norms' 0.20 ms -- the C4 step is 3 % SLOWER, so off.  The
+// fold's VALU was not what held the MFMA pipe at ~50 %: 25 % fewer VALU per tile bought 3.5 %.
+#ifndef I8_KEYS
+#define I8_KEYS 0
+#endif
+__global__ __launch_bounds__(256) void k_i8_prep(int batch, int cap, int cap64, const int *__restrict__ n1v,
+                                                 const int8_t *__restrict__ d, int *__restrict__ nrm,
+                                                 float *__restrict__ rnrm, int8_t *__restrict__ q1) {
+    const int t = threadIdx.x, sub = t & 15;
+    const long R = (long)batch * cap64;
+    const long base = (long)blockIdx.x * (16 * NRM_U) + (t >> 4);
+    int4 x[NRM_U];
+#pragma unroll
+    for (int u = 0; u < NRM_U; u++) {
+        const long r = base + 16 * u;
+        const long pr = r / cap64;
+        const int jj = (int)(r - pr * cap64);
+        const bool on = r < R && jj < min(max(n1v[min(pr, (long)batch - 1)], 0), cap);
+        x[u] = on ? reinterpret_cast<const int4 *>(d + (pr * cap + jj) * KD)[sub] : make_int4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < NRM_U; u++) {
+        int s = __builtin_amdgcn_sdot4(x[u].x, x[u].x, 0, false);
+        s = __builtin_amdgcn_sdot4(x[u].y, x[u].y, s, false);
+        s = __builtin_amdgcn_sdot4(x[u].z, x[u].z, s, false);
+        s = __builtin_amdgcn_sdot4(x[u].w, x[u].w, s, false);
+        s += swz_xor_i8(s, 1);
+        s += swz_xor_i8(s, 2);
+        s += swz_xor_i8(s, 4);
+        s += swz_xor_i8(s, 8);
+        const float rb = s > 0 ? 1.0f / sqrtf((float)s) : 0.f;
+        const float sc = 127.f * rb;
+        const int w4[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
+        int o4[4];
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+            unsigned f[4];
+#pragma unroll
+            for (int e = 0; e < 4; e++)  // magic sum: the low byte is RNE(b sc), two's complement
+                f[e] = __float_as_uint(__builtin_fmaf((float)((w4[v] << (24 - 8 * e)) >> 24), sc, 12582912.f));
+            const unsigned p01 = __builtin_amdgcn_perm(f[1], f[0], 0x0c0c0400u);
+            const unsigned p23 = __builtin_amdgcn_perm(f[3], f[2], 0x0c0c0400u);
+            o4[v] = (int)__builtin_amdgcn_perm(p23, p01, 0x05040100u);
+        }
+        const long r = base + 16 * u;
+        if (r < R) {
+            reinterpret_cast<int4 *>(q1 + r * KD)[sub] = make_int4(o4[0], o4[1], o4[2], o4[3]);
+            const long pr = r / cap64;
+            const int jj = (int)(r - pr * cap64);
+            if (sub == 0 && jj < cap) {
+                nrm[pr * cap + jj] = s;
+                if (rnrm) rnrm[pr * cap + jj] = rb;
+            }
+        }
+    }
+}
+
 // candidate (dot, nb, j) strictly better than current best?  max dot^2/nb, ties -> lower j
 __device__ __forceinline__ bool better(long long d, long long nb, int j, long long bd, long long bn, int bj) {
     if (bj < 0) return true;
@@ -151,6 +218,21 @@ __device__ __forceinline__ void fold3_i8(float a, float b, float &m1, float &m2)
     asm("v_max_f32 %0, %1, %2" : "=v"(m2) : "v"(m2), "v"(md));
 }
 
+// two values of one row into its lane-local top-2 on integer keys (D << sh) | tag (sh: the tag
+// width, a VGPR; tags in SGPRs) -- one asm block, no hazard padding between its instructions
+__device__ __forceinline__ void fold_keys_i8(int a, int b, int sh, unsigned ta, unsigned tb, float &m1f, float &m2f) {
+    int ka, kb, md, m1 = __float_as_int(m1f), m2 = __float_as_int(m2f);
+    asm("v_lshl_or_b32 %0, %5, %7, %8\n\t"
+        "v_lshl_or_b32 %1, %6, %7, %9\n\t"
+        "v_med3_i32 %2, %3, %0, %1\n\t"
+        "v_max3_i32 %3, %3, %0, %1\n\t"
+        "v_max_i32 %4, %4, %2"
+        : "=&v"(ka), "=&v"(kb), "=&v"(md), "+v"(m1), "+v"(m2)
+        : "v"(a), "v"(b), "v"(sh), "s"(ta), "s"(tb));
+    m1f = __int_as_float(m1);
+    m2f = __int_as_float(m2);
+}
+
 // D = 0x40800000 (the bits of 4.0) + A.B: the first k32 step of a chain, C as the inline
 // constant 4.0 (a builtin with a constant C gets it hoisted into 16 VGPRs); the chain's next
 // MFMA reads D as SrcC with exact overlap (hardware forwarding, no wait states)
@@ -159,11 +241,13 @@ __device__ __forceinline__ i32x16 mfma_i8_from4_m(i32x4 a, i32x4 b) {
     asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, 4.0" : "=&v"(d) : "v"(a), "v"(b));
     return d;
 }
+template <bool KEYS>
 __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, const int *__restrict__ n0v,
                                                       const int *__restrict__ n1v, const int8_t *__restrict__ desc0,
                                                       const int8_t *__restrict__ desc1, const int *__restrict__ nb_v,
                                                       const float *__restrict__ rnb_v, int *__restrict__ match_idx,
-                                                      int *__restrict__ match_dot) {
+                                                      int *__restrict__ match_dot, const int8_t *__restrict__ q1v,
+                                                      int cap64) {
     __shared__ __attribute__((aligned(16))) char lds[M_LDS];
     int *na_s = reinterpret_cast<int *>(lds + M_OFF_NA);
     const int L = xcd_remap(blockIdx.x, gridDim.x);
@@ -183,13 +267,15 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
     const float *rnb = rnb_v + (size_t)pair * cap;
     const int *nb = nb_v + (size_t)pair * cap;
     const int ntc = (n1 + M_BN - 1) / M_BN;
+    // KEYS: the tiles stream the unit-norm codes (cap64 rows per pair, zero past n1: no clamp)
+    const int8_t *Bt = KEYS ? q1v + (size_t)pair * cap64 * KD : B;
 
     // ---- B DMA: wave w fills rows w*RPW .. +RPW-1 of a tile, 4 rows (1 KiB) per instruction;
     //      lane l -> row (l >> 4), chunk position l & 15, source chunk (l & 15) ^ (row & 15) ----
     const int wu = __builtin_amdgcn_readfirstlane(w);
     const int dr = wu * M_RPW + (lane >> 4);
     const unsigned dcb = (unsigned)((lane & 15) ^ (dr & 15)) * 16;
-    unsigned oB[M_DPW], oR;
+    unsigned oB[M_DPW], oR = 0;
     const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char *)lds;
     const unsigned dst_w = lds_base + (unsigned)(wu * M_RPW * KD);
     // + every wave copies the tile's 64 rsqrt|b|^2 (identical bytes) so that all waves
@@ -197,20 +283,20 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
     //   compiler's vmcnt waits drain the whole DMA ring
 #define I8_STAGE(SLOT)                                                                       \
     do {                                                                                     \
-        glds16_i8<0, (SLOT) * M_SLOT>(B, oB[0], dst_w);                                      \
-        glds16_i8<0, (SLOT) * M_SLOT + 4 * KD>(B, oB[1], dst_w);                             \
+        glds16_i8<0, (SLOT) * M_SLOT>(Bt, oB[0], dst_w);                                     \
+        glds16_i8<0, (SLOT) * M_SLOT + 4 * KD>(Bt, oB[1], dst_w);                            \
         if constexpr (M_DPW == 4) {                                                          \
-            glds16_i8<0, (SLOT) * M_SLOT + 8 * KD>(B, oB[M_DPW - 2], dst_w);                 \
-            glds16_i8<0, (SLOT) * M_SLOT + 12 * KD>(B, oB[M_DPW - 1], dst_w);                \
+            glds16_i8<0, (SLOT) * M_SLOT + 8 * KD>(Bt, oB[M_DPW - 2], dst_w);                \
+            glds16_i8<0, (SLOT) * M_SLOT + 12 * KD>(Bt, oB[M_DPW - 1], dst_w);               \
         }                                                                                    \
-        glds4_i8<(SLOT) * M_SLOT + M_TILE>(rnb, oR, lds_base);                               \
+        if constexpr (!KEYS) glds4_i8<(SLOT) * M_SLOT + M_TILE>(rnb, oR, lds_base);          \
     } while (0)
 #define I8_OFFSETS(TC)                                                                       \
     do {                                                                                     \
         const int nb_ = (TC) * M_BN + dr;                                                    \
         _Pragma("unroll") for (int g_ = 0; g_ < M_DPW; g_++)                                 \
-            oB[g_] = (unsigned)min(nb_ + 4 * g_, n1 - 1) * KD + (dcb ^ (64u * g_));          \
-        oR = (unsigned)min((TC) * M_BN + lane, n1 - 1) * 4;                                  \
+            oB[g_] = (unsigned)(KEYS ? nb_ + 4 * g_ : min(nb_ + 4 * g_, n1 - 1)) * KD + (dcb ^ (64u * g_)); \
+        if constexpr (!KEYS) oR = (unsigned)min((TC) * M_BN + lane, n1 - 1) * 4;             \
     } while (0)
     // prologue: tiles 0, 1, 2 issued before the A rows are read, so that both latencies overlap
     for (int g = 0; g < M_NBUF - 1 && g < ntc; g++) {
@@ -256,19 +342,27 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
     // lane index): top-2 tracking needs no index registers.  Columns past n1 get r = 0 (f = 0).
     i32x16 acc[M_RG][2];
     float m1[M_RG][16], m2[M_RG][16];
+    const float kinit = KEYS ? __int_as_float((int)0x80000000) : -__builtin_inff();
 #pragma unroll
     for (int g = 0; g < M_RG; g++)
 #pragma unroll
         for (int q = 0; q < 16; q++) {
-            m1[g][q] = -__builtin_inff();
-            m2[g][q] = -__builtin_inff();
+            m1[g][q] = kinit;
+            m2[g][q] = kinit;
         }
+    // "tile -1" of group 1, folded beside tile 0, never a maximum: float -3e38 (f = fma(0, 0,
+    // -3e38)); KEYS -2^22 (below every D~, |D~| <= 256 128 127 < 2^22)
 #pragma unroll
-    for (int q = 0; q < 16; q++) {  // "tile -1" of group 1, folded beside tile 0: -3e38, never a maximum
-        acc[1][0][q] = 0;
-        acc[1][1][q] = 0;
+    for (int q = 0; q < 16; q++) {
+        acc[1][0][q] = KEYS ? -(1 << 22) : 0;
+        acc[1][1][q] = KEYS ? -(1 << 22) : 0;
     }
-    const int tb = 2 * ntc <= 256 ? 8 : 32 - __builtin_clz(2 * ntc - 1);
+    // tag width: KEYS -- the smallest that holds 2 ntc tags (keys (D~ << tb) | tag within 31
+    // bits for tb <= 8); float -- 8 (the low mantissa bits) or wider
+    const int tb = KEYS ? (2 * ntc <= 2 ? 1 : 32 - __builtin_clz(2 * ntc - 1))
+                        : (2 * ntc <= 256 ? 8 : 32 - __builtin_clz(2 * ntc - 1));
+    int vsh = tb;
+    asm volatile("" : "+v"(vsh));  // the key shift as a VGPR operand (the tags take the SGPR slot)
     const unsigned tkeep = ~((1u << tb) - 1u);
     unsigned vkeep = tkeep;
     asm volatile("" : "+v"(vkeep));  // a VGPR operand: v_and_or_b32 may read one SGPR only
@@ -280,9 +374,13 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
 #define I8_FOLD2(FG, S, G0, R0, R1, C0, C1)                                                  \
     do {                                                                                     \
         _Pragma("unroll") for (int q = 2 * (S); q < 2 * (S) + 2; q++) {                      \
-            const float a_ = __builtin_fmaf(__int_as_float(acc[FG][0][q]), (R0), (C0));      \
-            const float b_ = __builtin_fmaf(__int_as_float(acc[FG][1][q]), (R1), (C1));      \
-            fold3_i8(tag_i8(a_, vkeep, (G0)), tag_i8(b_, vkeep, (G0) + 1u), m1[FG][q], m2[FG][q]); \
+            if constexpr (KEYS) {                                                            \
+                fold_keys_i8(acc[FG][0][q], acc[FG][1][q], vsh, (G0), (G0) + 1u, m1[FG][q], m2[FG][q]); \
+            } else {                                                                         \
+                const float a_ = __builtin_fmaf(__int_as_float(acc[FG][0][q]), (R0), (C0));  \
+                const float b_ = __builtin_fmaf(__int_as_float(acc[FG][1][q]), (R1), (C1));  \
+                fold3_i8(tag_i8(a_, vkeep, (G0)), tag_i8(b_, vkeep, (G0) + 1u), m1[FG][q], m2[FG][q]); \
+            }                                                                                \
         }                                                                                    \
     } while (0)
 #define I8_SEG(J, G, FG, G0, R0, R1, C0, C1)                                                 \
@@ -301,8 +399,14 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
             if (s_ >= PF) {                                                                  \
                 const int m_ = s_ - PF;                                                      \
                 if (m_ == 0) {                                                               \
-                    acc[G][0] = mfma_i8_from4_m(aI[G][0], b0_[0]);                           \
-                    acc[G][1] = mfma_i8_from4_m(aI[G][0], b1_[0]);                           \
+                    if constexpr (KEYS) {                                                    \
+                        const i32x16 z_ = {};                                                \
+                        acc[G][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][0], b0_[0], z_, 0, 0, 0); \
+                        acc[G][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][0], b1_[0], z_, 0, 0, 0); \
+                    } else {                                                                 \
+                        acc[G][0] = mfma_i8_from4_m(aI[G][0], b0_[0]);                       \
+                        acc[G][1] = mfma_i8_from4_m(aI[G][0], b1_[0]);                       \
+                    }                                                                        \
                 } else {                                                                     \
                     acc[G][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b0_[m_], acc[G][0], 0, 0, 0); \
                     acc[G][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b1_[m_], acc[G][1], 0, 0, 0); \
@@ -326,7 +430,7 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
         }                                                                                    \
         const unsigned gp_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)max(tc - 1, 0));  \
         I8_SEG(J, 0, 1, gp_, pr0, pr1, pc0, pc1);                                            \
-        {                                                                                    \
+        if constexpr (!KEYS) {                                                               \
             const float *rl_ = reinterpret_cast<const float *>(lds + (J) * M_SLOT + M_TILE); \
             const int col_ = tc * M_BN + fr;                                                 \
             const float s0_ = col_ < n1 ? rl_[fr] : 0.f, s1_ = col_ + 32 < n1 ? rl_[fr + 32] : 0.f; \
@@ -338,7 +442,7 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
         const unsigned gc_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)tc);              \
         I8_SEG(J, 1, 0, gc_, pr0, pr1, pc0, pc1);                                            \
         if (ntile < ntc) {                                                                   \
-            wait_vm_i8<(M_DPW + 1) * (M_NBUF - 2)>();                                                  \
+            wait_vm_i8<(M_DPW + (KEYS ? 0 : 1)) * (M_NBUF - 2)>();                           \
         } else {                                                                             \
             wait_vm_i8<0>();                                                                 \
         }                                                                                    \
@@ -396,20 +500,25 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
             e1[2 * i + 1] = v.z;
             e2[2 * i + 1] = v.w;
         }
-        float M = -__builtin_inff(), M2 = -__builtin_inff();
+        // key order: float compares of the tagged screen values, or signed-int compares of the
+        // key bits (KEYS)
+        auto kgt = [](float a, float b) { return KEYS ? __float_as_int(a) > __float_as_int(b) : a > b; };
+        auto kmax = [&](float a, float b) { return kgt(a, b) ? a : b; };
+        auto kmin = [&](float a, float b) { return kgt(a, b) ? b : a; };
+        float M = kinit, M2 = kinit;
         int E = 0;
 #pragma unroll
         for (int i = 0; i < 16; i++) {  // equal maxima land in M2: ambiguous
-            M2 = fmaxf(fmaxf(M2, e2[i]), fminf(M, e1[i]));
-            E = e1[i] > M ? fh * 16 + i : E;
-            M = fmaxf(M, e1[i]);
+            M2 = kmax(kmax(M2, e2[i]), kmin(M, e1[i]));
+            E = kgt(e1[i], M) ? fh * 16 + i : E;
+            M = kmax(M, e1[i]);
         }
         {
             const float oM = __shfl_xor(M, 32, 64), oM2 = __shfl_xor(M2, 32, 64);
             const int oE = __shfl_xor(E, 32, 64);
-            M2 = fmaxf(fmaxf(M2, oM2), fminf(M, oM));
-            E = (oM > M || (oM == M && oE < E)) ? oE : E;
-            M = fmaxf(M, oM);
+            M2 = kmax(kmax(M2, oM2), kmin(M, oM));
+            E = (kgt(oM, M) || (!kgt(M, oM) && oE < E)) ? oE : E;
+            M = kmax(M, oM);
         }
 
         // ---- decide the row in its own two lanes: exact integer dots with the screen
@@ -419,16 +528,37 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
         //      ("deep" row, below) ----
         const int rl = w * 64 + g * 32 + fr;
         const bool live = row0 + rl < n0;
-        const bool cand = live && na_r[g] > 0 && M > 1e-30f;  // else every dot <= 0 (tagged zeros are subnormal)
-        const float lim = M * keep_frac;
-        const bool ambig = cand && M2 >= lim;
+        // float: a column below M (1 - 2^(tb-21)) cannot be (or tie) the maximiser.  KEYS: with
+        // |D~_j - 127 X_j| <= da for every column, a column that can reach the maximiser's X has
+        // D~ >= M - 2 da, and no column has a positive dot when M + da <= 0
+        bool cand, ambig;
+        float lim = 0.f;
+        double limd = 0.0;
+        if constexpr (KEYS) {
+            // a match needs X > 0.9 |a| (100 dot^2 > 81 |a|^2 |b|^2, dot > 0): rows with M + da <=
+            // 127 0.9 |a| have none -- decided without a dot (most unmatched rows: without this their
+            // runner-ups, inside the wide window, would make them ambiguous)
+            const double an = sqrt((double)na_r[g]);
+            const double da = an * (8.0 + 1.3e-4) * 1.0001 + 1e-6;
+            const double Mv = (double)(__float_as_int(M) >> tb);
+            cand = live && na_r[g] > 0 && Mv + da > 0.0 && Mv + da > 114.3 * an * (1.0 - 1e-9);
+            limd = Mv - 2.0 * da;
+            ambig = cand && (double)(__float_as_int(M2) >> tb) >= limd;
+        } else {
+            cand = live && na_r[g] > 0 && M > 1e-30f;  // else every dot <= 0 (tagged zeros are subnormal)
+            lim = M * keep_frac;
+            ambig = cand && M2 >= lim;
+        }
+        auto inside_w = [&](float e) {
+            return KEYS ? (double)(__float_as_int(e) >> tb) >= limd : e >= lim;
+        };
         int nc = cand ? 1 : 0;
         if (ambig) {  // both lanes of the row take this branch
             unsigned in1 = 0, in2 = 0;
 #pragma unroll
             for (int i = 0; i < 16; i++) {
-                in1 |= (e1[i] >= lim ? 1u : 0u) << i;
-                in2 |= (e2[i] >= lim ? 1u : 0u) << i;
+                in1 |= (inside_w(e1[i]) ? 1u : 0u) << i;
+                in2 |= (inside_w(e2[i]) ? 1u : 0u) << i;
             }
             const unsigned o1 = __shfl_xor(in1, 32, 64), o2 = __shfl_xor(in2, 32, 64);
             const unsigned inside = fh ? (o1 | (in1 << 16)) : (in1 | (o1 << 16));
@@ -440,7 +570,7 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
                 int k = fh ? __popc(o1) : 0;
 #pragma unroll
                 for (int i = 0; i < 16; i++)
-                    if (e1[i] >= lim) {
+                    if (inside_w(e1[i])) {
                         const unsigned tag = __float_as_uint(e1[i]) & ~tkeep;
                         clist[rl * M_NCAND + k++] = (int)(tag >> 1) * M_BN + (int)(tag & 1) * 32 + fh * 16 + i;
                     }
@@ -448,10 +578,15 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
         }
         const unsigned tagM = __float_as_uint(M) & ~tkeep;
         const int I = (int)(tagM >> 1) * M_BN + (int)(tagM & 1) * 32 + E;
+        if (KEYS && cand && !ambig && I >= n1) {  // a padding column (zero codes) on top: all columns
+            nc = -1;
+            if (fh == 0) lmask[rl] = 0xffffffffu;
+        }
         int bj = -1;
         long long bd = 0, bn = 1;
         for (int k = 0; k < nc; k++) {  // the row's two lanes run the same trip count
             const int j = ambig ? clist[rl * M_NCAND + k] : I;
+            if (KEYS && j >= n1) continue;  // padding columns are listed, never scored
             const int8_t *brow = B + (size_t)j * KD + fh * 16;
             i32x4 bv[KD / 32];
 #pragma unroll
@@ -535,9 +670,12 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
 
 namespace mv {
 
+static bool i8_keys(int cap) { return I8_KEYS && 2 * ((cap + M_BN - 1) / M_BN) <= 256; }
+static int i8_cap64(int cap) { return (cap + M_BN - 1) / M_BN * M_BN; }
+
 size_t allpairs_i8_scratch_bytes(int batch, int cap) {
     const size_t rows = (size_t)batch * cap;
-    return 2 * align_up(4 * rows, 256);
+    return 2 * align_up(4 * rows, 256) + (i8_keys(cap) ? align_up((size_t)batch * i8_cap64(cap) * KD, 256) : 0);
 }
 
 int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
@@ -547,10 +685,17 @@ int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const i
     const size_t rows = (size_t)batch * cap;
     int *nb = (int *)scratch;
     float *rnb = (float *)((char *)scratch + align_up(4 * rows, 256));
-    MV_REQUIRE((rows + 16 * NRM_U - 1) / (16 * NRM_U) < (1l << 31));
-    const int nblk = (int)((rows + 16 * NRM_U - 1) / (16 * NRM_U));
-    MV_PROF_BEGIN(s, "k_i8_norms");
-    hipLaunchKernelGGL(k_i8_norms, dim3(nblk), dim3(256), 0, s, (long)rows, desc1, nb, rnb);
+    const bool keys = i8_keys(cap);
+    const int cap64 = i8_cap64(cap);
+    int8_t *q1 = keys ? (int8_t *)((char *)scratch + 2 * align_up(4 * rows, 256)) : nullptr;
+    const size_t prow = keys ? (size_t)batch * cap64 : rows;
+    MV_REQUIRE((prow + 16 * NRM_U - 1) / (16 * NRM_U) < (1l << 31));
+    const int nblk = (int)((prow + 16 * NRM_U - 1) / (16 * NRM_U));
+    MV_PROF_BEGIN(s, keys ? "k_i8_prep" : "k_i8_norms");
+    if (keys)
+        hipLaunchKernelGGL(k_i8_prep, dim3(nblk), dim3(256), 0, s, batch, cap, cap64, n1, desc1, nb, rnb, q1);
+    else
+        hipLaunchKernelGGL(k_i8_norms, dim3(nblk), dim3(256), 0, s, (long)rows, desc1, nb, rnb);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     const int tiles_m = (cap + M_BM - 1) / M_BM;
@@ -558,8 +703,13 @@ int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const i
     MV_REQUIRE(mblocks < (1l << 31));
     MV_REQUIRE((long)cap * KD < (1l << 31));  // 32-bit DMA source offsets within a pair
     MV_PROF_BEGIN(s, "k_i8_match");
-    hipLaunchKernelGGL(k_i8_match, dim3((unsigned)mblocks), dim3(M_NT), 0, s, tiles_m, cap, n0, n1, desc0, desc1, nb,
-                       rnb, match_idx, match_dot);
+    MV_REQUIRE((long)cap64 * KD < (1l << 31));
+    if (keys)
+        hipLaunchKernelGGL(k_i8_match<true>, dim3((unsigned)mblocks), dim3(M_NT), 0, s, tiles_m, cap, n0, n1, desc0,
+                           desc1, nb, rnb, match_idx, match_dot, q1, cap64);
+    else
+        hipLaunchKernelGGL(k_i8_match<false>, dim3((unsigned)mblocks), dim3(M_NT), 0, s, tiles_m, cap, n0, n1, desc0,
+                           desc1, nb, rnb, match_idx, match_dot, (const int8_t *)nullptr, cap64);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     return MV_OK;

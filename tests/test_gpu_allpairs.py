@@ -280,6 +280,43 @@ def test_allpairs_i8_ties_and_near_ties(ctx, orc, torch_cuda):
         assert i2[5] == -1 and (i2 >= 0).sum() > a.shape[0] // 8
 
 
+def test_allpairs_i8_key_window(ctx, orc, torch_cuda):
+    """k_i8_match's integer keys (unit-norm re-quantised frame 1, window (8 + 1.3e-4) |a| in
+    127-units): queries re-observed with noise that puts their cosines around the 0.9
+    threshold, spiky columns (one component carries the norm: codes +-127), columns that are
+    scaled copies of others (equal cosines, first index wins), and frame-1 lengths that leave a
+    partial last tile (zero-code padding columns)."""
+    rng = np.random.default_rng(77)
+    pairs = []
+    for na, nb in ((700, 650), (333, 1027)):
+        b = np.clip(np.round(rng.standard_normal((nb, 256)) * 24), -128, 127)
+        sp = rng.choice(nb, nb // 8, replace=False)
+        b[sp] = np.round(b[sp] * 0.1)
+        b[sp, rng.integers(0, 256, sp.size)] = rng.choice([-127, 127], sp.size)
+        half = rng.choice(nb, nb // 10, replace=False)
+        b[half[1:]] = np.round(b[half[:-1]] / 2) * 1  # near copies at half scale
+        src = rng.integers(0, nb, na)
+        sig = rng.uniform(8.0, 15.0, na)[:, None]
+        a = np.clip(np.round(b[src] + rng.standard_normal((na, 256)) * sig), -128, 127)
+        pairs.append((a.astype(np.int8), b.astype(np.int8)))
+    idx, dot = run_i8(ctx, torch_cuda, pairs, cap=1100, decoys=True)
+    for q, (a, c) in enumerate(pairs):
+        i2, d2 = orc.allpairs_i8(a, c)
+        assert (idx[q, :a.shape[0]] == i2).all() and (dot[q, :a.shape[0]] == d2).all(), q
+        assert 0 < (i2 >= 0).sum() < a.shape[0]
+
+
+@pytest.mark.parametrize("n1,cap", [(8000, 8192), (8300, 8300)])
+def test_allpairs_i8_long_frame1(ctx, orc, torch_cuda, n1, cap):
+    """8192 columns: the widest integer-key tags (2 ntc = 256, tb = 8); past that the float
+    screen (k_i8_match<false>, wider tags)."""
+    a, b = synth.synth_pair_i8(90, n=n1)
+    a = a[:96].copy()
+    idx, dot = run_i8(ctx, torch_cuda, [(a, b)], cap=cap)
+    i2, d2 = orc.allpairs_i8(a, b)
+    assert (idx[0, :96] == i2).all() and (dot[0, :96] == d2).all()
+
+
 def test_allpairs_f32_quantisation_stress(ctx, screen, orc, torch_cuda):
     """Inputs aimed at the int8 screen's window (k_allpairs_q8.hip): rows of every scale up to
     the 2^+-40 range limits and past them (exact path), spiky rows (one component carries the

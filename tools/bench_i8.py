@@ -63,9 +63,10 @@ def run(batch=2048, kp=2048, steps=20, warmup=3, check=1, cpu_seconds=0.0):
     el = time.perf_counter() - t0
     mvtrack.profile_enable(False)
     stages = {}
-    for k in ("k_i8_norms", "k_i8_match"):
+    for k in ("k_i8_norms", "k_i8_prep", "k_i8_match"):
         ms, c = mvtrack.profile_query(k)
-        stages[k] = round(ms / max(c, 1), 4)
+        if c:
+            stages[k] = round(ms / c, 4)
     checked = 0
     if args.check:
         import oracle
