@@ -30,9 +30,10 @@
 // of its pair, so Bn = max_j |b_j| (from the fp32 |b_j|^2) and Eb = 8 max_j s_j (+ 2^-21 Bn on
 // the float path; the integer path's scaling is exact: |b_jk - q_jk / q_j| <= 1 / (2 q_j)) and
 // the pair's range flags are known to it after the sweep, before any decision.
-// LDS (135.8 KiB): staging 3 x 32 KiB | int8 ring 2 x 16.25 KiB | (|a|^2, s_a) per row |
-// per-wave statistics; the A images (8 x 8 KiB) use staging slot 2 + the ring before the
-// sweep, the epilogue (102 KiB) the staging + ring after it.
+// LDS (141.2 KiB): staging 3 x 32 KiB | int8 ring 2 x 17.25 KiB (+ 2.5 KiB: the exchange build's
+// 4-slot ring) | (|a|^2, s_a) per row | per-wave statistics | each column's key shift (4 KiB);
+// the A images (8 x 8 KiB) use staging slot 2 + the ring before the sweep, the epilogue (102 KiB)
+// the staging + ring after it.
 // Bound: HBM -- 2 KiB read + 4 B written per query row (2,105,344 B per 1024^2
 // pair); int8 MFMA 2 n0 n1 256 ops per pair beside it.
 #include "q8_common.hpp"
