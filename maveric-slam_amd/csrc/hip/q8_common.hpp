@@ -145,21 +145,32 @@ __device__ __forceinline__ float exact_dot(const float *__restrict__ a, const fl
     return s;
 }
 #ifndef Q8_COOP
-// 1: the deferred maximiser re-scores load their rows cooperatively (coop_exact_dots).  Measured
-// (tools/gpu_trace_exp.sh, SURVEY C1 noise): epilogue 47.5 k cycles per wave against 43.0 k for the
-// per-lane exact_dot -- the re-scores are bound by bytes in flight (one 8-KiB chunk per wave here,
-// 32 KiB in exact_dot's batches), not by the L1's line rate; kept as a switch, off
-#define Q8_COOP 0
+// 1: the deferred maximiser re-scores load their rows COOPERATIVELY (coop_exact_dots) with
+// Q8_COOP_PD 16-float chunks in flight.  Why: exact_dot's per-lane loads put 64 different rows
+// (64 cache lines) under every load instruction, so a wave's re-scores cost ~38 x 128 line
+// lookups of the L1 -- the near-threshold epilogue ran ~40 k cycles per wave, line-rate bound;
+// the cooperative loads touch 16 lines per instruction.  Round 4's first cooperative form (its
+// chunk loop fully unrolled: ~890 VGPRs spilled) lost (47.5 k cycles against 43.0 k); with the
+// rounds of PD chunks kept as a loop, PD = 2 (17 spills, fewer than exact_dot's build): one box
+// (profiles/r04n_coop_depth_ab.log) with scores 5.63-5.66 vs 5.85-5.86 ms, near threshold
+// 5.25-5.26 vs 5.30, headline 4.27-4.30 vs 4.34-4.35; PD = 4 spills 130 and loses 30 %.
+#define Q8_COOP 1
+#endif
+#ifndef Q8_COOP_PD
+#define Q8_COOP_PD 2
 #endif
 // The reference's sequential fp32 dot for the wave's 64 (row, column) pairs at once -- lane L's
 // pair: A row `arow`, B row `bcol` (< 0: none) -- with the rows' bytes loaded COOPERATIVELY: per
 // 16-float chunk, each load instruction takes 16 pairs' 64-B segments (4 lanes per segment, 16
-// segments per instruction instead of exact_dot's one 16-B piece of 64 different rows), staged
-// through the wave's own 8 KiB of LDS (`buf`: [pair][A | B][4 x 16 B], the 16-B quarters
-// XOR-swizzled by pair: at most 2-way bank conflicts), from where each lane reads its own pair's
-// chunk and adds its 16 products in order.  The next chunk's loads are in flight meanwhile.
+// segments per instruction instead of exact_dot's one 16-B piece of 64 different rows), PD chunks
+// in flight in registers, each staged through the wave's own 8 KiB of LDS (`buf`: [pair][A | B]
+// [4 x 16 B], the 16-B quarters XOR-swizzled by pair: at most 2-way bank conflicts), from where
+// each lane reads its own pair's chunk and adds its 16 products in order.
+template <int PD = Q8_COOP_PD>
 __device__ __forceinline__ float coop_exact_dots(const float *__restrict__ A, const float *__restrict__ B, int arow,
                                                  int bcol, int lane, char *buf) {
+    constexpr int NC = KD / 16;  // chunks
+    static_assert(PD >= 1 && PD <= NC, "chunks in flight");
     const int q = lane & 3;
     const float *pa[4];
     const float *pb[4];
@@ -176,33 +187,34 @@ __device__ __forceinline__ float coop_exact_dots(const float *__restrict__ A, co
     }
     const int roff = lane * 128;
     const int rsw = (lane >> 2) & 3;
-    float4 na[4], nb[4];  // the next chunk, in flight while this one is staged and summed
+    float4 qa[PD][4], qb[PD][4];  // chunks c .. c + PD - 1 in flight
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const bool on = (amask >> i) & 1u;
-        na[i] = on ? *reinterpret_cast<const float4 *>(pa[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
-        nb[i] = on ? *reinterpret_cast<const float4 *>(pb[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    float s = 0.f;
-    for (int c = 0; c < KD / 16; c++) {
-        float4 ca[4], cb[4];
+    for (int d = 0; d < PD; d++)
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            ca[i] = na[i];
-            cb[i] = nb[i];
+            const bool on = (amask >> i) & 1u;
+            qa[d][i] = on ? *reinterpret_cast<const float4 *>(pa[i] + 16 * d) : make_float4(0.f, 0.f, 0.f, 0.f);
+            qb[d][i] = on ? *reinterpret_cast<const float4 *>(pb[i] + 16 * d) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        if (c + 1 < KD / 16) {
+    float s = 0.f;
+    static_assert(NC % PD == 0, "whole rounds of PD chunks");
+#pragma unroll 1
+    for (int c0 = 0; c0 < NC; c0 += PD)  // not unrolled: the compiler would hoist every chunk's loads
+#pragma unroll
+    for (int d = 0; d < PD; d++) {
+        const int c = c0 + d;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            *reinterpret_cast<float4 *>(buf + soff[i]) = qa[d][i];
+            *reinterpret_cast<float4 *>(buf + soff[i] + 64) = qb[d][i];
+        }
+        if (c + PD < NC) {  // the freed slot takes chunk c + PD
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 const bool on = (amask >> i) & 1u;
-                na[i] = on ? *reinterpret_cast<const float4 *>(pa[i] + 16 * (c + 1)) : make_float4(0.f, 0.f, 0.f, 0.f);
-                nb[i] = on ? *reinterpret_cast<const float4 *>(pb[i] + 16 * (c + 1)) : make_float4(0.f, 0.f, 0.f, 0.f);
+                qa[d][i] = on ? *reinterpret_cast<const float4 *>(pa[i] + 16 * (c + PD)) : make_float4(0.f, 0.f, 0.f, 0.f);
+                qb[d][i] = on ? *reinterpret_cast<const float4 *>(pb[i] + 16 * (c + PD)) : make_float4(0.f, 0.f, 0.f, 0.f);
             }
-        }
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            *reinterpret_cast<float4 *>(buf + soff[i]) = ca[i];
-            *reinterpret_cast<float4 *>(buf + soff[i] + 64) = cb[i];
         }
         // a wave's LDS operations complete in order: its reads below see every lane's writes
         float4 a4[4], b4[4];
