@@ -83,6 +83,12 @@ __global__ __launch_bounds__(256) void k_i8_norms(long rows, const int8_t *__res
 #ifndef I8_KEYS
 #define I8_KEYS 0
 #endif
+// timing-only switch (no matches: every row's screen stays empty, so no row reads frame 1 again):
+// no fold -- the MFMAs and the tile stream alone.  Measured (profiles/r04q_i8_skeleton.log):
+// 1.79 ms against 2.29 with the fold, i.e. the skeleton itself reaches only 0.49 of the int8 peak
+#ifndef I8_EXP_NOFOLD
+#define I8_EXP_NOFOLD 0
+#endif
 __global__ __launch_bounds__(256) void k_i8_prep(int batch, int cap, int cap64, const int *__restrict__ n1v,
                                                  const int8_t *__restrict__ d, int *__restrict__ nrm,
                                                  float *__restrict__ rnrm, int8_t *__restrict__ q1) {
@@ -411,11 +417,15 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
                     acc[G][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b0_[m_], acc[G][0], 0, 0, 0); \
                     acc[G][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b1_[m_], acc[G][1], 0, 0, 0); \
                 }                                                                            \
-                if (m_ >= I8_LAG) I8_FOLD2(FG, m_ - I8_LAG, G0, R0, R1, C0, C1);             \
+                if (I8_EXP_NOFOLD) {                                                         \
+                    if (m_ >= I8_LAG)                                                        \
+                        asm volatile("" : : "v"(acc[FG][0][2 * (m_ - I8_LAG)]), "v"(acc[FG][1][2 * (m_ - I8_LAG)])); \
+                } else if (m_ >= I8_LAG) I8_FOLD2(FG, m_ - I8_LAG, G0, R0, R1, C0, C1);      \
             }                                                                                \
         }                                                                                    \
-        _Pragma("unroll") for (int m_ = KD / 32 - I8_LAG; m_ < KD / 32; m_++)                \
-            I8_FOLD2(FG, m_, G0, R0, R1, C0, C1);                                            \
+        if (!I8_EXP_NOFOLD)                                                                  \
+            _Pragma("unroll") for (int m_ = KD / 32 - I8_LAG; m_ < KD / 32; m_++)            \
+                I8_FOLD2(FG, m_, G0, R0, R1, C0, C1);                                        \
     } while (0)
     // ring: tile g lives in slot g % 4; at tile g issue tile g + 3 into the slot read at g - 1
     // (whose norms the previous tile left in pr*/pc*)
@@ -446,7 +456,7 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
         } else {                                                                             \
             wait_vm_i8<0>();                                                                 \
         }                                                                                    \
-        __syncthreads();                                                      \
+        __syncthreads();                                                                     \
     } while (0)
 
     wait_vm_i8<0>();  // the prologue's tiles (issued before the A rows) and the A rows

@@ -14,7 +14,7 @@ for v in ${TESTS_FOR:-ship}; do
 done
 for rep in 1 2; do
   for v in ${VARIANTS:-ship}; do
-    MV_LIB=$(lib $v) timeout -k 10 200 python tools/bench_i8.py --steps 20 --warmup 3 --check 1 --cpu-seconds 0 \
+    MV_LIB=$(lib $v) timeout -k 10 200 python tools/bench_i8.py --steps 20 --warmup 3 --check ${I8_CHECK:-1} --cpu-seconds 0 \
         > gpurun_out/i8_${v}_$rep.json 2> gpurun_out/i8_${v}_$rep.err
     rc=$?; [ $rc -eq 0 ] || { echo "bench $v rc=$rc"; tail -5 gpurun_out/i8_${v}_$rep.err; exit $rc; }
     python3 - "$v" "$rep" gpurun_out/i8_${v}_$rep.json <<'PY'
