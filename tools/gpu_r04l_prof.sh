@@ -4,5 +4,6 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 BASE="--steps 10 --warmup 2 --no-cpu-baseline --score-steps 0 --extra-steps 0 --window-steps 0 --pipeline 1"
-PROF_BENCH_ARGS="$BASE --check 0" bash tools/profile.sh r04l || exit $?
-PROF_BENCH_ARGS="$BASE --check 1 --noise 0.05" bash tools/profile.sh r04l_nt
+T=${PTAG:-r04l}
+PROF_BENCH_ARGS="$BASE --check 0" bash tools/profile.sh $T || exit $?
+PROF_BENCH_ARGS="$BASE --check 1 --noise 0.05" bash tools/profile.sh ${T}_nt
