@@ -114,7 +114,45 @@ struct Conv1aArgs {
     int H, W;  // source frame
     float in_inv, rs;
     const int *wpk, *bq;
+    const int8_t *qimg;  // SP_PRERESIZE: the resized, quantised frames [B][H][W] (k_sp_resize_q)
 };
+
+#ifndef SP_PRERESIZE
+// 1: the frames are resized + quantised ONCE per pixel by k_sp_resize_q (one pass, 4 byte
+// gathers per pixel) and conv1's workgroups load their tile + 2 pixels from it; 0: every
+// workgroup resizes its own tile + 2 pixels (1.4x the pixels, and the gathers + ~10 VALU per
+// pixel sit in the VALU-bound conv1 kernel).  Measured (profiles/r04s_sp_preresize_ab.log, one
+// box, bit-exact either way): 75.4-76.6 k frames/s against 76.7-76.8 k fused -- no gain, off
+#define SP_PRERESIZE 0
+#endif
+// F.interpolate (bilinear, align_corners=False, antialias=False) of the frame / 255 to H x W and
+// the input quantisation rint(x / in_scale) clamped to int8 -- exactly the fused path's
+// arithmetic (k / 255 by IEEE division from a table, the same fma chain and rounding)
+__global__ __launch_bounds__(256) void k_sp_resize_q(const uint8_t *__restrict__ img, int Hs, int Ws, int H, int W,
+                                                     float in_inv, long total, int8_t *__restrict__ q) {
+    __shared__ float lut[256];
+    const int t = threadIdx.x;
+    lut[t] = (float)t / 255.0f;
+    __syncthreads();
+    const long i = (long)blockIdx.x * 256 + t;
+    if (i >= total) return;
+    const long hw = (long)H * W;
+    const long b = i / hw;
+    const int p = (int)(i - b * hw), y = p / W, x = p - (p / W) * W;
+    const float sy = (float)Hs / (float)H, sx = (float)Ws / (float)W;
+    int ya, yb, xa, xb;
+    const float h1 = sp_src(sy, y, Hs, ya, yb), w1 = sp_src(sx, x, Ws, xa, xb);
+    const float h0 = 1.f - h1, w0 = 1.f - w1;
+    const uint8_t *im = img + b * Hs * Ws;
+    const float a00 = lut[im[ya * Ws + xa]], a01 = lut[im[ya * Ws + xb]];
+    const float a10 = lut[im[yb * Ws + xa]], a11 = lut[im[yb * Ws + xb]];
+    const float t0 = __builtin_fmaf(a00, w0, a01 * w1);
+    const float t1 = __builtin_fmaf(a10, w0, a11 * w1);
+    const float v = __builtin_fmaf(t0, h0, t1 * h1);
+    float qv = __builtin_rintf(v * in_inv);
+    qv = fminf(fmaxf(qv, -128.f), 127.f);
+    q[i] = (int8_t)(int)qv;
+}
 
 #ifndef SP_OCC64
 #define SP_OCC64 3  // workgroups per CU for the 64-channel layers (LDS 50 KB; VGPRs <= 168)
@@ -177,6 +215,15 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
         // the bilinear source rows / columns of the tile's QY rows and QX columns, once per
         // workgroup: (weight of the far sample, its complement, near / far offsets)
         __shared__ float4 rowc[QY], colc[QX];
+        if (c1.qimg) {  // SP_PRERESIZE: the tile + 2 pixels from the pre-resized frame
+            const int8_t *qi = c1.qimg + (size_t)b * H * W;
+            for (int i = t; i < QY * QX; i += SP_NT) {
+                const int r = i / QX, c = i % QX;
+                const int gy = y0 + r - 2, gx = x0 + c - 2;
+                qim[r * QXS + c] = gy >= 0 && gy < H && gx >= 0 && gx < W ? qi[(size_t)gy * W + gx] : (int8_t)0;
+            }
+            __syncthreads();
+        } else {
         lut[t] = (float)t / 255.0f;
         const float sy = (float)c1.H / (float)H, sx = (float)c1.W / (float)W;
         if (t < QY) {
@@ -227,6 +274,7 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
             qim[r * QXS + c] = (int8_t)v;
         }
         __syncthreads();
+        }
         // conv1a + relu over the tile + halo on v_mfma_f32_32x32x16_f16: K = the 9 taps (+ 7 zero),
         // A = the weights (lanes < 32: taps 0-7, lanes >= 32: tap 8), B = 32 tile pixels' taps;
         // pixels outside the image are conv1b's zero padding, not conv1a evaluated there
@@ -1033,8 +1081,16 @@ int sp_network(hipStream_t st, mv_superpoint *net, int batch, int H, int W, int 
     int h = oh, w = ow;
     MV_PROF_BEGIN(st, "k_sp_conv");
     {
+        // SP_PRERESIZE: the resized, quantised frames in A (free until conv2a writes it)
+        const long total = (long)batch * h * w;
+        if (SP_PRERESIZE) {
+            MV_REQUIRE(total < (1l << 40) && (total + 255) / 256 < (1l << 31));
+            hipLaunchKernelGGL(k_sp_resize_q, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, images, H, W, h,
+                               w, net->in_inv, total, A);
+            MV_LAUNCH_CHECK();
+        }
         const Conv1aArgs c1{images, H, W, net->in_inv, net->rs[0], reinterpret_cast<const int *>(wd + net->frag_off[0]),
-                            reinterpret_cast<const int *>(wd + net->bq_off[0])};
+                            reinterpret_cast<const int *>(wd + net->bq_off[0]), SP_PRERESIZE ? A : nullptr};
         if ((r = launch_conv<64, 3, true, true, 0, true>(st, net, 1, batch, h, w, nullptr, Bf, 64, c1)) != MV_OK)
             return r;
     }
