@@ -164,7 +164,10 @@ __device__ __forceinline__ bool better(long long d, long long nb, int j, long lo
 // ---------------------------------------------------------------------------
 // the fold of rows 2 s, 2 s + 1 runs one k32 step after the MFMAs of step s: the folded group's
 // accumulators come from the chain's LAST MFMA, issued at the end of the previous segment
-constexpr int I8_LAG = 1;
+#ifndef I8_LAG_N
+#define I8_LAG_N 1
+#endif
+constexpr int I8_LAG = I8_LAG_N;
 #ifndef I8_PF
 #define I8_PF 2  // k32 steps of B fragments read ahead of the MFMAs
 #endif
