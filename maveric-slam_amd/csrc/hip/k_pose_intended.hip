@@ -47,7 +47,8 @@ constexpr int NT = 256;
 #define PE_TRACE 0  // printf per-phase clock64() deltas of block 0 (timing experiments only)
 #endif
 #ifndef PE_WAVES
-#define PE_WAVES 4  // waves per SIMD (4: 128 VGPRs, 13 spilled, 3% faster than 3 at 142)
+#define PE_WAVES 4  // waves per SIMD (4: 128 VGPRs, 38 spilled, still faster than 3 at 155 without
+                    // spills: 0.523 vs 0.564 ms exact, 1.07 vs 1.17 ms noisy, profiles/r04y_pose_waves_ab.log)
 #endif
 constexpr int MAXP = 4096;  // correspondences per pair held in LDS (float4 each)
 
