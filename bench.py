@@ -82,6 +82,10 @@ def parse(argv=None):
                     help="N > 1: the collective backend (nccl = RCCL over xGMI, the product path; gloo stages the "
                          "per-step result gather through host memory -- how the N-rank GPU path is exercised on a "
                          "one-GPU box, where RCCL refuses two ranks on one device)")
+    ap.add_argument("--force-gather", action="store_true",
+                    help="initialise the process group (--dist-backend) and issue the per-step result all-gather "
+                         "even at world size 1 -- how the RCCL gather on the pipelined streams is exercised on a "
+                         "one-GPU box (a one-rank all_gather_into_tensor is a device-side copy through RCCL)")
     ap.add_argument("--harness-cpu", action="store_true",
                     help="test only: the multi-rank harness with the CPU oracle as the step (gloo)")
     return ap.parse_args(argv)
@@ -162,17 +166,19 @@ class ResultGather:
     """one all-gather per batch of every pair's result -- T (3x4 fp32) and the
     match count, 13 words = 52 B per pair -- into a [world * B, 13] buffer on every rank (rank 0
     keeps it for the report / trajectory chain).  Issued on the stream that produced the
-    results, so it is ordered after that batch's pose; a no-op at world size 1."""
+    results, so it is ordered after that batch's pose; a no-op without a process group (world
+    size 1 unless --force-gather)."""
 
     def __init__(self, torch, dist, world, B, device, slots, coll_device=None):
         self.torch, self.dist, self.world = torch, dist, world
+        self.active = dist.is_available() and dist.is_initialized()
         self.coll_device = device if coll_device is None else coll_device  # gloo + GPU results: via the host
         self.res = [torch.empty((B, 13), dtype=torch.float32, device=device) for _ in range(slots)]
         self.out = [torch.empty((world * B, 13), dtype=torch.float32, device=self.coll_device) for _ in range(slots)]
         self.count = 0
 
     def __call__(self, slot, T, nmatch, stream=None):
-        if self.world == 1:
+        if not self.active:
             return
         torch = self.torch
         with (torch.cuda.stream(stream) if stream is not None else _NullCtx()):
@@ -232,22 +238,31 @@ def pose_angles(T, Tg):
     return rot, tra
 
 
-def noisy_pose_line(torch, dev, cx, stream, pose_p, d0, d1, kp0, kp1, nn_, idx, T, nm, ni, st, fused, kmatch,
-                    steps, sync, barrier):
-    """The headline step with the pose on realistic keypoints: frame 1's keypoints moved by 0.5 px
-    Gaussian noise and 20 % of them replaced by uniform pixels (outlier correspondences), so the
-    RANSAC sees contamination and the Gauss-Newton iterates (the headline's exact projections let
-    it exit early).  Reports the rate, the pose kernel's time and the pose accuracy vs the truth."""
-    import mvtrack
+def noisy_keypoints(torch, dev, kp1, seed=1234):
+    """frame 1's keypoints moved by 0.5 px Gaussian noise and 20 % of them replaced by uniform
+    pixels (outlier correspondences)"""
     import synth
 
     g = torch.Generator(device=dev)
-    g.manual_seed(1234)
+    g.manual_seed(seed)
     B, n = kp1.shape[0], kp1.shape[1]
     k1 = kp1 + 0.5 * torch.randn(kp1.shape, generator=g, device=dev)
     out_m = torch.rand((B, n), generator=g, device=dev) < 0.2
     rnd = torch.rand((B, n, 2), generator=g, device=dev) * torch.tensor([synth.KITTI_W, synth.KITTI_H], device=dev)
-    k1 = torch.where(out_m[:, :, None], rnd, k1).contiguous()
+    return torch.where(out_m[:, :, None], rnd, k1).contiguous()
+
+
+def noisy_pose_line(torch, dev, cx, stream, pose_p, d0, d1, kp0, kp1, nn_, idx, T, nm, ni, st, fused, kmatch,
+                    steps, sync, barrier, label="frame 1: +0.5 px Gaussian noise, 20% replaced by uniform pixels "
+                                                "(outliers)"):
+    """The headline step with the pose on realistic keypoints (noisy_keypoints), so the RANSAC sees
+    contamination and the Gauss-Newton iterates (the headline's exact projections let it exit
+    early).  Reports the rate, the kernels' times and the pose accuracy vs the truth."""
+    import mvtrack
+    import synth
+
+    B = kp1.shape[0]
+    k1 = noisy_keypoints(torch, dev, kp1)
     cx.set_stream(torch.cuda.current_stream())
 
     def np_step():
@@ -267,7 +282,8 @@ def noisy_pose_line(torch, dev, cx, stream, pose_p, d0, d1, kp0, kp1, nn_, idx, 
     rot, tra = pose_angles(T.double().cpu().numpy(), synth.T_785_786)
     cx.set_stream(stream)
     return {"value": round(B * steps / el, 2), "unit": "pairs/s", "ms_per_step": round(el / steps * 1e3, 4),
-            "keypoints": "frame 1: +0.5 px Gaussian noise, 20% replaced by uniform pixels (outliers)",
+            "keypoints": label, "match_kernel_avg_ms": k_ms / max(k_n, 1),
+            "matches_per_pair": round(float(nm.sum().item()) / B, 1),
             "stages_ms": {kmatch: round(k_ms / max(k_n, 1), 4), "k_pose_ransac": round(p_ms / max(p_n, 1), 4)},
             "pose_ok": int((st == 0).sum().item()), "inliers_per_pair": round(float(ni.sum().item()) / B, 1),
             "rot_err_deg": {"median": round(float(np.median(rot)), 4), "p99": round(float(np.percentile(rot, 99)), 4)},
@@ -516,7 +532,12 @@ def main():
     # LOCAL_RANK -> device modulo the visible devices: N ranks may share a box with fewer GPUs
     # (a rehearsal of the N-rank path; with nccl, RCCL needs one device per rank)
     local = local % max(torch.cuda.device_count(), 1)
-    if world > 1:
+    if world > 1 or args.force_gather:
+        if world == 1:  # a one-rank group (--force-gather): the rendezvous on this host
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if args.dist_backend == "nccl":
             dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
         else:
@@ -576,7 +597,7 @@ def main():
 
     mvtrack.profile_enable(False)
     sync = torch.cuda.synchronize
-    barrier = dist.barrier if world > 1 else (lambda: None)
+    barrier = dist.barrier if gather.active else (lambda: None)
 
     # the headline: an unprofiled loop (no per-kernel events inside the measured wall time)
     elapsed = timed_loop(step, args.steps, args.warmup, sync, barrier)
@@ -640,12 +661,18 @@ def main():
         err = np.abs(R - synth.T_785_786[None, :, :3]).max(axis=(1, 2))
         assert ok == B and float(err.max()) < 1e-3, "pose failed: ok=%d max|dR|=%g" % (ok, err.max())
     gathered = None
-    if world > 1:  # the per-step all-gather's buffer: every rank's results, this rank's own equal to T
-        sync()
+    if gather.active:  # the per-step all-gather's buffers: every rank's results, this rank's own slice
+        sync()         # equal to its T and match count bit for bit, in every pipelined slot
+        for c in range(P):
+            g = gather.out[c].view(world, B, 13)
+            assert torch.equal(g[rank, :, :12].to(dev).view(torch.int32), Ts[c].reshape(B, 12).view(torch.int32)), \
+                "gathered T differs from this rank's (slot %d)" % c
+            assert torch.equal(g[rank, :, 12].contiguous().to(dev).view(torch.int32), nmatches[c]), \
+                "gathered match count differs from this rank's (slot %d)" % c
         g = gather.out[0].view(world, B, 13)
-        assert torch.equal(g[rank, :, :12].to(dev), Ts[0].reshape(B, 12)), "gathered results differ from this rank's"
         gathered = {"pairs_per_gather": int(g.shape[0] * g.shape[1]), "gathers_in_timed_steps": gathers_timed,
                     "bytes_per_gather": int(g.numel() * 4), "backend": args.dist_backend,
+                    "slots_checked_bitwise": P, "streams": "pipelined" if P > 1 else "current",
                     "ranks_per_device": "%d ranks on %d device(s)" % (world, torch.cuda.device_count())}
     sums = gather_checksums(torch, dist, [float(nmatch.sum().item()), float(ok)], coll_dev)
     pairs_total = B * args.steps * world
@@ -723,9 +750,27 @@ def main():
             "matches_per_pair": round(float(nmatches[0].sum().item()) / B, 1), "checked_pairs": 1}
         cx.set_stream(streams[0])
     if rank == 0 and world == 1 and args.extra_steps > 0:
+        # the realistic step: SURVEY C1 descriptors (sigma 0.05: re-observed cosines at the 0.8
+        # threshold, the exact re-scores timed) AND noisy / contaminated keypoints, with the match
+        # kernel's own roofline (traffic: the sigma-0.05 PMC summary -- the same kernel on the same
+        # descriptors as near_threshold)
+        r = noisy_pose_line(torch, dev, ctxs[0], streams[0], pose_p, e0, e1, ek0, ek1, nn_, idxs[0], Ts[0],
+                            nmatches[0], ninls[0], statuses[0], fused, kmatch, args.extra_steps, sync, barrier,
+                            label="SURVEY C1 descriptors (sigma 0.05) + frame 1 keypoints +0.5 px Gaussian noise, "
+                                  "20% replaced by uniform pixels (outliers)")
+        ks = r.pop("match_kernel_avg_ms") * 1e-3
+        algo = algorithmic_bytes_per_pair(n) * B
+        tr_r, tr_rs = pmc_traffic(kmatch, B, n, screen, fused, noise=0.05)
+        r["roofline"] = {"bound": "hbm", "kernel": kmatch, "avg_launch_ms": round(ks * 1e3, 4),
+                         "achieved": round(algo / ks / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(algo / ks / 1e9 / HBM_PEAK_GBS, 4), "traffic": tr_r, "traffic_source": tr_rs,
+                         "traffic_ratio": round(tr_r / algo, 4) if tr_r else None}
+        r["noise"] = 0.05
+        out["realistic"] = r
         out["noisy_pose"] = noisy_pose_line(torch, dev, ctxs[0], streams[0], pose_p, d0, d1, kp0, kp1, nn_,
                                             idxs[0], Ts[0], nmatches[0], ninls[0], statuses[0], fused, kmatch,
                                             args.extra_steps, sync, barrier)
+        out["noisy_pose"].pop("match_kernel_avg_ms")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, n)
         out["cpu_c0"] = cpu_c0(min(args.cpu_seconds, 8.0))
@@ -772,7 +817,7 @@ def main():
         print(json.dumps(out), flush=True)
     for cx in ctxs:
         cx.close()
-    if world > 1:
+    if gather.active:
         dist.destroy_process_group()
 
 

@@ -66,13 +66,21 @@ int mv_context_create(int device, mv_context **out);
 int mv_context_destroy(mv_context *ctx);
 /* Every later call runs on `hip_stream`; NULL is HIP's null (legacy default) stream, which is
  * what torch.cuda.current_stream() is until another stream is made current.  The new stream is
- * made to wait for the work already issued on the old one (the context's buffers -- scratch, the
- * all-pairs pair-exchange buffer -- are reused by the next launch). */
+ * made to wait for the work already issued on the old one (the context's buffers -- scratch,
+ * staged images -- are reused by the next launch).  Graph capture: switching onto a stream that
+ * is being captured, or off one, issues no event record / wait (they would invalidate or leak
+ * into the capture), so the caller orders the capture stream after the context's earlier work
+ * (e.g. synchronise before capturing) and synchronises the graph's launches before the context
+ * runs on another stream or grows its buffers (mv_context_reserve first: then nothing grows). */
 int mv_context_set_stream(mv_context *ctx, void *hip_stream);
 int mv_context_use_own_stream(mv_context *ctx); /* back to the context's own non-blocking stream */
 void *mv_context_stream(mv_context *ctx);
 int mv_context_synchronize(mv_context *ctx);
-/* Pre-size scratch for up to `batch` pairs of `cap` keypoints / cells. */
+/* Pre-size scratch for up to `batch` pairs of `cap` keypoints / cells, for the context's CURRENT
+ * all-pairs screen.  Under the default MV_SCREEN_I8 nothing is staged, so the staged int8 images
+ * that sequence mode (mv_match_sequence_*) needs are NOT reserved: they are allocated by its first
+ * call.  Before capturing sequence mode in a graph, either select MV_SCREEN_I8_STAGED, reserve,
+ * and switch back, or run it once at its largest shape. */
 int mv_context_reserve(mv_context *ctx, int batch, int cap);
 mv_context *mv_default_context(void); /* the calling thread's; NULL (stderr once) without a device */
 

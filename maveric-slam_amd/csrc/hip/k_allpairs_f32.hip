@@ -591,6 +591,7 @@ __global__ __launch_bounds__(NT, 8 / NW) void k_ap_match(int tiles_r, int cap, c
                     const int nc = __popc(inside);
                     for (int c = fh; c < nc; c += 2) {  // the row's two lanes split the list
                         const int j = clist[rl * NCAND + c];
+                        if ((unsigned)j >= (unsigned)n1) continue;  // an LDS-held index: checked
                         const float *ap = arow;
                         asm volatile("" : "+v"(ap));  // keep the A row's loads inside the loop
                         const float e = exact_dot(ap, B + (size_t)j * KD);
@@ -734,33 +735,6 @@ int launch_allpairs_f32_match(hipStream_t s, void *scratch, int batch, int cap, 
 
 }  // namespace mv
 
-namespace mv {
-void *q8d_exchange(mv_context *ctx, int batch, int cap, size_t *bytes) {
-    const size_t need = allpairs_q8d_xch_bytes(batch, cap);
-    *bytes = need;
-    if (!need) return nullptr;
-    if (need <= ctx->xch_bytes) {
-        *bytes = ctx->xch_bytes;
-        return ctx->xch;
-    }
-    if (ctx->xch) {
-        (void)quiesce(ctx);  // growing: nothing of this context may still use the old buffer
-        (void)hipFree(ctx->xch);
-        ctx->xch = nullptr;
-        ctx->xch_bytes = 0;
-    }
-    const size_t b = align_up(need, 1 << 20);
-    if (hipMalloc(&ctx->xch, b) != hipSuccess) {
-        set_error(MV_ERR_OUT_OF_MEMORY, "all-pairs exchange allocation of %zu bytes failed", b);
-        ctx->xch = nullptr;
-        return nullptr;
-    }
-    ctx->xch_bytes = b;
-    *bytes = b;
-    return ctx->xch;
-}
-}  // namespace mv
-
 namespace {
 void *ap_scratch(mv_context *ctx, size_t bytes) {
     if (bytes <= ctx->ap_scratch_bytes) return ctx->ap_scratch;
@@ -789,18 +763,14 @@ int ap_prepare(int screen, hipStream_t s, void *scr, int batch, int cap, const i
     return screen == MV_SCREEN_F16 ? mv::launch_allpairs_f32_prepare(s, scr, batch, cap, n1, desc1)
                                    : mv::launch_allpairs_q8_prepare(s, scr, batch, cap, n1, desc1);
 }
-// the match; MV_SCREEN_I8 reads both fp32 frames directly (no image, scr unused; the context's
-// pair-exchange buffer)
+// the match; MV_SCREEN_I8 reads both fp32 frames directly (no image, scr unused)
 int ap_match(mv_context *ctx, int screen, hipStream_t s, void *scr, int batch, int cap, const int *n0, const int *n1,
              const float *desc0, const float *desc1, double thresh, int *match_idx, float *match_score,
              int dmode = 0) {
-    if (screen == MV_SCREEN_I8) {
-        size_t xb = 0;
-        void *x = mv::q8d_exchange(ctx, batch, cap, &xb);
-        if (!x && xb) return MV_ERR_OUT_OF_MEMORY;
+    (void)ctx;
+    if (screen == MV_SCREEN_I8)
         return mv::launch_allpairs_q8d_match(s, batch, cap, n0, n1, desc0, desc1, thresh, match_idx, match_score,
-                                             dmode, x, xb);
-    }
+                                             dmode);
     return screen == MV_SCREEN_F16
                ? mv::launch_allpairs_f32_match(s, scr, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
                                                match_score, dmode)

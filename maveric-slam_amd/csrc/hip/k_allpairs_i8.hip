@@ -68,7 +68,8 @@ __global__ __launch_bounds__(256) void k_i8_norms(long rows, const int8_t *__res
     }
 }
 
-// Integer keys (I8_KEYS, the default while 2 ntc <= 256): frame 1 is re-quantised per column to
+// Integer keys (I8_KEYS: an experiment, OFF by default -- measured slower per step, below; when
+// on, used while 2 ntc <= 256): frame 1 is re-quantised per column to
 // unit-norm codes c_jk = RNE(b_jk s_j), s_j = RN(127 / |b_j|) (|c_jk| <= 127 since |b_jk| <= |b_j|),
 // so that the exact integer D~_ij = a_i . c_j is 127 X_ij (X = dot / |b_j|, the cosine times |a|)
 // within delta_i = (8 + 1.3e-4) |a_i| for EVERY column (|a . rho_j| <= |a| |rho_j| <= 8 |a|, the
@@ -82,12 +83,6 @@ __global__ __launch_bounds__(256) void k_i8_norms(long rows, const int8_t *__res
 // fold's VALU was not what held the MFMA pipe at ~50 %: 25 % fewer VALU per tile bought 3.5 %.
 #ifndef I8_KEYS
 #define I8_KEYS 0
-#endif
-// timing-only switch (no matches: every row's screen stays empty, so no row reads frame 1 again):
-// no fold -- the MFMAs and the tile stream alone.  Measured (profiles/r04q_i8_skeleton.log):
-// 1.79 ms against 2.29 with the fold, i.e. the skeleton itself reaches only 0.49 of the int8 peak
-#ifndef I8_EXP_NOFOLD
-#define I8_EXP_NOFOLD 0
 #endif
 __global__ __launch_bounds__(256) void k_i8_prep(int batch, int cap, int cap64, const int *__restrict__ n1v,
                                                  const int8_t *__restrict__ d, int *__restrict__ nrm,
@@ -420,15 +415,11 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
                     acc[G][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b0_[m_], acc[G][0], 0, 0, 0); \
                     acc[G][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b1_[m_], acc[G][1], 0, 0, 0); \
                 }                                                                            \
-                if (I8_EXP_NOFOLD) {                                                         \
-                    if (m_ >= I8_LAG)                                                        \
-                        asm volatile("" : : "v"(acc[FG][0][2 * (m_ - I8_LAG)]), "v"(acc[FG][1][2 * (m_ - I8_LAG)])); \
-                } else if (m_ >= I8_LAG) I8_FOLD2(FG, m_ - I8_LAG, G0, R0, R1, C0, C1);      \
+                if (m_ >= I8_LAG) I8_FOLD2(FG, m_ - I8_LAG, G0, R0, R1, C0, C1);             \
             }                                                                                \
         }                                                                                    \
-        if (!I8_EXP_NOFOLD)                                                                  \
-            _Pragma("unroll") for (int m_ = KD / 32 - I8_LAG; m_ < KD / 32; m_++)            \
-                I8_FOLD2(FG, m_, G0, R0, R1, C0, C1);                                        \
+        _Pragma("unroll") for (int m_ = KD / 32 - I8_LAG; m_ < KD / 32; m_++)                \
+            I8_FOLD2(FG, m_, G0, R0, R1, C0, C1);                                            \
     } while (0)
     // ring: tile g lives in slot g % 4; at tile g issue tile g + 3 into the slot read at g - 1
     // (whose norms the previous tile left in pr*/pc*)
@@ -599,7 +590,9 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
         long long bd = 0, bn = 1;
         for (int k = 0; k < nc; k++) {  // the row's two lanes run the same trip count
             const int j = ambig ? clist[rl * M_NCAND + k] : I;
-            if (KEYS && j >= n1) continue;  // padding columns are listed, never scored
+            // padding columns are listed, never scored; and no index read back from LDS reaches a
+            // global address unchecked (a synchronisation slip then fails parity, not the device)
+            if ((unsigned)j >= (unsigned)n1) continue;
             const int8_t *brow = B + (size_t)j * KD + fh * 16;
             i32x4 bv[KD / 32];
 #pragma unroll

@@ -1173,6 +1173,9 @@ extern "C" int mv_superpoint_forward_raw_dev(mv_context *ctx, mv_superpoint *net
     const size_t cells = (size_t)h * w;
     const size_t a_bytes = mv::align_up((size_t)batch * oh * ow * 16, 256);
     const size_t c_bytes = mv::align_up((size_t)batch * cells * (65 + 256), 256);  // the heads' codes
+    const long nblk = (long)batch * ((w + SP_DQ_COLS - 1) / SP_DQ_COLS);
+    // every shape check before anything is queued (the dequantisation's LDS holds SP_DQ_COLS columns)
+    MV_REQUIRE(nblk < (1l << 31) && (size_t)SP_DQ_COLS * h * 256 <= 64 * 1024);
     int r = sp_act(net, 2 * a_bytes + c_bytes);
     if (r != MV_OK) return r;
     int8_t *A = static_cast<int8_t *>(net->act), *Bf = A + a_bytes;
@@ -1181,8 +1184,6 @@ extern "C" int mv_superpoint_forward_raw_dev(mv_context *ctx, mv_superpoint *net
     if (net->used) MV_HIP_TRY(hipStreamWaitEvent(st, net->done, 0));
     if ((r = sp_network(st, net, batch, H, W, oh, ow, images, A, Bf, cs, cd)) != MV_OK) return r;
     MV_PROF_BEGIN(st, "k_sp_dequant_nchw");
-    const long nblk = (long)batch * ((w + SP_DQ_COLS - 1) / SP_DQ_COLS);
-    MV_REQUIRE(nblk < (1l << 31) && (size_t)SP_DQ_COLS * h * 256 <= 64 * 1024);
     for (int head = 0; head < 2; head++) {
         const int C = head ? 256 : 65;
         hipLaunchKernelGGL(k_sp_dequant_nchw, dim3((unsigned)nblk), dim3(256), (size_t)SP_DQ_COLS * h * C, st,

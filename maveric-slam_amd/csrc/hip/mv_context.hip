@@ -60,9 +60,24 @@ int quiesce(mv_context *ctx) {
     return MV_OK;
 }
 
-// the context moves off `old`: own_stream waits for everything issued on it so far
+// true when `s` is being captured into a graph -- or when the query itself is refused, which is
+// what the legacy NULL stream answers while another stream captures in global mode: no event may
+// then be recorded on it or waited for by it (a record on the legacy stream, or an uncaptured
+// event waited for by a capturing stream, invalidates the capture; a wait of own_stream on an
+// event recorded inside a capture pulls own_stream into it, unjoined)
+static bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess) {
+        (void)hipGetLastError();  // clear the sticky query error
+        return true;
+    }
+    return st != hipStreamCaptureStatusNone;
+}
+
+// the context moves off `old`: own_stream waits for everything issued on it so far (not when
+// `old` is being captured: the graph's launches are the caller's to order, see maveric_hip.h)
 static int retire_stream(mv_context *ctx, hipStream_t old) {
-    if (old == ctx->own_stream) return MV_OK;
+    if (old == ctx->own_stream || capturing(old)) return MV_OK;
     if (!ctx->ev_retire) MV_HIP_TRY(hipEventCreateWithFlags(&ctx->ev_retire, hipEventDisableTiming));
     MV_HIP_TRY(hipEventRecord(ctx->ev_retire, old));
     MV_HIP_TRY(hipStreamWaitEvent(ctx->own_stream, ctx->ev_retire, 0));
@@ -181,7 +196,6 @@ int mv_context_destroy(mv_context *ctx) {
     if (ctx->scratch) (void)hipFree(ctx->scratch);
     if (ctx->ap_scratch) (void)hipFree(ctx->ap_scratch);
     if (ctx->ap_scratch2) (void)hipFree(ctx->ap_scratch2);
-    if (ctx->xch) (void)hipFree(ctx->xch);
     if (ctx->stage_dev) (void)hipFree(ctx->stage_dev);
     (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
@@ -190,15 +204,25 @@ int mv_context_destroy(mv_context *ctx) {
 
 int mv_context_set_stream(mv_context *ctx, void *s) {
     MV_REQUIRE(ctx != nullptr);
+    if ((hipStream_t)s != ctx->stream && mv::capturing((hipStream_t)s)) {
+        // onto a capture stream: no event on either stream (a record on the legacy NULL stream
+        // during a global-mode capture invalidates it); the caller has synchronised before capturing
+        ctx->stream = (hipStream_t)s;
+        return MV_OK;
+    }
     if ((hipStream_t)s != ctx->stream) {
         MV_HIP_TRY(hipSetDevice(ctx->device));
         const int r = mv::retire_stream(ctx, ctx->stream);
         if (r != MV_OK) return r;
-        // the new stream also orders after the old one: the context's buffers (scratch, the
-        // pair exchange) are reused by its next launch
-        if (!ctx->ev_retire) MV_HIP_TRY(hipEventCreateWithFlags(&ctx->ev_retire, hipEventDisableTiming));
-        MV_HIP_TRY(hipEventRecord(ctx->ev_retire, ctx->stream));
-        MV_HIP_TRY(hipStreamWaitEvent((hipStream_t)s, ctx->ev_retire, 0));
+        // the new stream also orders after the old one: the context's buffers (scratch, staged
+        // images) are reused by its next launch.  Not across a capture: entering one, the caller
+        // has ordered the capture stream after the earlier work (a capture cannot wait for an
+        // uncaptured event); leaving one, nothing outside the graph can wait for it.
+        if (!mv::capturing(ctx->stream)) {
+            if (!ctx->ev_retire) MV_HIP_TRY(hipEventCreateWithFlags(&ctx->ev_retire, hipEventDisableTiming));
+            MV_HIP_TRY(hipEventRecord(ctx->ev_retire, ctx->stream));
+            MV_HIP_TRY(hipStreamWaitEvent((hipStream_t)s, ctx->ev_retire, 0));
+        }
     }
     ctx->stream = (hipStream_t)s;  // NULL is HIP's null stream (torch's default stream), not "unset"
     return MV_OK;
@@ -261,10 +285,6 @@ int mv_context_reserve(mv_context *ctx, int batch, int cap) {
         const size_t ab = mv::align_up(img, 1 << 20);
         if (hipMalloc(&ctx->ap_scratch2, ab) != hipSuccess) return MV_ERR_OUT_OF_MEMORY;
         ctx->ap_scratch2_bytes = ab;
-    }
-    if (ctx->ap_screen == MV_SCREEN_I8) {  // the one-pass screen's pair exchange
-        size_t xb = 0;
-        if (!mv::q8d_exchange(ctx, batch, cap, &xb) && xb) return MV_ERR_OUT_OF_MEMORY;
     }
     size_t need = mv::allpairs_i8_scratch_bytes(batch, cap);
     size_t b;

@@ -33,9 +33,6 @@ struct mv_context {
     // wait on it: own_stream then orders after all work issued on every stream the context left
     // (no stream handle is kept, so a caller may destroy a stream once the context moved off it)
     hipEvent_t ev_retire;
-    // the one-pass int8 screen's pair exchange (k_allpairs_direct.hip): codes + flags
-    void *xch;
-    size_t xch_bytes;
 };
 
 namespace mv {
@@ -126,15 +123,8 @@ int launch_allpairs_q8_match_prepare(hipStream_t s, void *scratch, int batch, in
                                      float *match_score, int dmode, void *next_scratch, int next_batch,
                                      int next_cap, const int *next_n1, const float *next_desc1);
 // the single-pass int8 screen (k_allpairs_direct.hip): no scratch, frame 1 quantised in-kernel
-// xch: the pair exchange's buffer (allpairs_q8d_xch_bytes; null or short: every block
-// quantises all of frame 1 itself)
-size_t allpairs_q8d_xch_bytes(int batch, int cap);
 int launch_allpairs_q8d_match(hipStream_t s, int batch, int cap, const int *n0, const int *n1, const float *desc0,
-                              const float *desc1, double thresh, int *match_idx, float *match_score, int dmode = 0,
-                              void *xch = nullptr, size_t xch_bytes = 0);
-// the context's exchange buffer grown to allpairs_q8d_xch_bytes(batch, cap) (nullptr: none needed
-// or the allocation failed -- then the error is set)
-void *q8d_exchange(mv_context *ctx, int batch, int cap, size_t *bytes);
+                              const float *desc1, double thresh, int *match_idx, float *match_score, int dmode = 0);
 size_t allpairs_i8_scratch_bytes(int batch, int cap);
 int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
                        const int8_t *desc0, const int8_t *desc1, int *match_idx, int *match_dot);

@@ -521,6 +521,7 @@ __device__ __forceinline__ void epilogue(char *epi, const float2 *rowv, float (&
                         const int nc = __popc(inside);
                         for (int c = fh; c < nc; c += 2) {  // the row's two lanes split the list
                             const int j = clist[rl * NCAND + c];
+                            if ((unsigned)j >= (unsigned)n1) continue;  // an LDS-held index: checked
                             const float *ap = arow;
                             asm volatile("" : "+v"(ap));  // keep the A row's loads inside the loop
                             const float e = exact_dot(ap, B + (size_t)j * KD);

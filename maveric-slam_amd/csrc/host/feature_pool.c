@@ -43,9 +43,14 @@ void mv_local_feature_update(mv_local_feature *f, int frame_num) {
 }
 
 /* :49-62: drops the oldest frame if it is older than oldest_keep_frame (one per call);
- * true when the feature has no frame left */
+ * true when the feature has no frame left.  A feature already without frames is left as it is:
+ * that state exists only after a delete that could not find its key (where the reference exits,
+ * mv_local_feature_pool_remove_old's error), and decrementing again would drive num_frames
+ * negative -- the next update would index the ring out of bounds (found by the host sanitizer
+ * build, tests/test_sanitize.py). */
 bool mv_local_feature_remove_old_frame(mv_local_feature *f, int oldest_keep_frame) {
     if (f->word_id == -1) return false;
+    if (f->num_frames <= 0) return true;
     if (f->frames[f->frame_ptr] < oldest_keep_frame) {
         f->frame_ptr = (f->frame_ptr + 1) % NF;
         f->num_frames--;

@@ -11,7 +11,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-ORACLE_SO = os.path.join(HERE, "liboracle.so")
+# MV_ORACLE_SO: another build of the same sources (tests/test_sanitize.py: the ASan/UBSan one)
+ORACLE_SO = os.environ.get("MV_ORACLE_SO") or os.path.join(HERE, "liboracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libmv_ref.so")
 
 _P = ctypes.c_void_p

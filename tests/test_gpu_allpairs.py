@@ -559,15 +559,13 @@ def test_allpairs_f32_full_size_survey_c1_noise(ctx, screen, orc, torch_cuda, sc
         assert 30 < (i2 >= 0).sum() < 500  # near the threshold: a minority of the re-observed rows pass
 
 
-def test_allpairs_f32_pair_exchange(ctx, screen, orc, torch_cuda):
-    """The one-pass kernel's pair exchange (k_allpairs_direct.hip sweep_x: a pair's two 512-row
-    blocks each quantise half of every frame-1 tile and hand the codes to each other) runs when
-    both blocks of a pair are live: cap in (512, 1024], n0 > 512, n1 > 128.  Mixed in one batch:
-    the smallest exchanging frame 1 (3 tiles), partial last tiles, n0 just past one block, pairs
-    that do not exchange (n0 <= 512, n1 <= 128), a pair whose frame 1 leaves the integer keys'
-    range (both blocks must take the float sweep together: the range flag of the partner's half
-    arrives with its final statistics) and one with a NaN in the partner's half of a late tile.
-    Indices and exact scores against the oracle, with and without scores."""
+def test_allpairs_f32_two_block_pairs(ctx, screen, orc, torch_cuda):
+    """Pairs whose query rows span both 512-row workgroups of the one-pass kernel (cap 1024:
+    each workgroup quantises all of frame 1 itself), mixed in one batch: 3-tile frames, partial
+    last tiles, n0 just past one workgroup, pairs with only one live workgroup (n0 <= 512) or one
+    column tile (n1 <= 128), a pair whose frame 1 leaves the integer keys' range (both workgroups
+    must take the float sweep) and one with a NaN in rows 32 .. 63 of a late tile.  Indices and
+    exact scores against the oracle, with and without scores."""
     rng = np.random.default_rng(77)
     shapes = [(513, 129), (1024, 1024), (700, 191), (600, 1000), (1000, 193), (512, 1024), (900, 128),
               (1024, 257), (777, 1024), (1024, 1023)]

@@ -26,12 +26,6 @@ ctx.set_stream(torch.cuda.current_stream())
 for _ in range(3):
     ctx.match_allpairs_f32(d0, d1, nn_, nn_, idx, sc)
 torch.cuda.synchronize()
-_lib = mvtrack.lib()
-if hasattr(_lib, "mv_debug_exchange_counts"):  # the pair exchange's events over these 3 launches
-    cnt = (ctypes.c_uint * 8)()
-    _lib.mv_debug_exchange_counts(cnt, 1)
-    names_x = ["waits", "polls", "foreign_xcd", "timeouts", "solo_waves", "final_ok", "final_recompute", "imports"]
-    print("exchange events (3 launches, per wave / per block):", dict(zip(names_x, list(cnt))))
 NW = 8
 nblk = min(B * 2, 16384)
 buf = np.zeros(nblk * NW * 10, np.uint64)
