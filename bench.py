@@ -618,7 +618,13 @@ def main():
     screen = ctxs[0].allpairs_screen()
     kmatch, ksplit = {"i8": ("k_q8d_match", None), "i8s": ("k_q8_match", "k_q8_split"),
                       "f16": ("k_ap_match", "k_ap_split")}[screen]
+    kfb = None
+    if screen == "i8" and mvtrack.profile_query("k_q8t_match")[1] > 0:
+        # one workgroup per pair (cap <= 1024); k_q8d_handback then redoes only the pairs it hands back
+        # (outside the integer keys' range: none in this data -- its launch is the workgroups' exit)
+        kmatch, kfb = "k_q8t_match", "k_q8d_handback"
     k_ms, k_n = mvtrack.profile_query(kmatch)
+    fb_ms, fb_n = mvtrack.profile_query(kfb) if kfb else (0.0, 0)
     s_ms, s_n = mvtrack.profile_query(ksplit) if ksplit else (0.0, 0)
     p_ms, p_n = mvtrack.profile_query("k_pose_ransac")
     with_scores = None
@@ -702,12 +708,13 @@ def main():
                                   "per-pair results (T + count, 52 B per pair)" % world},
         "roofline": roofline(kmatch, screen, B, n, k_avg_s, fused),
         "screen": screen,
-        "staging": {"i8": "none (frame 1 quantised inside k_q8d_match)",
+        "staging": {"i8": "none (frame 1 quantised inside the match workgroup)",
                     "i8s": "fused into k_q8_match (next batch)" if fused else "k_q8_split on the auxiliary stream",
                     "f16": "k_ap_split"}[screen],
         "stages_ms_per_step": dict({kmatch: round(k_avg_s * 1e3, 4),
                                     "k_pose_ransac": round(p_ms / max(p_n, 1), 4)},
-                                   **({ksplit: round(s_ms / max(s_n, 1), 4)} if ksplit else {})),
+                                   **({ksplit: round(s_ms / max(s_n, 1), 4)} if ksplit else {}),
+                                   **({kfb + " (hand-backs only)": round(fb_ms / max(fb_n, 1), 4)} if kfb else {})),
         "with_scores": with_scores,
         "result_gather": gathered,
         "checked_pairs": checked, "pose_ok": int(sum(float(x[1]) for x in sums)),

@@ -195,7 +195,11 @@ __device__ __forceinline__ void dma_half(const float *B, int h, int n1, int wu, 
 // bytes; clamped padding rows duplicate row n1 - 1): max s_j (the window's Eb), max |b_j|^2
 // (Bn), and `bad`: IK -- a value outside [-IK_MMAX, IK_MMAX] or non-finite (the pair takes the
 // float path); float -- non-finite or a row scale outside [2^-40, 2^40] (the exact path).
-template <bool IK>
+// GRP (k_q8t_match): one exponent e for each group of 4 consecutive columns (a wave's 4 rows of
+// the half: the max of their m_j by two lane swaps), so that the transposed fold needs one key
+// shift per group; the group's shift byte goes to the slot's shift table (byte D_TILE + 4 (2 jb +
+// h) + q for group 8 jb + 2 q + h) -- the per-column words are not written.
+template <bool IK, bool GRP = false>
 struct QHalf {
     f32x4v x0, x1, x2, x3;
     float m, qa, qb, q, s;
@@ -246,7 +250,12 @@ struct QHalf {
         }
         if constexpr (IK) {
             // e from m's biased exponent: [1/2, 2) -> 0, [1/4, 1/2) -> 1, below -> 2 (m q_e < 128)
-            const int e = min(max(126 - (int)((__float_as_uint(m) >> 23) & 0xffu), 0), 2);
+            float mg = m;
+            if constexpr (GRP) {  // the group's max: lanes 16 apart (ds_swizzle), then 32 apart
+                mg = fmaxf(mg, swz_xor<16>(mg));
+                mg = fmaxf(mg, __shfl_xor(mg, 32, 64));
+            }
+            const int e = min(max(126 - (int)((__float_as_uint(mg) >> 23) & 0xffu), 0), 2);
             q = j < n1 ? __builtin_ldexpf(127.f, e) : 0.f;
             s = __builtin_ldexpf(1.f / 127.f, -e);  // = 1 / q rounded: the Eb bound
             sh = tb + 2 - e;
@@ -277,7 +286,14 @@ struct QHalf {
                                           unsigned char *cs) {
         const int r = t >> 4, sub = t & 15, row = 32 * hh + r;
         *reinterpret_cast<i32x4 *>(rq + row * D_RS + (D_PAD ? sub << 4 : (sub ^ (row & 15)) << 4)) = code;
-        if constexpr (IK) {
+        if constexpr (IK && GRP) {
+            if ((t & 63) == 0) {  // the wave's group: 8 hh + w -> jb = hh, q = (w >> 1) & 3, h = w & 1
+                const int w = t >> 6;
+                rq[D_TILE + 4 * (2 * hh + (w & 1)) + ((w >> 1) & 3)] = (char)sh;
+            }
+            if (sub == 0 && live) cs[row] = (unsigned char)sh;
+            bad = bad | (live & !((qa <= 1e30f) & (m <= IK_MMAX)));
+        } else if constexpr (IK) {
             if (sub == 0) {
                 reinterpret_cast<int *>(rq + D_TILE)[row] = sh;
                 if (live) cs[row] = (unsigned char)sh;
@@ -509,16 +525,15 @@ __device__ __forceinline__ Sweep block_stats(Sweep st, float *misc, int w, int l
     return r;
 }
 
-__global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, const int *__restrict__ n0v,
-                                                       const int *__restrict__ n1v, const float *__restrict__ desc0,
-                                                       const float *__restrict__ desc1, double thresh, int dmode,
-                                                       int *__restrict__ match_idx, float *__restrict__ match_score) {
-    __shared__ __attribute__((aligned(16))) char lds[D_LDS];
+// row block L of the launch (pair L / tiles_r, rows 512 (L % tiles_r) ..)
+__device__ __forceinline__ void q8d_block(char *lds, int L, int tiles_r, int cap, const int *__restrict__ n0v,
+                                          const int *__restrict__ n1v, const float *__restrict__ desc0,
+                                          const float *__restrict__ desc1, double thresh, int dmode,
+                                          int *__restrict__ match_idx, float *__restrict__ match_score) {
 #ifdef MV_TRACE
     unsigned long long ts_[10] = {};
     D_STAMP(0);
 #endif
-    const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int pair = L / tiles_r, tr = L % tiles_r;
     const int n0 = min(max(n0v[pair], 0), cap), n1 = min(max(n1v[pair], 0), cap);
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -590,12 +605,433 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, con
                           oidx, oscore, thresh, dmode);
 }
 
+
+__global__ __launch_bounds__(D_NT, 2) void k_q8d_match(int tiles_r, int cap, const int *__restrict__ n0v,
+                                                       const int *__restrict__ n1v, const float *__restrict__ desc0,
+                                                       const float *__restrict__ desc1, double thresh, int dmode,
+                                                       int *__restrict__ match_idx, float *__restrict__ match_score) {
+    __shared__ __attribute__((aligned(16))) char lds[D_LDS];
+    q8d_block(lds, xcd_remap(blockIdx.x, gridDim.x), tiles_r, cap, n0v, n1v, desc0, desc1, thresh, dmode, match_idx,
+              match_score);
+}
+// the pairs k_q8t_match handed back (flags `only`), a grid-stride loop over the row blocks: a
+// few workgroups scan the flags instead of one exiting workgroup per row block
+__global__ __launch_bounds__(D_NT, 2) void k_q8d_handback(int tiles_r, int cap, const int *__restrict__ n0v,
+                                                          const int *__restrict__ n1v, const float *__restrict__ desc0,
+                                                          const float *__restrict__ desc1, double thresh,
+                                                          int *__restrict__ match_idx, float *__restrict__ match_score,
+                                                          const int *__restrict__ only, int nblocks) {
+    __shared__ __attribute__((aligned(16))) char lds[D_LDS];
+    for (int L = blockIdx.x; L < nblocks; L += gridDim.x) {
+        if (!only[L / tiles_r]) continue;  // uniform: one flag per workgroup
+        q8d_block(lds, L, tiles_r, cap, n0v, n1v, desc0, desc1, thresh, 0, match_idx, match_score);
+        __syncthreads();  // the next row block reuses the LDS
+    }
+}
+
+// =============================================================================================
+// k_q8t_match -- ONE workgroup per pair (cap <= 1024): frame 1 quantised ONCE per pair.
+// k_q8d_match's two 512-row workgroups each quantise the whole of frame 1 (~190 of its ~350 VALU
+// per tile and wave).  Here 8 waves own 128 query rows each, which the 256-register budget holds
+// only in the TRANSPOSED product: the frame-1 tile is the MFMA A operand (32 columns j x 32 k,
+// read from the int8 ring) and the wave's frame-0 codes the B operand (aI, 4 groups x 8 k32 steps
+// = 128 VGPRs), so D[j][i] leaves each lane ONE query row i = 32 g + (lane & 31) and 16 columns
+// j = 8 (r >> 2) + (r & 3) + 4 (lane >> 5) -- the lane-local top-2 is 2 registers per group
+// instead of 32.  Keys: (D << (tb + 2 - e)) | tag with the tag (2 tc + jb) 16 + r (the column up to
+// the lane half, which the lane itself is) in an SGPR and the shift in a VGPR, one shift per group
+// of 4 consecutive columns (QHalf<true, true>: e uniform over the group, so the 4 shifts of a lane
+// and column block come from one LDS dword).  Per tile and wave: 8 units (jb, g) of 8 MFMAs,
+// every unit folding the previous unit's 16 values (5 VALU per 2 values) beside its MFMAs and
+// reading its fragments from LDS one k32 step ahead; the next tile's quantisation in 7 stages over
+// units 0..3 (half A) and 4..7 (half B).
+// Range: a pair whose frame 1 leaves the integer keys' range (a value outside +-1.003, a
+// non-finite value, |b_j|^2 > 4 -- keys then need more than 31 bits at tb = 9) is marked in
+// `fallback` and redone by k_q8d_match (its float path), launched after this kernel with the flags.
+constexpr int T_RG = 4;                             // 32-row groups per wave: 128 query rows
+constexpr int T_BM = 32 * T_RG * D_NW;              // 1024 rows: the whole pair
+constexpr int T_OFF_ROW = D_OFF_RING + 2 * D_SLOT;  // [T_BM] float2 (|a|^2, s_a)
+constexpr int T_OFF_MISC = T_OFF_ROW + T_BM * 8;    // [NW][4] per-wave statistics
+constexpr int T_OFF_COL = T_OFF_MISC + D_NW * 16;   // each frame-1 column's key shift (1 B)
+constexpr int T_LDS = T_OFF_COL + T_BM;
+constexpr int T_EPI_MASK = D_NW * 8192;             // epilogue: [NW] 8-KiB re-score buffers, [T_BM] wide masks
+static_assert(T_EPI_MASK + T_BM * 4 <= T_OFF_ROW, "the epilogue fits staging + ring");
+static_assert(D_OFF_AIMG + D_NW * 32 * KD <= T_OFF_ROW, "A images fit staging slot 2 + the ring");
+static_assert(T_LDS <= 160 * 1024, "one workgroup per CU");
+constexpr float T_B2MAX = 4.f;  // |b_j|^2 bound of the keys' range at tb <= 9
+
+__device__ __forceinline__ Sweep sweep_t(char *lds, const float *B, int n1, int t, int lane, int wu, unsigned chunk16,
+                                         unsigned lds_base, const i32x4 (&aI)[T_RG][KD / 32], float (&m1)[T_RG],
+                                         float (&m2)[T_RG], int tb) {
+    const int ntc = (n1 + BN - 1) / BN, nh = 2 * ntc;
+    const int fr = lane & 31, fh = lane >> 5;
+    char *ring = lds + D_OFF_RING;
+    unsigned char *colsh = reinterpret_cast<unsigned char *>(lds + T_OFF_COL);
+    Sweep st = {0.f, 0.f, false};
+    if (nh > 2) {
+        dma_half(B, 2, n1, wu, chunk16, lds_base + 2 * D_HALF);
+        wait_vm<4>();
+    } else {
+        wait_vm<0>();
+    }
+    __syncthreads();  // halves 0, 1 landed
+    {
+        QHalf<true, true> h;
+#pragma unroll
+        for (int hh = 0; hh < 2; hh++) {
+            h.load(lds + hh * D_HALF, t);
+            h.absmax();
+            h.sumsq();
+            h.reduce(32 * hh + (t >> 4), n1, tb);
+            h.pack01();
+            h.pack23();
+            h.store(ring, hh, t, true, st.smax, st.b2max, st.bad, colsh);
+        }
+    }
+    __syncthreads();  // tile 0 in ring slot 0; staging slots 0, 1 free
+    if (nh > 3) dma_half(B, 3, n1, wu, chunk16, lds_base);
+
+    const int rdb = fr * D_RS + fh * 16;  // frame-1 fragment: ring row 32 jb + fr, k chunk 2 s + fh
+    const float kinit = __int_as_float((int)0x80000000);
+#pragma unroll
+    for (int g = 0; g < T_RG; g++) {
+        m1[g] = kinit;
+        m2[g] = kinit;
+    }
+    i32x16 acc[2];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {  // the unit before tile 0: folded, then discarded
+        acc[0][q] = 0;
+        acc[1][q] = 0;
+    }
+    int sv0[4] = {0, 0, 0, 0}, sv1[4] = {0, 0, 0, 0};  // key shifts of groups q of column block 0 / 1
+    QHalf<true, true> qh;
+
+    // unit U of the tile: column block jb = U >> 2, row group g = U & 3: 8 MFMAs into acc[U & 1],
+    // each beside the fold of 2 of the previous unit's 16 values (acc[(U + 1) & 1], row group
+    // (U + 3) & 3, shifts PSV, tags PT + r), and quantisation stages 2 (U & 3), 2 (U & 3) + 1 at
+    // k32 steps 1 and 5
+#define T_UNIT(U, PSV, PT, STG, HH, J0, LIVE)                                                 \
+    do {                                                                                     \
+        const char *base_ = rs + rdb + ((U) >> 2) * 32 * D_RS;                               \
+        i32x4 b_[KD / 32];                                                                   \
+        _Pragma("unroll") for (int s_ = 0; s_ < KD / 32 + 1; s_++) {                         \
+            if (s_ == 1 || s_ == 5) {                                                        \
+                const int k_ = 2 * ((U) & 3) + (s_ == 5);                                    \
+                if (k_ == 0) qh.load((STG), t);                                              \
+                else if (k_ == 1) qh.absmax();                                               \
+                else if (k_ == 2) qh.sumsq();                                                \
+                else if (k_ == 3) qh.reduce((J0) + (t >> 4), n1, tb);                        \
+                else if (k_ == 4) qh.pack01();                                               \
+                else if (k_ == 5) qh.pack23();                                               \
+                else if (k_ == 6) qh.store(rq, (HH), t, (LIVE), st.smax, st.b2max, st.bad, colsh + (tc + 1) * BN); \
+            }                                                                                \
+            if (s_ < KD / 32) b_[s_] = *reinterpret_cast<const i32x4 *>(base_ + 32 * s_);    \
+            if (s_ >= 1) {                                                                   \
+                const int m_ = s_ - 1;                                                       \
+                if (m_ == 0) {                                                               \
+                    const i32x16 z_ = {};                                                    \
+                    acc[(U) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(b_[0], aI[(U) & 3][0], z_, 0, 0, 0); \
+                } else {                                                                     \
+                    acc[(U) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(b_[m_], aI[(U) & 3][m_], acc[(U) & 1], 0, 0, 0); \
+                }                                                                            \
+                fold_keys(acc[((U) + 1) & 1][2 * m_], acc[((U) + 1) & 1][2 * m_ + 1], PSV[m_ >> 1], PSV[m_ >> 1], \
+                          (PT) + 2u * m_, (PT) + 2u * m_ + 1u, m1[((U) + 3) & 3], m2[((U) + 3) & 3]); \
+            }                                                                                \
+            __builtin_amdgcn_sched_barrier(0);                                               \
+        }                                                                                    \
+    } while (0)
+
+    int sA = 2, sB = 0;  // staging slots of halves 2t + 2, 2t + 3
+    for (int tc = 0; tc < ntc; tc++) {
+        if (2 * tc + 3 < nh) {  // half 2t + 2 landed (2t + 3 may be in flight)
+            wait_vm<4>();
+        } else {
+            wait_vm<0>();
+        }
+        D_SYNC();  // tile t complete in its slot; the slot of tile t - 1 and staging of half 2t + 1 free
+        const int sN = 3 - sA - sB;
+        if (2 * tc + 4 < nh) dma_half(B, 2 * tc + 4, n1, wu, chunk16, lds_base + (unsigned)(sN * D_HALF));
+        const char *rs = ring + (tc & 1) * D_SLOT;
+        char *rq = ring + ((tc + 1) & 1) * D_SLOT;
+        const char *stA = lds + sA * D_HALF, *stB = lds + sB * D_HALF;
+        const bool live = tc + 1 < ntc;
+        const unsigned tg0 = __builtin_amdgcn_readfirstlane(32u * (unsigned)tc);  // (2 tc + jb) 16
+        const unsigned tgp = tg0 - 16u;                                           // tile tc - 1, jb 1
+        const unsigned tg1 = tg0 + 16u;
+        {
+            const unsigned d_ = *reinterpret_cast<const unsigned *>(rs + D_TILE + 4 * fh);
+            sv0[0] = (int)d_;
+            sv0[1] = (int)(d_ >> 8);
+            sv0[2] = (int)(d_ >> 16);
+            sv0[3] = (int)(d_ >> 24);
+        }
+        T_UNIT(0, sv1, tgp, stA, 0, 32 * (2 * tc + 2), live);
+        if (tc == 0) {  // unit 0 of tile 0 folded the zeros of "unit -1"
+            m1[3] = kinit;
+            m2[3] = kinit;
+        }
+        T_UNIT(1, sv0, tg0, stA, 0, 32 * (2 * tc + 2), live);
+        T_UNIT(2, sv0, tg0, stA, 0, 32 * (2 * tc + 2), live);
+        T_UNIT(3, sv0, tg0, stA, 0, 32 * (2 * tc + 2), live);
+        if (2 * tc + 4 < nh) {  // half 2t + 3 landed (2t + 4 may be in flight)
+            wait_vm<4>();
+        } else {
+            wait_vm<0>();
+        }
+        // half 2t + 2's staging rows were read by this wave's own load stage: free for 2t + 5
+        if (2 * tc + 5 < nh) dma_half(B, 2 * tc + 5, n1, wu, chunk16, lds_base + (unsigned)(sA * D_HALF));
+        {
+            const unsigned d_ = *reinterpret_cast<const unsigned *>(rs + D_TILE + 4 * (2 + fh));
+            sv1[0] = (int)d_;
+            sv1[1] = (int)(d_ >> 8);
+            sv1[2] = (int)(d_ >> 16);
+            sv1[3] = (int)(d_ >> 24);
+        }
+        T_UNIT(4, sv0, tg0, stB, 1, 32 * (2 * tc + 3), live);
+        T_UNIT(5, sv1, tg1, stB, 1, 32 * (2 * tc + 3), live);
+        T_UNIT(6, sv1, tg1, stB, 1, 32 * (2 * tc + 3), live);
+        T_UNIT(7, sv1, tg1, stB, 1, 32 * (2 * tc + 3), live);
+        const int nA = sN, nB = sA;
+        sA = nA;
+        sB = nB;
+    }
+#undef T_UNIT
+    {  // unit 7 of the last tile
+        const unsigned tl = __builtin_amdgcn_readfirstlane(32u * (unsigned)(ntc - 1) + 16u);
+#pragma unroll
+        for (int m_ = 0; m_ < KD / 32; m_++)
+            fold_keys(acc[1][2 * m_], acc[1][2 * m_ + 1], sv1[m_ >> 1], sv1[m_ >> 1], tl + 2u * m_, tl + 2u * m_ + 1u,
+                      m1[3], m2[3]);
+    }
+    return st;
+}
+
+// The transposed layout's decisions (the IK window of q8_common.hpp's epilogue, dmode 0): row
+// i = 32 g + fr of the wave sits in lanes fr (columns with (j >> 2) & 1 = 0) and fr + 32 (= 1), each
+// with its half's (m1, m2).  Runner-up outside the window: the maximiser, exactly scored only when
+// the window straddles the threshold (or scores are asked for) -- deferred, cooperatively loaded
+// (coop_exact_dots) two groups at a time; inside: each half's m1 is a candidate when inside, and a
+// half whose m2 is inside may hide more -- the wave re-scores every column of such "wide" halves.
+__device__ __forceinline__ void epilogue_t(char *epi, const float2 *rowv, const float (&m1)[T_RG],
+                                           const float (&m2)[T_RG], double Bn, double Eb, int tb, int w, int lane,
+                                           int n0, int n1, const float *__restrict__ A, const float *__restrict__ B,
+                                           int *__restrict__ oidx, float *__restrict__ oscore, double thresh,
+                                           const unsigned char *colsh) {
+    const int fr = lane & 31, fh = lane >> 5;
+    const double u24 = 5.9604644775390625e-08;
+    const double gam_e = KD * u24 / (1.0 - KD * u24);
+    const unsigned tmask = (1u << tb) - 1u;
+    auto kv = [&](float a) { return (double)(__float_as_int(a) >> tb); };
+    auto kcol = [&](float a, int h) {  // the column of key a held by lane half h
+        const unsigned tg = __float_as_uint(a) & tmask;
+        return (int)(tg >> 4) * 32 + 8 * (int)((tg >> 2) & 3u) + (int)(tg & 3u) + 4 * h;
+    };
+    unsigned *lmask = reinterpret_cast<unsigned *>(epi + T_EPI_MASK);
+    char *cbuf = epi + w * 8192;
+    float bs_g[T_RG];
+    int bj_g[T_RG], need_g[T_RG];
+    bool out_g[T_RG];
+    unsigned wide_rows[T_RG];
+#pragma unroll
+    for (int g = 0; g < T_RG; g++) {
+        const float e1 = m1[g], e2 = m2[g];
+        const float o1 = __shfl_xor(e1, 32, 64), o2 = __shfl_xor(e2, 32, 64);
+        const int i1 = __float_as_int(e1), j1 = __float_as_int(o1);
+        const float M = i1 >= j1 ? e1 : o1;                 // equal keys: M2 = M, ambiguous
+        const int Mh = i1 > j1 ? fh : (j1 > i1 ? 1 - fh : 0);
+        const float lo1 = i1 >= j1 ? o1 : e1;
+        const float M2 = __int_as_float(max(max(__float_as_int(e2), __float_as_int(o2)), __float_as_int(lo1)));
+        const int rl = w * (32 * T_RG) + g * 32 + fr;
+        const bool live = rl < n0;
+        const float2 rv = rowv[rl];
+        float bs = -__builtin_inff();
+        int bj = 0x7fffffff, need = -1;
+        bool wide = live && rv.y < 0.f;  // a row outside the int8 range: every column
+        unsigned wm = 3u;
+        if (live && !(rv.y < 0.f)) {
+            const double s_a = (double)rv.y;
+            const double an = sqrt(fmax((double)rv.x, 0.0)) * 1.0001;
+            const double ea = 8.001 * s_a + 4.76837158203125e-07 * an;
+            const double dq = (an * Eb + ea * Bn + ea * Eb) * 1.0001;
+            const double delta = dq + u24 * (an * Bn + dq) * 1.01 + gam_e * an * Bn + 1e-30;
+            const double sa_k = s_a * (1.0 / 508.0);
+            const double Ms = kv(M) * sa_k;
+            const double M2s = __float_as_int(M2) != (int)0x80000000 ? kv(M2) * sa_k : -__builtin_inf();
+            const double dp = delta;
+            double dpI = dp;  // the maximiser's own column window (its 1 / q_I)
+            const int I = kcol(M, Mh);
+            if (I < n1) {
+                const int eI = tb + 2 - (int)colsh[I];
+                const double EbI = 8.0001 * (double)__builtin_ldexpf(1.f / 127.f, -eI) + 1e-30;
+                const double dqI = (an * EbI + ea * Bn + ea * EbI) * 1.0001;
+                dpI = fmin(dp, dqI + u24 * (an * Bn + dqI) * 1.01 + gam_e * an * Bn + 1e-30);
+            }
+            const double lo = Ms - dpI - dp;
+            if (Ms + dpI > thresh || M2s + dp > thresh) {
+                if (M2s < lo) {
+                    if (I >= n1) {  // a padding column (zero codes) on top: all real dots below 0
+                        wide = true;
+                    } else if (!oscore && Ms - dpI > fmax(thresh, 0.0)) {
+                        bs = FLT_MAX;  // sure: the maximiser clears the threshold, no dot needed
+                        bj = I;
+                    } else {
+                        need = I;
+                    }
+                } else {  // both lanes of the row take this branch
+                    const double lim = lo / sa_k;
+                    const bool in1 = kv(e1) >= lim, in2 = kv(e2) >= lim;
+                    const bool oin1 = __shfl_xor(in1 ? 1 : 0, 32, 64) != 0;
+                    const bool oin2 = __shfl_xor(in2 ? 1 : 0, 32, 64) != 0;
+                    if (in2 || oin2) {  // a half holds two columns inside: re-score its columns
+                        wide = true;
+                        wm = (in1 ? 1u << fh : 0u) | (oin1 ? 1u << (1 - fh) : 0u);
+                    } else if (in1) {
+                        const int j = kcol(e1, fh);
+                        if ((unsigned)j < (unsigned)n1) {
+                            const float *ap = A + (size_t)rl * KD;
+                            asm volatile("" : "+v"(ap));
+                            bs = exact_dot(ap, B + (size_t)j * KD);
+                            bj = j;
+                        }
+                    }
+                }
+            }
+        }
+        {  // the row's two lanes: the better exact candidate (ambiguous rows)
+            const float ob = __shfl_xor(bs, 32, 64);
+            const int oj = __shfl_xor(bj, 32, 64);
+            if (better(0, ob, oj, bs, bj)) {
+                bs = ob;
+                bj = oj;
+            }
+        }
+        bs_g[g] = bs;
+        bj_g[g] = bj;
+        need_g[g] = need;
+        out_g[g] = fh == 0 && live && !wide;
+        if (fh == 0 && wide) lmask[rl] = wm;
+        wide_rows[g] = (unsigned)__ballot(fh == 0 && wide);
+    }
+    // the deferred maximiser scores, two groups per call: lane (fr, fh) takes row fr of group 2 c + fh
+#pragma unroll
+    for (int c = 0; c < T_RG / 2; c++) {
+        const int Ih = fh ? need_g[2 * c + 1] : need_g[2 * c];
+        float e = 0.f;
+        if (__ballot(Ih >= 0))
+            e = coop_exact_dots(A, B, w * (32 * T_RG) + (2 * c + fh) * 32 + fr, Ih, lane, cbuf);
+        const float eo = __shfl_xor(e, 32, 64);
+        const float e0 = fh ? eo : e, e1 = fh ? e : eo;
+        if (need_g[2 * c] >= 0) {
+            bs_g[2 * c] = e0;
+            bj_g[2 * c] = need_g[2 * c];
+        }
+        if (need_g[2 * c + 1] >= 0) {
+            bs_g[2 * c + 1] = e1;
+            bj_g[2 * c + 1] = need_g[2 * c + 1];
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < T_RG; g++)
+        if (out_g[g]) {
+            const int rl = w * (32 * T_RG) + g * 32 + fr;
+            const bool keep = bj_g[g] != 0x7fffffff && (double)bs_g[g] > thresh && bs_g[g] > 0.f;
+            oidx[rl] = keep ? bj_g[g] : -1;
+            if (oscore) oscore[rl] = keep ? bs_g[g] : 0.f;
+        }
+    // wide rows (rare): every column of the listed halves, one column per lane at a time
+#pragma unroll
+    for (int g = 0; g < T_RG; g++)
+        for (unsigned dm = wide_rows[g]; dm; dm &= dm - 1) {
+            const int r = w * (32 * T_RG) + g * 32 + __builtin_ctz(dm);
+            const unsigned wm = lmask[r];
+            const float *a = A + (size_t)r * KD;
+            float ws = -__builtin_inff();
+            int wj = 0x7fffffff;
+            for (int j = lane; j < n1; j += 64) {
+                if (!((wm >> ((j >> 2) & 1)) & 1u)) continue;
+                const float *ap = a;
+                asm volatile("" : "+v"(ap));
+                const float e = exact_dot(ap, B + (size_t)j * KD);
+                if (better(0, e, j, ws, wj)) {
+                    ws = e;
+                    wj = j;
+                }
+            }
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const float ob = __shfl_xor(ws, o, 64);
+                const int oj = __shfl_xor(wj, o, 64);
+                if (better(0, ob, oj, ws, wj)) {
+                    ws = ob;
+                    wj = oj;
+                }
+            }
+            if (lane == 0) {
+                const bool keep = wj != 0x7fffffff && (double)ws > thresh && ws > 0.f;
+                oidx[r] = keep ? wj : -1;
+                if (oscore) oscore[r] = keep ? ws : 0.f;
+            }
+        }
+}
+
+__global__ __launch_bounds__(D_NT, 2) void k_q8t_match(int cap, const int *__restrict__ n0v,
+                                                       const int *__restrict__ n1v, const float *__restrict__ desc0,
+                                                       const float *__restrict__ desc1, double thresh,
+                                                       int *__restrict__ match_idx, float *__restrict__ match_score,
+                                                       int *__restrict__ fallback) {
+    __shared__ __attribute__((aligned(16))) char lds[T_LDS];
+    const int pair = blockIdx.x;
+    const int n0 = min(max(n0v[pair], 0), cap), n1 = min(max(n1v[pair], 0), cap);
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    int *oidx = match_idx + (size_t)pair * cap;
+    float *oscore = match_score ? match_score + (size_t)pair * cap : nullptr;  // null: indices only
+    for (int r = t; r < cap; r += D_NT)
+        if (r >= n0 || n1 <= 0) {  // rows in [n0, cap): no match
+            oidx[r] = -1;
+            if (oscore) oscore[r] = 0.f;
+        }
+    if (n0 <= 0 || n1 <= 0) return;
+    const float *A = desc0 + (size_t)pair * cap * KD;
+    const float *B = desc1 + (size_t)pair * cap * KD;
+    const int ntc = (n1 + BN - 1) / BN;
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    const unsigned chunk16 = (unsigned)(4 * (lane & 15) + (lane >> 4)) * 16;
+    const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char *)lds;
+    float2 *rowv = reinterpret_cast<float2 *>(lds + T_OFF_ROW);
+    float *misc = reinterpret_cast<float *>(lds + T_OFF_MISC);
+    // ---- prologue: halves 0, 1 in flight beside the A phase (128 rows per wave) ----
+    dma_half(B, 0, n1, wu, chunk16, lds_base);
+    dma_half(B, 1, n1, wu, chunk16, lds_base + D_HALF);
+    i32x4 aI[T_RG][KD / 32];
+    a_phase<false, D_QB, false, T_RG>(lds + D_OFF_AIMG + w * 32 * KD, rowv, w * (32 * T_RG), 0, n0, lane, A, nullptr,
+                                      nullptr, nullptr, false, aI);
+    __syncthreads();  // the A images (staging slot 2 + the ring) are consumed
+    float m1[T_RG], m2[T_RG];
+    const int tb = 32 - __builtin_clz(32 * ntc - 1);  // tags (2 tc + jb) 16 + r < 32 ntc
+    const Sweep st = block_stats(sweep_t(lds, B, n1, t, lane, wu, chunk16, lds_base, aI, m1, m2, tb), misc, w, lane);
+    if (st.bad || !(st.b2max <= T_B2MAX)) {  // outside the keys' range: k_q8d_match redoes the pair
+        if (t == 0) fallback[pair] = 1;
+        return;
+    }
+    const double Bn = sqrt((double)st.b2max) * 1.0001;
+    const double Eb = 8.0001 * (double)st.smax + 1e-30;
+    epilogue_t(lds, rowv, m1, m2, Bn, Eb, tb, w, lane, n0, n1, A, B, oidx, oscore, thresh,
+               reinterpret_cast<const unsigned char *>(lds + T_OFF_COL));
+}
+
 }  // namespace
 
 namespace mv {
 
+int launch_allpairs_q8d_handback(hipStream_t s, int batch, int cap, const int *n0, const int *n1, const float *desc0,
+                                 const float *desc1, double thresh, int *match_idx, float *match_score,
+                                 const int *only);
+
 int launch_allpairs_q8d_match(hipStream_t s, int batch, int cap, const int *n0, const int *n1, const float *desc0,
-                              const float *desc1, double thresh, int *match_idx, float *match_score, int dmode) {
+                              const float *desc1, double thresh, int *match_idx, float *match_score, int dmode,
+                              const int *only) {
+    if (only) return launch_allpairs_q8d_handback(s, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
+                                                  match_score, only);
     MV_REQUIRE(batch > 0 && cap > 0 && n0 && n1 && desc0 && desc1 && match_idx);
     MV_REQUIRE(((uintptr_t)desc0 & 15) == 0 && ((uintptr_t)desc1 & 15) == 0);
     MV_REQUIRE((long)cap * KD * 4 < (1l << 32));  // 32-bit DMA source offsets within a pair
@@ -608,6 +1044,48 @@ int launch_allpairs_q8d_match(hipStream_t s, int batch, int cap, const int *n0, 
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     return MV_OK;
+}
+
+
+int launch_allpairs_q8d_handback(hipStream_t s, int batch, int cap, const int *n0, const int *n1, const float *desc0,
+                                 const float *desc1, double thresh, int *match_idx, float *match_score,
+                                 const int *only) {
+    const int tiles_r = (cap + D_BM - 1) / D_BM;
+    const long blocks = (long)batch * tiles_r;
+    MV_REQUIRE(blocks < (1l << 31) && (long)cap * KD * 4 < (1l << 32));
+    MV_PROF_BEGIN(s, "k_q8d_handback");
+    hipLaunchKernelGGL(k_q8d_handback, dim3((unsigned)min(blocks, 1024l)), dim3(D_NT), 0, s, tiles_r, cap, n0, n1,
+                       desc0, desc1, thresh, match_idx, match_score, only, (int)blocks);
+    MV_PROF_END(s);
+    MV_LAUNCH_CHECK();
+    return MV_OK;
+}
+
+// k_q8t_match (one workgroup per pair) where it applies -- cap <= 1024, the indices / scores
+// match (dmode 0) -- with the pairs it hands back (outside the integer keys' range) redone by
+// k_q8d_match in the same stream: flags[batch] in `scratch` (zeroed here)
+bool allpairs_q8t_applies(int cap, int dmode) {
+    static const int off = [] {
+        const char *e = getenv("MV_Q8_KERNEL");  // "d": k_q8d_match only (A/B of the two layouts)
+        return e && e[0] == 'd' ? 1 : 0;
+    }();
+    return !off && dmode == 0 && cap > 0 && cap <= T_BM;
+}
+size_t allpairs_q8t_scratch_bytes(int batch) { return align_up((size_t)batch * 4, 256); }
+
+int launch_allpairs_q8t_match(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
+                              const float *desc0, const float *desc1, double thresh, int *match_idx,
+                              float *match_score) {
+    MV_REQUIRE(batch > 0 && cap > 0 && cap <= T_BM && n0 && n1 && desc0 && desc1 && match_idx && scratch);
+    MV_REQUIRE(((uintptr_t)desc0 & 15) == 0 && ((uintptr_t)desc1 & 15) == 0);
+    int *flags = static_cast<int *>(scratch);
+    MV_HIP_TRY(hipMemsetAsync(flags, 0, (size_t)batch * 4, s));
+    MV_PROF_BEGIN(s, "k_q8t_match");
+    hipLaunchKernelGGL(k_q8t_match, dim3((unsigned)batch), dim3(D_NT), 0, s, cap, n0, n1, desc0, desc1, thresh,
+                       match_idx, match_score, flags);
+    MV_PROF_END(s);
+    MV_LAUNCH_CHECK();
+    return launch_allpairs_q8d_match(s, batch, cap, n0, n1, desc0, desc1, thresh, match_idx, match_score, 0, flags);
 }
 
 }  // namespace mv

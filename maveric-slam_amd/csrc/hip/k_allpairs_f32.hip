@@ -767,10 +767,16 @@ int ap_prepare(int screen, hipStream_t s, void *scr, int batch, int cap, const i
 int ap_match(mv_context *ctx, int screen, hipStream_t s, void *scr, int batch, int cap, const int *n0, const int *n1,
              const float *desc0, const float *desc1, double thresh, int *match_idx, float *match_score,
              int dmode = 0) {
-    (void)ctx;
-    if (screen == MV_SCREEN_I8)
+    if (screen == MV_SCREEN_I8) {
+        if (mv::allpairs_q8t_applies(cap, dmode)) {
+            void *fl = mv::scratch(ctx, mv::allpairs_q8t_scratch_bytes(batch));
+            if (!fl) return MV_ERR_OUT_OF_MEMORY;
+            return mv::launch_allpairs_q8t_match(s, fl, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
+                                                 match_score);
+        }
         return mv::launch_allpairs_q8d_match(s, batch, cap, n0, n1, desc0, desc1, thresh, match_idx, match_score,
                                              dmode);
+    }
     return screen == MV_SCREEN_F16
                ? mv::launch_allpairs_f32_match(s, scr, batch, cap, n0, n1, desc0, desc1, thresh, match_idx,
                                                match_score, dmode)

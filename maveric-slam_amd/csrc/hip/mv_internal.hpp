@@ -123,8 +123,18 @@ int launch_allpairs_q8_match_prepare(hipStream_t s, void *scratch, int batch, in
                                      float *match_score, int dmode, void *next_scratch, int next_batch,
                                      int next_cap, const int *next_n1, const float *next_desc1);
 // the single-pass int8 screen (k_allpairs_direct.hip): no scratch, frame 1 quantised in-kernel
+// only: per-pair flags -- the workgroups of pairs whose flag is 0 exit at once (k_q8t_match's
+// hand-backs); null: every pair
 int launch_allpairs_q8d_match(hipStream_t s, int batch, int cap, const int *n0, const int *n1, const float *desc0,
-                              const float *desc1, double thresh, int *match_idx, float *match_score, int dmode = 0);
+                              const float *desc1, double thresh, int *match_idx, float *match_score, int dmode = 0,
+                              const int *only = nullptr);
+// the one-workgroup-per-pair transposed kernel (k_allpairs_direct.hip), k_q8d_match for its
+// hand-backs; scratch >= allpairs_q8t_scratch_bytes(batch)
+bool allpairs_q8t_applies(int cap, int dmode);
+size_t allpairs_q8t_scratch_bytes(int batch);
+int launch_allpairs_q8t_match(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
+                              const float *desc0, const float *desc1, double thresh, int *match_idx,
+                              float *match_score);
 size_t allpairs_i8_scratch_bytes(int batch, int cap);
 int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
                        const int8_t *desc0, const int8_t *desc1, int *match_idx, int *match_dot);

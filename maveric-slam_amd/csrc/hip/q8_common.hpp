@@ -260,15 +260,16 @@ __device__ __forceinline__ bool better(int dmode, float v, int j, float bv, int 
 //      EA: also rowe[r] = |rho|^2, the row's quantisation residual in code units (rho_k = a_k q -
 //      c_k, from the same magic sum), so that the epilogue's A term is s_a |rho| + |1 - q s_a| |a|
 //      instead of the worst case 8 s_a (every component off by half a step).
-template <bool AI8, int QB = 4, bool EA = false>  // QB: row quads (4 loads per lane each) in flight
+//      NG: 32-row groups (RG = 2 for the 64-row waves; k_q8t_match's 128-row waves take 4).
+template <bool AI8, int QB = 4, bool EA = false, int NG = RG>  // QB: row quads (4 loads per lane each) in flight
 __device__ __forceinline__ void a_phase(char *img, float2 *rowv, int rbase, int row0, int n0, int lane,
                                         const float *__restrict__ A, const char *__restrict__ QA,
                                         const float *__restrict__ s0p, const float *__restrict__ na2p, bool bad0,
-                                        i32x4 (&aI)[RG][KD / 32], float *rowe = nullptr) {
+                                        i32x4 (&aI)[NG][KD / 32], float *rowe = nullptr) {
     const int fr = lane & 31, fh = lane >> 5;
     const int sub = lane & 15, rq = lane >> 4;
 #pragma unroll
-    for (int g = 0; g < RG; g++) {
+    for (int g = 0; g < NG; g++) {
         if constexpr (AI8) {
             // lane sub holds chunk sub (k = 16 sub .. +15) of row 4 qd + rq, stored at the
             // swizzled chunk the readback expects

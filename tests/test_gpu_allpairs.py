@@ -585,3 +585,32 @@ def test_allpairs_f32_two_block_pairs(ctx, screen, orc, torch_cuda):
             if scores:
                 assert (bits(sc[k, :n0]) == bits(s2)).all(), k
             assert (i2 >= 0).sum() > min(n0, c.shape[0]) // 4, k
+
+
+@pytest.mark.parametrize("scores", [True, False])
+def test_allpairs_f32_handbacks_across_the_grid(ctx, orc, torch_cuda, scores):
+    """The default screen at cap <= 1024 runs k_q8t_match (one workgroup per pair); a pair outside
+    its integer keys' range -- a component beyond +-1.003, |b_j|^2 > 4 with every component inside,
+    a NaN -- is handed back to k_q8d_match's float path (k_q8d_handback: a grid-stride loop of at
+    most 1024 workgroups over the flagged row blocks).  520 pairs at cap 1024 = 1040 row blocks,
+    so the loop takes more than one trip; every pair against the oracle (indices, exact scores)."""
+    rng = np.random.default_rng(1234)
+    B, n = 520, 64
+    pairs = []
+    for b in range(B):
+        p = synth.synth_pair_f32(5000 + b, n=n, n1=n, noise=0.2)
+        a, c = p["desc0"], p["desc1"].copy()
+        if b % 7 == 3:
+            c[rng.integers(n), rng.integers(256)] = np.float32(1.5)
+        elif b % 11 == 5:
+            c[rng.integers(n), :16] = np.float32(0.7)  # |b_j|^2 = 7.84 + ..., every component < 1.003
+        elif b == 100:
+            c[7, 200] = np.nan
+        pairs.append((a, c))
+    idx, sc = run_f32(ctx, torch_cuda, pairs, cap=1024, scores=scores)
+    for b, (a, c) in enumerate(pairs):
+        i2, s2 = orc.allpairs_f32(a, c, 0.8)
+        assert (idx[b, :n] == i2).all(), b
+        assert (idx[b, n:] == -1).all(), b
+        if scores:
+            assert (bits(sc[b, :n]) == bits(s2)).all(), b

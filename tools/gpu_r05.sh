@@ -22,10 +22,10 @@ if [ "${BENCH:-1}" = 1 ]; then
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
 r = d["roofline"]
-print("headline %.0f pairs/s  %s %.4f ms  frac %.4f  traffic_ratio %s" % (d["value"], r["kernel"], r["avg_launch_ms"], r["frac"], r["traffic_ratio"]))
+print("headline %.0f pairs/s  %s %.4f ms  frac %.4f  traffic_ratio %s  stages %s" % (d["value"], r["kernel"], r["avg_launch_ms"], r["frac"], r["traffic_ratio"], d["stages_ms_per_step"]))
 for k in ("with_scores", "near_threshold", "realistic", "noisy_pose", "i8_allpairs", "sequence", "superpoint", "image_to_pose", "keypoints", "window_frontend"):
     v = d.get(k)
-    if v: print(k, json.dumps({kk: vv for kk, vv in v.items() if kk in ("value", "ms_per_step", "stages_ms", "k_q8d_match_ms", "hbm_frac_8d", "roofline", "mfma_roofline", "hbm_roofline", "pose_ok", "rot_err_deg", "tdir_err_deg", "matches_per_pair")})[:600])
+    if v: print(k, json.dumps({kk: vv for kk, vv in v.items() if kk in ("value", "ms_per_step", "stages_ms", "k_q8d_match_ms", "k_q8t_match_ms", "hbm_frac_8d", "roofline", "mfma_roofline", "hbm_roofline", "pose_ok", "rot_err_deg", "tdir_err_deg", "matches_per_pair")})[:600])
 PY
 fi
 if [ "${PROF:-0}" = 1 ]; then
