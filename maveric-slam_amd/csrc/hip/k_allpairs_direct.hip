@@ -622,8 +622,12 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8d_handback(int tiles_r, int cap, 
                                                           int *__restrict__ match_idx, float *__restrict__ match_score,
                                                           const int *__restrict__ only, int nblocks) {
     __shared__ __attribute__((aligned(16))) char lds[D_LDS];
-    for (int L = blockIdx.x; L < nblocks; L += gridDim.x) {
-        if (!only[L / tiles_r]) continue;  // uniform: one flag per workgroup
+    // the flag scan first, in scalar registers: a workgroup with nothing handed back leaves before
+    // any of the (spilling) float-path code runs
+    int L = blockIdx.x;
+    while (L < nblocks && !__builtin_amdgcn_readfirstlane(only[L / tiles_r])) L += gridDim.x;
+    for (; L < nblocks; L += gridDim.x) {
+        if (!__builtin_amdgcn_readfirstlane(only[L / tiles_r])) continue;  // uniform: one flag per block
         q8d_block(lds, L, tiles_r, cap, n0v, n1v, desc0, desc1, thresh, 0, match_idx, match_score);
         __syncthreads();  // the next row block reuses the LDS
     }
@@ -980,6 +984,10 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8t_match(int cap, const int *__res
                                                        int *__restrict__ match_idx, float *__restrict__ match_score,
                                                        int *__restrict__ fallback) {
     __shared__ __attribute__((aligned(16))) char lds[T_LDS];
+#ifdef MV_TRACE
+    unsigned long long ts_[10] = {};
+    D_STAMP(0);
+#endif
     const int pair = blockIdx.x;
     const int n0 = min(max(n0v[pair], 0), cap), n1 = min(max(n1v[pair], 0), cap);
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -1005,10 +1013,12 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8t_match(int cap, const int *__res
     i32x4 aI[T_RG][KD / 32];
     a_phase<false, D_QB, false, T_RG>(lds + D_OFF_AIMG + w * 32 * KD, rowv, w * (32 * T_RG), 0, n0, lane, A, nullptr,
                                       nullptr, nullptr, false, aI);
+    D_STAMP(1);
     __syncthreads();  // the A images (staging slot 2 + the ring) are consumed
     float m1[T_RG], m2[T_RG];
     const int tb = 32 - __builtin_clz(32 * ntc - 1);  // tags (2 tc + jb) 16 + r < 32 ntc
     const Sweep st = block_stats(sweep_t(lds, B, n1, t, lane, wu, chunk16, lds_base, aI, m1, m2, tb), misc, w, lane);
+    D_STAMP(2);
     if (st.bad || !(st.b2max <= T_B2MAX)) {  // outside the keys' range: k_q8d_match redoes the pair
         if (t == 0) fallback[pair] = 1;
         return;
@@ -1017,6 +1027,16 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8t_match(int cap, const int *__res
     const double Eb = 8.0001 * (double)st.smax + 1e-30;
     epilogue_t(lds, rowv, m1, m2, Bn, Eb, tb, w, lane, n0, n1, A, B, oidx, oscore, thresh,
                reinterpret_cast<const unsigned char *>(lds + T_OFF_COL));
+#ifdef MV_TRACE
+    D_STAMP(3);
+    if (lane == 0 && blockIdx.x < D_TRACE_BLOCKS) {
+        unsigned long long *o = g_d_trace + ((size_t)blockIdx.x * D_NW + w) * 10;
+        for (int k = 0; k < 6; k++) o[k] = ts_[k];  // memtime x 4, memrealtime at entry / after A
+        o[6] = __smid();
+        o[7] = __builtin_amdgcn_s_memrealtime();
+        o[9] = ts_[9];
+    }
+#endif
 }
 
 }  // namespace

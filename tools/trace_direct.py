@@ -1,4 +1,4 @@
-"""Phase timing of k_q8d_match (library built with EXTRA=-DMV_TRACE, e.g. MV_LIB=
+"""Phase timing of k_q8t_match (one workgroup per pair; MV_Q8_KERNEL=d: k_q8d_match, two) (library built with EXTRA=-DMV_TRACE, e.g. MV_LIB=
 build_variants/libmaveric_trace.so from tools/build_variant.sh trace -DMV_TRACE): per (block, wave)
 s_memtime stamps at entry, A phase done, sweep + statistics done, epilogue done.
 Env: TB pairs (8192), TN per-component noise of the re-observed rows (bench default 0.3/16;
@@ -27,7 +27,7 @@ for _ in range(3):
     ctx.match_allpairs_f32(d0, d1, nn_, nn_, idx, sc)
 torch.cuda.synchronize()
 NW = 8
-nblk = min(B * 2, 16384)
+nblk = min(B * (2 if os.environ.get("MV_Q8_KERNEL", "")[:1] == "d" else 1), 16384)
 buf = np.zeros(nblk * NW * 10, np.uint64)
 lib = mvtrack.lib()
 lib.mv_debug_direct_trace.argtypes = [ctypes.c_void_p, ctypes.c_long]
