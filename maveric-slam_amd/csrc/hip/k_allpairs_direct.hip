@@ -1074,7 +1074,7 @@ int launch_allpairs_q8d_handback(hipStream_t s, int batch, int cap, const int *n
     const long blocks = (long)batch * tiles_r;
     MV_REQUIRE(blocks < (1l << 31) && (long)cap * KD * 4 < (1l << 32));
     MV_PROF_BEGIN(s, "k_q8d_handback");
-    hipLaunchKernelGGL(k_q8d_handback, dim3((unsigned)min(blocks, 1024l)), dim3(D_NT), 0, s, tiles_r, cap, n0, n1,
+    hipLaunchKernelGGL(k_q8d_handback, dim3((unsigned)min(blocks, 256l)), dim3(D_NT), 0, s, tiles_r, cap, n0, n1,
                        desc0, desc1, thresh, match_idx, match_score, only, (int)blocks);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();

@@ -592,7 +592,7 @@ def test_allpairs_f32_handbacks_across_the_grid(ctx, orc, torch_cuda, scores):
     """The default screen at cap <= 1024 runs k_q8t_match (one workgroup per pair); a pair outside
     its integer keys' range -- a component beyond +-1.003, |b_j|^2 > 4 with every component inside,
     a NaN -- is handed back to k_q8d_match's float path (k_q8d_handback: a grid-stride loop of at
-    most 1024 workgroups over the flagged row blocks).  520 pairs at cap 1024 = 1040 row blocks,
+    most 256 workgroups over the flagged row blocks).  520 pairs at cap 1024 = 1040 row blocks,
     so the loop takes more than one trip; every pair against the oracle (indices, exact scores)."""
     rng = np.random.default_rng(1234)
     B, n = 520, 64
