@@ -662,6 +662,9 @@ static_assert(T_EPI_MASK + T_BM * 4 <= T_OFF_ROW, "the epilogue fits staging + r
 static_assert(D_OFF_AIMG + D_NW * 32 * KD <= T_OFF_ROW, "A images fit staging slot 2 + the ring");
 static_assert(T_LDS <= 160 * 1024, "one workgroup per CU");
 constexpr float T_B2MAX = 4.f;  // |b_j|^2 bound of the keys' range at tb <= 9
+#ifndef T_PFD
+#define T_PFD 1  // k32 steps the frame-1 fragments are read ahead of their MFMA
+#endif
 
 __device__ __forceinline__ Sweep sweep_t(char *lds, const float *B, int n1, int t, int lane, int wu, unsigned chunk16,
                                          unsigned lds_base, const i32x4 (&aI)[T_RG][KD / 32], float (&m1)[T_RG],
@@ -745,6 +748,38 @@ __device__ __forceinline__ Sweep sweep_t(char *lds, const float *B, int n1, int 
         }                                                                                    \
     } while (0)
 
+#if T_PFD > 1
+    // the fragments read T_PFD k32 steps ahead across the tile's units (fb_: the tile's 64 k32
+    // steps, constant indices: only the T_PFD + 1 live ones take registers)
+#undef T_UNIT
+#define T_UNIT(U, PSV, PT, STG, HH, J0, LIVE)                                                 \
+    do {                                                                                     \
+        _Pragma("unroll") for (int s_ = 0; s_ < KD / 32; s_++) {                             \
+            if (s_ == 0 || s_ == 4) {                                                        \
+                const int k_ = 2 * ((U) & 3) + (s_ == 4);                                    \
+                if (k_ == 0) qh.load((STG), t);                                              \
+                else if (k_ == 1) qh.absmax();                                               \
+                else if (k_ == 2) qh.sumsq();                                                \
+                else if (k_ == 3) qh.reduce((J0) + (t >> 4), n1, tb);                        \
+                else if (k_ == 4) qh.pack01();                                               \
+                else if (k_ == 5) qh.pack23();                                               \
+                else if (k_ == 6) qh.store(rq, (HH), t, (LIVE), st.smax, st.b2max, st.bad, colsh + (tc + 1) * BN); \
+            }                                                                                \
+            const int gn_ = 8 * (U) + s_ + T_PFD;                                            \
+            if (gn_ < 64) fb_[gn_] = *reinterpret_cast<const i32x4 *>(rs + rdb + (gn_ >> 5) * 32 * D_RS + 32 * (gn_ & 7)); \
+            if (s_ == 0) {                                                                   \
+                const i32x16 z_ = {};                                                        \
+                acc[(U) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fb_[8 * (U)], aI[(U) & 3][0], z_, 0, 0, 0); \
+            } else {                                                                         \
+                acc[(U) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fb_[8 * (U) + s_], aI[(U) & 3][s_], acc[(U) & 1], 0, 0, 0); \
+            }                                                                                \
+            fold_keys(acc[((U) + 1) & 1][2 * s_], acc[((U) + 1) & 1][2 * s_ + 1], PSV[s_ >> 1], PSV[s_ >> 1], \
+                      (PT) + 2u * s_, (PT) + 2u * s_ + 1u, m1[((U) + 3) & 3], m2[((U) + 3) & 3]);  \
+            __builtin_amdgcn_sched_barrier(0);                                               \
+        }                                                                                    \
+    } while (0)
+#endif
+
     int sA = 2, sB = 0;  // staging slots of halves 2t + 2, 2t + 3
     for (int tc = 0; tc < ntc; tc++) {
         if (2 * tc + 3 < nh) {  // half 2t + 2 landed (2t + 3 may be in flight)
@@ -753,6 +788,11 @@ __device__ __forceinline__ Sweep sweep_t(char *lds, const float *B, int n1, int 
             wait_vm<0>();
         }
         D_SYNC();  // tile t complete in its slot; the slot of tile t - 1 and staging of half 2t + 1 free
+#if T_PFD > 1
+        i32x4 fb_[64];
+        _Pragma("unroll") for (int p_ = 0; p_ < T_PFD; p_++)
+            fb_[p_] = *reinterpret_cast<const i32x4 *>(ring + (tc & 1) * D_SLOT + rdb + 32 * p_);
+#endif
         const int sN = 3 - sA - sB;
         if (2 * tc + 4 < nh) dma_half(B, 2 * tc + 4, n1, wu, chunk16, lds_base + (unsigned)(sN * D_HALF));
         const char *rs = ring + (tc & 1) * D_SLOT;
