@@ -73,7 +73,10 @@ static_assert(D_LDS <= 160 * 1024, "one workgroup per CU");
 constexpr int D_PF = 1;       // k32 steps of B fragments read ahead of the MFMAs
 constexpr int QS_LOAD = 1;    // the k32 step whose slot issues the quantisation's staging reads
 #ifndef D_QB
-#define D_QB 4  // A phase: frame-0 row quads in flight per wave (4 x 16-B loads per lane each)
+// A phase: frame-0 row quads in flight per wave (4 x 16-B loads per lane each); fewer bytes in
+// flight measured faster in both kernels (k_q8t_match 2: 3.505, 4: 3.54, 8: 3.91 ms --
+// profiles/r05h_flag_qb_ab.json; k_q8d_match round 4: 2: 4.153-4.161, 4: 4.176-4.195 ms)
+#define D_QB 2
 #endif
 constexpr float IK_MMAX = 1.003f;  // integer path: max |b_jk| allowed (RNE(x 127) stays <= 127)
 #ifndef D_CC
@@ -662,9 +665,6 @@ static_assert(T_EPI_MASK + T_BM * 4 <= T_OFF_ROW, "the epilogue fits staging + r
 static_assert(D_OFF_AIMG + D_NW * 32 * KD <= T_OFF_ROW, "A images fit staging slot 2 + the ring");
 static_assert(T_LDS <= 160 * 1024, "one workgroup per CU");
 constexpr float T_B2MAX = 4.f;  // |b_j|^2 bound of the keys' range at tb <= 9
-#ifndef T_FLAG
-#define T_FLAG 0  // 1: each unit's first two k32 steps fold nothing (the previous unit's last MFMA is in flight)
-#endif
 #ifndef T_PFD
 #define T_PFD 2  // k32 steps the frame-1 fragments are read ahead of their MFMA (1: 3.66 ms, 2: 3.53, 3: 3.52 -- profiles/r05g_pfd_ab.json)
 #endif
@@ -758,7 +758,7 @@ __device__ __forceinline__ Sweep sweep_t(char *lds, const float *B, int n1, int 
 #define T_UNIT(U, PSV, PT, STG, HH, J0, LIVE)                                                 \
     do {                                                                                     \
         _Pragma("unroll") for (int s_ = 0; s_ < KD / 32; s_++) {                             \
-            if (s_ == 0 || s_ == (T_FLAG ? 1 : 4)) {                                         \
+            if (s_ == 0 || s_ == 4) {                                                        \
                 const int k_ = 2 * ((U) & 3) + (s_ != 0);                                    \
                 if (k_ == 0) qh.load((STG), t);                                              \
                 else if (k_ == 1) qh.absmax();                                               \
@@ -776,10 +776,8 @@ __device__ __forceinline__ Sweep sweep_t(char *lds, const float *B, int n1, int 
             } else {                                                                         \
                 acc[(U) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fb_[8 * (U) + s_], aI[(U) & 3][s_], acc[(U) & 1], 0, 0, 0); \
             }                                                                                \
-            _Pragma("unroll") for (int p_ = 0; p_ < 8; p_++)                                  \
-                if (T_FLAG ? (s_ == 2 ? p_ < 2 : s_ == 3 ? (p_ == 2 || p_ == 3) : (s_ >= 4 && p_ == s_)) : p_ == s_) \
-                    fold_keys(acc[((U) + 1) & 1][2 * p_], acc[((U) + 1) & 1][2 * p_ + 1], PSV[p_ >> 1], PSV[p_ >> 1], \
-                              (PT) + 2u * p_, (PT) + 2u * p_ + 1u, m1[((U) + 3) & 3], m2[((U) + 3) & 3]); \
+            fold_keys(acc[((U) + 1) & 1][2 * s_], acc[((U) + 1) & 1][2 * s_ + 1], PSV[s_ >> 1], PSV[s_ >> 1], \
+                      (PT) + 2u * s_, (PT) + 2u * s_ + 1u, m1[((U) + 3) & 3], m2[((U) + 3) & 3]);  \
             __builtin_amdgcn_sched_barrier(0);                                               \
         }                                                                                    \
     } while (0)
