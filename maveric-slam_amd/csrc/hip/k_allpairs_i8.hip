@@ -672,11 +672,333 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
         }
 }
 
+
+// ---------------------------------------------------------------------------
+// k_i8t_match: the int8 all-pairs (configs[4]) in the TRANSPOSED product of k_q8t_match
+// (k_allpairs_direct.hip): a 512-thread workgroup owns 1024 query rows (8 waves x 128), frame 1's
+// unit-norm codes (k_i8_prep) are the MFMA A operand (32 columns x 32 k from the LDS ring) and the
+// wave's frame-0 rows the B operand (4 groups x 8 k32 steps = 128 VGPRs), so each lane holds ONE
+// query row and 16 columns per column block: the lane-local top-2 is 2 registers per row group
+// and each frame-1 fragment read from LDS feeds 4 MFMAs (one per row group) instead of 2.  Every
+// column has the same scale (127 units), so the key is (D~ << tb) | tag with the shift tb in one
+// VGPR and the tag (2 tc + jb) 16 + r in an SGPR: 2.5 VALU per screened value, no per-column
+// multiply.  Tiles of 64 columns stream by LDS-DMA into a 4-slot ring (3 in flight, 16-B chunks
+// XOR-swizzled by row, so the fragment reads are conflict-free; each lane's 8 chunk offsets are
+// loop-invariant registers).  Decisions: k_i8_match's KEYS rules (window (8 + 1.3e-4) |a| in
+// 127-units, rows below the 0.9 cosine bound decided without a dot), exact integer dots from the
+// row's own two lanes, deep halves re-scored by the wave.  |D~| <= 2032 * 135 < 2^19, so keys fit
+// 31 bits up to tb = 12 (n1 <= 8192).
+// ---------------------------------------------------------------------------
+constexpr int IT_NW = 8, IT_NT = 64 * IT_NW, IT_RG = 4, IT_BM = 32 * IT_RG * IT_NW;  // 1024 rows
+constexpr int IT_NBUF = 4, IT_TILE = M_BN * KD;                                     // 16 KiB slots
+constexpr int IT_RPW = M_BN / IT_NW, IT_DPW = IT_RPW / 4;                           // 8 rows, 2 pieces
+constexpr int IT_OFF_NA = IT_NBUF * IT_TILE;       // [IT_BM] i32 |a|^2
+constexpr int IT_OFF_LM = IT_OFF_NA + IT_BM * 4;   // [IT_BM] deep rows' halves
+constexpr int IT_LDS = IT_OFF_LM + IT_BM * 4;
+static_assert(IT_LDS <= 160 * 1024, "LDS");
+static_assert(IT_DPW == 2, "8 waves: 2 DMA pieces per wave and tile");
+
+__global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, const int *__restrict__ n0v,
+                                                        const int *__restrict__ n1v,
+                                                        const int8_t *__restrict__ desc0,
+                                                        const int8_t *__restrict__ desc1, const int *__restrict__ nb_v,
+                                                        int *__restrict__ match_idx, int *__restrict__ match_dot,
+                                                        const int8_t *__restrict__ q1v, int cap64) {
+    __shared__ __attribute__((aligned(16))) char lds[IT_LDS];
+    int *na_s = reinterpret_cast<int *>(lds + IT_OFF_NA);
+    unsigned *lmask = reinterpret_cast<unsigned *>(lds + IT_OFF_LM);
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    const int pair = L / tiles_r, tr = L % tiles_r;
+    const int n0 = min(max(n0v[pair], 0), cap), n1 = min(max(n1v[pair], 0), cap);
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int row0 = tr * IT_BM;
+    int *oidx = match_idx + (size_t)pair * cap + row0;
+    int *odot = match_dot + (size_t)pair * cap + row0;
+    for (int r = t; r < IT_BM && row0 + r < cap; r += IT_NT)
+        if (row0 + r >= n0 || n1 <= 0) {
+            oidx[r] = -1;
+            odot[r] = 0;
+        }
+    if (row0 >= n0 || n1 <= 0) return;
+    const int8_t *A = desc0 + (size_t)pair * cap * KD;
+    const int8_t *B = desc1 + (size_t)pair * cap * KD;
+    const int *nb = nb_v + (size_t)pair * cap;
+    const int ntc = (n1 + M_BN - 1) / M_BN;
+    const int8_t *Bt = q1v + (size_t)pair * cap64 * KD;  // unit-norm codes, zero rows past n1
+
+    // ---- B DMA: wave w fills rows 8 w .. +7 of a tile, 4 rows (1 KiB) per instruction; lane l ->
+    //      row 8 w + (l >> 4) (+ 4), chunk position l & 15 <- source chunk (l & 15) ^ (row & 15) ----
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    const int dr = wu * IT_RPW + (lane >> 4);
+    const unsigned dcb = (unsigned)((lane & 15) ^ (dr & 15)) * 16;
+    const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char *)lds;
+    const unsigned dst_w = lds_base + (unsigned)(wu * IT_RPW * KD);
+    // (row dr + 4: its chunk swizzle (dr + 4) & 15 = (dr & 15) ^ 4 -- bit 2 of dr is 0 -- so its
+    // source offset is (o_ ^ 64) + 4 rows, and its LDS rows 4 later)
+#define IT_STAGE(TC, SLOT)                                                                   \
+    do {                                                                                     \
+        const unsigned o_ = (unsigned)((TC) * M_BN + dr) * KD + dcb;                         \
+        glds16_i8<0, (SLOT) * IT_TILE>(Bt, o_, dst_w);                                       \
+        glds16_i8<4 * KD, (SLOT) * IT_TILE + 4 * KD>(Bt, o_ ^ 64u, dst_w);                   \
+    } while (0)
+    // prologue: tiles 0, 1, 2 before the A rows are read
+    if (ntc > 0) IT_STAGE(0, 0);
+    if (ntc > 1) IT_STAGE(1, 1);
+    if (ntc > 2) IT_STAGE(2, 2);
+
+    // ---- A: the wave's 4 x 32 rows (w 128 + 32 g + fr) as the B operand (lane l: row l & 31,
+    //      k = 32 s + 16 (l >> 5) .. +15 at k32 step s); |a|^2 along the way ----
+    const int fr = lane & 31, fh = lane >> 5;
+    i32x4 aI[IT_RG][KD / 32];
+    int na_r[IT_RG];
+#pragma unroll
+    for (int g = 0; g < IT_RG; g++) {
+        const int8_t *arow = A + (size_t)min(row0 + w * (32 * IT_RG) + g * 32 + fr, n0 - 1) * KD + fh * 16;
+#pragma unroll
+        for (int s2 = 0; s2 < KD / 32; s2++) aI[g][s2] = *reinterpret_cast<const i32x4 *>(arow + s2 * 32);
+    }
+#pragma unroll
+    for (int g = 0; g < IT_RG; g++) {
+        int q = 0;
+#pragma unroll
+        for (int s2 = 0; s2 < KD / 32; s2++)
+#pragma unroll
+            for (int u = 0; u < 4; u++) q = __builtin_amdgcn_sdot4(aI[g][s2][u], aI[g][s2][u], q, false);
+        q += __shfl_xor(q, 32, 64);
+        if (fh == 0) na_s[w * (32 * IT_RG) + g * 32 + fr] = q;
+        na_r[g] = q;
+    }
+
+    // fragment of column block jb, k32 step s: ring row 32 jb + fr, chunk (2 s + fh) ^ (fr & 15)
+    const int xsw = fh ^ (fr & 15);
+    int cho[KD / 32];
+#pragma unroll
+    for (int s2 = 0; s2 < KD / 32; s2++) {
+        cho[s2] = fr * KD + (((2 * s2) ^ xsw) << 4);
+        asm volatile("" : "+v"(cho[s2]));  // loop-invariant offsets, kept in registers
+    }
+    const int tb = 32 - __builtin_clz(32 * ntc - 1);  // tags (2 tc + jb) 16 + r < 32 ntc
+    int vsh = tb;
+    asm volatile("" : "+v"(vsh));  // the key shift as a VGPR operand (the tags take the SGPR slot)
+    const float kinit = __int_as_float((int)0x80000000);
+    float m1[IT_RG], m2[IT_RG];
+#pragma unroll
+    for (int g = 0; g < IT_RG; g++) {
+        m1[g] = kinit;
+        m2[g] = kinit;
+    }
+    i32x16 acc[2];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {  // the unit before tile 0: folded, then discarded
+        acc[0][q] = 0;
+        acc[1][q] = 0;
+    }
+    // unit U (column block U >> 2, row group U & 3) of the tile in ring slot SL: 8 MFMAs into
+    // acc[U & 1], each beside the fold of 2 of the previous unit's values; fragments 2 k32 steps
+    // ahead across the tile's units (fb_: constant indices)
+#define IT_UNIT(U, PT)                                                                       \
+    do {                                                                                     \
+        _Pragma("unroll") for (int s_ = 0; s_ < KD / 32; s_++) {                             \
+            const int gn_ = 8 * (U) + s_ + 2;                                                \
+            if (gn_ < 64) fb_[gn_] = *reinterpret_cast<const i32x4 *>(rs + (gn_ >> 5) * 32 * KD + cho[gn_ & 7]); \
+            if (s_ == 0) {                                                                   \
+                const i32x16 z_ = {};                                                        \
+                acc[(U) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fb_[8 * (U)], aI[(U) & 3][0], z_, 0, 0, 0); \
+            } else {                                                                         \
+                acc[(U) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fb_[8 * (U) + s_], aI[(U) & 3][s_], acc[(U) & 1], 0, 0, 0); \
+            }                                                                                \
+            fold_keys_i8(acc[((U) + 1) & 1][2 * s_], acc[((U) + 1) & 1][2 * s_ + 1], vsh, (PT) + 2u * s_, \
+                         (PT) + 2u * s_ + 1u, m1[((U) + 3) & 3], m2[((U) + 3) & 3]);           \
+            __builtin_amdgcn_sched_barrier(0);                                               \
+        }                                                                                    \
+    } while (0)
+
+    wait_vm_i8<0>();  // the prologue's tiles and the A rows
+    __syncthreads();
+    for (int tc = 0; tc < ntc; tc++) {
+        if (tc + 3 < ntc) {  // tile tc + 3 into the slot tile tc - 1 left (every wave is past it)
+            const int sl_ = (tc + 3) & 3;
+            if (sl_ == 0) IT_STAGE(tc + 3, 0);
+            else if (sl_ == 1) IT_STAGE(tc + 3, 1);
+            else if (sl_ == 2) IT_STAGE(tc + 3, 2);
+            else IT_STAGE(tc + 3, 3);
+        }
+        const char *rs = lds + (tc & 3) * IT_TILE;
+        const unsigned tg0 = __builtin_amdgcn_readfirstlane(32u * (unsigned)tc);
+        const unsigned tgp = tg0 - 16u, tg1 = tg0 + 16u;
+        i32x4 fb_[64];
+        fb_[0] = *reinterpret_cast<const i32x4 *>(rs + cho[0]);
+        fb_[1] = *reinterpret_cast<const i32x4 *>(rs + cho[1]);
+        IT_UNIT(0, tgp);
+        if (tc == 0) {
+            m1[3] = kinit;
+            m2[3] = kinit;
+        }
+        IT_UNIT(1, tg0);
+        IT_UNIT(2, tg0);
+        IT_UNIT(3, tg0);
+        IT_UNIT(4, tg0);
+        IT_UNIT(5, tg1);
+        IT_UNIT(6, tg1);
+        IT_UNIT(7, tg1);
+        if (tc + 3 < ntc) {  // tile tc + 1 landed (tc + 2, tc + 3 may be in flight)
+            wait_vm_i8<2 * IT_DPW>();
+        } else if (tc + 2 < ntc) {
+            wait_vm_i8<IT_DPW>();
+        } else {
+            wait_vm_i8<0>();
+        }
+        __syncthreads();
+    }
+    {  // unit 7 of the last tile
+        const unsigned tl = __builtin_amdgcn_readfirstlane(32u * (unsigned)(ntc - 1) + 16u);
+#pragma unroll
+        for (int s_ = 0; s_ < KD / 32; s_++)
+            fold_keys_i8(acc[1][2 * s_], acc[1][2 * s_ + 1], vsh, tl + 2u * s_, tl + 2u * s_ + 1u, m1[3], m2[3]);
+    }
+#undef IT_UNIT
+#undef IT_STAGE
+
+    // ---- decisions: row i = 32 g + fr of the wave in lanes fr (columns with (j >> 2) & 1 = 0) and
+    //      fr + 32 (= 1) ----
+    const unsigned tmask = (1u << tb) - 1u;
+    auto kcol = [&](float a, int h) {
+        const unsigned tg = __float_as_uint(a) & tmask;
+        return (int)(tg >> 4) * 32 + 8 * (int)((tg >> 2) & 3u) + (int)(tg & 3u) + 4 * h;
+    };
+    unsigned deep_rows[IT_RG];
+#pragma unroll
+    for (int g = 0; g < IT_RG; g++) {
+        const float e1 = m1[g], e2 = m2[g];
+        const float o1 = __shfl_xor(e1, 32, 64), o2 = __shfl_xor(e2, 32, 64);
+        const int i1 = __float_as_int(e1), j1 = __float_as_int(o1);
+        const float M = i1 >= j1 ? e1 : o1;
+        const int Mh = i1 > j1 ? fh : (j1 > i1 ? 1 - fh : 0);
+        const int M2i = max(max(__float_as_int(e2), __float_as_int(o2)), min(i1, j1));
+        const int rl = w * (32 * IT_RG) + g * 32 + fr;
+        const bool live = row0 + rl < n0;
+        const double an = sqrt((double)na_r[g]);
+        const double da = an * (8.0 + 1.3e-4) * 1.0001 + 1e-6;
+        const double Mv = (double)(__float_as_int(M) >> tb);
+        const bool cand = live && na_r[g] > 0 && Mv + da > 0.0 && Mv + da > 114.3 * an * (1.0 - 1e-9);
+        const double limd = Mv - 2.0 * da;
+        const bool ambig = cand && (double)(M2i >> tb) >= limd;
+        const bool in1 = (double)(__float_as_int(e1) >> tb) >= limd, in2 = (double)(__float_as_int(e2) >> tb) >= limd;
+        const bool oin1 = __shfl_xor(in1 ? 1 : 0, 32, 64) != 0, oin2 = __shfl_xor(in2 ? 1 : 0, 32, 64) != 0;
+        const int I = kcol(M, Mh);
+        int nc = cand ? 1 : 0;
+        int cj0 = I, cj1 = -1;  // candidates (the row's two lanes run the same list)
+        unsigned wm = 3u;
+        if (ambig) {
+            if (in2 || oin2) {  // a half holds two columns inside: its every column is a candidate
+                nc = -1;
+                wm = (in1 ? 1u << fh : 0u) | (oin1 ? 1u << (1 - fh) : 0u);
+            } else {
+                const int jm = kcol(e1, fh), jo = __shfl_xor(jm, 32, 64);
+                const int ja = fh ? jo : jm, jb2 = fh ? jm : jo;  // half 0's, half 1's maximum
+                const bool ia = fh ? oin1 : in1, ib = fh ? in1 : oin1;
+                nc = (ia ? 1 : 0) + (ib ? 1 : 0);
+                cj0 = ia ? ja : jb2;
+                cj1 = ia && ib ? jb2 : -1;
+            }
+        } else if (cand && I >= n1) {  // a padding column (zero codes) on top: all columns
+            nc = -1;
+        }
+        int bj = -1;
+        long long bd = 0, bn = 1;
+        for (int k = 0; k < nc; k++) {
+            const int j = k == 0 ? cj0 : cj1;
+            if ((unsigned)j >= (unsigned)n1) continue;  // never a global read past the frame
+            const int8_t *brow = B + (size_t)j * KD + fh * 16;
+            i32x4 bv[KD / 32];
+#pragma unroll
+            for (int s2 = 0; s2 < KD / 32; s2++) bv[s2] = *reinterpret_cast<const i32x4 *>(brow + s2 * 32);
+            const long long nbj = nb[j];
+            int part = 0;
+#pragma unroll
+            for (int s2 = 0; s2 < KD / 32; s2++)
+#pragma unroll
+                for (int u = 0; u < 4; u++) part = __builtin_amdgcn_sdot4(aI[g][s2][u], bv[s2][u], part, false);
+            part += __shfl_xor(part, 32, 64);
+            if (part > 0 && nbj > 0 && better(part, nbj, j, bd, bn, bj)) {
+                bj = j;
+                bd = part;
+                bn = nbj;
+            }
+        }
+        if (fh == 0 && live && nc >= 0) {
+            const long long na = na_r[g];
+            const bool keep = bj >= 0 &&
+                              (unsigned __int128)(100ll * bd * bd) > (unsigned __int128)81 * (unsigned long long)(na * bn);
+            oidx[rl] = keep ? bj : -1;
+            odot[rl] = keep ? (int)bd : 0;
+        }
+        if (fh == 0 && live && nc < 0) lmask[rl] = wm;
+        deep_rows[g] = (unsigned)__ballot(fh == 0 && live && nc < 0);
+    }
+    // ---- deep rows (rare): every column of the listed halves, one column per lane at a time ----
+#pragma unroll
+    for (int g = 0; g < IT_RG; g++)
+        for (unsigned dm = deep_rows[g]; dm; dm &= dm - 1) {
+            const int rl = w * (32 * IT_RG) + g * 32 + __builtin_ctz(dm);
+            const unsigned wm = lmask[rl];
+            const i32x4 *arow = reinterpret_cast<const i32x4 *>(A + (size_t)(row0 + rl) * KD);
+            i32x4 av[KD / 16];
+#pragma unroll
+            for (int v = 0; v < KD / 16; v++) av[v] = arow[v];
+            int bj = -1;
+            long long bd = 0, bn = 1;
+            for (int j = lane; j < n1; j += 64) {
+                if (!((wm >> ((j >> 2) & 1)) & 1u)) continue;
+                const i32x4 *brow = reinterpret_cast<const i32x4 *>(B + (size_t)j * KD);
+                i32x4 bv[KD / 16];
+#pragma unroll
+                for (int v = 0; v < KD / 16; v++) bv[v] = brow[v];
+                const long long nbj = nb[j];
+                int d = 0;
+#pragma unroll
+                for (int v = 0; v < KD / 16; v++)
+#pragma unroll
+                    for (int u = 0; u < 4; u++) d = __builtin_amdgcn_sdot4(av[v][u], bv[v][u], d, false);
+                if (d > 0 && nbj > 0 && better(d, nbj, j, bd, bn, bj)) {
+                    bj = j;
+                    bd = d;
+                    bn = nbj;
+                }
+            }
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const long long od = __shfl_xor(bd, o, 64), on = __shfl_xor(bn, o, 64);
+                const int oj = __shfl_xor(bj, o, 64);
+                if (oj >= 0 && better(od, on, oj, bd, bn, bj)) {
+                    bj = oj;
+                    bd = od;
+                    bn = on;
+                }
+            }
+            if (lane == 0) {
+                const long long na = na_s[rl];
+                const bool keep = bj >= 0 &&
+                                  (unsigned __int128)(100ll * bd * bd) > (unsigned __int128)81 * (unsigned long long)(na * bn);
+                oidx[rl] = keep ? bj : -1;
+                odot[rl] = keep ? (int)bd : 0;
+            }
+        }
+}
+
 }  // namespace
 
 namespace mv {
 
-static bool i8_keys(int cap) { return I8_KEYS && 2 * ((cap + M_BN - 1) / M_BN) <= 256; }
+// k_i8t_match (the default while n1 <= 8192: keys within 31 bits; MV_I8_KERNEL=m selects k_i8_match)
+static bool i8_transposed(int cap) {
+    static const int off = [] {
+        const char *e = getenv("MV_I8_KERNEL");
+        return e && e[0] == 'm' ? 1 : 0;
+    }();
+    return !off && cap <= 8192;
+}
+static bool i8_keys(int cap) { return (I8_KEYS || i8_transposed(cap)) && 2 * ((cap + M_BN - 1) / M_BN) <= 256; }
 static int i8_cap64(int cap) { return (cap + M_BN - 1) / M_BN * M_BN; }
 
 size_t allpairs_i8_scratch_bytes(int batch, int cap) {
@@ -704,12 +1026,23 @@ int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const i
         hipLaunchKernelGGL(k_i8_norms, dim3(nblk), dim3(256), 0, s, (long)rows, desc1, nb, rnb);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
+    MV_REQUIRE((long)cap * KD < (1l << 31));  // 32-bit DMA source offsets within a pair
+    MV_REQUIRE((long)cap64 * KD < (1l << 31));
+    if (i8_transposed(cap)) {
+        const int tiles_t = (cap + IT_BM - 1) / IT_BM;
+        const long tblocks = (long)batch * tiles_t;
+        MV_REQUIRE(tblocks < (1l << 31));
+        MV_PROF_BEGIN(s, "k_i8t_match");
+        hipLaunchKernelGGL(k_i8t_match, dim3((unsigned)tblocks), dim3(IT_NT), 0, s, tiles_t, cap, n0, n1, desc0, desc1,
+                           nb, match_idx, match_dot, q1, cap64);
+        MV_PROF_END(s);
+        MV_LAUNCH_CHECK();
+        return MV_OK;
+    }
     const int tiles_m = (cap + M_BM - 1) / M_BM;
     const long mblocks = (long)batch * tiles_m;
     MV_REQUIRE(mblocks < (1l << 31));
-    MV_REQUIRE((long)cap * KD < (1l << 31));  // 32-bit DMA source offsets within a pair
     MV_PROF_BEGIN(s, "k_i8_match");
-    MV_REQUIRE((long)cap64 * KD < (1l << 31));
     if (keys)
         hipLaunchKernelGGL(k_i8_match<true>, dim3((unsigned)mblocks), dim3(M_NT), 0, s, tiles_m, cap, n0, n1, desc0,
                            desc1, nb, rnb, match_idx, match_dot, q1, cap64);

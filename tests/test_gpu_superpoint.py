@@ -140,3 +140,35 @@ def test_superpoint_one_net_two_streams(ctx, orc, torch_cuda, sp, weights):
         imgs = sets[k % 2][:2]
         got = tuple(t.cpu().numpy()[:2] for t in o)
         _check(orc, weights, imgs, got, 192, 640)
+
+
+def test_network_int8_descriptors_through_int8_allpairs(ctx, orc, torch_cuda, sp):
+    """configs[4] on descriptors the NETWORK produced (not synthetic draws): the int8 desc of KITTI
+    00 frames 000000 / 000001 from mv_superpoint_forward_dev (1920 cells x 256 each, bit-exact to
+    the oracle above) matched all-pairs on the int8 matrix cores (k_i8t_match, both 1024-row
+    workgroups of the pair live), indices and exact dots equal to the oracle's; both directions."""
+    ims = load_golden("kitti00_images.npz")
+    imgs = [ims["img_000000"], ims["img_000001"]]
+    _, desc, _, _ = _run(ctx, torch_cuda, sp, imgs, 192, 640)
+    dev = torch_cuda.device("cuda:0")
+    for a, c in ((desc[0], desc[1]), (desc[1], desc[0])):
+        n = a.shape[0]
+        cap = 2048
+        D0 = np.zeros((1, cap, 256), np.int8)
+        D1 = np.zeros((1, cap, 256), np.int8)
+        D0[0, :n], D1[0, :n] = a, c
+        nn_ = torch_cuda.full((1,), n, dtype=torch_cuda.int32, device=dev)
+        idx = torch_cuda.full((1, cap), -7, dtype=torch_cuda.int32, device=dev)
+        dot = torch_cuda.zeros((1, cap), dtype=torch_cuda.int32, device=dev)
+        ctx.set_stream(torch_cuda.cuda.current_stream())
+        try:
+            ctx.match_allpairs_i8(torch_cuda.from_numpy(D0).to(dev), torch_cuda.from_numpy(D1).to(dev), nn_, nn_, idx,
+                                  dot)
+            torch_cuda.cuda.synchronize()
+        finally:
+            ctx.set_stream(None)
+        i2, d2 = orc.allpairs_i8(a, c)
+        got_i, got_d = idx.cpu().numpy()[0], dot.cpu().numpy()[0]
+        assert (got_i[:n] == i2).all() and (got_d[:n] == d2).all()
+        assert (got_i[n:] == -1).all()
+        assert (i2 >= 0).sum() > 100  # consecutive frames: many cells re-observed above cos 0.9

@@ -63,7 +63,7 @@ def run(batch=2048, kp=2048, steps=20, warmup=3, check=1, cpu_seconds=0.0):
     el = time.perf_counter() - t0
     mvtrack.profile_enable(False)
     stages = {}
-    for k in ("k_i8_norms", "k_i8_prep", "k_i8_match"):
+    for k in ("k_i8_norms", "k_i8_prep", "k_i8_match", "k_i8t_match"):
         ms, c = mvtrack.profile_query(k)
         if c:
             stages[k] = round(ms / c, 4)
@@ -76,12 +76,13 @@ def run(batch=2048, kp=2048, steps=20, warmup=3, check=1, cpu_seconds=0.0):
             assert (idx[b].cpu().numpy() == i2).all(), "int8 match differs from the oracle"
             checked += 1
     ops = 2.0 * n * n * D * B
-    scr = stages["k_i8_match"] * 1e-3
+    km = "k_i8t_match" if "k_i8t_match" in stages else "k_i8_match"  # the transposed kernel (default)
+    scr = stages[km] * 1e-3
     out = {"metric": "int8 all-pairs frame-pairs/sec (%d kp x 256-D, exact cosine)" % n,
            "value": round(B / (el / args.steps), 1), "unit": "pairs/s", "batch": B,
            "ms_per_step": round(el / args.steps * 1e3, 4), "stages_ms": stages,
            "matches_avg": float((idx >= 0).float().sum(1).mean()),
-           "mfma_roofline": {"kernel": "k_i8_match", "achieved_TOPS": round(ops / scr / 1e12, 1) if scr else None,
+           "mfma_roofline": {"kernel": km, "achieved_TOPS": round(ops / scr / 1e12, 1) if scr else None,
                              "peak_TOPS": I8_PEAK_TOPS,
                              "frac": round(ops / scr / 1e12 / I8_PEAK_TOPS, 4) if scr else None},
            "checked_pairs": checked}
