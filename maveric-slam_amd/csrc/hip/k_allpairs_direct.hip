@@ -133,6 +133,21 @@ __device__ __forceinline__ void fold_keys(int a, int b, int sha, int shb, unsign
     m1f = __int_as_float(m1);
     m2f = __int_as_float(m2);
 }
+// the same with the keys built by compiler-visible instructions, for the first values folded after
+// an MFMA chain's last instruction: the compiler pads the MFMA-result -> VALU hazard before its own
+// instructions, not before an asm block (k_i8t_match's first pair per unit read stale registers)
+__device__ __forceinline__ void fold_keys_cv(int a, int b, int sha, int shb, unsigned ta, unsigned tb, float &m1f,
+                                             float &m2f) {
+    const int ka = (int)(((unsigned)a << (sha & 31)) | ta), kb = (int)(((unsigned)b << (shb & 31)) | tb);
+    int md, m1 = __float_as_int(m1f), m2 = __float_as_int(m2f);
+    asm("v_med3_i32 %0, %1, %3, %4\n\t"
+        "v_max3_i32 %1, %1, %3, %4\n\t"
+        "v_max_i32 %2, %2, %0"
+        : "=&v"(md), "+v"(m1), "+v"(m2)
+        : "v"(ka), "v"(kb));
+    m1f = __int_as_float(m1);
+    m2f = __int_as_float(m2);
+}
 // sum of an int over a row's 16 lanes (every lane of the 16 ends with it)
 __device__ __forceinline__ void row16_sum_i(int &c) {
     asm("s_nop 1\n\t"
@@ -776,8 +791,12 @@ __device__ __forceinline__ Sweep sweep_t(char *lds, const float *B, int n1, int 
             } else {                                                                         \
                 acc[(U) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fb_[8 * (U) + s_], aI[(U) & 3][s_], acc[(U) & 1], 0, 0, 0); \
             }                                                                                \
-            fold_keys(acc[((U) + 1) & 1][2 * s_], acc[((U) + 1) & 1][2 * s_ + 1], PSV[s_ >> 1], PSV[s_ >> 1], \
-                      (PT) + 2u * s_, (PT) + 2u * s_ + 1u, m1[((U) + 3) & 3], m2[((U) + 3) & 3]);  \
+            if (s_ == 0)                                                                     \
+                fold_keys_cv(acc[((U) + 1) & 1][0], acc[((U) + 1) & 1][1], PSV[0], PSV[0], (PT), (PT) + 1u, \
+                             m1[((U) + 3) & 3], m2[((U) + 3) & 3]);                          \
+            else                                                                             \
+                fold_keys(acc[((U) + 1) & 1][2 * s_], acc[((U) + 1) & 1][2 * s_ + 1], PSV[s_ >> 1], PSV[s_ >> 1], \
+                          (PT) + 2u * s_, (PT) + 2u * s_ + 1u, m1[((U) + 3) & 3], m2[((U) + 3) & 3]); \
             __builtin_amdgcn_sched_barrier(0);                                               \
         }                                                                                    \
     } while (0)

@@ -237,6 +237,23 @@ __device__ __forceinline__ void fold_keys_i8(int a, int b, int sh, unsigned ta, 
     m2f = __int_as_float(m2);
 }
 
+// the same with the keys built by compiler-visible instructions: for the first values folded after
+// an MFMA chain's LAST instruction -- the compiler pads the MFMA-result -> VALU read hazard before
+// its own instructions, not before an asm block (asm reading a result 2 instructions after its MFMA
+// got stale registers: k_i8t_match's first fold pair per unit)
+__device__ __forceinline__ void fold_keys_i8_cv(int a, int b, int sh, unsigned ta, unsigned tb, float &m1f,
+                                                float &m2f) {
+    const int ka = (int)(((unsigned)a << (sh & 31)) | ta), kb = (int)(((unsigned)b << (sh & 31)) | tb);
+    int md, m1 = __float_as_int(m1f), m2 = __float_as_int(m2f);
+    asm("v_med3_i32 %0, %1, %3, %4\n\t"
+        "v_max3_i32 %1, %1, %3, %4\n\t"
+        "v_max_i32 %2, %2, %0"
+        : "=&v"(md), "+v"(m1), "+v"(m2)
+        : "v"(ka), "v"(kb));
+    m1f = __int_as_float(m1);
+    m2f = __int_as_float(m2);
+}
+
 // D = 0x40800000 (the bits of 4.0) + A.B: the first k32 step of a chain, C as the inline
 // constant 4.0 (a builtin with a constant C gets it hoisted into 16 VGPRs); the chain's next
 // MFMA reads D as SrcC with exact overlap (hardware forwarding, no wait states)
@@ -807,8 +824,12 @@ __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, co
             } else {                                                                         \
                 acc[(U) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fb_[8 * (U) + s_], aI[(U) & 3][s_], acc[(U) & 1], 0, 0, 0); \
             }                                                                                \
-            fold_keys_i8(acc[((U) + 1) & 1][2 * s_], acc[((U) + 1) & 1][2 * s_ + 1], vsh, (PT) + 2u * s_, \
-                         (PT) + 2u * s_ + 1u, m1[((U) + 3) & 3], m2[((U) + 3) & 3]);           \
+            if (s_ == 0)                                                                     \
+                fold_keys_i8_cv(acc[((U) + 1) & 1][0], acc[((U) + 1) & 1][1], vsh, (PT), (PT) + 1u, \
+                                m1[((U) + 3) & 3], m2[((U) + 3) & 3]);                       \
+            else                                                                             \
+                fold_keys_i8(acc[((U) + 1) & 1][2 * s_], acc[((U) + 1) & 1][2 * s_ + 1], vsh, (PT) + 2u * s_, \
+                             (PT) + 2u * s_ + 1u, m1[((U) + 3) & 3], m2[((U) + 3) & 3]);       \
             __builtin_amdgcn_sched_barrier(0);                                               \
         }                                                                                    \
     } while (0)
