@@ -714,6 +714,9 @@ constexpr int IT_OFF_LM = IT_OFF_NA + IT_BM * 4;   // [IT_BM] deep rows' halves
 constexpr int IT_LDS = IT_OFF_LM + IT_BM * 4;
 static_assert(IT_LDS <= 160 * 1024, "LDS");
 static_assert(IT_DPW == 2, "8 waves: 2 DMA pieces per wave and tile");
+#ifndef IT_REUSE
+#define IT_REUSE 1  // a column block's 8 fragments read once and kept for its 4 row groups
+#endif
 
 __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, const int *__restrict__ n0v,
                                                         const int *__restrict__ n1v,
@@ -813,17 +816,32 @@ __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, co
     // unit U (column block U >> 2, row group U & 3) of the tile in ring slot SL: 8 MFMAs into
     // acc[U & 1], each beside the fold of 2 of the previous unit's values; fragments 2 k32 steps
     // ahead across the tile's units (fb_: constant indices)
+#if IT_REUSE
+    // the column block's 8 fragments (32 VGPRs) feed its 4 units: read once per block (block 1's
+    // replace block 0's, one k32 step at a time, during unit 3, each right after its last MFMA)
+#define IT_FRAG(U, S) fq_[S]
+#define IT_NEXT(U, S)                                                                        \
+    if ((U) == 3) fq_[S] = *reinterpret_cast<const i32x4 *>(rs + 32 * KD + cho[S]);
+#else
+    // fragments re-read per unit, 2 k32 steps ahead across the tile's units (fb_: constant indices)
+#define IT_FRAG(U, S) fb_[8 * (U) + (S)]
+#define IT_NEXT(U, S)                                                                        \
+    {                                                                                        \
+        const int gn_ = 8 * (U) + (S) + 2;                                                   \
+        if (gn_ < 64) fb_[gn_] = *reinterpret_cast<const i32x4 *>(rs + (gn_ >> 5) * 32 * KD + cho[gn_ & 7]); \
+    }
+#endif
 #define IT_UNIT(U, PT)                                                                       \
     do {                                                                                     \
         _Pragma("unroll") for (int s_ = 0; s_ < KD / 32; s_++) {                             \
-            const int gn_ = 8 * (U) + s_ + 2;                                                \
-            if (gn_ < 64) fb_[gn_] = *reinterpret_cast<const i32x4 *>(rs + (gn_ >> 5) * 32 * KD + cho[gn_ & 7]); \
+            if (!IT_REUSE) { IT_NEXT(U, s_) }                                                \
             if (s_ == 0) {                                                                   \
                 const i32x16 z_ = {};                                                        \
-                acc[(U) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fb_[8 * (U)], aI[(U) & 3][0], z_, 0, 0, 0); \
+                acc[(U) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(IT_FRAG(U, 0), aI[(U) & 3][0], z_, 0, 0, 0); \
             } else {                                                                         \
-                acc[(U) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fb_[8 * (U) + s_], aI[(U) & 3][s_], acc[(U) & 1], 0, 0, 0); \
+                acc[(U) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(IT_FRAG(U, s_), aI[(U) & 3][s_], acc[(U) & 1], 0, 0, 0); \
             }                                                                                \
+            if (IT_REUSE) { IT_NEXT(U, s_) }                                                 \
             if (s_ == 0)                                                                     \
                 fold_keys_i8_cv(acc[((U) + 1) & 1][0], acc[((U) + 1) & 1][1], vsh, (PT), (PT) + 1u, \
                                 m1[((U) + 3) & 3], m2[((U) + 3) & 3]);                       \
@@ -847,9 +865,15 @@ __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, co
         const char *rs = lds + (tc & 3) * IT_TILE;
         const unsigned tg0 = __builtin_amdgcn_readfirstlane(32u * (unsigned)tc);
         const unsigned tgp = tg0 - 16u, tg1 = tg0 + 16u;
+#if IT_REUSE
+        i32x4 fq_[KD / 32];
+#pragma unroll
+        for (int s2 = 0; s2 < KD / 32; s2++) fq_[s2] = *reinterpret_cast<const i32x4 *>(rs + cho[s2]);
+#else
         i32x4 fb_[64];
         fb_[0] = *reinterpret_cast<const i32x4 *>(rs + cho[0]);
         fb_[1] = *reinterpret_cast<const i32x4 *>(rs + cho[1]);
+#endif
         IT_UNIT(0, tgp);
         if (tc == 0) {
             m1[3] = kinit;
@@ -879,6 +903,8 @@ __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, co
     }
 #undef IT_UNIT
 #undef IT_STAGE
+#undef IT_FRAG
+#undef IT_NEXT
 
     // ---- decisions: row i = 32 g + fr of the wave in lanes fr (columns with (j >> 2) & 1 = 0) and
     //      fr + 32 (= 1) ----
