@@ -717,6 +717,12 @@ static_assert(IT_DPW == 2, "8 waves: 2 DMA pieces per wave and tile");
 #ifndef IT_REUSE
 #define IT_REUSE 1  // a column block's 8 fragments read once and kept for its 4 row groups
 #endif
+#ifndef IT_XPF
+// > 0: the next tile's first IT_XPF block-0 fragments are read during unit 7 (each right after its
+// last MFMA), so no tile starts on exposed LDS latency; the barrier at a tile's end then needs the
+// next TWO tiles landed (one tile of DMA in flight across it instead of two).  8 spills ~150 VGPRs.
+#define IT_XPF 2
+#endif
 
 __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, const int *__restrict__ n0v,
                                                         const int *__restrict__ n1v,
@@ -821,7 +827,8 @@ __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, co
     // replace block 0's, one k32 step at a time, during unit 3, each right after its last MFMA)
 #define IT_FRAG(U, S) fq_[S]
 #define IT_NEXT(U, S)                                                                        \
-    if ((U) == 3) fq_[S] = *reinterpret_cast<const i32x4 *>(rs + 32 * KD + cho[S]);
+    if ((U) == 3) fq_[S] = *reinterpret_cast<const i32x4 *>(rs + 32 * KD + cho[S]);            \
+    if (IT_XPF && (U) == 7 && (S) < IT_XPF) fq_[S] = *reinterpret_cast<const i32x4 *>(rn + cho[S]);
 #else
     // fragments re-read per unit, 2 k32 steps ahead across the tile's units (fb_: constant indices)
 #define IT_FRAG(U, S) fb_[8 * (U) + (S)]
@@ -854,6 +861,11 @@ __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, co
 
     wait_vm_i8<0>();  // the prologue's tiles and the A rows
     __syncthreads();
+#if IT_REUSE
+    i32x4 fq_[KD / 32];  // tile 0's block-0 fragments (later tiles': read during the tile before)
+#pragma unroll
+    for (int s2 = 0; s2 < KD / 32; s2++) fq_[s2] = *reinterpret_cast<const i32x4 *>(lds + cho[s2]);
+#endif
     for (int tc = 0; tc < ntc; tc++) {
         if (tc + 3 < ntc) {  // tile tc + 3 into the slot tile tc - 1 left (every wave is past it)
             const int sl_ = (tc + 3) & 3;
@@ -866,9 +878,11 @@ __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, co
         const unsigned tg0 = __builtin_amdgcn_readfirstlane(32u * (unsigned)tc);
         const unsigned tgp = tg0 - 16u, tg1 = tg0 + 16u;
 #if IT_REUSE
-        i32x4 fq_[KD / 32];
+        const char *rn = lds + ((tc + 1) & 3) * IT_TILE;  // the next tile's slot (landed: see the wait below)
+        if (tc > 0) {  // (IT_XPF: the first IT_XPF came during the tile before)
 #pragma unroll
-        for (int s2 = 0; s2 < KD / 32; s2++) fq_[s2] = *reinterpret_cast<const i32x4 *>(rs + cho[s2]);
+            for (int s2 = IT_XPF; s2 < KD / 32; s2++) fq_[s2] = *reinterpret_cast<const i32x4 *>(rs + cho[s2]);
+        }
 #else
         i32x4 fb_[64];
         fb_[0] = *reinterpret_cast<const i32x4 *>(rs + cho[0]);
@@ -886,9 +900,9 @@ __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, co
         IT_UNIT(5, tg1);
         IT_UNIT(6, tg1);
         IT_UNIT(7, tg1);
-        if (tc + 3 < ntc) {  // tile tc + 1 landed (tc + 2, tc + 3 may be in flight)
-            wait_vm_i8<2 * IT_DPW>();
-        } else if (tc + 2 < ntc) {
+        if (tc + 3 < ntc) {  // tile tc + 1 (IT_XPF: and tc + 2) landed; tc + 3 (and tc + 2) may fly
+            wait_vm_i8<(IT_XPF ? 1 : 2) * IT_DPW>();
+        } else if (tc + 2 < ntc && !IT_XPF) {
             wait_vm_i8<IT_DPW>();
         } else {
             wait_vm_i8<0>();
