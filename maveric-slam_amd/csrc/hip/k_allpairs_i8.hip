@@ -717,12 +717,9 @@ static_assert(IT_DPW == 2, "8 waves: 2 DMA pieces per wave and tile");
 #ifndef IT_REUSE
 #define IT_REUSE 1  // a column block's 8 fragments read once and kept for its 4 row groups
 #endif
-#ifndef IT_XPF
-// > 0: the next tile's first IT_XPF block-0 fragments are read during unit 7 (each right after its
-// last MFMA), so no tile starts on exposed LDS latency; the barrier at a tile's end then needs the
-// next TWO tiles landed (one tile of DMA in flight across it instead of two).  8 spills ~150 VGPRs.
-#define IT_XPF 2
-#endif
+// (Measured and not kept: the next tile's first 2 / 4 block-0 fragments read during unit 7 with
+// the barrier waiting for two tiles -- 1.978-1.986 ms against 1.976-1.986 without; all 8 spill
+// ~150 VGPRs -- profiles/r05l_i8_xpf_ab.json.)
 
 __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, const int *__restrict__ n0v,
                                                         const int *__restrict__ n1v,
@@ -827,8 +824,7 @@ __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, co
     // replace block 0's, one k32 step at a time, during unit 3, each right after its last MFMA)
 #define IT_FRAG(U, S) fq_[S]
 #define IT_NEXT(U, S)                                                                        \
-    if ((U) == 3) fq_[S] = *reinterpret_cast<const i32x4 *>(rs + 32 * KD + cho[S]);            \
-    if (IT_XPF && (U) == 7 && (S) < IT_XPF) fq_[S] = *reinterpret_cast<const i32x4 *>(rn + cho[S]);
+    if ((U) == 3) fq_[S] = *reinterpret_cast<const i32x4 *>(rs + 32 * KD + cho[S]);
 #else
     // fragments re-read per unit, 2 k32 steps ahead across the tile's units (fb_: constant indices)
 #define IT_FRAG(U, S) fb_[8 * (U) + (S)]
@@ -878,10 +874,9 @@ __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, co
         const unsigned tg0 = __builtin_amdgcn_readfirstlane(32u * (unsigned)tc);
         const unsigned tgp = tg0 - 16u, tg1 = tg0 + 16u;
 #if IT_REUSE
-        const char *rn = lds + ((tc + 1) & 3) * IT_TILE;  // the next tile's slot (landed: see the wait below)
-        if (tc > 0) {  // (IT_XPF: the first IT_XPF came during the tile before)
+        if (tc > 0) {
 #pragma unroll
-            for (int s2 = IT_XPF; s2 < KD / 32; s2++) fq_[s2] = *reinterpret_cast<const i32x4 *>(rs + cho[s2]);
+            for (int s2 = 0; s2 < KD / 32; s2++) fq_[s2] = *reinterpret_cast<const i32x4 *>(rs + cho[s2]);
         }
 #else
         i32x4 fb_[64];
@@ -900,9 +895,9 @@ __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, co
         IT_UNIT(5, tg1);
         IT_UNIT(6, tg1);
         IT_UNIT(7, tg1);
-        if (tc + 3 < ntc) {  // tile tc + 1 (IT_XPF: and tc + 2) landed; tc + 3 (and tc + 2) may fly
-            wait_vm_i8<(IT_XPF ? 1 : 2) * IT_DPW>();
-        } else if (tc + 2 < ntc && !IT_XPF) {
+        if (tc + 3 < ntc) {  // tile tc + 1 landed (tc + 2, tc + 3 may be in flight)
+            wait_vm_i8<2 * IT_DPW>();
+        } else if (tc + 2 < ntc) {
             wait_vm_i8<IT_DPW>();
         } else {
             wait_vm_i8<0>();
