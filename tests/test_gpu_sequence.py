@@ -10,6 +10,16 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["i8", "i8s"])
+def seq_screen(request, ctx):
+    """the default screen runs sequence mode as k_q8t_match over the pairs in place (cap <= 1024);
+    the staged int8 screen through each frame's image once (k_q8_match<AI8>): both must equal the
+    oracle"""
+    ctx.set_allpairs_screen(request.param)
+    yield request.param
+    ctx.set_allpairs_screen("i8")
+
+
 def _bits(a):
     return np.ascontiguousarray(a).view(np.uint32)
 
@@ -49,7 +59,7 @@ def _run_seq(ctx, torch, D, ns, scores=True):
     return idx.cpu().numpy(), (sc.cpu().numpy() if scores else None)
 
 
-def test_sequence_vs_oracle_ragged(ctx, orc, torch_cuda):
+def test_sequence_vs_oracle_ragged(ctx, orc, torch_cuda, seq_screen):
     rng = np.random.default_rng(17)
     cap = 640
     ns = [640, 513, 0, 300, 640, 1, 257, 640]
@@ -72,7 +82,7 @@ def test_sequence_vs_oracle_ragged(ctx, orc, torch_cuda):
 
 
 @pytest.mark.parametrize("scores", [True, False])
-def test_sequence_full_size_equals_pairs(ctx, orc, torch_cuda, scores):
+def test_sequence_full_size_equals_pairs(ctx, orc, torch_cuda, scores, seq_screen):
     """65 frames x 1024 keypoints: equal to the independent-pair match of (frame b, frame b + 1),
     bit for bit, and to the oracle on the first and last pair."""
     torch = torch_cuda
@@ -120,7 +130,7 @@ def test_sequence_refuses_f16_screen_and_short_tracks(ctx, torch_cuda):
         ctx.match_sequence_f32(D[:1], n[:1], idx, None)
 
 
-def test_sequence_run_prepare_chain(ctx, orc, torch_cuda):
+def test_sequence_run_prepare_chain(ctx, orc, torch_cuda, seq_screen):
     """A track processed in chunks: the first chunk prepared, then each chunk matched while the next one's frames are staged in the
     same launch; chunks of different lengths and caps, ragged counts, scores and indices-only,
     each equal to the oracle pair by pair; a run without its prepare is refused."""

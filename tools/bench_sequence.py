@@ -114,8 +114,9 @@ def run(frames=8193, kp=1024, steps=20, warmup=3, check=1, pipeline=3, fused=Tru
         step()
     torch.cuda.synchronize()
     mvtrack.profile_enable(False)
-    st = {k: mvtrack.profile_query(k) for k in ("k_q8_split", "k_q8_match_seq", "k_pose_ransac")}
-    stages = {k: round(ms / max(c, 1), 4) for k, (ms, c) in st.items()}
+    st = {k: mvtrack.profile_query(k) for k in ("k_q8_split", "k_q8_match_seq", "k_q8t_match", "k_q8d_handback",
+                                                 "k_pose_ransac")}
+    stages = {k: round(ms / max(c, 1), 4) for k, (ms, c) in st.items() if c > 0}
     o = outs[0]
     checked = 0
     if check > 0:
@@ -137,14 +138,21 @@ def run(frames=8193, kp=1024, steps=20, warmup=3, check=1, pipeline=3, fused=Tru
     # index (4 B per row); fused: the next chunk's staging (per row 1 KiB read + 268 B written)
     split_bytes = F * n * (KD * 4 + 268)
     seq_bytes = F * n * 268 + B * n * 4 + (split_bytes if fused else 0)
-    mseq = stages["k_q8_match_seq"] * 1e-3
+    kseq = "k_q8_match_seq"
+    if "k_q8t_match" in stages:  # the default screen: the one-pass kernel over the pairs in place --
+        kseq = "k_q8t_match"     # both fp32 frames of every pair read (2 x 1 KiB per row) + the index
+        seq_bytes = B * n * (2 * KD * 4 + 4)
+        fused = False
+    mseq = stages[kseq] * 1e-3
     return {
-        "metric": "tracked frame-pairs/sec, sequence mode (consecutive frames, each quantised once), "
+        "metric": "tracked frame-pairs/sec, sequence mode (consecutive frames), "
                   "1024kp x 256-D KITTI shape",
         "value": round(B * steps / el, 2), "unit": "pairs/s", "ms_per_step": round(el / steps * 1e3, 4),
         "frames_per_step": F, "pairs_per_step": B, "pipeline": P, "stages_ms": stages,
-        "staging": "fused into k_q8_match_seq (next chunk)" if fused else "k_q8_split per chunk",
-        "hbm_roofline": {"kernel": "k_q8_match_seq", "bytes_per_launch": seq_bytes,
+        "staging": ("none: k_q8t_match reads the fp32 frames in place (pair b = frames b, b + 1)"
+                    if kseq == "k_q8t_match" else
+                    "fused into k_q8_match_seq (next chunk)" if fused else "k_q8_split per chunk"),
+        "hbm_roofline": {"kernel": kseq, "bytes_per_launch": seq_bytes,
                          "GBs": round(seq_bytes / mseq / 1e9, 1) if mseq > 0 else None,
                          "frac": round(seq_bytes / mseq / 1e9 / HBM_PEAK_GBS, 4) if mseq > 0 else None,
                          "includes_next_chunk_staging": fused, "peak_GBs": HBM_PEAK_GBS},
