@@ -878,7 +878,7 @@ __device__ __forceinline__ Sweep sweep_t(char *lds, const float *B, int n1, int 
 // the window straddles the threshold (or scores are asked for) -- deferred, cooperatively loaded
 // (coop_exact_dots) two groups at a time; inside: each half's m1 is a candidate when inside, and a
 // half whose m2 is inside may hide more -- the wave re-scores every column of such "wide" halves.
-__device__ __forceinline__ void epilogue_t(char *epi, const float2 *rowv, const float (&m1)[T_RG],
+__device__ __forceinline__ unsigned epilogue_t(char *epi, const float2 *rowv, const float (&m1)[T_RG],
                                            const float (&m2)[T_RG], double Bn, double Eb, int tb, int w, int lane,
                                            int n0, int n1, const float *__restrict__ A, const float *__restrict__ B,
                                            int *__restrict__ oidx, float *__restrict__ oscore, double thresh,
@@ -978,6 +978,12 @@ __device__ __forceinline__ void epilogue_t(char *epi, const float2 *rowv, const 
         if (fh == 0 && wide) lmask[rl] = wm;
         wide_rows[g] = (unsigned)__ballot(fh == 0 && wide);
     }
+    unsigned nwide = 0, nneed = 0;  // (traced builds) the wave's wide rows and deferred dots
+#pragma unroll
+    for (int g = 0; g < T_RG; g++) {
+        nwide += __popc(wide_rows[g]);
+        nneed += __popcll(__ballot(need_g[g] >= 0));
+    }
     // the deferred maximiser scores, two groups per call: lane (fr, fh) takes row fr of group 2 c + fh
 #pragma unroll
     for (int c = 0; c < T_RG / 2; c++) {
@@ -1038,6 +1044,7 @@ __device__ __forceinline__ void epilogue_t(char *epi, const float2 *rowv, const 
                 if (oscore) oscore[r] = keep ? ws : 0.f;
             }
         }
+    return nwide << 16 | nneed;
 }
 
 __global__ __launch_bounds__(D_NT, 2) void k_q8t_match(int cap, const int *__restrict__ n0v,
@@ -1087,15 +1094,18 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8t_match(int cap, const int *__res
     }
     const double Bn = sqrt((double)st.b2max) * 1.0001;
     const double Eb = 8.0001 * (double)st.smax + 1e-30;
-    epilogue_t(lds, rowv, m1, m2, Bn, Eb, tb, w, lane, n0, n1, A, B, oidx, oscore, thresh,
-               reinterpret_cast<const unsigned char *>(lds + T_OFF_COL));
+    const unsigned ecnt = epilogue_t(lds, rowv, m1, m2, Bn, Eb, tb, w, lane, n0, n1, A, B, oidx, oscore, thresh,
+                                     reinterpret_cast<const unsigned char *>(lds + T_OFF_COL));
+    (void)ecnt;
 #ifdef MV_TRACE
     D_STAMP(3);
+    ts_[8] = ecnt;
     if (lane == 0 && blockIdx.x < D_TRACE_BLOCKS) {
         unsigned long long *o = g_d_trace + ((size_t)blockIdx.x * D_NW + w) * 10;
         for (int k = 0; k < 6; k++) o[k] = ts_[k];  // memtime x 4, memrealtime at entry / after A
         o[6] = __smid();
         o[7] = __builtin_amdgcn_s_memrealtime();
+        o[8] = ts_[8];
         o[9] = ts_[9];
     }
 #endif

@@ -554,13 +554,15 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
 // pixels x 128 output channels; its 64 KiB input tile is staged into LDS with all 16 loads of a
 // thread in flight at once (each pixel's 16 chunks padded to 17: conflict-free fragment reads
 // at compile-time offsets), wave w owns tile rows 2w, 2w + 1 against 4 channel blocks (8 MFMAs
-// per k32 step); weights from L2 two steps ahead; the heads' outputs in the Frame layout.
+// per k32 step); weights from L2 two steps ahead; the heads' outputs in the Frame layout
+// (OMODE 1) or, OMODE 2, already dequantised as run()'s NCHW float32 [B][C][H][W] (out is a
+// float *, cstride = C, dq = the head's out_scale: PyTorch's dequantise dq * (float) code).
 constexpr int H1_TY = 8, H1_PS = 17, H1_CB = 4;
 template <int OMODE>
 __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv1x1(const int8_t *__restrict__ in, int H, int W,
                                                          const i32x4 *__restrict__ wf, const int *__restrict__ bq,
                                                          float rs, int ngroups, int tiles_x, int tiles_y,
-                                                         int8_t *__restrict__ out, int cstride) {
+                                                         int8_t *__restrict__ out, int cstride, float dq) {
     constexpr int NS = 8, NCH = 16, NCHUNK = H1_TY * TX * NCH;  // 256 channels
     __shared__ i32x4 tile[H1_TY * TX * H1_PS];
     int bid = blockIdx.x;
@@ -651,6 +653,30 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv1x1(const int8_t *__restric
             int8_t *gd = out + ((size_t)b * H * W + (size_t)gx * H + y0) * cstride;
             const int8_t *ls = stg + col * run;
             for (int o = lane; o < nb; o += 64) gd[o] = ls[o];
+        }
+        return;
+    }
+    if (OMODE == 2) {
+        // channel plane co: lanes fr = 0..31 on 32 consecutive pixels of a row (128 B per half-wave)
+        float *fo = reinterpret_cast<float *>(out);
+        const size_t plane = (size_t)H * W;
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int gy = y0 + 2 * w + j, gx = x0 + fr;
+            if (gy >= H || gx >= W) continue;
+            float *px = fo + (size_t)b * cstride * plane + (size_t)gy * W + gx;
+#pragma unroll
+            for (int cb = 0; cb < H1_CB; cb++)
+#pragma unroll
+                for (int qq = 0; qq < 4; qq++) {
+                    const int co = 32 * (H1_CB * g + cb) + 8 * qq + 4 * fh;
+                    if (co >= cstride) continue;
+                    int v[4];
+                    requant4(v, acc[j][cb][4 * qq], acc[j][cb][4 * qq + 1], acc[j][cb][4 * qq + 2], acc[j][cb][4 * qq + 3], rs, lo);
+#pragma unroll
+                    for (int e = 0; e < 4; e++)
+                        if (co + e < cstride) px[(size_t)(co + e) * plane] = dq * (float)(v[e] - SP_MAGIC_BITS);
+                }
         }
         return;
     }
@@ -901,7 +927,7 @@ int launch_conv(hipStream_t st, const mv_superpoint *net, int li, int B, int H, 
 
 template <int OMODE>
 int launch_conv1x1(hipStream_t st, const mv_superpoint *net, int li, int B, int H, int W, const int8_t *in,
-                   int8_t *out, int cstride) {
+                   int8_t *out, int cstride, float dq = 0.f) {
     const int tiles_x = (W + TX - 1) / TX, tiles_y = (H + H1_TY - 1) / H1_TY;
     const int ngroups = (net->cout_pad[li] + 32 * H1_CB - 1) / (32 * H1_CB);
     MV_REQUIRE(net->cout_pad[li] % (32 * H1_CB) == 0);  // whole 128-channel groups (65 -> 128, 256)
@@ -912,7 +938,7 @@ int launch_conv1x1(hipStream_t st, const mv_superpoint *net, int li, int B, int 
     hipLaunchKernelGGL((k_sp_conv1x1<OMODE>), dim3((unsigned)blocks), dim3(SP_NT), 0, st, in, H, W,
                        reinterpret_cast<const i32x4 *>(wd + net->frag_off[li]),
                        reinterpret_cast<const int *>(wd + net->bq_off[li]), net->rs[li], ngroups, tiles_x, tiles_y,
-                       out, cstride);
+                       out, cstride, dq);
     MV_LAUNCH_CHECK();
     return MV_OK;
 }
@@ -1031,51 +1057,12 @@ extern "C" int mv_superpoint_destroy(mv_superpoint *net) {
 }
 
 namespace {
-// run()'s network outputs as pairwise_pnp.py receives them (outs = net.forward(inp), :197-199: the
-// quantized model's DeQuantStub): the heads' int8 codes [B][cells][C] (cell = gx * Hc + gy, the
-// Frame layout) -> code * (float) out_scale as NCHW float32 [B][C][Hc][Wc] (PyTorch's dequantise:
-// one float product, fma(scale, code, 0)).  Workgroup = (frame, 4 grid columns): the columns'
-// 4 * Hc cells are CONTIGUOUS in the Frame layout (4 Hc C bytes), read with 16-B loads into LDS;
-// then thread -> (c, gy) writes the 4 columns' values as one 16-B store.
-constexpr int SP_DQ_COLS = 4;
-__global__ __launch_bounds__(256) void k_sp_dequant_nchw(const int8_t *__restrict__ codes, int C, int Hc, int Wc,
-                                                         float scale, float *__restrict__ out) {
-    extern __shared__ __attribute__((aligned(16))) int8_t dq_lds[];
-    const int ncb = (Wc + SP_DQ_COLS - 1) / SP_DQ_COLS;
-    const long b = blockIdx.x / ncb;
-    const int x0 = (blockIdx.x % ncb) * SP_DQ_COLS;
-    const int nx = min(SP_DQ_COLS, Wc - x0);
-    const long cells = (long)Hc * Wc;
-    const int8_t *src = codes + (b * cells + (long)x0 * Hc) * C;
-    const int nbytes = nx * Hc * C;  // contiguous
-    const int t = threadIdx.x;
-    // 16-B pieces while aligned, the tail byte by byte (C = 65 rows are not 16-B multiples)
-    const int head = (int)((16 - ((uintptr_t)src & 15)) & 15);
-    for (int i = t; i < min(head, nbytes); i += 256) dq_lds[i] = src[i];
-    const int body = max(nbytes - head, 0) / 16;
-    for (int i = t; i < body; i += 256)
-        *reinterpret_cast<int4 *>(dq_lds + head + 16 * i) = *reinterpret_cast<const int4 *>(src + head + 16 * i);
-    for (int i = head + 16 * body + t; i < nbytes; i += 256) dq_lds[i] = src[i];
-    __syncthreads();
-    float *dst = out + b * C * cells;
-    for (int q = t; q < C * Hc; q += 256) {
-        const int c = q / Hc, gy = q % Hc;
-        float v[SP_DQ_COLS];
-#pragma unroll
-        for (int i = 0; i < SP_DQ_COLS; i++) v[i] = i < nx ? scale * (float)dq_lds[(i * Hc + gy) * C + c] : 0.f;
-        float *o = dst + ((long)c * Hc + gy) * Wc + x0;
-        if (nx == SP_DQ_COLS && (((uintptr_t)o & 15) == 0)) {
-            *reinterpret_cast<float4 *>(o) = make_float4(v[0], v[1], v[2], v[3]);
-        } else {
-            for (int i = 0; i < nx; i++) o[i] = v[i];
-        }
-    }
-}
-
 // the network on `batch` frames into the heads' int8 codes semi [B][cells][65], desc [B][cells][256]
-// (Frame layout, before run()'s min-gap step); act: the two activation buffers of a_bytes each
+// (Frame layout, before run()'s min-gap step) or, semi_f / desc_f given, into the heads'
+// dequantised NCHW float32 outputs (run()'s net.forward); act: the two activation buffers of
+// a_bytes each
 int sp_network(hipStream_t st, mv_superpoint *net, int batch, int H, int W, int oh, int ow, const uint8_t *images,
-               int8_t *A, int8_t *Bf, int8_t *semi, int8_t *desc) {
+               int8_t *A, int8_t *Bf, int8_t *semi, int8_t *desc, float *semi_f = nullptr, float *desc_f = nullptr) {
     const char *wd = static_cast<const char *>(net->wdev);
     int r;
     int h = oh, w = ow;
@@ -1105,9 +1092,17 @@ int sp_network(hipStream_t st, mv_superpoint *net, int batch, int H, int W, int 
     if ((r = launch_conv<128, 3, false, true, 0>(st, net, 7, batch, h, w, A, Bf, 128)) != MV_OK) return r;
     // heads: Bf holds the shared encoder output
     if ((r = launch_conv<128, 3, false, true, 0>(st, net, 8, batch, h, w, Bf, A, 256)) != MV_OK) return r;
-    if ((r = launch_conv1x1<1>(st, net, 9, batch, h, w, A, semi, 65)) != MV_OK) return r;
+    if (semi_f)
+        r = launch_conv1x1<2>(st, net, 9, batch, h, w, A, reinterpret_cast<int8_t *>(semi_f), 65, net->dq_semi);
+    else
+        r = launch_conv1x1<1>(st, net, 9, batch, h, w, A, semi, 65);
+    if (r != MV_OK) return r;
     if ((r = launch_conv<128, 3, false, true, 0>(st, net, 10, batch, h, w, Bf, A, 256)) != MV_OK) return r;
-    if ((r = launch_conv1x1<1>(st, net, 11, batch, h, w, A, desc, 256)) != MV_OK) return r;
+    if (desc_f)
+        r = launch_conv1x1<2>(st, net, 11, batch, h, w, A, reinterpret_cast<int8_t *>(desc_f), 256, net->dq_desc);
+    else
+        r = launch_conv1x1<1>(st, net, 11, batch, h, w, A, desc, 256);
+    if (r != MV_OK) return r;
     MV_PROF_END(st);
     return MV_OK;
 }
@@ -1169,28 +1164,17 @@ extern "C" int mv_superpoint_forward_raw_dev(mv_context *ctx, mv_superpoint *net
     MV_REQUIRE((long)oh * ow * 64 < (1l << 31) && (long)batch * H * W < (1l << 40));
     MV_REQUIRE(((uintptr_t)semi & 15) == 0 && ((uintptr_t)coarse_desc & 15) == 0);
     MV_HIP_TRY(hipSetDevice(ctx->device));
-    const int h = oh / 8, w = ow / 8;
-    const size_t cells = (size_t)h * w;
+    // run()'s network outputs as pairwise_pnp.py receives them (outs = net.forward(inp), :197-199:
+    // the quantized model's DeQuantStub): the heads' epilogue writes code * (float) out_scale as
+    // NCHW float32 [B][C][oh / 8][ow / 8] directly (no int8 intermediate)
     const size_t a_bytes = mv::align_up((size_t)batch * oh * ow * 16, 256);
-    const size_t c_bytes = mv::align_up((size_t)batch * cells * (65 + 256), 256);  // the heads' codes
-    const long nblk = (long)batch * ((w + SP_DQ_COLS - 1) / SP_DQ_COLS);
-    // every shape check before anything is queued (the dequantisation's LDS holds SP_DQ_COLS columns)
-    MV_REQUIRE(nblk < (1l << 31) && (size_t)SP_DQ_COLS * h * 256 <= 64 * 1024);
-    int r = sp_act(net, 2 * a_bytes + c_bytes);
+    int r = sp_act(net, 2 * a_bytes);
     if (r != MV_OK) return r;
     int8_t *A = static_cast<int8_t *>(net->act), *Bf = A + a_bytes;
-    int8_t *cs = Bf + a_bytes, *cd = cs + (size_t)batch * cells * 65;
     hipStream_t st = ctx->stream;
     if (net->used) MV_HIP_TRY(hipStreamWaitEvent(st, net->done, 0));
-    if ((r = sp_network(st, net, batch, H, W, oh, ow, images, A, Bf, cs, cd)) != MV_OK) return r;
-    MV_PROF_BEGIN(st, "k_sp_dequant_nchw");
-    for (int head = 0; head < 2; head++) {
-        const int C = head ? 256 : 65;
-        hipLaunchKernelGGL(k_sp_dequant_nchw, dim3((unsigned)nblk), dim3(256), (size_t)SP_DQ_COLS * h * C, st,
-                           head ? cd : cs, C, h, w, head ? net->dq_desc : net->dq_semi, head ? coarse_desc : semi);
-        MV_LAUNCH_CHECK();
-    }
-    MV_PROF_END(st);
+    if ((r = sp_network(st, net, batch, H, W, oh, ow, images, A, Bf, nullptr, nullptr, semi, coarse_desc)) != MV_OK)
+        return r;
     MV_HIP_TRY(hipEventRecord(net->done, st));
     net->used = true;
     return MV_OK;

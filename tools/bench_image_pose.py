@@ -80,7 +80,7 @@ def run(frames=257, steps=10, warmup=2, check=1):
     torch.cuda.synchronize()
     mvtrack.profile_enable(False)
     stages = {}
-    for k in ("k_sp_conv", "k_sp_dequant_nchw", "k_kp_heat", "k_kp_nms", "k_kp_sample_planes", "k_kp_normalize",
+    for k in ("k_sp_conv", "k_kp_heat", "k_kp_nms", "k_kp_sample_planes", "k_kp_normalize",
               "k_q8t_match", "k_q8d_handback", "k_q8d_match", "k_pose_ransac"):
         ms, c = mvtrack.profile_query(k)
         if c:

@@ -40,6 +40,9 @@ print("per-wave phase cycles (median / p10 / p90 / max):")
 for k, nm in enumerate(names):
     v = d[:, :, k].ravel()
     print("  %-12s %9.0f %9.0f %9.0f %9.0f" % (nm, np.median(v), np.percentile(v, 10), np.percentile(v, 90), v.max()))
+c = tr[:, :, 8]
+print("wide rows per pair: mean %.2f p90 %.0f max %d; deferred dots per pair mean %.1f" % (
+    (c >> 16).sum(1).mean(), np.percentile((c >> 16).sum(1), 90), (c >> 16).sum(1).max(), (c & 0xffff).sum(1).mean()))
 tot = st[:, :, 3] - st[:, :, 0]
 print("wave total median %.0f; sweep per tile %.0f" % (np.median(tot), np.median(d[:, :, 1]) / 16))
 sm = tr[:, 0, 6]
