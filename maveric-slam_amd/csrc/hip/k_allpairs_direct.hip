@@ -676,7 +676,20 @@ constexpr int T_OFF_MISC = T_OFF_ROW + T_BM * 8;    // [NW][4] per-wave statisti
 constexpr int T_OFF_COL = T_OFF_MISC + D_NW * 16;   // each frame-1 column's key shift (1 B)
 constexpr int T_LDS = T_OFF_COL + T_BM;
 constexpr int T_EPI_MASK = D_NW * 8192;             // epilogue: [NW] 8-KiB re-score buffers, [T_BM] wide masks
-static_assert(T_EPI_MASK + T_BM * 4 <= T_OFF_ROW, "the epilogue fits staging + ring");
+// re-screened wide rows (rescan_t): [T_BM] int key limits, [NW][128] the wave's rows, [NW][32 x 2]
+// candidate lists of T_RS_CAP columns (one per row of a batch and lane half)
+#ifndef T_RESCREEN
+#define T_RESCREEN 1  // 0: wide rows scored against every column of their halves (A/B)
+#endif
+constexpr unsigned T_RESCAN = 0x80000000u;            // wide-mask bit: the row is re-screened
+constexpr int T_RS_CAP = 16;
+#ifndef T_RS_CF
+#define T_RS_CF 8  // re-screen: frame-1 columns in flight per wave
+#endif
+constexpr int T_EPI_LIM = T_EPI_MASK + T_BM * 4;
+constexpr int T_EPI_SLOT = T_EPI_LIM + T_BM * 4;
+constexpr int T_EPI_CL = T_EPI_SLOT + D_NW * 128 * 4;
+static_assert(T_EPI_CL + D_NW * 64 * T_RS_CAP * 4 <= T_OFF_ROW, "the epilogue fits staging + ring");
 static_assert(D_OFF_AIMG + D_NW * 32 * KD <= T_OFF_ROW, "A images fit staging slot 2 + the ring");
 static_assert(T_LDS <= 160 * 1024, "one workgroup per CU");
 constexpr float T_B2MAX = 4.f;  // |b_j|^2 bound of the keys' range at tb <= 9
@@ -864,12 +877,155 @@ __device__ __forceinline__ Sweep sweep_t(char *lds, const float *B, int n1, int 
 #undef T_UNIT
     {  // unit 7 of the last tile
         const unsigned tl = __builtin_amdgcn_readfirstlane(32u * (unsigned)(ntc - 1) + 16u);
+        // the first pair by compiler-visible instructions: the MFMA-result hazard is padded before
+        // them (an asm block right after the chain's last MFMA would read stale registers)
+        fold_keys_cv(acc[1][0], acc[1][1], sv1[0], sv1[0], tl, tl + 1u, m1[3], m2[3]);
 #pragma unroll
-        for (int m_ = 0; m_ < KD / 32; m_++)
+        for (int m_ = 1; m_ < KD / 32; m_++)
             fold_keys(acc[1][2 * m_], acc[1][2 * m_ + 1], sv1[m_ >> 1], sv1[m_ >> 1], tl + 2u * m_, tl + 2u * m_ + 1u,
                       m1[3], m2[3]);
     }
     return st;
+}
+
+// Wide rows of k_q8t_match (a lane half holds two columns inside the window, so more may hide
+// below its runner-up) re-screened instead of scored against every column of the half: a row
+// lane holds only its half's top 2, and SuperPoint's own descriptors put ~4 % of the rows there
+// (15.8 per 394-keypoint pair; each cost n1 / 2 sequential 256-term dots: the epilogue's p90 was
+// 487 k cycles per wave against a 55 k sweep -- profiles/r05d_wide_rows.json).  The wave takes its
+// re-screened rows 32 at a time: their codes again as the A phase made them (same m, q, pack4:
+// the same integers) as the MFMA B operand, then per 32-column block of frame 1 the codes again
+// as the sweep made them (q_j = 127 * 2^e_j from the column's key shift in colsh) through the
+// wave's 8-KiB buffer, 8 MFMAs, and every column whose integer key D << (2 - e_j) reaches the
+// row's limit (the window's lo, in key units, rounded up: the same test as the candidates
+// above) is listed.  The listed columns -- a superset of those that can beat the maximiser --
+// are scored exactly (coop_exact_dots, one round per list position).  A (row, half) listing more
+// than T_RS_CAP columns falls back to the full re-score (lmask = both halves, T_RESCAN cleared).
+__device__ __forceinline__ void rescan_t(char *epi, const unsigned (&wide_rows)[T_RG], int tb, int w, int lane, int n1,
+                                         const float *__restrict__ A, const float *__restrict__ B,
+                                         int *__restrict__ oidx, float *__restrict__ oscore, double thresh,
+                                         const unsigned char *colsh) {
+    const int fr = lane & 31, fh = lane >> 5, sub = lane & 15, rq = lane >> 4;
+    unsigned *lmask = reinterpret_cast<unsigned *>(epi + T_EPI_MASK);
+    const int *limi = reinterpret_cast<const int *>(epi + T_EPI_LIM);
+    int *slots = reinterpret_cast<int *>(epi + T_EPI_SLOT) + w * 128;
+    int *mycl = reinterpret_cast<int *>(epi + T_EPI_CL) + (w * 64 + fh * 32 + fr) * T_RS_CAP;
+    char *buf = epi + w * 8192;
+    // the wave's rows lane (groups 0, 1) and lane + 64 (groups 2, 3)
+    const int rA = w * (32 * T_RG) + lane, rB = rA + 64;
+    const bool wA = (((fh ? wide_rows[1] : wide_rows[0]) >> fr) & 1u) && (lmask[rA] & T_RESCAN);
+    const bool wB = (((fh ? wide_rows[3] : wide_rows[2]) >> fr) & 1u) && (lmask[rB] & T_RESCAN);
+    const unsigned long long bA = __ballot(wA), bB = __ballot(wB);
+    const int na = __popcll(bA), nall = na + __popcll(bB);
+    if (nall == 0) return;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    if (wA) slots[__popcll(bA & below)] = rA;
+    if (wB) slots[na + __popcll(bB & below)] = rB;
+    const int nblk = (n1 + 31) / 32;
+    for (int b0 = 0; b0 < nall; b0 += 32) {
+        const int ns = min(32, nall - b0);
+        // the batch's rows as the A phase quantised them: 16 lanes per row, 4 rows per pass
+#pragma unroll 2
+        for (int qd = 0; qd < 8; qd++) {
+            const int sl = 4 * qd + rq;
+            const float *ar = A + (size_t)slots[b0 + min(sl, ns - 1)] * KD;
+            f32x4v x[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) x[u] = *reinterpret_cast<const f32x4v *>(ar + 4 * (sub + 16 * u));
+            float m = 0.f;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                m = absmax3(m, x[u][0], x[u][1]);
+                m = absmax3(m, x[u][2], x[u][3]);
+            }
+            m = fmaxf(m, swz_xor<1>(m));
+            m = fmaxf(m, swz_xor<2>(m));
+            m = fmaxf(m, swz_xor<4>(m));
+            m = fmaxf(m, swz_xor<8>(m));
+            const float q = m > 0.f ? 127.f * __builtin_amdgcn_rcpf(m) : 0.f;
+            char *rowp = buf + sl * KD + 4 * (sub & 3);
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                *reinterpret_cast<int *>(rowp + ((((sub >> 2) + 4 * u) ^ (sl & 15)) << 4)) =
+                    pack4(x[u][0], x[u][1], x[u][2], x[u][3], q);
+        }
+        i32x4 aF[KD / 32];
+#pragma unroll
+        for (int s2 = 0; s2 < KD / 32; s2++)
+            aF[s2] = *reinterpret_cast<const i32x4 *>(buf + fr * KD + (((2 * s2 + fh) ^ (fr & 15)) << 4));
+        const bool mine = fr < ns;
+        const int myrow = slots[b0 + min(fr, ns - 1)];
+        const int lim = limi[myrow];
+        int cnt = 0;
+        for (int blk = 0; blk < nblk; blk++) {
+            // frame-1 columns 32 blk + c as the sweep quantised them: one 1-KiB column per load
+            // instruction (lane l: floats 4 l .. +3), 8 columns in flight
+#pragma unroll
+            for (int c0 = 0; c0 < 32; c0 += T_RS_CF) {
+                f32x4v x[T_RS_CF];
+#pragma unroll
+                for (int i = 0; i < T_RS_CF; i++) {
+                    const int j = min(32 * blk + c0 + i, n1 - 1);
+                    x[i] = *reinterpret_cast<const f32x4v *>(B + (size_t)j * KD + 4 * lane);
+                }
+#pragma unroll
+                for (int i = 0; i < T_RS_CF; i++) {
+                    const int c = c0 + i, j = 32 * blk + c;
+                    const float qc = j < n1 ? __builtin_ldexpf(127.f, tb + 2 - (int)colsh[j]) : 0.f;
+                    *reinterpret_cast<int *>(buf + c * KD + (((lane >> 2) ^ (c & 15)) << 4) + 4 * (lane & 3)) =
+                        pack4(x[i][0], x[i][1], x[i][2], x[i][3], qc);
+                }
+            }
+            i32x4 bF[KD / 32];
+#pragma unroll
+            for (int s2 = 0; s2 < KD / 32; s2++)
+                bF[s2] = *reinterpret_cast<const i32x4 *>(buf + fr * KD + (((2 * s2 + fh) ^ (fr & 15)) << 4));
+            const i32x16 z = {};
+            i32x16 acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(bF[0], aF[0], z, 0, 0, 0);
+#pragma unroll
+            for (int s2 = 1; s2 < KD / 32; s2++) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(bF[s2], aF[s2], acc, 0, 0, 0);
+            if (mine) {
+#pragma unroll
+                for (int qq = 0; qq < 4; qq++) {
+                    const int jq = 32 * blk + 8 * qq + 4 * fh;  // a 4-column group: one key shift
+                    const int d = jq < n1 ? (int)colsh[jq] - tb : 0;
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        const int j = jq + e;
+                        if (j < n1 && acc[4 * qq + e] * (1 << d) >= lim) {
+                            if (cnt < T_RS_CAP) mycl[cnt] = j;
+                            cnt++;
+                        }
+                    }
+                }
+            }
+        }
+        const int ocnt = __shfl_xor(cnt, 32, 64);  // every lane: a cross-lane read of an inactive lane is 0
+        const bool ovf = mine && (cnt > T_RS_CAP || ocnt > T_RS_CAP);
+        if (ovf && fh == 0) lmask[myrow] = 3u;  // the full re-score below takes the row
+        const int myc = mine && !ovf ? cnt : 0;
+        float bs = -__builtin_inff();
+        int bj = 0x7fffffff;
+        for (int k = 0; __ballot(k < myc); k++) {
+            const int j = k < myc ? mycl[k] : -1;
+            const float e = coop_exact_dots(A, B, myrow, j, lane, buf);
+            if (j >= 0 && better(0, e, j, bs, bj)) {
+                bs = e;
+                bj = j;
+            }
+        }
+        const float ob = __shfl_xor(bs, 32, 64);
+        const int oj = __shfl_xor(bj, 32, 64);
+        if (better(0, ob, oj, bs, bj)) {
+            bs = ob;
+            bj = oj;
+        }
+        if (mine && !ovf && fh == 0) {
+            const bool keep = bj != 0x7fffffff && (double)bs > thresh && bs > 0.f;
+            oidx[myrow] = keep ? bj : -1;
+            if (oscore) oscore[myrow] = keep ? bs : 0.f;
+        }
+    }
 }
 
 // The transposed layout's decisions (the IK window of q8_common.hpp's epilogue, dmode 0): row
@@ -913,6 +1069,8 @@ __device__ __forceinline__ unsigned epilogue_t(char *epi, const float2 *rowv, co
         float bs = -__builtin_inff();
         int bj = 0x7fffffff, need = -1;
         bool wide = live && rv.y < 0.f;  // a row outside the int8 range: every column
+        bool rescan = false;             // wide, re-screened (rescan_t) against limit lim_k
+        int lim_k = 0;
         unsigned wm = 3u;
         if (live && !(rv.y < 0.f)) {
             const double s_a = (double)rv.y;
@@ -948,8 +1106,10 @@ __device__ __forceinline__ unsigned epilogue_t(char *epi, const float2 *rowv, co
                     const bool in1 = kv(e1) >= lim, in2 = kv(e2) >= lim;
                     const bool oin1 = __shfl_xor(in1 ? 1 : 0, 32, 64) != 0;
                     const bool oin2 = __shfl_xor(in2 ? 1 : 0, 32, 64) != 0;
-                    if (in2 || oin2) {  // a half holds two columns inside: re-score its columns
+                    if (in2 || oin2) {  // a half holds two columns inside: re-screen the row
                         wide = true;
+                        rescan = true;
+                        lim_k = (int)fmin(fmax(ceil(lim), -2147483647.0), 2147483647.0);
                         wm = (in1 ? 1u << fh : 0u) | (oin1 ? 1u << (1 - fh) : 0u);
                     } else if (in1) {
                         const int j = kcol(e1, fh);
@@ -975,7 +1135,10 @@ __device__ __forceinline__ unsigned epilogue_t(char *epi, const float2 *rowv, co
         bj_g[g] = bj;
         need_g[g] = need;
         out_g[g] = fh == 0 && live && !wide;
-        if (fh == 0 && wide) lmask[rl] = wm;
+        if (fh == 0 && wide) {
+            lmask[rl] = wm | (rescan ? T_RESCAN : 0u);
+            if (rescan) reinterpret_cast<int *>(epi + T_EPI_LIM)[rl] = lim_k;
+        }
         wide_rows[g] = (unsigned)__ballot(fh == 0 && wide);
     }
     unsigned nwide = 0, nneed = 0;  // (traced builds) the wave's wide rows and deferred dots
@@ -1010,12 +1173,17 @@ __device__ __forceinline__ unsigned epilogue_t(char *epi, const float2 *rowv, co
             oidx[rl] = keep ? bj_g[g] : -1;
             if (oscore) oscore[rl] = keep ? bs_g[g] : 0.f;
         }
-    // wide rows (rare): every column of the listed halves, one column per lane at a time
+#if T_RESCREEN
+    rescan_t(epi, wide_rows, tb, w, lane, n1, A, B, oidx, oscore, thresh, colsh);
+#endif
+    // wide rows not re-screened (rows outside the int8 range, a padding column on top, an
+    // overflowing list): every column of the listed halves, one column per lane at a time
 #pragma unroll
     for (int g = 0; g < T_RG; g++)
         for (unsigned dm = wide_rows[g]; dm; dm &= dm - 1) {
             const int r = w * (32 * T_RG) + g * 32 + __builtin_ctz(dm);
             const unsigned wm = lmask[r];
+            if (T_RESCREEN && (wm & T_RESCAN)) continue;
             const float *a = A + (size_t)r * KD;
             float ws = -__builtin_inff();
             int wj = 0x7fffffff;

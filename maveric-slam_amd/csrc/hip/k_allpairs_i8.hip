@@ -906,8 +906,10 @@ __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, co
     }
     {  // unit 7 of the last tile
         const unsigned tl = __builtin_amdgcn_readfirstlane(32u * (unsigned)(ntc - 1) + 16u);
+        // the first pair compiler-visible: the MFMA-result hazard padded before it
+        fold_keys_i8_cv(acc[1][0], acc[1][1], vsh, tl, tl + 1u, m1[3], m2[3]);
 #pragma unroll
-        for (int s_ = 0; s_ < KD / 32; s_++)
+        for (int s_ = 1; s_ < KD / 32; s_++)
             fold_keys_i8(acc[1][2 * s_], acc[1][2 * s_ + 1], vsh, tl + 2u * s_, tl + 2u * s_ + 1u, m1[3], m2[3]);
     }
 #undef IT_UNIT

@@ -49,7 +49,7 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int SP_NT = 256;          // 4 waves
-constexpr int TY = 16, TX = 32;     // conv output tile (before pooling)
+constexpr int TX = 32;  // the 1 x 1 heads' tile width (k_sp_conv: SpGeo)
 
 // Requantisation, bit-identical to clamp(rint((float) a * rs), lo, 127): the product rounded to
 // float, + 1.5 * 2^23 rounds it to an integer (round to nearest even) held in the low mantissa
@@ -157,11 +157,22 @@ __global__ __launch_bounds__(256) void k_sp_resize_q(const uint8_t *__restrict__
 #ifndef SP_OCC64
 #define SP_OCC64 3  // workgroups per CU for the 64-channel layers (LDS 50 KB; VGPRs <= 168)
 #endif
-template <int CIN, int KS, bool POOL, bool RELU, int OMODE, bool FUSE1A = false>
+// Tile geometry.  GEO 0: 16 x 32 output pixels, a wave's 4 MFMA pixel blocks are its 4 rows of
+// 32.  GEO 1 (the 24 x 80 layers: conv4a/b, convPa/Da at 192 x 640): 24 x 16 pixels, a wave's 3
+// blocks are 2 rows x 16 columns each (lane fr -> row fr >> 4, column fr & 15), so 24 x 80 is 5
+// whole tiles -- GEO 0 covers it with 2 x 3 tiles of which 37.5 % lie outside the frame.
+template <int GEO> struct SpGeo {
+    static constexpr int TY = GEO ? 24 : 16, TX = GEO ? 16 : 32;
+    static constexpr int JN = GEO ? 3 : 4, RB = GEO ? 2 : 1, WR = JN * RB;  // blocks, rows per block / wave
+};
+template <int CIN, int KS, bool POOL, bool RELU, int OMODE, bool FUSE1A = false, int GEO = 0>
 __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(const int8_t *__restrict__ in, int H, int W,
                                                       const i32x4 *__restrict__ wf, const int *__restrict__ bq,
                                                       float rs, int ngroups, int tiles_x, int tiles_y,
                                                       int8_t *__restrict__ out, int cstride, Conv1aArgs c1) {
+    using G = SpGeo<GEO>;
+    static_assert(GEO == 0 || (CIN != 64 && !POOL && OMODE == 0 && !FUSE1A), "GEO 1: the 128-channel unpooled layers");
+    constexpr int TY = G::TY, TX = G::TX, JN = G::JN, RB = G::RB, WR = G::WR;
     constexpr int P = KS / 2, IY = TY + 2 * P, IX = TX + 2 * P, NCH = CIN / 16, NS = KS * KS * CIN / 32;
     constexpr int PF = (CIN == 64 && SP_OCC64 > 2) ? 2 : 4;  // weight fragments in flight (k32 steps)
     static_assert(CIN % 32 == 0 && NCH <= 16, "channels in 32-k steps, at most 256");
@@ -368,15 +379,17 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
     // a wave whose 4 rows all lie below the frame (the 24-row layers' second tile row: a quarter
     // of their waves) has nothing to compute; the 128-channel epilogue has no block barrier
     if constexpr (CIN != 64) {
-        if (y0 + 4 * w >= H) return;
+        if (y0 + WR * w >= H) return;
     }
     // ---- K loop: 9 taps (or 1) x CIN / 32 steps, fully unrolled: every LDS offset a constant ----
-    i32x16 acc[4][2];
-    // per-lane bases: row 4w + j, column fr, chunk half fh (padded layout); XOR terms per kx
-    const i32x4 *lb = tile + ((4 * w) * IX + fr) * PS + (PADL ? fh : 0);
+    i32x16 acc[JN][2];
+    // per-lane bases: the lane's pixel (row WR w + [fr >> 4], column fr or fr & 15), chunk half fh
+    // (padded layout); XOR terms per kx
+    const int prow = WR * w + (GEO ? fr >> 4 : 0), pcol = GEO ? fr & 15 : fr;
+    const i32x4 *lb = tile + (prow * IX + pcol) * PS + (PADL ? fh : 0);
     int xs[KS];
 #pragma unroll
-    for (int kx = 0; kx < KS; kx++) xs[kx] = fh ^ (((fr + kx) / SWS) & (NCH - 1));
+    for (int kx = 0; kx < KS; kx++) xs[kx] = fh ^ (((pcol + kx) / SWS) & (NCH - 1));
 #pragma unroll
     for (int s = 0; s < NS; s++) {
         const i32x4 a0 = ra[s % PF], a1 = rb[s % PF];
@@ -386,8 +399,8 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
         }
         const int tap = s * 32 / CIN, ky = tap / KS, kx = tap % KS, c0 = (s * 32 % CIN) / 16;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int off = ((j + ky) * IX + kx) * PS;
+        for (int j = 0; j < JN; j++) {
+            const int off = ((RB * j + ky) * IX + kx) * PS;
             const i32x4 bv = PADL ? lb[off + c0] : lb[off + (c0 ^ xs[kx])];
             acc[j][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bv, s == 0 ? b0 : acc[j][0], 0, 0, 0);
             acc[j][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bv, s == 0 ? b1 : acc[j][1], 0, 0, 0);
@@ -513,8 +526,8 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
         }
     } else {
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int gy = y0 + 4 * w + j, gx = x0 + fr;
+        for (int j = 0; j < JN; j++) {
+            const int gy = y0 + prow + RB * j, gx = x0 + pcol;
             if (gy >= H || gx >= W) continue;  // both lanes of a pair (same fr) or neither
             int8_t *dst = OMODE == 0 ? out + (((size_t)b * H + gy) * W + gx) * cstride
                                      : out + ((size_t)b * H * W + (size_t)gx * H + gy) * cstride;
@@ -908,16 +921,17 @@ __global__ __launch_bounds__(SP_NT) void k_sp_min_gap(int8_t *__restrict__ semi,
     }
 }
 
-template <int CIN, int KS, bool POOL, bool RELU, int OMODE, bool FUSE1A = false>
+template <int CIN, int KS, bool POOL, bool RELU, int OMODE, bool FUSE1A = false, int GEO = 0>
 int launch_conv(hipStream_t st, const mv_superpoint *net, int li, int B, int H, int W, const int8_t *in,
                 int8_t *out, int cstride, Conv1aArgs c1 = Conv1aArgs{}) {
-    const int tiles_x = (W + TX - 1) / TX, tiles_y = (H + TY - 1) / TY, ngroups = net->cout_pad[li] / 64;
+    using G = SpGeo<GEO>;
+    const int tiles_x = (W + G::TX - 1) / G::TX, tiles_y = (H + G::TY - 1) / G::TY, ngroups = net->cout_pad[li] / 64;
     const long blocks = (long)B * ngroups * tiles_y * tiles_x;
     MV_REQUIRE(blocks < (1l << 31));
     // the epilogue stores 16 B per lane: NHWC outputs with 16-B aligned pixels
     MV_REQUIRE((OMODE != 0 && !POOL) || (cstride % 16 == 0 && cstride >= 64 * ngroups && ((uintptr_t)out & 15) == 0));
     const char *wd = static_cast<const char *>(net->wdev);
-    hipLaunchKernelGGL((k_sp_conv<CIN, KS, POOL, RELU, OMODE, FUSE1A>), dim3((unsigned)blocks), dim3(SP_NT), 0, st, in,
+    hipLaunchKernelGGL((k_sp_conv<CIN, KS, POOL, RELU, OMODE, FUSE1A, GEO>), dim3((unsigned)blocks), dim3(SP_NT), 0, st, in,
                        H, W, reinterpret_cast<const i32x4 *>(wd + net->frag_off[li]),
                        reinterpret_cast<const int *>(wd + net->bq_off[li]), net->rs[li], ngroups, tiles_x, tiles_y,
                        out, cstride, c1);
@@ -941,6 +955,20 @@ int launch_conv1x1(hipStream_t st, const mv_superpoint *net, int li, int B, int 
                        out, cstride, dq);
     MV_LAUNCH_CHECK();
     return MV_OK;
+}
+
+// the 128-channel unpooled layers: the tile geometry covering H x W with fewer padded pixels
+// (GEO 1 wins at 24 x 80: 1920 against 3072)
+#ifndef SP_GEO
+#define SP_GEO 1  // 0: always the 16 x 32 tiles (A/B)
+#endif
+template <int CIN, int KS, bool POOL, bool RELU, int OMODE>
+int launch_conv_geo(hipStream_t st, const mv_superpoint *net, int li, int B, int H, int W, const int8_t *in,
+                    int8_t *out, int cstride) {
+    auto area = [&](int ty, int tx) { return (long)((H + ty - 1) / ty) * ty * ((W + tx - 1) / tx) * tx; };
+    if (SP_GEO && area(SpGeo<1>::TY, SpGeo<1>::TX) < area(SpGeo<0>::TY, SpGeo<0>::TX))
+        return launch_conv<CIN, KS, POOL, RELU, OMODE, false, 1>(st, net, li, B, H, W, in, out, cstride);
+    return launch_conv<CIN, KS, POOL, RELU, OMODE, false, 0>(st, net, li, B, H, W, in, out, cstride);
 }
 
 constexpr int SP_CIN[12] = {1, 64, 64, 64, 64, 128, 128, 128, 128, 256, 128, 256};
@@ -1088,16 +1116,16 @@ int sp_network(hipStream_t st, mv_superpoint *net, int batch, int H, int W, int 
     if ((r = launch_conv<64, 3, false, true, 0>(st, net, 4, batch, h, w, Bf, A, 128)) != MV_OK) return r;
     if ((r = launch_conv<128, 3, true, true, 0>(st, net, 5, batch, h, w, A, Bf, 128)) != MV_OK) return r;
     h /= 2, w /= 2;
-    if ((r = launch_conv<128, 3, false, true, 0>(st, net, 6, batch, h, w, Bf, A, 128)) != MV_OK) return r;
-    if ((r = launch_conv<128, 3, false, true, 0>(st, net, 7, batch, h, w, A, Bf, 128)) != MV_OK) return r;
+    if ((r = launch_conv_geo<128, 3, false, true, 0>(st, net, 6, batch, h, w, Bf, A, 128)) != MV_OK) return r;
+    if ((r = launch_conv_geo<128, 3, false, true, 0>(st, net, 7, batch, h, w, A, Bf, 128)) != MV_OK) return r;
     // heads: Bf holds the shared encoder output
-    if ((r = launch_conv<128, 3, false, true, 0>(st, net, 8, batch, h, w, Bf, A, 256)) != MV_OK) return r;
+    if ((r = launch_conv_geo<128, 3, false, true, 0>(st, net, 8, batch, h, w, Bf, A, 256)) != MV_OK) return r;
     if (semi_f)
         r = launch_conv1x1<2>(st, net, 9, batch, h, w, A, reinterpret_cast<int8_t *>(semi_f), 65, net->dq_semi);
     else
         r = launch_conv1x1<1>(st, net, 9, batch, h, w, A, semi, 65);
     if (r != MV_OK) return r;
-    if ((r = launch_conv<128, 3, false, true, 0>(st, net, 10, batch, h, w, Bf, A, 256)) != MV_OK) return r;
+    if ((r = launch_conv_geo<128, 3, false, true, 0>(st, net, 10, batch, h, w, Bf, A, 256)) != MV_OK) return r;
     if (desc_f)
         r = launch_conv1x1<2>(st, net, 11, batch, h, w, A, reinterpret_cast<int8_t *>(desc_f), 256, net->dq_desc);
     else

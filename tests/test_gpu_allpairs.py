@@ -614,3 +614,40 @@ def test_allpairs_f32_handbacks_across_the_grid(ctx, orc, torch_cuda, scores):
         assert (idx[b, n:] == -1).all(), b
         if scores:
             assert (bits(sc[b, :n]) == bits(s2)).all(), b
+
+
+@pytest.mark.parametrize("scores", [True, False])
+def test_allpairs_f32_wide_rows_rescreened(ctx, screen, orc, torch_cuda, scores):
+    """Clustered frame-1 columns (near-duplicates within the int8 window, as SuperPoint's own
+    descriptors of repeated texture give): a query row then holds two or more in-window columns
+    in one lane half of k_q8t_match -- a wide row, re-screened on the matrix cores (rescan_t) and
+    its listed columns scored exactly; clusters of 40-80 members overflow the 16-column lists and
+    take the full re-score.  Mixed cluster sizes, thresholds around the cluster scores, ragged
+    pairs; indices (and exact scores) against the oracle."""
+    rng = np.random.default_rng(4242)
+    pairs = []
+    for k, (n0, nc, spread) in enumerate([(400, 120, 0.02), (1024, 200, 0.01), (300, 40, 0.05), (700, 90, 0.003)]):
+        cen = rng.standard_normal((nc, 256)).astype(np.float32)
+        cen /= np.linalg.norm(cen, axis=1, keepdims=True)
+        sizes = rng.integers(1, 12, nc)
+        sizes[:3] = [40, 64, 80]  # overflowing lists
+        cols = []
+        for c in range(nc):
+            m = cen[c] + spread * rng.standard_normal((sizes[c], 256)).astype(np.float32)
+            cols.append(m / np.linalg.norm(m, axis=1, keepdims=True))
+        b = np.concatenate(cols)[:1024]
+        b = b[rng.permutation(b.shape[0])].astype(np.float32)
+        q = cen[rng.integers(0, nc, n0)] + 0.15 * rng.standard_normal((n0, 256)).astype(np.float32) / 16
+        a = (q / np.linalg.norm(q, axis=1, keepdims=True)).astype(np.float32)
+        pairs.append((a, b))
+    for thr in (0.8, 0.97):
+        idx, sc = run_f32(ctx, torch_cuda, pairs, cap=1024, thresh=thr, scores=scores)
+        for k, (a, c) in enumerate(pairs):
+            i2, s2 = orc.allpairs_f32(a, c, thr)
+            n0 = a.shape[0]
+            assert (idx[k, :n0] == i2).all(), (k, thr)
+            assert (idx[k, n0:] == -1).all(), k
+            if scores:
+                assert (bits(sc[k, :n0]) == bits(s2)).all(), (k, thr)
+            if thr == 0.8:
+                assert (i2 >= 0).sum() > n0 // 2, k
