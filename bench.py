@@ -279,12 +279,14 @@ def noisy_pose_line(torch, dev, cx, stream, pose_p, d0, d1, kp0, kp1, nn_, idx, 
     mvtrack.profile_enable(False)
     k_ms, k_n = mvtrack.profile_query(kmatch)
     p_ms, p_n = mvtrack.profile_query("k_pose_ransac")
+    rs_ms, rs_n = mvtrack.profile_query("k_q8t_rescan")
     rot, tra = pose_angles(T.double().cpu().numpy(), synth.T_785_786)
     cx.set_stream(stream)
     return {"value": round(B * steps / el, 2), "unit": "pairs/s", "ms_per_step": round(el / steps * 1e3, 4),
             "keypoints": label, "match_kernel_avg_ms": k_ms / max(k_n, 1),
             "matches_per_pair": round(float(nm.sum().item()) / B, 1),
-            "stages_ms": {kmatch: round(k_ms / max(k_n, 1), 4), "k_pose_ransac": round(p_ms / max(p_n, 1), 4)},
+            "stages_ms": dict({kmatch: round(k_ms / max(k_n, 1), 4), "k_pose_ransac": round(p_ms / max(p_n, 1), 4)},
+                              **({"k_q8t_rescan": round(rs_ms / rs_n, 4)} if rs_n else {})),
             "pose_ok": int((st == 0).sum().item()), "inliers_per_pair": round(float(ni.sum().item()) / B, 1),
             "rot_err_deg": {"median": round(float(np.median(rot)), 4), "p99": round(float(np.percentile(rot, 99)), 4)},
             "tdir_err_deg": {"median": round(float(np.median(tra)), 4), "p99": round(float(np.percentile(tra, 99)), 4)}}
@@ -625,6 +627,7 @@ def main():
         kmatch, kfb = "k_q8t_match", "k_q8d_handback"
     k_ms, k_n = mvtrack.profile_query(kmatch)
     fb_ms, fb_n = mvtrack.profile_query(kfb) if kfb else (0.0, 0)
+    rs_ms, rs_n = mvtrack.profile_query("k_q8t_rescan") if kfb else (0.0, 0)
     s_ms, s_n = mvtrack.profile_query(ksplit) if ksplit else (0.0, 0)
     p_ms, p_n = mvtrack.profile_query("k_pose_ransac")
     with_scores = None
@@ -714,7 +717,8 @@ def main():
         "stages_ms_per_step": dict({kmatch: round(k_avg_s * 1e3, 4),
                                     "k_pose_ransac": round(p_ms / max(p_n, 1), 4)},
                                    **({ksplit: round(s_ms / max(s_n, 1), 4)} if ksplit else {}),
-                                   **({kfb + " (hand-backs only)": round(fb_ms / max(fb_n, 1), 4)} if kfb else {})),
+                                   **({kfb + " (hand-backs only)": round(fb_ms / max(fb_n, 1), 4)} if kfb else {}),
+                                   **({"k_q8t_rescan (wide rows only)": round(rs_ms / rs_n, 4)} if rs_n else {})),
         "with_scores": with_scores,
         "result_gather": gathered,
         "checked_pairs": checked, "pose_ok": int(sum(float(x[1]) for x in sums)),
@@ -817,7 +821,7 @@ def main():
         import bench_image_pose
 
         r = bench_image_pose.run(frames=257, steps=args.extra_steps, warmup=2, check=1)
-        out["image_to_pose"] = {k: r[k] for k in ("metric", "value", "unit", "frames_per_step", "ms_per_step",
+        out["image_to_pose"] = {k: r[k] for k in ("metric", "value", "unit", "frames_per_step", "pipelines", "ms_per_step",
                                                    "stages_ms_per_step", "keypoints_per_frame", "matches_per_pair",
                                                    "pose_ok", "checked_pairs")}
     if rank == 0:

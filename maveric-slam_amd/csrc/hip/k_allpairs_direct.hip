@@ -676,20 +676,18 @@ constexpr int T_OFF_MISC = T_OFF_ROW + T_BM * 8;    // [NW][4] per-wave statisti
 constexpr int T_OFF_COL = T_OFF_MISC + D_NW * 16;   // each frame-1 column's key shift (1 B)
 constexpr int T_LDS = T_OFF_COL + T_BM;
 constexpr int T_EPI_MASK = D_NW * 8192;             // epilogue: [NW] 8-KiB re-score buffers, [T_BM] wide masks
-// re-screened wide rows (rescan_t): [T_BM] int key limits, [NW][128] the wave's rows, [NW][32 x 2]
-// candidate lists of T_RS_CAP columns (one per row of a batch and lane half)
+static_assert(T_EPI_MASK + T_BM * 4 <= T_OFF_ROW, "the epilogue fits staging + ring");
 #ifndef T_RESCREEN
-#define T_RESCREEN 1  // 0: wide rows scored against every column of their halves (A/B)
+#define T_RESCREEN 1  // 0: wide rows scored against every column of their halves in k_q8t_match (A/B)
 #endif
-constexpr unsigned T_RESCAN = 0x80000000u;            // wide-mask bit: the row is re-screened
-constexpr int T_RS_CAP = 16;
-#ifndef T_RS_CF
-#define T_RS_CF 8  // re-screen: frame-1 columns in flight per wave
-#endif
-constexpr int T_EPI_LIM = T_EPI_MASK + T_BM * 4;
-constexpr int T_EPI_SLOT = T_EPI_LIM + T_BM * 4;
-constexpr int T_EPI_CL = T_EPI_SLOT + D_NW * 128 * 4;
-static_assert(T_EPI_CL + D_NW * 64 * T_RS_CAP * 4 <= T_OFF_ROW, "the epilogue fits staging + ring");
+constexpr unsigned T_RESCAN = 0x80000000u;  // wide-mask bit: the row is left to k_q8t_rescan
+// a row left to k_q8t_rescan: its match index holds INT_MIN + lim + 2^28 (< -1, never an index),
+// lim = the window's low end in key units, rounded up and clamped to +-2^28 (clamping only widens)
+constexpr int T_LIM_BIAS = 1 << 28;
+__device__ __forceinline__ int rs_encode(int lim) {
+    return (int)(0x80000000u + (unsigned)(min(max(lim, -T_LIM_BIAS), T_LIM_BIAS) + T_LIM_BIAS));
+}
+__device__ __forceinline__ int rs_decode(int v) { return (int)((unsigned)v - 0x80000000u) - T_LIM_BIAS; }
 static_assert(D_OFF_AIMG + D_NW * 32 * KD <= T_OFF_ROW, "A images fit staging slot 2 + the ring");
 static_assert(T_LDS <= 160 * 1024, "one workgroup per CU");
 constexpr float T_B2MAX = 4.f;  // |b_j|^2 bound of the keys' range at tb <= 9
@@ -888,146 +886,6 @@ __device__ __forceinline__ Sweep sweep_t(char *lds, const float *B, int n1, int 
     return st;
 }
 
-// Wide rows of k_q8t_match (a lane half holds two columns inside the window, so more may hide
-// below its runner-up) re-screened instead of scored against every column of the half: a row
-// lane holds only its half's top 2, and SuperPoint's own descriptors put ~4 % of the rows there
-// (15.8 per 394-keypoint pair; each cost n1 / 2 sequential 256-term dots: the epilogue's p90 was
-// 487 k cycles per wave against a 55 k sweep -- profiles/r05d_wide_rows.json).  The wave takes its
-// re-screened rows 32 at a time: their codes again as the A phase made them (same m, q, pack4:
-// the same integers) as the MFMA B operand, then per 32-column block of frame 1 the codes again
-// as the sweep made them (q_j = 127 * 2^e_j from the column's key shift in colsh) through the
-// wave's 8-KiB buffer, 8 MFMAs, and every column whose integer key D << (2 - e_j) reaches the
-// row's limit (the window's lo, in key units, rounded up: the same test as the candidates
-// above) is listed.  The listed columns -- a superset of those that can beat the maximiser --
-// are scored exactly (coop_exact_dots, one round per list position).  A (row, half) listing more
-// than T_RS_CAP columns falls back to the full re-score (lmask = both halves, T_RESCAN cleared).
-__device__ __forceinline__ void rescan_t(char *epi, const unsigned (&wide_rows)[T_RG], int tb, int w, int lane, int n1,
-                                         const float *__restrict__ A, const float *__restrict__ B,
-                                         int *__restrict__ oidx, float *__restrict__ oscore, double thresh,
-                                         const unsigned char *colsh) {
-    const int fr = lane & 31, fh = lane >> 5, sub = lane & 15, rq = lane >> 4;
-    unsigned *lmask = reinterpret_cast<unsigned *>(epi + T_EPI_MASK);
-    const int *limi = reinterpret_cast<const int *>(epi + T_EPI_LIM);
-    int *slots = reinterpret_cast<int *>(epi + T_EPI_SLOT) + w * 128;
-    int *mycl = reinterpret_cast<int *>(epi + T_EPI_CL) + (w * 64 + fh * 32 + fr) * T_RS_CAP;
-    char *buf = epi + w * 8192;
-    // the wave's rows lane (groups 0, 1) and lane + 64 (groups 2, 3)
-    const int rA = w * (32 * T_RG) + lane, rB = rA + 64;
-    const bool wA = (((fh ? wide_rows[1] : wide_rows[0]) >> fr) & 1u) && (lmask[rA] & T_RESCAN);
-    const bool wB = (((fh ? wide_rows[3] : wide_rows[2]) >> fr) & 1u) && (lmask[rB] & T_RESCAN);
-    const unsigned long long bA = __ballot(wA), bB = __ballot(wB);
-    const int na = __popcll(bA), nall = na + __popcll(bB);
-    if (nall == 0) return;
-    const unsigned long long below = (1ull << lane) - 1ull;
-    if (wA) slots[__popcll(bA & below)] = rA;
-    if (wB) slots[na + __popcll(bB & below)] = rB;
-    const int nblk = (n1 + 31) / 32;
-    for (int b0 = 0; b0 < nall; b0 += 32) {
-        const int ns = min(32, nall - b0);
-        // the batch's rows as the A phase quantised them: 16 lanes per row, 4 rows per pass
-#pragma unroll 2
-        for (int qd = 0; qd < 8; qd++) {
-            const int sl = 4 * qd + rq;
-            const float *ar = A + (size_t)slots[b0 + min(sl, ns - 1)] * KD;
-            f32x4v x[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) x[u] = *reinterpret_cast<const f32x4v *>(ar + 4 * (sub + 16 * u));
-            float m = 0.f;
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                m = absmax3(m, x[u][0], x[u][1]);
-                m = absmax3(m, x[u][2], x[u][3]);
-            }
-            m = fmaxf(m, swz_xor<1>(m));
-            m = fmaxf(m, swz_xor<2>(m));
-            m = fmaxf(m, swz_xor<4>(m));
-            m = fmaxf(m, swz_xor<8>(m));
-            const float q = m > 0.f ? 127.f * __builtin_amdgcn_rcpf(m) : 0.f;
-            char *rowp = buf + sl * KD + 4 * (sub & 3);
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-                *reinterpret_cast<int *>(rowp + ((((sub >> 2) + 4 * u) ^ (sl & 15)) << 4)) =
-                    pack4(x[u][0], x[u][1], x[u][2], x[u][3], q);
-        }
-        i32x4 aF[KD / 32];
-#pragma unroll
-        for (int s2 = 0; s2 < KD / 32; s2++)
-            aF[s2] = *reinterpret_cast<const i32x4 *>(buf + fr * KD + (((2 * s2 + fh) ^ (fr & 15)) << 4));
-        const bool mine = fr < ns;
-        const int myrow = slots[b0 + min(fr, ns - 1)];
-        const int lim = limi[myrow];
-        int cnt = 0;
-        for (int blk = 0; blk < nblk; blk++) {
-            // frame-1 columns 32 blk + c as the sweep quantised them: one 1-KiB column per load
-            // instruction (lane l: floats 4 l .. +3), 8 columns in flight
-#pragma unroll
-            for (int c0 = 0; c0 < 32; c0 += T_RS_CF) {
-                f32x4v x[T_RS_CF];
-#pragma unroll
-                for (int i = 0; i < T_RS_CF; i++) {
-                    const int j = min(32 * blk + c0 + i, n1 - 1);
-                    x[i] = *reinterpret_cast<const f32x4v *>(B + (size_t)j * KD + 4 * lane);
-                }
-#pragma unroll
-                for (int i = 0; i < T_RS_CF; i++) {
-                    const int c = c0 + i, j = 32 * blk + c;
-                    const float qc = j < n1 ? __builtin_ldexpf(127.f, tb + 2 - (int)colsh[j]) : 0.f;
-                    *reinterpret_cast<int *>(buf + c * KD + (((lane >> 2) ^ (c & 15)) << 4) + 4 * (lane & 3)) =
-                        pack4(x[i][0], x[i][1], x[i][2], x[i][3], qc);
-                }
-            }
-            i32x4 bF[KD / 32];
-#pragma unroll
-            for (int s2 = 0; s2 < KD / 32; s2++)
-                bF[s2] = *reinterpret_cast<const i32x4 *>(buf + fr * KD + (((2 * s2 + fh) ^ (fr & 15)) << 4));
-            const i32x16 z = {};
-            i32x16 acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(bF[0], aF[0], z, 0, 0, 0);
-#pragma unroll
-            for (int s2 = 1; s2 < KD / 32; s2++) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(bF[s2], aF[s2], acc, 0, 0, 0);
-            if (mine) {
-#pragma unroll
-                for (int qq = 0; qq < 4; qq++) {
-                    const int jq = 32 * blk + 8 * qq + 4 * fh;  // a 4-column group: one key shift
-                    const int d = jq < n1 ? (int)colsh[jq] - tb : 0;
-#pragma unroll
-                    for (int e = 0; e < 4; e++) {
-                        const int j = jq + e;
-                        if (j < n1 && acc[4 * qq + e] * (1 << d) >= lim) {
-                            if (cnt < T_RS_CAP) mycl[cnt] = j;
-                            cnt++;
-                        }
-                    }
-                }
-            }
-        }
-        const int ocnt = __shfl_xor(cnt, 32, 64);  // every lane: a cross-lane read of an inactive lane is 0
-        const bool ovf = mine && (cnt > T_RS_CAP || ocnt > T_RS_CAP);
-        if (ovf && fh == 0) lmask[myrow] = 3u;  // the full re-score below takes the row
-        const int myc = mine && !ovf ? cnt : 0;
-        float bs = -__builtin_inff();
-        int bj = 0x7fffffff;
-        for (int k = 0; __ballot(k < myc); k++) {
-            const int j = k < myc ? mycl[k] : -1;
-            const float e = coop_exact_dots(A, B, myrow, j, lane, buf);
-            if (j >= 0 && better(0, e, j, bs, bj)) {
-                bs = e;
-                bj = j;
-            }
-        }
-        const float ob = __shfl_xor(bs, 32, 64);
-        const int oj = __shfl_xor(bj, 32, 64);
-        if (better(0, ob, oj, bs, bj)) {
-            bs = ob;
-            bj = oj;
-        }
-        if (mine && !ovf && fh == 0) {
-            const bool keep = bj != 0x7fffffff && (double)bs > thresh && bs > 0.f;
-            oidx[myrow] = keep ? bj : -1;
-            if (oscore) oscore[myrow] = keep ? bs : 0.f;
-        }
-    }
-}
-
 // The transposed layout's decisions (the IK window of q8_common.hpp's epilogue, dmode 0): row
 // i = 32 g + fr of the wave sits in lanes fr (columns with (j >> 2) & 1 = 0) and fr + 32 (= 1), each
 // with its half's (m1, m2).  Runner-up outside the window: the maximiser, exactly scored only when
@@ -1038,7 +896,7 @@ __device__ __forceinline__ unsigned epilogue_t(char *epi, const float2 *rowv, co
                                            const float (&m2)[T_RG], double Bn, double Eb, int tb, int w, int lane,
                                            int n0, int n1, const float *__restrict__ A, const float *__restrict__ B,
                                            int *__restrict__ oidx, float *__restrict__ oscore, double thresh,
-                                           const unsigned char *colsh) {
+                                           const unsigned char *colsh, int *rs_flag, unsigned char *rs_colsh) {
     const int fr = lane & 31, fh = lane >> 5;
     const double u24 = 5.9604644775390625e-08;
     const double gam_e = KD * u24 / (1.0 - KD * u24);
@@ -1135,13 +993,12 @@ __device__ __forceinline__ unsigned epilogue_t(char *epi, const float2 *rowv, co
         bj_g[g] = bj;
         need_g[g] = need;
         out_g[g] = fh == 0 && live && !wide;
-        if (fh == 0 && wide) {
-            lmask[rl] = wm | (rescan ? T_RESCAN : 0u);
-            if (rescan) reinterpret_cast<int *>(epi + T_EPI_LIM)[rl] = lim_k;
-        }
+        if (fh == 0 && wide) lmask[rl] = T_RESCREEN && rescan ? T_RESCAN : wm;
+        if (T_RESCREEN && fh == 0 && rescan) oidx[rl] = rs_encode(lim_k);  // k_q8t_rescan's work
         wide_rows[g] = (unsigned)__ballot(fh == 0 && wide);
     }
     unsigned nwide = 0, nneed = 0;  // (traced builds) the wave's wide rows and deferred dots
+    bool rescan_any = false;
 #pragma unroll
     for (int g = 0; g < T_RG; g++) {
         nwide += __popc(wide_rows[g]);
@@ -1173,17 +1030,17 @@ __device__ __forceinline__ unsigned epilogue_t(char *epi, const float2 *rowv, co
             oidx[rl] = keep ? bj_g[g] : -1;
             if (oscore) oscore[rl] = keep ? bs_g[g] : 0.f;
         }
-#if T_RESCREEN
-    rescan_t(epi, wide_rows, tb, w, lane, n1, A, B, oidx, oscore, thresh, colsh);
-#endif
-    // wide rows not re-screened (rows outside the int8 range, a padding column on top, an
-    // overflowing list): every column of the listed halves, one column per lane at a time
+    // wide rows left here (rows outside the int8 range, a padding column on top; with
+    // T_RESCREEN 0 every wide row): every column of the listed halves, one column per lane
 #pragma unroll
     for (int g = 0; g < T_RG; g++)
         for (unsigned dm = wide_rows[g]; dm; dm &= dm - 1) {
             const int r = w * (32 * T_RG) + g * 32 + __builtin_ctz(dm);
             const unsigned wm = lmask[r];
-            if (T_RESCREEN && (wm & T_RESCAN)) continue;
+            if (wm & T_RESCAN) {  // k_q8t_rescan's: the pair's column shifts and tag width for it
+                rescan_any = true;
+                continue;
+            }
             const float *a = A + (size_t)r * KD;
             float ws = -__builtin_inff();
             int wj = 0x7fffffff;
@@ -1212,6 +1069,11 @@ __device__ __forceinline__ unsigned epilogue_t(char *epi, const float2 *rowv, co
                 if (oscore) oscore[r] = keep ? ws : 0.f;
             }
         }
+    if (rescan_any) {  // wave-uniform; every such wave writes the same bytes
+        const i32x4 v = *reinterpret_cast<const i32x4 *>(colsh + 16 * lane);
+        *reinterpret_cast<i32x4 *>(rs_colsh + 16 * lane) = v;
+        if (lane == 0) *rs_flag = tb + 1;
+    }
     return nwide << 16 | nneed;
 }
 
@@ -1219,7 +1081,8 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8t_match(int cap, const int *__res
                                                        const int *__restrict__ n1v, const float *__restrict__ desc0,
                                                        const float *__restrict__ desc1, double thresh,
                                                        int *__restrict__ match_idx, float *__restrict__ match_score,
-                                                       int *__restrict__ fallback) {
+                                                       int *__restrict__ fallback, int *__restrict__ rs_flags,
+                                                       unsigned char *__restrict__ rs_colsh) {
     __shared__ __attribute__((aligned(16))) char lds[T_LDS];
 #ifdef MV_TRACE
     unsigned long long ts_[10] = {};
@@ -1263,7 +1126,8 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8t_match(int cap, const int *__res
     const double Bn = sqrt((double)st.b2max) * 1.0001;
     const double Eb = 8.0001 * (double)st.smax + 1e-30;
     const unsigned ecnt = epilogue_t(lds, rowv, m1, m2, Bn, Eb, tb, w, lane, n0, n1, A, B, oidx, oscore, thresh,
-                                     reinterpret_cast<const unsigned char *>(lds + T_OFF_COL));
+                                     reinterpret_cast<const unsigned char *>(lds + T_OFF_COL), rs_flags + pair,
+                                     rs_colsh + (size_t)pair * T_BM);
     (void)ecnt;
 #ifdef MV_TRACE
     D_STAMP(3);
@@ -1277,6 +1141,177 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8t_match(int cap, const int *__res
         o[9] = ts_[9];
     }
 #endif
+}
+
+// ---------------------------------------------------------------------------
+// k_q8t_rescan: the wide rows k_q8t_match leaves (a lane half holding two columns inside the
+// window: more may hide below its runner-up, and a row's two lanes keep only their halves' top 2).
+// Scoring every column of such a half exactly -- n1 / 2 sequential 256-term dots per row -- was
+// what SuperPoint's own descriptors made expensive: 15.8 wide rows per 394-keypoint pair (4 %),
+// the epilogue's p90 at 487 k cycles per wave against a 55 k sweep (profiles/r05d_wide_rows.json).
+// Instead each row is re-screened: one wave per workgroup takes a flagged pair's pending rows 32 at
+// a time, rebuilds their codes exactly as the A phase made them (same m, q, pack4: the same
+// integers) as the MFMA B operand, and per 32-column block of frame 1 rebuilds the codes as the
+// sweep made them (q_j = 127 * 2^e_j from the column's key shift, which k_q8t_match exported with
+// the tag width) through an 8-KiB LDS buffer; 8 MFMAs give the block's exact screen D_ij, and
+// every column whose key D << (2 - e_j) reaches the row's limit (the window's low end: the same
+// test k_q8t_match applies to its candidates) is listed -- a superset of the columns that can beat
+// the maximiser.  Listed columns are scored exactly (coop_exact_dots) whenever some lane's list
+// could overflow in the next block, and at the end.  A separate kernel so that k_q8t_match keeps
+// its registers (the in-kernel form pushed it from 240 VGPRs to 256 + 4 spilled: 0.6-3 % on the
+// headline, profiles/r05e_rescreen_ab.log).
+// ---------------------------------------------------------------------------
+constexpr int RS_CAP = 32;  // listed columns per (row, lane half) between exact-score rounds
+constexpr int RS_CF = 8;    // frame-1 columns in flight per lane
+
+__global__ __launch_bounds__(64) void k_q8t_rescan(int batch, int cap, const int *__restrict__ n1v,
+                                                   const float *__restrict__ desc0, const float *__restrict__ desc1,
+                                                   double thresh, int *__restrict__ match_idx,
+                                                   float *__restrict__ match_score, const int *__restrict__ rs_flags,
+                                                   const unsigned char *__restrict__ rs_colsh) {
+    __shared__ __attribute__((aligned(16))) char buf[32 * KD];  // row image / column stage / dot staging
+    __shared__ int cl[64 * RS_CAP];                              // [row fr][half fh] listed columns
+    __shared__ int slots[32], lims[32];
+    __shared__ __attribute__((aligned(16))) unsigned char colsh[T_BM];
+    const int lane = threadIdx.x, fr = lane & 31, fh = lane >> 5, sub = lane & 15, rq = lane >> 4;
+    int *mycl = cl + (fh * 32 + fr) * RS_CAP;
+    for (int pair = blockIdx.x; pair < batch; pair += gridDim.x) {
+        const int fl = __builtin_amdgcn_readfirstlane(rs_flags[pair]);
+        if (!fl) continue;
+        const int tb = fl - 1;
+        const int n1 = min(max(n1v[pair], 0), cap);
+        const float *A = desc0 + (size_t)pair * cap * KD;
+        const float *B = desc1 + (size_t)pair * cap * KD;
+        int *oidx = match_idx + (size_t)pair * cap;
+        float *oscore = match_score ? match_score + (size_t)pair * cap : nullptr;
+        *reinterpret_cast<i32x4 *>(colsh + 16 * lane) =
+            *reinterpret_cast<const i32x4 *>(rs_colsh + (size_t)pair * T_BM + 16 * lane);
+        const int nblk = (n1 + 31) / 32;
+        // one batch of ns pending rows (slots / lims)
+        auto run_batch = [&](int ns) {
+            // the rows' codes as the A phase made them: 16 lanes per row, 4 rows per pass
+#pragma unroll 2
+            for (int qd = 0; qd < 8; qd++) {
+                const int sl = 4 * qd + rq;
+                const float *ar = A + (size_t)slots[min(sl, ns - 1)] * KD;
+                f32x4v x[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) x[u] = *reinterpret_cast<const f32x4v *>(ar + 4 * (sub + 16 * u));
+                float m = 0.f;
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    m = absmax3(m, x[u][0], x[u][1]);
+                    m = absmax3(m, x[u][2], x[u][3]);
+                }
+                m = fmaxf(m, swz_xor<1>(m));
+                m = fmaxf(m, swz_xor<2>(m));
+                m = fmaxf(m, swz_xor<4>(m));
+                m = fmaxf(m, swz_xor<8>(m));
+                const float q = m > 0.f ? 127.f * __builtin_amdgcn_rcpf(m) : 0.f;
+                char *rowp = buf + sl * KD + 4 * (sub & 3);
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    *reinterpret_cast<int *>(rowp + ((((sub >> 2) + 4 * u) ^ (sl & 15)) << 4)) =
+                        pack4(x[u][0], x[u][1], x[u][2], x[u][3], q);
+            }
+            i32x4 aF[KD / 32];
+#pragma unroll
+            for (int s2 = 0; s2 < KD / 32; s2++)
+                aF[s2] = *reinterpret_cast<const i32x4 *>(buf + fr * KD + (((2 * s2 + fh) ^ (fr & 15)) << 4));
+            const bool mine = fr < ns;
+            const int myrow = slots[min(fr, ns - 1)];
+            const int lim = lims[min(fr, ns - 1)];
+            int cnt = 0;
+            float bs = -__builtin_inff();
+            int bj = 0x7fffffff;
+            auto flush = [&]() {  // exact scores of the listed columns, one list position per round
+                for (int k = 0; __ballot(k < cnt); k++) {
+                    const int j = k < cnt ? mycl[k] : -1;
+                    const float e = coop_exact_dots(A, B, myrow, j, lane, buf);
+                    if (j >= 0 && better(0, e, j, bs, bj)) {
+                        bs = e;
+                        bj = j;
+                    }
+                }
+                cnt = 0;
+            };
+            for (int blk = 0; blk < nblk; blk++) {
+                // columns 32 blk + c as the sweep quantised them: one 1-KiB column per load
+                // instruction (lane l: floats 4 l .. +3)
+#pragma unroll
+                for (int c0 = 0; c0 < 32; c0 += RS_CF) {
+                    f32x4v x[RS_CF];
+#pragma unroll
+                    for (int i = 0; i < RS_CF; i++) {
+                        const int j = min(32 * blk + c0 + i, n1 - 1);
+                        x[i] = *reinterpret_cast<const f32x4v *>(B + (size_t)j * KD + 4 * lane);
+                    }
+#pragma unroll
+                    for (int i = 0; i < RS_CF; i++) {
+                        const int c = c0 + i, j = 32 * blk + c;
+                        const float qc = j < n1 ? __builtin_ldexpf(127.f, tb + 2 - (int)colsh[j]) : 0.f;
+                        *reinterpret_cast<int *>(buf + c * KD + (((lane >> 2) ^ (c & 15)) << 4) + 4 * (lane & 3)) =
+                            pack4(x[i][0], x[i][1], x[i][2], x[i][3], qc);
+                    }
+                }
+                i32x4 bF[KD / 32];
+#pragma unroll
+                for (int s2 = 0; s2 < KD / 32; s2++)
+                    bF[s2] = *reinterpret_cast<const i32x4 *>(buf + fr * KD + (((2 * s2 + fh) ^ (fr & 15)) << 4));
+                const i32x16 z = {};
+                i32x16 acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(bF[0], aF[0], z, 0, 0, 0);
+#pragma unroll
+                for (int s2 = 1; s2 < KD / 32; s2++)
+                    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(bF[s2], aF[s2], acc, 0, 0, 0);
+                if (mine) {
+#pragma unroll
+                    for (int qq = 0; qq < 4; qq++) {
+                        const int jq = 32 * blk + 8 * qq + 4 * fh;  // a 4-column group: one key shift
+                        const int d = jq < n1 ? (int)colsh[jq] - tb : 0;
+#pragma unroll
+                        for (int e = 0; e < 4; e++) {
+                            const int j = jq + e;
+                            if (j < n1 && acc[4 * qq + e] * (1 << d) >= lim) mycl[cnt++] = j;
+                        }
+                    }
+                }
+                if (__ballot(cnt > RS_CAP - 16)) flush();  // the next block adds at most 16
+            }
+            flush();
+            const float ob = __shfl_xor(bs, 32, 64);
+            const int oj = __shfl_xor(bj, 32, 64);
+            if (better(0, ob, oj, bs, bj)) {
+                bs = ob;
+                bj = oj;
+            }
+            if (mine && fh == 0) {
+                const bool keep = bj != 0x7fffffff && (double)bs > thresh && bs > 0.f;
+                oidx[myrow] = keep ? bj : -1;
+                if (oscore) oscore[myrow] = keep ? bs : 0.f;
+            }
+        };
+        // the pending rows (index < -1), gathered 32 at a time in row order
+        int ns = 0;
+        for (int r0 = 0; r0 < cap; r0 += 64) {
+            const int r = r0 + lane;
+            const int v = r < cap ? oidx[r] : -1;
+            bool pend = v < -1;
+            for (unsigned long long mask = __ballot(pend); mask; mask = __ballot(pend)) {
+                const int rank = __popcll(mask & ((1ull << lane) - 1ull)), room = 32 - ns;
+                if (pend && rank < room) {
+                    slots[ns + rank] = r;
+                    lims[ns + rank] = rs_decode(v);
+                    pend = false;
+                }
+                ns += min(__popcll(mask), room);
+                if (ns == 32) {
+                    run_batch(32);
+                    ns = 0;
+                }
+            }
+        }
+        if (ns) run_batch(ns);
+    }
 }
 
 }  // namespace
@@ -1331,20 +1366,34 @@ bool allpairs_q8t_applies(int cap, int dmode) {
     }();
     return !off && dmode == 0 && cap > 0 && cap <= T_BM;
 }
-size_t allpairs_q8t_scratch_bytes(int batch) { return align_up((size_t)batch * 4, 256); }
+// scratch: [batch] hand-back flags | [batch] re-screen flags (tag width + 1) | [batch][T_BM] the
+// pairs' column key shifts (written only for pairs with re-screened rows)
+size_t allpairs_q8t_scratch_bytes(int batch) {
+    return 2 * align_up((size_t)batch * 4, 256) + (size_t)batch * T_BM;
+}
 
 int launch_allpairs_q8t_match(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
                               const float *desc0, const float *desc1, double thresh, int *match_idx,
                               float *match_score) {
     MV_REQUIRE(batch > 0 && cap > 0 && cap <= T_BM && n0 && n1 && desc0 && desc1 && match_idx && scratch);
     MV_REQUIRE(((uintptr_t)desc0 & 15) == 0 && ((uintptr_t)desc1 & 15) == 0);
+    const size_t fb = align_up((size_t)batch * 4, 256);
     int *flags = static_cast<int *>(scratch);
-    MV_HIP_TRY(hipMemsetAsync(flags, 0, (size_t)batch * 4, s));
+    int *rflags = reinterpret_cast<int *>(static_cast<char *>(scratch) + fb);
+    unsigned char *rcolsh = static_cast<unsigned char *>(scratch) + 2 * fb;
+    MV_HIP_TRY(hipMemsetAsync(flags, 0, 2 * fb, s));
     MV_PROF_BEGIN(s, "k_q8t_match");
     hipLaunchKernelGGL(k_q8t_match, dim3((unsigned)batch), dim3(D_NT), 0, s, cap, n0, n1, desc0, desc1, thresh,
-                       match_idx, match_score, flags);
+                       match_idx, match_score, flags, rflags, rcolsh);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
+    if (T_RESCREEN) {  // the wide rows it left: one wave per workgroup, a grid-stride loop over pairs
+        MV_PROF_BEGIN(s, "k_q8t_rescan");
+        hipLaunchKernelGGL(k_q8t_rescan, dim3((unsigned)min(batch, 2048)), dim3(64), 0, s, batch, cap, n1, desc0,
+                           desc1, thresh, match_idx, match_score, rflags, rcolsh);
+        MV_PROF_END(s);
+        MV_LAUNCH_CHECK();
+    }
     return launch_allpairs_q8d_match(s, batch, cap, n0, n1, desc0, desc1, thresh, match_idx, match_score, 0, flags);
 }
 

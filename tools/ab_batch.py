@@ -40,7 +40,7 @@ for B in [int(x) for x in os.environ.get("BS", "128,256,512,1024,2048,4096").spl
         torch.cuda.synchronize()
         mvtrack.profile_enable(False)
         st = {}
-        for k in ("k_q8t_match", "k_q8d_handback", "k_q8d_match"):
+        for k in ("k_q8t_match", "k_q8t_rescan", "k_q8d_handback", "k_q8d_match"):
             ms, c = mvtrack.profile_query(k)
             if c:
                 st[k] = round(ms / steps, 4)

@@ -58,7 +58,7 @@ for _ in range(steps):
 torch.cuda.synchronize()
 mvtrack.profile_enable(False)
 st = {}
-for k in ("k_q8t_match", "k_q8d_handback", "k_q8d_match"):
+for k in ("k_q8t_match", "k_q8t_rescan", "k_q8d_handback", "k_q8d_match"):
     ms, c = mvtrack.profile_query(k)
     if c:
         st[k] = round(ms / steps, 4)

@@ -35,60 +35,69 @@ def frames_kitti(F, seed=0):
     return out
 
 
-def run(frames=257, steps=10, warmup=2, check=1):
+def run(frames=257, steps=10, warmup=2, check=1, pipelines=2):
+    """pipelines: independent (context, SuperPoint net, buffers, HIP stream) sets taking the steps
+    in turn, so that one track's latency-bound stages (keypoint NMS: one block per frame; the
+    match and pose launches of 256 pairs) overlap the next track's network on the other stream,
+    as the headline's pipelined contexts do.  Stage times are measured on one pipeline alone."""
     dev = torch.device("cuda", 0)
     W = dict(np.load(os.path.join(ROOT, "tests", "golden", "superpoint_qnonorm.npz")))
     imgs = frames_kitti(frames)
     x = torch.from_numpy(np.stack(imgs)).to(dev)
     F, P = frames, frames - 1
-    ctx = mvtrack.Context(0)
-    ctx.set_stream(torch.cuda.current_stream())
-    sp = mvtrack.SuperPoint(ctx, W)
-    semi = torch.empty((F, 65, 24, 80), dtype=torch.float32, device=dev)
-    cdesc = torch.empty((F, 256, 24, 80), dtype=torch.float32, device=dev)
-    nkp = torch.empty(F, dtype=torch.int32, device=dev)
-    kp = torch.zeros((F, CAP, 2), dtype=torch.float32, device=dev)
-    conf = torch.zeros((F, CAP), dtype=torch.float32, device=dev)
-    desc = torch.zeros((F, CAP, 256), dtype=torch.float32, device=dev)
-    kst = torch.empty(F, dtype=torch.int32, device=dev)
-    idx = torch.empty((P, CAP), dtype=torch.int32, device=dev)
     K = synth.KITTI_K  # pairwise_pnp.py:667-669
     prm = mvtrack.pose_params(mvtrack.AS_INTENDED, fx=K[0, 0], fy=K[1, 1], cx=K[0, 2], cy=K[1, 2], hypotheses=256,
                               inlier_thresh=1.0, refine_iters=10, seed=7)
-    T = torch.empty((P, 3, 4), dtype=torch.float32, device=dev)
-    nm = torch.empty(P, dtype=torch.int32, device=dev)
-    ni = torch.empty(P, dtype=torch.int32, device=dev)
-    st = torch.empty(P, dtype=torch.int32, device=dev)
 
-    def step():
-        sp.forward_raw(x, 192, 640, out=(semi, cdesc))
-        ctx.keypoints(semi, cdesc, 192, 640, nkp, kp, conf, desc, kst)
-        ctx.match_allpairs_f32(desc[:P], desc[1:], nkp[:P], nkp[1:], idx, None, 0.8)
-        ctx.pose_from_matches(prm, nkp[:P], idx, kp[:P], kp[1:], T, nm, ni, st)
+    class Pipe:
+        def __init__(self):
+            self.stream = torch.cuda.Stream(device=dev)
+            self.ctx = mvtrack.Context(0)
+            self.ctx.set_stream(self.stream)
+            self.sp = mvtrack.SuperPoint(self.ctx, W)
+            e = lambda *shape, dt=torch.float32: torch.zeros(shape, dtype=dt, device=dev)  # noqa: E731
+            self.semi, self.cdesc = e(F, 65, 24, 80), e(F, 256, 24, 80)
+            self.nkp, self.kp, self.conf = e(F, dt=torch.int32), e(F, CAP, 2), e(F, CAP)
+            self.desc, self.kst = e(F, CAP, 256), e(F, dt=torch.int32)
+            self.idx = e(P, CAP, dt=torch.int32)
+            self.T, self.nm, self.ni, self.st = e(P, 3, 4), e(P, dt=torch.int32), e(P, dt=torch.int32), e(P, dt=torch.int32)
 
-    for _ in range(warmup):
-        step()
+        def step(self):
+            with torch.cuda.stream(self.stream):
+                self.sp.forward_raw(x, 192, 640, out=(self.semi, self.cdesc))
+                self.ctx.keypoints(self.semi, self.cdesc, 192, 640, self.nkp, self.kp, self.conf, self.desc, self.kst)
+                self.ctx.match_allpairs_f32(self.desc[:P], self.desc[1:], self.nkp[:P], self.nkp[1:], self.idx, None,
+                                            0.8)
+                self.ctx.pose_from_matches(prm, self.nkp[:P], self.idx, self.kp[:P], self.kp[1:], self.T, self.nm,
+                                           self.ni, self.st)
+
+    torch.cuda.synchronize()  # the inputs uploaded on the default stream
+    pipes = [Pipe() for _ in range(max(1, pipelines))]
+    for k in range(warmup * len(pipes)):
+        pipes[k % len(pipes)].step()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
+    for k in range(steps):
+        pipes[k % len(pipes)].step()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    p0 = pipes[0]
     mvtrack.profile_enable(True)
     for _ in range(steps):
-        step()
-    torch.cuda.synchronize()
+        p0.step()
+        torch.cuda.synchronize()
     mvtrack.profile_enable(False)
     stages = {}
     for k in ("k_sp_conv", "k_kp_heat", "k_kp_nms", "k_kp_sample_planes", "k_kp_normalize",
-              "k_q8t_match", "k_q8d_handback", "k_q8d_match", "k_pose_ransac"):
+              "k_q8t_match", "k_q8t_rescan", "k_q8d_handback", "k_q8d_match", "k_pose_ransac"):
         ms, c = mvtrack.profile_query(k)
         if c:
             stages[k] = round(ms / steps, 4)
+    nkp, idx, nm, st, kp = p0.nkp, p0.idx, p0.nm, p0.st, p0.kp
     res = {"metric": "image -> pose frame-pairs/sec (quantized SuperPoint + keypoints + fp32 all-pairs + pose), "
                      "KITTI 376x1241 frames, consecutive pairs",
            "value": round(P * steps / el, 1), "unit": "pairs/s", "frames_per_step": F, "steps": steps,
-           "ms_per_step": round(el / steps * 1e3, 4), "stages_ms_per_step": stages,
+           "pipelines": len(pipes), "ms_per_step": round(el / steps * 1e3, 4), "stages_ms_per_step": stages,
            "keypoints_per_frame": round(float(nkp.float().mean()), 1),
            "matches_per_pair": round(float(nm.float().mean()), 1), "pose_ok": int((st == 0).sum())}
     if check:
@@ -106,8 +115,11 @@ def run(frames=257, steps=10, warmup=2, check=1):
         i2, _ = oracle.allpairs_f32(chain[0], chain[1], 0.8)
         assert (idx[0, :i2.shape[0]].cpu().numpy() == i2).all(), "match differs from the oracle chain"
         res["checked_pairs"] = 1
-    sp.close()
-    ctx.close()
+        for pp in pipes[1:]:  # the same track on every pipeline: identical matches and poses
+            assert torch.equal(pp.idx, p0.idx) and torch.equal(pp.T, p0.T), "pipelines differ"
+    for pp in pipes:
+        pp.sp.close()
+        pp.ctx.close()
     return res
 
 
@@ -117,8 +129,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--check", type=int, default=1)
+    ap.add_argument("--pipelines", type=int, default=2)
     a = ap.parse_args()
-    print(json.dumps(run(a.frames, a.steps, a.warmup, a.check)))
+    print(json.dumps(run(a.frames, a.steps, a.warmup, a.check, a.pipelines)))
 
 
 if __name__ == "__main__":

@@ -114,7 +114,7 @@ def run(frames=8193, kp=1024, steps=20, warmup=3, check=1, pipeline=3, fused=Tru
         step()
     torch.cuda.synchronize()
     mvtrack.profile_enable(False)
-    st = {k: mvtrack.profile_query(k) for k in ("k_q8_split", "k_q8_match_seq", "k_q8t_match", "k_q8d_handback",
+    st = {k: mvtrack.profile_query(k) for k in ("k_q8_split", "k_q8_match_seq", "k_q8t_match", "k_q8t_rescan", "k_q8d_handback",
                                                  "k_pose_ransac")}
     stages = {k: round(ms / max(c, 1), 4) for k, (ms, c) in st.items() if c > 0}
     o = outs[0]

@@ -9,11 +9,13 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method threa
   tests/test_gpu_superpoint.py tests/test_gpu_image_to_pose.py > gpurun_out/${TAG}_geo_pytest.log 2>&1
 rc=$?; tail -2 gpurun_out/${TAG}_geo_pytest.log; [ $rc -eq 0 ] || exit $rc
 for rep in 1 2; do
-  for v in default spgeo0; do
+  for v in default spgeo0 ${EXTRA_VARIANTS:-}; do
     if [ $v = default ]; then L=""; else L="build_variants/libmaveric_$v.so"; fi
     MV_LIB=$L timeout -k 10 200 python tools/bench_superpoint.py --batch 64 --steps 10 --check 0 > gpurun_out/${TAG}_geo_sp_${v}_$rep.log 2>&1 || exit $?
     echo "$v rep $rep superpoint: $(tail -1 gpurun_out/${TAG}_geo_sp_${v}_$rep.log | cut -c1-300)"
   done
 done
-timeout -k 10 200 python tools/bench_image_pose.py > gpurun_out/${TAG}_geo_image_pose.json 2>gpurun_out/${TAG}_geo_image_pose.err || exit $?
-cat gpurun_out/${TAG}_geo_image_pose.json
+for pl in 1 2 3; do
+  timeout -k 10 200 python tools/bench_image_pose.py --pipelines $pl > gpurun_out/${TAG}_geo_image_pose_p$pl.json 2>gpurun_out/${TAG}_geo_image_pose.err || exit $?
+  cat gpurun_out/${TAG}_geo_image_pose_p$pl.json
+done
