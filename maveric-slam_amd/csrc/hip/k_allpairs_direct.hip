@@ -1149,8 +1149,8 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8t_match(int cap, const int *__res
 // Scoring every column of such a half exactly -- n1 / 2 sequential 256-term dots per row -- was
 // what SuperPoint's own descriptors made expensive: 15.8 wide rows per 394-keypoint pair (4 %),
 // the epilogue's p90 at 487 k cycles per wave against a 55 k sweep (profiles/r05d_wide_rows.json).
-// Instead each row is re-screened: one wave per workgroup takes a flagged pair's pending rows 32 at
-// a time, rebuilds their codes exactly as the A phase made them (same m, q, pack4: the same
+// Instead each row is re-screened: a workgroup of 4 waves takes a flagged pair's pending rows 32 at
+// a time (each wave every 4th 32-column block of frame 1; their bests merged in LDS), rebuilds their codes exactly as the A phase made them (same m, q, pack4: the same
 // integers) as the MFMA B operand, and per 32-column block of frame 1 rebuilds the codes as the
 // sweep made them (q_j = 127 * 2^e_j from the column's key shift, which k_q8t_match exported with
 // the tag width) through an 8-KiB LDS buffer; 8 MFMAs give the block's exact screen D_ij, and
@@ -1159,35 +1159,45 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8t_match(int cap, const int *__res
 // the maximiser.  Listed columns are scored exactly (coop_exact_dots) whenever some lane's list
 // could overflow in the next block, and at the end.  A separate kernel so that k_q8t_match keeps
 // its registers (the in-kernel form pushed it from 240 VGPRs to 256 + 4 spilled: 0.6-3 % on the
-// headline, profiles/r05e_rescreen_ab.log).
+// headline, profiles/r05e_rescreen_inkernel_ab.json).
 // ---------------------------------------------------------------------------
 constexpr int RS_CAP = 32;  // listed columns per (row, lane half) between exact-score rounds
 constexpr int RS_CF = 8;    // frame-1 columns in flight per lane
+constexpr int RS_NW = 4;    // waves per workgroup: column blocks w, w + 4, ... of the same rows
 
-__global__ __launch_bounds__(64) void k_q8t_rescan(int batch, int cap, const int *__restrict__ n1v,
-                                                   const float *__restrict__ desc0, const float *__restrict__ desc1,
-                                                   double thresh, int *__restrict__ match_idx,
-                                                   float *__restrict__ match_score, const int *__restrict__ rs_flags,
-                                                   const unsigned char *__restrict__ rs_colsh) {
-    __shared__ __attribute__((aligned(16))) char buf[32 * KD];  // row image / column stage / dot staging
-    __shared__ int cl[64 * RS_CAP];                              // [row fr][half fh] listed columns
-    __shared__ int slots[32], lims[32];
+__global__ __launch_bounds__(64 * RS_NW) void k_q8t_rescan(int batch, int cap, const int *__restrict__ n1v,
+                                                           const float *__restrict__ desc0,
+                                                           const float *__restrict__ desc1, double thresh,
+                                                           int *__restrict__ match_idx, float *__restrict__ match_score,
+                                                           const int *__restrict__ rs_flags,
+                                                           const unsigned char *__restrict__ rs_colsh) {
+    __shared__ __attribute__((aligned(16))) char bufs[RS_NW][32 * KD];  // per wave: row image / column stage / dots
+    __shared__ int cls[RS_NW][64 * RS_CAP];                              // per wave: [row fr][half fh] listed columns
+    __shared__ int slotss[RS_NW][32], limss[RS_NW][32];                  // per wave: the batch (identical copies)
+    __shared__ float red_s[RS_NW][32];
+    __shared__ int red_j[RS_NW][32];
     __shared__ __attribute__((aligned(16))) unsigned char colsh[T_BM];
-    const int lane = threadIdx.x, fr = lane & 31, fh = lane >> 5, sub = lane & 15, rq = lane >> 4;
-    int *mycl = cl + (fh * 32 + fr) * RS_CAP;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int fr = lane & 31, fh = lane >> 5, sub = lane & 15, rq = lane >> 4;
+    char *buf = bufs[w];
+    int *mycl = cls[w] + (fh * 32 + fr) * RS_CAP;
+    int *slots = slotss[w], *lims = limss[w];
     for (int pair = blockIdx.x; pair < batch; pair += gridDim.x) {
         const int fl = __builtin_amdgcn_readfirstlane(rs_flags[pair]);
-        if (!fl) continue;
+        if (!fl) continue;  // uniform over the workgroup
         const int tb = fl - 1;
         const int n1 = min(max(n1v[pair], 0), cap);
         const float *A = desc0 + (size_t)pair * cap * KD;
         const float *B = desc1 + (size_t)pair * cap * KD;
         int *oidx = match_idx + (size_t)pair * cap;
         float *oscore = match_score ? match_score + (size_t)pair * cap : nullptr;
-        *reinterpret_cast<i32x4 *>(colsh + 16 * lane) =
-            *reinterpret_cast<const i32x4 *>(rs_colsh + (size_t)pair * T_BM + 16 * lane);
+        __syncthreads();  // the previous pair's colsh / red reads done
+        if (w == 0)
+            *reinterpret_cast<i32x4 *>(colsh + 16 * lane) =
+                *reinterpret_cast<const i32x4 *>(rs_colsh + (size_t)pair * T_BM + 16 * lane);
+        __syncthreads();
         const int nblk = (n1 + 31) / 32;
-        // one batch of ns pending rows (slots / lims)
+        // one batch of ns pending rows (slots / lims): every wave, its share of the column blocks
         auto run_batch = [&](int ns) {
             // the rows' codes as the A phase made them: 16 lanes per row, 4 rows per pass
 #pragma unroll 2
@@ -1235,7 +1245,7 @@ __global__ __launch_bounds__(64) void k_q8t_rescan(int batch, int cap, const int
                 }
                 cnt = 0;
             };
-            for (int blk = 0; blk < nblk; blk++) {
+            for (int blk = w; blk < nblk; blk += RS_NW) {
                 // columns 32 blk + c as the sweep quantised them: one 1-KiB column per load
                 // instruction (lane l: floats 4 l .. +3)
 #pragma unroll
@@ -1284,13 +1294,27 @@ __global__ __launch_bounds__(64) void k_q8t_rescan(int batch, int cap, const int
                 bs = ob;
                 bj = oj;
             }
-            if (mine && fh == 0) {
+            if (fh == 0) {
+                red_s[w][fr] = bs;
+                red_j[w][fr] = bj;
+            }
+            __syncthreads();
+            if (w == 0 && fh == 0 && mine) {  // the waves' bests: the same order-free maximum
+#pragma unroll
+                for (int v = 1; v < RS_NW; v++)
+                    if (better(0, red_s[v][fr], red_j[v][fr], bs, bj)) {
+                        bs = red_s[v][fr];
+                        bj = red_j[v][fr];
+                    }
                 const bool keep = bj != 0x7fffffff && (double)bs > thresh && bs > 0.f;
                 oidx[myrow] = keep ? bj : -1;
                 if (oscore) oscore[myrow] = keep ? bs : 0.f;
             }
+            __syncthreads();  // red reused by the next batch
         };
-        // the pending rows (index < -1), gathered 32 at a time in row order
+        // the pending rows (index < -1), gathered 32 at a time in row order -- every wave the
+        // same list, into its own copy (the reads of oidx precede any write of this pair's rows:
+        // a batch writes only rows already gathered)
         int ns = 0;
         for (int r0 = 0; r0 < cap; r0 += 64) {
             const int r = r0 + lane;
@@ -1387,9 +1411,9 @@ int launch_allpairs_q8t_match(hipStream_t s, void *scratch, int batch, int cap, 
                        match_idx, match_score, flags, rflags, rcolsh);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
-    if (T_RESCREEN) {  // the wide rows it left: one wave per workgroup, a grid-stride loop over pairs
+    if (T_RESCREEN) {  // the wide rows it left: 4 waves per workgroup, a grid-stride loop over pairs
         MV_PROF_BEGIN(s, "k_q8t_rescan");
-        hipLaunchKernelGGL(k_q8t_rescan, dim3((unsigned)min(batch, 2048)), dim3(64), 0, s, batch, cap, n1, desc0,
+        hipLaunchKernelGGL(k_q8t_rescan, dim3((unsigned)min(batch, 1024)), dim3(64 * RS_NW), 0, s, batch, cap, n1, desc0,
                            desc1, thresh, match_idx, match_score, rflags, rcolsh);
         MV_PROF_END(s);
         MV_LAUNCH_CHECK();

@@ -115,8 +115,10 @@ def run(frames=257, steps=10, warmup=2, check=1, pipelines=2):
         i2, _ = oracle.allpairs_f32(chain[0], chain[1], 0.8)
         assert (idx[0, :i2.shape[0]].cpu().numpy() == i2).all(), "match differs from the oracle chain"
         res["checked_pairs"] = 1
-        for pp in pipes[1:]:  # the same track on every pipeline: identical matches and poses
-            assert torch.equal(pp.idx, p0.idx) and torch.equal(pp.T, p0.T), "pipelines differ"
+        for i, pp in enumerate(pipes[1:], 1):  # the same track on every pipeline: identical matches and poses
+            bad = [k for k in ("semi", "cdesc", "nkp", "kp", "desc", "idx", "T") if not torch.equal(getattr(pp, k),
+                                                                                                 getattr(p0, k))]
+            assert not bad, "pipeline %d differs from pipeline 0 in %s" % (i, bad)
     for pp in pipes:
         pp.sp.close()
         pp.ctx.close()
