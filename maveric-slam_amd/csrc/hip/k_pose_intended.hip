@@ -48,11 +48,13 @@ constexpr int NT = 256;
 #endif
 #ifndef PE_WAVES
 // waves per SIMD.  3: 155 VGPRs, no scratch.  4 (128 VGPRs, 38 VGPRs + 22 SGPRs spilled, 96 B of
-// scratch per lane) was ~8 % faster (0.523 vs 0.564 ms exact, 1.07 vs 1.17 ms noisy,
+// scratch per lane) was faster (0.523 vs 0.564 ms exact, 1.07 vs 1.17 ms noisy,
 // profiles/r04y_pose_waves_ab.log) but NOT deterministic: with the image -> pose chain running on
-// three streams at once, a few poses per 256-pair track came out different from the same track
+// three streams at once, some poses of a 256-pair track came out different from the same track
 // run alone (matches identical; tools/dbg_pipelines.py, profiles/r05m_pose_determinism.log), the
-// spill-free build bit-identical in every round -- so no scratch in this kernel
+// spill-free build bit-identical in every round -- so no scratch in this kernel.  (Measured and
+// not kept: every wave solving its group's normal equations itself, one barrier per Gauss-Newton
+// iteration instead of two: 1.105 vs 1.097-1.113 ms noisy, profiles/r05p_pose_rsolve_ab.log.)
 #define PE_WAVES 3
 #endif
 constexpr int MAXP = 4096;  // correspondences per pair held in LDS (float4 each)
@@ -503,9 +505,9 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
     __syncthreads();
     float best_cost = __builtin_inff();
     int best_h = 0x7fffffff;
-    // hypothesis h's 8 distinct samples (a counter-based stream: the survivors' owners draw theirs
-    // again below instead of keeping the best E in 9 registers through the loop)
-    auto draw8 = [&](int h, int (&idx)[8]) {
+    float best_e[9];
+    for (int h = t; h < a.hypotheses; h += NT) {
+        int idx[8];
         const unsigned long long base = a.seed ^ ((unsigned long long)b << 40) ^ ((unsigned long long)h << 8);
         int drawn = 0;
         unsigned long long r = 0;
@@ -523,11 +525,7 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
                 drawn++;
             }
         }
-        return drawn == 8;
-    };
-    for (int h = t; h < a.hypotheses; h += NT) {
-        int idx[8];
-        if (!draw8(h, idx)) continue;
+        if (drawn < 8) continue;
         float e[9];
         if (!eight_point(P, idx, e)) continue;
         f2v acc = {0.f, 0.f};
@@ -547,6 +545,8 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
         if (cost < best_cost || (cost == best_cost && h < best_h)) {
             best_cost = cost;
             best_h = h;
+#pragma unroll
+            for (int r = 0; r < 9; r++) best_e[r] = e[r];
         }
     }
     const long long tk2 = PE_TRACE ? clock64() : 0;
@@ -569,12 +569,8 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
                 if (lane == 0) s_sh[w * SURV + r] = -1;
             } else if (key == k) {  // the owner (keys are unique: hypothesis ids differ)
                 s_sh[w * SURV + r] = best_h;
-                int idx[8];
-                float e[9];
-                draw8(best_h, idx);       // the same samples and the same solve: the same E
-                eight_point(P, idx, e);
 #pragma unroll
-                for (int q = 0; q < 9; q++) s_sE[w * SURV + r][q] = e[q];
+                for (int q = 0; q < 9; q++) s_sE[w * SURV + r][q] = best_e[q];
                 key = ~0ull;
             }
         }
