@@ -54,7 +54,10 @@ constexpr int NT = 256;
 // run alone (matches identical; tools/dbg_pipelines.py, profiles/r05m_pose_determinism.log), the
 // spill-free build bit-identical in every round -- so no scratch in this kernel.  (Measured and
 // not kept: every wave solving its group's normal equations itself, one barrier per Gauss-Newton
-// iteration instead of two: 1.105 vs 1.097-1.113 ms noisy, profiles/r05p_pose_rsolve_ab.log.)
+// iteration instead of two: 1.105 vs 1.097-1.113 ms noisy, profiles/r05p_pose_rsolve_ab.log; each
+// start refined by ONE wave with wave reductions and no block barrier at all: 1.046-1.050 vs
+// 0.995-0.996 ms noisy, 0.516-0.517 vs 0.494 exact -- the per-point passes, not the barriers, set
+// the pace -- profiles/r05r_pose_wavegn_ab.log.)
 #define PE_WAVES 3
 #endif
 constexpr int MAXP = 4096;  // correspondences per pair held in LDS (float4 each)
