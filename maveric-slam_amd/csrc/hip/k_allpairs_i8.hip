@@ -262,16 +262,15 @@ __device__ __forceinline__ i32x16 mfma_i8_from4_m(i32x4 a, i32x4 b) {
     asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, 4.0" : "=&v"(d) : "v"(a), "v"(b));
     return d;
 }
+// the row block L (pair L / tiles_r, rows (L % tiles_r) M_BM ..) of k_i8_match -- also run by
+// k_i8m_handback for the pairs k_i8t_match hands back
 template <bool KEYS>
-__global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, const int *__restrict__ n0v,
-                                                      const int *__restrict__ n1v, const int8_t *__restrict__ desc0,
-                                                      const int8_t *__restrict__ desc1, const int *__restrict__ nb_v,
-                                                      const float *__restrict__ rnb_v, int *__restrict__ match_idx,
-                                                      int *__restrict__ match_dot, const int8_t *__restrict__ q1v,
-                                                      int cap64) {
-    __shared__ __attribute__((aligned(16))) char lds[M_LDS];
+__device__ __forceinline__ void i8m_block(char *lds, int L, int tiles_r, int cap, const int *__restrict__ n0v,
+                                          const int *__restrict__ n1v, const int8_t *__restrict__ desc0,
+                                          const int8_t *__restrict__ desc1, const int *__restrict__ nb_v,
+                                          const float *__restrict__ rnb_v, int *__restrict__ match_idx,
+                                          int *__restrict__ match_dot, const int8_t *__restrict__ q1v, int cap64) {
     int *na_s = reinterpret_cast<int *>(lds + M_OFF_NA);
-    const int L = xcd_remap(blockIdx.x, gridDim.x);
     const int pair = L / tiles_r, tr = L % tiles_r;
     const int n0 = min(max(n0v[pair], 0), cap), n1 = min(max(n1v[pair], 0), cap);
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -688,6 +687,36 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, cons
             }
         }
 }
+template <bool KEYS>
+__global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, const int *__restrict__ n0v,
+                                                      const int *__restrict__ n1v, const int8_t *__restrict__ desc0,
+                                                      const int8_t *__restrict__ desc1, const int *__restrict__ nb_v,
+                                                      const float *__restrict__ rnb_v, int *__restrict__ match_idx,
+                                                      int *__restrict__ match_dot, const int8_t *__restrict__ q1v,
+                                                      int cap64) {
+    __shared__ __attribute__((aligned(16))) char lds[M_LDS];
+    i8m_block<KEYS>(lds, xcd_remap(blockIdx.x, gridDim.x), tiles_r, cap, n0v, n1v, desc0, desc1, nb_v, rnb_v,
+                    match_idx, match_dot, q1v, cap64);
+}
+// The pairs k_i8t_match hands back (a row with two in-window columns in one lane half, whose deep
+// re-score would scan every column of the half -- the common case on the network's own
+// descriptors, many near-duplicate cells): k_i8_match's row blocks of those pairs (64 rows per
+// wave, up to 16 listed candidates per row): one workgroup per row block, which exits at once
+// unless its pair is flagged (a grid-stride loop over the flags spilled 2 VGPRs at 256: no
+// scratch in this file's kernels).
+__global__ __launch_bounds__(M_NT, 2) void k_i8m_handback(int tiles_r, int cap, const int *__restrict__ n0v,
+                                                          const int *__restrict__ n1v,
+                                                          const int8_t *__restrict__ desc0,
+                                                          const int8_t *__restrict__ desc1,
+                                                          const int *__restrict__ nb_v, int *__restrict__ match_idx,
+                                                          int *__restrict__ match_dot,
+                                                          const int8_t *__restrict__ q1v, int cap64,
+                                                          const int *__restrict__ only) {
+    __shared__ __attribute__((aligned(16))) char lds[M_LDS];
+    const int L = xcd_remap(blockIdx.x, gridDim.x);
+    if (!__builtin_amdgcn_readfirstlane(only[L / tiles_r])) return;  // uniform: one flag per block
+    i8m_block<true>(lds, L, tiles_r, cap, n0v, n1v, desc0, desc1, nb_v, nullptr, match_idx, match_dot, q1v, cap64);
+}
 
 
 // ---------------------------------------------------------------------------
@@ -714,6 +743,13 @@ constexpr int IT_OFF_LM = IT_OFF_NA + IT_BM * 4;   // [IT_BM] deep rows' halves
 constexpr int IT_LDS = IT_OFF_LM + IT_BM * 4;
 static_assert(IT_LDS <= 160 * 1024, "LDS");
 static_assert(IT_DPW == 2, "8 waves: 2 DMA pieces per wave and tile");
+#ifndef IT_HANDBACK
+// 1: a pair with a deep row (two in-window columns in one lane half) is handed to k_i8m_handback
+// whole.  On the network's own int8 descriptors (256 consecutive KITTI frames, 1920 cells each)
+// the in-kernel deep re-scores made k_i8t_match 7.84 ms against k_i8_match's 0.29
+// (tools/ab_real_i8.py, profiles/r05s_i8_real_desc.log); 0: the deep rows scored here (A/B)
+#define IT_HANDBACK 1
+#endif
 #ifndef IT_REUSE
 #define IT_REUSE 1  // a column block's 8 fragments read once and kept for its 4 row groups
 #endif
@@ -726,7 +762,8 @@ __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, co
                                                         const int8_t *__restrict__ desc0,
                                                         const int8_t *__restrict__ desc1, const int *__restrict__ nb_v,
                                                         int *__restrict__ match_idx, int *__restrict__ match_dot,
-                                                        const int8_t *__restrict__ q1v, int cap64) {
+                                                        const int8_t *__restrict__ q1v, int cap64,
+                                                        int *__restrict__ handback) {
     __shared__ __attribute__((aligned(16))) char lds[IT_LDS];
     int *na_s = reinterpret_cast<int *>(lds + IT_OFF_NA);
     unsigned *lmask = reinterpret_cast<unsigned *>(lds + IT_OFF_LM);
@@ -925,6 +962,7 @@ __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, co
         return (int)(tg >> 4) * 32 + 8 * (int)((tg >> 2) & 3u) + (int)(tg & 3u) + 4 * h;
     };
     unsigned deep_rows[IT_RG];
+    bool hand = false;
 #pragma unroll
     for (int g = 0; g < IT_RG; g++) {
         const float e1 = m1[g], e2 = m2[g];
@@ -950,6 +988,7 @@ __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, co
         if (ambig) {
             if (in2 || oin2) {  // a half holds two columns inside: its every column is a candidate
                 nc = -1;
+                hand = true;  // (IT_HANDBACK: the pair goes to k_i8m_handback instead)
                 wm = (in1 ? 1u << fh : 0u) | (oin1 ? 1u << (1 - fh) : 0u);
             } else {
                 const int jm = kcol(e1, fh), jo = __shfl_xor(jm, 32, 64);
@@ -993,6 +1032,10 @@ __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, co
         }
         if (fh == 0 && live && nc < 0) lmask[rl] = wm;
         deep_rows[g] = (unsigned)__ballot(fh == 0 && live && nc < 0);
+    }
+    if (IT_HANDBACK && __ballot(hand)) {  // the pair is redone in k_i8_match's layout: no deep re-scores here
+        if (lane == 0) handback[pair] = 1;
+        return;
     }
     // ---- deep rows (rare): every column of the listed halves, one column per lane at a time ----
 #pragma unroll
@@ -1061,7 +1104,8 @@ static int i8_cap64(int cap) { return (cap + M_BN - 1) / M_BN * M_BN; }
 
 size_t allpairs_i8_scratch_bytes(int batch, int cap) {
     const size_t rows = (size_t)batch * cap;
-    return 2 * align_up(4 * rows, 256) + (i8_keys(cap) ? align_up((size_t)batch * i8_cap64(cap) * KD, 256) : 0);
+    return 2 * align_up(4 * rows, 256) + (i8_keys(cap) ? align_up((size_t)batch * i8_cap64(cap) * KD, 256) : 0) +
+           align_up((size_t)batch * 4, 256);  // k_i8t_match's hand-back flags
 }
 
 int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
@@ -1090,11 +1134,24 @@ int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const i
         const int tiles_t = (cap + IT_BM - 1) / IT_BM;
         const long tblocks = (long)batch * tiles_t;
         MV_REQUIRE(tblocks < (1l << 31));
+        int *flags = (int *)((char *)scratch + 2 * align_up(4 * rows, 256) +
+                             align_up((size_t)batch * cap64 * KD, 256));
+        MV_HIP_TRY(hipMemsetAsync(flags, 0, (size_t)batch * 4, s));
         MV_PROF_BEGIN(s, "k_i8t_match");
         hipLaunchKernelGGL(k_i8t_match, dim3((unsigned)tblocks), dim3(IT_NT), 0, s, tiles_t, cap, n0, n1, desc0, desc1,
-                           nb, match_idx, match_dot, q1, cap64);
+                           nb, match_idx, match_dot, q1, cap64, flags);
         MV_PROF_END(s);
         MV_LAUNCH_CHECK();
+        if (IT_HANDBACK) {
+            const int tiles_m = (cap + M_BM - 1) / M_BM;
+            const long mblocks = (long)batch * tiles_m;
+            MV_REQUIRE(mblocks < (1l << 31));
+            MV_PROF_BEGIN(s, "k_i8m_handback");
+            hipLaunchKernelGGL(k_i8m_handback, dim3((unsigned)mblocks), dim3(M_NT), 0, s, tiles_m, cap, n0, n1, desc0,
+                               desc1, nb, match_idx, match_dot, q1, cap64, flags);
+            MV_PROF_END(s);
+            MV_LAUNCH_CHECK();
+        }
         return MV_OK;
     }
     const int tiles_m = (cap + M_BM - 1) / M_BM;
