@@ -747,7 +747,11 @@ static_assert(IT_DPW == 2, "8 waves: 2 DMA pieces per wave and tile");
 // 1: a pair with a deep row (two in-window columns in one lane half) is handed to k_i8m_handback
 // whole.  On the network's own int8 descriptors (256 consecutive KITTI frames, 1920 cells each)
 // the in-kernel deep re-scores made k_i8t_match 7.84 ms against k_i8_match's 0.29
-// (tools/ab_real_i8.py, profiles/r05s_i8_real_desc.log); 0: the deep rows scored here (A/B)
+// (tools/ab_real_i8.py, profiles/r05s_i8_real_desc.log); 0: the deep rows scored here (A/B).
+// Measured and not kept: the deep rows re-screened on the matrix cores as k_q8t_rescan does for
+// the fp32 path -- 1.00 ms per 256 network pairs against 0.69 with the hand-back: those pairs
+// have hundreds of deep rows each, and k_i8_match's 16-candidate lists are the better layout
+// for them (profiles/r05t_i8_rescan.log)
 #define IT_HANDBACK 1
 #endif
 #ifndef IT_REUSE

@@ -52,7 +52,7 @@ for _ in range(steps):
 torch.cuda.synchronize()
 mvtrack.profile_enable(False)
 st = {}
-for k in ("k_i8_prep", "k_i8t_match", "k_i8_norms", "k_i8_match"):
+for k in ("k_i8_prep", "k_i8t_match", "k_i8t_rescan", "k_i8m_handback", "k_i8_norms", "k_i8_match"):
     ms, c = mvtrack.profile_query(k)
     if c:
         st[k] = round(ms / steps, 4)
