@@ -65,7 +65,7 @@ int quiesce(mv_context *ctx) {
 // then be recorded on it or waited for by it (a record on the legacy stream, or an uncaptured
 // event waited for by a capturing stream, invalidates the capture; a wait of own_stream on an
 // event recorded inside a capture pulls own_stream into it, unjoined)
-static bool capturing(hipStream_t s) {
+bool capturing(hipStream_t s) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &st) != hipSuccess) {
         (void)hipGetLastError();  // clear the sticky query error
@@ -197,6 +197,7 @@ int mv_context_destroy(mv_context *ctx) {
     if (ctx->ap_scratch) (void)hipFree(ctx->ap_scratch);
     if (ctx->ap_scratch2) (void)hipFree(ctx->ap_scratch2);
     if (ctx->stage_dev) (void)hipFree(ctx->stage_dev);
+    if (ctx->i8_count_host) (void)hipHostFree(ctx->i8_count_host);
     (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
     return MV_OK;

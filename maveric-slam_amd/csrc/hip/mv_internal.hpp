@@ -33,6 +33,11 @@ struct mv_context {
     // wait on it: own_stream then orders after all work issued on every stream the context left
     // (no stream handle is kept, so a caller may destroy a stream once the context moved off it)
     hipEvent_t ev_retire;
+    // int8 all-pairs adaptive dispatch (mv_match_allpairs_i8_dev): pinned count of the pairs the
+    // last measuring call handed back, that call's batch, calls so far
+    int *i8_count_host;
+    int i8_meas_batch;
+    unsigned i8_calls;
 };
 
 namespace mv {
@@ -40,6 +45,8 @@ namespace mv {
 void set_error(int status, const char *fmt, ...);
 int set_status(int status);
 
+// true while `s` is captured into a graph (or the query is refused: see mv_context.hip)
+bool capturing(hipStream_t s);
 // Grow (never shrink) the context scratch; returns nullptr on failure.
 void *scratch(mv_context *ctx, size_t bytes);
 void *stage(mv_context *ctx, size_t bytes);
@@ -137,7 +144,8 @@ int launch_allpairs_q8t_match(hipStream_t s, void *scratch, int batch, int cap, 
                               float *match_score);
 size_t allpairs_i8_scratch_bytes(int batch, int cap);
 int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const int *n0, const int *n1,
-                       const int8_t *desc0, const int8_t *desc1, int *match_idx, int *match_dot);
+                       const int8_t *desc0, const int8_t *desc1, int *match_idx, int *match_dot, bool direct = false,
+                       int *count_host = nullptr);
 size_t pose_scratch_bytes(int batch, int cap);
 int launch_pose(hipStream_t s, void *scratch, const mv_pose_params *p, int batch, int cap, const int *n,
                 const float *pts0, const float *pts1, const int *match_idx, const float *kp1, float *T,

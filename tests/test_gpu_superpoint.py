@@ -172,3 +172,43 @@ def test_network_int8_descriptors_through_int8_allpairs(ctx, orc, torch_cuda, sp
         assert (got_i[:n] == i2).all() and (got_d[:n] == d2).all()
         assert (got_i[n:] == -1).all()
         assert (i2 >= 0).sum() > 100  # consecutive frames: many cells re-observed above cos 0.9
+
+
+def test_int8_allpairs_adaptive_dispatch(ctx, orc, torch_cuda, sp):
+    """mv_match_allpairs_i8_dev's adaptive dispatch: after a call whose pairs k_i8t_match mostly
+    handed back (the network's own descriptors), the next calls run k_i8_match directly; then a
+    batch of well-separated synthetic descriptors -- every call's indices and dots equal to the
+    oracle's, whichever kernel ran (the pinned count is read without waiting, so the switch may
+    come a call later: both paths are checked over the sequence)."""
+    ims = load_golden("kitti00_images.npz")
+    imgs = [ims["img_000000"], ims["img_000001"]]
+    _, desc, _, _ = _run(ctx, torch_cuda, sp, imgs, 192, 640)
+    dev = torch_cuda.device("cuda:0")
+    cap, n = 2048, desc[0].shape[0]
+    rng = np.random.default_rng(5)
+    syn = rng.integers(-60, 61, (2, n, 256)).astype(np.int8)
+    syn[1, :n // 2] = syn[0, :n // 2]  # half the rows re-observed exactly
+    cases = [(desc[0], desc[1])] * 4 + [(syn[0], syn[1])] * 2 + [(desc[1], desc[0])] * 2
+    exp = {}
+    ctx.set_stream(torch_cuda.cuda.current_stream())
+    try:
+        for k, (a, c) in enumerate(cases):
+            D0 = np.zeros((2, cap, 256), np.int8)
+            D1 = np.zeros((2, cap, 256), np.int8)
+            D0[:, :n], D1[:, :n] = a, c
+            nn_ = torch_cuda.full((2,), n, dtype=torch_cuda.int32, device=dev)
+            idx = torch_cuda.full((2, cap), -7, dtype=torch_cuda.int32, device=dev)
+            dot = torch_cuda.zeros((2, cap), dtype=torch_cuda.int32, device=dev)
+            ctx.match_allpairs_i8(torch_cuda.from_numpy(D0).to(dev), torch_cuda.from_numpy(D1).to(dev), nn_, nn_, idx,
+                                  dot)
+            torch_cuda.cuda.synchronize()
+            key = (a.tobytes()[:64], c.tobytes()[:64])
+            if key not in exp:
+                exp[key] = orc.allpairs_i8(a, c)
+            i2, d2 = exp[key]
+            for b in range(2):
+                got_i, got_d = idx.cpu().numpy()[b], dot.cpu().numpy()[b]
+                assert (got_i[:n] == i2).all() and (got_d[:n] == d2).all(), (k, b)
+                assert (got_i[n:] == -1).all(), (k, b)
+    finally:
+        ctx.set_stream(None)
