@@ -1190,10 +1190,10 @@ extern "C" int mv_match_allpairs_i8_dev(mv_context *ctx, int batch, int cap, con
     // network's own descriptors that is nearly every pair (k_i8t 0.23 + hand-back 0.28 ms per 256
     // KITTI pairs against 0.29 for k_i8_match alone), on well-separated descriptors none (k_i8t
     // ~16 % faster).  So: when the last measured call handed back more than half its pairs, the
-    // next 15 calls run k_i8_match directly, then the transposed kernel measures again.  The count
-    // arrives by an async copy into pinned memory, read without waiting (a stale value only
-    // delays the switch); results are identical either way (both kernels are integer-exact); a
-    // captured stream always takes the transposed path.
+    // following calls run k_i8_match directly (every 16th takes the transposed kernel again).  The
+    // count arrives by an async copy into pinned memory, read without waiting: until it lands
+    // the previous decision holds and no new measurement starts; results are identical either
+    // way (both kernels are integer-exact); a captured stream always takes the transposed path.
     bool direct = false;
     int *count_host = nullptr;
     if (!mv::capturing(ctx->stream)) {
@@ -1201,14 +1201,19 @@ extern "C" int mv_match_allpairs_i8_dev(mv_context *ctx, int batch, int cap, con
             void *h = nullptr;
             if (hipHostMalloc(&h, 64, 0) == hipSuccess) {
                 ctx->i8_count_host = static_cast<int *>(h);
-                *ctx->i8_count_host = -1;
+                *ctx->i8_count_host = -2;  // -2: no measurement in flight, -1: in flight, >= 0: landed
             }
         }
         if (ctx->i8_count_host) {
-            const int c = *static_cast<volatile int *>(ctx->i8_count_host);
-            direct = (ctx->i8_calls % 16) != 0 && c >= 0 && 2l * c > ctx->i8_meas_batch;
-            if (!direct) {
-                *ctx->i8_count_host = -1;
+            volatile int *ch = ctx->i8_count_host;
+            const int c = *ch;
+            if (c >= 0) {  // a measurement landed: it decides until the next one
+                ctx->i8_prefer_m = 2l * c > ctx->i8_meas_batch;
+                *ch = -2;
+            }
+            direct = ctx->i8_prefer_m && (ctx->i8_calls % 16) != 0;
+            if (!direct && *ch == -2) {  // measure this call
+                *ch = -1;
                 ctx->i8_meas_batch = batch;
                 count_host = ctx->i8_count_host;
             }

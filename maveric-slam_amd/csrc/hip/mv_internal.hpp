@@ -38,6 +38,7 @@ struct mv_context {
     int *i8_count_host;
     int i8_meas_batch;
     unsigned i8_calls;
+    bool i8_prefer_m;  // the last landed measurement: most pairs handed back
 };
 
 namespace mv {
