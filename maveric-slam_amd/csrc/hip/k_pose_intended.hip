@@ -46,6 +46,15 @@ constexpr int NT = 256;
 #ifndef PE_TRACE
 #define PE_TRACE 0  // printf per-phase clock64() deltas of block 0 (timing experiments only)
 #endif
+#ifndef PE_PREM
+// correspondences in the preemptive scoring subset of the 256 hypotheses (the 8 survivors are then
+// scored on all).  Same-box A/B (profiles/r05u_pose_prem_ab.log): 128 / 64 / 32 points -- exact
+// data 0.498 / 0.442 / 0.415 ms, 0.5 px + 20 % outliers 0.996 / 0.939 / 0.905 ms per 8192 pairs,
+// pose errors unchanged (realistic line p99: rotation 0.085 / 0.086 / 0.086 deg, translation
+// direction 2.51 / 2.54 / 2.56 deg), every pose test green; 64 kept (the subset still ranks
+// hypotheses under heavier contamination than the bench's)
+#define PE_PREM 64
+#endif
 #ifndef PE_WAVES
 // waves per SIMD.  3: 155 VGPRs, no scratch.  4 (128 VGPRs, 38 VGPRs + 22 SGPRs spilled, 96 B of
 // scratch per lane) was faster (0.523 vs 0.564 ms exact, 1.07 vs 1.17 ms noisy,
@@ -495,7 +504,7 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
     //         Every hypothesis is scored on an evenly strided subset of PRE_M
     //         correspondences; the SURV best of each wave survive (preemptive RANSAC,
     //         Nister 2003) and are re-scored on all correspondences cooperatively. ----
-    constexpr int PRE_M = 128, SURV = 2, NS = 4 * SURV;
+    constexpr int PRE_M = PE_PREM, SURV = 2, NS = 4 * SURV;
     const int m = min(n, PRE_M);
     const unsigned step16 = ((unsigned)n << 16) / (unsigned)m;  // subset point k: (k * step16) >> 16 < n
     // the subset in point-pair layout (points 2k, 2k+1 of it in s_sub[k])
