@@ -730,6 +730,152 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv1x1(const int8_t *__restric
     }
 }
 
+// The 1 x 1 heads as a weight-stationary pass (SP_HEAD 1).  The heads are data movement: 256 B
+// of input per pixel against 65 / 256 outputs, ~2 k MFMA cycles per 64 KiB tile -- k_sp_conv1x1's
+// 576 / 1152 tile workgroups (2 per CU) ran 1.1 / 2.3 rounds of load-then-compute each (25 / 28
+// us per 64 frames, profiles/r05w_sp_layers.txt).  Here a workgroup keeps its share of the
+// weights in registers (wave w: channel blocks CBW w .. CBW w + CBW - 1, 8 k32 fragments each)
+// and streams HD_NB consecutive 32-pixel blocks through a double-buffered LDS tile, the loads of
+// the next HD_D blocks in flight in registers while a block is multiplied -- straight-line code
+// (no loop back-edge, across which the compiler would wait for every outstanding load).  Blocks
+// follow the output order: Frame cells (x H + y) for OMODE 1, so a block's semi outputs are
+// 32 x 65 contiguous bytes (staged in LDS, stored as whole words by the next block), row-major
+// pixels for OMODE 2 (run()'s NCHW planes: 32 consecutive floats per channel).  The integer
+// products, bias and requantisation are k_sp_conv1x1's: bit-identical.
+#ifndef SP_HEAD
+#define SP_HEAD 1  // 0: k_sp_conv1x1 (A/B)
+#endif
+constexpr int HD_PS = 17, HD_D = 3, HD_NB = 8;
+// FULL: every frame whole blocks (H W % 32 == 0), every workgroup HD_NB of them and out 4-B
+// aligned -- no lane or block guards, so the loads stay in flight (a load under a branch is sunk
+// to its use, a store under one makes the compiler wait for every outstanding load at the join);
+// otherwise the guarded form.
+template <int OMODE, int NCB, bool FULL>
+__global__ __launch_bounds__(SP_NT, 2) void k_sp_head(const int8_t *__restrict__ in, int H, int W, int nblk_f,
+                                                      int nblk, const i32x4 *__restrict__ wf,
+                                                      const int *__restrict__ bq, float rs,
+                                                      int8_t *__restrict__ out, int cstride, float dq) {
+    constexpr int CBW = (NCB + 3) / 4, NS = 8;
+    constexpr bool STAGE = OMODE == 1 && NCB * 32 < 128;  // the semi head: 65-byte cells
+    __shared__ i32x4 tile[2][32 * HD_PS];
+    __shared__ int stg[STAGE ? 2 : 1][STAGE ? 32 * 65 / 4 + 1 : 1];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, fr = lane & 31, fh = lane >> 5;
+    const int HW = H * W;
+    const int kb = blockIdx.x * HD_NB, nmine = min(HD_NB, nblk - kb);
+    // the wave's weights and bias first (the block loads after them: waiting for a block's loads
+    // then implies the weights, in the in-order count).  A wave past the last channel block (the
+    // semi head's wave 3) recomputes the last one and stores the same values again.
+    i32x4 aw[CBW][NS];
+    i32x16 bias[CBW];
+    int cbs[CBW];
+#pragma unroll
+    for (int c = 0; c < CBW; c++) {
+        const int cb = min(CBW * w + c, NCB - 1);
+        cbs[c] = cb;
+#pragma unroll
+        for (int s = 0; s < NS; s++) aw[c][s] = wf[((size_t)cb * NS + s) * 64 + lane];
+#pragma unroll
+        for (int qq = 0; qq < 4; qq++) {
+            const i32x4 x = *reinterpret_cast<const i32x4 *>(bq + 32 * cb + 8 * qq + 4 * fh);
+#pragma unroll
+            for (int e = 0; e < 4; e++) bias[c][4 * qq + e] = x[e];
+        }
+    }
+    // block j of this workgroup (j >= nmine: the last one again, loaded but never used): frame
+    // fb[j], first pixel 32 fi[j]
+    int fb[HD_NB], fi[HD_NB];
+    fb[0] = kb / nblk_f;
+    fi[0] = kb - fb[0] * nblk_f;
+#pragma unroll
+    for (int j = 1; j < HD_NB; j++) {
+        const bool wrap = fi[j - 1] + 1 == nblk_f, past = j >= nmine;
+        fb[j] = past ? fb[j - 1] : fb[j - 1] + (wrap ? 1 : 0);
+        fi[j] = past ? fi[j - 1] : (wrap ? 0 : fi[j - 1] + 1);
+    }
+    // thread t loads chunks t and t + 256 of a block: pixels (t >> 4) and (t >> 4) + 16, chunk t & 15
+    auto load = [&](int j, i32x4 (&r)[2]) {
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            int p = 32 * fi[j] + (t >> 4) + 16 * u;
+            if (!FULL) p = min(p, HW - 1);  // clamped: never stored
+            const int y = OMODE == 1 ? p % H : p / W, x = OMODE == 1 ? p / H : p % W;
+            r[u] = *reinterpret_cast<const i32x4 *>(in + ((size_t)fb[j] * HW + (size_t)y * W + x) * 256 + (t & 15) * 16);
+        }
+    };
+    i32x4 R[HD_D][2];
+#pragma unroll
+    for (int d = 0; d < HD_D; d++) load(d, R[d]);
+    auto stage_out = [&](int j) {  // block j's staged semi bytes -> out
+        int8_t *gd = out + ((size_t)fb[j] * HW + 32 * fi[j]) * 65;
+        if (FULL) {  // 520 words: 4 B aligned (H W % 4 == 0, out 4-B aligned)
+            int *gw = reinterpret_cast<int *>(gd);
+            gw[t] = stg[j & 1][t];
+            gw[t + SP_NT] = stg[j & 1][t + SP_NT];
+            if (t < 32 * 65 / 4 - 2 * SP_NT) gw[t + 2 * SP_NT] = stg[j & 1][t + 2 * SP_NT];
+            return;
+        }
+        const int nb = min(32, HW - 32 * fi[j]) * 65;
+        const int8_t *ls = reinterpret_cast<const int8_t *>(stg[j & 1]);
+        for (int o = t; o < nb; o += SP_NT) gd[o] = ls[o];
+    };
+    const int lo = SP_MAGIC_BITS - 128;  // the heads have no relu
+#pragma unroll
+    for (int j = 0; j < HD_NB; j++) {
+        if (!FULL && j >= nmine) break;  // workgroup-uniform
+        i32x4 *tb = tile[j & 1];
+#pragma unroll
+        for (int u = 0; u < 2; u++) tb[((t >> 4) + 16 * u) * HD_PS + (t & 15)] = R[j % HD_D][u];
+        __syncthreads();
+        if (STAGE && j > 0) stage_out(j - 1);
+        if (j + HD_D < HD_NB) load(j + HD_D, R[j % HD_D]);  // past nmine: a repeat, unused
+        i32x16 acc[CBW];
+        const i32x4 *lb = tb + fr * HD_PS + fh;
+#pragma unroll
+        for (int s = 0; s < NS; s++) {
+            const i32x4 bv = lb[2 * s];
+#pragma unroll
+            for (int c = 0; c < CBW; c++)
+                acc[c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aw[c][s], bv, s == 0 ? bias[c] : acc[c], 0, 0, 0);
+        }
+        const int p = 32 * fi[j] + fr;
+        const bool inside = FULL || p < HW;
+#pragma unroll
+        for (int c = 0; c < CBW; c++) {
+            const int cb = cbs[c];
+            int dw[4];  // OMODE 1, 256 channels: the packed codes, 4 per word
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) {
+                const int co = 32 * cb + 8 * qq + 4 * fh;
+                int v[4];
+                requant4(v, acc[c][4 * qq], acc[c][4 * qq + 1], acc[c][4 * qq + 2], acc[c][4 * qq + 3], rs, lo);
+                if constexpr (OMODE == 2) {
+                    float *fo = reinterpret_cast<float *>(out) + ((size_t)fb[j] * cstride + co) * HW + p;
+#pragma unroll
+                    for (int e = 0; e < 4; e++)
+                        if (inside && (NCB * 32 == 256 || co + e < cstride))
+                            fo[(size_t)e * HW] = dq * (float)(v[e] - SP_MAGIC_BITS);
+                } else if constexpr (STAGE) {
+                    int8_t *cell = reinterpret_cast<int8_t *>(stg[j & 1]) + fr * 65;
+#pragma unroll
+                    for (int e = 0; e < 4; e++)
+                        if (co + e < 65) cell[co + e] = (int8_t)v[e];
+                } else {
+                    dw[qq] = pack4b(v[0], v[1], v[2], v[3]);
+                }
+            }
+            if constexpr (OMODE == 1 && !STAGE) {  // channels 32 cb + 16 fh .. + 15 per lane
+                if (inside)
+                    *reinterpret_cast<i32x4 *>(out + ((size_t)fb[j] * HW + p) * cstride + 32 * cb + 16 * fh) =
+                        regroup16(dw);
+            }
+        }
+    }
+    if (STAGE) {
+        __syncthreads();
+        stage_out(nmine - 1);
+    }
+}
+
 // run()'s output quantisation (superpoint_inference.py:199-206), head h (0: semi, C = 65;
 // 1: desc, C = 256) of frame b, split over SP_MG_CHUNKS workgroups per head: k_sp_presence ORs
 // the 256-code presence mask of a chunk into pres[b][h][chunk][8] (its own slot: no atomics, no
@@ -957,6 +1103,39 @@ int launch_conv1x1(hipStream_t st, const mv_superpoint *net, int li, int B, int 
     return MV_OK;
 }
 
+// the heads through k_sp_head (SP_HEAD) or k_sp_conv1x1
+template <int OMODE>
+int launch_head(hipStream_t st, const mv_superpoint *net, int li, int B, int H, int W, const int8_t *in, int8_t *out,
+                int cstride, float dq = 0.f) {
+    if (!SP_HEAD) return launch_conv1x1<OMODE>(st, net, li, B, H, W, in, out, cstride, dq);
+    const int HW = H * W, nblk_f = (HW + 31) / 32;
+    const long nblk = (long)B * nblk_f;
+    MV_REQUIRE((long)B * HW * 256 < (1l << 40) && nblk > 0 && nblk < (1l << 31) - HD_NB);
+    MV_REQUIRE((cstride == 65 || cstride == 256) && (OMODE == 2 || cstride == 65 || ((uintptr_t)out & 15) == 0));
+    const unsigned grid = (unsigned)((nblk + HD_NB - 1) / HD_NB);
+    const char *wd = static_cast<const char *>(net->wdev);
+    const i32x4 *wf = reinterpret_cast<const i32x4 *>(wd + net->frag_off[li]);
+    const int *bq = reinterpret_cast<const int *>(wd + net->bq_off[li]);
+    const bool full = HW % 32 == 0 && nblk % HD_NB == 0 && ((uintptr_t)out & 3) == 0;
+#define MV_HEAD(NCB, FULL)                                                                                      \
+    hipLaunchKernelGGL((k_sp_head<OMODE, NCB, FULL>), dim3(grid), dim3(SP_NT), 0, st, in, H, W, nblk_f, (int)nblk, \
+                       wf, bq, net->rs[li], out, cstride, dq)
+    if (cstride == 65) {
+        if (full)
+            MV_HEAD(3, true);
+        else
+            MV_HEAD(3, false);
+    } else {
+        if (full)
+            MV_HEAD(8, true);
+        else
+            MV_HEAD(8, false);
+    }
+#undef MV_HEAD
+    MV_LAUNCH_CHECK();
+    return MV_OK;
+}
+
 // the 128-channel unpooled layers: the tile geometry covering H x W with fewer padded pixels
 // (GEO 1 wins at 24 x 80: 1920 against 3072)
 #ifndef SP_GEO
@@ -1121,15 +1300,15 @@ int sp_network(hipStream_t st, mv_superpoint *net, int batch, int H, int W, int 
     // heads: Bf holds the shared encoder output
     if ((r = launch_conv_geo<128, 3, false, true, 0>(st, net, 8, batch, h, w, Bf, A, 256)) != MV_OK) return r;
     if (semi_f)
-        r = launch_conv1x1<2>(st, net, 9, batch, h, w, A, reinterpret_cast<int8_t *>(semi_f), 65, net->dq_semi);
+        r = launch_head<2>(st, net, 9, batch, h, w, A, reinterpret_cast<int8_t *>(semi_f), 65, net->dq_semi);
     else
-        r = launch_conv1x1<1>(st, net, 9, batch, h, w, A, semi, 65);
+        r = launch_head<1>(st, net, 9, batch, h, w, A, semi, 65);
     if (r != MV_OK) return r;
     if ((r = launch_conv_geo<128, 3, false, true, 0>(st, net, 10, batch, h, w, Bf, A, 256)) != MV_OK) return r;
     if (desc_f)
-        r = launch_conv1x1<2>(st, net, 11, batch, h, w, A, reinterpret_cast<int8_t *>(desc_f), 256, net->dq_desc);
+        r = launch_head<2>(st, net, 11, batch, h, w, A, reinterpret_cast<int8_t *>(desc_f), 256, net->dq_desc);
     else
-        r = launch_conv1x1<1>(st, net, 11, batch, h, w, A, desc, 256);
+        r = launch_head<1>(st, net, 11, batch, h, w, A, desc, 256);
     if (r != MV_OK) return r;
     MV_PROF_END(st);
     return MV_OK;
