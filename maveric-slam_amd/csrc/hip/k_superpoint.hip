@@ -154,6 +154,12 @@ __global__ __launch_bounds__(256) void k_sp_resize_q(const uint8_t *__restrict__
     q[i] = (int8_t)(int)qv;
 }
 
+#ifndef SP_KSB
+#define SP_KSB 1  // a scheduling barrier after each k32 step of k_sp_conv's K loop (0: free scheduling, A/B)
+#endif
+#ifndef SP_BPF
+#define SP_BPF 0  // 1: k_sp_conv's B fragments one k32 step ahead (A/B)
+#endif
 #ifndef SP_OCC64
 #define SP_OCC64 3  // workgroups per CU for the 64-channel layers (LDS 50 KB; VGPRs <= 168)
 #endif
@@ -390,6 +396,19 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
     int xs[KS];
 #pragma unroll
     for (int kx = 0; kx < KS; kx++) xs[kx] = fh ^ (((pcol + kx) / SWS) & (NCH - 1));
+    // the B fragments of k32 step s (SP_BPF: those of step s + 1 read before step s's MFMAs, so
+    // the LDS latency hides under them)
+    auto bfrag = [&](int s, int j) {
+        const int tap = s * 32 / CIN, ky = tap / KS, kx = tap % KS, c0 = (s * 32 % CIN) / 16;
+        const int off = ((RB * j + ky) * IX + kx) * PS;
+        return PADL ? lb[off + c0] : lb[off + (c0 ^ xs[kx])];
+    };
+    constexpr bool BPF = SP_BPF && (CIN != 64 || SP_OCC64 <= 2);  // the 3-per-CU 64-channel build has no room
+    i32x4 bn[JN];
+    if (BPF) {
+#pragma unroll
+        for (int j = 0; j < JN; j++) bn[j] = bfrag(0, j);
+    }
 #pragma unroll
     for (int s = 0; s < NS; s++) {
         const i32x4 a0 = ra[s % PF], a1 = rb[s % PF];
@@ -397,15 +416,18 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
             ra[s % PF] = wa[(s + PF) * 64];
             rb[s % PF] = wb[(s + PF) * 64];
         }
-        const int tap = s * 32 / CIN, ky = tap / KS, kx = tap % KS, c0 = (s * 32 % CIN) / 16;
+        i32x4 bc[JN];
 #pragma unroll
         for (int j = 0; j < JN; j++) {
-            const int off = ((RB * j + ky) * IX + kx) * PS;
-            const i32x4 bv = PADL ? lb[off + c0] : lb[off + (c0 ^ xs[kx])];
-            acc[j][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bv, s == 0 ? b0 : acc[j][0], 0, 0, 0);
-            acc[j][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bv, s == 0 ? b1 : acc[j][1], 0, 0, 0);
+            bc[j] = BPF ? bn[j] : bfrag(s, j);
+            if (BPF && s + 1 < NS) bn[j] = bfrag(s + 1, j);
         }
-        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < JN; j++) {
+            acc[j][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bc[j], s == 0 ? b0 : acc[j][0], 0, 0, 0);
+            acc[j][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bc[j], s == 0 ? b1 : acc[j][1], 0, 0, 0);
+        }
+        if (SP_KSB) __builtin_amdgcn_sched_barrier(0);
     }
 
     // ---- epilogue: lane = pixel fr of each row; 16 couts (4 groups of 4) per 32-cout block ----
@@ -745,20 +767,31 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv1x1(const int8_t *__restric
 #ifndef SP_HEAD
 #define SP_HEAD 1  // 0: k_sp_conv1x1 (A/B)
 #endif
+#ifndef SP_HEAD_PRES
+#define SP_HEAD_PRES 1  // 0: the presence masks by k_sp_presence after the heads (A/B)
+#endif
 constexpr int HD_PS = 17, HD_D = 3, HD_NB = 8;
+constexpr int SP_MG_CHUNKS = 32;  // presence-mask chunks per (frame, head): k_sp_presence's split
 // FULL: every frame whole blocks (H W % 32 == 0), every workgroup HD_NB of them and out 4-B
 // aligned -- no lane or block guards, so the loads stay in flight (a load under a branch is sunk
 // to its use, a store under one makes the compiler wait for every outstanding load at the join);
 // otherwise the guarded form.
-template <int OMODE, int NCB, bool FULL>
+// PRES (OMODE 1, FULL, frames of >= HD_NB blocks: a workgroup spans at most 2 frames): run()'s
+// presence mask of the head's codes (k_sp_presence's work) from the epilogue -- each code marks
+// a word of an LDS "seen" array per frame, ORed at the end into chunk 0 of pres[frame][head]
+// (zeroed by the launcher) with vector atomics.
+template <int OMODE, int NCB, bool FULL, bool PRES = false>
 __global__ __launch_bounds__(SP_NT, 2) void k_sp_head(const int8_t *__restrict__ in, int H, int W, int nblk_f,
                                                       int nblk, const i32x4 *__restrict__ wf,
                                                       const int *__restrict__ bq, float rs,
-                                                      int8_t *__restrict__ out, int cstride, float dq) {
+                                                      int8_t *__restrict__ out, int cstride, float dq,
+                                                      unsigned *__restrict__ pres) {
     constexpr int CBW = (NCB + 3) / 4, NS = 8;
     constexpr bool STAGE = OMODE == 1 && NCB * 32 < 128;  // the semi head: 65-byte cells
+    static_assert(!PRES || (OMODE == 1 && FULL), "presence from the int8 heads' full form");
     __shared__ i32x4 tile[2][32 * HD_PS];
     __shared__ int stg[STAGE ? 2 : 1][STAGE ? 32 * 65 / 4 + 1 : 1];
+    __shared__ int seen[PRES ? 2 : 1][PRES ? 256 : 1];  // per frame slot: code + 128 present
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, fr = lane & 31, fh = lane >> 5;
     const int HW = H * W;
     const int kb = blockIdx.x * HD_NB, nmine = min(HD_NB, nblk - kb);
@@ -819,6 +852,10 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_head(const int8_t *__restrict__
         for (int o = t; o < nb; o += SP_NT) gd[o] = ls[o];
     };
     const int lo = SP_MAGIC_BITS - 128;  // the heads have no relu
+    if (PRES) {
+        seen[0][t] = 0;
+        seen[1][t] = 0;  // ordered before the marks by the first block's barrier
+    }
 #pragma unroll
     for (int j = 0; j < HD_NB; j++) {
         if (!FULL && j >= nmine) break;  // workgroup-uniform
@@ -862,6 +899,12 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_head(const int8_t *__restrict__
                 } else {
                     dw[qq] = pack4b(v[0], v[1], v[2], v[3]);
                 }
+                if constexpr (PRES) {  // the code's low byte + 128 (the magic's low byte is 0)
+                    int *sn = seen[fb[j] - fb[0]];
+#pragma unroll
+                    for (int e = 0; e < 4; e++)
+                        if (NCB * 32 == 256 || co + e < cstride) sn[(v[e] + 128) & 255] = 1;
+                }
             }
             if constexpr (OMODE == 1 && !STAGE) {  // channels 32 cb + 16 fh .. + 15 per lane
                 if (inside)
@@ -870,9 +913,19 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_head(const int8_t *__restrict__
             }
         }
     }
-    if (STAGE) {
-        __syncthreads();
-        stage_out(nmine - 1);
+    if (STAGE || PRES) __syncthreads();
+    if (STAGE) stage_out(nmine - 1);
+    if (PRES && w < 2) {  // wave w: frame slot w (slot 1 only when the workgroup reaches the next frame)
+        const int b = fb[0] + w;
+        if (b <= fb[HD_NB - 1]) {
+            unsigned *pw = pres + (size_t)(b * 2 + (NCB == 8 ? 1 : 0)) * SP_MG_CHUNKS * 8;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {  // codes 64 k .. 64 k + 63: words 2 k, 2 k + 1
+                const unsigned long long bm = __ballot(seen[w][64 * k + lane] != 0);
+                if (lane < 2 && (unsigned)(bm >> (32 * lane)) != 0u)
+                    atomicOr(pw + 2 * k + lane, (unsigned)(bm >> (32 * lane)));
+            }
+        }
     }
 }
 
@@ -883,7 +936,6 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_head(const int8_t *__restrict__
 // ORs a head's chunk masks, derives the smallest
 // gap between present dequantised codes (every workgroup, from the same mask) and rounds its
 // chunk to that step in place.
-constexpr int SP_MG_CHUNKS = 32;
 
 __device__ __forceinline__ void sp_head(int8_t *semi, int8_t *desc, long cells, int b, int h, int8_t *&base, long &lo,
                                         long &hi) {
@@ -1106,7 +1158,8 @@ int launch_conv1x1(hipStream_t st, const mv_superpoint *net, int li, int B, int 
 // the heads through k_sp_head (SP_HEAD) or k_sp_conv1x1
 template <int OMODE>
 int launch_head(hipStream_t st, const mv_superpoint *net, int li, int B, int H, int W, const int8_t *in, int8_t *out,
-                int cstride, float dq = 0.f) {
+                int cstride, float dq = 0.f, unsigned *pres = nullptr, bool *pres_done = nullptr) {
+    if (pres_done) *pres_done = false;
     if (!SP_HEAD) return launch_conv1x1<OMODE>(st, net, li, B, H, W, in, out, cstride, dq);
     const int HW = H * W, nblk_f = (HW + 31) / 32;
     const long nblk = (long)B * nblk_f;
@@ -1117,22 +1170,28 @@ int launch_head(hipStream_t st, const mv_superpoint *net, int li, int B, int H, 
     const i32x4 *wf = reinterpret_cast<const i32x4 *>(wd + net->frag_off[li]);
     const int *bq = reinterpret_cast<const int *>(wd + net->bq_off[li]);
     const bool full = HW % 32 == 0 && nblk % HD_NB == 0 && ((uintptr_t)out & 3) == 0;
-#define MV_HEAD(NCB, FULL)                                                                                      \
-    hipLaunchKernelGGL((k_sp_head<OMODE, NCB, FULL>), dim3(grid), dim3(SP_NT), 0, st, in, H, W, nblk_f, (int)nblk, \
-                       wf, bq, net->rs[li], out, cstride, dq)
+    const bool fuse = OMODE == 1 && pres && full && nblk_f >= HD_NB && SP_HEAD_PRES;
+#define MV_HEAD(NCB, FULL, PRES)                                                                                   \
+    hipLaunchKernelGGL((k_sp_head<OMODE, NCB, FULL, PRES>), dim3(grid), dim3(SP_NT), 0, st, in, H, W, nblk_f,         \
+                       (int)nblk, wf, bq, net->rs[li], out, cstride, dq, pres)
     if (cstride == 65) {
-        if (full)
-            MV_HEAD(3, true);
+        if (fuse)
+            MV_HEAD(3, true, OMODE == 1);
+        else if (full)
+            MV_HEAD(3, true, false);
         else
-            MV_HEAD(3, false);
+            MV_HEAD(3, false, false);
     } else {
-        if (full)
-            MV_HEAD(8, true);
+        if (fuse)
+            MV_HEAD(8, true, OMODE == 1);
+        else if (full)
+            MV_HEAD(8, true, false);
         else
-            MV_HEAD(8, false);
+            MV_HEAD(8, false, false);
     }
 #undef MV_HEAD
     MV_LAUNCH_CHECK();
+    if (pres_done) *pres_done = fuse;
     return MV_OK;
 }
 
@@ -1269,7 +1328,9 @@ namespace {
 // dequantised NCHW float32 outputs (run()'s net.forward); act: the two activation buffers of
 // a_bytes each
 int sp_network(hipStream_t st, mv_superpoint *net, int batch, int H, int W, int oh, int ow, const uint8_t *images,
-               int8_t *A, int8_t *Bf, int8_t *semi, int8_t *desc, float *semi_f = nullptr, float *desc_f = nullptr) {
+               int8_t *A, int8_t *Bf, int8_t *semi, int8_t *desc, float *semi_f = nullptr, float *desc_f = nullptr,
+               unsigned *pres = nullptr, bool *pres_done = nullptr) {
+    if (pres_done) *pres_done = false;
     const char *wd = static_cast<const char *>(net->wdev);
     int r;
     int h = oh, w = ow;
@@ -1299,17 +1360,22 @@ int sp_network(hipStream_t st, mv_superpoint *net, int batch, int H, int W, int 
     if ((r = launch_conv_geo<128, 3, false, true, 0>(st, net, 7, batch, h, w, A, Bf, 128)) != MV_OK) return r;
     // heads: Bf holds the shared encoder output
     if ((r = launch_conv_geo<128, 3, false, true, 0>(st, net, 8, batch, h, w, Bf, A, 256)) != MV_OK) return r;
+    bool pd0 = false, pd1 = false;
+    if (pres && !semi_f) {  // the heads OR into chunk 0 of each (frame, head): the rest stays zero
+        MV_HIP_TRY(hipMemsetAsync(pres, 0, (size_t)batch * 2 * SP_MG_CHUNKS * 8 * sizeof(unsigned), st));
+    }
     if (semi_f)
         r = launch_head<2>(st, net, 9, batch, h, w, A, reinterpret_cast<int8_t *>(semi_f), 65, net->dq_semi);
     else
-        r = launch_head<1>(st, net, 9, batch, h, w, A, semi, 65);
+        r = launch_head<1>(st, net, 9, batch, h, w, A, semi, 65, 0.f, pres, &pd0);
     if (r != MV_OK) return r;
     if ((r = launch_conv_geo<128, 3, false, true, 0>(st, net, 10, batch, h, w, Bf, A, 256)) != MV_OK) return r;
     if (desc_f)
         r = launch_head<2>(st, net, 11, batch, h, w, A, reinterpret_cast<int8_t *>(desc_f), 256, net->dq_desc);
     else
-        r = launch_head<1>(st, net, 11, batch, h, w, A, desc, 256);
+        r = launch_head<1>(st, net, 11, batch, h, w, A, desc, 256, 0.f, pres, &pd1);
     if (r != MV_OK) return r;
+    if (pres_done) *pres_done = pd0 && pd1;  // the same geometry: both or neither
     MV_PROF_END(st);
     return MV_OK;
 }
@@ -1348,13 +1414,18 @@ extern "C" int mv_superpoint_forward_dev(mv_context *ctx, mv_superpoint *net, in
     // the activations belong to the net, not the context: order this forward after the previous
     // one on whatever stream (context) it ran (free on the same stream)
     if (net->used) MV_HIP_TRY(hipStreamWaitEvent(st, net->done, 0));
-    if ((r = sp_network(st, net, batch, H, W, oh, ow, images, A, Bf, semi, desc)) != MV_OK) return r;
+    unsigned *pres = reinterpret_cast<unsigned *>(Bf + a_bytes);
+    bool pres_done = false;
+    if ((r = sp_network(st, net, batch, H, W, oh, ow, images, A, Bf, semi, desc, nullptr, nullptr, pres, &pres_done)) !=
+        MV_OK)
+        return r;
     const int h = oh / 8, w = ow / 8;
     MV_PROF_BEGIN(st, "k_sp_min_gap");
-    unsigned *pres = reinterpret_cast<unsigned *>(Bf + a_bytes);
-    hipLaunchKernelGGL(k_sp_presence, dim3((unsigned)batch, 2, SP_MG_CHUNKS), dim3(SP_NT), 0, st, semi, desc,
-                       (long)h * w, pres);
-    MV_LAUNCH_CHECK();
+    if (!pres_done) {
+        hipLaunchKernelGGL(k_sp_presence, dim3((unsigned)batch, 2, SP_MG_CHUNKS), dim3(SP_NT), 0, st, semi, desc,
+                           (long)h * w, pres);
+        MV_LAUNCH_CHECK();
+    }
     hipLaunchKernelGGL(k_sp_min_gap, dim3((unsigned)batch, 2, SP_MG_CHUNKS), dim3(SP_NT), 0, st, semi, desc,
                        (long)h * w, net->dq_semi, net->dq_desc, pres, semi_scale, desc_scale);
     MV_LAUNCH_CHECK();
