@@ -42,6 +42,9 @@ constexpr int NMS_T = 1024;  // threads of the per-frame block
 #endif
 static_assert(KP_CH == 2 || KP_CH == 4, "KP_CH");
 constexpr int KP_PLANE_CELLS = 9216;  // cells whose 4 channel planes fit LDS (144 KiB): KITTI 47x155 = 7285
+#ifndef KP_PLANE_CELLS_S
+#define KP_PLANE_CELLS_S 2048  // the small-frame instantiation (0: always the 144 KiB one, A/B)
+#endif
 constexpr int NC_LDS = 8192;  // candidates per frame held in LDS (more: the global per-pixel path)
 constexpr int ROW_LDS = 2048; // heat rows indexed in LDS
 #ifndef KP_NMS_GLOBAL
@@ -638,12 +641,15 @@ template <int CH>
 struct KpCh {
     float v[CH];
 };
-template <int CH>
+// CELLS: the LDS capacity in cells -- KP_PLANE_CELLS (one 144 KiB workgroup per CU) or
+// KP_PLANE_CELLS_S for frames of at most that many cells (the network at 192 x 640: 24 x 80 =
+// 1920 cells, 32 KiB: several workgroups per CU, whose copies and samples overlap)
+template <int CH, int CELLS>
 __global__ __launch_bounds__(256) void k_kp_sample_planes(int B, int cap, int Hc, int Wc, int H, int W, int Wh,
                                                           const int *__restrict__ num_kp,
                                                           const int *__restrict__ slot_pix,
                                                           const float *__restrict__ coarse, float *__restrict__ desc) {
-    __shared__ __attribute__((aligned(16))) float plf[CH * KP_PLANE_CELLS + 4];
+    __shared__ __attribute__((aligned(16))) float plf[CH * CELLS + 4];
     constexpr int LG = 32 / CH;  // workgroups whose pieces share a 128-B line of a row
     const int i = blockIdx.x, xcd = i & 7, k = i >> 3;
     const int G = xcd + 8 * (k / LG);  // (frame, line group)
@@ -777,8 +783,13 @@ extern "C" int mv_keypoints_dev(mv_context *ctx, const mv_kp_params *p, int batc
     const long waves = (long)batch * cap;
     if (kp_planes_path(Hc, Wc)) {
         MV_PROF_BEGIN(s, "k_kp_sample_planes");
-        hipLaunchKernelGGL(k_kp_sample_planes<KP_CH>, dim3((unsigned)batch * (256 / KP_CH)), dim3(256), 0, s, batch,
-                           cap, Hc, Wc, H, W, Wc * 8, num_kp, m.slot_pix, coarse_desc, desc);
+        if (KP_PLANE_CELLS_S && HW <= KP_PLANE_CELLS_S)
+            hipLaunchKernelGGL((k_kp_sample_planes<KP_CH, (KP_PLANE_CELLS_S ? KP_PLANE_CELLS_S : 1)>),
+                               dim3((unsigned)batch * (256 / KP_CH)), dim3(256), 0, s, batch, cap, Hc, Wc, H, W, Wc * 8,
+                               num_kp, m.slot_pix, coarse_desc, desc);
+        else
+            hipLaunchKernelGGL((k_kp_sample_planes<KP_CH, KP_PLANE_CELLS>), dim3((unsigned)batch * (256 / KP_CH)),
+                               dim3(256), 0, s, batch, cap, Hc, Wc, H, W, Wc * 8, num_kp, m.slot_pix, coarse_desc, desc);
         MV_PROF_END(s);
         MV_LAUNCH_CHECK();
         MV_PROF_BEGIN(s, "k_kp_normalize");
