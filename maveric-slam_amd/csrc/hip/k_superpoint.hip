@@ -157,6 +157,12 @@ __global__ __launch_bounds__(256) void k_sp_resize_q(const uint8_t *__restrict__
 #ifndef SP_KSB
 #define SP_KSB 1  // a scheduling barrier after each k32 step of k_sp_conv's K loop (0: free scheduling, A/B)
 #endif
+#ifndef SP_LIF64
+#define SP_LIF64 8  // the 64-channel layers' 16-B tile loads in flight per thread (A/B)
+#endif
+#ifndef SP_PRIO
+#define SP_PRIO 0  // 1: s_setprio 1 over k_sp_conv's K loop (A/B)
+#endif
 #ifndef SP_BPF
 #define SP_BPF 0  // 1: k_sp_conv's B fragments one k32 step ahead (A/B)
 #endif
@@ -360,7 +366,7 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
     // of 8 pixels instead -- conflict-free LDS stores -- made the 64-channel layers 3-4x slower:
     // the loads must stay lane-contiguous)
     const int8_t *src = in + (size_t)b * H * W * CIN;
-    constexpr int LIF = 8;  // 16-B loads in flight per thread (12 / 16 measured the same)
+    constexpr int LIF = CIN == 64 ? SP_LIF64 : 8;  // 16-B loads in flight per thread (12 / 16 measured the same)
     for (int i0 = 0; i0 < (FUSE1A ? 0 : NCHUNK); i0 += LIF * SP_NT) {
         i32x4 v[LIF];
 #pragma unroll
@@ -403,6 +409,7 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
         const int off = ((RB * j + ky) * IX + kx) * PS;
         return PADL ? lb[off + c0] : lb[off + (c0 ^ xs[kx])];
     };
+    if (SP_PRIO) __builtin_amdgcn_s_setprio(1);  // the K loop ahead of co-resident waves' VALU phases
     constexpr bool BPF = SP_BPF && (CIN != 64 || SP_OCC64 <= 2);  // the 3-per-CU 64-channel build has no room
     i32x4 bn[JN];
     if (BPF) {
@@ -430,6 +437,7 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
         if (SP_KSB) __builtin_amdgcn_sched_barrier(0);
     }
 
+    if (SP_PRIO) __builtin_amdgcn_s_setprio(0);
     // ---- epilogue: lane = pixel fr of each row; 16 couts (4 groups of 4) per 32-cout block ----
     const int lo = SP_MAGIC_BITS + (RELU ? 0 : -128);
     if constexpr (CIN == 64) {
