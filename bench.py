@@ -817,10 +817,16 @@ def main():
         r = bench_superpoint.run(batch=64, steps=args.extra_steps, warmup=2, check=1)
         out["superpoint"] = {k: r[k] for k in ("metric", "value", "unit", "batch", "ms_per_step", "stages_ms",
                                                 "mfma_roofline", "oracle_exact")}
-        # the fp32 path of pairwise_pnp.py:577-694 from 8-bit frames to poses (SURVEY 8(f)1 + 2)
-        import bench_image_pose
-
-        r = bench_image_pose.run(frames=257, steps=args.extra_steps, warmup=2, check=1)
+        # the fp32 path of pairwise_pnp.py:577-694 from 8-bit frames to poses (SURVEY 8(f)1 + 2), in
+        # a child process of its own: run inside this one, after the lines above, the same
+        # two-stream chain measured 69-74 k pairs/s against 77-79 k alone (same stage times; no
+        # single earlier line reproduced it: tools/dbg_ip_queues.py), so it is timed as a user runs it
+        cp = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "bench_image_pose.py"), "--frames", "257",
+                             "--steps", str(args.extra_steps), "--warmup", "2", "--check", "1"],
+                            capture_output=True, text=True, timeout=300)
+        if cp.returncode != 0:
+            raise RuntimeError("bench_image_pose.py failed (%d): %s" % (cp.returncode, cp.stderr[-2000:]))
+        r = json.loads([ln for ln in cp.stdout.splitlines() if ln.startswith("{")][-1])
         out["image_to_pose"] = {k: r[k] for k in ("metric", "value", "unit", "frames_per_step", "pipelines", "ms_per_step",
                                                    "stages_ms_per_step", "keypoints_per_frame", "matches_per_pair",
                                                    "pose_ok", "checked_pairs")}
