@@ -41,7 +41,6 @@ struct mv_superpoint {
     size_t act_bytes;
     hipEvent_t done;      // recorded after each forward on its stream: the buffers' last use
     bool used;
-    int cus;              // compute units of the device (k_sp_conv1p: one workgroup each)
 };
 
 namespace {
@@ -591,381 +590,6 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
                 }
             }
         }
-    }
-}
-
-// conv1 as ONE persistent workgroup per CU with split roles (SP_CONV1P): the fused
-// conv1a + relu + conv1b + relu + 2 x 2 pool of k_sp_conv<64, 3, true, true, 0, true> -- the
-// same arithmetic, bit for bit -- but tile i + 1's resize and conv1a (VALU, image gathers) run
-// on four "producer" waves while four "consumer" waves multiply tile i on the matrix cores
-// (k_sp_conv's 3 independent workgroups per CU overlapped them only by chance: MFMA busy 0.46
-// of the SIMDs' cycles, profiles/r05q_superpoint_summary.json).  Waves w and w + 4 share SIMD
-// w: consumer w (output rows 4 w .. 4 w + 3 of the 16 x 32 tile) and producer w.
-//  - double-buffered input tile in LDS (the padded 5-chunk layout of k_sp_conv's 64-channel
-//    tiles); one workgroup barrier per tile: the consumer has finished tile i's reads and the
-//    producer tile i + 1's writes;
-//  - a producer wave owns conv1a rows C1P_R[w] .. C1P_R[w + 1] of the 18-row tile + halo and
-//    resizes, into its own LDS rows, the image rows that window needs (2 halo rows computed twice
-//    by neighbouring waves): no barrier inside the producer phase;
-//  - the consumer's weight fragments stream through a ring of 3 steps that wraps into the next
-//    tile's first steps (18 k32 steps = 6 rounds of 3), its B fragments one step ahead, and its
-//    pooled outputs leave through its own 2 KiB of LDS staging.
-#ifndef C1P_TRACE
-#define C1P_TRACE 0  // printf k_sp_conv1p's per-role work / barrier-wait cycles of workgroup 0 (timing only)
-#endif
-#ifndef SP_CONV1P
-#define SP_CONV1P 0  // 1: the split-role persistent conv1 (measured slower: profiles/r05ae_sp_conv1p_split_roles.log)
-#endif
-constexpr int C1P_TY = 16, C1P_TX = 32, C1P_IY = 18, C1P_IX = 34, C1P_PS = 5, C1P_QX = 36, C1P_QXS = 38;
-#ifndef C1P_NP
-#define C1P_NP 4  // producer waves: 4 (one per SIMD) or 8 (two per SIMD; 12-wave workgroup, <= 170 VGPRs)
-#endif
-constexpr int C1P_NS = 18, C1P_PF = C1P_NP == 8 ? 2 : 3, C1P_QR = C1P_NP == 8 ? 5 : 7;
-constexpr bool C1P_BPF = C1P_NP != 8;  // the consumer's B fragments a step ahead (register room)
-constexpr int C1P_NT = 256 + 64 * C1P_NP;
-#ifndef C1P_DBG
-#define C1P_DBG 0  // timing experiments only (wrong results): 1 consumers alone, 2 producers alone
-#endif
-#ifndef C1P_PPRIO
-#define C1P_PPRIO 0  // 1: s_setprio 3 over the producer's conv1a MFMA issue (A/B)
-#endif
-#ifndef C1P_GB
-#define C1P_GB 3  // conv1a blocks of 32 pixels in flight per producer wave
-#endif  // k32 steps; weight ring; resized rows per producer
-__constant__ int C1P_R[C1P_NP + 1] = {
-#if C1P_NP == 8
-    0, 3, 5, 7, 9, 12, 14, 16, 18
-#else
-    0, 5, 10, 14, 18
-#endif
-};
-__global__ __launch_bounds__(C1P_NT, C1P_NP == 8 ? 3 : 2) void k_sp_conv1p(int B, int H, int W, int tiles_x, int tiles_y,
-                                                      const i32x4 *__restrict__ wf, const int *__restrict__ bq,
-                                                      float rs, int8_t *__restrict__ out, Conv1aArgs c1) {
-    constexpr int TY = C1P_TY, TX = C1P_TX, IY = C1P_IY, IX = C1P_IX, PS = C1P_PS, QX = C1P_QX, QXS = C1P_QXS;
-    constexpr int NS = C1P_NS, PF = C1P_PF, PB = 64;
-    static_assert(NS % PF == 0, "the weight ring wraps onto the next tile");
-    __shared__ i32x4 tile[2][IY * IX * PS];
-    __shared__ __attribute__((aligned(16))) char stg[4][2 * 16 * PB];
-    __shared__ int8_t qim[C1P_NP][C1P_QR * QXS];
-    __shared__ float4 rowc[2][C1P_NP][C1P_QR], colc[2][C1P_NP][QX];
-    __shared__ float lut[256];
-    const int t = threadIdx.x, lane = t & 63, w = (t >> 6) & 3, fr = lane & 31, fh = lane >> 5;
-    const bool consumer = t < 256;
-    const int pw = consumer ? 0 : (t - 256) >> 6;  // producer wave index
-    const long ntiles = (long)B * tiles_y * tiles_x;
-    if (t < 256) lut[t] = (float)t / 255.0f;
-    auto tile_at = [&](long k, int &b, int &y0, int &x0) {
-        const int tx = (int)(k % tiles_x);
-        const long r = k / tiles_x;
-        y0 = (int)(r % tiles_y) * TY;
-        x0 = tx * TX;
-        b = (int)(r / tiles_y);
-    };
-    auto chunk_at = [&](int px, int c) { return px * PS + c; };
-
-    // the two roles in separate branches, each with its own registers and loop, the same number
-    // of workgroup barriers in each: one after the first tile's build, one per tile
-    const long k0 = blockIdx.x;
-    if (k0 >= ntiles) return;  // workgroup-uniform
-    __syncthreads();  // lut
-    if (consumer) {
-    // ---- consumer state: the weight ring and the bias (each chain's first C operand) ----
-    const i32x4 *wa = wf + lane, *wb = wa + NS * 64;
-    i32x4 ra[PF], rb[PF];
-#pragma unroll
-    for (int u = 0; u < PF; u++) {
-        ra[u] = wa[u * 64];
-        rb[u] = wb[u * 64];
-    }
-    const int lo = SP_MAGIC_BITS;  // relu
-    auto consume = [&](long k, const i32x4 *tb) {
-        int b, y0, x0;
-        tile_at(k, b, y0, x0);
-        const i32x4 *lb = tb + (4 * w * IX + fr) * PS + fh;
-        // the weight and bias addresses made opaque per tile: invariant across tiles, the compiler
-        // would otherwise hoist all 36 fragment loads out of the tile loop (288 live VGPRs)
-        int wz = 0;
-        asm volatile("" : "+s"(wz));
-        const i32x4 *wat = wa + wz, *wbt = wb + wz;
-        const int *bqt = bq + wz;
-        i32x16 b0, b1;  // the bias, each chain's first C operand (reloaded per tile: registers)
-#pragma unroll
-        for (int qq = 0; qq < 4; qq++) {
-            const i32x4 u0 = *reinterpret_cast<const i32x4 *>(bqt + 8 * qq + 4 * fh);
-            const i32x4 u1 = *reinterpret_cast<const i32x4 *>(bqt + 32 + 8 * qq + 4 * fh);
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                b0[4 * qq + e] = u0[e];
-                b1[4 * qq + e] = u1[e];
-            }
-        }
-        auto bfrag = [&](int s, int j) {
-            const int tap = s * 32 / 64, ky = tap / 3, kx = tap % 3, c0 = (s * 32 % 64) / 16;
-            return lb[((j + ky) * IX + kx) * PS + c0];
-        };
-        i32x16 acc[4][2];
-        i32x4 bn[4];
-        if (C1P_BPF) {
-#pragma unroll
-            for (int j = 0; j < 4; j++) bn[j] = bfrag(0, j);
-        }
-#pragma unroll
-        for (int s = 0; s < NS; s++) {
-            const i32x4 a0 = ra[s % PF], a1 = rb[s % PF];
-            const int sn = (s + PF) % NS;  // past the last step: the next tile's first ones
-            ra[s % PF] = wat[sn * 64];
-            rb[s % PF] = wbt[sn * 64];
-            i32x4 bc[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                if (C1P_BPF) {
-                    bc[j] = bn[j];
-                    if (s + 1 < NS) bn[j] = bfrag(s + 1, j);
-                } else {
-                    bc[j] = bfrag(s, j);
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                acc[j][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bc[j], s == 0 ? b0 : acc[j][0], 0, 0, 0);
-                acc[j][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bc[j], s == 0 ? b1 : acc[j][1], 0, 0, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        // pooled epilogue (k_sp_conv's FUSE1A form) through this wave's own staging rows
-        char *sg = stg[w];
-        const int Ho = H / 2, Wo = W / 2;
-#pragma unroll
-        for (int jp = 0; jp < 2; jp++) {
-            const int cbx = fr & 1;
-            int m[16];
-#pragma unroll
-            for (int q = 0; q < 16; q++) {
-                int v0 = max(acc[2 * jp][0][q], acc[2 * jp + 1][0][q]);
-                int v1 = max(acc[2 * jp][1][q], acc[2 * jp + 1][1][q]);
-                v0 = max(v0, __builtin_amdgcn_update_dpp(0, v0, 0xB1, 0xF, 0xF, false));  // lane ^ 1
-                v1 = max(v1, __builtin_amdgcn_update_dpp(0, v1, 0xB1, 0xF, 0xF, false));
-                m[q] = cbx ? v1 : v0;
-            }
-            int dw[4];
-#pragma unroll
-            for (int qq = 0; qq < 4; qq++) {
-                int v[4];
-                requant4(v, m[4 * qq], m[4 * qq + 1], m[4 * qq + 2], m[4 * qq + 3], rs, lo);
-                dw[qq] = pack4b(v[0], v[1], v[2], v[3]);
-            }
-            const int pa = (fr >> 1) * PB + (((2 * cbx + fh + (fr >> 2)) & 3) << 4);
-            *reinterpret_cast<i32x4 *>(sg + jp * 16 * PB + pa) = regroup16(dw);
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_wave_barrier();
-        const int ra_ = (lane >> 2) * PB + ((((lane & 3) + (lane >> 3)) & 3) << 4);
-#pragma unroll
-        for (int jp = 0; jp < 2; jp++) {
-            const int p = lane >> 2, kk = lane & 3;  // 16 pooled pixels x 4 chunks
-            const int gy = y0 + 4 * w + 2 * jp, gx = x0 + 2 * p;
-            const i32x4 v = *reinterpret_cast<const i32x4 *>(sg + jp * 16 * PB + ra_);
-            if (gy < H && gx < W)
-                *reinterpret_cast<i32x4 *>(out + (((size_t)b * Ho + gy / 2) * Wo + gx / 2) * 64 + 16 * kk) = v;
-        }
-    };
-
-        __syncthreads();
-        long long tw = 0, tc = 0;  // C1P_TRACE: cycles in consume / waiting at the barrier
-        for (long k = k0;; k += gridDim.x) {
-            const long long c0 = C1P_TRACE ? (long long)clock64() : 0;
-            if (C1P_DBG != 2) consume(k, tile[((k - k0) / gridDim.x) & 1]);  // C1P_DBG 2: producers alone (timing)
-            else if (tile[((k - k0) / gridDim.x) & 1][t][0] == 0x7fffffff) out[t] = 1;  // keeps the tile live
-            const long long c1_ = C1P_TRACE ? (long long)clock64() : 0;
-            __syncthreads();  // tile i read (and this wave's staging reads done), tile i + 1 written
-            if (C1P_TRACE) {
-                tc += c1_ - c0;
-                tw += (long long)clock64() - c1_;
-            }
-            if (k + gridDim.x >= ntiles) break;
-        }
-        if (C1P_TRACE && blockIdx.x == 0 && lane == 0) printf("conv1p consumer wave %d: work %lld wait %lld\n", w, tc, tw);
-    } else {
-    // ---- producer state: conv1a weights (f16 A operand) and biases, once ----
-    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-    typedef float f32x16 __attribute__((ext_vector_type(16)));
-    h8 a1c[2];
-    f32x16 bias1[2];
-    const int R0 = C1P_R[pw], R1 = C1P_R[pw + 1], NQR = R1 - R0 + 2;
-    {
-#pragma unroll
-        for (int cb = 0; cb < 2; cb++) {
-            const int co = 32 * cb + fr;
-            const unsigned lo = (unsigned)(fh ? c1.wpk[3 * co + 2] : c1.wpk[3 * co]);
-            const unsigned hi = fh ? 0u : (unsigned)c1.wpk[3 * co + 1];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                a1c[cb][k] = (_Float16)(float)(((int)(lo << (24 - 8 * k))) >> 24);
-                a1c[cb][4 + k] = (_Float16)(float)(((int)(hi << (24 - 8 * k))) >> 24);
-            }
-#pragma unroll
-            for (int q = 0; q < 16; q++) bias1[cb][q] = (float)c1.bq[32 * cb + (q & 3) + 8 * (q >> 2) + 4 * fh];
-        }
-    }
-    // tile k's resize + conv1a into tb (producer wave w: conv1a rows R0 .. R1 - 1), in three
-    // pieces so that the NEXT tile's image gathers are in flight during this tile's conv1a:
-    // geometry + gathers (into g4, bilinear rows / columns into parity par of rowc / colc),
-    // resize (g4 -> this wave's qim rows), conv1a (qim -> the tile)
-    long long t_rs = 0, t_ca = 0;  // C1P_TRACE: resize / conv1a cycles
-    constexpr int NQ = (C1P_QR * QX + 63) / 64;
-    uint8_t g4[NQ][4];
-    auto gather = [&](long k, int par) {
-        int b, y0, x0;
-        tile_at(k, b, y0, x0);
-        const float sy = (float)c1.H / (float)H, sx = (float)c1.W / (float)W;
-        if (lane < QX) {
-            int xa, xb;
-            const float w1 = sp_src(sx, min(max(x0 + lane - 2, 0), W - 1), c1.W, xa, xb);
-            colc[par][pw][lane] = make_float4(w1, 1.f - w1, __int_as_float(xa), __int_as_float(xb));
-        } else if (lane >= 40 && lane < 40 + NQR) {  // image rows y0 + R0 - 2 + i
-            int ya, yb;
-            const float h1 = sp_src(sy, min(max(y0 + R0 + (lane - 40) - 2, 0), H - 1), c1.H, ya, yb);
-            rowc[par][pw][lane - 40] = make_float4(h1, 1.f - h1, __int_as_float(ya * c1.W), __int_as_float(yb * c1.W));
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-        __builtin_amdgcn_wave_barrier();
-        const uint8_t *im = c1.img + (size_t)b * c1.H * c1.W;
-#pragma unroll
-        for (int u = 0; u < NQ; u++) {  // every gather in flight before any is used
-            const int i = min(lane + 64 * u, NQR * QX - 1), r = i / QX, c = i % QX;
-            const float4 rc = rowc[par][pw][r], cc = colc[par][pw][c];
-            const int ra = __float_as_int(rc.z), rb = __float_as_int(rc.w);
-            const int xa = __float_as_int(cc.z), xb = __float_as_int(cc.w);
-            g4[u][0] = im[ra + xa];
-            g4[u][1] = im[ra + xb];
-            g4[u][2] = im[rb + xa];
-            g4[u][3] = im[rb + xb];
-        }
-    };
-    auto resize = [&](long k, int par) {
-        int b, y0, x0;
-        tile_at(k, b, y0, x0);
-#pragma unroll
-        for (int u = 0; u < NQ; u++) {
-            const int i = lane + 64 * u;
-            if (i >= NQR * QX) break;
-            const int r = i / QX, c = i % QX;
-            const int gy = y0 + R0 + r - 2, gx = x0 + c - 2;
-            int v = 0;
-            if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
-                const float4 rc = rowc[par][pw][r], cc = colc[par][pw][c];
-                const float h1 = rc.x, h0 = rc.y, w1 = cc.x, w0 = cc.y;
-                const float a00 = lut[g4[u][0]], a01 = lut[g4[u][1]];
-                const float a10 = lut[g4[u][2]], a11 = lut[g4[u][3]];
-                const float t0 = __builtin_fmaf(a00, w0, a01 * w1);
-                const float t1 = __builtin_fmaf(a10, w0, a11 * w1);
-                const float x = __builtin_fmaf(t0, h0, t1 * h1);
-                float qv = __builtin_rintf(x * c1.in_inv);
-                qv = fminf(fmaxf(qv, -128.f), 127.f);
-                v = (int)qv;
-            }
-            qim[pw][r * QXS + c] = (int8_t)v;
-        }
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_wave_barrier();
-    };
-    auto conv1a = [&](long k, i32x4 *tb) {
-        int b, y0, x0;
-        tile_at(k, b, y0, x0);
-        // conv1a + relu over rows R0 .. R1 - 1 of the tile + halo (k_sp_conv's FUSE1A form), three
-        // 32-pixel blocks at a time (their LDS reads, then their 6 MFMAs, then their requantisation:
-        // one block at a time left this single wave latency-bound)
-        const int npx = (R1 - R0) * IX;
-        constexpr int GB = C1P_GB;
-#pragma unroll 1
-        for (int j0 = 0; j0 < npx; j0 += 32 * GB) {
-            h8 bv[GB];
-            int pxs[GB], jls[GB];
-            bool ins[GB];
-#pragma unroll
-            for (int u = 0; u < GB; u++) {
-                const int jl = j0 + 32 * u + fr, jc = min(jl, npx - 1);
-                const int r = R0 + jc / IX, x = jc % IX;
-                const int8_t *q0 = qim[pw] + (r - R0) * QXS + x;
-                const int gy = y0 + r - 1, gx = x0 + x - 1;
-                jls[u] = jl;
-                pxs[u] = r * IX + x;
-                ins[u] = jl < npx && gy >= 0 && gy < H && gx >= 0 && gx < W;
-                if (fh == 0) {
-                    bv[u][0] = (_Float16)(float)q0[0];
-                    bv[u][1] = (_Float16)(float)q0[1];
-                    bv[u][2] = (_Float16)(float)q0[2];
-                    bv[u][3] = (_Float16)(float)q0[QXS];
-                    bv[u][4] = (_Float16)(float)q0[QXS + 1];
-                    bv[u][5] = (_Float16)(float)q0[QXS + 2];
-                    bv[u][6] = (_Float16)(float)q0[2 * QXS];
-                    bv[u][7] = (_Float16)(float)q0[2 * QXS + 1];
-                } else {
-                    bv[u] = h8{};
-                    bv[u][0] = (_Float16)(float)q0[2 * QXS + 2];
-                }
-            }
-            f32x16 d[GB][2];
-            if (C1P_PPRIO) __builtin_amdgcn_s_setprio(3);  // the producer's few MFMAs ahead of the consumer's stream
-#pragma unroll
-            for (int u = 0; u < GB; u++)
-#pragma unroll
-                for (int cb = 0; cb < 2; cb++)
-                    d[u][cb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1c[cb], bv[u], bias1[cb], 0, 0, 0);
-            if (C1P_PPRIO) __builtin_amdgcn_s_setprio(0);
-#pragma unroll
-            for (int u = 0; u < GB; u++)
-#pragma unroll
-                for (int cb = 0; cb < 2; cb++) {
-                    int dw[4];
-#pragma unroll
-                    for (int qq = 0; qq < 4; qq++) {
-                        int v[4];
-#pragma unroll
-                        for (int e = 0; e < 4; e++) v[e] = requant_bitsf(d[u][cb][4 * qq + e], c1.rs, SP_MAGIC_BITS);
-                        dw[qq] = pack4b(v[0], v[1], v[2], v[3]);
-                    }
-                    const i32x4 chunk = regroup16(dw);
-                    if (jls[u] < npx) tb[chunk_at(pxs[u], 2 * cb + fh)] = ins[u] ? chunk : i32x4{0, 0, 0, 0};
-                }
-        }
-    };
-
-        // tile i + 1: resized from the gathers issued during tile i's conv1a, then the gathers of
-        // tile i + 2, then tile i + 1's conv1a
-        const long G = gridDim.x;
-        gather(k0, 0);
-        resize(k0, 0);
-        if (k0 + G < ntiles) gather(k0 + G, 1);
-        conv1a(k0, tile[0]);
-        __syncthreads();
-        long long tw = 0, tc = 0;
-        for (long k = k0;; k += G) {
-            const long kn = k + G;
-            const int in = (int)((kn - k0) / G);  // tile index of kn in this workgroup
-            const long long c0 = C1P_TRACE ? (long long)clock64() : 0;
-            if (kn < ntiles && C1P_DBG != 1) {  // C1P_DBG 1: consumers alone (timing)
-                resize(kn, in & 1);
-                if (kn + G < ntiles) gather(kn + G, (in + 1) & 1);
-                const long long cm = C1P_TRACE ? (long long)clock64() : 0;
-                conv1a(kn, tile[in & 1]);
-                if (C1P_TRACE) {
-                    __builtin_amdgcn_s_waitcnt(0);
-                    t_rs += cm - c0;
-                    t_ca += (long long)clock64() - cm;
-                }
-            }
-            const long long c1_ = C1P_TRACE ? (long long)clock64() : 0;
-            __syncthreads();
-            if (C1P_TRACE) {
-                tc += c1_ - c0;
-                tw += (long long)clock64() - c1_;
-            }
-            if (kn >= ntiles) break;
-        }
-        if (C1P_TRACE && blockIdx.x == 0 && lane == 0)
-            printf("conv1p producer wave %d: work %lld wait %lld (resize %lld conv1a %lld)\n", pw, tc, tw, t_rs, t_ca);
     }
 }
 
@@ -1608,11 +1232,8 @@ extern "C" int mv_superpoint_create(mv_context *ctx, const mv_sp_weights *wt, mv
         MV_REQUIRE(L.w_scale > 0.0 && L.out_scale > 0.0);
     }
     MV_HIP_TRY(hipSetDevice(ctx->device));
-    int cus = 0;
-    MV_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
     mv_superpoint *net = new mv_superpoint();
     net->device = ctx->device;
-    net->cus = cus > 0 ? cus : 1;
     net->in_inv = 1.0f / (float)wt->in_scale;
     net->dq_semi = (float)wt->layer[9].out_scale;
     net->dq_desc = (float)wt->layer[11].out_scale;
@@ -1733,18 +1354,8 @@ int sp_network(hipStream_t st, mv_superpoint *net, int batch, int H, int W, int 
         }
         const Conv1aArgs c1{images, H, W, net->in_inv, net->rs[0], reinterpret_cast<const int *>(wd + net->frag_off[0]),
                             reinterpret_cast<const int *>(wd + net->bq_off[0]), SP_PRERESIZE ? A : nullptr};
-        if (SP_CONV1P && !SP_PRERESIZE) {
-            const int tiles_x = (w + C1P_TX - 1) / C1P_TX, tiles_y = (h + C1P_TY - 1) / C1P_TY;
-            const long ntiles = (long)batch * tiles_y * tiles_x;
-            MV_REQUIRE(net->cout_pad[1] == 64 && ntiles < (1l << 40));
-            const unsigned grid = (unsigned)std::min<long>(ntiles, net->cus);
-            hipLaunchKernelGGL(k_sp_conv1p, dim3(grid), dim3(C1P_NT), 0, st, batch, h, w, tiles_x, tiles_y,
-                               reinterpret_cast<const i32x4 *>(wd + net->frag_off[1]),
-                               reinterpret_cast<const int *>(wd + net->bq_off[1]), net->rs[1], Bf, c1);
-            MV_LAUNCH_CHECK();
-        } else if ((r = launch_conv<64, 3, true, true, 0, true>(st, net, 1, batch, h, w, nullptr, Bf, 64, c1)) != MV_OK) {
+        if ((r = launch_conv<64, 3, true, true, 0, true>(st, net, 1, batch, h, w, nullptr, Bf, 64, c1)) != MV_OK)
             return r;
-        }
     }
     h /= 2, w /= 2;
     if ((r = launch_conv<64, 3, false, true, 0>(st, net, 2, batch, h, w, Bf, A, 64)) != MV_OK) return r;
