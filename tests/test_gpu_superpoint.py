@@ -69,6 +69,20 @@ def test_superpoint_random_frames_vs_oracle(ctx, orc, torch_cuda, sp, weights, s
     _check(orc, weights, imgs, got, oh, ow)
 
 
+@pytest.mark.parametrize("nf,shape,oh,ow", [(4, (64, 64), 64, 64), (8, (96, 128), 64, 128), (3, (200, 300), 192, 224)])
+def test_superpoint_head_block_forms(ctx, orc, torch_cuda, sp, weights, nf, shape, oh, ow):
+    """k_sp_head's forms: whole 32-cell blocks and whole 8-block workgroups (4 x 64 cells: the
+    unguarded form, frames under 8 blocks so the presence pass stays separate; 8 x 128 cells:
+    4 blocks per frame, 2 frames per workgroup) and the guarded form (3 x 672 cells: 21 blocks per
+    frame, 63 blocks, not a whole number of workgroups)"""
+    rng = np.random.default_rng(nf * 1000 + oh)
+    yy, xx = np.mgrid[0:shape[0], 0:shape[1]]
+    imgs = [(127 + 120 * np.sin(xx / (5.0 + k)) * np.cos(yy / (4.0 + k)) + rng.integers(-20, 21, shape)).clip(0, 255)
+            .astype(np.uint8) for k in range(nf)]
+    got = _run(ctx, torch_cuda, sp, imgs, oh, ow)
+    _check(orc, weights, imgs, got, oh, ow)
+
+
 def test_superpoint_flat_frame(ctx, orc, torch_cuda, sp, weights):
     imgs = [np.zeros((64, 64), np.uint8), np.full((64, 64), 255, np.uint8)]
     got = _run(ctx, torch_cuda, sp, imgs, 64, 64)
