@@ -50,7 +50,13 @@ constexpr int ROW_LDS = 2048; // heat rows indexed in LDS
 #ifndef KP_NMS_GLOBAL
 #define KP_NMS_GLOBAL 0  // 1: always the global per-pixel path (the LDS path's timing baseline)
 #endif
-constexpr int HN = 8;        // listed higher-priority neighbours per candidate
+#ifndef KP_HN
+// 16: the 192 x 640 network frames' dense candidates (2.2 % of pixels) rescanned their window
+// every NMS round whenever more than 8 higher neighbours were listed (A/B in DESIGN 4.3)
+#define KP_HN 16
+#endif
+static_assert(KP_HN % 4 == 0, "16-B list pieces");
+constexpr int HN = KP_HN;    // listed higher-priority neighbours per candidate
 constexpr int SORT_N = 4096; // survivors sorted in LDS (more: ranked by counting)
 __host__ __device__ inline long hn_cands(long P) { return (P + 7) / 8; }  // candidates with a list (more: rescanned)
 
@@ -391,9 +397,16 @@ __global__ __launch_bounds__(NMS_T) void k_kp_nms(int Hh, int Wh, int H, int W, 
             bool supp = false, blocked = false;
             const int c = k < HNC ? hcnt[k] : HN + 1;
             if (c <= HN) {
-                int q[HN];
+                int q[HN];  // the list in 16-B pieces (HN * 4 B per candidate: 16-B aligned)
+                const int4 *h4 = reinterpret_cast<const int4 *>(hn + (long)k * HN);
 #pragma unroll
-                for (int i = 0; i < HN; i++) q[i] = i < c ? hn[(long)k * HN + i] : -1;
+                for (int i4 = 0; i4 < HN / 4; i4++) {
+                    const int4 v = 4 * i4 < c ? h4[i4] : make_int4(-1, -1, -1, -1);
+                    q[4 * i4] = 4 * i4 < c ? v.x : -1;
+                    q[4 * i4 + 1] = 4 * i4 + 1 < c ? v.y : -1;
+                    q[4 * i4 + 2] = 4 * i4 + 2 < c ? v.z : -1;
+                    q[4 * i4 + 3] = 4 * i4 + 3 < c ? v.w : -1;
+                }
 #pragma unroll
                 for (int i = 0; i < HN; i++) {
                     if (q[i] < 0) continue;
