@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Which kernel, running concurrently on another stream, changes k_pose_ransac's results?
+Stream A repeats the pose on one fixed track's matches; stream B repeats one other stage
+(SuperPoint network, keypoints, the all-pairs match) on its own buffers.  Every pose result is
+compared with a solo run, bit for bit.  GPU only (diagnosis)."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "maveric-slam_amd"), os.path.join(ROOT, "tools")):
+    sys.path.insert(0, p)
+import mvtrack  # noqa: E402
+import synth  # noqa: E402
+from bench_image_pose import CAP, frames_kitti  # noqa: E402
+
+dev = torch.device("cuda", 0)
+F, P = 257, 256
+W = dict(np.load(os.path.join(ROOT, "tests", "golden", "superpoint_qnonorm.npz")))
+x = torch.from_numpy(np.stack(frames_kitti(F))).to(dev)
+K = synth.KITTI_K
+prm = mvtrack.pose_params(mvtrack.AS_INTENDED, fx=K[0, 0], fy=K[1, 1], cx=K[0, 2], cy=K[1, 2], hypotheses=256,
+                          inlier_thresh=1.0, refine_iters=10, seed=7)
+e = lambda *shape, dt=torch.float32: torch.zeros(shape, dtype=dt, device=dev)  # noqa: E731
+
+
+class Pipe:
+    def __init__(self):
+        self.stream = torch.cuda.Stream(device=dev)
+        self.ctx = mvtrack.Context(0)
+        self.ctx.set_stream(self.stream)
+        self.sp = mvtrack.SuperPoint(self.ctx, W)
+        self.semi, self.cdesc = e(F, 65, 24, 80), e(F, 256, 24, 80)
+        self.nkp, self.kp, self.conf = e(F, dt=torch.int32), e(F, CAP, 2), e(F, CAP)
+        self.desc, self.kst = e(F, CAP, 256), e(F, dt=torch.int32)
+        self.idx = e(P, CAP, dt=torch.int32)
+        self.T, self.nm, self.ni, self.st = e(P, 3, 4), e(P, dt=torch.int32), e(P, dt=torch.int32), e(P, dt=torch.int32)
+
+    def net(self):
+        self.sp.forward_raw(x, 192, 640, out=(self.semi, self.cdesc))
+
+    def kps(self):
+        self.ctx.keypoints(self.semi, self.cdesc, 192, 640, self.nkp, self.kp, self.conf, self.desc, self.kst)
+
+    def match(self):
+        self.ctx.match_allpairs_f32(self.desc[:P], self.desc[1:], self.nkp[:P], self.nkp[1:], self.idx, None, 0.8)
+
+    def pose(self):
+        self.ctx.pose_from_matches(prm, self.nkp[:P], self.idx, self.kp[:P], self.kp[1:], self.T, self.nm, self.ni,
+                                   self.st)
+
+    def all(self):
+        with torch.cuda.stream(self.stream):
+            self.net(), self.kps(), self.match(), self.pose()
+
+
+torch.cuda.synchronize()
+a, b = Pipe(), Pipe()
+a.all(), b.all()
+torch.cuda.synchronize()
+ref = a.T.clone()
+if os.environ.get("OOB"):  # does stream B's stage alone change a's buffers (no pose running on A)?
+    snap = {k: getattr(a, k).clone() for k in ("semi", "cdesc", "nkp", "kp", "desc", "idx", "T", "nm", "ni", "st")}
+    for stage in os.environ.get("STAGES", "net,kps,match,pose").split(","):
+        with torch.cuda.stream(b.stream):
+            for _ in range(3):
+                getattr(b, stage)()
+        torch.cuda.synchronize()
+        changed = [k for k, v in snap.items() if not torch.equal(getattr(a, k), v)]
+        print("stage %-5s alone on B: a's buffers changed: %s" % (stage, changed), flush=True)
+    sys.exit(0)
+for stage in os.environ.get("STAGES", "none,net,kps,match,pose,all").split(","):
+    bad = 0
+    for r in range(int(os.environ.get("ROUNDS", "6"))):
+        with torch.cuda.stream(a.stream):
+            a.pose()
+        with torch.cuda.stream(b.stream):
+            for _ in range(2):
+                if stage == "all":
+                    b.net(), b.kps(), b.match(), b.pose()
+                elif stage != "none":
+                    getattr(b, stage)()
+        with torch.cuda.stream(a.stream):
+            a.pose()
+        torch.cuda.synchronize()
+        d = (a.T - ref).abs().amax(dim=(1, 2))
+        bad += int((d > 0).sum())
+    print("concurrent %-5s: pose pairs differing from the solo run: %d" % (stage, bad), flush=True)
+    if bad and os.environ.get("RERUN"):
+        with torch.cuda.stream(a.stream):
+            a.pose()
+        torch.cuda.synchronize()
+        print("   a.pose() again alone: %d pairs differ" % int(((a.T - ref).abs().amax(dim=(1, 2)) > 0).sum()), flush=True)
