@@ -802,6 +802,9 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
 #pragma unroll
         for (int i = 0; i < 3; i++) tv[i] = s_cand[gid][bc][9 + i];
         tangent_basis_f(tv, bs);
+        // with refine_iters = 0 no Gauss-Newton barrier separates these reads of the start from
+        // thread 0's write of the refined pose into candidate slot 0 below (concurrent schedule)
+        if (a.refine_iters == 0) __syncthreads();
         float csc = th_max;  // the Cauchy scale
         bool act = true;     // this group still iterates (group-uniform)
         for (int it = 0; it < a.refine_iters; it++) {

@@ -21,8 +21,9 @@ F, P = 257, 256
 W = dict(np.load(os.path.join(ROOT, "tests", "golden", "superpoint_qnonorm.npz")))
 x = torch.from_numpy(np.stack(frames_kitti(F))).to(dev)
 K = synth.KITTI_K
-prm = mvtrack.pose_params(mvtrack.AS_INTENDED, fx=K[0, 0], fy=K[1, 1], cx=K[0, 2], cy=K[1, 2], hypotheses=256,
-                          inlier_thresh=1.0, refine_iters=10, seed=7)
+prm = mvtrack.pose_params(mvtrack.AS_INTENDED, fx=K[0, 0], fy=K[1, 1], cx=K[0, 2], cy=K[1, 2],
+                          hypotheses=int(os.environ.get("HYPS", "256")), inlier_thresh=1.0,
+                          refine_iters=int(os.environ.get("REFINE", "10")), seed=7)
 e = lambda *shape, dt=torch.float32: torch.zeros(shape, dtype=dt, device=dev)  # noqa: E731
 
 
@@ -50,6 +51,9 @@ class Pipe:
     def pose(self):
         self.ctx.pose_from_matches(prm, self.nkp[:P], self.idx, self.kp[:P], self.kp[1:], self.T, self.nm, self.ni,
                                    self.st)
+
+    def copy(self):  # a memory-bound torch kernel of the heads' size (126 MB written as fp32)
+        self.cdesc.copy_(self.cdesc * 1.0)
 
     def all(self):
         with torch.cuda.stream(self.stream):
