@@ -52,6 +52,17 @@ class Pipe:
         self.ctx.pose_from_matches(prm, self.nkp[:P], self.idx, self.kp[:P], self.kp[1:], self.T, self.nm, self.ni,
                                    self.st)
 
+    def net8(self):  # the int8 forward: the same layers, heads written as int8 cells (+ run()'s min gap)
+        if not hasattr(self, "o8"):
+            cells = 24 * 80
+            self.o8 = (torch.empty((F, cells, 65), dtype=torch.int8, device=dev),
+                       torch.empty((F, cells, 256), dtype=torch.int8, device=dev),
+                       torch.empty(F, dtype=torch.float32, device=dev), torch.empty(F, dtype=torch.float32, device=dev))
+        self.sp.forward(x, 192, 640, out=self.o8)
+
+    def scat(self):  # fp32 stores scattered over 256 channel planes, as the raw heads write them
+        self.cdesc.view(F, 256, -1).transpose(1, 2).copy_(self.desc.new_ones(F, 1920, 256) * 0.5)
+
     def copy(self):  # a memory-bound torch kernel of the heads' size (126 MB written as fp32)
         self.cdesc.copy_(self.cdesc * 1.0)
 
