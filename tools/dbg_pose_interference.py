@@ -76,6 +76,7 @@ a, b = Pipe(), Pipe()
 a.all(), b.all()
 torch.cuda.synchronize()
 ref = a.T.clone()
+ref_nm = a.nm.clone()
 if os.environ.get("OOB"):  # does stream B's stage alone change a's buffers (no pose running on A)?
     snap = {k: getattr(a, k).clone() for k in ("semi", "cdesc", "nkp", "kp", "desc", "idx", "T", "nm", "ni", "st")}
     for stage in os.environ.get("STAGES", "net,kps,match,pose").split(","):
@@ -102,6 +103,14 @@ for stage in os.environ.get("STAGES", "none,net,kps,match,pose,all").split(","):
         torch.cuda.synchronize()
         d = (a.T - ref).abs().amax(dim=(1, 2))
         bad += int((d > 0).sum())
+        badnm = int((a.nm != ref_nm).sum())
+        if os.environ.get("NM") and badnm:
+            idx_ = torch.nonzero(a.nm != ref_nm).flatten()[:6]
+            got, exp = a.nm[idx_], ref_nm[idx_]
+            if os.environ.get("NM") == "f":
+                got, exp = got.view(torch.float32), exp.view(torch.float32)
+            print("   round %d: num_matches (phase checksum) differs in %d pairs: pairs %s got %s solo %s" % (
+                r, badnm, idx_.tolist(), got.tolist(), exp.tolist()), flush=True)
     print("concurrent %-5s: pose pairs differing from the solo run: %d" % (stage, bad), flush=True)
     if bad and os.environ.get("RERUN"):
         with torch.cuda.stream(a.stream):
