@@ -778,7 +778,10 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv1x1(const int8_t *__restric
 #ifndef SP_HEAD_PRES
 #define SP_HEAD_PRES 1  // 0: the presence masks by k_sp_presence after the heads (A/B)
 #endif
-constexpr int HD_PS = 17, HD_D = 3, HD_NB = 8;
+#ifndef SP_HD_NB
+#define SP_HD_NB 8  // 32-pixel blocks per k_sp_head workgroup (4 / 16 measured 1-2 % slower: profiles/r05ak_sp_head_nb_ab.log)
+#endif
+constexpr int HD_PS = 17, HD_D = 3, HD_NB = SP_HD_NB;
 constexpr int SP_MG_CHUNKS = 32;  // presence-mask chunks per (frame, head): k_sp_presence's split
 // FULL: every frame whole blocks (H W % 32 == 0), every workgroup HD_NB of them and out 4-B
 // aligned -- no lane or block guards, so the loads stay in flight (a load under a branch is sunk
