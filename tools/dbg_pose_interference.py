@@ -27,9 +27,25 @@ prm = mvtrack.pose_params(mvtrack.AS_INTENDED, fx=K[0, 0], fy=K[1, 1], cx=K[0, 2
 e = lambda *shape, dt=torch.float32: torch.zeros(shape, dtype=dt, device=dev)  # noqa: E731
 
 
+def cu_stream(half):
+    """a HIP stream restricted to one half of the CUs (hipExtStreamCreateWithCUMask), as a torch stream"""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    n = torch.cuda.get_device_properties(0).multi_processor_count
+    words = (n + 31) // 32
+    mask = (ctypes.c_uint32 * words)()
+    for c in range(n):
+        if (c % 2) == half:  # interleaved halves: every shader engine keeps CUs in both
+            mask[c // 32] |= 1 << (c % 32)
+    st = ctypes.c_void_p()
+    rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(words), mask)
+    assert rc == 0, rc
+    return torch.cuda.ExternalStream(st.value, device=dev)
+
+
 class Pipe:
-    def __init__(self):
-        self.stream = torch.cuda.Stream(device=dev)
+    def __init__(self, half=None):
+        self.stream = torch.cuda.Stream(device=dev) if half is None else cu_stream(half)
         self.ctx = mvtrack.Context(0)
         self.ctx.set_stream(self.stream)
         self.sp = mvtrack.SuperPoint(self.ctx, W)
@@ -72,7 +88,8 @@ class Pipe:
 
 
 torch.cuda.synchronize()
-a, b = Pipe(), Pipe()
+cm = os.environ.get("CUMASK")  # "split": A and B on disjoint CU halves; "same": both on half 0
+a, b = (Pipe(0), Pipe(1)) if cm == "split" else ((Pipe(0), Pipe(0)) if cm == "same" else (Pipe(), Pipe()))
 a.all(), b.all()
 torch.cuda.synchronize()
 ref = a.T.clone()
