@@ -79,6 +79,12 @@ class Pipe:
     def scat(self):  # fp32 stores scattered over 256 channel planes, as the raw heads write them
         self.cdesc.view(F, 256, -1).transpose(1, 2).copy_(self.desc.new_ones(F, 1920, 256) * 0.5)
 
+    def gemm(self):  # a library MFMA GEMM (hipBLASLt bf16), no kernel of ours
+        if not hasattr(self, "g"):
+            self.g = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
+        for _ in range(4):
+            self.g2 = self.g @ self.g
+
     def copy(self):  # a memory-bound torch kernel of the heads' size (126 MB written as fp32)
         self.cdesc.copy_(self.cdesc * 1.0)
 
