@@ -35,7 +35,8 @@ def cu_stream(half):
     words = (n + 31) // 32
     mask = (ctypes.c_uint32 * words)()
     for c in range(n):
-        if (c % 2) == half:  # interleaved halves: every shader engine keeps CUs in both
+        sel = ((c // 2) % 2) if os.environ.get("CUPAIRS") else (c % 2)  # CUPAIRS: whole CU pairs per half
+        if sel == half:  # interleaved halves: every shader engine keeps CUs in both
             mask[c // 32] |= 1 << (c % 32)
     st = ctypes.c_void_p()
     rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(words), mask)
