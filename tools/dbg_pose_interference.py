@@ -21,7 +21,8 @@ F, P = 257, 256
 W = dict(np.load(os.path.join(ROOT, "tests", "golden", "superpoint_qnonorm.npz")))
 x = torch.from_numpy(np.stack(frames_kitti(F))).to(dev)
 K = synth.KITTI_K
-prm = mvtrack.pose_params(mvtrack.AS_INTENDED, fx=K[0, 0], fy=K[1, 1], cx=K[0, 2], cy=K[1, 2],
+prm = mvtrack.pose_params(mvtrack.AS_BUILT if os.environ.get("MODE") == "built" else mvtrack.AS_INTENDED,
+                          fx=K[0, 0], fy=K[1, 1], cx=K[0, 2], cy=K[1, 2],
                           hypotheses=int(os.environ.get("HYPS", "256")), inlier_thresh=1.0,
                           refine_iters=int(os.environ.get("REFINE", "10")), seed=7)
 e = lambda *shape, dt=torch.float32: torch.zeros(shape, dtype=dt, device=dev)  # noqa: E731
