@@ -56,7 +56,10 @@ constexpr int NT = 256;
 #define PE_PREM 64
 #endif
 #ifndef PE_WAVES
-// waves per SIMD.  3: 155 VGPRs, no scratch.  4 (128 VGPRs, 38 VGPRs + 22 SGPRs spilled, 96 B of
+// waves per SIMD, a lower bound.  Built without SLP packing (Makefile, profiles/r05al_pose_noslp_ab.log)
+// the kernel takes 119 VGPRs and no scratch, i.e. 4 waves per SIMD either way; the history below is
+// that of the SLP-packed build, whose cross-stream nondeterminism went with the packing.
+// SLP-packed: 3: 155 VGPRs, no scratch.  4 (128 VGPRs, 38 VGPRs + 22 SGPRs spilled, 96 B of
 // scratch per lane) was faster (0.523 vs 0.564 ms exact, 1.07 vs 1.17 ms noisy,
 // profiles/r04y_pose_waves_ab.log) but NOT deterministic: with the image -> pose chain running on
 // three streams at once, some poses of a 256-pair track came out different from the same track
