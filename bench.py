@@ -28,6 +28,7 @@ CPU C0 path, windowed front-end, int8 all-pairs, sequence mode, keypoints.
 """
 import argparse
 import ctypes  # noqa: F401  (ctypes-backed oracle calls release the GIL)
+import datetime
 import json
 import os
 import socket
@@ -88,6 +89,12 @@ def parse(argv=None):
                          "one-GPU box (a one-rank all_gather_into_tensor is a device-side copy through RCCL)")
     ap.add_argument("--harness-cpu", action="store_true",
                     help="test only: the multi-rank harness with the CPU oracle as the step (gloo)")
+    ap.add_argument("--dist-timeout", type=float, default=180.0,
+                    help="N > 1: seconds a collective may wait for a peer before the process group fails (a dead "
+                         "or hung rank ends the run instead of blocking the survivors for the 10-minute default)")
+    ap.add_argument("--rank-grace", type=float, default=5.0,
+                    help="spawned ranks: seconds the surviving ranks get after one rank fails before they are "
+                         "terminated (they are blocked in the step's all-gather by then)")
     return ap.parse_args(argv)
 
 
@@ -104,21 +111,112 @@ def free_port():
     return port
 
 
-def spawn_ranks(n, argv):
+# Per-rank progress of the timed loop in a small shared file (spawned ranks only): slot r holds
+# (steps issued, first-step start, last-step end, pairs per step) as float64, written by rank r after
+# each timed step (two stores into a memory map, no syscall), read by the spawning parent when a rank
+# fails -- SURVEY §5's "per-GPU worker failure = drop that GPU's pairs".
+_PROGRESS = {"map": None, "rank": 0, "pairs": 0}
+
+
+def progress_open(path, world, rank, pairs_per_step):
+    if not path:
+        return
+    _PROGRESS["map"] = np.memmap(path, dtype=np.float64, mode="r+", shape=(world, 4))
+    _PROGRESS["rank"], _PROGRESS["pairs"] = rank, pairs_per_step
+    _PROGRESS["map"][rank] = (0.0, 0.0, 0.0, float(pairs_per_step))
+
+
+def _fail_hook(step_i):
+    """test hook (tests/test_dist.py): MV_BENCH_KILL_RANK=r with MV_BENCH_KILL_STEP=k makes rank r die
+    abruptly (exit 17, no cleanup) at its k-th timed step -- a lost GPU / worker in the middle of the
+    per-step all-gathers."""
+    kr = os.environ.get("MV_BENCH_KILL_RANK")
+    if kr is not None and int(kr) == int(os.environ.get("RANK", "0")) and \
+            step_i == int(os.environ.get("MV_BENCH_KILL_STEP", "0")):
+        sys.stderr.write("rank %s: MV_BENCH_KILL_RANK test hook, exiting at timed step %d\n" % (kr, step_i))
+        sys.stderr.flush()
+        os._exit(17)
+
+
+def spawn_ranks(n, argv, grace=5.0):
     """--gpus N without a launcher: N child processes, one rank per GPU, started before this
-    process touches the GPU; their exit status is ours.  Rank 0 prints the JSON line."""
+    process touches the GPU.  All children are polled: when one exits non-zero, the others get
+    `grace` seconds and are then terminated (they would otherwise block in the next all-gather
+    until the process-group timeout), and this process prints rank 0's JSON line itself, from the
+    surviving ranks' progress: their pairs only, the failed ranks named in `ranks_failed`, exit
+    status non-zero.  All children successful: their status (0) is ours, rank 0 printed the line."""
+    import tempfile
+
     env = dict(os.environ)
     env.update(WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()),
                LOCAL_WORLD_SIZE=str(n))
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    fd, prog_path = tempfile.mkstemp(prefix="mv_bench_progress_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    os.write(fd, bytes(n * 4 * 8))
+    os.close(fd)
+    env["MV_BENCH_PROGRESS"] = prog_path
     procs = []
-    for r in range(n):
-        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=e))
-    rc = 0
-    for p in procs:
-        rc = max(rc, p.wait())
-    return rc
+    t_start = time.time()
+    try:
+        for r in range(n):
+            e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=e))
+        failed, t_fail = [], None
+        while True:
+            rcs = [p.poll() for p in procs]
+            for r, rc in enumerate(rcs):
+                if rc not in (None, 0, PEER_LOST) and not any(f["rank"] == r for f in failed):
+                    failed.append({"rank": r, "exit": rc, "after_s": round(time.time() - t_start, 2)})
+                    t_fail = t_fail or time.time()
+            if all(rc is not None for rc in rcs):
+                break
+            if t_fail is not None and time.time() - t_fail > grace:
+                for p in procs:
+                    if p.poll() is None:
+                        p.terminate()
+                for p in procs:
+                    try:
+                        p.wait(timeout=10)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        p.wait()
+                break
+            time.sleep(0.05)
+        if not failed:
+            # every non-zero exit was a survivor's lost collective: no rank names itself the cause
+            if any(p.returncode == PEER_LOST for p in procs):
+                failed = [{"rank": r, "exit": p.returncode, "after_s": None} for r, p in enumerate(procs)
+                          if p.returncode == PEER_LOST]
+                print(json.dumps({"metric": METRIC, "value": None, "n_gpus": n, "partial": True,
+                                  "error": "collectives failed on ranks %s with no rank failing first" %
+                                           [f["rank"] for f in failed], "ranks_failed": failed}), flush=True)
+                return PEER_LOST
+            return 0
+        first = failed[0]["rank"]  # the first rank seen failing (polled in order)
+        prog = np.fromfile(prog_path, dtype=np.float64).reshape(n, 4)
+        dead = {f["rank"] for f in failed}
+        alive = [r for r in range(n) if r not in dead]
+        pairs = sum(int(prog[r, 0]) * int(prog[r, 3]) for r in alive)
+        span = max([prog[r, 2] - prog[r, 1] for r in alive if prog[r, 0] > 0] or [0.0])
+        out = {"metric": METRIC, "value": round(pairs / span, 2) if span > 0 else None, "unit": "pairs/s",
+               "n_gpus": n, "higher_is_better": True, "scaling": "weak", "partial": True,
+               "error": "rank %d exited with status %d; the other ranks were stopped" % (
+                   first, [f["exit"] for f in failed if f["rank"] == first][0]),
+               "ranks_failed": sorted(failed, key=lambda f: f["after_s"]),
+               "ranks_surviving": [{"rank": r, "steps_issued": int(prog[r, 0]), "pairs_per_step": int(prog[r, 3]),
+                                    "seconds": round(float(prog[r, 2] - prog[r, 1]), 4)} for r in alive],
+               "note": "value = pairs of the surviving ranks' timed steps (host-issued; the failed ranks' pairs "
+                       "dropped) / their longest span -- SURVEY 5: per-GPU worker failure drops that GPU's pairs"}
+        print(json.dumps(out), flush=True)
+        return max(1, max(f["exit"] if f["exit"] > 0 else 1 for f in failed))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        try:
+            os.unlink(prog_path)
+        except OSError:
+            pass
 
 
 def timed_loop(step, steps, warmup, sync, barrier):
@@ -129,8 +227,14 @@ def timed_loop(step, steps, warmup, sync, barrier):
     barrier()
     sync()
     t0 = time.perf_counter()
-    for _ in range(steps):
+    pm, pr = _PROGRESS["map"], _PROGRESS["rank"]
+    if pm is not None:
+        pm[pr, 0], pm[pr, 1] = 0.0, time.time()
+    for i in range(steps):
+        _fail_hook(i)
         step()
+        if pm is not None:
+            pm[pr, 0], pm[pr, 2] = float(i + 1), time.time()
     sync()
     barrier()
     return time.perf_counter() - t0
@@ -310,6 +414,16 @@ def design_bytes_per_pair(screen, n, fused):
     return n * (KD * 4 + KD * 2 + 4 + 4)
 
 
+def profile_order_key(path):
+    """profiles/rNN<tag>_summary.json in the order they were made: round NN, then the tag as the
+    profiles name it (a < ... < z < aa < ab ...: shorter tags first -- a plain name sort would put
+    r06z above r06aa and r05v above r05al)"""
+    import re
+
+    m = re.match(r"r(\d+)([a-z]*)", os.path.basename(path))
+    return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+
+
 def pmc_traffic(kernel, B, n, screen, fused, noise=None):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of THIS
     command: profiles/*_summary.json written by tools/profile.sh over bench.py itself (bench_args
@@ -317,7 +431,8 @@ def pmc_traffic(kernel, B, n, screen, fused, noise=None):
     (None: the default noise, i.e. no --noise in the profiled arguments).  None when absent."""
     import glob
 
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")), reverse=True):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")), key=profile_order_key,
+                    reverse=True):
         try:
             d = json.load(open(f))
         except Exception:
@@ -477,8 +592,9 @@ def main_cpu_harness(args, world, rank):
     import oracle
 
     if world > 1:
-        dist.init_process_group(backend="gloo")
+        dist.init_process_group(backend="gloo", timeout=datetime.timedelta(seconds=args.dist_timeout))
     B, n = args.batch, args.kp
+    progress_open(os.environ.get("MV_BENCH_PROGRESS"), world, rank, B)
     pairs = []
     for b in range(B):
         r = np.random.default_rng(pair_seed(rank, b))
@@ -509,6 +625,10 @@ def main_cpu_harness(args, world, rank):
            "gathered_matches": int(gathered[:, 12].contiguous().view(torch.int32).sum()),
            "gathered_ranks": sorted(set(int(x) for x in gathered[:, 3].tolist())),
            "all_gathers": gather.count}
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, {"rank": rank, "device": "cpu", "backend": dist.get_backend(), "pid": os.getpid()})
+        out["ranks"] = ranks
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -518,7 +638,7 @@ def main_cpu_harness(args, world, rank):
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:], args.rank_grace))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -540,14 +660,16 @@ def main():
             os.environ.setdefault("MASTER_PORT", str(free_port()))
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
+        to = datetime.timedelta(seconds=args.dist_timeout)
         if args.dist_backend == "nccl":
-            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local), timeout=to)
         else:
-            dist.init_process_group(backend="gloo")
+            dist.init_process_group(backend="gloo", timeout=to)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     B, n = args.batch, args.kp
+    progress_open(os.environ.get("MV_BENCH_PROGRESS"), world, rank, B)
 
     d0, d1, kp0, kp1 = gen_batch(torch, dev, B, n, seed=pair_seed(rank, 0), noise=args.noise)
     nn_ = torch.full((B,), n, dtype=torch.int32, device=dev)
@@ -679,7 +801,13 @@ def main():
             assert torch.equal(g[rank, :, 12].contiguous().to(dev).view(torch.int32), nmatches[c]), \
                 "gathered match count differs from this rank's (slot %d)" % c
         g = gather.out[0].view(world, B, 13)
-        gathered = {"pairs_per_gather": int(g.shape[0] * g.shape[1]), "gathers_in_timed_steps": gathers_timed,
+        props = torch.cuda.get_device_properties(local)
+        me = {"rank": rank, "device": local, "backend": dist.get_backend(),
+              "pci_bus": "%s:%s" % (getattr(props, "pci_domain_id", "?"), getattr(props, "pci_bus_id", "?")),
+              "pid": os.getpid()}
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me)  # validation only: which device / backend every rank ran on
+        gathered = {"ranks": ranks, "pairs_per_gather": int(g.shape[0] * g.shape[1]), "gathers_in_timed_steps": gathers_timed,
                     "bytes_per_gather": int(g.numel() * 4), "backend": args.dist_backend,
                     "slots_checked_bitwise": P, "streams": "pipelined" if P > 1 else "current",
                     "ranks_per_device": "%d ranks on %d device(s)" % (world, torch.cuda.device_count())}
@@ -840,5 +968,23 @@ def main():
         dist.destroy_process_group()
 
 
+PEER_LOST = 75  # a rank's collective failed because a peer died or hung (it is a survivor, not the cause)
+
+
+def _collective_error(e):
+    """the exception was raised inside torch.distributed (a collective or the rendezvous store)"""
+    import traceback
+
+    return any("torch/distributed" in fr.filename.replace(os.sep, "/") for fr in traceback.extract_tb(e.__traceback__))
+
+
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except Exception as exc:  # noqa: BLE001
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1 and _collective_error(exc):
+            sys.stderr.write("rank %s: a collective failed (%s: %s) -- a peer rank died or hung; exiting %d\n" % (
+                os.environ.get("RANK", "?"), type(exc).__name__, str(exc)[:300], PEER_LOST))
+            sys.stderr.flush()
+            os._exit(PEER_LOST)
+        raise

@@ -44,47 +44,33 @@ using namespace q8;
 
 constexpr int D_NW = 8, D_NT = 64 * D_NW, D_BM = 32 * RG * D_NW;  // 512 rows per workgroup
 constexpr int D_HROWS = 32, D_HALF = D_HROWS * KD * 4;             // one staging slot: 32 fp32 rows
-#ifndef D_PAD
-#define D_PAD 1  // int8 ring rows padded to 272 B (conflict-free, immediate-offset fragment reads)
-#endif
-// the int8 tile ring: 64 rows (columns of frame 1) of 256 codes, row stride D_RS; D_PAD: 272 B
-// (17 chunks: the 16-lane phases of a ds_read_b128 hit distinct banks, and every B-fragment address
-// is a per-lane base + a compile-time offset); else 256 B with the 16-B chunks XOR-swizzled by row
-constexpr int D_RS = D_PAD ? KD + 16 : KD;
+// the int8 tile ring: 64 rows (columns of frame 1) of 256 codes, row stride D_RS = 272 B (17
+// chunks: the 16-lane phases of a ds_read_b128 hit distinct banks, and every B-fragment address is
+// a per-lane base + a compile-time offset; round 3's 256-B rows with XOR-swizzled chunks needed
+// per-read address VALU, 20 per tile and wave)
+constexpr int D_RS = KD + 16;
 constexpr int D_TILE = BN * D_RS, D_SLOT = D_TILE + BN * 4;        // + the tile's 64 per-column words
 constexpr int D_OFF_RING = 3 * D_HALF;                              // 2 int8 tile slots
 // [BM] float2 (|a|^2, s_a), past the int8 ring
 constexpr int D_OFF_ROW = D_OFF_RING + 2 * D_SLOT;
 constexpr int D_OFF_MISC = D_OFF_ROW + D_BM * 8;                    // [NW][4] per-wave statistics
-#ifndef D_COLWIN
-#define D_COLWIN 1  // the epilogue's window per maximiser column (0: the pair's widest, for A/B)
-#endif
 constexpr int D_OFF_COL = D_OFF_MISC + D_NW * 16;  // integer path: each frame-1 column's key shift (1 B)
 constexpr int D_NCOL = 64 * BN;           // the integer path's column limit (2 ntc <= 128)
-#ifndef D_EXACT_EA
-#define D_EXACT_EA 0  // the A phase measures each row's quantisation residual (rowe) for the window
-#endif
-constexpr int D_OFF_ROWE = D_OFF_COL + D_NCOL;  // [BM] float |rho|^2 per row (D_EXACT_EA)
-constexpr int D_LDS = D_OFF_ROWE + (D_EXACT_EA ? D_BM * 4 : 0);
+constexpr int D_LDS = D_OFF_COL + D_NCOL;
 constexpr int D_OFF_AIMG = 2 * D_HALF;  // A images: staging slot 2 + the ring (before the sweep)
 static_assert(D_OFF_AIMG + D_NW * 32 * KD <= D_OFF_ROW, "A images fit staging slot 2 + the ring");
 static_assert(epi_bytes<D_NW>() <= D_OFF_ROW, "the epilogue fits staging + ring");
 static_assert(D_LDS <= 160 * 1024, "one workgroup per CU");
 constexpr int D_PF = 1;       // k32 steps of B fragments read ahead of the MFMAs
 constexpr int QS_LOAD = 1;    // the k32 step whose slot issues the quantisation's staging reads
-#ifndef D_QB
 // A phase: frame-0 row quads in flight per wave (4 x 16-B loads per lane each); fewer bytes in
 // flight measured faster in both kernels (k_q8t_match 2: 3.505, 4: 3.54, 8: 3.91 ms --
 // profiles/r05h_flag_qb_ab.json; k_q8d_match round 4: 2: 4.153-4.161, 4: 4.176-4.195 ms)
-#define D_QB 2
-#endif
+constexpr int D_QB = 2;
 constexpr float IK_MMAX = 1.003f;  // integer path: max |b_jk| allowed (RNE(x 127) stays <= 127)
-#ifndef D_CC
-// 1: integer path, |b_j| bounded from the codes (v_dot4) and NaN caught by v_maximum3 instead of
-// summing the fp32 squares (12 VALU per tile and wave fewer) -- fails the out-of-range parity test
-// (tests/test_gpu_allpairs.py::test_allpairs_f32_out_of_screen_range): experimental, off
-#define D_CC 0
-#endif
+// (Measured and not kept, round 5: |b_j| bounded from the codes by v_dot4 and NaN caught by
+// v_maximum3 instead of summing the fp32 squares -- 12 VALU per tile and wave fewer, but it failed
+// tests/test_gpu_allpairs.py::test_allpairs_f32_out_of_screen_range.)
 
 #ifdef MV_TRACE  // phase stamps (s_memtime) per (block, wave): tools/trace_direct.py
 constexpr int D_TRACE_BLOCKS = 16384;
@@ -230,19 +216,7 @@ struct QHalf {
         x2 = *reinterpret_cast<const f32x4v *>(src + 512);
         x3 = *reinterpret_cast<const f32x4v *>(src + 768);
     }
-    static constexpr bool CC = IK && D_CC;  // |b_j| from the codes
     __device__ __forceinline__ void absmax() {
-        if constexpr (CC) {
-            m = absmaximum3(0.f, x0[0], x0[1]);
-            m = absmaximum3(m, x0[2], x0[3]);
-            m = absmaximum3(m, x1[0], x1[1]);
-            m = absmaximum3(m, x1[2], x1[3]);
-            m = absmaximum3(m, x2[0], x2[1]);
-            m = absmaximum3(m, x2[2], x2[3]);
-            m = absmaximum3(m, x3[0], x3[1]);
-            m = absmaximum3(m, x3[2], x3[3]);
-            return;
-        }
         m = absmax3(0.f, x0[0], x0[1]);
         m = absmax3(m, x0[2], x0[3]);
         m = absmax3(m, x1[0], x1[1]);
@@ -253,19 +227,14 @@ struct QHalf {
         m = absmax3(m, x3[2], x3[3]);
     }
     __device__ __forceinline__ void sumsq() {
-        if constexpr (CC) return;
         qa = __builtin_fmaf(x0[0], x0[0], __builtin_fmaf(x0[1], x0[1], __builtin_fmaf(x0[2], x0[2], x0[3] * x0[3])));
         qb = __builtin_fmaf(x1[0], x1[0], __builtin_fmaf(x1[1], x1[1], __builtin_fmaf(x1[2], x1[2], x1[3] * x1[3])));
         qa = __builtin_fmaf(x2[0], x2[0], __builtin_fmaf(x2[1], x2[1], __builtin_fmaf(x2[2], x2[2], __builtin_fmaf(x2[3], x2[3], qa))));
         qb = __builtin_fmaf(x3[0], x3[0], __builtin_fmaf(x3[1], x3[1], __builtin_fmaf(x3[2], x3[2], __builtin_fmaf(x3[3], x3[3], qb))));
     }
     __device__ __forceinline__ void reduce(int j, int n1, int tb) {
-        if constexpr (CC) {
-            row16_max(m);
-        } else {
-            qa = qa + qb;
-            row16_max_sum(m, qa);  // qa = |b|^2 from here on
-        }
+        qa = qa + qb;
+        row16_max_sum(m, qa);  // qa = |b|^2 from here on
         if constexpr (IK) {
             // e from m's biased exponent: [1/2, 2) -> 0, [1/4, 1/2) -> 1, below -> 2 (m q_e < 128)
             float mg = m;
@@ -289,21 +258,12 @@ struct QHalf {
     __device__ __forceinline__ void pack23() {
         code[2] = pack4(x2[0], x2[1], x2[2], x2[3], q);
         code[3] = pack4(x3[0], x3[1], x3[2], x3[3], q);
-        if constexpr (CC) {  // |c_j|^2 of the codes; |b_j| <= s_j (|c_j| + 8) (|b_jk - c_jk s_j| <= s_j / 2)
-            int c2 = __builtin_amdgcn_sdot4(code[0], code[0], 0, false);
-            c2 = __builtin_amdgcn_sdot4(code[1], code[1], c2, false);
-            c2 = __builtin_amdgcn_sdot4(code[2], code[2], c2, false);
-            c2 = __builtin_amdgcn_sdot4(code[3], code[3], c2, false);
-            row16_sum_i(c2);
-            const float bn = s * (__builtin_amdgcn_sqrtf((float)c2) + 8.0f) * 1.0001f;  // v_sqrt: 1 ulp
-            qa = bn * bn;  // an upper bound of |b_j|^2 (the window's Bn)
-        }
     }
     // cs: the tile's entries of the per-column key shifts kept for the epilogue (IK; live halves)
     __device__ __forceinline__ void store(char *rq, int hh, int t, bool live, float &smax, float &b2max, bool &bad,
                                           unsigned char *cs) {
         const int r = t >> 4, sub = t & 15, row = 32 * hh + r;
-        *reinterpret_cast<i32x4 *>(rq + row * D_RS + (D_PAD ? sub << 4 : (sub ^ (row & 15)) << 4)) = code;
+        *reinterpret_cast<i32x4 *>(rq + row * D_RS + (sub << 4)) = code;
         if constexpr (IK && GRP) {
             if ((t & 63) == 0) {  // the wave's group: 8 hh + w -> jb = hh, q = (w >> 1) & 3, h = w & 1
                 const int w = t >> 6;
@@ -316,7 +276,7 @@ struct QHalf {
                 reinterpret_cast<int *>(rq + D_TILE)[row] = sh;
                 if (live) cs[row] = (unsigned char)sh;
             }
-            bad = bad | (live & !((qa <= 1e30f) & (m <= IK_MMAX)));  // CC: m carries any NaN
+            bad = bad | (live & !((qa <= 1e30f) & (m <= IK_MMAX)));
         } else {
             if (sub == 0) reinterpret_cast<float *>(rq + D_TILE)[row] = s;
             bad = bad | (live & !((qa <= FLT_MAX) & ((m == 0.f) | ((m >= SCALE_LO) & (m <= SCALE_HI)))));
@@ -373,8 +333,7 @@ __device__ __forceinline__ Sweep sweep(char *lds, const float *B, int n1, int t,
     if (nh > 3) dma_half(B, 3, n1, wu, chunk16, lds_base);
 
     // B fragment: column block c (0, 1), lane row 32 c + fr, k32 step s: chunk (2 s + fh)
-    const int rdb = fr * D_RS + (D_PAD ? fh * 16 : 0);
-    const int xsw = fh ^ (fr & 15);  // !D_PAD: chunk (2 s + fh) ^ (fr & 15) = 2 s ^ xsw
+    const int rdb = fr * D_RS + fh * 16;
 
     i32x16 acc[RG][2];
     const float kinit = IK ? __int_as_float((int)0x80000000) : -__builtin_inff();
@@ -419,8 +378,6 @@ __device__ __forceinline__ Sweep sweep(char *lds, const float *B, int n1, int t,
 #define D_SEG(G, FG, G0, STG, HH, J0, LIVE)                                                  \
     do {                                                                                     \
         const char *base = rs + rdb;                                                         \
-        int xs_ = xsw;                                                                       \
-        if (!D_PAD) asm volatile("" : "+v"(xs_)); /* per-use offsets: not 8 loop-invariant VGPRs */ \
         i32x4 b0_[KD / 32], b1_[KD / 32];                                                    \
         QHalf<IK> qh_;                                                                       \
         _Pragma("unroll") for (int s_ = 0; s_ < KD / 32 + D_PF; s_++) {                      \
@@ -432,7 +389,7 @@ __device__ __forceinline__ Sweep sweep(char *lds, const float *B, int n1, int t,
             else if (s_ == QS_LOAD + 5) qh_.pack23();                                        \
             else if (s_ == QS_LOAD + 6) qh_.store(rq, (HH), t, (LIVE), st.smax, st.b2max, st.bad, colsh + (tc + 1) * BN); \
             if (s_ < KD / 32) {                                                              \
-                const int ch_ = D_PAD ? 32 * s_ : ((2 * s_) ^ xs_) * 16;                     \
+                const int ch_ = 32 * s_;                                                     \
                 b0_[s_] = *reinterpret_cast<const i32x4 *>(base + ch_);                      \
                 b1_[s_] = *reinterpret_cast<const i32x4 *>(base + 32 * D_RS + ch_);          \
             }                                                                                \
@@ -577,9 +534,8 @@ __device__ __forceinline__ void q8d_block(char *lds, int L, int tiles_r, int cap
     dma_half(B, 0, n1, wu, chunk16, lds_base);
     dma_half(B, 1, n1, wu, chunk16, lds_base + D_HALF);
     i32x4 aI[RG][KD / 32];
-    float *rowe = D_EXACT_EA ? reinterpret_cast<float *>(lds + D_OFF_ROWE) : nullptr;
-    a_phase<false, D_QB, D_EXACT_EA>(lds + D_OFF_AIMG + w * 32 * KD, rowv, w * 64, row0, n0, lane, A, nullptr,
-                                     nullptr, nullptr, false, aI, rowe);
+    a_phase<false, D_QB>(lds + D_OFF_AIMG + w * 32 * KD, rowv, w * 64, row0, n0, lane, A, nullptr, nullptr,
+                         nullptr, false, aI);
     D_STAMP(1);
     __syncthreads();  // the A images (staging slot 2 + the ring) are consumed
     float m1[RG][16], m2[RG][16];
@@ -597,8 +553,7 @@ __device__ __forceinline__ void q8d_block(char *lds, int L, int tiles_r, int cap
             // the window per maximiser column (its own 1 / q_j)
             epilogue<D_NW, true>(lds, rowv, m1, m2, Bn, Eb, false, tbi, ~((1u << tbi) - 1u), w, lane, row0, n0,
                                  n1, A, B, oidx, oscore, thresh, dmode, 1.0 / 508.0,
-                                 !D_COLWIN ? nullptr : reinterpret_cast<const unsigned char *>(lds + D_OFF_COL),
-                                 rowe);
+                                 reinterpret_cast<const unsigned char *>(lds + D_OFF_COL));
             D_STAMP(3);
 #ifdef MV_TRACE
             if (lane == 0 && blockIdx.x < D_TRACE_BLOCKS) {
@@ -677,9 +632,6 @@ constexpr int T_OFF_COL = T_OFF_MISC + D_NW * 16;   // each frame-1 column's key
 constexpr int T_LDS = T_OFF_COL + T_BM;
 constexpr int T_EPI_MASK = D_NW * 8192;             // epilogue: [NW] 8-KiB re-score buffers, [T_BM] wide masks
 static_assert(T_EPI_MASK + T_BM * 4 <= T_OFF_ROW, "the epilogue fits staging + ring");
-#ifndef T_RESCREEN
-#define T_RESCREEN 1  // 0: wide rows scored against every column of their halves in k_q8t_match (A/B)
-#endif
 constexpr unsigned T_RESCAN = 0x80000000u;  // wide-mask bit: the row is left to k_q8t_rescan
 // a row left to k_q8t_rescan: its match index holds INT_MIN + lim + 2^28 (< -1, never an index),
 // lim = the window's low end in key units, rounded up and clamped to +-2^28 (clamping only widens)
@@ -691,9 +643,7 @@ __device__ __forceinline__ int rs_decode(int v) { return (int)((unsigned)v - 0x8
 static_assert(D_OFF_AIMG + D_NW * 32 * KD <= T_OFF_ROW, "A images fit staging slot 2 + the ring");
 static_assert(T_LDS <= 160 * 1024, "one workgroup per CU");
 constexpr float T_B2MAX = 4.f;  // |b_j|^2 bound of the keys' range at tb <= 9
-#ifndef T_PFD
-#define T_PFD 2  // k32 steps the frame-1 fragments are read ahead of their MFMA (1: 3.66 ms, 2: 3.53, 3: 3.52 -- profiles/r05g_pfd_ab.json)
-#endif
+constexpr int T_PFD = 2;  // k32 steps the frame-1 fragments are read ahead of their MFMA (1: 3.66 ms, 2: 3.53, 3: 3.52 -- profiles/r05g_pfd_ab.json)
 
 __device__ __forceinline__ Sweep sweep_t(char *lds, const float *B, int n1, int t, int lane, int wu, unsigned chunk16,
                                          unsigned lds_base, const i32x4 (&aI)[T_RG][KD / 32], float (&m1)[T_RG],
@@ -745,42 +695,8 @@ __device__ __forceinline__ Sweep sweep_t(char *lds, const float *B, int n1, int 
     // unit U of the tile: column block jb = U >> 2, row group g = U & 3: 8 MFMAs into acc[U & 1],
     // each beside the fold of 2 of the previous unit's 16 values (acc[(U + 1) & 1], row group
     // (U + 3) & 3, shifts PSV, tags PT + r), and quantisation stages 2 (U & 3), 2 (U & 3) + 1 at
-    // k32 steps 1 and 5
-#define T_UNIT(U, PSV, PT, STG, HH, J0, LIVE)                                                 \
-    do {                                                                                     \
-        const char *base_ = rs + rdb + ((U) >> 2) * 32 * D_RS;                               \
-        i32x4 b_[KD / 32];                                                                   \
-        _Pragma("unroll") for (int s_ = 0; s_ < KD / 32 + 1; s_++) {                         \
-            if (s_ == 1 || s_ == 5) {                                                        \
-                const int k_ = 2 * ((U) & 3) + (s_ == 5);                                    \
-                if (k_ == 0) qh.load((STG), t);                                              \
-                else if (k_ == 1) qh.absmax();                                               \
-                else if (k_ == 2) qh.sumsq();                                                \
-                else if (k_ == 3) qh.reduce((J0) + (t >> 4), n1, tb);                        \
-                else if (k_ == 4) qh.pack01();                                               \
-                else if (k_ == 5) qh.pack23();                                               \
-                else if (k_ == 6) qh.store(rq, (HH), t, (LIVE), st.smax, st.b2max, st.bad, colsh + (tc + 1) * BN); \
-            }                                                                                \
-            if (s_ < KD / 32) b_[s_] = *reinterpret_cast<const i32x4 *>(base_ + 32 * s_);    \
-            if (s_ >= 1) {                                                                   \
-                const int m_ = s_ - 1;                                                       \
-                if (m_ == 0) {                                                               \
-                    const i32x16 z_ = {};                                                    \
-                    acc[(U) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(b_[0], aI[(U) & 3][0], z_, 0, 0, 0); \
-                } else {                                                                     \
-                    acc[(U) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(b_[m_], aI[(U) & 3][m_], acc[(U) & 1], 0, 0, 0); \
-                }                                                                            \
-                fold_keys(acc[((U) + 1) & 1][2 * m_], acc[((U) + 1) & 1][2 * m_ + 1], PSV[m_ >> 1], PSV[m_ >> 1], \
-                          (PT) + 2u * m_, (PT) + 2u * m_ + 1u, m1[((U) + 3) & 3], m2[((U) + 3) & 3]); \
-            }                                                                                \
-            __builtin_amdgcn_sched_barrier(0);                                               \
-        }                                                                                    \
-    } while (0)
-
-#if T_PFD > 1
-    // the fragments read T_PFD k32 steps ahead across the tile's units (fb_: the tile's 64 k32
-    // steps, constant indices: only the T_PFD + 1 live ones take registers)
-#undef T_UNIT
+    // k32 steps 0 and 4; the fragments read T_PFD k32 steps ahead across the tile's units (fb_: the
+    // tile's 64 k32 steps, constant indices: only the T_PFD + 1 live ones take registers)
 #define T_UNIT(U, PSV, PT, STG, HH, J0, LIVE)                                                 \
     do {                                                                                     \
         _Pragma("unroll") for (int s_ = 0; s_ < KD / 32; s_++) {                             \
@@ -811,7 +727,6 @@ __device__ __forceinline__ Sweep sweep_t(char *lds, const float *B, int n1, int 
             __builtin_amdgcn_sched_barrier(0);                                               \
         }                                                                                    \
     } while (0)
-#endif
 
     int sA = 2, sB = 0;  // staging slots of halves 2t + 2, 2t + 3
     for (int tc = 0; tc < ntc; tc++) {
@@ -821,11 +736,9 @@ __device__ __forceinline__ Sweep sweep_t(char *lds, const float *B, int n1, int 
             wait_vm<0>();
         }
         D_SYNC();  // tile t complete in its slot; the slot of tile t - 1 and staging of half 2t + 1 free
-#if T_PFD > 1
         i32x4 fb_[64];
         _Pragma("unroll") for (int p_ = 0; p_ < T_PFD; p_++)
             fb_[p_] = *reinterpret_cast<const i32x4 *>(ring + (tc & 1) * D_SLOT + rdb + 32 * p_);
-#endif
         const int sN = 3 - sA - sB;
         if (2 * tc + 4 < nh) dma_half(B, 2 * tc + 4, n1, wu, chunk16, lds_base + (unsigned)(sN * D_HALF));
         const char *rs = ring + (tc & 1) * D_SLOT;
@@ -993,8 +906,8 @@ __device__ __forceinline__ unsigned epilogue_t(char *epi, const float2 *rowv, co
         bj_g[g] = bj;
         need_g[g] = need;
         out_g[g] = fh == 0 && live && !wide;
-        if (fh == 0 && wide) lmask[rl] = T_RESCREEN && rescan ? T_RESCAN : wm;
-        if (T_RESCREEN && fh == 0 && rescan) oidx[rl] = rs_encode(lim_k);  // k_q8t_rescan's work
+        if (fh == 0 && wide) lmask[rl] = rescan ? T_RESCAN : wm;
+        if (fh == 0 && rescan) oidx[rl] = rs_encode(lim_k);  // k_q8t_rescan's work
         wide_rows[g] = (unsigned)__ballot(fh == 0 && wide);
     }
     unsigned nwide = 0, nneed = 0;  // (traced builds) the wave's wide rows and deferred dots
@@ -1031,7 +944,7 @@ __device__ __forceinline__ unsigned epilogue_t(char *epi, const float2 *rowv, co
             if (oscore) oscore[rl] = keep ? bs_g[g] : 0.f;
         }
     // wide rows left here (rows outside the int8 range, a padding column on top; with
-    // T_RESCREEN 0 every wide row): every column of the listed halves, one column per lane
+    // round 5's first form every wide row): every column of the listed halves, one column per lane
 #pragma unroll
     for (int g = 0; g < T_RG; g++)
         for (unsigned dm = wide_rows[g]; dm; dm &= dm - 1) {
@@ -1111,7 +1024,7 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8t_match(int cap, const int *__res
     dma_half(B, 0, n1, wu, chunk16, lds_base);
     dma_half(B, 1, n1, wu, chunk16, lds_base + D_HALF);
     i32x4 aI[T_RG][KD / 32];
-    a_phase<false, D_QB, false, T_RG>(lds + D_OFF_AIMG + w * 32 * KD, rowv, w * (32 * T_RG), 0, n0, lane, A, nullptr,
+    a_phase<false, D_QB, T_RG>(lds + D_OFF_AIMG + w * 32 * KD, rowv, w * (32 * T_RG), 0, n0, lane, A, nullptr,
                                       nullptr, nullptr, false, aI);
     D_STAMP(1);
     __syncthreads();  // the A images (staging slot 2 + the ring) are consumed
@@ -1411,13 +1324,12 @@ int launch_allpairs_q8t_match(hipStream_t s, void *scratch, int batch, int cap, 
                        match_idx, match_score, flags, rflags, rcolsh);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
-    if (T_RESCREEN) {  // the wide rows it left: 4 waves per workgroup, a grid-stride loop over pairs
-        MV_PROF_BEGIN(s, "k_q8t_rescan");
-        hipLaunchKernelGGL(k_q8t_rescan, dim3((unsigned)min(batch, 1024)), dim3(64 * RS_NW), 0, s, batch, cap, n1, desc0,
-                           desc1, thresh, match_idx, match_score, rflags, rcolsh);
-        MV_PROF_END(s);
-        MV_LAUNCH_CHECK();
-    }
+    // the wide rows it left: 4 waves per workgroup, a grid-stride loop over pairs
+    MV_PROF_BEGIN(s, "k_q8t_rescan");
+    hipLaunchKernelGGL(k_q8t_rescan, dim3((unsigned)min(batch, 1024)), dim3(64 * RS_NW), 0, s, batch, cap, n1, desc0,
+                       desc1, thresh, match_idx, match_score, rflags, rcolsh);
+    MV_PROF_END(s);
+    MV_LAUNCH_CHECK();
     return launch_allpairs_q8d_match(s, batch, cap, n0, n1, desc0, desc1, thresh, match_idx, match_score, 0, flags);
 }
 

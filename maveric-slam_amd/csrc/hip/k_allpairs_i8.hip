@@ -1196,7 +1196,12 @@ extern "C" int mv_match_allpairs_i8_dev(mv_context *ctx, int batch, int cap, con
     // way (both kernels are integer-exact); a captured stream always takes the transposed path.
     bool direct = false;
     int *count_host = nullptr;
-    if (!mv::capturing(ctx->stream)) {
+    bool cap_now = false;
+    {
+        const int rc = mv::capture_state(ctx->stream, &cap_now);
+        if (rc != MV_OK) return rc;
+    }
+    if (!cap_now) {
         if (!ctx->i8_count_host) {
             void *h = nullptr;
             if (hipHostMalloc(&h, 64, 0) == hipSuccess) {
@@ -1212,7 +1217,9 @@ extern "C" int mv_match_allpairs_i8_dev(mv_context *ctx, int batch, int cap, con
                 *ch = -2;
             }
             direct = ctx->i8_prefer_m && (ctx->i8_calls % 16) != 0;
-            if (!direct && *ch == -2) {  // measure this call
+            // measure this call -- only where the launch below enqueues the count copy (the transposed
+            // path with hand-backs), so that no measurement is marked in flight that never lands
+            if (!direct && *ch == -2 && IT_HANDBACK && mv::i8_transposed(cap)) {
                 *ch = -1;
                 ctx->i8_meas_batch = batch;
                 count_host = ctx->i8_count_host;
@@ -1220,6 +1227,8 @@ extern "C" int mv_match_allpairs_i8_dev(mv_context *ctx, int batch, int cap, con
             ctx->i8_calls++;
         }
     }
-    return mv::launch_allpairs_i8(ctx->stream, scr, batch, cap, n0, n1, desc0, desc1, match_idx, match_dot, direct,
-                                  count_host);
+    const int rc = mv::launch_allpairs_i8(ctx->stream, scr, batch, cap, n0, n1, desc0, desc1, match_idx, match_dot,
+                                          direct, count_host);
+    if (rc != MV_OK && count_host) *count_host = -2;  // the count copy was not enqueued
+    return rc;
 }

@@ -31,32 +31,16 @@
 namespace {
 
 constexpr int NMS_T = 1024;  // threads of the per-frame block
-#ifndef KP_TRACE
-#define KP_TRACE 0  // printf k_kp_nms's per-phase clock64() deltas for frame 0 (timing only)
-#endif
-#ifndef KP_TRANSPOSE
-#define KP_TRANSPOSE 0  // 1: always the NCHW->NHWC transpose + per-keypoint-wave sampling
-#endif
-#ifndef KP_CH
-#define KP_CH 4  // channels per k_kp_sample_planes workgroup (4: 144 KiB of LDS, 2: 72 KiB)
-#endif
-static_assert(KP_CH == 2 || KP_CH == 4, "KP_CH");
-constexpr int KP_PLANE_CELLS = 9216;  // cells whose 4 channel planes fit LDS (144 KiB): KITTI 47x155 = 7285
-#ifndef KP_PLANE_CELLS_S
-#define KP_PLANE_CELLS_S 2048  // the small-frame instantiation (0: always the 144 KiB one, A/B)
-#endif
+constexpr int KP_CH = 4;                 // channels per k_kp_sample_planes workgroup (144 KiB of LDS)
+constexpr int KP_PLANE_CELLS = 9216;     // cells whose 4 channel planes fit LDS (144 KiB): KITTI 47x155 = 7285
+constexpr int KP_PLANE_CELLS_S = 2048;   // the small-frame instantiation (32 KiB: several workgroups per CU)
 constexpr int NC_LDS = 8192;  // candidates per frame held in LDS (more: the global per-pixel path)
 constexpr int ROW_LDS = 2048; // heat rows indexed in LDS
-#ifndef KP_NMS_GLOBAL
-#define KP_NMS_GLOBAL 0  // 1: always the global per-pixel path (the LDS path's timing baseline)
-#endif
-#ifndef KP_HN
-// 16: the 192 x 640 network frames' dense candidates (2.2 % of pixels) rescanned their window
-// every NMS round whenever more than 8 higher neighbours were listed (A/B in DESIGN 4.3)
-#define KP_HN 16
-#endif
-static_assert(KP_HN % 4 == 0, "16-B list pieces");
-constexpr int HN = KP_HN;    // listed higher-priority neighbours per candidate
+// listed higher-priority neighbours per candidate.  16: the 192 x 640 network frames' dense
+// candidates (2.2 % of pixels) rescanned their window every NMS round whenever more than 8 higher
+// neighbours were listed (A/B in DESIGN 4.3)
+constexpr int HN = 16;
+static_assert(HN % 4 == 0, "16-B list pieces");
 constexpr int SORT_N = 4096; // survivors sorted in LDS (more: ranked by counting)
 __host__ __device__ inline long hn_cands(long P) { return (P + 7) / 8; }  // candidates with a list (more: rescanned)
 
@@ -73,7 +57,7 @@ struct KpScratch {
 };
 
 size_t a256(size_t x) { return mv::align_up(x, 256); }
-bool kp_planes_path(int Hc, int Wc) { return (long)Hc * Wc <= KP_PLANE_CELLS && !KP_TRANSPOSE; }
+bool kp_planes_path(int Hc, int Wc) { return (long)Hc * Wc <= KP_PLANE_CELLS; }
 
 size_t kp_scratch_bytes(int B, int Hc, int Wc, int cap) {
     const size_t P = (size_t)Hc * Wc * 64;
@@ -278,7 +262,6 @@ __global__ __launch_bounds__(NMS_T) void k_kp_nms(int Hh, int Wh, int H, int W, 
     //     to keep that many bytes in flight), and writes its candidates in pixel order to its
     //     own segment of two scratch arrays free at this point (kept: pixel, hn: confidence
     //     bits); after the block scan each wave moves its segment to its final ids
-    const long long tk0 = KP_TRACE ? clock64() : 0;
     constexpr int NWV = NMS_T / 64, CU_ = 8;
     const long cw = ((P + NWV * 256 * CU_ - 1) / (NWV * 256 * CU_)) * (256 * CU_);  // pixels per wave
     const long q0 = min(P, (long)w * cw), q1 = min(P, q0 + cw);  // multiples of 4 (P = 64 Hc Wc)
@@ -327,7 +310,7 @@ __global__ __launch_bounds__(NMS_T) void k_kp_nms(int Hh, int Wh, int H, int W, 
         s_base = acc;
     }
     __syncthreads();
-    const bool lds_path = s_base <= NC_LDS && Hh <= ROW_LDS && !KP_NMS_GLOBAL;  // block-uniform
+    const bool lds_path = s_base <= NC_LDS && Hh <= ROW_LDS;  // block-uniform
     {
         const int off = wsum[w];
         for (int i = lane; i < cntw; i += 64) {
@@ -365,7 +348,6 @@ __global__ __launch_bounds__(NMS_T) void k_kp_nms(int Hh, int Wh, int H, int W, 
     //     keeps those without any; later rounds only read the listed neighbours' states.
     const int d = nms_dist;
     __syncthreads();
-    const long long tk1 = KP_TRACE ? clock64() : 0;
     for (int k = t; k < nc; k += NMS_T) {
         const int pk = cpix[k];
         const float ck = cconf[k];
@@ -383,11 +365,8 @@ __global__ __launch_bounds__(NMS_T) void k_kp_nms(int Hh, int Wh, int H, int W, 
             else st[pk] = 1;
         }
     }
-    int rounds = 0;
     __syncthreads();
-    const long long tk2 = KP_TRACE ? clock64() : 0;
     for (;;) {
-        rounds++;
         if (t == 0) s_flag = 0;
         __syncthreads();
         int undecided = 0;
@@ -444,7 +423,6 @@ __global__ __launch_bounds__(NMS_T) void k_kp_nms(int Hh, int Wh, int H, int W, 
     }
 
     // (c) survivors inside the border; slot = rank (confidence desc, ties reversed row-major)
-    const long long tk3 = KP_TRACE ? clock64() : 0;
     if (t == 0) s_nk = 0;
     __syncthreads();
     for (int k = t; k < nc; k += NMS_T) {
@@ -528,9 +506,6 @@ __global__ __launch_bounds__(NMS_T) void k_kp_nms(int Hh, int Wh, int H, int W, 
         num_kp[b] = min(nk, cap);
         status[b] = nk > cap ? MV_ERR_CAPACITY : MV_OK;
     }
-    if (KP_TRACE && b == 0 && t == 0)
-        printf("nms phases (clk): compact %lld list %lld rounds %lld (%d) survivors+sort %lld  nc %d nk %d\n",
-               tk1 - tk0, tk2 - tk1, tk3 - tk2, rounds, clock64() - tk3, nc, nk);
 }
 
 // grid_sample's coordinate arithmetic for a keypoint at heatmap pixel pix (row-major, Wh
@@ -796,8 +771,8 @@ extern "C" int mv_keypoints_dev(mv_context *ctx, const mv_kp_params *p, int batc
     const long waves = (long)batch * cap;
     if (kp_planes_path(Hc, Wc)) {
         MV_PROF_BEGIN(s, "k_kp_sample_planes");
-        if (KP_PLANE_CELLS_S && HW <= KP_PLANE_CELLS_S)
-            hipLaunchKernelGGL((k_kp_sample_planes<KP_CH, (KP_PLANE_CELLS_S ? KP_PLANE_CELLS_S : 1)>),
+        if (HW <= KP_PLANE_CELLS_S)
+            hipLaunchKernelGGL((k_kp_sample_planes<KP_CH, KP_PLANE_CELLS_S>),
                                dim3((unsigned)batch * (256 / KP_CH)), dim3(256), 0, s, batch, cap, Hc, Wc, H, W, Wc * 8,
                                num_kp, m.slot_pix, coarse_desc, desc);
         else

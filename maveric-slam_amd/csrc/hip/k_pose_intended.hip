@@ -42,20 +42,13 @@
 namespace {
 
 constexpr int NT = 256;
-// timing experiments only (wrong results): skip the GN per-point pass / reduction / solve
-#ifndef PE_TRACE
-#define PE_TRACE 0  // printf per-phase clock64() deltas of block 0 (timing experiments only)
-#endif
-#ifndef PE_PREM
 // correspondences in the preemptive scoring subset of the 256 hypotheses (the 8 survivors are then
 // scored on all).  Same-box A/B (profiles/r05u_pose_prem_ab.log): 128 / 64 / 32 points -- exact
 // data 0.498 / 0.442 / 0.415 ms, 0.5 px + 20 % outliers 0.996 / 0.939 / 0.905 ms per 8192 pairs,
 // pose errors unchanged (realistic line p99: rotation 0.085 / 0.086 / 0.086 deg, translation
 // direction 2.51 / 2.54 / 2.56 deg), every pose test green; 64 kept (the subset still ranks
 // hypotheses under heavier contamination than the bench's)
-#define PE_PREM 64
-#endif
-#ifndef PE_WAVES
+constexpr int PE_PREM = 64;
 // waves per SIMD, a lower bound.  Built without SLP packing (Makefile, profiles/r05al_pose_noslp_ab.log)
 // the kernel takes 119 VGPRs and no scratch, i.e. 4 waves per SIMD either way; the history below is
 // that of the SLP-packed build, whose cross-stream nondeterminism went with the packing.
@@ -70,8 +63,7 @@ constexpr int NT = 256;
 // start refined by ONE wave with wave reductions and no block barrier at all: 1.046-1.050 vs
 // 0.995-0.996 ms noisy, 0.516-0.517 vs 0.494 exact -- the per-point passes, not the barriers, set
 // the pace -- profiles/r05r_pose_wavegn_ab.log.)
-#define PE_WAVES 3
-#endif
+constexpr int PE_WAVES = 3;
 constexpr int MAXP = 4096;  // correspondences per pair held in LDS (float4 each)
 
 __device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
@@ -235,7 +227,7 @@ __device__ __forceinline__ F3 mul_sym(const float A[3][3], const F3 &x) {
 // The two leading eigenvectors (v1: largest eigenvalue) of the symmetric PSD 3x3 A, in
 // closed form and float (E is a float estimate; the Gauss-Newton stage refines the pose
 // in float from here).  Replaces a cyclic Jacobi in double, whose serial sweeps on one
-// lane cost ~17k of the block's ~133k cycles (this: ~3k, measured with PE_TRACE):
+// lane cost ~17k of the block's ~133k cycles (this: ~3k; per-phase clock64() stamps, round 3):
 //   - the smallest eigenvalue from the trigonometric solution of the characteristic
 //     cubic: for an essential matrix (l1 = l2, r = -1) l3 = q + 2p cos(pi - d) is flat
 //     in d, so the angle's rounding enters squared;
@@ -413,7 +405,6 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
     __shared__ int wsum[4];
     const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int n_in = min(max(nv[b], 0), a.cap);
-    const long long tk0 = PE_TRACE ? clock64() : 0;
 
     // ---- 1. compaction (query order) + normalisation ----
     const int per = (n_in + NT - 1) / NT;
@@ -500,7 +491,6 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
         return;
     }
 
-    const long long tk1 = PE_TRACE ? clock64() : 0;
     // ---- 2. hypotheses, preemptively MSAC-scored (sum of min(Sampson^2, thr^2); plain
     //         inlier counting cannot separate an outlier-contaminated 8-point solution that
     //         still explains every inlier within the band -- near-pure forward motion).
@@ -564,7 +554,6 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
             for (int r = 0; r < 9; r++) best_e[r] = e[r];
         }
     }
-    const long long tk2 = PE_TRACE ? clock64() : 0;
     // ---- 3. survivors: the SURV lowest (partial cost, hypothesis id) keys of each wave (cost
     //         >= 0, so its bits order as uint), then full MSAC of the NS survivors ----
     __shared__ int s_sh[NS];
@@ -695,8 +684,6 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
     const float th_max = sqrtf(a.thr2), th_min = 0.01f * th_max, r_cap = 3.f * th_max;
     float bR[9], bT[3], bcost = __builtin_inff();
     int bn = 0;
-    const long long tk3 = PE_TRACE ? clock64() : 0;
-    long long tk4 = 0, tk5 = 0;
     // the schedule as a compile-time parameter: each gets its own code (constant strides)
     auto refine = [&](auto par_c) {
     constexpr bool par = decltype(par_c)::value;
@@ -766,7 +753,6 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
                 votes[c] += (det > 0.f && n1 > 0.f && n2 > 0.f) ? 1 : 0;
             }
         }
-        if (PE_TRACE && rd == 0) tk4 = clock64();
 #pragma unroll
         for (int c = 0; c < 4; c++) {
             int v = votes[c];
@@ -788,7 +774,6 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
                 bc = c;
             }
         }
-        if (PE_TRACE && rd == 0) tk5 = clock64();
 
         // ---- robust Gauss-Newton: iteratively reweighted, Cauchy weights 1 / (1 + (r / c)^2)
         //      on the Sampson residuals below 3 thr (none above), the scale c_0 = thr,
@@ -1053,11 +1038,6 @@ __global__ __launch_bounds__(NT, PE_WAVES) void k_pose_ransac(PoseArgs a, const 
         num_inliers[b] = bn;
         if (num_matches) num_matches[b] = n_all;
         status[b] = MV_OK;
-    }
-    if (PE_TRACE && b == 0 && t == 0) {
-        const long long tk6 = clock64();
-        printf("pose phases (clk): compact %lld hyp+score %lld argmin %lld decomp %lld cheir %lld gn %lld\n",
-               tk1 - tk0, tk2 - tk1, tk3 - tk2, tk4 - tk3, tk5 - tk4, tk6 - tk5);
     }
 }
 

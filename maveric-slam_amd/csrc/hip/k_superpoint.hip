@@ -49,7 +49,6 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int SP_NT = 256;          // 4 waves
-constexpr int TX = 32;  // the 1 x 1 heads' tile width (k_sp_conv: SpGeo)
 
 // Requantisation, bit-identical to clamp(rint((float) a * rs), lo, 127): the product rounded to
 // float, + 1.5 * 2^23 rounds it to an integer (round to nearest even) held in the low mantissa
@@ -114,61 +113,14 @@ struct Conv1aArgs {
     int H, W;  // source frame
     float in_inv, rs;
     const int *wpk, *bq;
-    const int8_t *qimg;  // SP_PRERESIZE: the resized, quantised frames [B][H][W] (k_sp_resize_q)
 };
 
-#ifndef SP_PRERESIZE
-// 1: the frames are resized + quantised ONCE per pixel by k_sp_resize_q (one pass, 4 byte
-// gathers per pixel) and conv1's workgroups load their tile + 2 pixels from it; 0: every
-// workgroup resizes its own tile + 2 pixels (1.4x the pixels, and the gathers + ~10 VALU per
-// pixel sit in the VALU-bound conv1 kernel).  Measured (profiles/r04s_sp_preresize_ab.log, one
-// box, bit-exact either way): 75.4-76.6 k frames/s against 76.7-76.8 k fused -- no gain, off
-#define SP_PRERESIZE 0
-#endif
-// F.interpolate (bilinear, align_corners=False, antialias=False) of the frame / 255 to H x W and
-// the input quantisation rint(x / in_scale) clamped to int8 -- exactly the fused path's
-// arithmetic (k / 255 by IEEE division from a table, the same fma chain and rounding)
-__global__ __launch_bounds__(256) void k_sp_resize_q(const uint8_t *__restrict__ img, int Hs, int Ws, int H, int W,
-                                                     float in_inv, long total, int8_t *__restrict__ q) {
-    __shared__ float lut[256];
-    const int t = threadIdx.x;
-    lut[t] = (float)t / 255.0f;
-    __syncthreads();
-    const long i = (long)blockIdx.x * 256 + t;
-    if (i >= total) return;
-    const long hw = (long)H * W;
-    const long b = i / hw;
-    const int p = (int)(i - b * hw), y = p / W, x = p - (p / W) * W;
-    const float sy = (float)Hs / (float)H, sx = (float)Ws / (float)W;
-    int ya, yb, xa, xb;
-    const float h1 = sp_src(sy, y, Hs, ya, yb), w1 = sp_src(sx, x, Ws, xa, xb);
-    const float h0 = 1.f - h1, w0 = 1.f - w1;
-    const uint8_t *im = img + b * Hs * Ws;
-    const float a00 = lut[im[ya * Ws + xa]], a01 = lut[im[ya * Ws + xb]];
-    const float a10 = lut[im[yb * Ws + xa]], a11 = lut[im[yb * Ws + xb]];
-    const float t0 = __builtin_fmaf(a00, w0, a01 * w1);
-    const float t1 = __builtin_fmaf(a10, w0, a11 * w1);
-    const float v = __builtin_fmaf(t0, h0, t1 * h1);
-    float qv = __builtin_rintf(v * in_inv);
-    qv = fminf(fmaxf(qv, -128.f), 127.f);
-    q[i] = (int8_t)(int)qv;
-}
-
-#ifndef SP_KSB
-#define SP_KSB 1  // a scheduling barrier after each k32 step of k_sp_conv's K loop (0: free scheduling, A/B)
-#endif
-#ifndef SP_LIF64
-#define SP_LIF64 8  // the 64-channel layers' 16-B tile loads in flight per thread (A/B)
-#endif
-#ifndef SP_PRIO
-#define SP_PRIO 0  // 1: s_setprio 1 over k_sp_conv's K loop (A/B)
-#endif
-#ifndef SP_BPF
-#define SP_BPF 0  // 1: k_sp_conv's B fragments one k32 step ahead (A/B)
-#endif
-#ifndef SP_OCC64
-#define SP_OCC64 3  // workgroups per CU for the 64-channel layers (LDS 50 KB; VGPRs <= 168)
-#endif
+// workgroups per CU for the 64-channel layers (LDS 50 KB; VGPRs <= 168; 2 per CU measured 4-6 %
+// slower, profiles/r05f_sp_geo_ab.log).  Measured and left out (profiles/r05x, r05aa): B fragments a
+// k32 step ahead, s_setprio 1 over the K loop, 10 tile loads in flight, free scheduling of the K loop
+// (no sched_barrier per k32 step), the frames resized once per pixel by a separate pass
+// (profiles/r04s_sp_preresize_ab.log) -- all within noise or slower.
+constexpr int SP_OCC64 = 3;
 // Tile geometry.  GEO 0: 16 x 32 output pixels, a wave's 4 MFMA pixel blocks are its 4 rows of
 // 32.  GEO 1 (the 24 x 80 layers: conv4a/b, convPa/Da at 192 x 640): 24 x 16 pixels, a wave's 3
 // blocks are 2 rows x 16 columns each (lane fr -> row fr >> 4, column fr & 15), so 24 x 80 is 5
@@ -186,7 +138,7 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
     static_assert(GEO == 0 || (CIN != 64 && !POOL && OMODE == 0 && !FUSE1A), "GEO 1: the 128-channel unpooled layers");
     constexpr int TY = G::TY, TX = G::TX, JN = G::JN, RB = G::RB, WR = G::WR;
     constexpr int P = KS / 2, IY = TY + 2 * P, IX = TX + 2 * P, NCH = CIN / 16, NS = KS * KS * CIN / 32;
-    constexpr int PF = (CIN == 64 && SP_OCC64 > 2) ? 2 : 4;  // weight fragments in flight (k32 steps)
+    constexpr int PF = CIN == 64 ? 2 : 4;  // weight fragments in flight (k32 steps)
     static_assert(CIN % 32 == 0 && NCH <= 16, "channels in 32-k steps, at most 256");
     // LDS tile layout.  64 channels: each pixel's 4 chunks padded to 5 (an odd stride: 16 lanes
     // reading one chunk of 16 consecutive pixels hit 16 distinct bank groups), so a B fragment's
@@ -238,15 +190,6 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
         // the bilinear source rows / columns of the tile's QY rows and QX columns, once per
         // workgroup: (weight of the far sample, its complement, near / far offsets)
         __shared__ float4 rowc[QY], colc[QX];
-        if (c1.qimg) {  // SP_PRERESIZE: the tile + 2 pixels from the pre-resized frame
-            const int8_t *qi = c1.qimg + (size_t)b * H * W;
-            for (int i = t; i < QY * QX; i += SP_NT) {
-                const int r = i / QX, c = i % QX;
-                const int gy = y0 + r - 2, gx = x0 + c - 2;
-                qim[r * QXS + c] = gy >= 0 && gy < H && gx >= 0 && gx < W ? qi[(size_t)gy * W + gx] : (int8_t)0;
-            }
-            __syncthreads();
-        } else {
         lut[t] = (float)t / 255.0f;
         const float sy = (float)c1.H / (float)H, sx = (float)c1.W / (float)W;
         if (t < QY) {
@@ -297,7 +240,6 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
             qim[r * QXS + c] = (int8_t)v;
         }
         __syncthreads();
-        }
         // conv1a + relu over the tile + halo on v_mfma_f32_32x32x16_f16: K = the 9 taps (+ 7 zero),
         // A = the weights (lanes < 32: taps 0-7, lanes >= 32: tap 8), B = 32 tile pixels' taps;
         // pixels outside the image are conv1b's zero padding, not conv1a evaluated there
@@ -366,7 +308,7 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
     // of 8 pixels instead -- conflict-free LDS stores -- made the 64-channel layers 3-4x slower:
     // the loads must stay lane-contiguous)
     const int8_t *src = in + (size_t)b * H * W * CIN;
-    constexpr int LIF = CIN == 64 ? SP_LIF64 : 8;  // 16-B loads in flight per thread (12 / 16 measured the same)
+    constexpr int LIF = 8;  // 16-B loads in flight per thread (10 / 12 / 16 measured the same)
     for (int i0 = 0; i0 < (FUSE1A ? 0 : NCHUNK); i0 += LIF * SP_NT) {
         i32x4 v[LIF];
 #pragma unroll
@@ -402,20 +344,12 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
     int xs[KS];
 #pragma unroll
     for (int kx = 0; kx < KS; kx++) xs[kx] = fh ^ (((pcol + kx) / SWS) & (NCH - 1));
-    // the B fragments of k32 step s (SP_BPF: those of step s + 1 read before step s's MFMAs, so
-    // the LDS latency hides under them)
+    // the B fragments of k32 step s
     auto bfrag = [&](int s, int j) {
         const int tap = s * 32 / CIN, ky = tap / KS, kx = tap % KS, c0 = (s * 32 % CIN) / 16;
         const int off = ((RB * j + ky) * IX + kx) * PS;
         return PADL ? lb[off + c0] : lb[off + (c0 ^ xs[kx])];
     };
-    if (SP_PRIO) __builtin_amdgcn_s_setprio(1);  // the K loop ahead of co-resident waves' VALU phases
-    constexpr bool BPF = SP_BPF && (CIN != 64 || SP_OCC64 <= 2);  // the 3-per-CU 64-channel build has no room
-    i32x4 bn[JN];
-    if (BPF) {
-#pragma unroll
-        for (int j = 0; j < JN; j++) bn[j] = bfrag(0, j);
-    }
 #pragma unroll
     for (int s = 0; s < NS; s++) {
         const i32x4 a0 = ra[s % PF], a1 = rb[s % PF];
@@ -425,19 +359,15 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
         }
         i32x4 bc[JN];
 #pragma unroll
-        for (int j = 0; j < JN; j++) {
-            bc[j] = BPF ? bn[j] : bfrag(s, j);
-            if (BPF && s + 1 < NS) bn[j] = bfrag(s + 1, j);
-        }
+        for (int j = 0; j < JN; j++) bc[j] = bfrag(s, j);
 #pragma unroll
         for (int j = 0; j < JN; j++) {
             acc[j][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bc[j], s == 0 ? b0 : acc[j][0], 0, 0, 0);
             acc[j][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bc[j], s == 0 ? b1 : acc[j][1], 0, 0, 0);
         }
-        if (SP_KSB) __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(0);  // one k32 step at a time
     }
 
-    if (SP_PRIO) __builtin_amdgcn_s_setprio(0);
     // ---- epilogue: lane = pixel fr of each row; 16 couts (4 groups of 4) per 32-cout block ----
     const int lo = SP_MAGIC_BITS + (RELU ? 0 : -128);
     if constexpr (CIN == 64) {
@@ -593,177 +523,11 @@ __global__ __launch_bounds__(SP_NT, CIN == 64 ? SP_OCC64 : 2) void k_sp_conv(con
     }
 }
 
-// The 1 x 1 heads (convPb, convDb: 256 input channels, no halo): a workgroup takes 8 x 32
-// pixels x 128 output channels; its 64 KiB input tile is staged into LDS with all 16 loads of a
-// thread in flight at once (each pixel's 16 chunks padded to 17: conflict-free fragment reads
-// at compile-time offsets), wave w owns tile rows 2w, 2w + 1 against 4 channel blocks (8 MFMAs
-// per k32 step); weights from L2 two steps ahead; the heads' outputs in the Frame layout
-// (OMODE 1) or, OMODE 2, already dequantised as run()'s NCHW float32 [B][C][H][W] (out is a
-// float *, cstride = C, dq = the head's out_scale: PyTorch's dequantise dq * (float) code).
-constexpr int H1_TY = 8, H1_PS = 17, H1_CB = 4;
-template <int OMODE>
-__global__ __launch_bounds__(SP_NT, 2) void k_sp_conv1x1(const int8_t *__restrict__ in, int H, int W,
-                                                         const i32x4 *__restrict__ wf, const int *__restrict__ bq,
-                                                         float rs, int ngroups, int tiles_x, int tiles_y,
-                                                         int8_t *__restrict__ out, int cstride, float dq) {
-    constexpr int NS = 8, NCH = 16, NCHUNK = H1_TY * TX * NCH;  // 256 channels
-    __shared__ i32x4 tile[H1_TY * TX * H1_PS];
-    int bid = blockIdx.x;
-    const int tx = bid % tiles_x;
-    bid /= tiles_x;
-    const int ty = bid % tiles_y;
-    bid /= tiles_y;
-    const int g = bid % ngroups, b = bid / ngroups;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6, fr = lane & 31, fh = lane >> 5;
-    const int y0 = ty * H1_TY, x0 = tx * TX;
-    // the first weight fragments and the bias (each chain's first C operand) before the tile
-    const i32x4 *wa = wf + (size_t)(H1_CB * g) * NS * 64 + lane;
-    i32x4 aq[3][H1_CB];
-#pragma unroll
-    for (int s = 0; s < 2; s++)
-#pragma unroll
-        for (int cb = 0; cb < H1_CB; cb++) aq[s][cb] = wa[(cb * NS + s) * 64];
-    i32x16 bvs[H1_CB];
-#pragma unroll
-    for (int cb = 0; cb < H1_CB; cb++)
-#pragma unroll
-        for (int qq = 0; qq < 4; qq++) {
-            const i32x4 x = *reinterpret_cast<const i32x4 *>(bq + 32 * (H1_CB * g + cb) + 8 * qq + 4 * fh);
-#pragma unroll
-            for (int e = 0; e < 4; e++) bvs[cb][4 * qq + e] = x[e];
-        }
-    {  // the tile: 16 chunks per thread, every load issued before the first store
-        i32x4 v[NCHUNK / SP_NT];
-#pragma unroll
-        for (int u = 0; u < NCHUNK / SP_NT; u++) {
-            const int i = u * SP_NT + t, c = i % NCH, px = i / NCH, x = px % TX, r = px / TX;
-            const int gy = min(y0 + r, H - 1), gx = min(x0 + x, W - 1);  // clamped: never stored
-            v[u] = *reinterpret_cast<const i32x4 *>(in + (((size_t)b * H + gy) * W + gx) * 256 + c * 16);
-        }
-#pragma unroll
-        for (int u = 0; u < NCHUNK / SP_NT; u++) {
-            const int i = u * SP_NT + t, c = i % NCH, px = i / NCH;
-            tile[px * H1_PS + c] = v[u];
-        }
-    }
-    __syncthreads();
-    i32x16 acc[2][H1_CB];  // from the quantised bias, as in k_sp_conv
-    const i32x4 *lb = tile + ((2 * w) * TX + fr) * H1_PS + fh;
-#pragma unroll
-    for (int s = 0; s < NS; s++) {
-        if (s + 2 < NS) {
-#pragma unroll
-            for (int cb = 0; cb < H1_CB; cb++) aq[(s + 2) % 3][cb] = wa[(cb * NS + s + 2) * 64];
-        }
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            const i32x4 bv = lb[j * TX * H1_PS + 2 * s];
-#pragma unroll
-            for (int cb = 0; cb < H1_CB; cb++)
-                acc[j][cb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aq[s % 3][cb], bv, s == 0 ? bvs[cb] : acc[j][cb], 0, 0, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    const int lo = SP_MAGIC_BITS - 128;  // the heads have no relu
-    if (OMODE == 1 && cstride % 16 != 0) {
-        // the semi head (65 channels, Frame layout: a cell's 65 B, a tile column's 8 cells
-        // consecutive): the outputs go through LDS in that order, then leave as whole column runs
-        // of 8 x 65 B with consecutive lanes on consecutive bytes (the direct form stored single
-        // bytes 65 B apart: one partial line per lane per store)
-        __syncthreads();  // every wave past its last read of the input tile
-        int8_t *stg = reinterpret_cast<int8_t *>(tile);
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            int8_t *cell = stg + (fr * H1_TY + 2 * w + j) * cstride;
-#pragma unroll
-            for (int cb = 0; cb < H1_CB; cb++)
-#pragma unroll
-                for (int qq = 0; qq < 4; qq++) {
-                    const int co = 32 * (H1_CB * g + cb) + 8 * qq + 4 * fh;
-                    if (co >= cstride) continue;
-                    int v[4];
-                    requant4(v, acc[j][cb][4 * qq], acc[j][cb][4 * qq + 1], acc[j][cb][4 * qq + 2], acc[j][cb][4 * qq + 3], rs, lo);
-#pragma unroll
-                    for (int e = 0; e < 4; e++)
-                        if (co + e < cstride) cell[co + e] = (int8_t)v[e];
-                }
-        }
-        __syncthreads();
-        const int run = H1_TY * cstride, nb = min(H1_TY, H - y0) * cstride;  // a column's bytes, inside
-        for (int col = w; col < TX; col += SP_NT / 64) {  // a wave per column, lanes on bytes
-            const int gx = x0 + col;
-            if (gx >= W) break;
-            int8_t *gd = out + ((size_t)b * H * W + (size_t)gx * H + y0) * cstride;
-            const int8_t *ls = stg + col * run;
-            for (int o = lane; o < nb; o += 64) gd[o] = ls[o];
-        }
-        return;
-    }
-    if (OMODE == 2) {
-        // channel plane co: lanes fr = 0..31 on 32 consecutive pixels of a row (128 B per half-wave)
-        float *fo = reinterpret_cast<float *>(out);
-        const size_t plane = (size_t)H * W;
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            const int gy = y0 + 2 * w + j, gx = x0 + fr;
-            if (gy >= H || gx >= W) continue;
-            float *px = fo + (size_t)b * cstride * plane + (size_t)gy * W + gx;
-#pragma unroll
-            for (int cb = 0; cb < H1_CB; cb++)
-#pragma unroll
-                for (int qq = 0; qq < 4; qq++) {
-                    const int co = 32 * (H1_CB * g + cb) + 8 * qq + 4 * fh;
-                    if (co >= cstride) continue;
-                    int v[4];
-                    requant4(v, acc[j][cb][4 * qq], acc[j][cb][4 * qq + 1], acc[j][cb][4 * qq + 2], acc[j][cb][4 * qq + 3], rs, lo);
-#pragma unroll
-                    for (int e = 0; e < 4; e++)
-                        if (co + e < cstride) px[(size_t)(co + e) * plane] = dq * (float)(v[e] - SP_MAGIC_BITS);
-                }
-        }
-        return;
-    }
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-        const int gy = y0 + 2 * w + j, gx = x0 + fr;
-        if (gy >= H || gx >= W) continue;
-        int8_t *dst = OMODE == 0 ? out + (((size_t)b * H + gy) * W + gx) * cstride
-                                 : out + ((size_t)b * H * W + (size_t)gx * H + gy) * cstride;
-#pragma unroll
-        for (int cb = 0; cb < H1_CB; cb++) {
-            if (cstride % 16 == 0 && 32 * (H1_CB * g + cb) < cstride) {  // convDb (256 channels)
-                int d[4];
-#pragma unroll
-                for (int qq = 0; qq < 4; qq++) {
-                    int v[4];
-                    requant4(v, acc[j][cb][4 * qq], acc[j][cb][4 * qq + 1], acc[j][cb][4 * qq + 2], acc[j][cb][4 * qq + 3], rs, lo);
-                    d[qq] = pack4b(v[0], v[1], v[2], v[3]);
-                }
-                *reinterpret_cast<i32x4 *>(dst + 32 * (H1_CB * g + cb) + 16 * fh) = regroup16(d);
-                continue;
-            }
-#pragma unroll
-            for (int qq = 0; qq < 4; qq++) {
-                const int co = 32 * (H1_CB * g + cb) + 8 * qq + 4 * fh;
-                if (co >= cstride) continue;
-                int v[4];
-                requant4(v, acc[j][cb][4 * qq], acc[j][cb][4 * qq + 1], acc[j][cb][4 * qq + 2], acc[j][cb][4 * qq + 3], rs, lo);
-                if (OMODE == 0 || (cstride % 4 == 0 && co + 4 <= cstride)) {
-                    *reinterpret_cast<int *>(dst + co) = pack4b(v[0], v[1], v[2], v[3]);
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 4; e++)
-                        if (co + e < cstride) dst[co + e] = (int8_t)v[e];
-                }
-            }
-        }
-    }
-}
-
-// The 1 x 1 heads as a weight-stationary pass (SP_HEAD 1).  The heads are data movement: 256 B
-// of input per pixel against 65 / 256 outputs, ~2 k MFMA cycles per 64 KiB tile -- k_sp_conv1x1's
-// 576 / 1152 tile workgroups (2 per CU) ran 1.1 / 2.3 rounds of load-then-compute each (25 / 28
-// us per 64 frames, profiles/r05w_sp_layers.txt).  Here a workgroup keeps its share of the
+// The 1 x 1 heads (convPb, convDb: 256 input channels, no halo) as a weight-stationary pass.  The
+// heads are data movement: 256 B of input per pixel against 65 / 256 outputs, ~2 k MFMA cycles per
+// 64 KiB tile -- round 4's tiled k_sp_conv1x1 (8 x 32 pixels x 128 channels per workgroup, in git
+// history up to round 5) ran its 576 / 1152 tile workgroups (2 per CU) in 1.1 / 2.3 rounds of
+// load-then-compute each (25 / 28 us per 64 frames, profiles/r05w_sp_layers.txt).  Here a workgroup keeps its share of the
 // weights in registers (wave w: channel blocks CBW w .. CBW w + CBW - 1, 8 k32 fragments each)
 // and streams HD_NB consecutive 32-pixel blocks through a double-buffered LDS tile, the loads of
 // the next HD_D blocks in flight in registers while a block is multiplied -- straight-line code
@@ -771,17 +535,11 @@ __global__ __launch_bounds__(SP_NT, 2) void k_sp_conv1x1(const int8_t *__restric
 // follow the output order: Frame cells (x H + y) for OMODE 1, so a block's semi outputs are
 // 32 x 65 contiguous bytes (staged in LDS, stored as whole words by the next block), row-major
 // pixels for OMODE 2 (run()'s NCHW planes: 32 consecutive floats per channel).  The integer
-// products, bias and requantisation are k_sp_conv1x1's: bit-identical.
-#ifndef SP_HEAD
-#define SP_HEAD 1  // 0: k_sp_conv1x1 (A/B)
-#endif
-#ifndef SP_HEAD_PRES
-#define SP_HEAD_PRES 1  // 0: the presence masks by k_sp_presence after the heads (A/B)
-#endif
-#ifndef SP_HD_NB
-#define SP_HD_NB 8  // 32-pixel blocks per k_sp_head workgroup (4 / 16 measured 1-2 % slower: profiles/r05ak_sp_head_nb_ab.log)
-#endif
-constexpr int HD_PS = 17, HD_D = 3, HD_NB = SP_HD_NB;
+// products, bias and requantisation are those of the 3 x 3 layers' epilogue: outputs in the Frame
+// layout (OMODE 1) or, OMODE 2, already dequantised as run()'s NCHW float32 [B][C][H][W] (out is a
+// float *, cstride = C, dq = the head's out_scale: PyTorch's dequantise dq * (float) code).
+// HD_NB: 32-pixel blocks per workgroup (4 / 16 measured 1-2 % slower: profiles/r05ak_sp_head_nb_ab.log).
+constexpr int HD_PS = 17, HD_D = 3, HD_NB = 8;
 constexpr int SP_MG_CHUNKS = 32;  // presence-mask chunks per (frame, head): k_sp_presence's split
 // FULL: every frame whole blocks (H W % 32 == 0), every workgroup HD_NB of them and out 4-B
 // aligned -- no lane or block guards, so the loads stay in flight (a load under a branch is sunk
@@ -1148,30 +906,11 @@ int launch_conv(hipStream_t st, const mv_superpoint *net, int li, int B, int H, 
     return MV_OK;
 }
 
-template <int OMODE>
-int launch_conv1x1(hipStream_t st, const mv_superpoint *net, int li, int B, int H, int W, const int8_t *in,
-                   int8_t *out, int cstride, float dq = 0.f) {
-    const int tiles_x = (W + TX - 1) / TX, tiles_y = (H + H1_TY - 1) / H1_TY;
-    const int ngroups = (net->cout_pad[li] + 32 * H1_CB - 1) / (32 * H1_CB);
-    MV_REQUIRE(net->cout_pad[li] % (32 * H1_CB) == 0);  // whole 128-channel groups (65 -> 128, 256)
-    MV_REQUIRE(!(OMODE == 1 && cstride % 16 != 0) || (long)TX * H1_TY * cstride <= (long)H1_TY * TX * H1_PS * 16);
-    const long blocks = (long)B * ngroups * tiles_y * tiles_x;
-    MV_REQUIRE(blocks < (1l << 31));
-    const char *wd = static_cast<const char *>(net->wdev);
-    hipLaunchKernelGGL((k_sp_conv1x1<OMODE>), dim3((unsigned)blocks), dim3(SP_NT), 0, st, in, H, W,
-                       reinterpret_cast<const i32x4 *>(wd + net->frag_off[li]),
-                       reinterpret_cast<const int *>(wd + net->bq_off[li]), net->rs[li], ngroups, tiles_x, tiles_y,
-                       out, cstride, dq);
-    MV_LAUNCH_CHECK();
-    return MV_OK;
-}
-
-// the heads through k_sp_head (SP_HEAD) or k_sp_conv1x1
+// the heads through k_sp_head
 template <int OMODE>
 int launch_head(hipStream_t st, const mv_superpoint *net, int li, int B, int H, int W, const int8_t *in, int8_t *out,
                 int cstride, float dq = 0.f, unsigned *pres = nullptr, bool *pres_done = nullptr) {
     if (pres_done) *pres_done = false;
-    if (!SP_HEAD) return launch_conv1x1<OMODE>(st, net, li, B, H, W, in, out, cstride, dq);
     const int HW = H * W, nblk_f = (HW + 31) / 32;
     const long nblk = (long)B * nblk_f;
     MV_REQUIRE((long)B * HW * 256 < (1l << 40) && nblk > 0 && nblk < (1l << 31) - HD_NB);
@@ -1181,7 +920,7 @@ int launch_head(hipStream_t st, const mv_superpoint *net, int li, int B, int H, 
     const i32x4 *wf = reinterpret_cast<const i32x4 *>(wd + net->frag_off[li]);
     const int *bq = reinterpret_cast<const int *>(wd + net->bq_off[li]);
     const bool full = HW % 32 == 0 && nblk % HD_NB == 0 && ((uintptr_t)out & 3) == 0;
-    const bool fuse = OMODE == 1 && pres && full && nblk_f >= HD_NB && SP_HEAD_PRES;
+    const bool fuse = OMODE == 1 && pres && full && nblk_f >= HD_NB;
 #define MV_HEAD(NCB, FULL, PRES)                                                                                   \
     hipLaunchKernelGGL((k_sp_head<OMODE, NCB, FULL, PRES>), dim3(grid), dim3(SP_NT), 0, st, in, H, W, nblk_f,         \
                        (int)nblk, wf, bq, net->rs[li], out, cstride, dq, pres)
@@ -1208,14 +947,11 @@ int launch_head(hipStream_t st, const mv_superpoint *net, int li, int B, int H, 
 
 // the 128-channel unpooled layers: the tile geometry covering H x W with fewer padded pixels
 // (GEO 1 wins at 24 x 80: 1920 against 3072)
-#ifndef SP_GEO
-#define SP_GEO 1  // 0: always the 16 x 32 tiles (A/B)
-#endif
 template <int CIN, int KS, bool POOL, bool RELU, int OMODE>
 int launch_conv_geo(hipStream_t st, const mv_superpoint *net, int li, int B, int H, int W, const int8_t *in,
                     int8_t *out, int cstride) {
     auto area = [&](int ty, int tx) { return (long)((H + ty - 1) / ty) * ty * ((W + tx - 1) / tx) * tx; };
-    if (SP_GEO && area(SpGeo<1>::TY, SpGeo<1>::TX) < area(SpGeo<0>::TY, SpGeo<0>::TX))
+    if (area(SpGeo<1>::TY, SpGeo<1>::TX) < area(SpGeo<0>::TY, SpGeo<0>::TX))
         return launch_conv<CIN, KS, POOL, RELU, OMODE, false, 1>(st, net, li, B, H, W, in, out, cstride);
     return launch_conv<CIN, KS, POOL, RELU, OMODE, false, 0>(st, net, li, B, H, W, in, out, cstride);
 }
@@ -1347,16 +1083,8 @@ int sp_network(hipStream_t st, mv_superpoint *net, int batch, int H, int W, int 
     int h = oh, w = ow;
     MV_PROF_BEGIN(st, "k_sp_conv");
     {
-        // SP_PRERESIZE: the resized, quantised frames in A (free until conv2a writes it)
-        const long total = (long)batch * h * w;
-        if (SP_PRERESIZE) {
-            MV_REQUIRE(total < (1l << 40) && (total + 255) / 256 < (1l << 31));
-            hipLaunchKernelGGL(k_sp_resize_q, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, images, H, W, h,
-                               w, net->in_inv, total, A);
-            MV_LAUNCH_CHECK();
-        }
         const Conv1aArgs c1{images, H, W, net->in_inv, net->rs[0], reinterpret_cast<const int *>(wd + net->frag_off[0]),
-                            reinterpret_cast<const int *>(wd + net->bq_off[0]), SP_PRERESIZE ? A : nullptr};
+                            reinterpret_cast<const int *>(wd + net->bq_off[0])};
         if ((r = launch_conv<64, 3, true, true, 0, true>(st, net, 1, batch, h, w, nullptr, Bf, 64, c1)) != MV_OK)
             return r;
     }

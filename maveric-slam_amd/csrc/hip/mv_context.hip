@@ -60,24 +60,38 @@ int quiesce(mv_context *ctx) {
     return MV_OK;
 }
 
-// true when `s` is being captured into a graph -- or when the query itself is refused, which is
-// what the legacy NULL stream answers while another stream captures in global mode: no event may
-// then be recorded on it or waited for by it (a record on the legacy stream, or an uncaptured
-// event waited for by a capturing stream, invalidates the capture; a wait of own_stream on an
-// event recorded inside a capture pulls own_stream into it, unjoined)
-bool capturing(hipStream_t s) {
+// *cap = whether `s` is being captured into a graph.  A query refused with a capture error is also
+// "capturing": that is what the legacy NULL stream answers while another stream captures in global
+// mode, and no event may then be recorded on it or waited for by it (a record on the legacy stream,
+// or an uncaptured event waited for by a capturing stream, invalidates the capture; a wait of
+// own_stream on an event recorded inside a capture pulls own_stream into it, unjoined).  Any other
+// refusal (an invalid or destroyed stream handle) is reported, not taken for a capture: skipping the
+// event record / wait would leave the context's reused scratch unordered.
+int capture_state(hipStream_t s, bool *cap) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &st) != hipSuccess) {
-        (void)hipGetLastError();  // clear the sticky query error
-        return true;
+    const hipError_t e = hipStreamIsCapturing(s, &st);
+    if (e == hipSuccess) {
+        *cap = st != hipStreamCaptureStatusNone;
+        return MV_OK;
     }
-    return st != hipStreamCaptureStatusNone;
+    (void)hipGetLastError();  // clear the sticky query error
+    if (e == hipErrorStreamCaptureImplicit || e == hipErrorStreamCaptureUnsupported ||
+        e == hipErrorStreamCaptureInvalidated || e == hipErrorStreamCaptureWrongThread) {
+        *cap = true;
+        return MV_OK;
+    }
+    *cap = false;
+    set_error(MV_ERR_HIP, "hipStreamIsCapturing: %s", hipGetErrorString(e));
+    return MV_ERR_HIP;
 }
 
 // the context moves off `old`: own_stream waits for everything issued on it so far (not when
 // `old` is being captured: the graph's launches are the caller's to order, see maveric_hip.h)
 static int retire_stream(mv_context *ctx, hipStream_t old) {
-    if (old == ctx->own_stream || capturing(old)) return MV_OK;
+    if (old == ctx->own_stream) return MV_OK;
+    bool cap = false;
+    const int rc = capture_state(old, &cap);
+    if (rc != MV_OK || cap) return rc;
     if (!ctx->ev_retire) MV_HIP_TRY(hipEventCreateWithFlags(&ctx->ev_retire, hipEventDisableTiming));
     MV_HIP_TRY(hipEventRecord(ctx->ev_retire, old));
     MV_HIP_TRY(hipStreamWaitEvent(ctx->own_stream, ctx->ev_retire, 0));
@@ -205,7 +219,12 @@ int mv_context_destroy(mv_context *ctx) {
 
 int mv_context_set_stream(mv_context *ctx, void *s) {
     MV_REQUIRE(ctx != nullptr);
-    if ((hipStream_t)s != ctx->stream && mv::capturing((hipStream_t)s)) {
+    bool cap_new = false;
+    if ((hipStream_t)s != ctx->stream) {
+        const int rc = mv::capture_state((hipStream_t)s, &cap_new);
+        if (rc != MV_OK) return rc;
+    }
+    if ((hipStream_t)s != ctx->stream && cap_new) {
         // onto a capture stream: no event on either stream (a record on the legacy NULL stream
         // during a global-mode capture invalidates it); the caller has synchronised before capturing
         ctx->stream = (hipStream_t)s;
@@ -219,7 +238,10 @@ int mv_context_set_stream(mv_context *ctx, void *s) {
         // images) are reused by its next launch.  Not across a capture: entering one, the caller
         // has ordered the capture stream after the earlier work (a capture cannot wait for an
         // uncaptured event); leaving one, nothing outside the graph can wait for it.
-        if (!mv::capturing(ctx->stream)) {
+        bool cap_old = false;
+        const int rc = mv::capture_state(ctx->stream, &cap_old);
+        if (rc != MV_OK) return rc;
+        if (!cap_old) {
             if (!ctx->ev_retire) MV_HIP_TRY(hipEventCreateWithFlags(&ctx->ev_retire, hipEventDisableTiming));
             MV_HIP_TRY(hipEventRecord(ctx->ev_retire, ctx->stream));
             MV_HIP_TRY(hipStreamWaitEvent((hipStream_t)s, ctx->ev_retire, 0));

@@ -47,7 +47,7 @@ void set_error(int status, const char *fmt, ...);
 int set_status(int status);
 
 // true while `s` is captured into a graph (or the query is refused: see mv_context.hip)
-bool capturing(hipStream_t s);
+int capture_state(hipStream_t s, bool *cap);  // MV_OK + *cap, or MV_ERR_HIP (reported)
 // Grow (never shrink) the context scratch; returns nullptr on failure.
 void *scratch(mv_context *ctx, size_t bytes);
 void *stage(mv_context *ctx, size_t bytes);

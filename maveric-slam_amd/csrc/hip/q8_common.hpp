@@ -144,8 +144,7 @@ __device__ __forceinline__ float exact_dot(const float *__restrict__ a, const fl
     }
     return s;
 }
-#ifndef Q8_COOP
-// 1: the deferred maximiser re-scores load their rows COOPERATIVELY (coop_exact_dots) with
+// The deferred maximiser re-scores load their rows COOPERATIVELY (coop_exact_dots) with
 // Q8_COOP_PD 16-float chunks in flight.  Why: exact_dot's per-lane loads put 64 different rows
 // (64 cache lines) under every load instruction, so a wave's re-scores cost ~38 x 128 line
 // lookups of the L1 -- the near-threshold epilogue ran ~40 k cycles per wave, line-rate bound;
@@ -154,11 +153,7 @@ __device__ __forceinline__ float exact_dot(const float *__restrict__ a, const fl
 // rounds of PD chunks kept as a loop, PD = 2 (17 spills, fewer than exact_dot's build): one box
 // (profiles/r04n_coop_depth_ab.log) with scores 5.63-5.66 vs 5.85-5.86 ms, near threshold
 // 5.25-5.26 vs 5.30, headline 4.27-4.30 vs 4.34-4.35; PD = 4 spills 130 and loses 30 %.
-#define Q8_COOP 1
-#endif
-#ifndef Q8_COOP_PD
-#define Q8_COOP_PD 2
-#endif
+constexpr int Q8_COOP_PD = 2;
 // The reference's sequential fp32 dot for the wave's 64 (row, column) pairs at once -- lane L's
 // pair: A row `arow`, B row `bcol` (< 0: none) -- with the rows' bytes loaded COOPERATIVELY: per
 // 16-float chunk, each load instruction takes 16 pairs' 64-B segments (4 lanes per segment, 16
@@ -257,15 +252,15 @@ __device__ __forceinline__ bool better(int dmode, float v, int j, float bv, int 
 //      rowv[r] = (|a|^2, s_a); s_a < 0 marks a row for the exact path (non-finite, zero or out
 //      of range).  AI8 (sequence mode): the rows arrive already quantised by k_q8_split (q0,
 //      s0, |a|^2, pair flag bad0) and are copied (256 B per row). ----
-//      EA: also rowe[r] = |rho|^2, the row's quantisation residual in code units (rho_k = a_k q -
-//      c_k, from the same magic sum), so that the epilogue's A term is s_a |rho| + |1 - q s_a| |a|
-//      instead of the worst case 8 s_a (every component off by half a step).
 //      NG: 32-row groups (RG = 2 for the 64-row waves; k_q8t_match's 128-row waves take 4).
-template <bool AI8, int QB = 4, bool EA = false, int NG = RG>  // QB: row quads (4 loads per lane each) in flight
+//      (Measured and not kept, round 4: the row's own quantisation residual |rho| measured here for
+//      the epilogue's A term instead of the worst case 8 s_a -- 0.7 % faster near the threshold,
+//      3 % slower on the headline.)
+template <bool AI8, int QB = 4, int NG = RG>  // QB: row quads (4 loads per lane each) in flight
 __device__ __forceinline__ void a_phase(char *img, float2 *rowv, int rbase, int row0, int n0, int lane,
                                         const float *__restrict__ A, const char *__restrict__ QA,
                                         const float *__restrict__ s0p, const float *__restrict__ na2p, bool bad0,
-                                        i32x4 (&aI)[NG][KD / 32], float *rowe = nullptr) {
+                                        i32x4 (&aI)[NG][KD / 32]) {
     const int fr = lane & 31, fh = lane >> 5;
     const int sub = lane & 15, rq = lane >> 4;
 #pragma unroll
@@ -326,22 +321,6 @@ __device__ __forceinline__ void a_phase(char *img, float2 *rowv, int rbase, int 
                     const float q = m > 0.f ? 127.f * __builtin_amdgcn_rcpf(m) : 0.f;
                     const bool afull = !(q2 <= FLT_MAX) || m < SCALE_LO || m > SCALE_HI;  // zero rows too
                     if (sub == 0) rowv[rbase + g * 32 + r] = make_float2(q2, afull ? -1.f : m * (1.f / 127.f));
-                    if constexpr (EA) {
-                        float r2 = 0.f;
-#pragma unroll
-                        for (int u = 0; u < 4; u++)
-#pragma unroll
-                            for (int i = 0; i < 4; i++) {
-                                const float f = __builtin_fmaf(x[qd][u][i], q, MAGIC_RNE);  // pack4's sum
-                                const float rho = __builtin_fmaf(x[qd][u][i], q, MAGIC_RNE - f);
-                                r2 = __builtin_fmaf(rho, rho, r2);
-                            }
-                        r2 += swz_xor<1>(r2);
-                        r2 += swz_xor<2>(r2);
-                        r2 += swz_xor<4>(r2);
-                        r2 += swz_xor<8>(r2);
-                        if (sub == 0) rowe[rbase + g * 32 + r] = r2;
-                    }
                     char *rowp = img + r * KD + 4 * (sub & 3);
 #pragma unroll
                     for (int u = 0; u < 4; u++)  // k = 4 sub + 64 u: chunk (sub >> 2) + 4 u
@@ -374,7 +353,7 @@ __device__ __forceinline__ void epilogue(char *epi, const float2 *rowv, float (&
                                          int row0, int n0, int n1, const float *__restrict__ A,
                                          const float *__restrict__ B, int *__restrict__ oidx,
                                          float *__restrict__ oscore, double thresh, int dmode, double bscale = 1.0,
-                                         const unsigned char *colsh = nullptr, const float *rowe = nullptr) {
+                                         const unsigned char *colsh = nullptr) {
     const int fr = lane & 31, fh = lane >> 5;
     const double u24 = 5.9604644775390625e-08;
     const double gam_e = KD * u24 / (1.0 - KD * u24);
@@ -450,10 +429,8 @@ __device__ __forceinline__ void epilogue(char *epi, const float2 *rowv, float (&
         if (live && !full) {
             const double s_a = (double)rv.y;
             const double an = sqrt(fmax((double)rv.x, 0.0)) * 1.0001;
-            // |eps_a| <= s_a |rho| + |1 - q s_a| |a| (|1 - q s_a| < 2^-21); |rho| <= 8 without rowe
-            // (rowe: the fp32 sum of the squared residuals, relative error < 2^-18)
-            const double ea = (rowe ? s_a * (sqrt((double)rowe[rl] * 1.0001) + 1e-15) : 8.001 * s_a) +
-                              4.76837158203125e-07 * an;
+            // |eps_a| <= s_a |rho| + |1 - q s_a| |a| (|1 - q s_a| < 2^-21), |rho| <= 8
+            const double ea = 8.001 * s_a + 4.76837158203125e-07 * an;
             const double dq = (an * Eb + ea * Bn + ea * Eb) * 1.0001;
             const double delta = dq + u24 * (an * Bn + dq) * 1.01 + gam_e * an * Bn + 1e-30;
             const double sa_k = s_a * bscale;  // screen units -> units of a.b
@@ -557,15 +534,8 @@ __device__ __forceinline__ void epilogue(char *epi, const float2 *rowv, float (&
     {
         const int Ih = fh ? need_g[1] : need_g[0];
         float e = 0.f;
-#if Q8_COOP
         if (__ballot(Ih >= 0))  // wave-uniform; the wave's own transpose slice is free by now
             e = coop_exact_dots(A, B, row0 + w * 64 + fh * 32 + fr, Ih, lane, mt);
-#else
-        if (Ih >= 0) {
-            const float *ap = A + (size_t)(row0 + w * 64 + fh * 32 + fr) * KD;
-            e = exact_dot(ap, B + (size_t)Ih * KD);
-        }
-#endif
         const float eo = __shfl_xor(e, 32, 64);
         const float e0 = fh ? eo : e, e1 = fh ? e : eo;
 #pragma unroll

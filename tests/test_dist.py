@@ -349,3 +349,73 @@ def test_two_rank_sequence_shards_gpu():
         assert ix == full[b].tolist(), b
         assert ix == oracle.allpairs_f32(D[b], D[b + 1], 0.8)[0].tolist(), b
     assert res[0] == res[1]
+
+
+def test_bench_dead_rank_fails_fast_and_drops_its_pairs():
+    """SURVEY §5 ("per-GPU worker failure = drop that GPU's pairs"), world size 3 over gloo: rank 1
+    dies abruptly in the middle of the timed steps (the MV_BENCH_KILL_RANK test hook, exit 17) while
+    the others wait in the per-step all-gather.  The spawning harness must notice within its grace
+    period -- not the 10-minute collective default -- stop the blocked survivors, exit non-zero, and
+    print a JSON line naming the dead rank, with the value computed from the surviving ranks' pairs."""
+    import json
+    import subprocess
+    import sys
+    import time
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MV_BENCH_KILL_RANK="1", MV_BENCH_KILL_STEP="2")
+    env.pop("WORLD_SIZE", None)
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "3", "--harness-cpu", "--batch", "3",
+                        "--kp", "32", "--steps", "6", "--warmup", "1", "--dist-timeout", "60", "--rank-grace", "2"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    took = time.time() - t0
+    assert r.returncode == 17, (r.returncode, r.stderr[-2000:])
+    assert took < 120, took
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["partial"] is True and d["n_gpus"] == 3
+    assert d["ranks_failed"][0]["rank"] == 1 and d["ranks_failed"][0]["exit"] == 17
+    assert "rank 1" in d["error"]
+    surv = {s["rank"]: s for s in d["ranks_surviving"]}
+    assert sorted(surv) == [0, 2]
+    # rank 1 died at its timed step 2: the survivors issued steps 0, 1 and were blocked in step 2's gather
+    assert all(s["steps_issued"] == 2 and s["pairs_per_step"] == 3 for s in surv.values())
+    assert d["value"] > 0
+    assert "MV_BENCH_KILL_RANK" in r.stderr
+
+
+def test_bench_names_every_rank_device_and_backend():
+    """the gathered per-rank record (rank, device, backend) that shows which ranks the collective saw"""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "3", "--harness-cpu", "--batch", "2",
+                        "--kp", "32", "--steps", "1", "--warmup", "0"], capture_output=True, text=True, timeout=240,
+                       env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert [x["rank"] for x in d["ranks"]] == [0, 1, 2]
+    assert all(x["backend"] == "gloo" for x in d["ranks"])
+    assert len({x["pid"] for x in d["ranks"]}) == 3
+
+
+def test_roofline_traffic_cites_the_newest_profile():
+    """bench.py's roofline.traffic comes from the newest matching profiles/r*_summary.json, newest by
+    round and tag (r05al after r05v, r06aa after r06z), not by a plain reverse name sort."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+
+    names = ["r05v_summary.json", "r05al_summary.json", "r06z_summary.json", "r06aa_summary.json", "r06_summary.json",
+             "r04zz_summary.json", "r06b_summary.json"]
+    got = sorted(names, key=bench.profile_order_key)
+    assert got == ["r04zz_summary.json", "r05v_summary.json", "r05al_summary.json", "r06_summary.json",
+                   "r06b_summary.json", "r06z_summary.json", "r06aa_summary.json"]
+    tr, src = bench.pmc_traffic("k_q8t_match", 8192, 1024, "i8", True)
+    assert src is None or (tr > 0 and src.startswith("profiles/r"))

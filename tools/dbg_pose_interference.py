@@ -112,6 +112,23 @@ if os.environ.get("OOB"):  # does stream B's stage alone change a's buffers (no 
         changed = [k for k, v in snap.items() if not torch.equal(getattr(a, k), v)]
         print("stage %-5s alone on B: a's buffers changed: %s" % (stage, changed), flush=True)
     sys.exit(0)
+if os.environ.get("FILLTEST"):  # solo runs, each after every CU's registers + LDS were filled with a pattern
+    import ctypes
+    fl = ctypes.CDLL(os.path.join(ROOT, "tools", "diag", "libstate_fill.so"))
+    sink = torch.zeros(4096, dtype=torch.int32, device=dev)
+    nb = 4 * torch.cuda.get_device_properties(0).multi_processor_count
+    for r in range(int(os.environ.get("ROUNDS", "8"))):
+        pat = (0x7FC00000, 0x3F800000, 0xFFFFFFFF, 0x00000000)[r % 4]
+        with torch.cuda.stream(a.stream):
+            rc = fl.mv_dbg_state_fill(ctypes.c_uint32(pat), ctypes.c_void_p(sink.data_ptr()), nb,
+                                      ctypes.c_void_p(a.stream.cuda_stream))
+            assert rc == 0, rc
+            a.pose()
+        torch.cuda.synchronize()
+        d = (a.T - ref).abs().amax(dim=(1, 2))
+        print("fill 0x%08x then pose solo: pairs differing from the first solo run: %d" % (pat, int((d > 0).sum())),
+              flush=True)
+    sys.exit(0)
 for stage in os.environ.get("STAGES", "none,net,kps,match,pose,all").split(","):
     bad = 0
     for r in range(int(os.environ.get("ROUNDS", "6"))):
