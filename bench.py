@@ -954,6 +954,7 @@ def main():
                             capture_output=True, text=True, timeout=300)
         if cp.returncode != 0:  # recorded, not raised: a secondary line must not take the headline with it
             out["image_to_pose"] = {"error": "bench_image_pose.py exit %d: %s" % (cp.returncode, cp.stderr[-600:])}
+            out.setdefault("secondary_errors", []).append("image_to_pose")  # visible at the top level
         else:
             r = json.loads([ln for ln in cp.stdout.splitlines() if ln.startswith("{")][-1])
             out["image_to_pose"] = {k: r.get(k) for k in ("metric", "value", "unit", "frames_per_step", "pipelines",

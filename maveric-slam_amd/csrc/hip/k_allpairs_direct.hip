@@ -1024,8 +1024,9 @@ __global__ __launch_bounds__(D_NT, 2) void k_q8t_match(int cap, const int *__res
     dma_half(B, 0, n1, wu, chunk16, lds_base);
     dma_half(B, 1, n1, wu, chunk16, lds_base + D_HALF);
     i32x4 aI[T_RG][KD / 32];
-    a_phase<false, D_QB, T_RG>(lds + D_OFF_AIMG + w * 32 * KD, rowv, w * (32 * T_RG), 0, n0, lane, A, nullptr,
-                                      nullptr, nullptr, false, aI);
+    // the A rows' loads software-pipelined (batch b + 1 issued before batch b is quantised): 3.504-3.514
+    // against 3.527-3.541 ms per launch, same box, ABAB (profiles/r06d_apipe_ab.log)
+    a_phase_pipe<D_QB, T_RG>(lds + D_OFF_AIMG + w * 32 * KD, rowv, w * (32 * T_RG), 0, n0, lane, A, aI);
     D_STAMP(1);
     __syncthreads();  // the A images (staging slot 2 + the ring) are consumed
     float m1[T_RG], m2[T_RG];

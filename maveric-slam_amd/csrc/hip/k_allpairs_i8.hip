@@ -68,22 +68,15 @@ __global__ __launch_bounds__(256) void k_i8_norms(long rows, const int8_t *__res
     }
 }
 
-// Integer keys (I8_KEYS: an experiment, OFF by default -- measured slower per step, below; when
-// on, used while 2 ntc <= 256): frame 1 is re-quantised per column to
-// unit-norm codes c_jk = RNE(b_jk s_j), s_j = RN(127 / |b_j|) (|c_jk| <= 127 since |b_jk| <= |b_j|),
-// so that the exact integer D~_ij = a_i . c_j is 127 X_ij (X = dot / |b_j|, the cosine times |a|)
-// within delta_i = (8 + 1.3e-4) |a_i| for EVERY column (|a . rho_j| <= |a| |rho_j| <= 8 |a|, the
-// s_j |b_j| = 127 (1 + eta), |eta| < 1e-6 term) -- one scale for the whole row, so the fold needs no
-// per-column multiply: key = (D~ << tb) | tag (one v_lshl_or_b32), v_max3_i32 / v_med3_i32 /
-// v_max_i32 top-2 (2.5 VALU per value against the float screen's 3.5).  The decisions stay the
-// exact integer dots with the ORIGINAL codes.  Rows [n1, cap64) of a pair are zero codes (the
-// match's tiles need no clamp; padding columns are excluded by index).  Measured (one box,
-// profiles/r04m_i8_keys_ab.log): k_i8_match 2.25 vs 2.33 ms, but k_i8_prep's extra 512 KiB per pair
-// written and read costs 0.35 vs k_i8_norms' 0.20 ms -- the C4 step is 3 % SLOWER, so off.  The
-// fold's VALU was not what held the MFMA pipe at ~50 %: 25 % fewer VALU per tile bought 3.5 %.
-#ifndef I8_KEYS
-#define I8_KEYS 0
-#endif
+// k_i8_prep: frame 1 re-quantised per column to unit-norm codes c_jk = RNE(b_jk s_j),
+// s_j = RN(127 / |b_j|) (|c_jk| <= 127 since |b_jk| <= |b_j|), so that the exact integer
+// D~_ij = a_i . c_j is 127 X_ij (X = dot / |b_j|, the cosine times |a|) within
+// delta_i = (8 + 1.3e-4) |a_i| for EVERY column (|a . rho_j| <= |a| |rho_j| <= 8 |a|, the
+// s_j |b_j| = 127 (1 + eta), |eta| < 1e-6 term) -- one scale for the whole row, so k_i8t_match's
+// fold needs no per-column multiply: key = (D~ << tb) | tag (one v_lshl_or_b32).  The decisions
+// stay the exact integer dots with the ORIGINAL codes.  Rows [n1, cap64) of a pair are zero codes.
+// (k_i8_match measured on these keys in round 4 -- profiles/r04m_i8_keys_ab.log -- was 3 % slower
+// per step than on its float screen: the prep's extra 512 KiB per pair; removed in round 6.)
 __global__ __launch_bounds__(256) void k_i8_prep(int batch, int cap, int cap64, const int *__restrict__ n1v,
                                                  const int8_t *__restrict__ d, int *__restrict__ nrm,
                                                  float *__restrict__ rnrm, int8_t *__restrict__ q1) {
@@ -159,13 +152,8 @@ __device__ __forceinline__ bool better(long long d, long long nb, int j, long lo
 // ---------------------------------------------------------------------------
 // the fold of rows 2 s, 2 s + 1 runs one k32 step after the MFMAs of step s: the folded group's
 // accumulators come from the chain's LAST MFMA, issued at the end of the previous segment
-#ifndef I8_LAG_N
-#define I8_LAG_N 1
-#endif
-constexpr int I8_LAG = I8_LAG_N;
-#ifndef I8_PF
-#define I8_PF 2  // k32 steps of B fragments read ahead of the MFMAs
-#endif
+constexpr int I8_LAG = 1;
+constexpr int I8_PF = 2;  // k32 steps of B fragments read ahead of the MFMAs
 // 4 waves (64 query rows each) per workgroup share one frame-1 tile ring, two workgroups per CU
 // (8 waves sharing one ring, one workgroup per CU -- half the DMA pieces per wave: 1.5 % slower)
 constexpr int M_NW = 4, M_NT = 64 * M_NW, M_RG = 2, M_BM = 32 * M_RG * M_NW, M_BN = 64, M_NBUF = 4;
@@ -264,12 +252,11 @@ __device__ __forceinline__ i32x16 mfma_i8_from4_m(i32x4 a, i32x4 b) {
 }
 // the row block L (pair L / tiles_r, rows (L % tiles_r) M_BM ..) of k_i8_match -- also run by
 // k_i8m_handback for the pairs k_i8t_match hands back
-template <bool KEYS>
 __device__ __forceinline__ void i8m_block(char *lds, int L, int tiles_r, int cap, const int *__restrict__ n0v,
                                           const int *__restrict__ n1v, const int8_t *__restrict__ desc0,
                                           const int8_t *__restrict__ desc1, const int *__restrict__ nb_v,
                                           const float *__restrict__ rnb_v, int *__restrict__ match_idx,
-                                          int *__restrict__ match_dot, const int8_t *__restrict__ q1v, int cap64) {
+                                          int *__restrict__ match_dot) {
     int *na_s = reinterpret_cast<int *>(lds + M_OFF_NA);
     const int pair = L / tiles_r, tr = L % tiles_r;
     const int n0 = min(max(n0v[pair], 0), cap), n1 = min(max(n1v[pair], 0), cap);
@@ -287,8 +274,7 @@ __device__ __forceinline__ void i8m_block(char *lds, int L, int tiles_r, int cap
     const float *rnb = rnb_v + (size_t)pair * cap;
     const int *nb = nb_v + (size_t)pair * cap;
     const int ntc = (n1 + M_BN - 1) / M_BN;
-    // KEYS: the tiles stream the unit-norm codes (cap64 rows per pair, zero past n1: no clamp)
-    const int8_t *Bt = KEYS ? q1v + (size_t)pair * cap64 * KD : B;
+    const int8_t *Bt = B;
 
     // ---- B DMA: wave w fills rows w*RPW .. +RPW-1 of a tile, 4 rows (1 KiB) per instruction;
     //      lane l -> row (l >> 4), chunk position l & 15, source chunk (l & 15) ^ (row & 15) ----
@@ -309,14 +295,14 @@ __device__ __forceinline__ void i8m_block(char *lds, int L, int tiles_r, int cap
             glds16_i8<0, (SLOT) * M_SLOT + 8 * KD>(Bt, oB[M_DPW - 2], dst_w);                \
             glds16_i8<0, (SLOT) * M_SLOT + 12 * KD>(Bt, oB[M_DPW - 1], dst_w);               \
         }                                                                                    \
-        if constexpr (!KEYS) glds4_i8<(SLOT) * M_SLOT + M_TILE>(rnb, oR, lds_base);          \
+        glds4_i8<(SLOT) * M_SLOT + M_TILE>(rnb, oR, lds_base);                               \
     } while (0)
 #define I8_OFFSETS(TC)                                                                       \
     do {                                                                                     \
         const int nb_ = (TC) * M_BN + dr;                                                    \
         _Pragma("unroll") for (int g_ = 0; g_ < M_DPW; g_++)                                 \
-            oB[g_] = (unsigned)(KEYS ? nb_ + 4 * g_ : min(nb_ + 4 * g_, n1 - 1)) * KD + (dcb ^ (64u * g_)); \
-        if constexpr (!KEYS) oR = (unsigned)min((TC) * M_BN + lane, n1 - 1) * 4;             \
+            oB[g_] = (unsigned)min(nb_ + 4 * g_, n1 - 1) * KD + (dcb ^ (64u * g_));          \
+        oR = (unsigned)min((TC) * M_BN + lane, n1 - 1) * 4;                                  \
     } while (0)
     // prologue: tiles 0, 1, 2 issued before the A rows are read, so that both latencies overlap
     for (int g = 0; g < M_NBUF - 1 && g < ntc; g++) {
@@ -362,7 +348,7 @@ __device__ __forceinline__ void i8m_block(char *lds, int L, int tiles_r, int cap
     // lane index): top-2 tracking needs no index registers.  Columns past n1 get r = 0 (f = 0).
     i32x16 acc[M_RG][2];
     float m1[M_RG][16], m2[M_RG][16];
-    const float kinit = KEYS ? __int_as_float((int)0x80000000) : -__builtin_inff();
+    const float kinit = -__builtin_inff();
 #pragma unroll
     for (int g = 0; g < M_RG; g++)
 #pragma unroll
@@ -371,16 +357,14 @@ __device__ __forceinline__ void i8m_block(char *lds, int L, int tiles_r, int cap
             m2[g][q] = kinit;
         }
     // "tile -1" of group 1, folded beside tile 0, never a maximum: float -3e38 (f = fma(0, 0,
-    // -3e38)); KEYS -2^22 (below every D~, |D~| <= 256 128 127 < 2^22)
+    // -3e38))
 #pragma unroll
     for (int q = 0; q < 16; q++) {
-        acc[1][0][q] = KEYS ? -(1 << 22) : 0;
-        acc[1][1][q] = KEYS ? -(1 << 22) : 0;
+        acc[1][0][q] = 0;
+        acc[1][1][q] = 0;
     }
-    // tag width: KEYS -- the smallest that holds 2 ntc tags (keys (D~ << tb) | tag within 31
-    // bits for tb <= 8); float -- 8 (the low mantissa bits) or wider
-    const int tb = KEYS ? (2 * ntc <= 2 ? 1 : 32 - __builtin_clz(2 * ntc - 1))
-                        : (2 * ntc <= 256 ? 8 : 32 - __builtin_clz(2 * ntc - 1));
+    // tag width: 8 (the low mantissa bits) or wider
+    const int tb = 2 * ntc <= 256 ? 8 : 32 - __builtin_clz(2 * ntc - 1);
     int vsh = tb;
     asm volatile("" : "+v"(vsh));  // the key shift as a VGPR operand (the tags take the SGPR slot)
     const unsigned tkeep = ~((1u << tb) - 1u);
@@ -394,13 +378,9 @@ __device__ __forceinline__ void i8m_block(char *lds, int L, int tiles_r, int cap
 #define I8_FOLD2(FG, S, G0, R0, R1, C0, C1)                                                  \
     do {                                                                                     \
         _Pragma("unroll") for (int q = 2 * (S); q < 2 * (S) + 2; q++) {                      \
-            if constexpr (KEYS) {                                                            \
-                fold_keys_i8(acc[FG][0][q], acc[FG][1][q], vsh, (G0), (G0) + 1u, m1[FG][q], m2[FG][q]); \
-            } else {                                                                         \
-                const float a_ = __builtin_fmaf(__int_as_float(acc[FG][0][q]), (R0), (C0));  \
-                const float b_ = __builtin_fmaf(__int_as_float(acc[FG][1][q]), (R1), (C1));  \
-                fold3_i8(tag_i8(a_, vkeep, (G0)), tag_i8(b_, vkeep, (G0) + 1u), m1[FG][q], m2[FG][q]); \
-            }                                                                                \
+            const float a_ = __builtin_fmaf(__int_as_float(acc[FG][0][q]), (R0), (C0));      \
+            const float b_ = __builtin_fmaf(__int_as_float(acc[FG][1][q]), (R1), (C1));      \
+            fold3_i8(tag_i8(a_, vkeep, (G0)), tag_i8(b_, vkeep, (G0) + 1u), m1[FG][q], m2[FG][q]); \
         }                                                                                    \
     } while (0)
 #define I8_SEG(J, G, FG, G0, R0, R1, C0, C1)                                                 \
@@ -419,14 +399,8 @@ __device__ __forceinline__ void i8m_block(char *lds, int L, int tiles_r, int cap
             if (s_ >= PF) {                                                                  \
                 const int m_ = s_ - PF;                                                      \
                 if (m_ == 0) {                                                               \
-                    if constexpr (KEYS) {                                                    \
-                        const i32x16 z_ = {};                                                \
-                        acc[G][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][0], b0_[0], z_, 0, 0, 0); \
-                        acc[G][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][0], b1_[0], z_, 0, 0, 0); \
-                    } else {                                                                 \
-                        acc[G][0] = mfma_i8_from4_m(aI[G][0], b0_[0]);                       \
-                        acc[G][1] = mfma_i8_from4_m(aI[G][0], b1_[0]);                       \
-                    }                                                                        \
+                    acc[G][0] = mfma_i8_from4_m(aI[G][0], b0_[0]);                           \
+                    acc[G][1] = mfma_i8_from4_m(aI[G][0], b1_[0]);                           \
                 } else {                                                                     \
                     acc[G][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b0_[m_], acc[G][0], 0, 0, 0); \
                     acc[G][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(aI[G][m_], b1_[m_], acc[G][1], 0, 0, 0); \
@@ -450,7 +424,7 @@ __device__ __forceinline__ void i8m_block(char *lds, int L, int tiles_r, int cap
         }                                                                                    \
         const unsigned gp_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)max(tc - 1, 0));  \
         I8_SEG(J, 0, 1, gp_, pr0, pr1, pc0, pc1);                                            \
-        if constexpr (!KEYS) {                                                               \
+        {                                                                                    \
             const float *rl_ = reinterpret_cast<const float *>(lds + (J) * M_SLOT + M_TILE); \
             const int col_ = tc * M_BN + fr;                                                 \
             const float s0_ = col_ < n1 ? rl_[fr] : 0.f, s1_ = col_ + 32 < n1 ? rl_[fr + 32] : 0.f; \
@@ -462,7 +436,7 @@ __device__ __forceinline__ void i8m_block(char *lds, int L, int tiles_r, int cap
         const unsigned gc_ = __builtin_amdgcn_readfirstlane(2u * (unsigned)tc);              \
         I8_SEG(J, 1, 0, gc_, pr0, pr1, pc0, pc1);                                            \
         if (ntile < ntc) {                                                                   \
-            wait_vm_i8<(M_DPW + (KEYS ? 0 : 1)) * (M_NBUF - 2)>();                           \
+            wait_vm_i8<(M_DPW + 1) * (M_NBUF - 2)>();                                        \
         } else {                                                                             \
             wait_vm_i8<0>();                                                                 \
         }                                                                                    \
@@ -520,9 +494,8 @@ __device__ __forceinline__ void i8m_block(char *lds, int L, int tiles_r, int cap
             e1[2 * i + 1] = v.z;
             e2[2 * i + 1] = v.w;
         }
-        // key order: float compares of the tagged screen values, or signed-int compares of the
-        // key bits (KEYS)
-        auto kgt = [](float a, float b) { return KEYS ? __float_as_int(a) > __float_as_int(b) : a > b; };
+        // key order: float compares of the tagged screen values
+        auto kgt = [](float a, float b) { return a > b; };
         auto kmax = [&](float a, float b) { return kgt(a, b) ? a : b; };
         auto kmin = [&](float a, float b) { return kgt(a, b) ? b : a; };
         float M = kinit, M2 = kinit;
@@ -548,30 +521,11 @@ __device__ __forceinline__ void i8m_block(char *lds, int L, int tiles_r, int cap
         //      ("deep" row, below) ----
         const int rl = w * 64 + g * 32 + fr;
         const bool live = row0 + rl < n0;
-        // float: a column below M (1 - 2^(tb-21)) cannot be (or tie) the maximiser.  KEYS: with
-        // |D~_j - 127 X_j| <= da for every column, a column that can reach the maximiser's X has
-        // D~ >= M - 2 da, and no column has a positive dot when M + da <= 0
-        bool cand, ambig;
-        float lim = 0.f;
-        double limd = 0.0;
-        if constexpr (KEYS) {
-            // a match needs X > 0.9 |a| (100 dot^2 > 81 |a|^2 |b|^2, dot > 0): rows with M + da <=
-            // 127 0.9 |a| have none -- decided without a dot (most unmatched rows: without this their
-            // runner-ups, inside the wide window, would make them ambiguous)
-            const double an = sqrt((double)na_r[g]);
-            const double da = an * (8.0 + 1.3e-4) * 1.0001 + 1e-6;
-            const double Mv = (double)(__float_as_int(M) >> tb);
-            cand = live && na_r[g] > 0 && Mv + da > 0.0 && Mv + da > 114.3 * an * (1.0 - 1e-9);
-            limd = Mv - 2.0 * da;
-            ambig = cand && (double)(__float_as_int(M2) >> tb) >= limd;
-        } else {
-            cand = live && na_r[g] > 0 && M > 1e-30f;  // else every dot <= 0 (tagged zeros are subnormal)
-            lim = M * keep_frac;
-            ambig = cand && M2 >= lim;
-        }
-        auto inside_w = [&](float e) {
-            return KEYS ? (double)(__float_as_int(e) >> tb) >= limd : e >= lim;
-        };
+        // a column below M (1 - 2^(tb-21)) cannot be (or tie) the maximiser
+        const bool cand = live && na_r[g] > 0 && M > 1e-30f;  // else every dot <= 0 (tagged zeros are subnormal)
+        const float lim = M * keep_frac;
+        const bool ambig = cand && M2 >= lim;
+        auto inside_w = [&](float e) { return e >= lim; };
         int nc = cand ? 1 : 0;
         if (ambig) {  // both lanes of the row take this branch
             unsigned in1 = 0, in2 = 0;
@@ -598,10 +552,6 @@ __device__ __forceinline__ void i8m_block(char *lds, int L, int tiles_r, int cap
         }
         const unsigned tagM = __float_as_uint(M) & ~tkeep;
         const int I = (int)(tagM >> 1) * M_BN + (int)(tagM & 1) * 32 + E;
-        if (KEYS && cand && !ambig && I >= n1) {  // a padding column (zero codes) on top: all columns
-            nc = -1;
-            if (fh == 0) lmask[rl] = 0xffffffffu;
-        }
         int bj = -1;
         long long bd = 0, bn = 1;
         for (int k = 0; k < nc; k++) {  // the row's two lanes run the same trip count
@@ -687,16 +637,14 @@ __device__ __forceinline__ void i8m_block(char *lds, int L, int tiles_r, int cap
             }
         }
 }
-template <bool KEYS>
 __global__ __launch_bounds__(M_NT, 2) void k_i8_match(int tiles_r, int cap, const int *__restrict__ n0v,
                                                       const int *__restrict__ n1v, const int8_t *__restrict__ desc0,
                                                       const int8_t *__restrict__ desc1, const int *__restrict__ nb_v,
                                                       const float *__restrict__ rnb_v, int *__restrict__ match_idx,
-                                                      int *__restrict__ match_dot, const int8_t *__restrict__ q1v,
-                                                      int cap64) {
+                                                      int *__restrict__ match_dot) {
     __shared__ __attribute__((aligned(16))) char lds[M_LDS];
-    i8m_block<KEYS>(lds, xcd_remap(blockIdx.x, gridDim.x), tiles_r, cap, n0v, n1v, desc0, desc1, nb_v, rnb_v,
-                    match_idx, match_dot, q1v, cap64);
+    i8m_block(lds, xcd_remap(blockIdx.x, gridDim.x), tiles_r, cap, n0v, n1v, desc0, desc1, nb_v, rnb_v,
+                    match_idx, match_dot);
 }
 // The pairs k_i8t_match hands back (a row with two in-window columns in one lane half, whose deep
 // re-score would scan every column of the half -- the common case on the network's own
@@ -717,8 +665,7 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8m_handback(int tiles_r, int cap, 
     if (!__builtin_amdgcn_readfirstlane(only[L / tiles_r])) return;  // uniform: one flag per block
     // k_i8_match's default form (the original codes and 1 / |b| from k_i8_prep: 3 % faster than
     // its unit-norm-key form, round 4)
-    i8m_block<false>(lds, L, tiles_r, cap, n0v, n1v, desc0, desc1, nb_v, rnb_v, match_idx, match_dot, nullptr,
-                     cap64);
+    i8m_block(lds, L, tiles_r, cap, n0v, n1v, desc0, desc1, nb_v, rnb_v, match_idx, match_dot);
 }
 
 
@@ -733,7 +680,7 @@ __global__ __launch_bounds__(M_NT, 2) void k_i8m_handback(int tiles_r, int cap, 
 // VGPR and the tag (2 tc + jb) 16 + r in an SGPR: 2.5 VALU per screened value, no per-column
 // multiply.  Tiles of 64 columns stream by LDS-DMA into a 4-slot ring (3 in flight, 16-B chunks
 // XOR-swizzled by row, so the fragment reads are conflict-free; each lane's 8 chunk offsets are
-// loop-invariant registers).  Decisions: k_i8_match's KEYS rules (window (8 + 1.3e-4) |a| in
+// loop-invariant registers).  Decisions: the integer-key rules (window (8 + 1.3e-4) |a| in
 // 127-units, rows below the 0.9 cosine bound decided without a dot), exact integer dots from the
 // row's own two lanes, deep halves re-scored by the wave.  |D~| <= 2032 * 135 < 2^19, so keys fit
 // 31 bits up to tb = 12 (n1 <= 8192).
@@ -746,20 +693,15 @@ constexpr int IT_OFF_LM = IT_OFF_NA + IT_BM * 4;   // [IT_BM] deep rows' halves
 constexpr int IT_LDS = IT_OFF_LM + IT_BM * 4;
 static_assert(IT_LDS <= 160 * 1024, "LDS");
 static_assert(IT_DPW == 2, "8 waves: 2 DMA pieces per wave and tile");
-#ifndef IT_HANDBACK
-// 1: a pair with a deep row (two in-window columns in one lane half) is handed to k_i8m_handback
+// A pair with a deep row (two in-window columns in one lane half) is handed to k_i8m_handback
 // whole.  On the network's own int8 descriptors (256 consecutive KITTI frames, 1920 cells each)
 // the in-kernel deep re-scores made k_i8t_match 7.84 ms against k_i8_match's 0.29
 // (tools/ab_real_i8.py, profiles/r05s_i8_real_desc.log); 0: the deep rows scored here (A/B).
 // Measured and not kept: the deep rows re-screened on the matrix cores as k_q8t_rescan does for
 // the fp32 path -- 1.00 ms per 256 network pairs against 0.69 with the hand-back: those pairs
 // have hundreds of deep rows each, and k_i8_match's 16-candidate lists are the better layout
-// for them (profiles/r05t_i8_rescan.log)
-#define IT_HANDBACK 1
-#endif
-#ifndef IT_REUSE
-#define IT_REUSE 1  // a column block's 8 fragments read once and kept for its 4 row groups
-#endif
+// for them (profiles/r05t_i8_rescan.log).  A column block's 8 fragments are read once and kept
+// for its 4 row groups (re-read per unit: 0.443-0.445 of the int8 peak against 0.46).
 // (Measured and not kept: the next tile's first 2 / 4 block-0 fragments read during unit 7 with
 // the barrier waiting for two tiles -- 1.978-1.986 ms against 1.976-1.986 without; all 8 spill
 // ~150 VGPRs -- profiles/r05l_i8_xpf_ab.json.)
@@ -863,32 +805,21 @@ __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, co
     // unit U (column block U >> 2, row group U & 3) of the tile in ring slot SL: 8 MFMAs into
     // acc[U & 1], each beside the fold of 2 of the previous unit's values; fragments 2 k32 steps
     // ahead across the tile's units (fb_: constant indices)
-#if IT_REUSE
     // the column block's 8 fragments (32 VGPRs) feed its 4 units: read once per block (block 1's
     // replace block 0's, one k32 step at a time, during unit 3, each right after its last MFMA)
 #define IT_FRAG(U, S) fq_[S]
 #define IT_NEXT(U, S)                                                                        \
     if ((U) == 3) fq_[S] = *reinterpret_cast<const i32x4 *>(rs + 32 * KD + cho[S]);
-#else
-    // fragments re-read per unit, 2 k32 steps ahead across the tile's units (fb_: constant indices)
-#define IT_FRAG(U, S) fb_[8 * (U) + (S)]
-#define IT_NEXT(U, S)                                                                        \
-    {                                                                                        \
-        const int gn_ = 8 * (U) + (S) + 2;                                                   \
-        if (gn_ < 64) fb_[gn_] = *reinterpret_cast<const i32x4 *>(rs + (gn_ >> 5) * 32 * KD + cho[gn_ & 7]); \
-    }
-#endif
 #define IT_UNIT(U, PT)                                                                       \
     do {                                                                                     \
         _Pragma("unroll") for (int s_ = 0; s_ < KD / 32; s_++) {                             \
-            if (!IT_REUSE) { IT_NEXT(U, s_) }                                                \
             if (s_ == 0) {                                                                   \
                 const i32x16 z_ = {};                                                        \
                 acc[(U) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(IT_FRAG(U, 0), aI[(U) & 3][0], z_, 0, 0, 0); \
             } else {                                                                         \
                 acc[(U) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(IT_FRAG(U, s_), aI[(U) & 3][s_], acc[(U) & 1], 0, 0, 0); \
             }                                                                                \
-            if (IT_REUSE) { IT_NEXT(U, s_) }                                                 \
+            IT_NEXT(U, s_)                                                                   \
             if (s_ == 0)                                                                     \
                 fold_keys_i8_cv(acc[((U) + 1) & 1][0], acc[((U) + 1) & 1][1], vsh, (PT), (PT) + 1u, \
                                 m1[((U) + 3) & 3], m2[((U) + 3) & 3]);                       \
@@ -901,11 +832,9 @@ __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, co
 
     wait_vm_i8<0>();  // the prologue's tiles and the A rows
     __syncthreads();
-#if IT_REUSE
     i32x4 fq_[KD / 32];  // tile 0's block-0 fragments (later tiles': read during the tile before)
 #pragma unroll
     for (int s2 = 0; s2 < KD / 32; s2++) fq_[s2] = *reinterpret_cast<const i32x4 *>(lds + cho[s2]);
-#endif
     for (int tc = 0; tc < ntc; tc++) {
         if (tc + 3 < ntc) {  // tile tc + 3 into the slot tile tc - 1 left (every wave is past it)
             const int sl_ = (tc + 3) & 3;
@@ -917,16 +846,10 @@ __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, co
         const char *rs = lds + (tc & 3) * IT_TILE;
         const unsigned tg0 = __builtin_amdgcn_readfirstlane(32u * (unsigned)tc);
         const unsigned tgp = tg0 - 16u, tg1 = tg0 + 16u;
-#if IT_REUSE
         if (tc > 0) {
 #pragma unroll
             for (int s2 = 0; s2 < KD / 32; s2++) fq_[s2] = *reinterpret_cast<const i32x4 *>(rs + cho[s2]);
         }
-#else
-        i32x4 fb_[64];
-        fb_[0] = *reinterpret_cast<const i32x4 *>(rs + cho[0]);
-        fb_[1] = *reinterpret_cast<const i32x4 *>(rs + cho[1]);
-#endif
         IT_UNIT(0, tgp);
         if (tc == 0) {
             m1[3] = kinit;
@@ -995,7 +918,7 @@ __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, co
         if (ambig) {
             if (in2 || oin2) {  // a half holds two columns inside: its every column is a candidate
                 nc = -1;
-                hand = true;  // (IT_HANDBACK: the pair goes to k_i8m_handback instead)
+                hand = true;  // the pair goes to k_i8m_handback
                 wm = (in1 ? 1u << fh : 0u) | (oin1 ? 1u << (1 - fh) : 0u);
             } else {
                 const int jm = kcol(e1, fh), jo = __shfl_xor(jm, 32, 64);
@@ -1040,7 +963,7 @@ __global__ __launch_bounds__(IT_NT, 2) void k_i8t_match(int tiles_r, int cap, co
         if (fh == 0 && live && nc < 0) lmask[rl] = wm;
         deep_rows[g] = (unsigned)__ballot(fh == 0 && live && nc < 0);
     }
-    if (IT_HANDBACK && __ballot(hand)) {  // the pair is redone in k_i8_match's layout: no deep re-scores here
+    if (__ballot(hand)) {  // the pair is redone in k_i8_match's layout: no deep re-scores here
         if (lane == 0 && atomicExch(handback + pair, 1) == 0) atomicAdd(nhand, 1);  // vector atomics
         return;
     }
@@ -1106,7 +1029,7 @@ static bool i8_transposed(int cap) {
     }();
     return !off && cap <= 8192;
 }
-static bool i8_keys(int cap) { return (I8_KEYS || i8_transposed(cap)) && 2 * ((cap + M_BN - 1) / M_BN) <= 256; }
+static bool i8_keys(int cap) { return i8_transposed(cap) && 2 * ((cap + M_BN - 1) / M_BN) <= 256; }
 static int i8_cap64(int cap) { return (cap + M_BN - 1) / M_BN * M_BN; }
 
 size_t allpairs_i8_scratch_bytes(int batch, int cap) {
@@ -1150,7 +1073,7 @@ int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const i
                            nb, match_idx, match_dot, q1, cap64, flags, flags + batch);
         MV_PROF_END(s);
         MV_LAUNCH_CHECK();
-        if (IT_HANDBACK) {
+        {
             const int tiles_m = (cap + M_BM - 1) / M_BM;
             const long mblocks = (long)batch * tiles_m;
             MV_REQUIRE(mblocks < (1l << 31));
@@ -1167,12 +1090,10 @@ int launch_allpairs_i8(hipStream_t s, void *scratch, int batch, int cap, const i
     const long mblocks = (long)batch * tiles_m;
     MV_REQUIRE(mblocks < (1l << 31));
     MV_PROF_BEGIN(s, "k_i8_match");
-    if (keys && !direct)
-        hipLaunchKernelGGL(k_i8_match<true>, dim3((unsigned)mblocks), dim3(M_NT), 0, s, tiles_m, cap, n0, n1, desc0,
-                           desc1, nb, rnb, match_idx, match_dot, q1, cap64);
-    else
-        hipLaunchKernelGGL(k_i8_match<false>, dim3((unsigned)mblocks), dim3(M_NT), 0, s, tiles_m, cap, n0, n1, desc0,
-                           desc1, nb, rnb, match_idx, match_dot, (const int8_t *)nullptr, cap64);
+    // (with keys: k_i8_prep wrote the unit-norm codes for k_i8t_match; this path reads the norms it
+    // also wrote -- the adaptive dispatch's direct calls and cap > 8192)
+    hipLaunchKernelGGL(k_i8_match, dim3((unsigned)mblocks), dim3(M_NT), 0, s, tiles_m, cap, n0, n1, desc0, desc1, nb,
+                       rnb, match_idx, match_dot);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     return MV_OK;
@@ -1219,7 +1140,7 @@ extern "C" int mv_match_allpairs_i8_dev(mv_context *ctx, int batch, int cap, con
             direct = ctx->i8_prefer_m && (ctx->i8_calls % 16) != 0;
             // measure this call -- only where the launch below enqueues the count copy (the transposed
             // path with hand-backs), so that no measurement is marked in flight that never lands
-            if (!direct && *ch == -2 && IT_HANDBACK && mv::i8_transposed(cap)) {
+            if (!direct && *ch == -2 && mv::i8_transposed(cap)) {
                 *ch = -1;
                 ctx->i8_meas_batch = batch;
                 count_host = ctx->i8_count_host;

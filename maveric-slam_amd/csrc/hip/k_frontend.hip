@@ -95,9 +95,12 @@ __global__ __launch_bounds__(256) void k_softmax(int total_rows, int cells, cons
     } else {
         scale_poly(scales[frame], sp);  // tiny frames
     }
-    // the row's 65 bytes: dwords re-aligned to the row start; mask of non-negative logits
+    // the row's 65 bytes: dwords re-aligned to the row start.  First a 16-bit mask of the dwords
+    // holding a non-negative logit (4 VALU per dword: alignbyte, bfi = ~u & 0x80808080, min, shift-or),
+    // then those dwords' non-negative bytes in ascending order (most logits are negative: typically
+    // 1-3 dwords per row)
     const int rb = t * kSemiC, o = rb & 3, d0 = rb >> 2;
-    unsigned mlo = 0, mhi = 0;
+    unsigned dm = 0;
     unsigned wv = (unsigned)lds32[d0];
 #pragma unroll
     for (int j = 0; j < 16; j++) {
@@ -105,26 +108,27 @@ __global__ __launch_bounds__(256) void k_softmax(int total_rows, int cells, cons
         const unsigned u = __builtin_amdgcn_alignbyte(wn, wv, o);  // bytes 4j .. 4j+3 of the row
         wv = wn;
         const unsigned nn = ~u & 0x80808080u;
-        const unsigned m4 = ((nn >> 7) | (nn >> 14) | (nn >> 21) | (nn >> 28)) & 0xFu;
-        if (j < 8)
-            mlo |= m4 << (4 * j);
-        else
-            mhi |= m4 << (4 * (j - 8));
+        dm |= min(nn, 1u) << j;
     }
     const int8_t *row = reinterpret_cast<const int8_t *>(lds32) + rb;
     int best = 64;
     float best_e = 0.0f;
     float den = 1.17549435e-38f;  // FLT_MIN (top_N.c:30)
-    unsigned long long m = ((unsigned long long)mhi << 32) | mlo;
-    while (m) {
-        const int i = __builtin_ctzll(m);
-        m &= m - 1;
-        const float e = approx_exp(sp, (int)row[i]);
-        if (e > best_e) {
-            best_e = e;
-            best = i;
+    while (dm) {
+        const int j = __builtin_ctz(dm);
+        dm &= dm - 1;
+        const unsigned u = __builtin_amdgcn_alignbyte((unsigned)lds32[d0 + j + 1], (unsigned)lds32[d0 + j], o);
+        unsigned nn = ~u & 0x80808080u;  // bit 8 k + 7: byte k of the dword is >= 0
+        while (nn) {
+            const int i = 4 * j + (__builtin_ctz(nn) >> 3);
+            nn &= nn - 1;
+            const float e = approx_exp(sp, (int)row[i]);
+            if (e > best_e) {
+                best_e = e;
+                best = i;
+            }
+            den += e;
         }
-        den += e;
     }
     const int x64 = (int)row[64];
     if (x64 >= 0) den += approx_exp(sp, x64);

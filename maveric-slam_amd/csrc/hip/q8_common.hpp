@@ -337,6 +337,72 @@ __device__ __forceinline__ void a_phase(char *img, float2 *rowv, int rbase, int 
     }
 }
 
+// a_phase<false, QB, NG> with the loads software-pipelined: batch b + 1's QB row quads are issued
+// before batch b is quantised (two register sets of QB x 4 f32x4), across the group boundaries, so
+// a wave always has 2 QB quads in flight instead of alternating between loading and quantising.
+template <int QB, int NG>
+__device__ __forceinline__ void a_phase_pipe(char *img, float2 *rowv, int rbase, int row0, int n0, int lane,
+                                             const float *__restrict__ A, i32x4 (&aI)[NG][KD / 32]) {
+    const int fr = lane & 31, fh = lane >> 5;
+    const int sub = lane & 15, rq = lane >> 4;
+    constexpr int NB = NG * 8 / QB;  // batches of QB quads (8 quads = 32 rows per group)
+    f32x4v xs[2][QB][4];
+    auto load = [&](int bt, f32x4v (&x)[QB][4]) {
+#pragma unroll
+        for (int qd = 0; qd < QB; qd++) {
+            const int rr = bt * QB * 4 + 4 * qd + rq;  // row within the wave's NG * 32
+            const float *ar = A + (size_t)min(row0 + rbase + rr, n0 - 1) * KD;
+#pragma unroll
+            for (int u = 0; u < 4; u++) x[qd][u] = *reinterpret_cast<const f32x4v *>(ar + 4 * (sub + 16 * u));
+        }
+    };
+    load(0, xs[0]);
+#pragma unroll
+    for (int bt = 0; bt < NB; bt++) {
+        if (bt + 1 < NB) load(bt + 1, xs[(bt + 1) & 1]);
+        const int g = bt * QB / 8;
+#pragma unroll
+        for (int qd = 0; qd < QB; qd++) {
+            const f32x4v(&x)[4] = xs[bt & 1][qd];
+            const int r = (bt * QB + qd) % 8 * 4 + rq;  // row within the group
+            float m = 0.f, qa = 0.f, qb = 0.f;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                m = absmax3(m, x[u][0], x[u][1]);
+                m = absmax3(m, x[u][2], x[u][3]);
+                qa = __builtin_fmaf(x[u][0], x[u][0], qa);
+                qb = __builtin_fmaf(x[u][1], x[u][1], qb);
+                qa = __builtin_fmaf(x[u][2], x[u][2], qa);
+                qb = __builtin_fmaf(x[u][3], x[u][3], qb);
+            }
+            float q2 = qa + qb;
+            m = fmaxf(m, swz_xor<1>(m));
+            q2 += swz_xor<1>(q2);
+            m = fmaxf(m, swz_xor<2>(m));
+            q2 += swz_xor<2>(q2);
+            m = fmaxf(m, swz_xor<4>(m));
+            q2 += swz_xor<4>(q2);
+            m = fmaxf(m, swz_xor<8>(m));
+            q2 += swz_xor<8>(q2);
+            const float q = m > 0.f ? 127.f * __builtin_amdgcn_rcpf(m) : 0.f;
+            const bool afull = !(q2 <= FLT_MAX) || m < SCALE_LO || m > SCALE_HI;  // zero rows too
+            if (sub == 0) rowv[rbase + g * 32 + r] = make_float2(q2, afull ? -1.f : m * (1.f / 127.f));
+            char *rowp = img + r * KD + 4 * (sub & 3);
+#pragma unroll
+            for (int u = 0; u < 4; u++)  // k = 4 sub + 64 u: chunk (sub >> 2) + 4 u
+                *reinterpret_cast<int *>(rowp + ((((sub >> 2) + 4 * u) ^ (r & 15)) << 4)) =
+                    pack4(x[u][0], x[u][1], x[u][2], x[u][3], q);
+        }
+        if ((bt + 1) * QB % 8 == 0) {  // group g complete in the image: back in the MFMA layout
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own image writes
+#pragma unroll
+            for (int s2 = 0; s2 < KD / 32; s2++)
+                aI[g][s2] = *reinterpret_cast<const i32x4 *>(img + fr * KD + (((2 * s2 + fh) ^ (fr & 15)) << 4));
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // the reads complete before the next group's writes
+        }
+    }
+}
+
 // ---- the epilogue (wave-local): per row the 32 lanes' (m1, m2) are merged through LDS (lanes
 //      fr and fr + 32 end with row fr's (M, E, M2)), then the row is decided in its two lanes;
 //      rare wide rows are re-scored by the whole wave.  epi = the block's epilogue LDS

@@ -176,3 +176,37 @@ def test_min_gap_edge_cases(orc):
     g = lib.orc_sp_min_gap(q.ctypes.data_as(ctypes.c_void_p), 3, 2, 2, 0.5, out.ctypes.data_as(ctypes.c_void_p))
     assert g == np.float32(2.5)
     assert out[0, 0] == 1 and out[3, 1] == -1  # cell p = gx * rows + gy
+
+
+def test_normalising_model_codes_do_not_fit_int8(orc):
+    """Why configs[4]'s int8 all-pairs runs on superpoint_quantized_nonorm.pt (the scripts' default,
+    pairwise_pnp.py:585): superpoint_quantized.pt holds the SAME quantised weights and only divides
+    the dequantised convDb output by its per-pixel L2 norm (superpoint_inference.py:79-80).  run()'s
+    output quantisation (:199-206: scale = the smallest gap between distinct values, codes =
+    round(x / scale)) then meets ~1.7e5 distinct unit-norm floats with a gap of ~3e-10, and 98 % of
+    its int32 codes fall outside int8 -- no int8 descriptor exists for the MFMA distance to consume.
+    Without the norm the codes are the network's own int8 outputs (252 distinct values, all in range).
+    The oracle network on KITTI 00 frame 000000 (the committed fixture); when the reference archive
+    is present, its weights are also checked to equal the _nonorm ones."""
+    import torch
+
+    import mvtrack
+
+    W = dict(load_golden("superpoint_qnonorm.npz"))
+    ref_pt = "/root/reference/python/superpoint_quantized.pt"
+    if os.path.exists(ref_pt):
+        Wn = mvtrack.superpoint_weights(ref_pt)
+        assert all(np.array_equal(Wn[k], W[k]) for k in W if k in Wn)
+    img = load_golden("kitti00_images.npz")["img_000000"]
+    _, _, _, _, _, dr = orc.sp_forward(img, orc.sp_net(W))
+    desc = torch.from_numpy(np.float32(W["convDb_meta"][2]) * dr.astype(np.float32))[None]
+    descn = desc.div(torch.unsqueeze(torch.norm(desc, p=2, dim=1), 1))
+
+    def run_codes(outs):
+        u = torch.unique(outs)
+        return torch.round(outs / torch.min(u[1:] - u[:-1])).to(torch.int64)
+
+    q_raw, q_norm = run_codes(desc[0]), run_codes(descn[0])
+    assert int(q_raw.min()) >= -128 and int(q_raw.max()) <= 127
+    outside = float(((q_norm < -128) | (q_norm > 127)).double().mean())
+    assert outside > 0.9 and int(q_norm.abs().max()) > 1 << 24
