@@ -78,7 +78,7 @@ def parse(argv=None):
                          "stream instead of inside the match launch")
     ap.add_argument("--window-steps", type=int, default=10,
                     help="secondary line (N = 1 only): the windowed int8 front-end of tracking_main.c "
-                         "(tools/bench_window.py, 7285-cell KITTI grid, 1024 pairs); 0 = skip")
+                         "(tools/bench_window.py, 7285-cell KITTI grid, 8192 pairs); 0 = skip")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="N > 1: the collective backend (nccl = RCCL over xGMI, the product path; gloo stages the "
                          "per-step result gather through host memory -- how the N-rank GPU path is exercised on a "
@@ -919,7 +919,7 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         import bench_window
 
-        w, _ = bench_window.run(batch=1024, steps=args.window_steps, warmup=2, check=1)
+        w, _ = bench_window.run(batch=8192, steps=args.window_steps, warmup=2, check=1)
         out["window_frontend"] = {k: w[k] for k in ("metric", "value", "unit", "ms_per_step", "semantics",
                                                      "stages_ms", "hbm_roofline", "checked_pairs")}
     if rank == 0 and world == 1 and args.extra_steps > 0:

@@ -59,7 +59,7 @@ def cpu_baseline(pairs, built, N, cells, seconds):
                       % (total, cells, N, dt, threads)}
 
 
-def run(batch=1024, steps=20, warmup=3, distinct=8, built=False, check=2, grid="kitti"):
+def run(batch=8192, steps=20, warmup=3, distinct=8, built=False, check=2, grid="kitti"):
     """Time the windowed front-end; returns the JSON dict (without cpu_baseline) and the pairs."""
     rows, cols, N = (47, 155, 1024) if grid == "kitti" else (24, 80, 100)
     B = batch
@@ -67,10 +67,12 @@ def run(batch=1024, steps=20, warmup=3, distinct=8, built=False, check=2, grid="
     dev = torch.device("cuda", 0)
     pairs = [synth.synth_window_pair(500 + k, rows=rows, cols=cols) for k in range(distinct)]
     pick = [b % distinct for b in range(B)]
-    semi0 = torch.from_numpy(np.stack([pairs[k][0]["semi"] for k in pick])).to(dev)
-    semi1 = torch.from_numpy(np.stack([pairs[k][1]["semi"] for k in pick])).to(dev)
-    desc0 = torch.from_numpy(np.stack([pairs[k][0]["desc"] for k in pick])).to(dev)
-    desc1 = torch.from_numpy(np.stack([pairs[k][1]["desc"] for k in pick])).to(dev)
+    tile = torch.tensor(pick, dtype=torch.long, device=dev)  # the distinct pairs tiled over the batch on the GPU
+
+    def upload(f, key):
+        return torch.from_numpy(np.stack([pairs[k][f][key] for k in range(distinct)])).to(dev)[tile].contiguous()
+
+    semi0, semi1, desc0, desc1 = upload(0, "semi"), upload(1, "semi"), upload(0, "desc"), upload(1, "desc")
     s = [mvtrack.scale_as_built(pairs[k][0]["semi_scale"]) if built else float(pairs[k][0]["semi_scale"])
          for k in pick]
     sc = torch.tensor(s, dtype=torch.float32, device=dev)
@@ -151,28 +153,38 @@ def run(batch=1024, steps=20, warmup=3, distinct=8, built=False, check=2, grid="
 
 
 def window_dram(B, cells, N, win_s):
-    """The window kernel's measured DRAM traffic per launch (rocprofv3 FETCH/WRITE, the newest
-    committed profiles/r*_summary.json that traced it; the kernel's reads depend on the synthetic
-    frames' validity, not on the build), its rate at this run's kernel time and the fraction of
-    the HBM peak it is -- the kernel is gather-latency-bound, not bandwidth-bound."""
+    """The window kernel's measured DRAM traffic (rocprofv3 FETCH/WRITE, the newest committed
+    profiles/r*_summary.json that traced it, per pair: that run's bytes per launch over its batch --
+    the reads depend on the synthetic frames' validity, not on the build), scaled to this batch,
+    its rate at this run's kernel time and the fraction of the HBM peak it is.  The kernel is not
+    bandwidth-bound (round 6: an LDS-DMA ring 2-3 tiles ahead did not speed it up,
+    profiles/r06g_window_ab.log; its VALU work per candidate is the bound)."""
     import glob
     import json
+    import re
 
+    if cells != 7285 or N != 1024:
+        return None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")), reverse=True):
         try:
-            k = json.load(open(f)).get("kernels", {}).get("k_window_wave")
+            d = json.load(open(f))
         except Exception:
             continue
-        if k and "hbm_bytes_per_launch" in k and B == 1024 and cells == 7285 and N == 1024:
-            by = k["hbm_bytes_per_launch"]
-            return {"bytes_per_launch": round(by), "GBs": round(by / win_s / 1e9, 1),
-                    "frac": round(by / win_s / 1e9 / HBM_PEAK_GBS, 4), "source": os.path.relpath(f, ROOT)}
+        k = d.get("kernels", {}).get("k_window_wave")
+        args = d.get("bench_args", "")
+        if not (k and "hbm_bytes_per_launch" in k and "bench_window" in args):
+            continue
+        m = re.search(r"--batch\s+(\d+)", args)
+        per_pair = k["hbm_bytes_per_launch"] / (int(m.group(1)) if m else 1024)  # 1024: the default before r06
+        by = per_pair * B
+        return {"bytes_per_launch": round(by), "GBs": round(by / win_s / 1e9, 1),
+                "frac": round(by / win_s / 1e9 / HBM_PEAK_GBS, 4), "source": os.path.relpath(f, ROOT)}
     return None
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--distinct", type=int, default=8, help="distinct synthetic pairs tiled over the batch")
