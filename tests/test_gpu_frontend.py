@@ -210,3 +210,30 @@ def test_dropin_symbols_match_oracle(orc, image0, ctx):
                         pp.ctypes.data_as(ctypes.c_void_p))
         st, pa2, ix2, pp2 = orc.compute_top_N(s, semi, 100)
         assert ns.value == len(pa2) and (pa[:ns.value] == pa2).all() and (bits(pp[:ns.value]) == bits(pp2)).all()
+
+
+@pytest.mark.parametrize("grid", [(24, 80), (47, 155)])
+def test_window_match_exact_ties_and_threshold(ctx, orc, grid):
+    """The as-intended window's float screens at their exact edges: every frame-0 cell holds an
+    integer multiple of one of three directions -- v = (-3, 4, 5), whose cosine with every frame-1
+    descriptor (multiples of u = (0, 1, 1)) is EXACTLY 0.9 (100 dot^2 == 81 |a|^2 |b|^2: no match,
+    the test is strict), and w1 = (-3, 5, 5), w2 = (-1, 2, 2) above it -- so a window holds many
+    candidates with exactly equal scores dot^2 / |b|^2 (m w and m' w tie for every m, m'), decided
+    by the scan position, and threshold-equal ones (tracking_main.c:18-57; oracle/mv_oracle.c)."""
+    rows, cols = grid
+    f0, f1 = synth.synth_window_pair(77, rows=rows, cols=cols)
+    cells = rows * cols
+    rng = np.random.default_rng(5)
+    dirs = np.array([[-3, 4, 5], [-3, 5, 5], [-1, 2, 2]], np.int64)
+    pick = rng.integers(0, 3, cells)
+    mult = rng.integers(1, 5, cells)
+    d0 = np.zeros((cells, 256), np.int8)
+    d0[:, :3] = (dirs[pick] * mult[:, None]).astype(np.int8)
+    d1 = np.zeros((cells, 256), np.int8)
+    d1[:, 1] = d1[:, 2] = rng.integers(1, 9, cells).astype(np.int8)
+    g0, g1 = dict(f0), dict(f1)
+    g0["desc"], g1["desc"] = d0, d1
+    N = 1024 if cells > 2000 else 100
+    n = _window_case(ctx, orc, g0, g1, False, N=N, cap=100000, max_matches=1024 if N == 1024 else 150)
+    assert n > 0
+    _window_case(ctx, orc, g0, g1, True, N=N, cap=100000, max_matches=1024 if N == 1024 else 150)

@@ -23,7 +23,48 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CAP = 1024
 
 
-def test_pose_bit_identical_beside_superpoint_network(torch_cuda):
+class _Pipe:
+    """one image -> pose chain on its own stream and context (tools/dbg_pose_interference.py's Pipe)"""
+
+    def __init__(self, torch, mvtrack, W, x, F, P, prm):
+        dev = torch.device("cuda:0")
+        e = lambda *shape, dt=torch.float32: torch.zeros(shape, dtype=dt, device=dev)  # noqa: E731
+        self.torch, self.x, self.P, self.prm = torch, x, P, prm
+        self.stream = torch.cuda.Stream(device=dev)
+        self.ctx = mvtrack.Context(0)
+        self.ctx.set_stream(self.stream)
+        self.sp = mvtrack.SuperPoint(self.ctx, W)
+        self.semi, self.cdesc = e(F, 65, 24, 80), e(F, 256, 24, 80)
+        self.nkp, self.kp, self.conf = e(F, dt=torch.int32), e(F, CAP, 2), e(F, CAP)
+        self.desc, self.kst = e(F, CAP, 256), e(F, dt=torch.int32)
+        self.idx = e(P, CAP, dt=torch.int32)
+        self.T, self.nm, self.ni, self.st = e(P, 3, 4), e(P, dt=torch.int32), e(P, dt=torch.int32), e(P, dt=torch.int32)
+
+    def net(self):
+        with self.torch.cuda.stream(self.stream):
+            self.sp.forward_raw(self.x, 192, 640, out=(self.semi, self.cdesc))
+
+    def pose(self):
+        P = self.P
+        with self.torch.cuda.stream(self.stream):
+            self.ctx.pose_from_matches(self.prm, self.nkp[:P], self.idx, self.kp[:P], self.kp[1:], self.T, self.nm,
+                                       self.ni, self.st)
+
+    def all(self):
+        P = self.P
+        self.net()
+        with self.torch.cuda.stream(self.stream):
+            self.ctx.keypoints(self.semi, self.cdesc, 192, 640, self.nkp, self.kp, self.conf, self.desc, self.kst)
+            self.ctx.match_allpairs_f32(self.desc[:P], self.desc[1:], self.nkp[:P], self.nkp[1:], self.idx, None, 0.8)
+        self.pose()
+
+    def close(self):
+        self.sp.close()
+        self.ctx.close()
+
+
+@pytest.mark.parametrize("semantics", ["as-intended", "as-built"])
+def test_pose_bit_identical_beside_superpoint_network(torch_cuda, semantics):
     import mvtrack
     import synth
 
@@ -31,59 +72,43 @@ def test_pose_bit_identical_beside_superpoint_network(torch_cuda):
     from bench_image_pose import frames_kitti
 
     torch = torch_cuda
-    dev = torch.device("cuda:0")
     F, P = 257, 256  # tools/dbg_pose_interference.py's track: 256 pairs of 257 network frames
     W = dict(load_golden("superpoint_qnonorm.npz"))
-    x = torch.from_numpy(np.stack(frames_kitti(F))).to(dev)
+    x = torch.from_numpy(np.stack(frames_kitti(F))).to(torch.device("cuda:0"))
     K = synth.KITTI_K
-    e = lambda *shape, dt=torch.float32: torch.zeros(shape, dtype=dt, device=dev)  # noqa: E731
-
-    sa, sb = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
-    ca, cb = mvtrack.Context(0), mvtrack.Context(0)
-    ca.set_stream(sa)
-    cb.set_stream(sb)
-    spa, spb = mvtrack.SuperPoint(ca, W), mvtrack.SuperPoint(cb, W)
+    sem = mvtrack.AS_INTENDED if semantics == "as-intended" else mvtrack.AS_BUILT
+    prm = mvtrack.pose_params(sem, fx=K[0, 0], fy=K[1, 1], cx=K[0, 2], cy=K[1, 2], hypotheses=256,
+                              inlier_thresh=1.0, refine_iters=10, seed=7)
+    torch.cuda.synchronize()
+    a = _Pipe(torch, mvtrack, W, x, F, P, prm)
+    b = _Pipe(torch, mvtrack, W, x, F, P, prm)
     try:
-        semi, cdesc = e(F, 65, 24, 80), e(F, 256, 24, 80)
-        semi_b, cdesc_b = e(F, 65, 24, 80), e(F, 256, 24, 80)
-        nkp, kp, conf, desc, kst = e(F, dt=torch.int32), e(F, CAP, 2), e(F, CAP), e(F, CAP, 256), e(F, dt=torch.int32)
-        idx = e(P, CAP, dt=torch.int32)
-        with torch.cuda.stream(sa):
-            spa.forward_raw(x, 192, 640, out=(semi, cdesc))
-            ca.keypoints(semi, cdesc, 192, 640, nkp, kp, conf, desc, kst)
-            ca.match_allpairs_f32(desc[:P], desc[1:], nkp[:P], nkp[1:], idx, None, 0.8)
+        a.all()
+        b.all()
         torch.cuda.synchronize()
-        assert int((kst == 0).sum()) == F and int(nkp.min()) > 100
-        for sem in (mvtrack.AS_INTENDED, mvtrack.AS_BUILT):
-            prm = mvtrack.pose_params(sem, fx=K[0, 0], fy=K[1, 1], cx=K[0, 2], cy=K[1, 2], hypotheses=256,
-                                      inlier_thresh=1.0, refine_iters=10, seed=7)
-            T, nm, ni, st = e(P, 3, 4), e(P, dt=torch.int32), e(P, dt=torch.int32), e(P, dt=torch.int32)
+        assert int((a.kst == 0).sum()) == F and int(a.nkp.min()) > 100
+        ref = (a.T.clone(), a.ni.clone(), a.st.clone())
+        assert int((ref[2] == 0).sum()) > P // 2
 
-            def pose():
-                ca.pose_from_matches(prm, nkp[:P], idx, kp[:P], kp[1:], T, nm, ni, st)
+        def differing():
+            d = (a.T.view(torch.int32) != ref[0].view(torch.int32)).reshape(P, 12).any(dim=1)
+            return int((d | (a.ni != ref[1]) | (a.st != ref[2])).sum())
 
-            with torch.cuda.stream(sa):
-                pose()
+        solo = beside = 0
+        for _ in range(2):  # alone: the pose is deterministic
+            a.pose()
+            a.pose()
             torch.cuda.synchronize()
-            ref = (T.clone(), ni.clone(), st.clone())
-            assert int((ref[2] == 0).sum()) > P // 2
-            differing = 0
-            for _ in range(4):  # tools/dbg_pose_interference.py's schedule, which made round 5's build differ
-                with torch.cuda.stream(sa):
-                    pose()
-                with torch.cuda.stream(sb):
-                    for _ in range(2):
-                        spb.forward_raw(x, 192, 640, out=(semi_b, cdesc_b))
-                with torch.cuda.stream(sa):
-                    pose()  # beside the network on stream B
-                torch.cuda.synchronize()
-                d = (T.view(torch.int32) != ref[0].view(torch.int32)).reshape(P, 12).any(dim=1)
-                d |= (ni != ref[1]) | (st != ref[2])
-                differing += int(d.sum())
-            assert differing == 0, "%s pose: %d pair results differ from the solo run beside the network" % (
-                "as-intended" if sem == mvtrack.AS_INTENDED else "as-built", differing)
+            solo += differing()
+        for _ in range(4):  # beside the network on stream B (the schedule that made round 5's build differ)
+            a.pose()
+            b.net()
+            b.net()
+            a.pose()
+            torch.cuda.synchronize()
+            beside += differing()
+        assert solo == 0 and beside == 0, "%s pose: %d (alone) / %d (beside the network) pair results differ" % (
+            semantics, solo, beside)
     finally:
-        spa.close()
-        spb.close()
-        ca.close()
-        cb.close()
+        a.close()
+        b.close()
