@@ -981,25 +981,43 @@ typedef int i32x4_t __attribute__((ext_vector_type(4)));
 // as-intended pass test 100 dot^2 > 81 |c|^2 |q|^2 and the exact running best.  The pass
 // test is screened in fp32 (relative error < 2^-20 on both sides) and decided in 64-bit
 // integers only within that margin.
+// the fold of one tile into the lane's 4 queries' bests, branch-free but for the rare exact cases:
+// the threshold test and the "beats the current best" test (d^2 / n, cross-multiplied) are both
+// screened in float with margins their rounding cannot cross (each side within 2.4e-7 of its exact
+// value) and decided exactly (64-bit integers) only inside the margins; fbq / fbn carry the best's
+// d^2 and n as floats for the screen (n < 2^24: the float is exact, and is the only copy kept).
+// Round 5's form -- better_i32 in a branch taken by every passing candidate, the best updated
+// inside it -- picked wrong winners on the GPU in windows full of exact ties
+// (tests/test_gpu_frontend.py::test_window_match_exact_ties_and_threshold: 38 of 99 matches), while
+// a CPU emulation of its algorithm agrees with the oracle and an -O1 build of it fails differently
+// (87): the code generated for it, not the algorithm (tools/diag/dbg_window_tie.py,
+// profiles/r06l_window_tie_bisect.log).  This form passes; 2.43 against 2.29 ms per 8192 pairs.
 __device__ __forceinline__ void window_fold(const i32x4_t &acc, bool cv, int cx, int cy, int cp, int cna, int r,
-                                            const int *rcx, const int *rcy, const int *rn2, int *bd, int *bn,
-                                            int *bk) {
-    const float fna81 = 81.0f * (float)cna;
+                                            const int *rcx, const int *rcy, const float *frn2, int *bd, int *bk,
+                                            float *fbq, float *fbn) {
+    const float fna = (float)cna, fna81 = 81.0f * fna;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
         const int d = acc[j];
         const bool in = cv && (unsigned)(cx - rcx[j] + r) <= (unsigned)(2 * r) &&
                         (unsigned)(cy - rcy[j] + r) <= (unsigned)(2 * r) && d > 0;
-        const float fd = (float)d;
-        const float lhs = 100.0f * fd * fd, rhs = fna81 * (float)rn2[j];
+        const float fd = (float)d, fd2 = fd * fd;
+        const float lhs = 100.0f * fd2, rhs = fna81 * frn2[j];
         bool pass = in && lhs > rhs * 1.000002f;
-        if (in && !pass && lhs >= rhs * 0.999998f)  // within the screen's margin: exact
-            pass = (unsigned long long)(100ll * d * d) > 81ull * (unsigned long long)((long long)cna * rn2[j]);
-        if (pass && better_i32(d, cna, cp, bd[j], bn[j], bk[j])) {
-            bd[j] = d;
-            bn[j] = cna;
-            bk[j] = cp;
+        const bool amb_t = in && !pass && lhs >= rhs * 0.999998f;
+        const float L = fd2 * fbn[j], Rr = fbq[j] * fna;  // none yet: fbq = 0, so any d > 0 beats it
+        bool win = L > Rr * 1.000001f;
+        const bool amb_b = !win && L >= Rr * 0.999999f;
+        if (amb_t || (pass && amb_b)) {  // rare: exact
+            if (amb_t)  // |a|^2 and |b|^2 < 2^24: exact as floats
+                pass = (unsigned long long)(100ll * d * d) > 81ull * (unsigned long long)((long long)cna * (int)frn2[j]);
+            win = better_i32(d, cna, cp, bd[j], (int)fbn[j], bk[j]);
         }
+        win = win && pass;
+        bd[j] = win ? d : bd[j];
+        bk[j] = win ? cp : bk[j];
+        fbq[j] = win ? fd2 : fbq[j];
+        fbn[j] = win ? fna : fbn[j];
     }
 }
 
@@ -1016,7 +1034,7 @@ constexpr int kWQ = 16;            // queries per wave
 constexpr int kWaveList = 512;     // candidate-list capacity per wave (more: several passes)
 
 __device__ __forceinline__ void load_bfrag(const int8_t *d0, int R, int xy, bool ok, int h, i32x4_t *bf) {
-    const i32x4_t *src = reinterpret_cast<const i32x4_t *>(d0 + ((long)(xy >> 6) * R + (xy & 63)) * kDescD + 16 * h);
+    const i32x4_t *src = reinterpret_cast<const i32x4_t *>(d0 + (unsigned)(((xy >> 6) * R + (xy & 63)) * kDescD + 16 * h));  // < 2^32: one frame
 #pragma unroll
     for (int s2 = 0; s2 < 4; s2++) bf[s2] = ok ? src[4 * s2] : i32x4_t{0, 0, 0, 0};
 }
@@ -1069,15 +1087,17 @@ __global__ __launch_bounds__(256, WIN_WPE) void k_window_wave(WinArgs a, int blo
     n2 += __shfl_xor(n2, 16, 64);
     n2 += __shfl_xor(n2, 32, 64);
     const int qcx = rv ? qp / R + a.shift_x : -(1 << 20), qcy = rv ? qp % R + a.shift_y : -(1 << 20);
-    int rn2[4], rcx[4], rcy[4], bd[4], bn[4], bk[4];
+    int rcx[4], rcy[4], bd[4], bk[4];
+    float frn2[4], fbq[4], fbn[4];  // |query|^2, the best's d^2 and |candidate|^2 (the norms exact)
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-        rn2[j] = __shfl(n2, 4 * h + j, 64);
+        frn2[j] = (float)__shfl(n2, 4 * h + j, 64);
         rcx[j] = __shfl(qcx, 4 * h + j, 64);
         rcy[j] = __shfl(qcy, 4 * h + j, 64);
         bd[j] = 0;
-        bn[j] = 1;
         bk[j] = -1;
+        fbq[j] = 0.f;
+        fbn[j] = 1.f;
     }
     // candidate list: columns cx0 .. cx1 (<= 64 when the 16 queries span <= 64 - 2r columns;
     // wider spans take the column groups in turn), scan order, in passes of kWaveList
@@ -1090,7 +1110,7 @@ __global__ __launch_bounds__(256, WIN_WPE) void k_window_wave(WinArgs a, int blo
             const int y = __shfl_up(incl, o, 64);
             if (lane >= o) incl += y;
         }
-        const int total = __shfl(incl, 63, 64);
+        const int total = __builtin_amdgcn_readfirstlane(__shfl(incl, 63, 64));  // uniform: scalar loops
         for (int lb = 0; lb < total; lb += kWaveList) {
             {
                 int pos = incl - cnt - lb;
@@ -1126,7 +1146,7 @@ __global__ __launch_bounds__(256, WIN_WPE) void k_window_wave(WinArgs a, int blo
                 const bool cv = cr < nc;
                 const int cx = cv ? xycur >> 6 : (1 << 24), cy = xycur & 63;
                 const int cp = cx * R + cy;
-                window_fold(acc, cv, cx, cy, cp, cna, r, rcx, rcy, rn2, bd, bn, bk);
+                window_fold(acc, cv, cx, cy, cp, cna, r, rcx, rcy, frn2, bd, bk, fbq, fbn);
                 if (more) {
 #pragma unroll
                     for (int s2 = 0; s2 < 4; s2++) bcur[s2] = bnxt[s2];
@@ -1137,15 +1157,17 @@ __global__ __launch_bounds__(256, WIN_WPE) void k_window_wave(WinArgs a, int blo
     }
 #pragma unroll
     for (int j = 0; j < 4; j++) {
+        int bn = (int)fbn[j];
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) {
-            const int od = __shfl_xor(bd[j], o, 64), on = __shfl_xor(bn[j], o, 64), ok = __shfl_xor(bk[j], o, 64);
-            if (better_i32(od, on, ok, bd[j], bn[j], bk[j])) {
+            const int od = __shfl_xor(bd[j], o, 64), on = __shfl_xor(bn, o, 64), ok = __shfl_xor(bk[j], o, 64);
+            if (better_i32(od, on, ok, bd[j], bn, bk[j])) {
                 bd[j] = od;
-                bn[j] = on;
+                bn = on;
                 bk[j] = ok;
             }
         }
+        fbn[j] = (float)bn;
     }
     if (col == 0) {
 #pragma unroll
@@ -1158,7 +1180,7 @@ __global__ __launch_bounds__(256, WIN_WPE) void k_window_wave(WinArgs a, int blo
                 res.best_patch = bk[j];
                 res.bx = bk[j] / R;
                 res.by = bk[j] % R;
-                res.score = (float)((double)bd[j] * (double)bd[j] / ((double)bn[j] * (double)rn2[j]));
+                res.score = (float)((double)bd[j] * (double)bd[j] / ((double)fbn[j] * (double)frn2[j]));
             }
             out[(long)pair * a.N + q0 + qi] = res;
         }
