@@ -47,10 +47,8 @@
 
 namespace {
 
-#ifndef AP_NW
-#define AP_NW 4  // waves per block (32 rows each): 4 -> two blocks per CU, 8 -> one
-#endif
-constexpr int NW = AP_NW, NT = 64 * NW, BM = 32 * NW, BN = 64, BK = 128, KD = 256, KS = KD / BK, RW = BM / NW;
+// NW: waves per block (32 rows each): 4 -> two blocks per CU, 8 -> one
+constexpr int NW = 4, NT = 64 * NW, BM = 32 * NW, BN = 64, BK = 128, KD = 256, KS = KD / BK, RW = BM / NW;
 constexpr int NBUF = 4;  // ring slots: two column tiles of KS = 2 slices
 constexpr int ROW_BYTES = KD * 2;                // fp16 row: 512 B
 constexpr int SL_ROW = BK * 2;                   // one row of one slice: 128 fp16 = 256 B = 16 chunks
@@ -154,12 +152,9 @@ __device__ __forceinline__ bool better(int dmode, float v, int j, float bv, int 
 }
 
 // The reference's sequential fp32 dot (mul then add, k = 0..255).  Latency-bound: loads go
-// out EXACT_U float4 per operand at a time (EXACT_U = 16: four round trips per dot).
-#ifndef EXACT_U
-#define EXACT_U 16
-#endif
+// out U = 16 float4 per operand at a time (four round trips per dot).
 __device__ __forceinline__ float exact_dot(const float *__restrict__ a, const float *__restrict__ b) {
-    constexpr int U = EXACT_U;
+    constexpr int U = 16;
     float s = 0.f;
 #pragma unroll
     for (int bt = 0; bt < KD / (4 * U); bt++) {
@@ -186,19 +181,14 @@ __device__ __forceinline__ float exact_dot(const float *__restrict__ a, const fl
 //      8-B store writes 256 contiguous bytes); SPLIT_RPG rows per lane group per iteration,
 //      all loads issued first; a 256-thread block strides over the batch (rows >= n1 are
 //      never read downstream) ----
-#ifndef SPLIT_RPG
-#define SPLIT_RPG 4
-#endif
+constexpr int SPLIT_RPG = 4;
 constexpr int SPLIT_ROWS = 8 * SPLIT_RPG;  // rows per block iteration: 8 row groups x SPLIT_RPG
 typedef float f32x4v __attribute__((ext_vector_type(4)));
-#ifndef SPLIT_WPE
-#define SPLIT_WPE 1  // 8 (with SPLIT_RPG 2: 46 VGPRs) lets split waves co-reside with two
-                     // k_ap_match waves; measured: 0.34 -> 0.44 ms beside the pose, and the
-                     // overlapped pipeline (bench --pipeline 2/3) only +2 %: not the default
-#endif
-#ifndef SPLIT_GRID
-#define SPLIT_GRID (256 * 64)  // grid-stride blocks at most
-#endif
+// waves per EU: 8 (with SPLIT_RPG 2: 46 VGPRs) lets split waves co-reside with two k_ap_match
+// waves; measured: 0.34 -> 0.44 ms beside the pose, and the overlapped pipeline (bench
+// --pipeline 2/3) only +2 %: 1 kept
+constexpr int SPLIT_WPE = 1;
+constexpr int SPLIT_GRID = 256 * 64;  // grid-stride blocks at most
 __global__ __launch_bounds__(256, SPLIT_WPE) void k_ap_split(int batch, int cap, const int *__restrict__ n1v,
                                                   const float *__restrict__ desc1, char *__restrict__ h1,
                                                   float *__restrict__ nrm1, int *__restrict__ bad) {

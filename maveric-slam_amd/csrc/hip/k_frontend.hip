@@ -1039,9 +1039,7 @@ __device__ __forceinline__ void load_bfrag(const int8_t *d0, int R, int xy, bool
     for (int s2 = 0; s2 < 4; s2++) bf[s2] = ok ? src[4 * s2] : i32x4_t{0, 0, 0, 0};
 }
 
-#ifndef WIN_WPE
-#define WIN_WPE 2
-#endif
+constexpr int WIN_WPE = 2;  // waves per EU the launch bound asks for (the kernel takes 126 VGPRs)
 __global__ __launch_bounds__(256, WIN_WPE) void k_window_wave(WinArgs a, int blocks_per_pair, int nblocks,
                                                      const unsigned long long *__restrict__ masks,
                                                      const int8_t *__restrict__ desc0,
