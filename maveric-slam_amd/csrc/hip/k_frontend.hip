@@ -981,39 +981,37 @@ typedef int i32x4_t __attribute__((ext_vector_type(4)));
 // as-intended pass test 100 dot^2 > 81 |c|^2 |q|^2 and the exact running best.  The pass
 // test is screened in fp32 (relative error < 2^-20 on both sides) and decided in 64-bit
 // integers only within that margin.
-// the fold of one tile into the lane's 4 queries' bests, branch-free but for the rare exact cases:
-// the threshold test and the "beats the current best" test (d^2 / n, cross-multiplied) are both
-// screened in float with margins their rounding cannot cross (each side within 2.4e-7 of its exact
-// value) and decided exactly (64-bit integers) only inside the margins; fbq / fbn carry the best's
-// d^2 and n as floats for the screen (n < 2^24: the float is exact, and is the only copy kept).
+// the fold of one tile into the lane's 4 queries' bests, branch-free but for the rare exact cases.
+// The threshold is the INITIAL best: 100 d^2 > 81 |a|^2 |q|^2 is "beats (d^2, n) = (81 |q|^2, 100)",
+// and whatever beats a best that passed the threshold passes it too -- so one test per candidate,
+// d^2 n_best > d_best^2 n (ties to the lower scan position), screened in float with margins its
+// rounding cannot cross (each side within 2e-7 of its exact value) and decided exactly (64-bit
+// integers) only inside the margins; fbq / fbn carry the best's d^2 and n as floats for the screen
+// (n < 2^24: the float is exact, and is the only copy kept; bk < 0: the threshold is the best).
 // Round 5's form -- better_i32 in a branch taken by every passing candidate, the best updated
 // inside it -- picked wrong winners on the GPU in windows full of exact ties
 // (tests/test_gpu_frontend.py::test_window_match_exact_ties_and_threshold: 38 of 99 matches), while
 // a CPU emulation of its algorithm agrees with the oracle and an -O1 build of it fails differently
 // (87): the code generated for it, not the algorithm (tools/diag/dbg_window_tie.py,
-// profiles/r06l_window_tie_bisect.log).  This form passes; 2.43 against 2.29 ms per 8192 pairs.
+// profiles/r06l_window_tie_bisect.log).
 __device__ __forceinline__ void window_fold(const i32x4_t &acc, bool cv, int cx, int cy, int cp, int cna, int r,
                                             const int *rcx, const int *rcy, const float *frn2, int *bd, int *bk,
                                             float *fbq, float *fbn) {
-    const float fna = (float)cna, fna81 = 81.0f * fna;
+    const float fna = (float)cna;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
         const int d = acc[j];
         const bool in = cv && (unsigned)(cx - rcx[j] + r) <= (unsigned)(2 * r) &&
                         (unsigned)(cy - rcy[j] + r) <= (unsigned)(2 * r) && d > 0;
         const float fd = (float)d, fd2 = fd * fd;
-        const float lhs = 100.0f * fd2, rhs = fna81 * frn2[j];
-        bool pass = in && lhs > rhs * 1.000002f;
-        const bool amb_t = in && !pass && lhs >= rhs * 0.999998f;
-        const float L = fd2 * fbn[j], Rr = fbq[j] * fna;  // none yet: fbq = 0, so any d > 0 beats it
-        bool win = L > Rr * 1.000001f;
-        const bool amb_b = !win && L >= Rr * 0.999999f;
-        if (amb_t || (pass && amb_b)) {  // rare: exact
-            if (amb_t)  // |a|^2 and |b|^2 < 2^24: exact as floats
-                pass = (unsigned long long)(100ll * d * d) > 81ull * (unsigned long long)((long long)cna * (int)frn2[j]);
-            win = better_i32(d, cna, cp, bd[j], (int)fbn[j], bk[j]);
+        const float L = fd2 * fbn[j], Rr = fbq[j] * fna;
+        bool win = in && L > Rr * 1.000002f;
+        if (in && !win && L >= Rr * 0.999998f) {  // rare: exact
+            if (bk[j] < 0)  // against the threshold; |a|^2 and |q|^2 < 2^24: exact as floats
+                win = (unsigned long long)(100ll * d * d) > 81ull * (unsigned long long)((long long)cna * (int)frn2[j]);
+            else
+                win = better_i32(d, cna, cp, bd[j], (int)fbn[j], bk[j]);
         }
-        win = win && pass;
         bd[j] = win ? d : bd[j];
         bk[j] = win ? cp : bk[j];
         fbq[j] = win ? fd2 : fbq[j];
@@ -1094,8 +1092,8 @@ __global__ __launch_bounds__(256, WIN_WPE) void k_window_wave(WinArgs a, int blo
         rcy[j] = __shfl(qcy, 4 * h + j, 64);
         bd[j] = 0;
         bk[j] = -1;
-        fbq[j] = 0.f;
-        fbn[j] = 1.f;
+        fbq[j] = 81.0f * frn2[j];  // the threshold as the initial best (81 |q|^2, 100)
+        fbn[j] = 100.f;
     }
     // candidate list: columns cx0 .. cx1 (<= 64 when the 16 queries span <= 64 - 2r columns;
     // wider spans take the column groups in turn), scan order, in passes of kWaveList
