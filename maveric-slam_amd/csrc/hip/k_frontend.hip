@@ -646,7 +646,10 @@ __global__ __launch_bounds__(256) void k_window_eval(WinArgs a, const int8_t *__
 //
 // k_window_mask: one 64-bit word per frame-0 grid column, bit y set when cell (x, y) is a
 // candidate (tracking_main.c:121-125: index != 64 and !(prob < 0.2), double compare).  A
-// column's cells are contiguous (p = x*rows + y), so one wave ballots one column.
+// column's cells are contiguous (p = x*rows + y), so a wave takes 64 columns = 64 * rows
+// consecutive cells: one ballot per 64 cells (dense 256-B loads), the ballot words in the wave's
+// LDS slice, then each lane cuts its column's rows bits out of (at most) two of them.  (Round 5:
+// one wave per column, 47 of 64 lanes loading 188 B -- 2.1 TB/s, launch-bound.)
 //
 // k_window_query: one wave walks kQPW consecutive top-N queries (patch order, so the windows
 // of a wave overlap in L1/L2).  Per query the wave reads the masks of the window's columns
@@ -661,16 +664,32 @@ constexpr int kWinList = 256;  // candidate-list capacity per wave (window cells
 __global__ __launch_bounds__(256) void k_window_mask(long total_cols, int rows, const int *__restrict__ mi0,
                                                      const float *__restrict__ pr0, double prob_thr,
                                                      unsigned long long *__restrict__ masks) {
-    const long col = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (col >= total_cols) return;
-    const int y = threadIdx.x & 63;
-    bool v = false;
-    if (y < rows) {
-        const long p = col * rows + y;
-        v = mi0[p] != 64 && !((double)pr0[p] < prob_thr);
+    __shared__ unsigned long long wb[4][64];  // per wave: rows ballot words of 64 cells (rows <= 64)
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long c0 = ((long)blockIdx.x * 4 + w) * 64;  // the wave's first column
+    if (c0 >= total_cols) return;                      // wave-uniform; no block barrier below
+    const int ncol = (int)min(64l, total_cols - c0);
+    const long cell0 = c0 * rows, ncell = (long)ncol * rows;
+#pragma unroll 8
+    for (int k = 0; k < rows; k++) {
+        const long i = (long)k * 64 + lane;
+        bool v = false;
+        if (i < ncell) {
+            const long p = cell0 + i;
+            v = mi0[p] != 64 && !((double)pr0[p] < prob_thr);
+        }
+        const unsigned long long bw = __ballot(v);
+        if (lane == 0) wb[w][k] = bw;
     }
-    const unsigned long long m = __ballot(v);
-    if (y == 0) masks[col] = m;
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own LDS writes
+    __builtin_amdgcn_wave_barrier();
+    if (lane < ncol) {
+        const int sb = lane * rows, k0 = sb >> 6, off = sb & 63;
+        unsigned long long m = wb[w][k0] >> off;
+        if (off + rows > 64) m |= wb[w][k0 + 1] << (64 - off);
+        if (rows < 64) m &= (1ull << rows) - 1ull;
+        masks[c0 + lane] = m;
+    }
 }
 
 struct QueryPrefetch {
@@ -1291,7 +1310,7 @@ extern "C" int mv_window_match_batch_dev(mv_context *ctx, const mv_window_params
         unsigned long long *masks = (unsigned long long *)(sc + qr_bytes);
         const long tcols = (long)batch * cols;
         MV_PROF_BEGIN(ctx->stream, "k_window_mask");
-        hipLaunchKernelGGL(k_window_mask, dim3((unsigned)((tcols + 3) / 4)), dim3(256), 0, ctx->stream, tcols, rows,
+        hipLaunchKernelGGL(k_window_mask, dim3((unsigned)((tcols + 255) / 256)), dim3(256), 0, ctx->stream, tcols, rows,
                            max_idx0, probs0, a.prob_thr, masks);
         MV_PROF_END(ctx->stream);
         MV_LAUNCH_CHECK();
