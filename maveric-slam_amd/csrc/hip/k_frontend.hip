@@ -177,128 +177,93 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int *total, int *wsum
     return off;
 }
 
-// k_top_n_select: one 1024-thread block per frame; thread t owns the
-// contiguous cells [t*per, (t+1)*per) so that scans preserve patch order.  With PER > 0
-// (per <= PER, e.g. the 7285-cell KITTI grid) a thread's cells are read once, all loads
-// in flight together, and kept in registers for the three passes.
-template <int PER>
-__global__ __launch_bounds__(1024) void k_top_n_select(int cells, const int *__restrict__ max_idx,
-                                                       const float *__restrict__ probs, int N, int cap,
-                                                       int *__restrict__ num_sel, int *__restrict__ patches,
-                                                       int *__restrict__ indices, float *__restrict__ sel_probs,
-                                                       int *__restrict__ status) {
-    __shared__ int wsum[16];
-    __shared__ float red_max[16], red_min[16];
-    const int f = blockIdx.x, t = threadIdx.x;
-    const int per = (cells + 1023) / 1024;
-    const int c0 = t * per, c1 = min(c0 + per, cells);
+// k_top_n_select: ONE WAVE per frame (4 frames per 256-thread block, no block barrier): the frame's
+// cells in chunks of 64 consecutive ones (coalesced loads), a ballot of the valid cells per chunk
+// -- so the selection keeps patch order by construction: a selected cell's slot is the running
+// count plus the popcount of the ballot below its lane (mbcnt).  Pass 1 counts the valid cells
+// (top_N.c:71-73: index != 64 and prob > 0.01, double compare) and their min / max prob; pass 2
+// (the frame's 58 KB again, from L2) writes every valid cell when they are at most N, otherwise
+// those with prob >= the interpolated threshold (top_N.c:95-133) until N are written.
+// (Round 5: one 1024-thread block per frame, two block-wide scans -- 0.348 ms per 8192 frames,
+// latency-bound.)
+__device__ __forceinline__ int lanes_below(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+__global__ __launch_bounds__(256) void k_top_n_select(int batch, int cells, const int *__restrict__ max_idx,
+                                                      const float *__restrict__ probs, int N, int cap,
+                                                      int *__restrict__ num_sel, int *__restrict__ patches,
+                                                      int *__restrict__ indices, float *__restrict__ sel_probs,
+                                                      int *__restrict__ status) {
+    const int lane = threadIdx.x & 63;
+    const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (f >= batch) return;  // wave-uniform
     const int *mi = max_idx + (long)f * cells;
     const float *pr = probs + (long)f * cells;
-    constexpr int NR = PER > 0 ? PER : 1;
-    int mi_r[NR];
-    float pr_r[NR];
-    if (PER > 0) {
-#pragma unroll
-        for (int k = 0; k < NR; k++) {
-            const int c = c0 + k;
-            mi_r[k] = c < c1 ? mi[c] : 64;
-            pr_r[k] = c < c1 ? pr[c] : 0.0f;
-        }
-    }
-    const int n = PER > 0 ? NR : c1 - c0;
-    // cell c0 + k: (index, prob); valid per top_N.c:71-73
-    auto cell = [&](int k, int &idx, float &p) {
-        if (PER > 0) {
-            idx = mi_r[k];
-            p = pr_r[k];
-        } else {
-            idx = mi[c0 + k];
-            p = pr[c0 + k];
-        }
-        return idx != 64 && (double)p > 0.01;
-    };
-    int nv_local = 0;
+    int nv = 0;
     float pmax = 0.0f, pmin = 3.40282347e+38f;  // FLT_MAX
-    for (int k = 0; k < n; k++) {
-        int idx;
-        float p;
-        if (cell(k, idx, p)) {
-            nv_local++;
-            pmax = fmaxf(pmax, p);
-            pmin = fminf(pmin, p);
+    constexpr int U = 4;                        // chunks in flight
+    for (int base = 0; base < cells; base += 64 * U) {
+        int idx[U];
+        float p[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int c = base + 64 * u + lane;
+            idx[u] = c < cells ? mi[c] : 64;
+            p[u] = c < cells ? pr[c] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const bool v = idx[u] != 64 && (double)p[u] > 0.01;
+            nv += __popcll(__ballot(v));
+            if (v) {
+                pmax = fmaxf(pmax, p[u]);
+                pmin = fminf(pmin, p[u]);
+            }
         }
     }
-    int nv;
-    int off = block_exclusive_scan<1024>(nv_local, &nv, wsum);
-    // block max / min (exact, order-independent)
-    for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {  // exact, order-independent
         pmax = fmaxf(pmax, __shfl_xor(pmax, o, 64));
         pmin = fminf(pmin, __shfl_xor(pmin, o, 64));
     }
-    if ((t & 63) == 0) {
-        red_max[t >> 6] = pmax;
-        red_min[t >> 6] = pmin;
-    }
-    __syncthreads();
-    if (t == 0) {
-        for (int i = 1; i < 16; i++) {
-            red_max[0] = fmaxf(red_max[0], red_max[i]);
-            red_min[0] = fminf(red_min[0], red_min[i]);
-        }
-    }
-    __syncthreads();
-    pmax = red_max[0];
-    pmin = red_min[0];
-    int *op = patches + (long)f * N;
-    int *oi = indices + (long)f * N;
-    float *opr = sel_probs + (long)f * N;
     if (nv >= cap) {  // the reference exits here (top_N.c:91-94)
-        if (t == 0) {
+        if (lane == 0) {
             num_sel[f] = 0;
             status[f] = MV_ERR_CAPACITY;
         }
         return;
     }
-    if (nv <= N) {
-        int k = off;
-        for (int j = 0; j < n; j++) {
-            int idx;
-            float p;
-            if (cell(j, idx, p)) {
-                op[k] = c0 + j;
-                oi[k] = idx;
-                opr[k] = p;
-                k++;
-            }
-        }
-        if (t == 0) {
-            num_sel[f] = nv;
-            status[f] = MV_OK;
-        }
-        return;
-    }
+    const bool all = nv <= N;
     const float split = (float)N / (float)nv;
-    const float thr = pmax * split + pmin * (1 - split);
-    int ns_local = 0;
-    for (int j = 0; j < n; j++) {
-        int idx;
-        float p;
-        if (cell(j, idx, p) && p >= thr) ns_local++;
-    }
-    int ns;
-    int k = block_exclusive_scan<1024>(ns_local, &ns, wsum);
-    for (int j = 0; j < n; j++) {
-        int idx;
-        float p;
-        if (k < N && cell(j, idx, p) && p >= thr) {
-            op[k] = c0 + j;
-            oi[k] = idx;
-            opr[k] = p;
-            k++;
+    const float thr = all ? 0.0f : pmax * split + pmin * (1 - split);
+    int *op = patches + (long)f * N;
+    int *oi = indices + (long)f * N;
+    float *opr = sel_probs + (long)f * N;
+    int k = 0;  // cells selected so far (wave-uniform)
+    for (int base = 0; base < cells && k < N; base += 64 * U) {
+        int idx[U];
+        float p[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int c = base + 64 * u + lane;
+            idx[u] = c < cells ? mi[c] : 64;
+            p[u] = c < cells ? pr[c] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const bool sel = idx[u] != 64 && (double)p[u] > 0.01 && (all || p[u] >= thr);
+            const unsigned long long m = __ballot(sel);
+            const int pos = k + lanes_below(m);
+            if (sel && pos < N) {
+                op[pos] = base + 64 * u + lane;
+                oi[pos] = idx[u];
+                opr[pos] = p[u];
+            }
+            k += __popcll(m);
         }
     }
-    if (t == 0) {
-        num_sel[f] = min(ns, N);
+    if (lane == 0) {
+        num_sel[f] = all ? nv : min(k, N);
         status[f] = MV_OK;
     }
 }
@@ -670,7 +635,6 @@ __global__ __launch_bounds__(256) void k_window_mask(long total_cols, int rows, 
     if (c0 >= total_cols) return;                      // wave-uniform; no block barrier below
     const int ncol = (int)min(64l, total_cols - c0);
     const long cell0 = c0 * rows, ncell = (long)ncol * rows;
-#pragma unroll 8
     for (int k = 0; k < rows; k++) {
         const long i = (long)k * 64 + lane;
         bool v = false;
@@ -1264,12 +1228,8 @@ int launch_top_n_select(hipStream_t s, int batch, int cells, const int *max_idx,
                         int cap, int *num_sel, int *patches, int *indices, float *sel_probs, int *status) {
     MV_REQUIRE(batch > 0 && cells > 0 && N > 0 && cap > 0);
     MV_PROF_BEGIN(s, "k_top_n_select");
-    if (cells <= 8 * 1024)
-        hipLaunchKernelGGL(k_top_n_select<8>, dim3(batch), dim3(1024), 0, s, cells, max_idx, probs, N, cap,
-                           num_sel, patches, indices, sel_probs, status);
-    else
-        hipLaunchKernelGGL(k_top_n_select<0>, dim3(batch), dim3(1024), 0, s, cells, max_idx, probs, N, cap,
-                           num_sel, patches, indices, sel_probs, status);
+    hipLaunchKernelGGL(k_top_n_select, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0, s, batch, cells, max_idx,
+                       probs, N, cap, num_sel, patches, indices, sel_probs, status);
     MV_PROF_END(s);
     MV_LAUNCH_CHECK();
     return MV_OK;
