@@ -87,6 +87,8 @@ def parse(argv=None):
                     help="initialise the process group (--dist-backend) and issue the per-step result all-gather "
                          "even at world size 1 -- how the RCCL gather on the pipelined streams is exercised on a "
                          "one-GPU box (a one-rank all_gather_into_tensor is a device-side copy through RCCL)")
+    ap.add_argument("--gather-every", type=int, default=0,
+                    help="steps whose per-pair results share one all-gather (0: the pipeline depth)")
     ap.add_argument("--harness-cpu", action="store_true",
                     help="test only: the multi-rank harness with the CPU oracle as the step (gloo)")
     ap.add_argument("--dist-timeout", type=float, default=180.0,
@@ -267,31 +269,52 @@ class _NullCtx:
 
 
 class ResultGather:
-    """one all-gather per batch of every pair's result -- T (3x4 fp32) and the
-    match count, 13 words = 52 B per pair -- into a [world * B, 13] buffer on every rank (rank 0
-    keeps it for the report / trajectory chain).  Issued on the stream that produced the
-    results, so it is ordered after that batch's pose; a no-op without a process group (world
-    size 1 unless --force-gather)."""
+    """an all-gather of every pair's result -- T (3x4 fp32) and the match count, 13
+    words = 52 B per pair -- into a [world * rows, 13] buffer on every rank (rank 0 keeps it for
+    the report / trajectory chain).  The results of `every` consecutive steps (one per pipelined
+    context, `every` = the pipeline depth by default) share ONE all-gather, issued on the last
+    step's stream after it has waited for the others' copies: one collective launch per pipeline
+    cycle instead of one per step (one GPU with a forced RCCL group: 1.6 % of the step against
+    2.6 % per step, profiles/r06bb_gather_ab.log).  A no-op without a process group (world size 1
+    unless --force-gather)."""
 
-    def __init__(self, torch, dist, world, B, device, slots, coll_device=None):
+    def __init__(self, torch, dist, world, B, device, slots, coll_device=None, every=1):
         self.torch, self.dist, self.world = torch, dist, world
         self.active = dist.is_available() and dist.is_initialized()
         self.coll_device = device if coll_device is None else coll_device  # gloo + GPU results: via the host
-        self.res = [torch.empty((B, 13), dtype=torch.float32, device=device) for _ in range(slots)]
-        self.out = [torch.empty((world * B, 13), dtype=torch.float32, device=self.coll_device) for _ in range(slots)]
-        self.count = 0
+        self.every, self.B = max(1, every), B
+        self.res = [torch.empty((self.every * B, 13), dtype=torch.float32, device=device) for _ in range(2)]
+        self.out = [torch.empty((world * self.every * B, 13), dtype=torch.float32, device=self.coll_device)
+                    for _ in range(2)]
+        self.count = 0  # collectives issued
+        self.steps = 0
+        self.events = []
 
     def __call__(self, slot, T, nmatch, stream=None):
         if not self.active:
             return
         torch = self.torch
+        k = self.steps % self.every  # this step's rows in the current group
+        g = (self.steps // self.every) & 1  # double-buffered groups
+        self.steps += 1
         with (torch.cuda.stream(stream) if stream is not None else _NullCtx()):
-            r = self.res[slot]
+            r = self.res[g][k * self.B:(k + 1) * self.B]
             r[:, :12].copy_(T.reshape(T.shape[0], 12))
             r[:, 12].copy_(nmatch.view(torch.float32))
-            if str(r.device) != str(self.coll_device):
-                r = r.to(self.coll_device)  # ordered on `stream` (a blocking copy for the host)
-            self.dist.all_gather_into_tensor(self.out[slot], r)
+            if k + 1 < self.every:
+                ev = torch.cuda.Event()
+                ev.record()
+                self.events.append(ev)
+                return
+            if self.events:  # the group's other copies, made on the other contexts' streams
+                cur = torch.cuda.current_stream()
+                for ev in self.events:
+                    cur.wait_event(ev)
+                self.events = []
+            full = self.res[g]
+            if str(full.device) != str(self.coll_device):
+                full = full.to(self.coll_device)  # ordered on `stream` (a blocking copy for the host)
+            self.dist.all_gather_into_tensor(self.out[g], full)
         self.count += 1
 
 
@@ -695,7 +718,7 @@ def main():
     K = synth.KITTI_K
     pose_p = mvtrack.pose_params(mvtrack.AS_INTENDED, fx=K[0, 0], fy=K[1, 1], cx=K[0, 2], cy=K[1, 2],
                                  hypotheses=args.hypotheses, inlier_thresh=1.0, refine_iters=10, seed=7)
-    gather = ResultGather(torch, dist, world, B, dev, P, coll_dev)
+    gather = ResultGather(torch, dist, world, B, dev, P, coll_dev, every=args.gather_every or P)
 
     # the reference keeps only the matched pairs (pairwise_pnp.py:649-657): no score output, so
     # the exact re-score runs only where the rounding window does not decide the row (indices
@@ -792,15 +815,17 @@ def main():
         err = np.abs(R - synth.T_785_786[None, :, :3]).max(axis=(1, 2))
         assert ok == B and float(err.max()) < 1e-3, "pose failed: ok=%d max|dR|=%g" % (ok, err.max())
     gathered = None
-    if gather.active:  # the per-step all-gather's buffers: every rank's results, this rank's own slice
-        sync()         # equal to its T and match count bit for bit, in every pipelined slot
-        for c in range(P):
-            g = gather.out[c].view(world, B, 13)
-            assert torch.equal(g[rank, :, :12].to(dev).view(torch.int32), Ts[c].reshape(B, 12).view(torch.int32)), \
-                "gathered T differs from this rank's (slot %d)" % c
-            assert torch.equal(g[rank, :, 12].contiguous().to(dev).view(torch.int32), nmatches[c]), \
-                "gathered match count differs from this rank's (slot %d)" % c
-        g = gather.out[0].view(world, B, 13)
+    if gather.active:  # the last all-gather's buffer: every rank's results, this rank's own slice
+        sync()         # equal to its T and match count bit for bit, for every step of the group
+        E = gather.every
+        g = gather.out[((gather.steps // E) - 1) & 1].view(world, E, B, 13)
+        for k in range(E):
+            c = k % P
+            assert torch.equal(g[rank, k, :, :12].to(dev).view(torch.int32), Ts[c].reshape(B, 12).view(torch.int32)), \
+                "gathered T differs from this rank's (step %d of the group)" % k
+            assert torch.equal(g[rank, k, :, 12].contiguous().to(dev).view(torch.int32), nmatches[c]), \
+                "gathered match count differs from this rank's (step %d of the group)" % k
+        g = g.reshape(world, E * B, 13)
         props = torch.cuda.get_device_properties(local)
         me = {"rank": rank, "device": local, "backend": dist.get_backend(),
               "pci_bus": "%s:%s" % (getattr(props, "pci_domain_id", "?"), getattr(props, "pci_bus_id", "?")),
@@ -809,7 +834,7 @@ def main():
         dist.all_gather_object(ranks, me)  # validation only: which device / backend every rank ran on
         gathered = {"ranks": ranks, "pairs_per_gather": int(g.shape[0] * g.shape[1]), "gathers_in_timed_steps": gathers_timed,
                     "bytes_per_gather": int(g.numel() * 4), "backend": args.dist_backend,
-                    "slots_checked_bitwise": P, "streams": "pipelined" if P > 1 else "current",
+                    "steps_per_gather": gather.every, "streams": "pipelined" if P > 1 else "current",
                     "ranks_per_device": "%d ranks on %d device(s)" % (world, torch.cuda.device_count())}
     sums = gather_checksums(torch, dist, [float(nmatch.sum().item()), float(ok)], coll_dev)
     pairs_total = B * args.steps * world

@@ -99,7 +99,7 @@ def test_pipelined_contexts_equal_sequential(ctx, orc, torch_cuda, P):
 def test_bench_two_ranks_on_the_hip_path():
     """bench.py's N-rank GPU path (not the --harness-cpu rehearsal): --gpus 2 spawns two rank
     processes that run the HIP match + pose on their own disjoint pair shards and all-gather every
-    pair's result per step.  On a one-GPU box both ranks map to cuda:0 (LOCAL_RANK modulo the
+    pair's result (one gather per pipeline cycle of 3 steps).  On a one-GPU box both ranks map to cuda:0 (LOCAL_RANK modulo the
     visible devices) and the gather goes through gloo (RCCL refuses two ranks on one device); the
     nccl branch is the same code with the device-resident gather.  Checks: n_gpus 2, the gathered
     buffer holds 2 x B pairs, each rank's slice equals its own results (asserted inside bench.py),
@@ -122,7 +122,9 @@ def test_bench_two_ranks_on_the_hip_path():
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert d["n_gpus"] == 2 and d["steps"] == 3
     g = d["result_gather"]
-    assert g["pairs_per_gather"] == 2 * B and g["backend"] == "gloo" and g["gathers_in_timed_steps"] >= 4
+    # the 3 pipelined contexts' results share one all-gather per cycle (4 steps: one full cycle)
+    assert g["steps_per_gather"] == 3 and g["pairs_per_gather"] == 2 * 3 * B and g["backend"] == "gloo"
+    assert g["gathers_in_timed_steps"] >= 1
     assert d["pose_ok"] == 2 * B and d["checked_pairs"] == 2 and d["value"] > 0
     assert d["with_scores"] is not None
 
@@ -192,9 +194,9 @@ def test_graph_capture_through_set_stream(ctx, orc, torch_cuda):
 def test_bench_rccl_result_gather_one_rank():
     """bench.py's per-step result all-gather through RCCL (scripts/run_pairwise_pnp.sh:
     7-20 shards the pairs): --force-gather builds an nccl process group at world size 1, so each
-    pipelined step's all_gather_into_tensor runs device-resident on the stream (one of three) that
-    produced the results.  bench.py asserts every slot's gathered rows equal that context's T and
-    match counts bit for bit; here: the backend is nccl, the gathers ran inside the timed steps, and
+    pipeline cycle's all_gather_into_tensor runs device-resident on the stream of the cycle's last
+    step, after waiting for the other two contexts' copies.  bench.py asserts every step's gathered
+    rows equal that context's T and match counts bit for bit; here: the backend is nccl, the gathers ran inside the timed steps, and
     the matches equal the oracle's (--check)."""
     import json
     import os
@@ -214,7 +216,7 @@ def test_bench_rccl_result_gather_one_rank():
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     g = d["result_gather"]
-    assert g is not None and g["backend"] == "nccl" and g["pairs_per_gather"] == B
-    assert g["slots_checked_bitwise"] == 3 and g["streams"] == "pipelined"
-    assert g["gathers_in_timed_steps"] >= 5  # warmup + timed steps
+    assert g is not None and g["backend"] == "nccl" and g["pairs_per_gather"] == 3 * B
+    assert g["steps_per_gather"] == 3 and g["streams"] == "pipelined"
+    assert g["gathers_in_timed_steps"] >= 1  # one per pipeline cycle of the 5 warmup + timed steps
     assert d["n_gpus"] == 1 and d["pose_ok"] == B and d["checked_pairs"] == 2
