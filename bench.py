@@ -967,7 +967,7 @@ def main():
         # the quantized SuperPoint network (KITTI frames -> int8 semi / desc)
         import bench_superpoint
 
-        r = bench_superpoint.run(batch=64, steps=args.extra_steps, warmup=2, check=1)
+        r = bench_superpoint.run(batch=512, steps=args.extra_steps, warmup=2, check=1)
         out["superpoint"] = {k: r[k] for k in ("metric", "value", "unit", "batch", "ms_per_step", "stages_ms",
                                                 "mfma_roofline", "oracle_exact")}
         # the fp32 path of pairwise_pnp.py:577-694 from 8-bit frames to poses (SURVEY 8(f)1 + 2), in

@@ -54,7 +54,7 @@ def cpu_baseline(imgs, weights, seconds):
                       % (total, dt, threads)}
 
 
-def run(batch=64, steps=10, warmup=2, check=1, cpu_seconds=0.0, oh=192, ow=640):
+def run(batch=512, steps=10, warmup=2, check=1, cpu_seconds=0.0, oh=192, ow=640):
     dev = torch.device("cuda", 0)
     W = dict(np.load(os.path.join(ROOT, "tests", "golden", "superpoint_qnonorm.npz")))
     ims = np.load(os.path.join(ROOT, "tests", "golden", "kitti00_images.npz"))
@@ -113,7 +113,7 @@ def run(batch=64, steps=10, warmup=2, check=1, cpu_seconds=0.0, oh=192, ow=640):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--check", type=int, default=1)
