@@ -955,7 +955,7 @@ def main():
         import bench_keypoints
         import bench_sequence
 
-        r = bench_i8.run(batch=2048, kp=2048, steps=args.extra_steps, warmup=2, check=1)
+        r = bench_i8.run(batch=8192, kp=2048, steps=args.extra_steps, warmup=2, check=1)
         out["i8_allpairs"] = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "stages_ms",
                                                   "mfma_roofline", "checked_pairs")}
         r = bench_sequence.run(frames=B + 1, kp=n, steps=args.extra_steps, warmup=2, check=1, pipeline=P)

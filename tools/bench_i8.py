@@ -22,7 +22,7 @@ I8_PEAK_TOPS = 5000.0  # MI355X_MICROARCH.md: v_mfma_i32_32x32x32_i8 = 2x the BF
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--batch", type=int, default=2048,
+    ap.add_argument("--batch", type=int, default=8192,
                     help="pairs per launch (256 / 1024 / 2048 measured 0.67 / 0.76 / 0.80 M pairs/s)")
     ap.add_argument("--kp", type=int, default=2048)
     ap.add_argument("--steps", type=int, default=20)
@@ -33,7 +33,7 @@ def main():
     print(json.dumps(run(args.batch, args.kp, args.steps, args.warmup, args.check, args.cpu_seconds)), flush=True)
 
 
-def run(batch=2048, kp=2048, steps=20, warmup=3, check=1, cpu_seconds=0.0):
+def run(batch=8192, kp=2048, steps=20, warmup=3, check=1, cpu_seconds=0.0):
     args = argparse.Namespace(batch=batch, kp=kp, steps=steps, warmup=warmup, check=check, cpu_seconds=cpu_seconds)
     B, n, D = args.batch, args.kp, 256
     dev = torch.device("cuda", 0)
