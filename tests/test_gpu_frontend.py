@@ -240,3 +240,14 @@ def test_window_match_exact_ties_and_threshold(ctx, orc, grid, radius):
     n = _window_case(ctx, orc, g0, g1, False, N=N, cap=100000, radius=radius, max_matches=M)
     assert n > 0
     _window_case(ctx, orc, g0, g1, True, N=N, cap=100000, radius=radius, max_matches=M)
+
+
+@pytest.mark.parametrize("grid", [(64, 12), (1, 300), (63, 7)])
+def test_window_match_grid_edges(ctx, orc, grid):
+    """grids at the column-mask edges: 64 rows (a column is exactly one mask word), one row (64
+    columns per ballot word), 63 rows (columns straddling ballot words) -- k_window_mask's 64
+    columns per wave and the per-wave window kernel, both semantics"""
+    rows, cols = grid
+    f0, f1 = synth.synth_window_pair(91, rows=rows, cols=cols)
+    for built in (False, True):
+        _window_case(ctx, orc, f0, f1, built, N=100, cap=100000)
