@@ -1015,10 +1015,15 @@ constexpr int kWQ = 16;            // queries per wave
 
 constexpr int kWaveList = 512;     // candidate-list capacity per wave (more: several passes)
 
-__device__ __forceinline__ void load_bfrag(const int8_t *d0, int R, int xy, bool ok, int h, i32x4_t *bf) {
+// (every lane loads a listed cell: lanes past the list's end repeat its last entry and are not
+// folded, so no load is masked -- the zero-filled masked form cost 16 VALU moves per tile:
+// 2.315 -> 2.278 ms, profiles/r06in_window_unmasked_ab.log.  Measured and not kept: two fragment
+// sets taking turns instead of the per-tile copy bcur = bnxt -- 145 VGPRs, 3 waves per SIMD, 2.65 ms;
+// capped at 128 VGPRs it spills, 2.65 ms, profiles/r06im_window_pingpong_ab.log)
+__device__ __forceinline__ void load_bfrag(const int8_t *d0, int R, int xy, int h, i32x4_t *bf) {
     const i32x4_t *src = reinterpret_cast<const i32x4_t *>(d0 + (unsigned)(((xy >> 6) * R + (xy & 63)) * kDescD + 16 * h));  // < 2^32: one frame
 #pragma unroll
-    for (int s2 = 0; s2 < 4; s2++) bf[s2] = ok ? src[4 * s2] : i32x4_t{0, 0, 0, 0};
+    for (int s2 = 0; s2 < 4; s2++) bf[s2] = src[4 * s2];
 }
 
 constexpr int WIN_WPE = 2;  // waves per EU the launch bound asks for (the kernel takes 126 VGPRs)
@@ -1107,12 +1112,12 @@ __global__ __launch_bounds__(256, WIN_WPE) void k_window_wave(WinArgs a, int blo
             const int ntiles = (nc + 15) >> 4;
             i32x4_t bcur[4], bnxt[4];
             int xycur = lst[min(col, nc - 1)];
-            load_bfrag(d0, R, xycur, col < nc, h, bcur);
+            load_bfrag(d0, R, xycur, h, bcur);
             for (int nt = 0; nt < ntiles; nt++) {  // B fragments one tile ahead
                 const int cr = nt * 16 + col;
                 const bool more = nt + 1 < ntiles;
                 const int xynxt = more ? lst[min(cr + 16, nc - 1)] : 0;
-                if (more) load_bfrag(d0, R, xynxt, cr + 16 < nc, h, bnxt);
+                if (more) load_bfrag(d0, R, xynxt, h, bnxt);
                 i32x4_t acc = {0, 0, 0, 0};
                 int cna = 0;
 #pragma unroll
