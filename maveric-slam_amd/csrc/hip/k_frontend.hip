@@ -1015,15 +1015,21 @@ constexpr int kWQ = 16;            // queries per wave
 
 constexpr int kWaveList = 512;     // candidate-list capacity per wave (more: several passes)
 
-// (every lane loads a listed cell: lanes past the list's end repeat its last entry and are not
-// folded, so no load is masked -- the zero-filled masked form cost 16 VALU moves per tile:
-// 2.315 -> 2.278 ms, profiles/r06in_window_unmasked_ab.log.  Measured and not kept: two fragment
-// sets taking turns instead of the per-tile copy bcur = bnxt -- 145 VGPRs, 3 waves per SIMD, 2.65 ms;
-// capped at 128 VGPRs it spills, 2.65 ms, profiles/r06im_window_pingpong_ab.log)
-__device__ __forceinline__ void load_bfrag(const int8_t *d0, int R, int xy, int h, i32x4_t *bf) {
-    const i32x4_t *src = reinterpret_cast<const i32x4_t *>(d0 + (unsigned)(((xy >> 6) * R + (xy & 63)) * kDescD + 16 * h));  // < 2^32: one frame
-#pragma unroll
-    for (int s2 = 0; s2 < 4; s2++) bf[s2] = src[4 * s2];
+
+constexpr int kWinTileB = 16 * kDescD;  // one staged tile: 16 candidates x 256 B
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 in the clobber list (as k_allpairs_i8.hip)
+// 64 lanes x 16 B from global (SGPR base + per-lane 32-bit offset) into LDS at M0 (wave-uniform)
+__device__ __forceinline__ void glds16_win(const void *sbase, unsigned voff, unsigned lds_byte) {
+    asm volatile(
+        "s_mov_b32 m0, %2\n\t"
+        "global_load_lds_dwordx4 %0, %1"
+        :
+        : "v"(voff), "s"(sbase), "s"(lds_byte)
+        : "memory", "m0");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm_win() {
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
 constexpr int WIN_WPE = 2;  // waves per EU the launch bound asks for (the kernel takes 126 VGPRs)
@@ -1035,6 +1041,7 @@ __global__ __launch_bounds__(256, WIN_WPE) void k_window_wave(WinArgs a, int blo
                                                      const int *__restrict__ patches1,
                                                      QueryResult *__restrict__ out) {
     __shared__ unsigned short lst_s[4][kWaveList];
+    __shared__ __attribute__((aligned(16))) char bst_s[4][2][kWinTileB];  // per wave: 2 staged tiles
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int b = blockIdx.x, per_xcd = gridDim.x >> 3;
     const int logical = (b & 7) * per_xcd + (b >> 3);
@@ -1110,19 +1117,45 @@ __global__ __launch_bounds__(256, WIN_WPE) void k_window_wave(WinArgs a, int blo
             }
             const int nc = min(kWaveList, total - lb);
             const int ntiles = (nc + 15) >> 4;
-            i32x4_t bcur[4], bnxt[4];
-            int xycur = lst[min(col, nc - 1)];
-            load_bfrag(d0, R, xycur, h, bcur);
-            auto tile = [&](int nt, int xyc) {
+            // B tiles by LDS-DMA into the wave's 2-slot ring, two tiles ahead of the MFMAs (no VGPRs
+            // held for the prefetch): instruction k of a tile stages candidates 4 k .. 4 k + 3, lane l
+            // -> candidate 4 k + (l >> 4), LDS chunk l & 15 <- source chunk (l & 15) ^ candidate
+            // (16-B chunks XOR-swizzled by candidate: the fragment reads are conflict-free); lanes past
+            // the list repeat its last cell and are not folded.  The sweep waits on these gathers, not
+            // on its VALU (rocprof: VALU issue ~35 % of the SIMD cycles, profiles/r06it_window_pmc.txt):
+            // one tile ahead in registers 2.226 ms, two ahead through LDS 2.13 (r06iu_window_dma_ab.log).
+            // (Round 6 before this: the register prefetch unmasked and its last tile peeled, 2.315 ->
+            // 2.226 ms, r06in / r06io; two register sets taking turns: 145 VGPRs, 2.65 ms, r06im.)
+            const unsigned ring = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char *)&bst_s[w][0][0];
+            auto stage = [&](int t) {
+                const unsigned dst = __builtin_amdgcn_readfirstlane(ring + (unsigned)((t & 1) * kWinTileB));
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int c = 4 * k + (lane >> 4);
+                    const int xy = lst[min(t * 16 + c, nc - 1)];
+                    const unsigned voff =
+                        (unsigned)(((xy >> 6) * R + (xy & 63)) * kDescD) + ((unsigned)((lane & 15) ^ c) << 4);
+                    glds16_win(d0, voff, dst + 1024u * k);
+                }
+            };
+            auto tile = [&](int nt) {
                 const int cr = nt * 16 + col;
+                const int xyc = lst[min(cr, nc - 1)];
+                const i32x4_t *sb = reinterpret_cast<const i32x4_t *>(&bst_s[w][nt & 1][0]) + col * 16;
+                i32x4_t bc[4];
+#pragma unroll
+                for (int s2 = 0; s2 < 4; s2++) bc[s2] = sb[(4 * s2 + h) ^ col];
                 i32x4_t acc = {0, 0, 0, 0};
                 int cna = 0;
 #pragma unroll
                 for (int s2 = 0; s2 < 4; s2++) {
-                    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[s2], bcur[s2], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[s2], bc[s2], acc, 0, 0, 0);
 #pragma unroll
-                    for (int u = 0; u < 4; u++) cna = __builtin_amdgcn_sdot4(bcur[s2][u], bcur[s2][u], cna, false);
+                    for (int u = 0; u < 4; u++) cna = __builtin_amdgcn_sdot4(bc[s2][u], bc[s2][u], cna, false);
                 }
+                // the slot's reads are done (their values were consumed above): stage tile nt + 2 into it
+                __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+                if (nt + 2 < ntiles) stage(nt + 2);
                 cna += __shfl_xor(cna, 16, 64);
                 cna += __shfl_xor(cna, 32, 64);
                 const bool cv = cr < nc;
@@ -1130,19 +1163,15 @@ __global__ __launch_bounds__(256, WIN_WPE) void k_window_wave(WinArgs a, int blo
                 const int cp = cx * R + cy;
                 window_fold(acc, cv, cx, cy, cp, cna, r, rcx, rcy, frn2, bd, bk, fbq, fbn);
             };
-            // B fragments one tile ahead; the last tile peeled, so that the loop's loads and the
-            // copy bcur = bnxt are unconditional (a conditional load made the compiler copy the
-            // fragments twice per tile: 2.280 -> 2.226 ms, profiles/r06io_window_peel_ab.log)
-            int nt = 0;
-            for (; nt + 1 < ntiles; nt++) {
-                const int xynxt = lst[min(nt * 16 + 16 + col, nc - 1)];
-                load_bfrag(d0, R, xynxt, h, bnxt);
-                tile(nt, xycur);
-#pragma unroll
-                for (int s2 = 0; s2 < 4; s2++) bcur[s2] = bnxt[s2];
-                xycur = xynxt;
+            stage(0);
+            if (ntiles > 1) stage(1);
+            for (int nt = 0; nt < ntiles; nt++) {  // wave-uniform
+                if (nt + 1 < ntiles)
+                    wait_vm_win<4>();  // tile nt landed (tile nt + 1's 4 pieces may be in flight)
+                else
+                    wait_vm_win<0>();
+                tile(nt);
             }
-            tile(nt, xycur);
         }
     }
 #pragma unroll
