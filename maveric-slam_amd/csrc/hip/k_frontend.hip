@@ -1041,7 +1041,9 @@ __global__ __launch_bounds__(256, WIN_WPE) void k_window_wave(WinArgs a, int blo
                                                      const int *__restrict__ patches1,
                                                      QueryResult *__restrict__ out) {
     __shared__ unsigned short lst_s[4][kWaveList];
-    __shared__ __attribute__((aligned(16))) char bst_s[4][2][kWinTileB];  // per wave: 2 staged tiles
+    // per wave: 2 staged tiles (3: 52 KiB per block, 3 blocks -- waves per SIMD -- per CU instead of 4,
+    // 2.56 against 2.12 ms, profiles/r06iv_window_ring3_ab.log)
+    __shared__ __attribute__((aligned(16))) char bst_s[4][2][kWinTileB];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int b = blockIdx.x, per_xcd = gridDim.x >> 3;
     const int logical = (b & 7) * per_xcd + (b >> 3);
