@@ -1007,9 +1007,9 @@ __device__ __forceinline__ void window_fold(const i32x4_t &acc, bool cv, int cx,
 // Window match, per-wave MFMA (as-intended; the default): one wave owns 16 consecutive
 // top-N queries of a pair -- patch order, so they span a few grid columns -- and sweeps the
 // candidates of the union of their windows' columns (column masks -> scan-ordered list in the
-// wave's LDS slice) with v_mfma_i32_16x16x64_i8, B fragments gathered straight from L2/HBM one
-// 16-candidate tile ahead.  No block barrier and no shared staging: latency is hidden by
-// occupancy (waves are independent).
+// wave's LDS slice) with v_mfma_i32_16x16x64_i8, the candidates' rows gathered by LDS-DMA into
+// the wave's own 2-tile ring two 16-candidate tiles ahead.  No block barrier and nothing shared
+// between waves: the rest of the gather latency is hidden by occupancy (4 waves per SIMD).
 // ---------------------------------------------------------------------------
 constexpr int kWQ = 16;            // queries per wave
 
