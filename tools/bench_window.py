@@ -157,15 +157,17 @@ def window_dram(B, cells, N, win_s):
     profiles/r*_summary.json that traced it, per pair: that run's bytes per launch over its batch --
     the reads depend on the synthetic frames' validity, not on the build), scaled to this batch,
     its rate at this run's kernel time and the fraction of the HBM peak it is.  The kernel is not
-    bandwidth-bound (round 6: an LDS-DMA ring 2-3 tiles ahead did not speed it up,
-    profiles/r06g_window_ab.log; its VALU work per candidate is the bound)."""
+    bandwidth-bound: its gathers' latency at 4 waves per SIMD is."""
     import glob
     import json
     import re
 
     if cells != 7285 or N != 1024:
         return None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")), reverse=True):
+    sys.path.insert(0, ROOT)
+    from bench import profile_order_key  # round, then tag length, then tag: the order they were made
+
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")), key=profile_order_key, reverse=True):
         try:
             d = json.load(open(f))
         except Exception:
