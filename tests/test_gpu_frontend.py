@@ -251,3 +251,31 @@ def test_window_match_grid_edges(ctx, orc, grid):
     f0, f1 = synth.synth_window_pair(91, rows=rows, cols=cols)
     for built in (False, True):
         _window_case(ctx, orc, f0, f1, built, N=100, cap=100000)
+
+
+def test_window_match_multipass_lists(ctx, orc):
+    """every frame-0 cell a candidate (one dominant logit) and frame 1's queries spread over the
+    47 x 155 grid (valid cells only on every 12th column, every 8th row): a wave's 16 queries span
+    ~36 columns, whose union (~44 columns x 47 rows) holds several times the 512-entry candidate
+    list, so the per-wave kernel sweeps it in passes (its LDS staging ring restarting per pass);
+    both semantics"""
+    rows, cols = 47, 155
+    f0, f1 = synth.synth_window_pair(93, rows=rows, cols=cols)
+    g0, g1 = dict(f0), dict(f1)
+    semi = np.full((rows * cols, 65), -128, np.int8)
+    semi[:, 7] = 100
+    g0["semi"] = semi
+    semi1 = np.full((rows * cols, 65), -128, np.int8)
+    semi1[:, 64] = 100  # the dustbin wins: not a query
+    p = np.arange(rows * cols)
+    on = ((p // rows) % 12 == 0) & ((p % rows) % 8 == 0)
+    semi1[on, 64] = -128
+    semi1[on, 9] = 100
+    g1["semi"] = semi1
+    r = orc.track_window(g0, g1, as_built=False, N=100, cap=100000, max_matches=150)
+    assert (r["max_idx0"] != 64).all() and len(r["patches1"]) == on.sum()
+    x = np.asarray(r["patches1"]) // rows
+    spans = [(min(x[i + 15] + 8, cols - 1) - max(x[i], 0) + 1) * rows for i in range(0, len(x) - 15, 16)]
+    assert max(spans) > 1024  # some wave's list takes three or more passes
+    for built in (False, True):
+        assert _window_case(ctx, orc, g0, g1, built, N=100, cap=100000, max_matches=150) > 0
